@@ -1,0 +1,188 @@
+/*
+ * spray_rt.h -- C ABI of the MI355X (gfx950) BVH traversal + ray/triangle
+ * intersection engine that drops in behind SpRay's scene intersect/occluded
+ * surface.
+ *
+ * Reference interface each entry point replaces (paths relative to the
+ * hyungman/SpRay tree):
+ *   spray_rt_domain_upload   TriMeshBuffer::load + mapEmbreeBuffer
+ *                            (src/render/trimesh_buffer.cc:117-169, :189-225):
+ *                            rtcNewTriangleMesh/rtcSetBuffer2/rtcCommit per
+ *                            cache block, here a device BVH per slot.
+ *   spray_rt_domain_bounds   WbvhEmbree::init/build
+ *                            (src/render/wbvh_embree.cc:31-111).
+ *   spray_rt_intersect1M     Scene::intersect (src/render/scene.h:157-173,
+ *                            scene.inl:189-199): rtcIntersect + the
+ *                            TriMeshBuffer::updateIntersection epilogue
+ *                            (trimesh_buffer.cc:328-360), over a stream of
+ *                            RTCRayIntersection records.
+ *   spray_rt_occluded1M      Scene::occluded (scene.h:175-195,
+ *                            scene.inl:201-209): rtcOccluded over RTCRay
+ *                            records.
+ *   spray_rt_domains1M       Scene::intersectDomains -> WbvhEmbree::intersect
+ *                            (scene.h:197, wbvh_embree.cc:126-148) +
+ *                            DomainList::sort (src/render/rays.h:71-79).
+ *   spray_rt_*_segments      the per-domain queue drains of the schedulers
+ *                            (src/ooc/ooc_tcontext.inl:28-100,
+ *                            src/insitu/insitu_tcontext.inl:125-186) in one
+ *                            launch.
+ *   spray_rt_*_scene         the speculative resolution of a ray over every
+ *                            domain of its list (ooc_isector.h:126-145 +
+ *                            ooc_vbuf.cc:54-112): nearest hit over all
+ *                            listed domains in one launch.
+ *
+ * Conventions
+ *  - Every function returns SPRAY_RT_OK (0) or a negative status; nothing
+ *    throws across the boundary.  spray_rt_last_error() gives the message.
+ *  - Ray/hit buffers may be host or device pointers.  With host pointers the
+ *    call is synchronous (results are in place on return), as Embree's is.
+ *    With device pointers the work is enqueued on the context's stream
+ *    (spray_rt_set_stream) and spray_rt_sync() waits for it.
+ *  - Result semantics: tfar is written only on a hit;
+ *    geomID becomes 0 on a hit / occlusion and is otherwise left as the
+ *    caller set it (0xFFFFFFFF); instID is never touched; color (byte
+ *    offset 60) and Ns (offset 84) are filled by the fused epilogue.
+ *  - One context per GPU; a context is driven by one host thread at a time.
+ */
+#ifndef SPRAY_RT_H_
+#define SPRAY_RT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPRAY_RT_OK 0
+#define SPRAY_RT_ERR_ARG (-1)
+#define SPRAY_RT_ERR_HIP (-2)
+#define SPRAY_RT_ERR_STATE (-3)
+#define SPRAY_RT_ERR_NOMEM (-4)
+#define SPRAY_RT_ERR_LIMIT (-5)
+
+#define SPRAY_RT_INVALID_ID 0xFFFFFFFFu
+#define SPRAY_RT_MAX_SCENE_DOMAINS 256
+
+typedef struct spray_rt_ctx* spray_rt_ctx_t;
+
+/* Embree-2 record layouts the stream calls accept (src/render/rays.h:246-274
+ * and embree2/rtcore_ray.h).  Only these byte offsets are read or written:
+ * org 0, dir 16, tnear 32, tfar 36, Ng 48, color 60, u 64, v 68, geomID 72,
+ * primID 76, Ns 84 (RTCRayIntersection; sizeof = 96). */
+typedef struct spray_rt_ray_intersection {
+  float org[3];
+  float align0;
+  float dir[3];
+  float align1;
+  float tnear;
+  float tfar;
+  float time;
+  uint32_t mask;
+  float Ng[3];
+  uint32_t color;
+  float u;
+  float v;
+  uint32_t geomID;
+  uint32_t primID;
+  uint32_t instID;
+  float Ns[3];
+} spray_rt_ray_intersection;
+
+/* Compact ray of the fused scene path: 32 B, two 16-B loads per lane. */
+typedef struct spray_rt_ray {
+  float org[3];
+  float tnear;
+  float dir[3];
+  float tfar;
+} spray_rt_ray;
+
+/* Scene-path hit record (48 B): t = +inf, prim = 0xFFFFFFFF, domain = -1 on
+ * a miss; ng = Embree 2 unnormalised geometry normal (v0-v1)x(v2-v0);
+ * color/ns = updateIntersection epilogue. */
+typedef struct spray_rt_hit {
+  float t, u, v;
+  uint32_t prim;
+  float ng[3];
+  uint32_t color;
+  float ns[3];
+  int32_t domain;
+} spray_rt_hit;
+
+/* ---- context ---- */
+int spray_rt_create(int hip_device, spray_rt_ctx_t* out);
+int spray_rt_destroy(spray_rt_ctx_t ctx);
+const char* spray_rt_last_error(spray_rt_ctx_t ctx);
+/* hip_stream: a hipStream_t (NULL = the context's own stream). */
+int spray_rt_set_stream(spray_rt_ctx_t ctx, void* hip_stream);
+int spray_rt_sync(spray_rt_ctx_t ctx);
+
+/* ---- domains / cache slots ---- */
+/* Uploads one domain mesh (world-space vertices) into cache slot `slot`
+ * (SceneInfo.cache_block): builds the BVH on the host and copies BVH,
+ * triangles and the epilogue arrays (faces, colors 0xRRGGBB per vertex,
+ * unnormalised vertex normals; either may be NULL) to the device.  async=0:
+ * returns after the copy completed; async=1: copies are enqueued on the
+ * context's upload stream and ordered before the next query. */
+int spray_rt_domain_upload(spray_rt_ctx_t ctx, int slot, const float* verts_xyz,
+                           size_t nverts, const uint32_t* faces, size_t nfaces,
+                           const uint32_t* colors_rgb, const float* vnormals,
+                           int async);
+/* Releases a slot's device memory. */
+int spray_rt_domain_release(spray_rt_ctx_t ctx, int slot);
+/* Domain world bounds [n][6] = lo.xyz hi.xyz (Domain::world_aabb). */
+int spray_rt_domain_bounds(spray_rt_ctx_t ctx, int ndomains,
+                           const float* aabb_min_max);
+/* Which slot holds domain `domain_id` for the scene path (-1 = none). */
+int spray_rt_map_domain(spray_rt_ctx_t ctx, int domain_id, int slot);
+/* BVH statistics of a slot: nodes, depth, triangles. */
+int spray_rt_slot_info(spray_rt_ctx_t ctx, int slot, size_t* nnodes,
+                       int* depth, size_t* ntris);
+
+/* ---- Embree-1M-style streams (drop-in) ---- */
+int spray_rt_intersect1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,
+                         size_t stride);
+int spray_rt_occluded1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,
+                        size_t stride);
+/* nseg segments: rays [offsets[i], offsets[i+1]) against slots[i];
+ * offsets has nseg+1 entries (host memory). */
+int spray_rt_intersect_segments(spray_rt_ctx_t ctx, const int* slots,
+                                const size_t* offsets, int nseg, void* rays,
+                                size_t stride);
+int spray_rt_occluded_segments(spray_rt_ctx_t ctx, const int* slots,
+                               const size_t* offsets, int nseg, void* rays,
+                               size_t stride);
+/* Sorted domain lists: org/dir are [M][3]; ids/ts are [M][maxhits],
+ * counts[M] (truncated at maxhits). */
+int spray_rt_domains1M(spray_rt_ctx_t ctx, const float* org, const float* dir,
+                       size_t M, int* ids, float* ts, int* counts, int maxhits);
+
+/* ---- fused scene path (all listed domains in one launch) ---- */
+int spray_rt_intersect_scene(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                             size_t M, spray_rt_hit* hits);
+int spray_rt_occluded_scene(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                            size_t M, uint8_t* occluded);
+
+/* ---- ray sources on the device (caller side of the hot path) ---- */
+/* cam[14] = pos[3], lowerleft[3], wvec[3], hvec[3], image_w, image_h
+ * (Camera::init, src/render/camera.h:128-166).  ooc::Tracer::genMultiEyes
+ * (src/ooc/ooc_tracer.inl:124-172) over blocking tile (tx,ty,tw,th):
+ * rays[n], n = tw*th*spp in bufid order; pixid/samid may be NULL.  All
+ * device pointers. */
+int spray_rt_eye_rays_ooc(spray_rt_ctx_t ctx, const float cam[14], int image_w,
+                          int spp, int tx, int ty, int tw, int th,
+                          spray_rt_ray* rays, int32_t* pixid, int32_t* samid);
+/* Point-light shadow rays of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-171)
+ * for every hit: compacted into out_rays/out_src (source ray index); the
+ * number written goes to *d_count (device int, zeroed by the call).
+ * shade[8] = light pos[3], light radiance[3]... see DESIGN.md:
+ * shade = {lx, ly, lz, lr, lg, lb, ks_r, ks_g, ks_b, shininess}. */
+int spray_rt_spawn_shadows_pt(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                              const spray_rt_hit* hits, size_t M,
+                              const float shade[10], spray_rt_ray* out_rays,
+                              int32_t* out_src, uint32_t* d_count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,272 @@
+// bvh_build.cpp -- canonical BVH2 builder (binned SAH, 32 bins x 3 axes,
+// <= 4 triangles per leaf, depth-first layout).  Compiled with
+// -ffp-contract=off: box areas, bin indices and SAH costs are evaluated in a
+// fixed order, so the tree is a deterministic function of the mesh (tests/
+// compare it node for node with the oracle's canonical tree).
+#include "bvh_build.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace spray_rt {
+namespace {
+
+constexpr float kInf = std::numeric_limits<float>::infinity();
+
+struct Box {
+  float lo[3], hi[3];
+  void clear() {
+    for (int j = 0; j < 3; ++j) {
+      lo[j] = kInf;
+      hi[j] = -kInf;
+    }
+  }
+  void grow(const Box& o) {
+    for (int j = 0; j < 3; ++j) {
+      if (o.lo[j] < lo[j]) lo[j] = o.lo[j];
+      if (o.hi[j] > hi[j]) hi[j] = o.hi[j];
+    }
+  }
+  void grow_point(const float* p) {
+    for (int j = 0; j < 3; ++j) {
+      if (p[j] < lo[j]) lo[j] = p[j];
+      if (p[j] > hi[j]) hi[j] = p[j];
+    }
+  }
+  // half surface area, evaluated (dx*dy + dy*dz) + dz*dx
+  float half_area() const {
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return (dx * dy + dy * dz) + dz * dx;
+  }
+};
+
+int ceil_log2(size_t x) {
+  int l = 0;
+  while ((size_t(1) << l) < x) ++l;
+  return l;
+}
+
+// Conservative padding of a finite child box (culling only).
+void pad(float lo[3], float hi[3]) {
+  if (!(std::isfinite(lo[0]) && std::isfinite(hi[0]))) return;
+  for (int j = 0; j < 3; ++j) {
+    float e = hi[j] - lo[j];
+    float m = std::fmax(std::fmax(std::fabs(lo[j]), std::fabs(hi[j])), e);
+    float p = m * kBoxPad;
+    lo[j] = lo[j] - p;
+    hi[j] = hi[j] + p;
+  }
+}
+
+class Builder {
+ public:
+  Builder(const float* v, const uint32_t* f, size_t nf, BvhImage* out)
+      : v_(v), f_(f), nf_(nf), out_(out) {
+    box_.resize(nf);
+    cent_.resize(3 * nf);
+    idx_.resize(nf);
+    tmp_.resize(nf);
+    for (size_t i = 0; i < nf; ++i) {
+      Box b;
+      b.clear();
+      for (int k = 0; k < 3; ++k) b.grow_point(v + 3 * size_t(f[3 * i + k]));
+      box_[i] = b;
+      for (int j = 0; j < 3; ++j) cent_[3 * i + j] = (b.lo[j] + b.hi[j]) * 0.5f;
+      idx_[i] = uint32_t(i);
+    }
+  }
+
+  void run() {
+    out_->nodes.clear();
+    out_->prims.clear();
+    out_->depth = 0;
+    if (nf_ == 0) return;
+    if (nf_ <= size_t(kLeafMax)) {
+      // root that is itself a leaf: left child = the leaf, right = empty box
+      size_t self = alloc();
+      Box lb;
+      int32_t lref = recurse(0, nf_, 1, &lb);
+      BvhNode& n = out_->nodes[self];
+      std::memcpy(n.l_lo, lb.lo, 12);
+      std::memcpy(n.l_hi, lb.hi, 12);
+      for (int j = 0; j < 3; ++j) n.r_lo[j] = n.r_hi[j] = kInf;  // never hit
+      n.left = lref;
+      n.right = ~int32_t(0);
+    } else {
+      Box rb;
+      recurse(0, nf_, 0, &rb);
+    }
+  }
+
+ private:
+  size_t alloc() {
+    out_->nodes.emplace_back();
+    std::memset(&out_->nodes.back(), 0, sizeof(BvhNode));
+    return out_->nodes.size() - 1;
+  }
+
+  int bin_of(uint32_t p, int axis, float lo, float scale) const {
+    int k = int((cent_[3 * p + axis] - lo) * scale);
+    return std::min(std::max(k, 0), kBins - 1);
+  }
+
+  int32_t recurse(size_t begin, size_t end, int depth, Box* bb_out) {
+    const size_t n = end - begin;
+    Box bb, cb;
+    bb.clear();
+    cb.clear();
+    for (size_t i = begin; i < end; ++i) {
+      uint32_t p = idx_[i];
+      bb.grow(box_[p]);
+      cb.grow_point(&cent_[3 * p]);
+    }
+    *bb_out = bb;
+    out_->depth = std::max(out_->depth, depth);
+    if (n <= size_t(kLeafMax)) {
+      uint32_t first = uint32_t(out_->prims.size());
+      for (size_t i = begin; i < end; ++i) out_->prims.push_back(idx_[i]);
+      return ~int32_t((first << 2) | uint32_t(n - 1));
+    }
+
+    float ext[3] = {cb.hi[0] - cb.lo[0], cb.hi[1] - cb.lo[1], cb.hi[2] - cb.lo[2]};
+    int best_axis = -1, best_split = -1;
+    const bool median =
+        depth + ceil_log2((n + kLeafMax - 1) / kLeafMax) >= kMaxDepth;
+    if (!median) {
+      float best = kInf;
+      for (int a = 0; a < 3; ++a) {
+        if (!(ext[a] > 0.0f)) continue;
+        const float scale = float(kBins) / ext[a];
+        Box bins[kBins];
+        uint32_t cnt[kBins];
+        for (int k = 0; k < kBins; ++k) {
+          bins[k].clear();
+          cnt[k] = 0;
+        }
+        for (size_t i = begin; i < end; ++i) {
+          uint32_t p = idx_[i];
+          int k = bin_of(p, a, cb.lo[a], scale);
+          bins[k].grow(box_[p]);
+          ++cnt[k];
+        }
+        float right_area[kBins];
+        uint32_t right_cnt[kBins];
+        Box acc;
+        acc.clear();
+        uint32_t c = 0;
+        for (int k = kBins - 1; k > 0; --k) {
+          acc.grow(bins[k]);
+          c += cnt[k];
+          right_area[k] = c ? acc.half_area() : 0.0f;
+          right_cnt[k] = c;
+        }
+        acc.clear();
+        c = 0;
+        for (int k = 0; k < kBins - 1; ++k) {
+          acc.grow(bins[k]);
+          c += cnt[k];
+          if (c == 0 || right_cnt[k + 1] == 0) continue;
+          float cost = float(c) * acc.half_area() +
+                       float(right_cnt[k + 1]) * right_area[k + 1];
+          if (cost < best) {
+            best = cost;
+            best_axis = a;
+            best_split = k + 1;
+          }
+        }
+      }
+    }
+
+    size_t mid;
+    if (best_axis >= 0) {
+      const float scale = float(kBins) / ext[best_axis];
+      size_t l = begin, r = 0;
+      for (size_t i = begin; i < end; ++i) {
+        uint32_t p = idx_[i];
+        if (bin_of(p, best_axis, cb.lo[best_axis], scale) < best_split)
+          idx_[l++] = p;
+        else
+          tmp_[r++] = p;
+      }
+      std::copy(tmp_.begin(), tmp_.begin() + r, idx_.begin() + l);
+      mid = l;
+    } else {
+      int a = 0;
+      if (ext[1] > ext[a]) a = 1;
+      if (ext[2] > ext[a]) a = 2;
+      if (ext[a] > 0.0f) {
+        const float* c = cent_.data();
+        std::sort(idx_.begin() + begin, idx_.begin() + end,
+                  [c, a](uint32_t x, uint32_t y) {
+                    float cx = c[3 * x + a], cy = c[3 * y + a];
+                    return cx < cy || (cx == cy && x < y);
+                  });
+      }
+      mid = begin + n / 2;
+    }
+
+    size_t self = alloc();
+    Box lb, rb;
+    int32_t lref = recurse(begin, mid, depth + 1, &lb);
+    int32_t rref = recurse(mid, end, depth + 1, &rb);
+    BvhNode& nd = out_->nodes[self];
+    std::memcpy(nd.l_lo, lb.lo, 12);
+    std::memcpy(nd.l_hi, lb.hi, 12);
+    std::memcpy(nd.r_lo, rb.lo, 12);
+    std::memcpy(nd.r_hi, rb.hi, 12);
+    nd.left = lref;
+    nd.right = rref;
+    return int32_t(self);
+  }
+
+  const float* v_;
+  const uint32_t* f_;
+  size_t nf_;
+  BvhImage* out_;
+  std::vector<Box> box_;
+  std::vector<float> cent_;
+  std::vector<uint32_t> idx_, tmp_;
+};
+
+}  // namespace
+
+bool build_bvh(const float* verts, size_t nverts, const uint32_t* faces,
+               size_t nfaces, BvhImage* out) {
+  for (size_t i = 0; i < 3 * nfaces; ++i)
+    if (faces[i] >= nverts) return false;
+  if (nfaces >= (size_t(1) << 29)) return false;
+  Builder b(verts, faces, nfaces, out);
+  b.run();
+  // padded child boxes for the device
+  for (BvhNode& n : out->nodes) {
+    pad(n.l_lo, n.l_hi);
+    pad(n.r_lo, n.r_hi);
+  }
+  // triangle records in leaf order: v0, e1 = v0 - v1, e2 = v2 - v0,
+  // Ng = e1 x e2 written with the kernels' explicit FMA form
+  out->tris.resize(12 * out->prims.size());
+  for (size_t i = 0; i < out->prims.size(); ++i) {
+    const uint32_t* f = faces + 3 * size_t(out->prims[i]);
+    const float* a = verts + 3 * size_t(f[0]);
+    const float* b = verts + 3 * size_t(f[1]);
+    const float* c = verts + 3 * size_t(f[2]);
+    float* r = &out->tris[12 * i];
+    r[0] = a[0];
+    r[1] = a[1];
+    r[2] = a[2];
+    r[3] = a[0] - b[0];
+    r[4] = a[1] - b[1];
+    r[5] = a[2] - b[2];
+    r[6] = c[0] - a[0];
+    r[7] = c[1] - a[1];
+    r[8] = c[2] - a[2];
+    r[9] = std::fma(r[4], r[8], -(r[5] * r[7]));
+    r[10] = std::fma(r[5], r[6], -(r[3] * r[8]));
+    r[11] = std::fma(r[3], r[7], -(r[4] * r[6]));
+  }
+  return true;
+}
+
+}  // namespace spray_rt

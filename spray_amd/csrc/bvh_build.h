@@ -1,0 +1,30 @@
+// bvh_build.h -- host builder of the per-domain BVH2 uploaded to HBM.
+//
+// Replaces the Embree bvh4.triangle4v build that TriMeshBuffer::mapEmbreeBuffer
+// triggers through rtcCommit (src/render/trimesh_buffer.cc:189-225).  The tree
+// is the canonical BVH2 of SURVEY.md 8(d): binned SAH over 32 bins on each
+// axis, leaves of <= 4 triangles, depth-first layout, so its node / triangle
+// counts are exactly the ones the algorithmic-byte formula is defined on.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "rt_common.h"
+
+namespace spray_rt {
+
+struct BvhImage {
+  std::vector<BvhNode> nodes;   // padded child boxes (device-ready)
+  std::vector<float> tris;      // [ntris][12] v0 e1 e2 Ng, leaf order
+  std::vector<uint32_t> prims;  // leaf order -> face index
+  int depth = 0;
+};
+
+// verts: [nverts][3] world space; faces: [nfaces][3].  Throws nothing;
+// returns false on invalid face indices.
+bool build_bvh(const float* verts, size_t nverts, const uint32_t* faces,
+               size_t nfaces, BvhImage* out);
+
+}  // namespace spray_rt

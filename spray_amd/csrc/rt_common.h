@@ -1,0 +1,58 @@
+// rt_common.h -- layouts shared by the host runtime and the gfx950 kernels.
+//
+// HBM layout of one cache slot (one domain), all 16-B aligned:
+//   nodes  : BvhNode[nnodes]        64 B  -- BVH2, both child boxes + refs
+//   tris   : float4[3 * ntris]      48 B  -- v0 | e1 | e2 | Ng packed in
+//                                            three float4 (leaf order)
+//   prims  : uint32[ntris]          4 B   -- leaf order -> PLY face index
+//   faces  : uint32[3 * nfaces]     epilogue gather (PLY order)
+//   colors : uint32[nverts]         0xRRGGBB per vertex
+//   normals: float[3 * nverts]      unnormalised vertex normals
+// A device-side SlotDesc table points at these; the scene path adds a
+// domain -> slot map and the domain AABBs.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+namespace spray_rt {
+
+constexpr int kLeafMax = 4;        // triangles per leaf (canonical BVH2)
+constexpr int kBins = 32;          // SAH bins per axis
+constexpr int kMaxDepth = 24;      // builder guarantees depth <= kMaxDepth
+constexpr int kStack = 24;         // per-lane traversal stack (LDS), >= kMaxDepth
+constexpr float kRayEpsilon = 0.001f;  // SPRAY_RAY_EPSILON, render/spray.h:46
+// Culling slack of the slab test (results never depend on culling as long as
+// it is conservative; tests/ check BVH == brute force bit-exactly).
+constexpr float kTfarSlack = 1.0000153f;  // 1 + 2^-16
+constexpr float kBoxPad = 1e-6f;          // relative node-box padding
+constexpr float kDirClamp = 1e-20f;       // |d| floor for the inverse dir
+
+// 64-B BVH2 node: left box, right box, child refs.  ref >= 0: internal node
+// index (slot-local); ref < 0: leaf ~((first << 2) | (count - 1)).
+struct alignas(16) BvhNode {
+  float l_lo[3];
+  float l_hi[3];
+  float r_lo[3];
+  float r_hi[3];
+  int32_t left;
+  int32_t right;
+  int32_t pad0;
+  int32_t pad1;
+};
+static_assert(sizeof(BvhNode) == 64, "node must be 64 B");
+
+struct alignas(16) SlotDesc {
+  const BvhNode* nodes;
+  const float* tris;        // 12 floats per triangle
+  const uint32_t* prims;
+  const uint32_t* faces;
+  const uint32_t* colors;
+  const float* normals;
+  uint32_t ntris;
+  uint32_t nverts;
+  uint32_t nnodes;
+  uint32_t pad;
+};
+
+}  // namespace spray_rt
