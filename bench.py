@@ -1,0 +1,223 @@
+"""Headline benchmark: Mrays/s (primary + shadow) on the 64-domain wavelets
+scene at 1024x1024, 8 spp (BASELINE.json, configs[1]).
+
+One step = one frame of the hot path over rays already resident in HBM:
+  1. closest hit of the 8,388,608 primary rays against every domain of their
+     sorted domain lists (spray_rt_intersect_scene: domain query + BVH2
+     traversal + updateIntersection epilogue, one launch),
+  2. point-light shadow-ray spawn of ooc::ShaderPt (compaction, 3 launches),
+  3. any hit of the spawned shadow rays (spray_rt_occluded_scene_devcount).
+Primary rays are generated once before timing by the reference's camera /
+sampler (ooc::Tracer::genMultiEyes over its 8 blocking tiles of 1024x128).
+
+Multi-GPU (torchrun, one process per GPU): every rank traces its own frame
+(frame replicas, weak scaling); barrier + max over ranks around the K timed
+steps.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+SCENE = os.path.join(SCENES, "wavelets64.spray")
+COUNTS = os.path.join(ROOT, "tests", "golden", "workload_counts.json")
+METRIC = "Mrays/s (primary+shadow), 64-domain wavelets, 1024x1024 8spp, 1/2/4/8 GPU"
+CAM = dict(pos=[90.172180, 84.141418, 82.480225], lookat=[30.0, 28.649426, 30.0],
+           up=[0.0, 1.0, 0.0], fov=90.0)
+W = H = 1024
+SPP = 8
+TILE_H = 128  # ImageScheduleTileList: 1M samples per rank -> 8 tiles of 1024x128
+SHADE = [0.0, 500.0, 1000.0, 1.0, 1.0, 1.0, 0.4, 0.4, 0.4, 10.0]  # light, --blinn
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def tiles():
+    return [(0, y, W, TILE_H) for y in range(0, H, TILE_H)]
+
+
+def algorithmic_bytes(n_rays, nodes, tris, out_bytes):
+    """sum_rays (32 + out) + sum_visits (64 N_node + 48 N_tri)."""
+    return n_rays * (32 + out_bytes) + 64 * nodes + 48 * tris
+
+
+def cpu_baseline(target_s=10.0):
+    """Oracle (C/OpenMP port of the reference path) on a bounded sample of the
+    same frame: whole 1024-pixel rows, 8 spp, primary + PT shadow rays."""
+    from oracle import pyoracle as po
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    sc, doms, lights = po.load_scene(SCENE, SCENES)
+    cam = po.camera_init(CAM["pos"], CAM["lookat"], CAM["up"], CAM["fov"], W, H)
+
+    def run(y0, rows):
+        org, d, _, _ = po.eye_rays_ooc(cam, W, SPP, (0, y0, W, rows))
+        t0 = time.perf_counter()
+        hits, _ = sc.intersect(org, d, threads)
+        so, sd, _ = po.spawn_shadows_pt(org, d, hits, SHADE[0:3], SHADE[3:6], SHADE[6:9],
+                                        SHADE[9])
+        sc.occluded(so, sd, threads)
+        return time.perf_counter() - t0, len(org) + len(so)
+
+    y0 = 448  # band through the middle of the frame (hit-dense rows)
+    dt, n = run(y0, 4)  # calibration
+    rows = int(max(4, min(H - y0, 4 * target_s / max(dt, 1e-3))))
+    dt, n = run(y0, rows)
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads,
+            "kind": "port",
+            "sample": "rows %d-%d of the 1024x1024x8spp frame: %d primary+shadow rays, "
+                      "oracle/oracle.c (C, OpenMP, %d threads), %.1f s" %
+                      (y0, y0 + rows - 1, n, threads, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import spray_amd
+    sc = spray_amd.Scene(SCENE, SCENES, cache_size=-1, device=local)
+    rt = sc.rt
+    stream = torch.cuda.current_stream()
+    rt.set_stream(stream)
+    dev = torch.device("cuda", local)
+
+    # ---- resident inputs: the frame's primary rays (8 tiles, tile-local seeds)
+    cam = spray_amd.camera_init(CAM["pos"], CAM["lookat"], CAM["up"], CAM["fov"], W, H)
+    n_prim = W * H * SPP
+    per_tile = W * TILE_H * SPP
+    prim = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
+    for k, t in enumerate(tiles()):
+        rt.eye_rays_ooc(cam, W, SPP, t, prim[k * per_tile * 32:(k + 1) * per_tile * 32])
+    hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
+    shadow = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
+    src = torch.empty(n_prim, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    occ = torch.empty(n_prim, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    # ---- canonical traversal counts (counting build, outside the timing)
+    ctr = torch.zeros(3, dtype=torch.int64, device=dev)
+    ctr2 = torch.zeros(3, dtype=torch.int64, device=dev)
+    rt.intersect_scene(prim, hits, counters=ctr)
+    rt.spawn_shadows_pt(prim, hits, n_prim, SHADE, shadow, src, cnt)
+    rt.occluded_scene_devcount(shadow, n_prim, cnt, occ, counters=ctr2)
+    torch.cuda.synchronize()
+    n_shadow = int(cnt.item())
+    gpu_counts = {"primary": {"nodes": int(ctr[0]), "tris": int(ctr[1]), "visits": int(ctr[2]),
+                              "rays": n_prim},
+                  "shadow": {"nodes": int(ctr2[0]), "tris": int(ctr2[1]), "visits": int(ctr2[2]),
+                             "rays": n_shadow}}
+    counts_src = "gpu counting build"
+    if os.path.exists(COUNTS):
+        ref = json.load(open(COUNTS))
+        if ref.get("primary") == gpu_counts["primary"] and ref.get("shadow") == gpu_counts["shadow"]:
+            counts_src = "oracle fixture tests/golden/workload_counts.json (== gpu counting build)"
+        else:
+            counts_src = "gpu counting build (MISMATCH vs oracle fixture)"
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        rt.intersect_scene(prim, hits)
+        if ev:
+            ev[1].record(stream)
+        rt.spawn_shadows_pt(prim, hits, n_prim, SHADE, shadow, src, cnt)
+        if ev:
+            ev[2].record(stream)
+        rt.occluded_scene_devcount(shadow, n_prim, cnt, occ)
+        if ev:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    assert int(cnt.item()) == n_shadow
+
+    ch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    sp_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ah_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    ms_step = elapsed / args.steps * 1e3
+    rays_step = n_prim + n_shadow
+    value = rays_step * world * args.steps / elapsed / 1e6
+
+    pc, sh = gpu_counts["primary"], gpu_counts["shadow"]
+    ch_bytes = algorithmic_bytes(n_prim, pc["nodes"], pc["tris"], 32)
+    ah_bytes = algorithmic_bytes(n_shadow, sh["nodes"], sh["tris"], 4)
+    ch_gbs = ch_bytes / (ch_ms * 1e-3) / 1e9
+    ah_gbs = ah_bytes / (ah_ms * 1e-3) / 1e9
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        try:
+            traffic = json.load(open(args.traffic)).get("scene_intersect_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (reference example mesh wavelet.ply x64, deterministic camera rays)",
+        "config": {"workload": "wavelets64 1024x1024x8spp PT primary+shadow, all 64 domains "
+                               "resident per GPU (configs[1])",
+                   "rays_per_step": rays_step, "primary_rays": n_prim, "shadow_rays": n_shadow,
+                   "parallelism": "frame replicas x%d (weak)" % world},
+        "roofline": {"bound": "hbm", "achieved": round(ch_gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ch_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel": "k_scene<closest-hit> (primary)",
+                     "bytes_per_launch": ch_bytes, "avg_launch_ms": round(ch_ms, 4),
+                     "counts": counts_src},
+        "kernels_ms": {"intersect_scene": round(ch_ms, 4), "spawn_pt": round(sp_ms, 4),
+                       "occluded_scene": round(ah_ms, 4),
+                       "occluded_achieved_GBs": round(ah_gbs, 1)},
+        "canonical_counts": gpu_counts,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    sc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -139,6 +139,14 @@ int spray_rt_map_domain(spray_rt_ctx_t ctx, int domain_id, int slot);
 int spray_rt_slot_info(spray_rt_ctx_t ctx, int slot, size_t* nnodes,
                        int* depth, size_t* ntris);
 
+/* Host-only: the canonical BVH2 a slot upload would build (no GPU needed).
+ * Call with NULL outputs for sizes.  nodes_out: 64-B nodes (padded boxes),
+ * tris_out: [ntris][12] v0 e1 e2 Ng, prims_out: leaf order -> face index. */
+int spray_rt_bvh_build_host(const float* verts_xyz, size_t nverts,
+                            const uint32_t* faces, size_t nfaces,
+                            size_t* nnodes, int* depth, void* nodes_out,
+                            float* tris_out, uint32_t* prims_out);
+
 /* ---- Embree-1M-style streams (drop-in) ---- */
 int spray_rt_intersect1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,
                          size_t stride);
@@ -162,6 +170,22 @@ int spray_rt_intersect_scene(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                              size_t M, spray_rt_hit* hits);
 int spray_rt_occluded_scene(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                             size_t M, uint8_t* occluded);
+/* Same, with per-launch traversal counters (device uint64[3]: node fetches,
+ * triangle tests, (ray, domain) visits) accumulated atomically -- the
+ * counting build used to verify the canonical traversal against the oracle. */
+int spray_rt_intersect_scene_counted(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                     size_t M, spray_rt_hit* hits,
+                                     unsigned long long* d_counters);
+int spray_rt_occluded_scene_counted(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                    size_t M, uint8_t* occluded,
+                                    unsigned long long* d_counters);
+/* Occlusion of the first *d_count (device uint32, e.g. written by
+ * spray_rt_spawn_shadows_pt) of at most max_rays device-resident rays, with
+ * no host round trip.  d_counters may be NULL. */
+int spray_rt_occluded_scene_devcount(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                     size_t max_rays, const uint32_t* d_count,
+                                     uint8_t* occluded,
+                                     unsigned long long* d_counters);
 
 /* ---- ray sources on the device (caller side of the hot path) ---- */
 /* cam[14] = pos[3], lowerleft[3], wvec[3], hvec[3], image_w, image_h

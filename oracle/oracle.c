@@ -980,6 +980,25 @@ static void epilogue(const or_domain* d, uint32_t prim, float u, float v,
   for (int k = 0; k < 3; ++k) h->ns[k] = (n0[k] * w + n1[k] * u) + n2[k] * v;
 }
 
+void or_epilogue(const uint32_t* faces, const uint32_t* colors,
+                 const float* normals, const uint32_t* prim, const float* u,
+                 const float* v, size_t n, uint32_t* color_out, float* ns_out) {
+  or_domain d;
+  memset(&d, 0, sizeof(d));
+  d.faces = (uint32_t*)faces;
+  d.colors = (uint32_t*)colors;
+  d.normals = (float*)normals;
+  for (size_t i = 0; i < n; ++i) {
+    if (prim[i] == 0xFFFFFFFFu) continue;
+    or_hit h;
+    epilogue(&d, prim[i], u[i], v[i], &h);
+    color_out[i] = h.color;
+    ns_out[3 * i] = h.ns[0];
+    ns_out[3 * i + 1] = h.ns[1];
+    ns_out[3 * i + 2] = h.ns[2];
+  }
+}
+
 void or_scene_intersect(const or_scene* s, const float* org, const float* dir,
                         size_t n, or_hit* hits, or_counts* cnt, int nthreads) {
   uint64_t tn = 0, tt = 0, tv = 0;

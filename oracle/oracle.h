@@ -101,6 +101,12 @@ void or_f64_intersect(const float* v, const uint32_t* f, size_t nf,
                       size_t n, double* t_out, int32_t* prim_out,
                       uint8_t* margin_out);
 
+/* TriMeshBuffer::updateIntersection for n hits of one domain (prim = face
+ * index; prim == 0xFFFFFFFF rows are skipped). */
+void or_epilogue(const uint32_t* faces, const uint32_t* colors,
+                 const float* normals, const uint32_t* prim, const float* u,
+                 const float* v, size_t n, uint32_t* color_out, float* ns_out);
+
 /* ---- canonical BVH2 (binned SAH, 32 bins, <=4 tris/leaf) ---- */
 typedef struct or_bvh or_bvh;
 or_bvh* or_bvh_build(const float* v, const uint32_t* f, size_t nf);

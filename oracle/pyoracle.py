@@ -93,6 +93,7 @@ def _declare(L):
         "or_brute_intersect": (None, [P, SZ, P, P, P, P, SZ, P, P, P, P]),
         "or_brute_occluded": (None, [P, SZ, P, P, P, P, SZ, P]),
         "or_f64_intersect": (None, [P, P, SZ, P, P, C.c_float, SZ, P, P, P]),
+        "or_epilogue": (None, [P, P, P, P, P, P, SZ, P, P]),
         "or_bvh_build": (P, [P, P, SZ]),
         "or_bvh_free": (None, [P]),
         "or_bvh_num_nodes": (SZ, [P]),
@@ -402,6 +403,15 @@ def f64_intersect(v, f, org, d, tnear=0.001):
     lib().or_f64_intersect(_p(f32(v)), _p(u32(f)), len(f), _p(f32(org)), _p(f32(d)),
                            float(tnear), n, _p(t), _p(p), _p(m))
     return t, p, m
+
+
+def epilogue(faces, colors, normals, prim, u, v):
+    n = len(prim)
+    col = np.zeros(n, np.uint32)
+    ns = np.zeros((n, 3), np.float32)
+    lib().or_epilogue(_p(u32(faces)), _p(u32(colors)), _p(f32(normals)), _p(u32(prim)),
+                      _p(f32(u)), _p(f32(v)), n, _p(col), _p(ns))
+    return col, ns
 
 
 class Bvh:

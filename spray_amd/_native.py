@@ -1,0 +1,103 @@
+"""ctypes binding of libspray_rt.so (include/spray_rt.h, include/spray_scene.h).
+
+The library is the product: gfx950 kernels + C ABI + host scene layer.  There
+is no fallback -- if the shared object is missing or fails to load, import of
+the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libspray_rt.so")
+
+# record layouts (include/spray_rt.h)
+RAY_DTYPE = np.dtype([("org", "<f4", 3), ("tnear", "<f4"), ("dir", "<f4", 3),
+                      ("tfar", "<f4")])
+HIT_DTYPE = np.dtype([("t", "<f4"), ("u", "<f4"), ("v", "<f4"), ("prim", "<u4"),
+                      ("ng", "<f4", 3), ("color", "<u4"), ("ns", "<f4", 3),
+                      ("domain", "<i4")])
+RTC_ISECT_DTYPE = np.dtype([("org", "<f4", 3), ("align0", "<f4"), ("dir", "<f4", 3),
+                            ("align1", "<f4"), ("tnear", "<f4"), ("tfar", "<f4"),
+                            ("time", "<f4"), ("mask", "<u4"), ("Ng", "<f4", 3),
+                            ("color", "<u4"), ("u", "<f4"), ("v", "<f4"),
+                            ("geomID", "<u4"), ("primID", "<u4"), ("instID", "<u4"),
+                            ("Ns", "<f4", 3)])
+assert RAY_DTYPE.itemsize == 32 and HIT_DTYPE.itemsize == 48
+assert RTC_ISECT_DTYPE.itemsize == 96
+
+INVALID_ID = 0xFFFFFFFF
+
+# every symbol the public headers declare: (restype, argtypes)
+P = C.c_void_p
+SZ = C.c_size_t
+I = C.c_int
+SIGNATURES = {
+    # spray_rt.h
+    "spray_rt_create": (I, [I, P]),
+    "spray_rt_destroy": (I, [P]),
+    "spray_rt_last_error": (C.c_char_p, [P]),
+    "spray_rt_set_stream": (I, [P, P]),
+    "spray_rt_sync": (I, [P]),
+    "spray_rt_domain_upload": (I, [P, I, P, SZ, P, SZ, P, P, I]),
+    "spray_rt_domain_release": (I, [P, I]),
+    "spray_rt_domain_bounds": (I, [P, I, P]),
+    "spray_rt_map_domain": (I, [P, I, I]),
+    "spray_rt_slot_info": (I, [P, I, P, P, P]),
+    "spray_rt_bvh_build_host": (I, [P, SZ, P, SZ, P, P, P, P, P]),
+    "spray_rt_intersect1M": (I, [P, I, P, SZ, SZ]),
+    "spray_rt_occluded1M": (I, [P, I, P, SZ, SZ]),
+    "spray_rt_intersect_segments": (I, [P, P, P, I, P, SZ]),
+    "spray_rt_occluded_segments": (I, [P, P, P, I, P, SZ]),
+    "spray_rt_domains1M": (I, [P, P, P, SZ, P, P, P, I]),
+    "spray_rt_intersect_scene": (I, [P, P, SZ, P]),
+    "spray_rt_occluded_scene": (I, [P, P, SZ, P]),
+    "spray_rt_intersect_scene_counted": (I, [P, P, SZ, P, P]),
+    "spray_rt_occluded_scene_counted": (I, [P, P, SZ, P, P]),
+    "spray_rt_occluded_scene_devcount": (I, [P, P, SZ, P, P, P]),
+    "spray_rt_eye_rays_ooc": (I, [P, P, I, I, I, I, I, I, P, P, P]),
+    "spray_rt_spawn_shadows_pt": (I, [P, P, P, SZ, P, P, P, P]),
+    # spray_scene.h
+    "spray_scene_create": (I, [C.c_char_p, C.c_char_p, I, I, P, C.c_char_p, SZ]),
+    "spray_scene_destroy": (I, [P]),
+    "spray_scene_last_error": (C.c_char_p, [P]),
+    "spray_scene_rt": (P, [P]),
+    "spray_scene_num_domains": (I, [P]),
+    "spray_scene_cache_capacity": (I, [P]),
+    "spray_scene_bounds": (I, [P, P, P]),
+    "spray_scene_num_lights": (I, [P]),
+    "spray_scene_light": (I, [P, I, P]),
+    "spray_scene_load": (I, [P, I, P]),
+    "spray_scene_intersect1": (I, [P, I, P, P, P]),
+    "spray_scene_occluded1": (I, [P, I, P, P, P]),
+    "spray_camera_init": (I, [P, P, P, C.c_float, I, I, P]),
+    "spray_scene_domain_mesh": (I, [P, I, P, P, P, P, P, P]),
+    "spray_host_parse_scene": (I, [C.c_char_p, C.c_char_p, P, P, P, P, P, C.c_char_p, SZ]),
+    "spray_host_domain_mesh": (I, [C.c_char_p, C.c_char_p, I, P, P, P, P, P, P]),
+}
+
+_lib = None
+
+
+class SprayRtError(RuntimeError):
+    pass
+
+
+def lib():
+    """Loads libspray_rt.so; raises if it is absent (no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                "spray_amd: %s is missing -- build it with `python -m spray_amd.build` "
+                "(there is no CPU fallback)" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib

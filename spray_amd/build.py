@@ -1,0 +1,63 @@
+"""Builds libspray_rt.so (gfx950 kernels + C ABI + host scene layer) in-tree.
+
+    python -m spray_amd.build          # or __graft_entry__.build()
+
+The shared object lands in spray_amd/lib/ (git-ignored, shipped with the
+tree to the GPU box).  Every translation unit is compiled with
+-ffp-contract=off so fused multiply-adds happen only where the kernels write
+fmaf() explicitly (bit parity with oracle/).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libspray_rt.so")
+ARCH = os.environ.get("SPRAY_AMD_ARCH", "gfx950")
+
+SOURCES = ["rt_kernels.hip", "rt_api.cpp", "bvh_build.cpp", "scene_host.cpp"]
+HEADERS = ["rt_common.h", "rt_kernels.h", "bvh_build.h", "scene_host.h"]
+PUBLIC = [os.path.join(ROOT, "include", h) for h in ("spray_rt.h", "spray_scene.h")]
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the HIP engine cannot be built")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + PUBLIC + [__file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

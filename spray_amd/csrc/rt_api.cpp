@@ -1,0 +1,639 @@
+// rt_api.cpp -- C ABI of the engine (include/spray_rt.h).
+//
+// Owns the per-slot device images (BVH, triangles, epilogue arrays), the
+// slot descriptor table, the domain boxes / domain->slot map of the scene
+// path, and staging for host-pointer streams.  No exception crosses the
+// boundary: every entry point returns a status and records a message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "bvh_build.h"
+#include "rt_common.h"
+#include "rt_kernels.h"
+#include "spray_rt.h"
+
+using namespace spray_rt;
+
+namespace {
+
+struct SlotHost {
+  void* dmem = nullptr;  // one allocation: nodes|tris|prims|faces|colors|normals
+  size_t bytes = 0;
+  SlotDesc desc{};
+  int depth = 0;
+  hipEvent_t ready = nullptr;  // async upload completion
+  void* pinned = nullptr;      // staging for async uploads
+  size_t pinned_bytes = 0;
+};
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+struct spray_rt_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t user_stream = nullptr;
+  hipStream_t upload_stream = nullptr;
+  std::vector<SlotHost> slots;
+  SlotDesc* d_slots = nullptr;
+  size_t d_slots_cap = 0;
+  bool slots_dirty = true;
+  // scene path
+  int ndom = 0;
+  float* d_boxes = nullptr;
+  int* d_dom2slot = nullptr;
+  std::vector<int> dom2slot;
+  bool dom_dirty = true;
+  // segment tables
+  int* d_seg_slot = nullptr;
+  size_t* d_seg_off = nullptr;
+  size_t seg_cap = 0;
+  // host-pointer staging
+  void* d_stage = nullptr;
+  size_t stage_cap = 0;
+  void* d_stage2 = nullptr;
+  size_t stage2_cap = 0;
+  void* d_stage3 = nullptr;
+  size_t stage3_cap = 0;
+  uint32_t* d_block_counts = nullptr;
+  size_t block_cap = 0;
+  std::string err;
+};
+
+namespace {
+
+int fail(spray_rt_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                   \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess)                                                   \
+      return fail(ctx, SPRAY_RT_ERR_HIP, "%s: %s", #expr,                   \
+                  hipGetErrorString(_e));                                   \
+  } while (0)
+
+hipStream_t stream_of(spray_rt_ctx* c) {
+  return c->user_stream ? c->user_stream : c->own_stream;
+}
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return SPRAY_RT_OK;
+  if (*buf) HIPCHK(c, hipFree(*buf));
+  *buf = nullptr;
+  *cap = 0;
+  size_t want = std::max(bytes, size_t(1) << 20);
+  HIPCHK(c, hipMalloc(buf, want));
+  *cap = want;
+  return SPRAY_RT_OK;
+}
+
+// Makes pending async uploads visible to the compute stream and pushes the
+// slot table / domain map when they changed.
+int prepare(spray_rt_ctx* c) {
+  hipStream_t s = stream_of(c);
+  for (SlotHost& sh : c->slots)
+    if (sh.ready) HIPCHK(c, hipStreamWaitEvent(s, sh.ready, 0));
+  if (c->slots_dirty) {
+    size_t n = std::max<size_t>(c->slots.size(), 1);
+    if (c->d_slots_cap < n) {
+      if (c->d_slots) HIPCHK(c, hipFree(c->d_slots));
+      HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_slots),
+                          n * sizeof(SlotDesc)));
+      c->d_slots_cap = n;
+    }
+    std::vector<SlotDesc> h(n);
+    for (size_t i = 0; i < c->slots.size(); ++i) h[i] = c->slots[i].desc;
+    HIPCHK(c, hipMemcpyAsync(c->d_slots, h.data(), n * sizeof(SlotDesc),
+                             hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamSynchronize(s));  // h goes out of scope
+    c->slots_dirty = false;
+  }
+  if (c->dom_dirty && c->ndom > 0) {
+    HIPCHK(c, hipMemcpyAsync(c->d_dom2slot, c->dom2slot.data(),
+                             c->ndom * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->dom_dirty = false;
+  }
+  return SPRAY_RT_OK;
+}
+
+int check_slot(spray_rt_ctx* c, int slot) {
+  if (slot < 0 || size_t(slot) >= c->slots.size() || !c->slots[slot].dmem)
+    return fail(c, SPRAY_RT_ERR_ARG, "slot %d is not loaded", slot);
+  return SPRAY_RT_OK;
+}
+
+int upload_segments(spray_rt_ctx* c, const int* slots, const size_t* offsets,
+                    int nseg) {
+  if (size_t(nseg) > c->seg_cap) {
+    if (c->d_seg_slot) HIPCHK(c, hipFree(c->d_seg_slot));
+    if (c->d_seg_off) HIPCHK(c, hipFree(c->d_seg_off));
+    size_t cap = std::max<size_t>(nseg, 64);
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_seg_slot), cap * sizeof(int)));
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_seg_off),
+                        (cap + 1) * sizeof(size_t)));
+    c->seg_cap = cap;
+  }
+  hipStream_t s = stream_of(c);
+  HIPCHK(c, hipMemcpyAsync(c->d_seg_slot, slots, nseg * sizeof(int),
+                           hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->d_seg_off, offsets, (nseg + 1) * sizeof(size_t),
+                           hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipStreamSynchronize(s));  // caller's host arrays may go away
+  return SPRAY_RT_OK;
+}
+
+// Runs a per-slot stream kernel over (possibly host-resident) AoS records.
+template <typename Launch>
+int run_rtc(spray_rt_ctx* c, const int* slots, const size_t* offsets, int nseg,
+            void* rays, size_t stride, Launch launch) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (nseg <= 0 || !slots || !offsets)
+    return fail(c, SPRAY_RT_ERR_ARG, "empty segment list");
+  if (stride < 80 || (stride & 3))
+    return fail(c, SPRAY_RT_ERR_ARG, "stride %zu too small or unaligned", stride);
+  size_t M = offsets[nseg];
+  if (offsets[0] != 0) return fail(c, SPRAY_RT_ERR_ARG, "offsets[0] must be 0");
+  for (int i = 0; i < nseg; ++i) {
+    if (offsets[i + 1] < offsets[i])
+      return fail(c, SPRAY_RT_ERR_ARG, "offsets not ascending");
+    if (offsets[i + 1] > offsets[i]) {
+      int r = check_slot(c, slots[i]);
+      if (r) return r;
+    }
+  }
+  if (M == 0) return SPRAY_RT_OK;
+  if (!rays) return fail(c, SPRAY_RT_ERR_ARG, "null ray buffer");
+  int r = prepare(c);
+  if (r) return r;
+  r = upload_segments(c, slots, offsets, nseg);
+  if (r) return r;
+  hipStream_t s = stream_of(c);
+  if (is_device_ptr(rays)) {
+    HIPCHK(c, launch(s, c->d_slots, c->d_seg_slot, c->d_seg_off, nseg,
+                     static_cast<char*>(rays), stride, M));
+    return SPRAY_RT_OK;
+  }
+  size_t bytes = M * stride;
+  r = ensure(c, &c->d_stage, &c->stage_cap, bytes);
+  if (r) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(c, launch(s, c->d_slots, c->d_seg_slot, c->d_seg_off, nseg,
+                   static_cast<char*>(c->d_stage), stride, M));
+  HIPCHK(c, hipMemcpyAsync(rays, c->d_stage, bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return SPRAY_RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spray_rt_create(int hip_device, spray_rt_ctx_t* out) {
+  if (!out) return SPRAY_RT_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    (void)hipGetLastError();
+    return SPRAY_RT_ERR_HIP;
+  }
+  if (hip_device < 0 || hip_device >= n) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = new (std::nothrow) spray_rt_ctx;
+  if (!c) return SPRAY_RT_ERR_NOMEM;
+  c->device = hip_device;
+  if (hipSetDevice(hip_device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SPRAY_RT_ERR_HIP;
+  }
+  *out = c;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_destroy(spray_rt_ctx_t c) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  for (SlotHost& s : c->slots) {
+    if (s.dmem) (void)hipFree(s.dmem);
+    if (s.ready) (void)hipEventDestroy(s.ready);
+    if (s.pinned) (void)hipHostFree(s.pinned);
+  }
+  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_seg_slot,
+                  c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
+                  c->d_block_counts};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->upload_stream) (void)hipStreamDestroy(c->upload_stream);
+  delete c;
+  return SPRAY_RT_OK;
+}
+
+const char* spray_rt_last_error(spray_rt_ctx_t c) {
+  return c ? c->err.c_str() : "null context";
+}
+
+int spray_rt_set_stream(spray_rt_ctx_t c, void* hip_stream) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  c->user_stream = static_cast<hipStream_t>(hip_stream);
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_sync(spray_rt_ctx_t c) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_domain_upload(spray_rt_ctx_t c, int slot, const float* verts,
+                           size_t nverts, const uint32_t* faces, size_t nfaces,
+                           const uint32_t* colors, const float* normals,
+                           int async) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (slot < 0 || slot > 1 << 20)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad slot %d", slot);
+  if ((nverts && !verts) || (nfaces && !faces))
+    return fail(c, SPRAY_RT_ERR_ARG, "null mesh arrays");
+  BvhImage img;
+  if (!build_bvh(verts, nverts, faces, nfaces, &img))
+    return fail(c, SPRAY_RT_ERR_ARG, "face index out of range or mesh too large");
+  if (size_t(slot) >= c->slots.size()) c->slots.resize(slot + 1);
+  SlotHost& sh = c->slots[slot];
+  HIPCHK(c, hipSetDevice(c->device));
+  // the previous image may still be read by queued work
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
+  if (sh.ready) HIPCHK(c, hipEventSynchronize(sh.ready));
+
+  const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
+  const size_t b_tris = align256(img.tris.size() * sizeof(float));
+  const size_t b_prims = align256(img.prims.size() * sizeof(uint32_t));
+  const size_t b_faces = align256(3 * nfaces * sizeof(uint32_t));
+  const size_t b_colors = colors ? align256(nverts * sizeof(uint32_t)) : 0;
+  const size_t b_normals = normals ? align256(3 * nverts * sizeof(float)) : 0;
+  const size_t total =
+      std::max<size_t>(256, b_nodes + b_tris + b_prims + b_faces + b_colors + b_normals);
+  if (sh.bytes < total) {
+    if (sh.dmem) HIPCHK(c, hipFree(sh.dmem));
+    sh.dmem = nullptr;
+    sh.bytes = 0;
+    HIPCHK(c, hipMalloc(&sh.dmem, total));
+    sh.bytes = total;
+  }
+  // host image of the slot (pinned when async)
+  std::vector<char> tmp;
+  char* host;
+  if (async) {
+    if (sh.pinned_bytes < total) {
+      if (sh.pinned) HIPCHK(c, hipHostFree(sh.pinned));
+      sh.pinned = nullptr;
+      HIPCHK(c, hipHostMalloc(&sh.pinned, total, hipHostMallocDefault));
+      sh.pinned_bytes = total;
+    }
+    host = static_cast<char*>(sh.pinned);
+  } else {
+    tmp.resize(total);
+    host = tmp.data();
+  }
+  size_t off = 0;
+  auto put = [&](const void* src, size_t n, size_t padded) {
+    if (n) std::memcpy(host + off, src, n);
+    size_t o = off;
+    off += padded;
+    return o;
+  };
+  const size_t o_nodes = put(img.nodes.data(), img.nodes.size() * sizeof(BvhNode), b_nodes);
+  const size_t o_tris = put(img.tris.data(), img.tris.size() * sizeof(float), b_tris);
+  const size_t o_prims = put(img.prims.data(), img.prims.size() * sizeof(uint32_t), b_prims);
+  const size_t o_faces = put(faces, 3 * nfaces * sizeof(uint32_t), b_faces);
+  const size_t o_colors = colors ? put(colors, nverts * sizeof(uint32_t), b_colors) : 0;
+  const size_t o_normals = normals ? put(normals, 3 * nverts * sizeof(float), b_normals) : 0;
+  char* d = static_cast<char*>(sh.dmem);
+  if (async) {
+    if (!sh.ready) HIPCHK(c, hipEventCreateWithFlags(&sh.ready, hipEventDisableTiming));
+    HIPCHK(c, hipMemcpyAsync(d, host, off, hipMemcpyHostToDevice, c->upload_stream));
+    HIPCHK(c, hipEventRecord(sh.ready, c->upload_stream));
+  } else {
+    HIPCHK(c, hipMemcpy(d, host, off, hipMemcpyHostToDevice));
+  }
+  SlotDesc& desc = sh.desc;
+  desc.nodes = reinterpret_cast<const BvhNode*>(d + o_nodes);
+  desc.tris = reinterpret_cast<const float*>(d + o_tris);
+  desc.prims = reinterpret_cast<const uint32_t*>(d + o_prims);
+  desc.faces = reinterpret_cast<const uint32_t*>(d + o_faces);
+  desc.colors = colors ? reinterpret_cast<const uint32_t*>(d + o_colors) : nullptr;
+  desc.normals = normals ? reinterpret_cast<const float*>(d + o_normals) : nullptr;
+  desc.ntris = uint32_t(img.prims.size());
+  desc.nverts = uint32_t(nverts);
+  desc.nnodes = uint32_t(img.nodes.size());
+  sh.depth = img.depth;
+  c->slots_dirty = true;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_bvh_build_host(const float* verts, size_t nverts,
+                            const uint32_t* faces, size_t nfaces,
+                            size_t* nnodes, int* depth, void* nodes_out,
+                            float* tris_out, uint32_t* prims_out) {
+  if ((nverts && !verts) || (nfaces && !faces)) return SPRAY_RT_ERR_ARG;
+  BvhImage img;
+  if (!build_bvh(verts, nverts, faces, nfaces, &img)) return SPRAY_RT_ERR_ARG;
+  if (nnodes) *nnodes = img.nodes.size();
+  if (depth) *depth = img.depth;
+  if (nodes_out)
+    std::memcpy(nodes_out, img.nodes.data(), img.nodes.size() * sizeof(BvhNode));
+  if (tris_out) std::memcpy(tris_out, img.tris.data(), img.tris.size() * sizeof(float));
+  if (prims_out)
+    std::memcpy(prims_out, img.prims.data(), img.prims.size() * sizeof(uint32_t));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_domain_release(spray_rt_ctx_t c, int slot) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (slot < 0 || size_t(slot) >= c->slots.size())
+    return fail(c, SPRAY_RT_ERR_ARG, "bad slot %d", slot);
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
+  SlotHost& sh = c->slots[slot];
+  if (sh.ready) HIPCHK(c, hipEventSynchronize(sh.ready));
+  if (sh.dmem) HIPCHK(c, hipFree(sh.dmem));
+  sh.dmem = nullptr;
+  sh.bytes = 0;
+  sh.desc = SlotDesc{};
+  c->slots_dirty = true;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_slot_info(spray_rt_ctx_t c, int slot, size_t* nnodes, int* depth,
+                       size_t* ntris) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  int r = check_slot(c, slot);
+  if (r) return r;
+  const SlotHost& sh = c->slots[slot];
+  if (nnodes) *nnodes = sh.desc.nnodes;
+  if (depth) *depth = sh.depth;
+  if (ntris) *ntris = sh.desc.ntris;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (ndomains < 0 || (ndomains && !boxes))
+    return fail(c, SPRAY_RT_ERR_ARG, "bad domain bounds");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
+  if (c->d_boxes) HIPCHK(c, hipFree(c->d_boxes));
+  if (c->d_dom2slot) HIPCHK(c, hipFree(c->d_dom2slot));
+  c->d_boxes = nullptr;
+  c->d_dom2slot = nullptr;
+  c->ndom = ndomains;
+  c->dom2slot.assign(ndomains, -1);
+  c->dom_dirty = true;
+  if (ndomains == 0) return SPRAY_RT_OK;
+  HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_boxes), 6 * ndomains * sizeof(float)));
+  HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_dom2slot), ndomains * sizeof(int)));
+  HIPCHK(c, hipMemcpy(c->d_boxes, boxes, 6 * ndomains * sizeof(float),
+                      hipMemcpyHostToDevice));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_map_domain(spray_rt_ctx_t c, int domain_id, int slot) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (domain_id < 0 || domain_id >= c->ndom)
+    return fail(c, SPRAY_RT_ERR_ARG, "domain %d out of range", domain_id);
+  if (slot >= 0) {
+    int r = check_slot(c, slot);
+    if (r) return r;
+  }
+  c->dom2slot[domain_id] = slot < 0 ? -1 : slot;
+  c->dom_dirty = true;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_intersect1M(spray_rt_ctx_t c, int slot, void* rays, size_t M,
+                         size_t stride) {
+  size_t off[2] = {0, M};
+  return run_rtc(c, &slot, off, 1, rays, stride, launch_rtc_intersect);
+}
+
+int spray_rt_occluded1M(spray_rt_ctx_t c, int slot, void* rays, size_t M,
+                        size_t stride) {
+  size_t off[2] = {0, M};
+  return run_rtc(c, &slot, off, 1, rays, stride, launch_rtc_occluded);
+}
+
+int spray_rt_intersect_segments(spray_rt_ctx_t c, const int* slots,
+                                const size_t* offsets, int nseg, void* rays,
+                                size_t stride) {
+  return run_rtc(c, slots, offsets, nseg, rays, stride, launch_rtc_intersect);
+}
+
+int spray_rt_occluded_segments(spray_rt_ctx_t c, const int* slots,
+                               const size_t* offsets, int nseg, void* rays,
+                               size_t stride) {
+  return run_rtc(c, slots, offsets, nseg, rays, stride, launch_rtc_occluded);
+}
+
+int spray_rt_domains1M(spray_rt_ctx_t c, const float* org, const float* dir,
+                       size_t M, int* ids, float* ts, int* counts, int maxhits) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (maxhits <= 0) return fail(c, SPRAY_RT_ERR_ARG, "maxhits must be > 0");
+  if (c->ndom == 0) return fail(c, SPRAY_RT_ERR_STATE, "no domain bounds set");
+  if (M == 0) return SPRAY_RT_OK;
+  if (!org || !dir || !ids || !ts || !counts)
+    return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = stream_of(c);
+  const bool dev = is_device_ptr(org);
+  if (dev) {
+    HIPCHK(c, launch_domains(s, c->d_boxes, c->ndom, org, dir, M, ids, ts,
+                             counts, maxhits));
+    return SPRAY_RT_OK;
+  }
+  const size_t b_in = 3 * M * sizeof(float);
+  const size_t b_ids = M * maxhits * sizeof(int);
+  const size_t b_cnt = M * sizeof(int);
+  int r = ensure(c, &c->d_stage, &c->stage_cap, 2 * b_in);
+  if (r) return r;
+  r = ensure(c, &c->d_stage2, &c->stage2_cap, 2 * b_ids);
+  if (r) return r;
+  r = ensure(c, &c->d_stage3, &c->stage3_cap, b_cnt);
+  if (r) return r;
+  char* din = static_cast<char*>(c->d_stage);
+  char* dout = static_cast<char*>(c->d_stage2);
+  HIPCHK(c, hipMemcpyAsync(din, org, b_in, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(din + b_in, dir, b_in, hipMemcpyHostToDevice, s));
+  HIPCHK(c, launch_domains(s, c->d_boxes, c->ndom, reinterpret_cast<float*>(din),
+                           reinterpret_cast<float*>(din + b_in), M,
+                           reinterpret_cast<int*>(dout),
+                           reinterpret_cast<float*>(dout + b_ids),
+                           static_cast<int*>(c->d_stage3), maxhits));
+  HIPCHK(c, hipMemcpyAsync(ids, dout, b_ids, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(ts, dout + b_ids, b_ids, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(counts, c->d_stage3, b_cnt, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return SPRAY_RT_OK;
+}
+
+static int scene_common(spray_rt_ctx* c, const void* rays, size_t M,
+                        const void* out) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (c->ndom <= 0) return fail(c, SPRAY_RT_ERR_STATE, "no domain bounds set");
+  if (c->ndom > SPRAY_RT_MAX_SCENE_DOMAINS)
+    return fail(c, SPRAY_RT_ERR_LIMIT, "scene path supports <= %d domains",
+                SPRAY_RT_MAX_SCENE_DOMAINS);
+  if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  return prepare(c);
+}
+
+// counters: optional device uint64[3] (nodes, tris, visits); exported for the
+// canonical-count tests and the bench's byte accounting cross-check.
+extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
+                                                const spray_rt_ray* rays,
+                                                size_t M, spray_rt_hit* hits,
+                                                unsigned long long* d_counters) {
+  int r = scene_common(c, rays, M, hits);
+  if (r) return r;
+  if (M == 0) return SPRAY_RT_OK;
+  hipStream_t s = stream_of(c);
+  if (is_device_ptr(rays)) {
+    HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
+                                     c->ndom, rays, M, hits, d_counters));
+    return SPRAY_RT_OK;
+  }
+  r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
+  if (r) return r;
+  r = ensure(c, &c->d_stage2, &c->stage2_cap, M * sizeof(spray_rt_hit));
+  if (r) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, M * sizeof(spray_rt_ray),
+                           hipMemcpyHostToDevice, s));
+  HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
+                                   c->ndom, static_cast<spray_rt_ray*>(c->d_stage),
+                                   M, static_cast<spray_rt_hit*>(c->d_stage2),
+                                   d_counters));
+  HIPCHK(c, hipMemcpyAsync(hits, c->d_stage2, M * sizeof(spray_rt_hit),
+                           hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return SPRAY_RT_OK;
+}
+
+extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
+                                               const spray_rt_ray* rays,
+                                               size_t M, uint8_t* occ,
+                                               unsigned long long* d_counters) {
+  int r = scene_common(c, rays, M, occ);
+  if (r) return r;
+  if (M == 0) return SPRAY_RT_OK;
+  hipStream_t s = stream_of(c);
+  if (is_device_ptr(rays)) {
+    HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
+                                    c->ndom, rays, M, nullptr, occ, d_counters));
+    return SPRAY_RT_OK;
+  }
+  r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
+  if (r) return r;
+  r = ensure(c, &c->d_stage2, &c->stage2_cap, M);
+  if (r) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, M * sizeof(spray_rt_ray),
+                           hipMemcpyHostToDevice, s));
+  HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
+                                  c->ndom, static_cast<spray_rt_ray*>(c->d_stage),
+                                  M, nullptr, static_cast<uint8_t*>(c->d_stage2),
+                                  d_counters));
+  HIPCHK(c, hipMemcpyAsync(occ, c->d_stage2, M, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return SPRAY_RT_OK;
+}
+
+extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
+                                                const spray_rt_ray* rays,
+                                                size_t max_rays,
+                                                const uint32_t* d_count,
+                                                uint8_t* occ,
+                                                unsigned long long* d_counters) {
+  int r = scene_common(c, rays, max_rays, occ);
+  if (r) return r;
+  if (max_rays == 0) return SPRAY_RT_OK;
+  if (!is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(d_count))
+    return fail(c, SPRAY_RT_ERR_ARG, "devcount variant needs device buffers");
+  HIPCHK(c, launch_scene_occluded(stream_of(c), c->d_slots, c->d_dom2slot,
+                                  c->d_boxes, c->ndom, rays, max_rays, d_count,
+                                  occ, d_counters));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_intersect_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                             size_t M, spray_rt_hit* hits) {
+  return spray_rt_intersect_scene_counted(c, rays, M, hits, nullptr);
+}
+
+int spray_rt_occluded_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                            size_t M, uint8_t* occluded) {
+  return spray_rt_occluded_scene_counted(c, rays, M, occluded, nullptr);
+}
+
+int spray_rt_eye_rays_ooc(spray_rt_ctx_t c, const float cam[14], int image_w,
+                          int spp, int tx, int ty, int tw, int th,
+                          spray_rt_ray* rays, int32_t* pixid, int32_t* samid) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (!cam || spp <= 0 || tw < 0 || th < 0)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad eye-ray arguments");
+  if (size_t(tw) * th * spp == 0) return SPRAY_RT_OK;
+  if (!is_device_ptr(rays) || (pixid && !is_device_ptr(pixid)) ||
+      (samid && !is_device_ptr(samid)))
+    return fail(c, SPRAY_RT_ERR_ARG, "eye-ray buffers must be device memory");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, launch_eye_rays_ooc(stream_of(c), cam, image_w, spp, tx, ty, tw, th,
+                                rays, pixid, samid));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_spawn_shadows_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                              const spray_rt_hit* hits, size_t M,
+                              const float shade[10], spray_rt_ray* out_rays,
+                              int32_t* out_src, uint32_t* d_count) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (!shade || !d_count) return fail(c, SPRAY_RT_ERR_ARG, "null argument");
+  if (M && (!is_device_ptr(rays) || !is_device_ptr(hits) ||
+            !is_device_ptr(out_rays) || !is_device_ptr(d_count)))
+    return fail(c, SPRAY_RT_ERR_ARG, "spawn buffers must be device memory");
+  HIPCHK(c, hipSetDevice(c->device));
+  size_t nb = (M + kBlock - 1) / kBlock + 1;
+  void* bc = c->d_block_counts;
+  int r = ensure(c, &bc, &c->block_cap, nb * sizeof(uint32_t));
+  if (r) return r;
+  c->d_block_counts = static_cast<uint32_t*>(bc);
+  HIPCHK(c, launch_spawn_pt(stream_of(c), rays, hits, M, shade, out_rays,
+                            out_src, d_count, c->d_block_counts));
+  return SPRAY_RT_OK;
+}
+
+}  // extern "C"

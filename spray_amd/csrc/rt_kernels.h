@@ -1,0 +1,53 @@
+// rt_kernels.h -- host-side launchers of the gfx950 kernels (rt_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_common.h"
+#include "spray_rt.h"
+
+namespace spray_rt {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// Per-slot streams over Embree record layouts (RTCRayIntersection / RTCRay)
+// with a byte stride.  seg_off has nseg+1 entries, seg_slot nseg (device).
+hipError_t launch_rtc_intersect(hipStream_t s, const SlotDesc* slots,
+                                const int* seg_slot, const size_t* seg_off,
+                                int nseg, char* rays, size_t stride, size_t M);
+hipError_t launch_rtc_occluded(hipStream_t s, const SlotDesc* slots,
+                               const int* seg_slot, const size_t* seg_off,
+                               int nseg, char* rays, size_t stride, size_t M);
+
+hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
+                          const float* org, const float* dir, size_t M,
+                          int* ids, float* ts, int* counts, int maxhits);
+
+// Fused scene path: domain list + per-domain traversal + epilogue.
+// counters (optional, device uint64[3]: nodes, tris, visits) enable the
+// counting variant used to verify the canonical traversal.
+hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
+                                  const int* dom2slot, const float* boxes,
+                                  int ndom, const spray_rt_ray* rays, size_t M,
+                                  spray_rt_hit* hits,
+                                  unsigned long long* counters);
+hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
+                                 const int* dom2slot, const float* boxes,
+                                 int ndom, const spray_rt_ray* rays, size_t M,
+                                 const uint32_t* d_count, uint8_t* occluded,
+                                 unsigned long long* counters);
+
+hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
+                               int spp, int tx, int ty, int tw, int th,
+                               spray_rt_ray* rays, int32_t* pixid,
+                               int32_t* samid);
+
+// Deterministic (ascending source index) compaction of PT shadow rays.
+// block_counts: device scratch of ceil(M/kBlock) + 1 uint32.
+hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
+                           const spray_rt_hit* hits, size_t M,
+                           const float* shade10, spray_rt_ray* out_rays,
+                           int32_t* out_src, uint32_t* d_count,
+                           uint32_t* block_counts);
+
+}  // namespace spray_rt

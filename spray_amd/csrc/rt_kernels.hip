@@ -1,0 +1,785 @@
+// rt_kernels.hip -- gfx950 kernels of the intersect / occluded hot path.
+//
+// One lane = one ray.  Per lane: a short traversal stack in LDS laid out
+// [depth][lane] (consecutive lanes hit consecutive banks), BVH2 nodes read as
+// four 16-B loads, triangles as three 16-B loads.  Compiled with
+// -ffp-contract=off: every fused multiply-add below is an explicit fmaf(), so
+// t/u/v/Ng are bit-identical to the CPU oracle (oracle/oracle.c) and to every
+// other kernel here -- VBuf compares t with == (ooc_vbuf.cc:41-52).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "rt_common.h"
+#include "rt_kernels.h"
+
+namespace spray_rt {
+namespace {
+
+constexpr float kInf = __builtin_inff();
+constexpr int32_t kNone = INT_MAX;
+
+// ---------------------------------------------------------------------------
+// ray / box / triangle primitives
+// ---------------------------------------------------------------------------
+struct Ray {
+  float ox, oy, oz;
+  float dx, dy, dz;
+  float ix, iy, iz;     // 1/d with |d| clamped at kDirClamp (culling only)
+  float oix, oiy, oiz;  // o * inv
+};
+
+__device__ __forceinline__ float clamp_dir(float d) {
+  return fabsf(d) < kDirClamp ? copysignf(kDirClamp, d) : d;
+}
+
+__device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx,
+                                        float dy, float dz) {
+  Ray r;
+  r.ox = ox; r.oy = oy; r.oz = oz;
+  r.dx = dx; r.dy = dy; r.dz = dz;
+  r.ix = 1.0f / clamp_dir(dx);
+  r.iy = 1.0f / clamp_dir(dy);
+  r.iz = 1.0f / clamp_dir(dz);
+  r.oix = ox * r.ix;
+  r.oiy = oy * r.iy;
+  r.oiz = oz * r.iz;
+  return r;
+}
+
+// Conservative slab test of a (padded) node box against [tnear, tfar].
+__device__ __forceinline__ bool slab(const Ray& r, float lx, float ly, float lz,
+                                     float hx, float hy, float hz, float tnear,
+                                     float tfar, float& tenter) {
+  float t0x = fmaf(lx, r.ix, -r.oix), t1x = fmaf(hx, r.ix, -r.oix);
+  float t0y = fmaf(ly, r.iy, -r.oiy), t1y = fmaf(hy, r.iy, -r.oiy);
+  float t0z = fmaf(lz, r.iz, -r.oiz), t1z = fmaf(hz, r.iz, -r.oiz);
+  float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)),
+                     fmaxf(fminf(t0z, t1z), tnear));
+  float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)),
+                     fminf(fmaxf(t0z, t1z), tfar * kTfarSlack));
+  tenter = tmin;
+  return tmin <= tmax;
+}
+
+// Embree 2.17 MoellerTrumboreIntersector1 restated (e1 = v0-v1, e2 = v2-v0,
+// Ng = e1 x e2; edge tests scaled by |den|); t, u, v by IEEE division.
+// Record: a = v0.xyz e1.x | b = e1.yz e2.xy | c = e2.z Ng.xyz
+__device__ __forceinline__ bool tri_test(const Ray& r, float tnear, float4 a,
+                                         float4 b, float4 c, float& t,
+                                         float& u, float& v) {
+  const float cx = a.x - r.ox, cy = a.y - r.oy, cz = a.z - r.oz;
+  const float rx = fmaf(r.dy, cz, -(r.dz * cy));
+  const float ry = fmaf(r.dz, cx, -(r.dx * cz));
+  const float rz = fmaf(r.dx, cy, -(r.dy * cx));
+  const float den = fmaf(c.w, r.dz, fmaf(c.z, r.dy, c.y * r.dx));
+  const float absden = fabsf(den);
+  float U = fmaf(rz, c.x, fmaf(ry, b.w, rx * b.z));  // R . e2
+  float V = fmaf(rz, b.y, fmaf(ry, b.x, rx * a.w));  // R . e1
+  float T = fmaf(c.w, cz, fmaf(c.z, cy, c.y * cx));  // Ng . C
+  if (den < 0.0f) {
+    U = -U;
+    V = -V;
+    T = -T;
+  }
+  if (!(den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden)) return false;
+  const float tt = T / absden;
+  if (!(tt > tnear)) return false;
+  t = tt;
+  u = U / absden;
+  v = V / absden;
+  return true;
+}
+
+// Reference domain-box test: intersectAabb (src/render/aabb.h:139-169) with
+// t0 = SPRAY_RAY_EPSILON, t1 = +inf (RTCRayExt::reset, rays.h:149-169).  The
+// exact float ops of the reference (division-based inverse, sub then mul).
+struct DRay {
+  float ox, oy, oz, ix, iy, iz;
+};
+__device__ __forceinline__ DRay make_dray(float ox, float oy, float oz,
+                                          float dx, float dy, float dz) {
+  DRay r;
+  r.ox = ox; r.oy = oy; r.oz = oz;
+  r.ix = 1.0f / dx;
+  r.iy = 1.0f / dy;
+  r.iz = 1.0f / dz;
+  return r;
+}
+__device__ __forceinline__ bool aabb_ref(const float* box, const DRay& r,
+                                         float& tmin_out) {
+  const bool sx = r.ix < 0.0f, sy = r.iy < 0.0f, sz = r.iz < 0.0f;
+  float tmin = ((sx ? box[3] : box[0]) - r.ox) * r.ix;
+  float tmax = ((sx ? box[0] : box[3]) - r.ox) * r.ix;
+  const float tymin = ((sy ? box[4] : box[1]) - r.oy) * r.iy;
+  const float tymax = ((sy ? box[1] : box[4]) - r.oy) * r.iy;
+  if ((tmin > tymax) || (tymin > tmax)) return false;
+  if (tymin > tmin) tmin = tymin;
+  if (tymax < tmax) tmax = tymax;
+  const float tzmin = ((sz ? box[5] : box[2]) - r.oz) * r.iz;
+  const float tzmax = ((sz ? box[2] : box[5]) - r.oz) * r.iz;
+  if ((tmin > tzmax) || (tzmin > tmax)) return false;
+  if (tzmin > tmin) tmin = tzmin;
+  if (tzmax < tmax) tmax = tzmax;
+  tmin_out = tmin;
+  return (tmin < kInf) && (tmax > kRayEpsilon);
+}
+
+// ---------------------------------------------------------------------------
+// BVH2 traversal of one slot (canonical order, see oracle.c traverse())
+// ---------------------------------------------------------------------------
+struct Best {
+  float t, u, v;
+  uint32_t prim;  // PLY face index (tie-break key)
+  uint32_t leaf;  // leaf-order triangle index (Ng lookup)
+};
+
+// ANY = occlusion (returns true at the first hit with t <= tfar_any).
+// Closest hit: keeps the lexicographic minimum of (t, prim) starting from
+// best; a candidate with t == best.t wins only with a smaller face index.
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
+                                           float tnear, float tfar_any,
+                                           Best& best, int32_t* stk,
+                                           unsigned& nnode, unsigned& ntri) {
+  const float4* __restrict__ nodes = reinterpret_cast<const float4*>(s.nodes);
+  const float4* __restrict__ tris = reinterpret_cast<const float4*>(s.tris);
+  const uint32_t* __restrict__ prims = s.prims;
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const float4* np = nodes + 4 * cur;
+    const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+    if (COUNT) ++nnode;
+    const float tcut = ANY ? tfar_any : best.t;
+    float tl, tr;
+    const bool hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tcut, tl);
+    const bool hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tcut, tr);
+    int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+    bool h0 = hl, h1 = hr;
+    if (hl && hr && tr < tl) {
+      const int32_t x = c0;
+      c0 = c1;
+      c1 = x;
+    } else if (!hl && hr) {
+      c0 = c1;
+      h0 = true;
+      h1 = false;
+    }
+    int32_t next = kNone;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int32_t c = k == 0 ? c0 : c1;
+      const bool h = k == 0 ? h0 : h1;
+      if (!h) continue;
+      if (c < 0) {
+        const uint32_t enc = ~uint32_t(c);
+        const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
+        for (uint32_t q = 0; q < cnt; ++q) {
+          const uint32_t p = first + q;
+          const float4 a = tris[3 * p], b = tris[3 * p + 1], cc = tris[3 * p + 2];
+          if (COUNT) ++ntri;
+          float t, u, v;
+          if (!tri_test(r, tnear, a, b, cc, t, u, v)) continue;
+          if (ANY) {
+            if (t <= tfar_any) return true;
+          } else {
+            const uint32_t pid = prims[p];
+            if (t < best.t || (t == best.t && pid < best.prim)) {
+              best.t = t;
+              best.u = u;
+              best.v = v;
+              best.prim = pid;
+              best.leaf = p;
+            }
+          }
+        }
+      } else if (next == kNone) {
+        next = c;
+      } else {
+        stk[sp * kBlock] = c;
+        ++sp;
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = stk[sp * kBlock];
+    }
+    cur = next;
+  }
+  return false;
+}
+
+// TriMeshBuffer::updateIntersection (src/render/trimesh_buffer.cc:328-360).
+__device__ __forceinline__ void epilogue(const SlotDesc& s, uint32_t prim,
+                                         float u, float v, uint32_t& color,
+                                         float& nsx, float& nsy, float& nsz) {
+  const uint32_t f0 = s.faces[3 * prim], f1 = s.faces[3 * prim + 1],
+                 f2 = s.faces[3 * prim + 2];
+  const float w = 1.f - u - v;
+  if (s.colors) {
+    const uint32_t c0 = s.colors[f0], c1 = s.colors[f1], c2 = s.colors[f2];
+    uint32_t ch[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int sh = 16 - 8 * k;
+      const float a = float((c0 >> sh) & 0xffu), b = float((c1 >> sh) & 0xffu),
+                  c = float((c2 >> sh) & 0xffu);
+      ch[k] = uint32_t((a * w + b * u) + c * v);
+    }
+    color = (ch[0] << 16) | (ch[1] << 8) | ch[2];
+  } else {
+    color = 0;
+  }
+  if (s.normals) {
+    const float* n0 = s.normals + 3 * f0;
+    const float* n1 = s.normals + 3 * f1;
+    const float* n2 = s.normals + 3 * f2;
+    nsx = (n0[0] * w + n1[0] * u) + n2[0] * v;
+    nsy = (n0[1] * w + n1[1] * u) + n2[1] * v;
+    nsz = (n0[2] * w + n1[2] * u) + n2[2] * v;
+  } else {
+    nsx = nsy = nsz = 0.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Embree-layout streams (RTCRayIntersection / RTCRay, byte stride)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int find_segment(const size_t* off, int nseg,
+                                            size_t i) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {  // last segment with off[seg] <= i
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rtc_intersect(
+    const SlotDesc* __restrict__ slots, const int* __restrict__ seg_slot,
+    const size_t* __restrict__ seg_off, int nseg, char* __restrict__ rays,
+    size_t stride, size_t M) {
+  __shared__ int32_t stack[kStack * kBlock];
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= M) return;
+  const int seg = nseg == 1 ? 0 : find_segment(seg_off, nseg, i);
+  const int slot = seg_slot[seg];
+  const SlotDesc s = slots[slot];
+  char* rec = rays + i * stride;
+  const float* f = reinterpret_cast<const float*>(rec);
+  const Ray r = make_ray(f[0], f[1], f[2], f[4], f[5], f[6]);
+  const float tnear = f[8];
+  Best best{f[9], 0.f, 0.f, 0xFFFFFFFFu, 0u};
+  unsigned a = 0, b = 0;
+  if (s.nnodes)
+    trace_slot<false, false>(s, r, tnear, 0.f, best, stack + threadIdx.x, a, b);
+  if (best.prim == 0xFFFFFFFFu) return;  // miss: record untouched
+  const float4 c = reinterpret_cast<const float4*>(s.tris)[3 * best.leaf + 2];
+  uint32_t color;
+  float nsx, nsy, nsz;
+  epilogue(s, best.prim, best.u, best.v, color, nsx, nsy, nsz);
+  float* o = reinterpret_cast<float*>(rec);
+  uint32_t* ou = reinterpret_cast<uint32_t*>(rec);
+  o[9] = best.t;          // tfar
+  o[12] = c.y;            // Ng
+  o[13] = c.z;
+  o[14] = c.w;
+  ou[15] = color;         // color (offset 60)
+  o[16] = best.u;
+  o[17] = best.v;
+  ou[18] = 0u;            // geomID (one mesh per slot)
+  ou[19] = best.prim;     // primID
+  o[21] = nsx;            // Ns (offset 84)
+  o[22] = nsy;
+  o[23] = nsz;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rtc_occluded(
+    const SlotDesc* __restrict__ slots, const int* __restrict__ seg_slot,
+    const size_t* __restrict__ seg_off, int nseg, char* __restrict__ rays,
+    size_t stride, size_t M) {
+  __shared__ int32_t stack[kStack * kBlock];
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= M) return;
+  const int seg = nseg == 1 ? 0 : find_segment(seg_off, nseg, i);
+  const SlotDesc s = slots[seg_slot[seg]];
+  char* rec = rays + i * stride;
+  const float* f = reinterpret_cast<const float*>(rec);
+  const Ray r = make_ray(f[0], f[1], f[2], f[4], f[5], f[6]);
+  Best best{0.f, 0.f, 0.f, 0u, 0u};
+  unsigned a = 0, b = 0;
+  if (s.nnodes &&
+      trace_slot<true, false>(s, r, f[8], f[9], best, stack + threadIdx.x, a, b))
+    reinterpret_cast<uint32_t*>(rec)[18] = 0u;  // geomID = 0: occluded
+}
+
+// ---------------------------------------------------------------------------
+// domain lists (WbvhEmbree::intersect + DomainList::sort)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_domains(
+    const float* __restrict__ boxes, int ndom, const float* __restrict__ org,
+    const float* __restrict__ dir, size_t M, int* __restrict__ ids,
+    float* __restrict__ ts, int* __restrict__ counts, int maxhits) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= M) return;
+  const DRay r = make_dray(org[3 * i], org[3 * i + 1], org[3 * i + 2],
+                           dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+  // selection: k-th entry = smallest (t, id) strictly after the previous one
+  float pt = -kInf;
+  int pid = -1;
+  int n = 0;
+  for (; n < maxhits; ++n) {
+    float bt = kInf;
+    int bid = -1;
+    for (int b = 0; b < ndom; ++b) {
+      float tm;
+      if (!aabb_ref(boxes + 6 * b, r, tm)) continue;
+      const bool after = tm > pt || (tm == pt && b > pid);
+      if (!after) continue;
+      if (bid < 0 || tm < bt) {
+        bt = tm;
+        bid = b;
+      }
+    }
+    if (bid < 0) break;
+    ids[i * maxhits + n] = bid;
+    ts[i * maxhits + n] = bt;
+    pt = bt;
+    pid = bid;
+  }
+  counts[i] = n;
+}
+
+// ---------------------------------------------------------------------------
+// fused scene path
+// ---------------------------------------------------------------------------
+// Domains of a ray are visited in (tmin, id) order (DomainList::sort); the
+// closest hit is carried across domains, a later domain replacing it only
+// when strictly nearer -- the earlier list entry wins a tie.
+template <int W, bool ANY, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_scene(
+    const SlotDesc* __restrict__ slots, const int* __restrict__ dom2slot,
+    const float* __restrict__ boxes, int ndom,
+    const spray_rt_ray* __restrict__ rays, size_t M,
+    const uint32_t* __restrict__ d_count, spray_rt_hit* __restrict__ hits,
+    uint8_t* __restrict__ occ, unsigned long long* __restrict__ counters) {
+  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ float sbox[6 * 64 * W];
+  if (d_count) {  // ray count produced on the device (spawned shadow rays)
+    const size_t dc = *d_count;
+    M = dc < M ? dc : M;
+    if (size_t(blockIdx.x) * kBlock >= M) return;  // whole block idle
+  }
+  for (int k = threadIdx.x; k < 6 * ndom; k += kBlock) sbox[k] = boxes[k];
+  __syncthreads();
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  unsigned nnode = 0, ntri = 0, nvisit = 0;
+  if (i < M) {
+    const float4* rp = reinterpret_cast<const float4*>(rays + i);
+    const float4 o4 = rp[0], d4 = rp[1];
+    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    uint64_t m[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint64_t bits = 0;
+      const int lim = min(64, ndom - 64 * w);
+      for (int j = 0; j < lim; ++j) {
+        float tm;
+        if (aabb_ref(sbox + 6 * (64 * w + j), dr, tm)) bits |= 1ull << j;
+      }
+      m[w] = bits;
+    }
+    Best best{ANY ? 0.f : d4.w, 0.f, 0.f, 0xFFFFFFFFu, 0u};
+    int best_dom = -1;
+    bool occluded = false;
+    int32_t* stk = stack + threadIdx.x;
+    for (;;) {
+      float st = kInf;
+      int sb = -1;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t bits = m[w];
+        while (bits) {
+          const int j = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          const int b = 64 * w + j;
+          float tm;
+          aabb_ref(sbox + 6 * b, dr, tm);
+          if (sb < 0 || tm < st) {
+            st = tm;
+            sb = b;
+          }
+        }
+      }
+      if (sb < 0) break;
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
+      const int slot = dom2slot[sb];
+      if (slot < 0) continue;
+      const SlotDesc s = slots[slot];
+      if (!s.nnodes) continue;
+      if (COUNT) ++nvisit;
+      if (ANY) {
+        if (trace_slot<true, COUNT>(s, r, o4.w, d4.w, best, stk, nnode, ntri)) {
+          occluded = true;
+          break;
+        }
+      } else {
+        Best local = best;
+        if (best_dom >= 0) local.prim = 0u;  // strictly nearer from now on
+        trace_slot<false, COUNT>(s, r, o4.w, 0.f, local, stk, nnode, ntri);
+        if (local.t < best.t || (best_dom < 0 && local.prim != 0xFFFFFFFFu)) {
+          best = local;
+          best_dom = sb;
+        }
+      }
+    }
+    if (ANY) {
+      occ[i] = occluded ? 1 : 0;
+    } else {
+      float4 h0, h1, h2;
+      if (best_dom < 0) {
+        h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+        h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+        h2 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+      } else {
+        const SlotDesc s = slots[dom2slot[best_dom]];
+        const float4 c = reinterpret_cast<const float4*>(s.tris)[3 * best.leaf + 2];
+        uint32_t color;
+        float nsx, nsy, nsz;
+        epilogue(s, best.prim, best.u, best.v, color, nsx, nsy, nsz);
+        h0 = make_float4(best.t, best.u, best.v, __uint_as_float(best.prim));
+        h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
+        h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
+      }
+      float4* hp = reinterpret_cast<float4*>(hits + i);
+      hp[0] = h0;
+      hp[1] = h1;
+      hp[2] = h2;
+    }
+  }
+  if (COUNT) {
+    atomicAdd(&counters[0], (unsigned long long)nnode);
+    atomicAdd(&counters[1], (unsigned long long)ntri);
+    atomicAdd(&counters[2], (unsigned long long)nvisit);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ray sources
+// ---------------------------------------------------------------------------
+struct Cam {
+  float p[14];
+};
+
+__device__ __forceinline__ uint32_t mm_mix(uint32_t hash, uint32_t k) {
+  k *= 0xcc9e2d51u;
+  k = (k << 15) | (k >> 17);
+  k *= 0x1b873593u;
+  hash ^= k;
+  hash = ((hash << 13) | (hash >> 19)) * 5u + 0xe6546b64u;
+  return hash;
+}
+__device__ __forceinline__ uint32_t mm_fin(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ float sampler_1d(uint32_t& s) {
+  s = s * 1664525u + 1013904223u;
+  return float(int32_t(s >> 1)) * 4.656612873077392578125e-10f;
+}
+
+// ooc::Tracer::genMultiEyes (src/ooc/ooc_tracer.inl:124-172) + Camera::
+// generateRay (camera.h:168-209), glm operand order.
+__global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
+    Cam cam, int image_w, int spp, int tx, int ty, int tw, int th,
+    spray_rt_ray* __restrict__ rays, int32_t* __restrict__ pixid,
+    int32_t* __restrict__ samid) {
+  const size_t bufid = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const size_t n = size_t(tw) * th * spp;
+  if (bufid >= n) return;
+  const int s = int(bufid % spp);
+  const int p = int(bufid / spp);
+  const int x0 = p % tw, y0 = p / tw;
+  const int x = tx + x0, y = ty + y0;
+  float fx = float(x), fy = float(y);
+  if (spp > 1) {
+    uint32_t st = mm_fin(mm_mix(0u, uint32_t(bufid)));
+    fx = float(x) + sampler_1d(st);
+    fy = float(y) + sampler_1d(st);
+  }
+  const float* c = cam.p;
+  const float u = fx / c[12], v = fy / c[13];
+  float dx = ((c[3] + c[6] * u) + c[9] * v) - c[0];
+  float dy = ((c[4] + c[7] * u) + c[10] * v) - c[1];
+  float dz = ((c[5] + c[8] * u) + c[11] * v) - c[2];
+  const float inv = 1.0f / sqrtf((dx * dx + dy * dy) + dz * dz);
+  dx = dx * inv;
+  dy = dy * inv;
+  dz = dz * inv;
+  float4* rp = reinterpret_cast<float4*>(rays + bufid);
+  rp[0] = make_float4(c[0], c[1], c[2], kRayEpsilon);
+  rp[1] = make_float4(dx, dy, dz, kInf);
+  if (pixid) pixid[bufid] = y * image_w + x;
+  if (samid) samid[bufid] = int32_t(bufid);
+  (void)s;
+}
+
+// ooc::ShaderPt point-light branch for camera rays (ooc_shader_pt.h:93-171,
+// blinnPhong reflection.h:202-214, hasPositive utils/math.h:76-78).
+struct ShadePt {
+  float lp[3], lr[3], ks[3], shininess;
+};
+
+__device__ __forceinline__ bool shadow_pt(const spray_rt_ray& ray,
+                                          const spray_rt_hit& h,
+                                          const ShadePt& sh, float pos[3],
+                                          float wi[3]) {
+  if (h.domain < 0) return false;
+  const float* o = ray.org;
+  const float* d = ray.dir;
+  pos[0] = d[0] * h.t + o[0];
+  pos[1] = d[1] * h.t + o[1];
+  pos[2] = d[2] * h.t + o[2];
+  const float kd[3] = {
+      float(double((h.color >> 16) & 0xffu) * 0.00392156862745098),
+      float(double((h.color >> 8) & 0xffu) * 0.00392156862745098),
+      float(double(h.color & 0xffu) * 0.00392156862745098)};
+  const float wo[3] = {-d[0], -d[1], -d[2]};
+  const float cos_i = (wo[0] * h.ns[0] + wo[1] * h.ns[1]) + wo[2] * h.ns[2];
+  float n[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  if (!(cos_i > 0.0f)) {
+    n[0] = -n[0];
+    n[1] = -n[1];
+    n[2] = -n[2];
+  }
+  float inv = 1.0f / sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);
+  n[0] *= inv;
+  n[1] *= inv;
+  n[2] *= inv;
+  float l[3] = {sh.lp[0] - pos[0], sh.lp[1] - pos[1], sh.lp[2] - pos[2]};
+  inv = 1.0f / sqrtf((l[0] * l[0] + l[1] * l[1]) + l[2] * l[2]);
+  wi[0] = l[0] * inv;
+  wi[1] = l[1] * inv;
+  wi[2] = l[2] * inv;
+  float ct = (n[0] * wi[0] + n[1] * wi[1]) + n[2] * wi[2];
+  ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
+  float hh[3] = {wi[0] + wo[0], wi[1] + wo[1], wi[2] + wo[2]};
+  inv = 1.0f / sqrtf((hh[0] * hh[0] + hh[1] * hh[1]) + hh[2] * hh[2]);
+  hh[0] *= inv;
+  hh[1] *= inv;
+  hh[2] *= inv;
+  float ndh = (n[0] * hh[0] + n[1] * hh[1]) + n[2] * hh[2];
+  ndh = ndh < 0.0f ? 0.0f : (ndh > 1.0f ? 1.0f : ndh);
+  const float pw = powf(ndh, sh.shininess);
+  bool pos_any = false;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float cs = sh.ks[k] * pw, cd = kd[k] * ct;
+    if ((sh.lr[k] * (cd + cs)) * 1.0f > 0.0f) pos_any = true;
+  }
+  return pos_any;
+}
+
+__device__ __forceinline__ uint32_t block_prefix(bool flag, uint32_t& total) {
+  // exclusive prefix of `flag` over the block (4 waves), in lane order
+  __shared__ uint32_t wsum[kBlock / 64];
+  const unsigned long long bal = __ballot(flag);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t in_wave =
+      __popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+  if (lane == 0) wsum[wave] = __popcll(bal);
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) {
+    if (w < wave) before += wsum[w];
+    total += wsum[w];
+  }
+  return before + in_wave;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spawn_pt_count(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
+    size_t M, ShadePt sh, uint32_t* __restrict__ block_counts) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  bool f = false;
+  if (i < M) {
+    float pos[3], wi[3];
+    f = shadow_pt(rays[i], hits[i], sh, pos, wi);
+  }
+  uint32_t total;
+  (void)block_prefix(f, total);
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+}
+
+// single-block exclusive scan over nb block counts; writes total to *d_count
+__global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ c,
+                                                      uint32_t nb,
+                                                      uint32_t* __restrict__ d_count) {
+  __shared__ uint32_t part[1024];
+  const uint32_t per = (nb + 1023) / 1024;
+  const uint32_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t k = b0; k < b1; ++k) s += c[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - s;  // exclusive
+  for (uint32_t k = b0; k < b1; ++k) {
+    const uint32_t x = c[k];
+    c[k] = run;
+    run += x;
+  }
+  if (threadIdx.x == 1023) *d_count = part[1023];
+}
+
+__global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
+    size_t M, ShadePt sh, const uint32_t* __restrict__ block_offsets,
+    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  bool f = false;
+  float pos[3] = {0, 0, 0}, wi[3] = {0, 0, 0};
+  if (i < M) f = shadow_pt(rays[i], hits[i], sh, pos, wi);
+  uint32_t total;
+  const uint32_t k = block_prefix(f, total) + block_offsets[blockIdx.x];
+  if (f) {
+    float4* op = reinterpret_cast<float4*>(out + k);
+    op[0] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
+    op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
+    if (src) src[k] = int32_t(i);
+  }
+}
+
+inline unsigned grid_for(size_t M) { return unsigned((M + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_rtc_intersect(hipStream_t s, const SlotDesc* slots,
+                                const int* seg_slot, const size_t* seg_off,
+                                int nseg, char* rays, size_t stride, size_t M) {
+  if (M == 0) return hipSuccess;
+  k_rtc_intersect<<<grid_for(M), kBlock, 0, s>>>(slots, seg_slot, seg_off, nseg,
+                                                 rays, stride, M);
+  return hipGetLastError();
+}
+
+hipError_t launch_rtc_occluded(hipStream_t s, const SlotDesc* slots,
+                               const int* seg_slot, const size_t* seg_off,
+                               int nseg, char* rays, size_t stride, size_t M) {
+  if (M == 0) return hipSuccess;
+  k_rtc_occluded<<<grid_for(M), kBlock, 0, s>>>(slots, seg_slot, seg_off, nseg,
+                                                rays, stride, M);
+  return hipGetLastError();
+}
+
+hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
+                          const float* org, const float* dir, size_t M,
+                          int* ids, float* ts, int* counts, int maxhits) {
+  if (M == 0) return hipSuccess;
+  k_domains<<<grid_for(M), kBlock, 0, s>>>(boxes, ndom, org, dir, M, ids, ts,
+                                           counts, maxhits);
+  return hipGetLastError();
+}
+
+template <bool ANY>
+static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
+                               const int* dom2slot, const float* boxes,
+                               int ndom, const spray_rt_ray* rays, size_t M,
+                               const uint32_t* d_count, spray_rt_hit* hits,
+                               uint8_t* occ, unsigned long long* counters) {
+  if (M == 0) return hipSuccess;
+  const unsigned g = grid_for(M);
+  if (ndom <= 64) {
+    if (counters)
+      k_scene<1, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+                                                 rays, M, d_count, hits, occ, counters);
+    else
+      k_scene<1, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+                                                  rays, M, d_count, hits, occ, counters);
+  } else {
+    if (counters)
+      k_scene<4, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+                                                 rays, M, d_count, hits, occ, counters);
+    else
+      k_scene<4, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+                                                  rays, M, d_count, hits, occ, counters);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
+                                  const int* dom2slot, const float* boxes,
+                                  int ndom, const spray_rt_ray* rays, size_t M,
+                                  spray_rt_hit* hits,
+                                  unsigned long long* counters) {
+  return launch_scene<false>(s, slots, dom2slot, boxes, ndom, rays, M, nullptr,
+                             hits, nullptr, counters);
+}
+
+hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
+                                 const int* dom2slot, const float* boxes,
+                                 int ndom, const spray_rt_ray* rays, size_t M,
+                                 const uint32_t* d_count, uint8_t* occluded,
+                                 unsigned long long* counters) {
+  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, rays, M, d_count,
+                            nullptr, occluded, counters);
+}
+
+hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
+                               int spp, int tx, int ty, int tw, int th,
+                               spray_rt_ray* rays, int32_t* pixid,
+                               int32_t* samid) {
+  const size_t n = size_t(tw) * th * spp;
+  if (n == 0) return hipSuccess;
+  Cam c;
+  for (int k = 0; k < 14; ++k) c.p[k] = cam14[k];
+  k_eye_rays_ooc<<<grid_for(n), kBlock, 0, s>>>(c, image_w, spp, tx, ty, tw, th,
+                                                rays, pixid, samid);
+  return hipGetLastError();
+}
+
+hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
+                           const spray_rt_hit* hits, size_t M,
+                           const float* shade10, spray_rt_ray* out_rays,
+                           int32_t* out_src, uint32_t* d_count,
+                           uint32_t* block_counts) {
+  ShadePt sh;
+  for (int k = 0; k < 3; ++k) {
+    sh.lp[k] = shade10[k];
+    sh.lr[k] = shade10[3 + k];
+    sh.ks[k] = shade10[6 + k];
+  }
+  sh.shininess = shade10[9];
+  if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+  const unsigned g = grid_for(M);
+  k_spawn_pt_count<<<g, kBlock, 0, s>>>(rays, hits, M, sh, block_counts);
+  k_scan_blocks<<<1, 1024, 0, s>>>(block_counts, g, d_count);
+  k_spawn_pt_write<<<g, kBlock, 0, s>>>(rays, hits, M, sh, block_counts,
+                                        out_rays, out_src);
+  return hipGetLastError();
+}
+
+}  // namespace spray_rt

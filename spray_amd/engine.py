@@ -1,0 +1,325 @@
+"""Python front-end of the engine: RtContext (spray_rt.h) and Scene
+(spray_scene.h).
+
+Buffers may be numpy arrays (host: the call is synchronous, like Embree's)
+or torch tensors on the GPU (device: enqueued on the context's stream; call
+``sync()``).  The method names follow the reference's scene surface
+(src/render/scene.h:153-205): load, intersect, occluded, intersectDomains.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._native import (HIT_DTYPE, INVALID_ID, RAY_DTYPE, RTC_ISECT_DTYPE,
+                      SprayRtError, lib)
+
+__all__ = ["RtContext", "Scene", "camera_init", "make_rays", "RAY_DTYPE",
+           "HIT_DTYPE", "RTC_ISECT_DTYPE", "INVALID_ID", "SprayRtError"]
+
+
+def _addr(x):
+    """(address, keepalive) of a numpy array / torch tensor / int / None."""
+    if x is None:
+        return None, None
+    if isinstance(x, int):
+        return x, None
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"]:
+            raise ValueError("arrays must be C-contiguous")
+        return x.ctypes.data, x
+    if hasattr(x, "data_ptr"):
+        if hasattr(x, "is_contiguous") and not x.is_contiguous():
+            raise ValueError("tensors must be contiguous")
+        return x.data_ptr(), x
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+def _nbytes(x):
+    if isinstance(x, np.ndarray):
+        return x.nbytes
+    return x.numel() * x.element_size()
+
+
+def camera_init(pos, lookat, up, vfov, w, h):
+    """Camera::init (src/render/camera.h:128-166) -> float32[14]."""
+    cam = np.zeros(14, np.float32)
+    p = np.asarray(pos, np.float32)
+    la = np.asarray(lookat, np.float32)
+    u = np.asarray(up, np.float32)
+    lib().spray_camera_init(p.ctypes.data, la.ctypes.data, u.ctypes.data,
+                            float(vfov), int(w), int(h), cam.ctypes.data)
+    return cam
+
+
+def make_rays(org, dir, tnear=0.001, tfar=np.inf):
+    """Packs org/dir [n,3] into the 32-B ray records of the scene path."""
+    org = np.asarray(org, np.float32).reshape(-1, 3)
+    r = np.zeros(len(org), RAY_DTYPE)
+    r["org"] = org
+    r["dir"] = np.asarray(dir, np.float32).reshape(-1, 3)
+    r["tnear"] = tnear
+    r["tfar"] = tfar
+    return r
+
+
+class RtContext:
+    """One engine context (one GPU).  ``owner=False`` wraps a context owned
+    by a Scene."""
+
+    def __init__(self, device=0, handle=None):
+        self._own = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            rc = lib().spray_rt_create(int(device), C.byref(h))
+            if rc != 0:
+                raise SprayRtError("spray_rt_create(%d) failed: %d" % (device, rc))
+            handle = h.value
+        self.h = handle
+
+    def close(self):
+        if getattr(self, "h", None) and self._own:
+            lib().spray_rt_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = lib().spray_rt_last_error(self.h)
+            raise SprayRtError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    # ---- context ----
+    def set_stream(self, stream):
+        """stream: torch.cuda.Stream, raw hipStream_t int, or None."""
+        if stream is not None and hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        self._check(lib().spray_rt_set_stream(self.h, stream), "set_stream")
+
+    def sync(self):
+        self._check(lib().spray_rt_sync(self.h), "sync")
+
+    # ---- domains ----
+    def upload_domain(self, slot, verts, faces, colors=None, normals=None, async_=False):
+        v = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
+        f = np.ascontiguousarray(faces, np.uint32).reshape(-1, 3)
+        c = None if colors is None else np.ascontiguousarray(colors, np.uint32)
+        n = None if normals is None else np.ascontiguousarray(normals, np.float32)
+        self._check(lib().spray_rt_domain_upload(
+            self.h, int(slot), v.ctypes.data, len(v), f.ctypes.data, len(f),
+            None if c is None else c.ctypes.data, None if n is None else n.ctypes.data,
+            1 if async_ else 0), "domain_upload")
+
+    def release_domain(self, slot):
+        self._check(lib().spray_rt_domain_release(self.h, int(slot)), "domain_release")
+
+    def domain_bounds(self, boxes):
+        b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+        self._check(lib().spray_rt_domain_bounds(self.h, len(b), b.ctypes.data),
+                    "domain_bounds")
+
+    def map_domain(self, domain_id, slot):
+        self._check(lib().spray_rt_map_domain(self.h, int(domain_id), int(slot)),
+                    "map_domain")
+
+    def slot_info(self, slot):
+        nn, nt = C.c_size_t(), C.c_size_t()
+        d = C.c_int()
+        self._check(lib().spray_rt_slot_info(self.h, int(slot), C.byref(nn), C.byref(d),
+                                             C.byref(nt)), "slot_info")
+        return {"nodes": nn.value, "depth": d.value, "tris": nt.value}
+
+    # ---- Embree-1M streams ----
+    def intersect1M(self, slot, rays, stride=96):
+        a, keep = _addr(rays)
+        n = _nbytes(rays) // stride
+        self._check(lib().spray_rt_intersect1M(self.h, int(slot), a, n, stride),
+                    "intersect1M")
+
+    def occluded1M(self, slot, rays, stride=96):
+        a, keep = _addr(rays)
+        n = _nbytes(rays) // stride
+        self._check(lib().spray_rt_occluded1M(self.h, int(slot), a, n, stride),
+                    "occluded1M")
+
+    def _segments(self, fn, slots, offsets, rays, stride, what):
+        s = np.ascontiguousarray(slots, np.int32)
+        o = np.ascontiguousarray(offsets, np.uint64)
+        assert len(o) == len(s) + 1
+        a, keep = _addr(rays)
+        self._check(fn(self.h, s.ctypes.data, o.ctypes.data, len(s), a, stride), what)
+
+    def intersect_segments(self, slots, offsets, rays, stride=96):
+        self._segments(lib().spray_rt_intersect_segments, slots, offsets, rays, stride,
+                       "intersect_segments")
+
+    def occluded_segments(self, slots, offsets, rays, stride=96):
+        self._segments(lib().spray_rt_occluded_segments, slots, offsets, rays, stride,
+                       "occluded_segments")
+
+    def domains1M(self, org, dir, maxhits):
+        org = np.ascontiguousarray(org, np.float32).reshape(-1, 3)
+        dir = np.ascontiguousarray(dir, np.float32).reshape(-1, 3)
+        n = len(org)
+        ids = np.zeros((n, maxhits), np.int32)
+        ts = np.zeros((n, maxhits), np.float32)
+        cnt = np.zeros(n, np.int32)
+        self._check(lib().spray_rt_domains1M(self.h, org.ctypes.data, dir.ctypes.data, n,
+                                             ids.ctypes.data, ts.ctypes.data,
+                                             cnt.ctypes.data, int(maxhits)), "domains1M")
+        return ids, ts, cnt
+
+    # ---- fused scene path ----
+    def intersect_scene(self, rays, hits=None, counters=None):
+        """rays: RAY_DTYPE numpy array or uint8/float torch tensor on the GPU
+        (32 B per ray); hits: HIT_DTYPE array / 48-B-per-ray tensor."""
+        n = _nbytes(rays) // 32
+        if hits is None:
+            hits = np.zeros(n, HIT_DTYPE)
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        c, k3 = _addr(counters)
+        self._check(lib().spray_rt_intersect_scene_counted(self.h, a, n, b, c),
+                    "intersect_scene")
+        return hits
+
+    def occluded_scene(self, rays, occ=None, counters=None):
+        n = _nbytes(rays) // 32
+        if occ is None:
+            occ = np.zeros(n, np.uint8)
+        a, k1 = _addr(rays)
+        b, k2 = _addr(occ)
+        c, k3 = _addr(counters)
+        self._check(lib().spray_rt_occluded_scene_counted(self.h, a, n, b, c),
+                    "occluded_scene")
+        return occ
+
+    def occluded_scene_devcount(self, rays, max_rays, d_count, occ, counters=None):
+        a, k1 = _addr(rays)
+        b, k2 = _addr(d_count)
+        c, k3 = _addr(occ)
+        e, k4 = _addr(counters)
+        self._check(lib().spray_rt_occluded_scene_devcount(self.h, a, int(max_rays), b, c, e),
+                    "occluded_scene_devcount")
+
+    # ---- device ray sources ----
+    def eye_rays_ooc(self, cam, image_w, spp, tile, rays, pixid=None, samid=None):
+        cam = np.ascontiguousarray(cam, np.float32)
+        tx, ty, tw, th = tile
+        a, k1 = _addr(rays)
+        b, k2 = _addr(pixid)
+        c, k3 = _addr(samid)
+        self._check(lib().spray_rt_eye_rays_ooc(self.h, cam.ctypes.data, int(image_w),
+                                                int(spp), tx, ty, tw, th, a, b, c),
+                    "eye_rays_ooc")
+
+    def spawn_shadows_pt(self, rays, hits, n, shade, out_rays, out_src, d_count):
+        shade = np.ascontiguousarray(shade, np.float32)
+        assert shade.size == 10
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        c, k3 = _addr(out_rays)
+        d, k4 = _addr(out_src)
+        e, k5 = _addr(d_count)
+        self._check(lib().spray_rt_spawn_shadows_pt(self.h, a, b, int(n), shade.ctypes.data,
+                                                    c, d, e), "spawn_shadows_pt")
+
+
+class Scene:
+    """GPU-backed scene (src/render/scene.h:62-251 surface)."""
+
+    def __init__(self, desc, ply_path="", cache_size=-1, device=0):
+        h = C.c_void_p()
+        err = C.create_string_buffer(1024)
+        rc = lib().spray_scene_create(desc.encode(), (ply_path or "").encode(),
+                                      int(cache_size), int(device), C.byref(h), err, 1024)
+        if rc != 0:
+            raise SprayRtError("Scene(%s) failed (%d): %s" % (desc, rc, err.value.decode()))
+        self.h = h.value
+        self.rt = RtContext(handle=lib().spray_scene_rt(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().spray_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = lib().spray_scene_last_error(self.h)
+            raise SprayRtError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def getNumDomains(self):
+        return lib().spray_scene_num_domains(self.h)
+
+    def cache_capacity(self):
+        return lib().spray_scene_cache_capacity(self.h)
+
+    def domain_bounds(self):
+        n = self.getNumDomains()
+        boxes = np.zeros((n, 6), np.float32)
+        bound = np.zeros(6, np.float32)
+        lib().spray_scene_bounds(self.h, boxes.ctypes.data, bound.ctypes.data)
+        return boxes, bound
+
+    def getLights(self):
+        out = []
+        for i in range(lib().spray_scene_num_lights(self.h)):
+            b = np.zeros(7, np.float32)
+            lib().spray_scene_light(self.h, i, b.ctypes.data)
+            out.append({"type": "point" if b[0] == 0 else "diffuse", "pos": b[1:4].copy(),
+                        "rad": b[4:7].copy()})
+        return out
+
+    def load(self, domain_id):
+        """Scene::load(id, SceneInfo*) -> cache block."""
+        blk = C.c_int()
+        self._check(lib().spray_scene_load(self.h, int(domain_id), C.byref(blk)), "load")
+        return blk.value
+
+    def intersect(self, cache_block, org, dir):
+        """Scene::intersect for one ray -> (hit, RTC_ISECT_DTYPE record)."""
+        rec = np.zeros(1, RTC_ISECT_DTYPE)
+        o = np.asarray(org, np.float32)
+        d = np.asarray(dir, np.float32)
+        hit = lib().spray_scene_intersect1(self.h, int(cache_block), o.ctypes.data,
+                                           d.ctypes.data, rec.ctypes.data)
+        return bool(hit), rec[0]
+
+    def occluded(self, cache_block, org, dir):
+        rec = np.zeros(1, RTC_ISECT_DTYPE)
+        o = np.asarray(org, np.float32)
+        d = np.asarray(dir, np.float32)
+        return bool(lib().spray_scene_occluded1(self.h, int(cache_block), o.ctypes.data,
+                                                d.ctypes.data, rec.ctypes.data))
+
+    def intersectDomains(self, org, dir, maxhits=None):
+        """Sorted (ids, ts) per ray; org/dir [n,3]."""
+        n = self.getNumDomains()
+        ids, ts, cnt = self.rt.domains1M(org, dir, maxhits or n)
+        return ids, ts, cnt
+
+    def domain_mesh(self, domain_id):
+        nv, nf = C.c_size_t(), C.c_size_t()
+        self._check(lib().spray_scene_domain_mesh(self.h, int(domain_id), C.byref(nv),
+                                                  C.byref(nf), None, None, None, None),
+                    "domain_mesh")
+        v = np.zeros((nv.value, 3), np.float32)
+        f = np.zeros((nf.value, 3), np.uint32)
+        c = np.zeros(nv.value, np.uint32)
+        n = np.zeros((nv.value, 3), np.float32)
+        self._check(lib().spray_scene_domain_mesh(self.h, int(domain_id), C.byref(nv),
+                                                  C.byref(nf), v.ctypes.data, f.ctypes.data,
+                                                  c.ctypes.data, n.ctypes.data),
+                    "domain_mesh")
+        return v, f, c, n
