@@ -113,7 +113,8 @@ typedef struct spray_rt_hit {
 int spray_rt_create(int hip_device, spray_rt_ctx_t* out);
 int spray_rt_destroy(spray_rt_ctx_t ctx);
 const char* spray_rt_last_error(spray_rt_ctx_t ctx);
-/* hip_stream: a hipStream_t (NULL = the context's own stream). */
+/* Enqueue all further work on hip_stream (a hipStream_t; NULL = the null
+ * stream).  A new context uses a private non-blocking stream. */
 int spray_rt_set_stream(spray_rt_ctx_t ctx, void* hip_stream);
 int spray_rt_sync(spray_rt_ctx_t ctx);
 

@@ -41,6 +41,7 @@ struct spray_rt_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t user_stream = nullptr;
+  bool user_stream_set = false;
   hipStream_t upload_stream = nullptr;
   std::vector<SlotHost> slots;
   SlotDesc* d_slots = nullptr;
@@ -89,7 +90,7 @@ int fail(spray_rt_ctx* c, int code, const char* fmt, ...) {
   } while (0)
 
 hipStream_t stream_of(spray_rt_ctx* c) {
-  return c->user_stream ? c->user_stream : c->own_stream;
+  return c->user_stream_set ? c->user_stream : c->own_stream;
 }
 
 bool is_device_ptr(const void* p) {
@@ -265,6 +266,7 @@ const char* spray_rt_last_error(spray_rt_ctx_t c) {
 int spray_rt_set_stream(spray_rt_ctx_t c, void* hip_stream) {
   if (!c) return SPRAY_RT_ERR_ARG;
   c->user_stream = static_cast<hipStream_t>(hip_stream);
+  c->user_stream_set = true;
   return SPRAY_RT_OK;
 }
 

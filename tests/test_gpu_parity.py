@@ -178,7 +178,7 @@ def scene64(spray, oracle):
     sc.close()
 
 
-def bench_tile(oracle, tile=(0, 384, 256, 64), spp=8):
+def bench_tile(oracle, tile=(384, 448, 256, 64), spp=8):
     cam = oracle.camera_init(BENCH_CAMERA["pos"], BENCH_CAMERA["lookat"], BENCH_CAMERA["up"],
                              BENCH_CAMERA["fov"], 1024, 1024)
     org, d, pix, sam = oracle.eye_rays_ooc(cam, 1024, spp, tile)
