@@ -12,7 +12,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libspray_rt.so")
+# SPRAY_RT_LIB selects a diagnostic build (scripts/diag_variants.py); the
+# default is the in-tree engine.
+LIB_PATH = os.environ.get("SPRAY_RT_LIB") or os.path.join(HERE, "lib", "libspray_rt.so")
 
 # record layouts (include/spray_rt.h)
 RAY_DTYPE = np.dtype([("org", "<f4", 3), ("tnear", "<f4"), ("dir", "<f4", 3),

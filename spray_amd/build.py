@@ -41,22 +41,25 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, defines=(), out=None):
+    """Builds the engine; `defines`/`out` produce diagnostic variants (never
+    the shipped library)."""
+    target = out or LIB
+    if not force and not defines and out is None and not _stale():
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    tmp = LIB + ".tmp"
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    tmp = target + ".tmp"
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
-           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, *["-D" + d for d in defines],
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

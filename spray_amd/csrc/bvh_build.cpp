@@ -62,19 +62,28 @@ void pad(float lo[3], float hi[3]) {
 
 class Builder {
  public:
+  // triangles
   Builder(const float* v, const uint32_t* f, size_t nf, BvhImage* out)
-      : v_(v), f_(f), nf_(nf), out_(out) {
-    box_.resize(nf);
-    cent_.resize(3 * nf);
-    idx_.resize(nf);
-    tmp_.resize(nf);
+      : nf_(nf), out_(out) {
+    init(nf);
     for (size_t i = 0; i < nf; ++i) {
       Box b;
       b.clear();
       for (int k = 0; k < 3; ++k) b.grow_point(v + 3 * size_t(f[3 * i + k]));
-      box_[i] = b;
-      for (int j = 0; j < 3; ++j) cent_[3 * i + j] = (b.lo[j] + b.hi[j]) * 0.5f;
-      idx_[i] = uint32_t(i);
+      set_prim(i, b);
+    }
+  }
+  // boxes [n][6]
+  Builder(const float* boxes, size_t n, int leaf_max, BvhImage* out)
+      : nf_(n), out_(out), leaf_max_(leaf_max) {
+    init(n);
+    for (size_t i = 0; i < n; ++i) {
+      Box b;
+      for (int j = 0; j < 3; ++j) {
+        b.lo[j] = boxes[6 * i + j];
+        b.hi[j] = boxes[6 * i + 3 + j];
+      }
+      set_prim(i, b);
     }
   }
 
@@ -83,7 +92,7 @@ class Builder {
     out_->prims.clear();
     out_->depth = 0;
     if (nf_ == 0) return;
-    if (nf_ <= size_t(kLeafMax)) {
+    if (nf_ <= size_t(leaf_max_)) {
       // root that is itself a leaf: left child = the leaf, right = empty box
       size_t self = alloc();
       Box lb;
@@ -93,7 +102,7 @@ class Builder {
       std::memcpy(n.l_hi, lb.hi, 12);
       for (int j = 0; j < 3; ++j) n.r_lo[j] = n.r_hi[j] = kInf;  // never hit
       n.left = lref;
-      n.right = ~int32_t(0);
+      n.right = leaf_max_ == kLeafMax ? ~int32_t(0) : kNoChild;
     } else {
       Box rb;
       recurse(0, nf_, 0, &rb);
@@ -101,6 +110,18 @@ class Builder {
   }
 
  private:
+  void init(size_t n) {
+    box_.resize(n);
+    cent_.resize(3 * n);
+    idx_.resize(n);
+    tmp_.resize(n);
+  }
+  void set_prim(size_t i, const Box& b) {
+    box_[i] = b;
+    for (int j = 0; j < 3; ++j) cent_[3 * i + j] = (b.lo[j] + b.hi[j]) * 0.5f;
+    idx_[i] = uint32_t(i);
+  }
+
   size_t alloc() {
     out_->nodes.emplace_back();
     std::memset(&out_->nodes.back(), 0, sizeof(BvhNode));
@@ -124,7 +145,7 @@ class Builder {
     }
     *bb_out = bb;
     out_->depth = std::max(out_->depth, depth);
-    if (n <= size_t(kLeafMax)) {
+    if (n <= size_t(leaf_max_)) {
       uint32_t first = uint32_t(out_->prims.size());
       for (size_t i = begin; i < end; ++i) out_->prims.push_back(idx_[i]);
       return ~int32_t((first << 2) | uint32_t(n - 1));
@@ -133,7 +154,7 @@ class Builder {
     float ext[3] = {cb.hi[0] - cb.lo[0], cb.hi[1] - cb.lo[1], cb.hi[2] - cb.lo[2]};
     int best_axis = -1, best_split = -1;
     const bool median =
-        depth + ceil_log2((n + kLeafMax - 1) / kLeafMax) >= kMaxDepth;
+        depth + ceil_log2((n + leaf_max_ - 1) / leaf_max_) >= kMaxDepth;
     if (!median) {
       float best = kInf;
       for (int a = 0; a < 3; ++a) {
@@ -221,10 +242,9 @@ class Builder {
     return int32_t(self);
   }
 
-  const float* v_;
-  const uint32_t* f_;
   size_t nf_;
   BvhImage* out_;
+  int leaf_max_ = kLeafMax;
   std::vector<Box> box_;
   std::vector<float> cent_;
   std::vector<uint32_t> idx_, tmp_;
@@ -266,6 +286,28 @@ bool build_bvh(const float* verts, size_t nverts, const uint32_t* faces,
     r[10] = std::fma(r[5], r[6], -(r[3] * r[8]));
     r[11] = std::fma(r[3], r[7], -(r[4] * r[6]));
   }
+  return true;
+}
+
+bool build_domain_tree(const float* boxes, size_t n, std::vector<BvhNode>* out,
+                       int* depth) {
+  out->clear();
+  *depth = 0;
+  if (n == 0) return true;
+  if (n >= (size_t(1) << 29)) return false;
+  BvhImage img;
+  Builder b(boxes, n, 1, &img);
+  b.run();
+  // leaves hold one box each: rewrite ~((first << 2) | 0) as ~(id << 2)
+  for (BvhNode& nd : img.nodes) {
+    for (int32_t* ref : {&nd.left, &nd.right}) {
+      if (*ref >= 0 || *ref == kNoChild) continue;
+      uint32_t first = ~uint32_t(*ref) >> 2;
+      *ref = ~int32_t(img.prims[first] << 2);
+    }
+  }
+  *out = std::move(img.nodes);
+  *depth = img.depth;
   return true;
 }
 

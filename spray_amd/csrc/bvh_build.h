@@ -27,4 +27,14 @@ struct BvhImage {
 bool build_bvh(const float* verts, size_t nverts, const uint32_t* faces,
                size_t nfaces, BvhImage* out);
 
+// Top-level tree over domain boxes [n][6] (lo, hi): same builder, one domain
+// per leaf (ref ~(id << 2)), EXACT union boxes (no padding) so that the
+// reference's intersectAabb evaluated on a parent accepts whenever it accepts
+// a child (float sub/mul are monotone), i.e. the tree prunes nothing the
+// brute-force domain test would keep.  An empty right child has ref
+// kNoChild and an all-+inf box.
+constexpr int32_t kNoChild = INT32_MIN;
+bool build_domain_tree(const float* boxes, size_t n, std::vector<BvhNode>* out,
+                       int* depth);
+
 }  // namespace spray_rt

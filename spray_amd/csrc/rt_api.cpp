@@ -51,6 +51,8 @@ struct spray_rt_ctx {
   int ndom = 0;
   float* d_boxes = nullptr;
   int* d_dom2slot = nullptr;
+  BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
+  int ntlas = 0;
   std::vector<int> dom2slot;
   bool dom_dirty = true;
   // segment tables
@@ -248,7 +250,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
     if (s.ready) (void)hipEventDestroy(s.ready);
     if (s.pinned) (void)hipHostFree(s.pinned);
   }
-  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_seg_slot,
+  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
                   c->d_block_counts};
   for (void* b : bufs)
@@ -413,8 +415,11 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   HIPCHK(c, hipStreamSynchronize(stream_of(c)));
   if (c->d_boxes) HIPCHK(c, hipFree(c->d_boxes));
   if (c->d_dom2slot) HIPCHK(c, hipFree(c->d_dom2slot));
+  if (c->d_tlas) HIPCHK(c, hipFree(c->d_tlas));
   c->d_boxes = nullptr;
   c->d_dom2slot = nullptr;
+  c->d_tlas = nullptr;
+  c->ntlas = 0;
   c->ndom = ndomains;
   c->dom2slot.assign(ndomains, -1);
   c->dom_dirty = true;
@@ -423,6 +428,16 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_dom2slot), ndomains * sizeof(int)));
   HIPCHK(c, hipMemcpy(c->d_boxes, boxes, 6 * ndomains * sizeof(float),
                       hipMemcpyHostToDevice));
+  std::vector<BvhNode> tlas;
+  int depth = 0;
+  if (!build_domain_tree(boxes, size_t(ndomains), &tlas, &depth))
+    return fail(c, SPRAY_RT_ERR_LIMIT, "too many domains");
+  if (ndomains <= SPRAY_RT_MAX_SCENE_DOMAINS) {  // scene path stages it in LDS
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_tlas), tlas.size() * sizeof(BvhNode)));
+    HIPCHK(c, hipMemcpy(c->d_tlas, tlas.data(), tlas.size() * sizeof(BvhNode),
+                        hipMemcpyHostToDevice));
+    c->ntlas = int(tlas.size());
+  }
   return SPRAY_RT_OK;
 }
 
@@ -528,7 +543,8 @@ extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
   hipStream_t s = stream_of(c);
   if (is_device_ptr(rays)) {
     HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                     c->ndom, rays, M, hits, d_counters));
+                                     c->ndom, c->d_tlas, c->ntlas, rays, M, hits,
+                                     d_counters));
     return SPRAY_RT_OK;
   }
   r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
@@ -538,7 +554,8 @@ extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
   HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, M * sizeof(spray_rt_ray),
                            hipMemcpyHostToDevice, s));
   HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                   c->ndom, static_cast<spray_rt_ray*>(c->d_stage),
+                                   c->ndom, c->d_tlas, c->ntlas,
+                                   static_cast<spray_rt_ray*>(c->d_stage),
                                    M, static_cast<spray_rt_hit*>(c->d_stage2),
                                    d_counters));
   HIPCHK(c, hipMemcpyAsync(hits, c->d_stage2, M * sizeof(spray_rt_hit),
@@ -557,7 +574,8 @@ extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
   hipStream_t s = stream_of(c);
   if (is_device_ptr(rays)) {
     HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                    c->ndom, rays, M, nullptr, occ, d_counters));
+                                    c->ndom, c->d_tlas, c->ntlas, rays, M, nullptr,
+                                    occ, d_counters));
     return SPRAY_RT_OK;
   }
   r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
@@ -567,7 +585,8 @@ extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
   HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, M * sizeof(spray_rt_ray),
                            hipMemcpyHostToDevice, s));
   HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                  c->ndom, static_cast<spray_rt_ray*>(c->d_stage),
+                                  c->ndom, c->d_tlas, c->ntlas,
+                                  static_cast<spray_rt_ray*>(c->d_stage),
                                   M, nullptr, static_cast<uint8_t*>(c->d_stage2),
                                   d_counters));
   HIPCHK(c, hipMemcpyAsync(occ, c->d_stage2, M, hipMemcpyDeviceToHost, s));
@@ -587,7 +606,8 @@ extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
   if (!is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(d_count))
     return fail(c, SPRAY_RT_ERR_ARG, "devcount variant needs device buffers");
   HIPCHK(c, launch_scene_occluded(stream_of(c), c->d_slots, c->d_dom2slot,
-                                  c->d_boxes, c->ndom, rays, max_rays, d_count,
+                                  c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
+                                  max_rays, d_count,
                                   occ, d_counters));
   return SPRAY_RT_OK;
 }

@@ -28,12 +28,14 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 // counting variant used to verify the canonical traversal.
 hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
                                   const int* dom2slot, const float* boxes,
-                                  int ndom, const spray_rt_ray* rays, size_t M,
+                                  int ndom, const BvhNode* tlas, int ntlas,
+                                  const spray_rt_ray* rays, size_t M,
                                   spray_rt_hit* hits,
                                   unsigned long long* counters);
 hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  const int* dom2slot, const float* boxes,
-                                 int ndom, const spray_rt_ray* rays, size_t M,
+                                 int ndom, const BvhNode* tlas, int ntlas,
+                                 const spray_rt_ray* rays, size_t M,
                                  const uint32_t* d_count, uint8_t* occluded,
                                  unsigned long long* counters);
 

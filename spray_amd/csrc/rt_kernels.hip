@@ -8,6 +8,8 @@
 // other kernel here -- VBuf compares t with == (ooc_vbuf.cc:41-52).
 #include <hip/hip_runtime.h>
 
+#include <hipcub/block/block_scan.hpp>
+
 #include <climits>
 #include <cstdint>
 
@@ -19,6 +21,26 @@ namespace {
 
 constexpr float kInf = __builtin_inff();
 constexpr int32_t kNone = INT_MAX;
+
+// Pointers read out of the slot table are generic; re-qualify them as global
+// so the loads are global_load_* (not flat_*, which also ticks lgkmcnt).
+#define GAS __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const GAS T* gptr(const T* p) {
+  return (const GAS T*)(p);
+}
+typedef float v4f __attribute__((ext_vector_type(4)));
+// 16-B global load of element i of a float4 array
+__device__ __forceinline__ float4 ld4(const void* base, size_t i) {
+  const v4f v = reinterpret_cast<const GAS v4f*>(gptr(base))[i];
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 1 = domain mask
+// only, 2 = mask + ordered domain selection, no BVH traversal.
+#ifndef SPRAY_DIAG_MODE
+#define SPRAY_DIAG_MODE 0
+#endif
 
 // ---------------------------------------------------------------------------
 // ray / box / triangle primitives
@@ -107,23 +129,28 @@ __device__ __forceinline__ DRay make_dray(float ox, float oy, float oz,
   r.iz = 1.0f / dz;
   return r;
 }
-__device__ __forceinline__ bool aabb_ref(const float* box, const DRay& r,
-                                         float& tmin_out) {
+__device__ __forceinline__ bool aabb_ref6(float lx, float ly, float lz, float hx,
+                                          float hy, float hz, const DRay& r,
+                                          float& tmin_out) {
   const bool sx = r.ix < 0.0f, sy = r.iy < 0.0f, sz = r.iz < 0.0f;
-  float tmin = ((sx ? box[3] : box[0]) - r.ox) * r.ix;
-  float tmax = ((sx ? box[0] : box[3]) - r.ox) * r.ix;
-  const float tymin = ((sy ? box[4] : box[1]) - r.oy) * r.iy;
-  const float tymax = ((sy ? box[1] : box[4]) - r.oy) * r.iy;
+  float tmin = ((sx ? hx : lx) - r.ox) * r.ix;
+  float tmax = ((sx ? lx : hx) - r.ox) * r.ix;
+  const float tymin = ((sy ? hy : ly) - r.oy) * r.iy;
+  const float tymax = ((sy ? ly : hy) - r.oy) * r.iy;
   if ((tmin > tymax) || (tymin > tmax)) return false;
   if (tymin > tmin) tmin = tymin;
   if (tymax < tmax) tmax = tymax;
-  const float tzmin = ((sz ? box[5] : box[2]) - r.oz) * r.iz;
-  const float tzmax = ((sz ? box[2] : box[5]) - r.oz) * r.iz;
+  const float tzmin = ((sz ? hz : lz) - r.oz) * r.iz;
+  const float tzmax = ((sz ? lz : hz) - r.oz) * r.iz;
   if ((tmin > tzmax) || (tzmin > tmax)) return false;
   if (tzmin > tmin) tmin = tzmin;
   if (tzmax < tmax) tmax = tzmax;
   tmin_out = tmin;
   return (tmin < kInf) && (tmax > kRayEpsilon);
+}
+__device__ __forceinline__ bool aabb_ref(const float* box, const DRay& r,
+                                         float& tmin_out) {
+  return aabb_ref6(box[0], box[1], box[2], box[3], box[4], box[5], r, tmin_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -143,14 +170,15 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
                                            float tnear, float tfar_any,
                                            Best& best, int32_t* stk,
                                            unsigned& nnode, unsigned& ntri) {
-  const float4* __restrict__ nodes = reinterpret_cast<const float4*>(s.nodes);
-  const float4* __restrict__ tris = reinterpret_cast<const float4*>(s.tris);
-  const uint32_t* __restrict__ prims = s.prims;
+  const void* nodes = s.nodes;
+  const void* tris = s.tris;
+  const GAS uint32_t* __restrict__ prims = gptr(s.prims);
   int sp = 0;
   int32_t cur = 0;
   for (;;) {
-    const float4* np = nodes + 4 * cur;
-    const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+    const size_t nb = 4 * size_t(cur);
+    const float4 n0 = ld4(nodes, nb), n1 = ld4(nodes, nb + 1), n2 = ld4(nodes, nb + 2),
+                 n3 = ld4(nodes, nb + 3);
     if (COUNT) ++nnode;
     const float tcut = ANY ? tfar_any : best.t;
     float tl, tr;
@@ -178,7 +206,8 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
         const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
         for (uint32_t q = 0; q < cnt; ++q) {
           const uint32_t p = first + q;
-          const float4 a = tris[3 * p], b = tris[3 * p + 1], cc = tris[3 * p + 2];
+          const float4 a = ld4(tris, 3 * size_t(p)), b = ld4(tris, 3 * size_t(p) + 1),
+                       cc = ld4(tris, 3 * size_t(p) + 2);
           if (COUNT) ++ntri;
           float t, u, v;
           if (!tri_test(r, tnear, a, b, cc, t, u, v)) continue;
@@ -216,11 +245,13 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
 __device__ __forceinline__ void epilogue(const SlotDesc& s, uint32_t prim,
                                          float u, float v, uint32_t& color,
                                          float& nsx, float& nsy, float& nsz) {
-  const uint32_t f0 = s.faces[3 * prim], f1 = s.faces[3 * prim + 1],
-                 f2 = s.faces[3 * prim + 2];
+  const GAS uint32_t* faces = gptr(s.faces);
+  const uint32_t f0 = faces[3 * prim], f1 = faces[3 * prim + 1],
+                 f2 = faces[3 * prim + 2];
   const float w = 1.f - u - v;
   if (s.colors) {
-    const uint32_t c0 = s.colors[f0], c1 = s.colors[f1], c2 = s.colors[f2];
+    const GAS uint32_t* colors = gptr(s.colors);
+    const uint32_t c0 = colors[f0], c1 = colors[f1], c2 = colors[f2];
     uint32_t ch[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -234,9 +265,9 @@ __device__ __forceinline__ void epilogue(const SlotDesc& s, uint32_t prim,
     color = 0;
   }
   if (s.normals) {
-    const float* n0 = s.normals + 3 * f0;
-    const float* n1 = s.normals + 3 * f1;
-    const float* n2 = s.normals + 3 * f2;
+    const GAS float* n0 = gptr(s.normals) + 3 * f0;
+    const GAS float* n1 = gptr(s.normals) + 3 * f1;
+    const GAS float* n2 = gptr(s.normals) + 3 * f2;
     nsx = (n0[0] * w + n1[0] * u) + n2[0] * v;
     nsy = (n0[1] * w + n1[1] * u) + n2[1] * v;
     nsz = (n0[2] * w + n1[2] * u) + n2[2] * v;
@@ -280,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void k_rtc_intersect(
   if (s.nnodes)
     trace_slot<false, false>(s, r, tnear, 0.f, best, stack + threadIdx.x, a, b);
   if (best.prim == 0xFFFFFFFFu) return;  // miss: record untouched
-  const float4 c = reinterpret_cast<const float4*>(s.tris)[3 * best.leaf + 2];
+  const float4 c = ld4(s.tris, 3 * size_t(best.leaf) + 2);
   uint32_t color;
   float nsx, nsy, nsz;
   epilogue(s, best.prim, best.u, best.v, color, nsx, nsy, nsz);
@@ -362,21 +393,25 @@ __global__ __launch_bounds__(kBlock) void k_domains(
 // Domains of a ray are visited in (tmin, id) order (DomainList::sort); the
 // closest hit is carried across domains, a later domain replacing it only
 // when strictly nearer -- the earlier list entry wins a tie.
+// The domain mask comes from the top-level tree (exact union boxes, exact
+// intersectAabb at every node: monotone, so it equals the brute-force test).
 template <int W, bool ANY, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_scene(
     const SlotDesc* __restrict__ slots, const int* __restrict__ dom2slot,
-    const float* __restrict__ boxes, int ndom,
-    const spray_rt_ray* __restrict__ rays, size_t M,
+    const float* __restrict__ boxes, int ndom, const BvhNode* __restrict__ tlas,
+    int ntlas, const spray_rt_ray* __restrict__ rays, size_t M,
     const uint32_t* __restrict__ d_count, spray_rt_hit* __restrict__ hits,
     uint8_t* __restrict__ occ, unsigned long long* __restrict__ counters) {
   __shared__ int32_t stack[kStack * kBlock];
   __shared__ float sbox[6 * 64 * W];
+  __shared__ float4 stl[4 * 64 * W];
   if (d_count) {  // ray count produced on the device (spawned shadow rays)
     const size_t dc = *d_count;
     M = dc < M ? dc : M;
     if (size_t(blockIdx.x) * kBlock >= M) return;  // whole block idle
   }
   for (int k = threadIdx.x; k < 6 * ndom; k += kBlock) sbox[k] = boxes[k];
+  for (int k = threadIdx.x; k < 4 * ntlas; k += kBlock) stl[k] = ld4(tlas, k);
   __syncthreads();
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   unsigned nnode = 0, ntri = 0, nvisit = 0;
@@ -387,19 +422,55 @@ __global__ __launch_bounds__(kBlock) void k_scene(
     const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     uint64_t m[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint64_t bits = 0;
-      const int lim = min(64, ndom - 64 * w);
-      for (int j = 0; j < lim; ++j) {
+    for (int w = 0; w < W; ++w) m[w] = 0;
+    int32_t* stk = stack + threadIdx.x;
+    if (ntlas > 0) {
+      int sp = 0;
+      int32_t cur = 0;
+      for (;;) {
+        const float4 a = stl[4 * cur], b = stl[4 * cur + 1], c = stl[4 * cur + 2],
+                     e = stl[4 * cur + 3];
+        const int32_t cl = __float_as_int(e.x), cr = __float_as_int(e.y);
         float tm;
-        if (aabb_ref(sbox + 6 * (64 * w + j), dr, tm)) bits |= 1ull << j;
+        const bool hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
+        const bool hr =
+            cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+        int32_t next = kNone;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int32_t ch = k == 0 ? cl : cr;
+          if (!(k == 0 ? hl : hr)) continue;
+          if (ch < 0) {
+            const int d = int(~uint32_t(ch) >> 2);
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              if (w == (d >> 6)) m[w] |= 1ull << (d & 63);
+          } else if (next == kNone) {
+            next = ch;
+          } else {
+            stk[sp * kBlock] = ch;
+            ++sp;
+          }
+        }
+        if (next == kNone) {
+          if (sp == 0) break;
+          --sp;
+          next = stk[sp * kBlock];
+        }
+        cur = next;
       }
-      m[w] = bits;
+    }
+    if (SPRAY_DIAG_MODE == 1) {  // diagnostic: domain mask only
+      uint32_t pc = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) pc += __popcll(m[w]);
+      if (!ANY) hits[i].prim = pc;
+      else occ[i] = uint8_t(pc);
+      return;
     }
     Best best{ANY ? 0.f : d4.w, 0.f, 0.f, 0xFFFFFFFFu, 0u};
     int best_dom = -1;
     bool occluded = false;
-    int32_t* stk = stack + threadIdx.x;
     for (;;) {
       float st = kInf;
       int sb = -1;
@@ -427,6 +498,11 @@ __global__ __launch_bounds__(kBlock) void k_scene(
       const SlotDesc s = slots[slot];
       if (!s.nnodes) continue;
       if (COUNT) ++nvisit;
+      if (SPRAY_DIAG_MODE == 2) {  // diagnostic: no traversal
+        best.prim = sb;
+        best_dom = sb;
+        continue;
+      }
       if (ANY) {
         if (trace_slot<true, COUNT>(s, r, o4.w, d4.w, best, stk, nnode, ntri)) {
           occluded = true;
@@ -450,9 +526,12 @@ __global__ __launch_bounds__(kBlock) void k_scene(
         h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
         h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
         h2 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+      } else if (SPRAY_DIAG_MODE == 2) {
+        h0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(best.prim));
+        h1 = h2 = h0;
       } else {
         const SlotDesc s = slots[dom2slot[best_dom]];
-        const float4 c = reinterpret_cast<const float4*>(s.tris)[3 * best.leaf + 2];
+        const float4 c = ld4(s.tris, 3 * size_t(best.leaf) + 2);
         uint32_t color;
         float nsx, nsy, nsz;
         epilogue(s, best.prim, best.u, best.v, color, nsx, nsy, nsz);
@@ -626,30 +705,24 @@ __global__ __launch_bounds__(kBlock) void k_spawn_pt_count(
   if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
 }
 
-// single-block exclusive scan over nb block counts; writes total to *d_count
+// single-block exclusive scan over nb block counts (coalesced 1024-wide
+// chunks, hipCUB block scan); writes the total to *d_count
 __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ c,
                                                       uint32_t nb,
                                                       uint32_t* __restrict__ d_count) {
-  __shared__ uint32_t part[1024];
-  const uint32_t per = (nb + 1023) / 1024;
-  const uint32_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
-  uint32_t s = 0;
-  for (uint32_t k = b0; k < b1; ++k) s += c[k];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += v;
+  using Scan = hipcub::BlockScan<uint32_t, 1024>;
+  __shared__ typename Scan::TempStorage tmp;
+  uint32_t run = 0;
+  for (uint32_t base = 0; base < nb; base += 1024) {
+    const uint32_t k = base + threadIdx.x;
+    const uint32_t x = k < nb ? c[k] : 0u;
+    uint32_t ex, agg;
+    Scan(tmp).ExclusiveSum(x, ex, agg);
+    if (k < nb) c[k] = run + ex;
+    run += agg;
     __syncthreads();
   }
-  uint32_t run = part[threadIdx.x] - s;  // exclusive
-  for (uint32_t k = b0; k < b1; ++k) {
-    const uint32_t x = c[k];
-    c[k] = run;
-    run += x;
-  }
-  if (threadIdx.x == 1023) *d_count = part[1023];
+  if (threadIdx.x == 0) *d_count = run;
 }
 
 __global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
@@ -707,24 +780,25 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 template <bool ANY>
 static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
                                const int* dom2slot, const float* boxes,
-                               int ndom, const spray_rt_ray* rays, size_t M,
+                               int ndom, const BvhNode* tlas, int ntlas,
+                               const spray_rt_ray* rays, size_t M,
                                const uint32_t* d_count, spray_rt_hit* hits,
                                uint8_t* occ, unsigned long long* counters) {
   if (M == 0) return hipSuccess;
   const unsigned g = grid_for(M);
   if (ndom <= 64) {
     if (counters)
-      k_scene<1, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+      k_scene<1, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
                                                  rays, M, d_count, hits, occ, counters);
     else
-      k_scene<1, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+      k_scene<1, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
                                                   rays, M, d_count, hits, occ, counters);
   } else {
     if (counters)
-      k_scene<4, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+      k_scene<4, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
                                                  rays, M, d_count, hits, occ, counters);
     else
-      k_scene<4, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom,
+      k_scene<4, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
                                                   rays, M, d_count, hits, occ, counters);
   }
   return hipGetLastError();
@@ -732,20 +806,22 @@ static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
 
 hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
                                   const int* dom2slot, const float* boxes,
-                                  int ndom, const spray_rt_ray* rays, size_t M,
+                                  int ndom, const BvhNode* tlas, int ntlas,
+                                  const spray_rt_ray* rays, size_t M,
                                   spray_rt_hit* hits,
                                   unsigned long long* counters) {
-  return launch_scene<false>(s, slots, dom2slot, boxes, ndom, rays, M, nullptr,
-                             hits, nullptr, counters);
+  return launch_scene<false>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
+                             M, nullptr, hits, nullptr, counters);
 }
 
 hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  const int* dom2slot, const float* boxes,
-                                 int ndom, const spray_rt_ray* rays, size_t M,
+                                 int ndom, const BvhNode* tlas, int ntlas,
+                                 const spray_rt_ray* rays, size_t M,
                                  const uint32_t* d_count, uint8_t* occluded,
                                  unsigned long long* counters) {
-  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, rays, M, d_count,
-                            nullptr, occluded, counters);
+  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
+                            M, d_count, nullptr, occluded, counters);
 }
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
