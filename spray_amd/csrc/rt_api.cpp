@@ -67,6 +67,7 @@ struct spray_rt_ctx {
   void* d_stage3 = nullptr;
   size_t stage3_cap = 0;
   uint32_t* d_block_counts = nullptr;
+  uint32_t* d_heads = nullptr;  // work-queue heads of the persistent launches
   size_t block_cap = 0;
   std::string err;
 };
@@ -252,7 +253,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
   }
   void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
-                  c->d_block_counts};
+                  c->d_block_counts, c->d_heads};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -528,6 +529,8 @@ static int scene_common(spray_rt_ctx* c, const void* rays, size_t M,
                 SPRAY_RT_MAX_SCENE_DOMAINS);
   if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
   HIPCHK(c, hipSetDevice(c->device));
+  if (!c->d_heads)
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), 8 * 32 * sizeof(uint32_t)));
   return prepare(c);
 }
 
@@ -544,7 +547,7 @@ extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
   if (is_device_ptr(rays)) {
     HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
                                      c->ndom, c->d_tlas, c->ntlas, rays, M, hits,
-                                     d_counters));
+                                     d_counters, c->d_heads));
     return SPRAY_RT_OK;
   }
   r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
@@ -557,7 +560,7 @@ extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
                                    c->ndom, c->d_tlas, c->ntlas,
                                    static_cast<spray_rt_ray*>(c->d_stage),
                                    M, static_cast<spray_rt_hit*>(c->d_stage2),
-                                   d_counters));
+                                   d_counters, c->d_heads));
   HIPCHK(c, hipMemcpyAsync(hits, c->d_stage2, M * sizeof(spray_rt_hit),
                            hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
@@ -575,7 +578,7 @@ extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
   if (is_device_ptr(rays)) {
     HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
                                     c->ndom, c->d_tlas, c->ntlas, rays, M, nullptr,
-                                    occ, d_counters));
+                                    occ, d_counters, c->d_heads));
     return SPRAY_RT_OK;
   }
   r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
@@ -588,7 +591,7 @@ extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
                                   c->ndom, c->d_tlas, c->ntlas,
                                   static_cast<spray_rt_ray*>(c->d_stage),
                                   M, nullptr, static_cast<uint8_t*>(c->d_stage2),
-                                  d_counters));
+                                  d_counters, c->d_heads));
   HIPCHK(c, hipMemcpyAsync(occ, c->d_stage2, M, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return SPRAY_RT_OK;
@@ -608,7 +611,7 @@ extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
   HIPCHK(c, launch_scene_occluded(stream_of(c), c->d_slots, c->d_dom2slot,
                                   c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
                                   max_rays, d_count,
-                                  occ, d_counters));
+                                  occ, d_counters, c->d_heads));
   return SPRAY_RT_OK;
 }
 

@@ -24,6 +24,8 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
                           int* ids, float* ts, int* counts, int maxhits);
 
 // Fused scene path: domain list + per-domain traversal + epilogue.
+// heads: device scratch of 8*32 uint32 (per-XCD work-queue heads, zeroed by
+// the launcher with a memset on the same stream).
 // counters (optional, device uint64[3]: nodes, tris, visits) enable the
 // counting variant used to verify the canonical traversal.
 hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
@@ -31,13 +33,13 @@ hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
                                   int ndom, const BvhNode* tlas, int ntlas,
                                   const spray_rt_ray* rays, size_t M,
                                   spray_rt_hit* hits,
-                                  unsigned long long* counters);
+                                  unsigned long long* counters, uint32_t* heads);
 hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  const int* dom2slot, const float* boxes,
                                  int ndom, const BvhNode* tlas, int ntlas,
                                  const spray_rt_ray* rays, size_t M,
                                  const uint32_t* d_count, uint8_t* occluded,
-                                 unsigned long long* counters);
+                                 unsigned long long* counters, uint32_t* heads);
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                int spp, int tx, int ty, int tw, int th,

@@ -395,35 +395,40 @@ __global__ __launch_bounds__(kBlock) void k_domains(
 // when strictly nearer -- the earlier list entry wins a tie.
 // The domain mask comes from the top-level tree (exact union boxes, exact
 // intersectAabb at every node: monotone, so it equals the brute-force test).
+struct SceneArgs {
+  const SlotDesc* slots;
+  const int* dom2slot;
+  const float* boxes;
+  int ndom;
+  const BvhNode* tlas;
+  int ntlas;
+  const spray_rt_ray* rays;
+  size_t M;
+  const uint32_t* d_count;  // device ray count (spawned rays) or null
+  spray_rt_hit* hits;
+  uint8_t* occ;
+  unsigned long long* counters;
+  uint32_t* heads;  // 8 queue heads, 32 words apart (persistent launch)
+};
+
 template <int W, bool ANY, bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_scene(
-    const SlotDesc* __restrict__ slots, const int* __restrict__ dom2slot,
-    const float* __restrict__ boxes, int ndom, const BvhNode* __restrict__ tlas,
-    int ntlas, const spray_rt_ray* __restrict__ rays, size_t M,
-    const uint32_t* __restrict__ d_count, spray_rt_hit* __restrict__ hits,
-    uint8_t* __restrict__ occ, unsigned long long* __restrict__ counters) {
-  __shared__ int32_t stack[kStack * kBlock];
-  __shared__ float sbox[6 * 64 * W];
-  __shared__ float4 stl[4 * 64 * W];
-  if (d_count) {  // ray count produced on the device (spawned shadow rays)
-    const size_t dc = *d_count;
-    M = dc < M ? dc : M;
-    if (size_t(blockIdx.x) * kBlock >= M) return;  // whole block idle
-  }
-  for (int k = threadIdx.x; k < 6 * ndom; k += kBlock) sbox[k] = boxes[k];
-  for (int k = threadIdx.x; k < 4 * ntlas; k += kBlock) stl[k] = ld4(tlas, k);
-  __syncthreads();
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  unsigned nnode = 0, ntri = 0, nvisit = 0;
-  if (i < M) {
-    const float4* rp = reinterpret_cast<const float4*>(rays + i);
+__device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
+                                          const float* sbox, const float4* stl,
+                                          int32_t* stk, unsigned& nnode,
+                                          unsigned& ntri, unsigned& nvisit) {
+  const SlotDesc* __restrict__ slots = A.slots;
+  const int* __restrict__ dom2slot = A.dom2slot;
+  const int ntlas = A.ntlas;
+  spray_rt_hit* __restrict__ hits = A.hits;
+  uint8_t* __restrict__ occ = A.occ;
+  {
+    const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
     const float4 o4 = rp[0], d4 = rp[1];
     const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
-    int32_t* stk = stack + threadIdx.x;
     if (ntlas > 0) {
       int sp = 0;
       int32_t cur = 0;
@@ -545,10 +550,57 @@ __global__ __launch_bounds__(kBlock) void k_scene(
       hp[2] = h2;
     }
   }
+}
+
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
+
+// Persistent launch: each wave dequeues 64-ray chunks.  Queue q owns the
+// contiguous ray range [q*M/8, (q+1)*M/8) -- an image band -- and is drained
+// first by the waves of XCD q (L2 locality: an XCD's L2 holds the BVH nodes of
+// its band); a wave whose queue is empty steals from the others.  No wave
+// waits on another: every wave exits once all eight queues are drained.
+// The heads are zeroed by a memset node before every launch.
+template <int W, bool ANY, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
+  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ float sbox[6 * 64 * W];
+  __shared__ float4 stl[4 * 64 * W];
+  size_t M = A.M;
+  if (A.d_count) {  // ray count produced on the device (spawned shadow rays)
+    const size_t dc = *A.d_count;
+    M = dc < M ? dc : M;
+  }
+  for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
+  for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
+  __syncthreads();
+  unsigned nnode = 0, ntri = 0, nvisit = 0;
+  int32_t* stk = stack + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const size_t per = (M + 7) / 8;
+  const uint32_t home = xcc_id() & 7u;
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t q = (home + k) & 7u;
+    const size_t begin = size_t(q) * per;
+    const size_t end = begin + per < M ? begin + per : M;
+    if (begin >= end) continue;
+    for (;;) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&A.heads[32 * q], 64u);
+      base = __builtin_amdgcn_readfirstlane(base);
+      const size_t i0 = begin + base;
+      if (i0 >= end) break;
+      const size_t i = i0 + lane;
+      if (i < end) scene_ray<W, ANY, COUNT>(A, i, sbox, stl, stk, nnode, ntri, nvisit);
+    }
+  }
   if (COUNT) {
-    atomicAdd(&counters[0], (unsigned long long)nnode);
-    atomicAdd(&counters[1], (unsigned long long)ntri);
-    atomicAdd(&counters[2], (unsigned long long)nvisit);
+    atomicAdd(&A.counters[0], (unsigned long long)nnode);
+    atomicAdd(&A.counters[1], (unsigned long long)ntri);
+    atomicAdd(&A.counters[2], (unsigned long long)nvisit);
   }
 }
 
@@ -777,31 +829,37 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
   return hipGetLastError();
 }
 
+template <int W, bool ANY, bool COUNT>
+static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
+  static int grid = 0;  // resident blocks (per device; gfx950 only)
+  if (!grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scene<W, ANY, COUNT>,
+                                                 kBlock, 0);
+    grid = cus * (per_cu > 0 ? per_cu : 1);
+  }
+  hipError_t e = hipMemsetAsync(a.heads, 0, 8 * 32 * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  k_scene<W, ANY, COUNT><<<grid, kBlock, 0, s>>>(a);
+  return hipGetLastError();
+}
+
 template <bool ANY>
 static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
                                const int* dom2slot, const float* boxes,
                                int ndom, const BvhNode* tlas, int ntlas,
                                const spray_rt_ray* rays, size_t M,
                                const uint32_t* d_count, spray_rt_hit* hits,
-                               uint8_t* occ, unsigned long long* counters) {
+                               uint8_t* occ, unsigned long long* counters,
+                               uint32_t* heads) {
   if (M == 0) return hipSuccess;
-  const unsigned g = grid_for(M);
-  if (ndom <= 64) {
-    if (counters)
-      k_scene<1, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
-                                                 rays, M, d_count, hits, occ, counters);
-    else
-      k_scene<1, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
-                                                  rays, M, d_count, hits, occ, counters);
-  } else {
-    if (counters)
-      k_scene<4, ANY, true><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
-                                                 rays, M, d_count, hits, occ, counters);
-    else
-      k_scene<4, ANY, false><<<g, kBlock, 0, s>>>(slots, dom2slot, boxes, ndom, tlas, ntlas,
-                                                  rays, M, d_count, hits, occ, counters);
-  }
-  return hipGetLastError();
+  const SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M,
+                    d_count, hits, occ, counters, heads};
+  if (ndom <= 64)
+    return counters ? launch_scene_t<1, ANY, true>(s, a) : launch_scene_t<1, ANY, false>(s, a);
+  return counters ? launch_scene_t<4, ANY, true>(s, a) : launch_scene_t<4, ANY, false>(s, a);
 }
 
 hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
@@ -809,9 +867,9 @@ hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
                                   int ndom, const BvhNode* tlas, int ntlas,
                                   const spray_rt_ray* rays, size_t M,
                                   spray_rt_hit* hits,
-                                  unsigned long long* counters) {
+                                  unsigned long long* counters, uint32_t* heads) {
   return launch_scene<false>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
-                             M, nullptr, hits, nullptr, counters);
+                             M, nullptr, hits, nullptr, counters, heads);
 }
 
 hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
@@ -819,9 +877,9 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  int ndom, const BvhNode* tlas, int ntlas,
                                  const spray_rt_ray* rays, size_t M,
                                  const uint32_t* d_count, uint8_t* occluded,
-                                 unsigned long long* counters) {
+                                 unsigned long long* counters, uint32_t* heads) {
   return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
-                            M, d_count, nullptr, occluded, counters);
+                            M, d_count, nullptr, occluded, counters, heads);
 }
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
