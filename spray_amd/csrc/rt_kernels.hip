@@ -587,14 +587,17 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
     const size_t begin = size_t(q) * per;
     const size_t end = begin + per < M ? begin + per : M;
     if (begin >= end) continue;
-    for (;;) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&A.heads[32 * q], 64u);
-      base = __builtin_amdgcn_readfirstlane(base);
-      const size_t i0 = begin + base;
-      if (i0 >= end) break;
-      const size_t i = i0 + lane;
+    // the next chunk is dequeued before the current one is traced, so the
+    // atomic's latency overlaps the traversal
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&A.heads[32 * q], 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    while (begin + base < end) {
+      uint32_t next = 0;
+      if (lane == 0) next = atomicAdd(&A.heads[32 * q], 64u);
+      const size_t i = begin + base + lane;
       if (i < end) scene_ray<W, ANY, COUNT>(A, i, sbox, stl, stk, nnode, ntri, nvisit);
+      base = __builtin_amdgcn_readfirstlane(next);
     }
   }
   if (COUNT) {
