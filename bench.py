@@ -5,7 +5,8 @@ One step = one frame of the hot path over rays already resident in HBM:
   1. closest hit of the 8,388,608 primary rays against every domain of their
      sorted domain lists (spray_rt_intersect_scene: domain query + BVH2
      traversal + updateIntersection epilogue, one launch),
-  2. point-light shadow-ray spawn of ooc::ShaderPt (compaction, 3 launches),
+  2. point-light shadow-ray spawn of ooc::ShaderPt -- fused into the epilogue
+     of (1) (spray_rt_intersect_scene_spawn_pt: wave-aggregated append),
   3. any hit of the spawned shadow rays (spray_rt_occluded_scene_devcount).
 Primary rays are generated once before timing by the reference's camera /
 sampler (ooc::Tracer::genMultiEyes over its 8 blocking tiles of 1024x128).
@@ -146,13 +147,13 @@ def main():
             counts_src = "gpu counting build (MISMATCH vs oracle fixture)"
 
     def step(ev=None):
+        # closest hit with the PT shadow spawn fused into its epilogue, then
+        # any hit over the spawned rays (count stays on the device)
         if ev:
             ev[0].record(stream)
-        rt.intersect_scene(prim, hits)
+        rt.intersect_scene_spawn_pt(prim, hits, SHADE, shadow, src, cnt)
         if ev:
             ev[1].record(stream)
-        rt.spawn_shadows_pt(prim, hits, n_prim, SHADE, shadow, src, cnt)
-        if ev:
             ev[2].record(stream)
         rt.occluded_scene_devcount(shadow, n_prim, cnt, occ)
         if ev:
@@ -209,10 +210,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(ch_gbs, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ch_gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "k_scene<closest-hit> (primary)",
+                     "kernel": "k_scene<closest-hit, fused PT spawn> (primary)",
                      "bytes_per_launch": ch_bytes, "avg_launch_ms": round(ch_ms, 4),
                      "counts": counts_src},
-        "kernels_ms": {"intersect_scene": round(ch_ms, 4), "spawn_pt": round(sp_ms, 4),
+        "kernels_ms": {"intersect_scene_spawn_pt": round(ch_ms, 4),
                        "occluded_scene": round(ah_ms, 4),
                        "occluded_achieved_GBs": round(ah_gbs, 1)},
         "canonical_counts": gpu_counts,

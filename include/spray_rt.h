@@ -180,6 +180,15 @@ int spray_rt_intersect_scene_counted(spray_rt_ctx_t ctx, const spray_rt_ray* ray
 int spray_rt_occluded_scene_counted(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                                     size_t M, uint8_t* occluded,
                                     unsigned long long* d_counters);
+/* Closest hit with the point-light shadow spawn of ooc::ShaderPt fused into
+ * the epilogue (shade as for spray_rt_spawn_shadows_pt): out_rays[M] /
+ * out_src[M] receive the spawned rays -- the same set as
+ * spray_rt_spawn_shadows_pt produces, in unspecified order -- and *d_count
+ * their number.  Device buffers only. */
+int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                      size_t M, spray_rt_hit* hits,
+                                      const float shade[10], spray_rt_ray* out_rays,
+                                      int32_t* out_src, uint32_t* d_count);
 /* Occlusion of the first *d_count (device uint32, e.g. written by
  * spray_rt_spawn_shadows_pt) of at most max_rays device-resident rays, with
  * no host round trip.  d_counters may be NULL. */

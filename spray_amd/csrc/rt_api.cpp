@@ -615,6 +615,24 @@ extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
   return SPRAY_RT_OK;
 }
 
+int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                                      size_t M, spray_rt_hit* hits,
+                                      const float shade[10], spray_rt_ray* out_rays,
+                                      int32_t* out_src, uint32_t* d_count) {
+  int r = scene_common(c, rays, M, hits);
+  if (r) return r;
+  if (!shade || !d_count) return fail(c, SPRAY_RT_ERR_ARG, "null argument");
+  if (!is_device_ptr(d_count) ||
+      (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(out_rays) ||
+             (out_src && !is_device_ptr(out_src)))))
+    return fail(c, SPRAY_RT_ERR_ARG, "fused spawn needs device buffers");
+  HIPCHK(c, launch_scene_intersect_pt(stream_of(c), c->d_slots, c->d_dom2slot,
+                                      c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
+                                      M, hits, c->d_heads, shade, out_rays, out_src,
+                                      d_count));
+  return SPRAY_RT_OK;
+}
+
 int spray_rt_intersect_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
                              size_t M, spray_rt_hit* hits) {
   return spray_rt_intersect_scene_counted(c, rays, M, hits, nullptr);

@@ -41,6 +41,17 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  const uint32_t* d_count, uint8_t* occluded,
                                  unsigned long long* counters, uint32_t* heads);
 
+// Closest hit with the PT shadow-ray spawn fused into the epilogue:
+// out_rays/out_src appended (wave-aggregated atomics; deterministic set,
+// unordered), *d_count = number written (zeroed by the launcher).
+hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
+                                     const int* dom2slot, const float* boxes,
+                                     int ndom, const BvhNode* tlas, int ntlas,
+                                     const spray_rt_ray* rays, size_t M,
+                                     spray_rt_hit* hits, uint32_t* heads,
+                                     const float* shade10, spray_rt_ray* out_rays,
+                                     int32_t* out_src, uint32_t* d_count);
+
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                int spp, int tx, int ty, int tw, int th,
                                spray_rt_ray* rays, int32_t* pixid,

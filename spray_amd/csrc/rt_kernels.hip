@@ -22,6 +22,8 @@ namespace {
 constexpr float kInf = __builtin_inff();
 constexpr int32_t kNone = INT_MAX;
 
+inline unsigned grid_for(size_t M) { return unsigned((M + kBlock - 1) / kBlock); }
+
 // Pointers read out of the slot table are generic; re-qualify them as global
 // so the loads are global_load_* (not flat_*, which also ticks lgkmcnt).
 #define GAS __attribute__((address_space(1)))
@@ -35,6 +37,23 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
   const v4f v = reinterpret_cast<const GAS v4f*>(gptr(base))[i];
   return make_float4(v.x, v.y, v.z, v.w);
 }
+
+// Work distribution of the scene kernels (measured, profiles/): closest hit
+// = persistent waves dequeuing 128-ray chunks from per-XCD queues; any hit =
+// one ray per lane over a plain grid (its waves are short: the persistent
+// tail costs more than it saves).
+#ifndef SPRAY_CHUNK_CH
+#define SPRAY_CHUNK_CH 128
+#endif
+#ifndef SPRAY_CHUNK_AH
+#define SPRAY_CHUNK_AH 64
+#endif
+#ifndef SPRAY_PERSIST_CH
+#define SPRAY_PERSIST_CH 1
+#endif
+#ifndef SPRAY_PERSIST_AH
+#define SPRAY_PERSIST_AH 0
+#endif
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 1 = domain mask
 // only, 2 = mask + ordered domain selection, no BVH traversal.
@@ -393,6 +412,62 @@ __global__ __launch_bounds__(kBlock) void k_domains(
 // Domains of a ray are visited in (tmin, id) order (DomainList::sort); the
 // closest hit is carried across domains, a later domain replacing it only
 // when strictly nearer -- the earlier list entry wins a tie.
+// ooc::ShaderPt point-light branch for camera rays (ooc_shader_pt.h:93-171,
+// blinnPhong reflection.h:202-214, hasPositive utils/math.h:76-78).
+struct ShadePt {
+  float lp[3], lr[3], ks[3], shininess;
+};
+
+__device__ __forceinline__ bool shadow_pt(const spray_rt_ray& ray,
+                                          const spray_rt_hit& h,
+                                          const ShadePt& sh, float pos[3],
+                                          float wi[3]) {
+  if (h.domain < 0) return false;
+  const float* o = ray.org;
+  const float* d = ray.dir;
+  pos[0] = d[0] * h.t + o[0];
+  pos[1] = d[1] * h.t + o[1];
+  pos[2] = d[2] * h.t + o[2];
+  const float kd[3] = {
+      float(double((h.color >> 16) & 0xffu) * 0.00392156862745098),
+      float(double((h.color >> 8) & 0xffu) * 0.00392156862745098),
+      float(double(h.color & 0xffu) * 0.00392156862745098)};
+  const float wo[3] = {-d[0], -d[1], -d[2]};
+  const float cos_i = (wo[0] * h.ns[0] + wo[1] * h.ns[1]) + wo[2] * h.ns[2];
+  float n[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  if (!(cos_i > 0.0f)) {
+    n[0] = -n[0];
+    n[1] = -n[1];
+    n[2] = -n[2];
+  }
+  float inv = 1.0f / sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);
+  n[0] *= inv;
+  n[1] *= inv;
+  n[2] *= inv;
+  float l[3] = {sh.lp[0] - pos[0], sh.lp[1] - pos[1], sh.lp[2] - pos[2]};
+  inv = 1.0f / sqrtf((l[0] * l[0] + l[1] * l[1]) + l[2] * l[2]);
+  wi[0] = l[0] * inv;
+  wi[1] = l[1] * inv;
+  wi[2] = l[2] * inv;
+  float ct = (n[0] * wi[0] + n[1] * wi[1]) + n[2] * wi[2];
+  ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
+  float hh[3] = {wi[0] + wo[0], wi[1] + wo[1], wi[2] + wo[2]};
+  inv = 1.0f / sqrtf((hh[0] * hh[0] + hh[1] * hh[1]) + hh[2] * hh[2]);
+  hh[0] *= inv;
+  hh[1] *= inv;
+  hh[2] *= inv;
+  float ndh = (n[0] * hh[0] + n[1] * hh[1]) + n[2] * hh[2];
+  ndh = ndh < 0.0f ? 0.0f : (ndh > 1.0f ? 1.0f : ndh);
+  const float pw = powf(ndh, sh.shininess);
+  bool pos_any = false;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float cs = sh.ks[k] * pw, cd = kd[k] * ct;
+    if ((sh.lr[k] * (cd + cs)) * 1.0f > 0.0f) pos_any = true;
+  }
+  return pos_any;
+}
+
 // The domain mask comes from the top-level tree (exact union boxes, exact
 // intersectAabb at every node: monotone, so it equals the brute-force test).
 struct SceneArgs {
@@ -409,13 +484,19 @@ struct SceneArgs {
   uint8_t* occ;
   unsigned long long* counters;
   uint32_t* heads;  // 8 queue heads, 32 words apart (persistent launch)
+  // fused PT shadow spawn (closest hit only)
+  ShadePt shade;
+  spray_rt_ray* sh_out;
+  int32_t* sh_src;
+  uint32_t* sh_count;
 };
 
-template <int W, bool ANY, bool COUNT>
+template <int W, bool ANY, bool COUNT, bool SPAWN>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                           const float* sbox, const float4* stl,
                                           int32_t* stk, unsigned& nnode,
-                                          unsigned& ntri, unsigned& nvisit) {
+                                          unsigned& ntri, unsigned& nvisit,
+                                          bool& spawn, float* pos, float* wi) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int ntlas = A.ntlas;
@@ -548,6 +629,23 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
       hp[0] = h0;
       hp[1] = h1;
       hp[2] = h2;
+      if (SPAWN && best_dom >= 0) {
+        spray_rt_hit h;
+        h.t = h0.x;
+        h.color = __float_as_uint(h1.w);
+        h.ns[0] = h2.x;
+        h.ns[1] = h2.y;
+        h.ns[2] = h2.z;
+        h.domain = best_dom;
+        spray_rt_ray ray;
+        ray.org[0] = o4.x;
+        ray.org[1] = o4.y;
+        ray.org[2] = o4.z;
+        ray.dir[0] = d4.x;
+        ray.dir[1] = d4.y;
+        ray.dir[2] = d4.z;
+        spawn = shadow_pt(ray, h, A.shade, pos, wi);
+      }
     }
   }
 }
@@ -564,7 +662,28 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // its band); a wave whose queue is empty steals from the others.  No wave
 // waits on another: every wave exits once all eight queues are drained.
 // The heads are zeroed by a memset node before every launch.
-template <int W, bool ANY, bool COUNT>
+// Wave-aggregated append of the spawned shadow rays (one atomic per wave):
+// the set is deterministic, its order in sh_out is not.
+__device__ __forceinline__ void append_shadow(const SceneArgs& A, bool flag,
+                                              size_t i, const float* pos,
+                                              const float* wi) {
+  const unsigned long long bal = __ballot(flag);
+  if (!bal) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(A.sh_count, uint32_t(__popcll(bal)));
+  base = __builtin_amdgcn_readfirstlane(base);
+  if (flag) {
+    const uint32_t k =
+        base + uint32_t(__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))));
+    float4* op = reinterpret_cast<float4*>(A.sh_out + k);
+    op[0] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
+    op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
+    if (A.sh_src) A.sh_src[k] = int32_t(i);
+  }
+}
+
+template <int W, bool ANY, bool COUNT, bool SPAWN>
 __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   __shared__ int32_t stack[kStack * kBlock];
   __shared__ float sbox[6 * 64 * W];
@@ -579,25 +698,43 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   __syncthreads();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
   int32_t* stk = stack + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const size_t per = (M + 7) / 8;
-  const uint32_t home = xcc_id() & 7u;
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t q = (home + k) & 7u;
-    const size_t begin = size_t(q) * per;
-    const size_t end = begin + per < M ? begin + per : M;
-    if (begin >= end) continue;
-    // the next chunk is dequeued before the current one is traced, so the
-    // atomic's latency overlaps the traversal
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&A.heads[32 * q], 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    while (begin + base < end) {
-      uint32_t next = 0;
-      if (lane == 0) next = atomicAdd(&A.heads[32 * q], 64u);
-      const size_t i = begin + base + lane;
-      if (i < end) scene_ray<W, ANY, COUNT>(A, i, sbox, stl, stk, nnode, ntri, nvisit);
-      base = __builtin_amdgcn_readfirstlane(next);
+  bool flag = false;
+  float pos[3], wi[3];
+  constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
+  if (!kPersist) {
+    const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (i < M)
+      scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
+                                      pos, wi);
+    if (SPAWN) append_shadow(A, flag, i, pos, wi);
+  } else {
+    constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
+    const int lane = threadIdx.x & 63;
+    const size_t per = (M + 7) / 8;
+    const uint32_t home = xcc_id() & 7u;
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t q = (home + k) & 7u;
+      const size_t begin = size_t(q) * per;
+      const size_t end = begin + per < M ? begin + per : M;
+      if (begin >= end) continue;
+      // the next chunk is dequeued before the current one is traced, so the
+      // atomic's latency overlaps the traversal
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&A.heads[32 * q], kChunk);
+      base = __builtin_amdgcn_readfirstlane(base);
+      while (begin + base < end) {
+        uint32_t next = 0;
+        if (lane == 0) next = atomicAdd(&A.heads[32 * q], kChunk);
+        for (uint32_t c = 0; c < kChunk; c += 64) {
+          const size_t i = begin + base + c + lane;
+          flag = false;
+          if (i < end)
+            scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit,
+                                            flag, pos, wi);
+          if (SPAWN) append_shadow(A, flag, i, pos, wi);
+        }
+        base = __builtin_amdgcn_readfirstlane(next);
+      }
     }
   }
   if (COUNT) {
@@ -671,62 +808,6 @@ __global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
   (void)s;
 }
 
-// ooc::ShaderPt point-light branch for camera rays (ooc_shader_pt.h:93-171,
-// blinnPhong reflection.h:202-214, hasPositive utils/math.h:76-78).
-struct ShadePt {
-  float lp[3], lr[3], ks[3], shininess;
-};
-
-__device__ __forceinline__ bool shadow_pt(const spray_rt_ray& ray,
-                                          const spray_rt_hit& h,
-                                          const ShadePt& sh, float pos[3],
-                                          float wi[3]) {
-  if (h.domain < 0) return false;
-  const float* o = ray.org;
-  const float* d = ray.dir;
-  pos[0] = d[0] * h.t + o[0];
-  pos[1] = d[1] * h.t + o[1];
-  pos[2] = d[2] * h.t + o[2];
-  const float kd[3] = {
-      float(double((h.color >> 16) & 0xffu) * 0.00392156862745098),
-      float(double((h.color >> 8) & 0xffu) * 0.00392156862745098),
-      float(double(h.color & 0xffu) * 0.00392156862745098)};
-  const float wo[3] = {-d[0], -d[1], -d[2]};
-  const float cos_i = (wo[0] * h.ns[0] + wo[1] * h.ns[1]) + wo[2] * h.ns[2];
-  float n[3] = {h.ns[0], h.ns[1], h.ns[2]};
-  if (!(cos_i > 0.0f)) {
-    n[0] = -n[0];
-    n[1] = -n[1];
-    n[2] = -n[2];
-  }
-  float inv = 1.0f / sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);
-  n[0] *= inv;
-  n[1] *= inv;
-  n[2] *= inv;
-  float l[3] = {sh.lp[0] - pos[0], sh.lp[1] - pos[1], sh.lp[2] - pos[2]};
-  inv = 1.0f / sqrtf((l[0] * l[0] + l[1] * l[1]) + l[2] * l[2]);
-  wi[0] = l[0] * inv;
-  wi[1] = l[1] * inv;
-  wi[2] = l[2] * inv;
-  float ct = (n[0] * wi[0] + n[1] * wi[1]) + n[2] * wi[2];
-  ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
-  float hh[3] = {wi[0] + wo[0], wi[1] + wo[1], wi[2] + wo[2]};
-  inv = 1.0f / sqrtf((hh[0] * hh[0] + hh[1] * hh[1]) + hh[2] * hh[2]);
-  hh[0] *= inv;
-  hh[1] *= inv;
-  hh[2] *= inv;
-  float ndh = (n[0] * hh[0] + n[1] * hh[1]) + n[2] * hh[2];
-  ndh = ndh < 0.0f ? 0.0f : (ndh > 1.0f ? 1.0f : ndh);
-  const float pw = powf(ndh, sh.shininess);
-  bool pos_any = false;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float cs = sh.ks[k] * pw, cd = kd[k] * ct;
-    if ((sh.lr[k] * (cd + cs)) * 1.0f > 0.0f) pos_any = true;
-  }
-  return pos_any;
-}
-
 __device__ __forceinline__ uint32_t block_prefix(bool flag, uint32_t& total) {
   // exclusive prefix of `flag` over the block (4 waves), in lane order
   __shared__ uint32_t wsum[kBlock / 64];
@@ -798,8 +879,6 @@ __global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
   }
 }
 
-inline unsigned grid_for(size_t M) { return unsigned((M + kBlock - 1) / kBlock); }
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -832,21 +911,34 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
   return hipGetLastError();
 }
 
-template <int W, bool ANY, bool COUNT>
+template <int W, bool ANY, bool COUNT, bool SPAWN>
 static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
-  static int grid = 0;  // resident blocks (per device; gfx950 only)
-  if (!grid) {
+  constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
+  static int grid = 0;  // resident blocks (per process; gfx950 only)
+  if (kPersist && !grid) {
     int dev = 0, cus = 0, per_cu = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scene<W, ANY, COUNT>,
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scene<W, ANY, COUNT, SPAWN>,
                                                  kBlock, 0);
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
-  hipError_t e = hipMemsetAsync(a.heads, 0, 8 * 32 * sizeof(uint32_t), s);
+  hipError_t e = hipSuccess;
+  if (kPersist) e = hipMemsetAsync(a.heads, 0, 8 * 32 * sizeof(uint32_t), s);
+  if (e == hipSuccess && SPAWN) e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
-  k_scene<W, ANY, COUNT><<<grid, kBlock, 0, s>>>(a);
+  const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
+  k_scene<W, ANY, COUNT, SPAWN><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
+}
+
+template <bool ANY, bool SPAWN>
+static hipError_t launch_scene_w(hipStream_t s, const SceneArgs& a, int ndom) {
+  if (ndom <= 64)
+    return a.counters ? launch_scene_t<1, ANY, true, SPAWN>(s, a)
+                      : launch_scene_t<1, ANY, false, SPAWN>(s, a);
+  return a.counters ? launch_scene_t<4, ANY, true, SPAWN>(s, a)
+                    : launch_scene_t<4, ANY, false, SPAWN>(s, a);
 }
 
 template <bool ANY>
@@ -856,13 +948,26 @@ static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
                                const spray_rt_ray* rays, size_t M,
                                const uint32_t* d_count, spray_rt_hit* hits,
                                uint8_t* occ, unsigned long long* counters,
-                               uint32_t* heads) {
-  if (M == 0) return hipSuccess;
-  const SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M,
-                    d_count, hits, occ, counters, heads};
-  if (ndom <= 64)
-    return counters ? launch_scene_t<1, ANY, true>(s, a) : launch_scene_t<1, ANY, false>(s, a);
-  return counters ? launch_scene_t<4, ANY, true>(s, a) : launch_scene_t<4, ANY, false>(s, a);
+                               uint32_t* heads, const float* shade10 = nullptr,
+                               spray_rt_ray* sh_out = nullptr,
+                               int32_t* sh_src = nullptr,
+                               uint32_t* sh_count = nullptr) {
+  if (M == 0) {
+    if (sh_count) return hipMemsetAsync(sh_count, 0, sizeof(uint32_t), s);
+    return hipSuccess;
+  }
+  SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M, d_count, hits,
+              occ, counters, heads, ShadePt{}, sh_out, sh_src, sh_count};
+  if (shade10) {
+    for (int k = 0; k < 3; ++k) {
+      a.shade.lp[k] = shade10[k];
+      a.shade.lr[k] = shade10[3 + k];
+      a.shade.ks[k] = shade10[6 + k];
+    }
+    a.shade.shininess = shade10[9];
+    return launch_scene_w<ANY, true>(s, a, ndom);
+  }
+  return launch_scene_w<ANY, false>(s, a, ndom);
 }
 
 hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
@@ -883,6 +988,18 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  unsigned long long* counters, uint32_t* heads) {
   return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
                             M, d_count, nullptr, occluded, counters, heads);
+}
+
+hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
+                                     const int* dom2slot, const float* boxes,
+                                     int ndom, const BvhNode* tlas, int ntlas,
+                                     const spray_rt_ray* rays, size_t M,
+                                     spray_rt_hit* hits, uint32_t* heads,
+                                     const float* shade10, spray_rt_ray* out_rays,
+                                     int32_t* out_src, uint32_t* d_count) {
+  return launch_scene<false>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
+                             M, nullptr, hits, nullptr, nullptr, heads, shade10,
+                             out_rays, out_src, d_count);
 }
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,

@@ -199,6 +199,19 @@ class RtContext:
                     "occluded_scene")
         return occ
 
+    def intersect_scene_spawn_pt(self, rays, hits, shade, out_rays, out_src, d_count):
+        """Closest hit + fused PT shadow spawn (device buffers)."""
+        n = _nbytes(rays) // 32
+        shade = np.ascontiguousarray(shade, np.float32)
+        assert shade.size == 10
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        c, k3 = _addr(out_rays)
+        d, k4 = _addr(out_src)
+        e, k5 = _addr(d_count)
+        self._check(lib().spray_rt_intersect_scene_spawn_pt(self.h, a, n, b, shade.ctypes.data,
+                                                            c, d, e), "intersect_scene_spawn_pt")
+
     def occluded_scene_devcount(self, rays, max_rays, d_count, occ, counters=None):
         a, k1 = _addr(rays)
         b, k2 = _addr(d_count)

@@ -351,3 +351,36 @@ def test_two_domain_example(spray, oracle):
     compare_hits(hits, oh)
     assert set(np.unique(oh["domain"])) == {-1, 0, 1}
     sc.close()
+
+
+def test_fused_spawn_matches_oracle(spray, oracle, scene64):
+    """intersect_scene_spawn_pt: same hits, and the same SET of shadow rays
+    as the oracle / the deterministic spawn (order unspecified)."""
+    import torch
+    sc, osc, doms, lights = scene64
+    _, org, d, _ = bench_tile(oracle, (320, 400, 384, 64), 8)
+    n = len(org)
+    rays = torch.from_numpy(spray.make_rays(org, d).view(np.uint8)).cuda()
+    hits = torch.zeros(n * 48, dtype=torch.uint8, device="cuda")
+    shade = np.array([0, 500, 1000, 1, 1, 1, 0.4, 0.4, 0.4, 10.0], np.float32)
+    srays = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    src = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.full((1,), 12345, dtype=torch.int32, device="cuda")
+    sc.rt.intersect_scene_spawn_pt(rays, hits, shade, srays, src, cnt)
+    occ = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    sc.rt.occluded_scene_devcount(srays, n, cnt, occ)
+    sc.rt.sync()
+    m = int(cnt.item())
+    oh, _ = osc.intersect(org, d)
+    compare_hits(hits.cpu().numpy().view(spray.HIT_DTYPE), oh)
+    so, sd, osrc = oracle.spawn_shadows_pt(org, d, oh, lights[0]["pos"], lights[0]["rad"],
+                                           [0.4, 0.4, 0.4], 10.0)
+    assert m == len(so)
+    g_src = src[:m].cpu().numpy()
+    order = np.argsort(g_src)
+    assert np.array_equal(g_src[order], osrc)
+    sr = srays[: m * 32].cpu().numpy().view(spray.RAY_DTYPE)[order]
+    assert np.array_equal(sr["org"].view(np.uint32), so.view(np.uint32))
+    assert np.array_equal(sr["dir"].view(np.uint32), sd.view(np.uint32))
+    oocc, _ = osc.occluded(so, sd)
+    assert np.array_equal(occ[:m].cpu().numpy()[order], oocc)
