@@ -41,9 +41,19 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  const uint32_t* d_count, uint8_t* occluded,
                                  unsigned long long* counters, uint32_t* heads);
 
-// Closest hit with the PT shadow-ray spawn fused into the epilogue:
-// out_rays/out_src appended (wave-aggregated atomics; deterministic set,
-// unordered), *d_count = number written (zeroed by the launcher).
+// Closest hit with the PT shadow-ray spawn fused into the epilogue, written
+// in the spawn layout (see spray_rt.h): rays from source band q appended at
+// out[q*S...], counter block d_count[288] (word 0 total, 32*(q+1) band q),
+// zeroed by the launcher.  Wave-aggregated atomics: deterministic set,
+// unspecified order inside a band.
+constexpr int kSpawnCounterWords = 32 * 9;
+size_t spawn_band_size(size_t M);
+hipError_t launch_scene_occluded_spawned(hipStream_t s, const SlotDesc* slots,
+                                         const int* dom2slot, const float* boxes,
+                                         int ndom, const BvhNode* tlas, int ntlas,
+                                         const spray_rt_ray* rays, size_t M_src,
+                                         const uint32_t* spawn_counts,
+                                         uint8_t* occluded, uint32_t* heads);
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
                                      const int* dom2slot, const float* boxes,
                                      int ndom, const BvhNode* tlas, int ntlas,

@@ -38,10 +38,9 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// Work distribution of the scene kernels (measured, profiles/): closest hit
-// = persistent waves dequeuing 128-ray chunks from per-XCD queues; any hit =
-// one ray per lane over a plain grid (its waves are short: the persistent
-// tail costs more than it saves).
+// Work distribution of the scene kernels (measured, profiles/): persistent
+// waves dequeuing chunks from per-XCD band queues (closest hit 128 rays, any
+// hit 64).  SPRAY_PERSIST_*=0 selects a plain one-ray-per-lane grid.
 #ifndef SPRAY_CHUNK_CH
 #define SPRAY_CHUNK_CH 128
 #endif
@@ -52,7 +51,7 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
 #define SPRAY_PERSIST_CH 1
 #endif
 #ifndef SPRAY_PERSIST_AH
-#define SPRAY_PERSIST_AH 0
+#define SPRAY_PERSIST_AH 1
 #endif
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 1 = domain mask
@@ -488,8 +487,17 @@ struct SceneArgs {
   ShadePt shade;
   spray_rt_ray* sh_out;
   int32_t* sh_src;
-  uint32_t* sh_count;
+  uint32_t* sh_count;  // spawn counter block (kSpawnWords words, see below)
+  bool seg_in;         // input rays in the spawn layout, d_count = its block
 };
+
+// Spawn layout: the rays spawned from source band q (band = the ray range
+// [q*S, (q+1)*S), S = band_size(M)) are appended to out[q*S ...]; counter
+// block word 0 = total, word 32*(q+1) = count of band q.
+constexpr int kSpawnWords = 32 * 9;
+__device__ __host__ __forceinline__ size_t band_size(size_t M) {
+  return (((M + 7) / 8) + 127) / 128 * 128;
+}
 
 template <int W, bool ANY, bool COUNT, bool SPAWN>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
@@ -665,17 +673,22 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // Wave-aggregated append of the spawned shadow rays (one atomic per wave):
 // the set is deterministic, its order in sh_out is not.
 __device__ __forceinline__ void append_shadow(const SceneArgs& A, bool flag,
-                                              size_t i, const float* pos,
+                                              size_t i, uint32_t band,
+                                              const float* pos,
                                               const float* wi) {
   const unsigned long long bal = __ballot(flag);
   if (!bal) return;
   const int lane = threadIdx.x & 63;
+  const uint32_t n = uint32_t(__popcll(bal));
   uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(A.sh_count, uint32_t(__popcll(bal)));
+  if (lane == 0) {
+    base = atomicAdd(&A.sh_count[32 * (band + 1)], n);
+    atomicAdd(&A.sh_count[0], n);
+  }
   base = __builtin_amdgcn_readfirstlane(base);
   if (flag) {
-    const uint32_t k =
-        base + uint32_t(__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))));
+    const size_t k = size_t(band) * band_size(A.M) + base +
+        uint32_t(__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))));
     float4* op = reinterpret_cast<float4*>(A.sh_out + k);
     op[0] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
     op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
@@ -688,10 +701,14 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   __shared__ int32_t stack[kStack * kBlock];
   __shared__ float sbox[6 * 64 * W];
   __shared__ float4 stl[4 * 64 * W];
-  size_t M = A.M;
-  if (A.d_count) {  // ray count produced on the device (spawned shadow rays)
+  // rays of band q: [q*S, q*S + n_q); n_q = S (clipped to M) unless the input
+  // is a spawn layout (n_q from its counter block) or a device count prefix
+  const size_t M = A.M;
+  const size_t S = band_size(M);
+  size_t dense = M;
+  if (A.d_count && !A.seg_in) {
     const size_t dc = *A.d_count;
-    M = dc < M ? dc : M;
+    dense = dc < M ? dc : M;
   }
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
@@ -701,21 +718,30 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   bool flag = false;
   float pos[3], wi[3];
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
+  auto band_end = [&](uint32_t q) -> size_t {
+    const size_t b = size_t(q) * S;
+    if (A.seg_in) {
+      const size_t n = A.d_count[32 * (q + 1)];
+      return b + (n < S ? n : S);
+    }
+    const size_t e = b + S;
+    return e < dense ? e : dense;
+  };
   if (!kPersist) {
     const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (i < M)
+    const uint32_t q = uint32_t(i / S);
+    if (q < 8 && i < band_end(q))
       scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
                                       pos, wi);
-    if (SPAWN) append_shadow(A, flag, i, pos, wi);
+    if (SPAWN) append_shadow(A, flag, i, q, pos, wi);
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     const int lane = threadIdx.x & 63;
-    const size_t per = (M + 7) / 8;
     const uint32_t home = xcc_id() & 7u;
     for (uint32_t k = 0; k < 8; ++k) {
       const uint32_t q = (home + k) & 7u;
-      const size_t begin = size_t(q) * per;
-      const size_t end = begin + per < M ? begin + per : M;
+      const size_t begin = size_t(q) * S;
+      const size_t end = band_end(q);
       if (begin >= end) continue;
       // the next chunk is dequeued before the current one is traced, so the
       // atomic's latency overlaps the traversal
@@ -731,7 +757,7 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
           if (i < end)
             scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit,
                                             flag, pos, wi);
-          if (SPAWN) append_shadow(A, flag, i, pos, wi);
+          if (SPAWN) append_shadow(A, flag, i, q, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
       }
@@ -925,9 +951,10 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, 8 * 32 * sizeof(uint32_t), s);
-  if (e == hipSuccess && SPAWN) e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
+  if (e == hipSuccess && SPAWN)
+    e = hipMemsetAsync(a.sh_count, 0, kSpawnWords * sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
-  const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
+  const unsigned g = kPersist ? unsigned(grid) : grid_for(8 * band_size(a.M));
   k_scene<W, ANY, COUNT, SPAWN><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
@@ -951,13 +978,13 @@ static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
                                uint32_t* heads, const float* shade10 = nullptr,
                                spray_rt_ray* sh_out = nullptr,
                                int32_t* sh_src = nullptr,
-                               uint32_t* sh_count = nullptr) {
+                               uint32_t* sh_count = nullptr, bool seg_in = false) {
   if (M == 0) {
-    if (sh_count) return hipMemsetAsync(sh_count, 0, sizeof(uint32_t), s);
+    if (sh_count) return hipMemsetAsync(sh_count, 0, kSpawnWords * sizeof(uint32_t), s);
     return hipSuccess;
   }
   SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M, d_count, hits,
-              occ, counters, heads, ShadePt{}, sh_out, sh_src, sh_count};
+              occ, counters, heads, ShadePt{}, sh_out, sh_src, sh_count, seg_in};
   if (shade10) {
     for (int k = 0; k < 3; ++k) {
       a.shade.lp[k] = shade10[k];
@@ -989,6 +1016,19 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
   return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
                             M, d_count, nullptr, occluded, counters, heads);
 }
+
+hipError_t launch_scene_occluded_spawned(hipStream_t s, const SlotDesc* slots,
+                                         const int* dom2slot, const float* boxes,
+                                         int ndom, const BvhNode* tlas, int ntlas,
+                                         const spray_rt_ray* rays, size_t M_src,
+                                         const uint32_t* spawn_counts,
+                                         uint8_t* occluded, uint32_t* heads) {
+  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
+                            M_src, spawn_counts, nullptr, occluded, nullptr, heads,
+                            nullptr, nullptr, nullptr, nullptr, true);
+}
+
+size_t spawn_band_size(size_t M) { return band_size(M); }
 
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
                                      const int* dom2slot, const float* boxes,

@@ -199,8 +199,25 @@ class RtContext:
                     "occluded_scene")
         return occ
 
+    @staticmethod
+    def spawn_band(M):
+        return lib().spray_rt_spawn_band(int(M))
+
+    @staticmethod
+    def spawn_capacity(M):
+        return lib().spray_rt_spawn_capacity(int(M))
+
+    def occluded_scene_spawned(self, rays, M_src, d_counts, occ):
+        """Any hit over rays in the spawn layout of M_src source rays."""
+        a, k1 = _addr(rays)
+        b, k2 = _addr(d_counts)
+        c, k3 = _addr(occ)
+        self._check(lib().spray_rt_occluded_scene_spawned(self.h, a, int(M_src), b, c),
+                    "occluded_scene_spawned")
+
     def intersect_scene_spawn_pt(self, rays, hits, shade, out_rays, out_src, d_count):
-        """Closest hit + fused PT shadow spawn (device buffers)."""
+        """Closest hit + fused PT shadow spawn in the spawn layout (device
+        buffers; d_count = uint32[288] counter block)."""
         n = _nbytes(rays) // 32
         shade = np.ascontiguousarray(shade, np.float32)
         assert shade.size == 10

@@ -355,32 +355,47 @@ def test_two_domain_example(spray, oracle):
 
 def test_fused_spawn_matches_oracle(spray, oracle, scene64):
     """intersect_scene_spawn_pt: same hits, and the same SET of shadow rays
-    as the oracle / the deterministic spawn (order unspecified)."""
+    as the oracle / the deterministic spawn, in the banded spawn layout;
+    occluded_scene_spawned over that layout."""
     import torch
     sc, osc, doms, lights = scene64
     _, org, d, _ = bench_tile(oracle, (320, 400, 384, 64), 8)
     n = len(org)
+    cap = sc.rt.spawn_capacity(n)
+    S = sc.rt.spawn_band(n)
+    assert cap == 8 * S >= n and S % 128 == 0
     rays = torch.from_numpy(spray.make_rays(org, d).view(np.uint8)).cuda()
     hits = torch.zeros(n * 48, dtype=torch.uint8, device="cuda")
     shade = np.array([0, 500, 1000, 1, 1, 1, 0.4, 0.4, 0.4, 10.0], np.float32)
-    srays = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
-    src = torch.zeros(n, dtype=torch.int32, device="cuda")
-    cnt = torch.full((1,), 12345, dtype=torch.int32, device="cuda")
-    sc.rt.intersect_scene_spawn_pt(rays, hits, shade, srays, src, cnt)
-    occ = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    sc.rt.occluded_scene_devcount(srays, n, cnt, occ)
+    srays = torch.zeros(cap * 32, dtype=torch.uint8, device="cuda")
+    src = torch.full((cap,), -1, dtype=torch.int32, device="cuda")
+    cnts = torch.full((288,), 777, dtype=torch.int32, device="cuda")
+    sc.rt.intersect_scene_spawn_pt(rays, hits, shade, srays, src, cnts)
+    occ = torch.full((cap,), 9, dtype=torch.uint8, device="cuda")
+    sc.rt.occluded_scene_spawned(srays, n, cnts, occ)
     sc.rt.sync()
-    m = int(cnt.item())
+    c = cnts.cpu().numpy()
+    bands = [int(c[32 * (q + 1)]) for q in range(8)]
+    assert int(c[0]) == sum(bands)
     oh, _ = osc.intersect(org, d)
     compare_hits(hits.cpu().numpy().view(spray.HIT_DTYPE), oh)
     so, sd, osrc = oracle.spawn_shadows_pt(org, d, oh, lights[0]["pos"], lights[0]["rad"],
                                            [0.4, 0.4, 0.4], 10.0)
-    assert m == len(so)
-    g_src = src[:m].cpu().numpy()
+    sr_all = srays.cpu().numpy().view(spray.RAY_DTYPE)
+    src_all = src.cpu().numpy()
+    occ_all = occ.cpu().numpy()
+    idx = np.concatenate([np.arange(q * S, q * S + bands[q]) for q in range(8)])
+    g_src = src_all[idx]
+    # every spawned ray sits in the band of its source
+    assert np.array_equal(g_src // S, idx // S)
     order = np.argsort(g_src)
     assert np.array_equal(g_src[order], osrc)
-    sr = srays[: m * 32].cpu().numpy().view(spray.RAY_DTYPE)[order]
+    sr = sr_all[idx][order]
     assert np.array_equal(sr["org"].view(np.uint32), so.view(np.uint32))
     assert np.array_equal(sr["dir"].view(np.uint32), sd.view(np.uint32))
     oocc, _ = osc.occluded(so, sd)
-    assert np.array_equal(occ[:m].cpu().numpy()[order], oocc)
+    assert np.array_equal(occ_all[idx][order], oocc)
+    # positions outside the bands are untouched
+    mask = np.ones(cap, bool)
+    mask[idx] = False
+    assert (occ_all[mask] == 9).all() and (src_all[mask] == -1).all()
