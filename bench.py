@@ -6,8 +6,9 @@ One step = one frame of the hot path over rays already resident in HBM:
      sorted domain lists (spray_rt_intersect_scene: domain query + BVH2
      traversal + updateIntersection epilogue, one launch),
   2. point-light shadow-ray spawn of ooc::ShaderPt -- fused into the epilogue
-     of (1) (spray_rt_intersect_scene_spawn_pt: wave-aggregated append),
-  3. any hit of the spawned shadow rays (spray_rt_occluded_scene_devcount).
+     of (1) (spray_rt_intersect_scene_spawn_pt: positional, with a valid flag),
+  3. any hit of the spawned shadow rays (spray_rt_occluded_scene_masked:
+     in-wave ballot compaction of the valid rays).
 Primary rays are generated once before timing by the reference's camera /
 sampler (ooc::Tracer::genMultiEyes over its 8 blocking tiles of 1024x128).
 
@@ -120,12 +121,12 @@ def main():
     for k, t in enumerate(tiles()):
         rt.eye_rays_ooc(cam, W, SPP, t, prim[k * per_tile * 32:(k + 1) * per_tile * 32])
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
-    cap = rt.spawn_capacity(n_prim)
-    shadow = torch.empty(cap * 32, dtype=torch.uint8, device=dev)
-    src = torch.empty(cap, dtype=torch.int32, device=dev)
+    shadow = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
+    src = torch.empty(n_prim, dtype=torch.int32, device=dev)
+    valid = torch.empty(n_prim, dtype=torch.uint8, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    cnts = torch.zeros(288, dtype=torch.int32, device=dev)  # spawn counter block
-    occ = torch.empty(cap, dtype=torch.uint8, device=dev)
+    nsh = torch.zeros(1, dtype=torch.int32, device=dev)
+    occ = torch.empty(n_prim, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
     # ---- canonical traversal counts (counting build, outside the timing)
@@ -153,11 +154,11 @@ def main():
         # any hit over the spawned rays (count stays on the device)
         if ev:
             ev[0].record(stream)
-        rt.intersect_scene_spawn_pt(prim, hits, SHADE, shadow, src, cnts)
+        rt.intersect_scene_spawn_pt(prim, hits, SHADE, shadow, valid, nsh)
         if ev:
             ev[1].record(stream)
             ev[2].record(stream)
-        rt.occluded_scene_spawned(shadow, n_prim, cnts, occ)
+        rt.occluded_scene_masked(shadow, valid, occ)
         if ev:
             ev[3].record(stream)
 
@@ -179,7 +180,7 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    assert int(cnts[0].item()) == n_shadow
+    assert int(nsh.item()) == n_shadow
 
     ch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     sp_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))

@@ -181,26 +181,22 @@ int spray_rt_occluded_scene_counted(spray_rt_ctx_t ctx, const spray_rt_ray* rays
                                     size_t M, uint8_t* occluded,
                                     unsigned long long* d_counters);
 /* Closest hit with the point-light shadow spawn of ooc::ShaderPt fused into
- * the epilogue (shade as for spray_rt_spawn_shadows_pt).  Spawned rays are
- * written in the "spawn layout": the rays spawned from source band q (the
- * source rays [q*S, (q+1)*S), S = spray_rt_spawn_band(M), q = 0..7) are
- * appended at out_rays[q*S ...]; the counter block d_counts (device uint32
- * [288], zeroed by the call) receives the total in word 0 and the count of
- * band q in word 32*(q+1).  out_rays / out_src need spray_rt_spawn_capacity(M)
- * entries.  The set of spawned rays equals spray_rt_spawn_shadows_pt's; their
- * order inside a band is unspecified.  Device buffers only. */
-size_t spray_rt_spawn_band(size_t M);
-size_t spray_rt_spawn_capacity(size_t M);
+ * the epilogue (shade as for spray_rt_spawn_shadows_pt), written
+ * positionally: out_valid[i] = 1 and out_rays[i] = the shadow ray when
+ * source ray i spawns one, out_valid[i] = 0 otherwise.  *d_count (device
+ * uint32, may be NULL) receives the number spawned.  Deterministic.  Device
+ * buffers only. */
 int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                                       size_t M, spray_rt_hit* hits,
                                       const float shade[10], spray_rt_ray* out_rays,
-                                      int32_t* out_src, uint32_t* d_counts);
-/* Occlusion of rays in the spawn layout of M source rays (the output of
- * spray_rt_intersect_scene_spawn_pt); occluded[] uses the same positions.
- * Band q is drained first by XCD q, the die whose L2 traced its sources. */
-int spray_rt_occluded_scene_spawned(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
-                                    size_t M_src, const uint32_t* d_counts,
-                                    uint8_t* occluded);
+                                      uint8_t* out_valid, uint32_t* d_count);
+/* Any hit over the rays i < M with valid[i] != 0 (e.g. the positional spawn
+ * output): occluded[i] is written for those rays only.  The kernel re-packs
+ * the sparse valid rays into full wavefronts (ballot + prefix into an LDS
+ * ring) in near-source order.  Device buffers only. */
+int spray_rt_occluded_scene_masked(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                   size_t M, const uint8_t* valid,
+                                   uint8_t* occluded);
 /* Occlusion of the first *d_count (device uint32, e.g. written by
  * spray_rt_spawn_shadows_pt) of at most max_rays device-resident rays, with
  * no host round trip.  d_counters may be NULL. */

@@ -61,9 +61,7 @@ SIGNATURES = {
     "spray_rt_occluded_scene_counted": (I, [P, P, SZ, P, P]),
     "spray_rt_occluded_scene_devcount": (I, [P, P, SZ, P, P, P]),
     "spray_rt_intersect_scene_spawn_pt": (I, [P, P, SZ, P, P, P, P, P]),
-    "spray_rt_occluded_scene_spawned": (I, [P, P, SZ, P, P]),
-    "spray_rt_spawn_band": (SZ, [SZ]),
-    "spray_rt_spawn_capacity": (SZ, [SZ]),
+    "spray_rt_occluded_scene_masked": (I, [P, P, SZ, P, P]),
     "spray_rt_eye_rays_ooc": (I, [P, P, I, I, I, I, I, I, P, P, P]),
     "spray_rt_spawn_shadows_pt": (I, [P, P, P, SZ, P, P, P, P]),
     # spray_scene.h

@@ -615,38 +615,34 @@ extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
   return SPRAY_RT_OK;
 }
 
-size_t spray_rt_spawn_band(size_t M) { return spawn_band_size(M); }
-size_t spray_rt_spawn_capacity(size_t M) { return 8 * spawn_band_size(M); }
-
 int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                       size_t M, spray_rt_hit* hits,
                                       const float shade[10], spray_rt_ray* out_rays,
-                                      int32_t* out_src, uint32_t* d_counts) {
+                                      uint8_t* out_valid, uint32_t* d_count) {
   int r = scene_common(c, rays, M, hits);
   if (r) return r;
-  if (!shade || !d_counts) return fail(c, SPRAY_RT_ERR_ARG, "null argument");
-  if (!is_device_ptr(d_counts) ||
+  if (!shade) return fail(c, SPRAY_RT_ERR_ARG, "null shade parameters");
+  if ((d_count && !is_device_ptr(d_count)) ||
       (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(out_rays) ||
-             (out_src && !is_device_ptr(out_src)))))
+             !is_device_ptr(out_valid))))
     return fail(c, SPRAY_RT_ERR_ARG, "fused spawn needs device buffers");
   HIPCHK(c, launch_scene_intersect_pt(stream_of(c), c->d_slots, c->d_dom2slot,
                                       c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
-                                      M, hits, c->d_heads, shade, out_rays, out_src,
-                                      d_counts));
+                                      M, hits, c->d_heads, shade, out_rays, out_valid,
+                                      d_count));
   return SPRAY_RT_OK;
 }
 
-int spray_rt_occluded_scene_spawned(spray_rt_ctx_t c, const spray_rt_ray* rays,
-                                    size_t M_src, const uint32_t* d_counts,
-                                    uint8_t* occ) {
-  int r = scene_common(c, rays, M_src, occ);
+int spray_rt_occluded_scene_masked(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                                   size_t M, const uint8_t* valid, uint8_t* occ) {
+  int r = scene_common(c, rays, M, occ);
   if (r) return r;
-  if (M_src == 0) return SPRAY_RT_OK;
-  if (!is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(d_counts))
-    return fail(c, SPRAY_RT_ERR_ARG, "spawn-layout occlusion needs device buffers");
-  HIPCHK(c, launch_scene_occluded_spawned(stream_of(c), c->d_slots, c->d_dom2slot,
-                                          c->d_boxes, c->ndom, c->d_tlas, c->ntlas,
-                                          rays, M_src, d_counts, occ, c->d_heads));
+  if (M == 0) return SPRAY_RT_OK;
+  if (!valid || !is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(valid))
+    return fail(c, SPRAY_RT_ERR_ARG, "masked occlusion needs device buffers");
+  HIPCHK(c, launch_scene_occluded_masked(stream_of(c), c->d_slots, c->d_dom2slot,
+                                         c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
+                                         M, valid, occ, nullptr, c->d_heads));
   return SPRAY_RT_OK;
 }
 

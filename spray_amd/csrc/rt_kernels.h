@@ -41,26 +41,24 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                                  const uint32_t* d_count, uint8_t* occluded,
                                  unsigned long long* counters, uint32_t* heads);
 
-// Closest hit with the PT shadow-ray spawn fused into the epilogue, written
-// in the spawn layout (see spray_rt.h): rays from source band q appended at
-// out[q*S...], counter block d_count[288] (word 0 total, 32*(q+1) band q),
-// zeroed by the launcher.  Wave-aggregated atomics: deterministic set,
-// unspecified order inside a band.
-constexpr int kSpawnCounterWords = 32 * 9;
-size_t spawn_band_size(size_t M);
-hipError_t launch_scene_occluded_spawned(hipStream_t s, const SlotDesc* slots,
-                                         const int* dom2slot, const float* boxes,
-                                         int ndom, const BvhNode* tlas, int ntlas,
-                                         const spray_rt_ray* rays, size_t M_src,
-                                         const uint32_t* spawn_counts,
-                                         uint8_t* occluded, uint32_t* heads);
+// Closest hit with the PT shadow-ray spawn fused into the epilogue,
+// positional: out_rays[i] / out_valid[i] for source ray i; *d_count (may be
+// null) = number spawned, zeroed by the launcher.
+// Any hit over the rays with valid[i] != 0 (in-wave compaction); occluded[i]
+// written for those rays only.
+hipError_t launch_scene_occluded_masked(hipStream_t s, const SlotDesc* slots,
+                                       const int* dom2slot, const float* boxes,
+                                       int ndom, const BvhNode* tlas, int ntlas,
+                                       const spray_rt_ray* rays, size_t M,
+                                       const uint8_t* valid, uint8_t* occluded,
+                                       unsigned long long* counters, uint32_t* heads);
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
                                      const int* dom2slot, const float* boxes,
                                      int ndom, const BvhNode* tlas, int ntlas,
                                      const spray_rt_ray* rays, size_t M,
                                      spray_rt_hit* hits, uint32_t* heads,
                                      const float* shade10, spray_rt_ray* out_rays,
-                                     int32_t* out_src, uint32_t* d_count);
+                                     uint8_t* out_valid, uint32_t* d_count);
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                int spp, int tx, int ty, int tw, int th,

@@ -483,20 +483,19 @@ struct SceneArgs {
   uint8_t* occ;
   unsigned long long* counters;
   uint32_t* heads;  // 8 queue heads, 32 words apart (persistent launch)
-  // fused PT shadow spawn (closest hit only)
+  // fused PT shadow spawn (closest hit): positional output
   ShadePt shade;
-  spray_rt_ray* sh_out;
-  int32_t* sh_src;
-  uint32_t* sh_count;  // spawn counter block (kSpawnWords words, see below)
-  bool seg_in;         // input rays in the spawn layout, d_count = its block
+  spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
+  uint8_t* sh_valid;     // [M] 1 if source i spawned a shadow ray
+  uint32_t* sh_count;    // optional total
+  // masked input (any hit): trace only rays with valid[i] != 0
+  const uint8_t* valid;
 };
 
-// Spawn layout: the rays spawned from source band q (band = the ray range
-// [q*S, (q+1)*S), S = band_size(M)) are appended to out[q*S ...]; counter
-// block word 0 = total, word 32*(q+1) = count of band q.
-constexpr int kSpawnWords = 32 * 9;
+// Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): the unit of
+// XCD affinity of the persistent launches.
 __device__ __host__ __forceinline__ size_t band_size(size_t M) {
-  return (((M + 7) / 8) + 127) / 128 * 128;
+  return (((M + 7) / 8) + 63) / 64 * 64;
 }
 
 template <int W, bool ANY, bool COUNT, bool SPAWN>
@@ -670,29 +669,22 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // its band); a wave whose queue is empty steals from the others.  No wave
 // waits on another: every wave exits once all eight queues are drained.
 // The heads are zeroed by a memset node before every launch.
-// Wave-aggregated append of the spawned shadow rays (one atomic per wave):
-// the set is deterministic, its order in sh_out is not.
-__device__ __forceinline__ void append_shadow(const SceneArgs& A, bool flag,
-                                              size_t i, uint32_t band,
-                                              const float* pos,
-                                              const float* wi) {
-  const unsigned long long bal = __ballot(flag);
-  if (!bal) return;
-  const int lane = threadIdx.x & 63;
-  const uint32_t n = uint32_t(__popcll(bal));
-  uint32_t base = 0;
-  if (lane == 0) {
-    base = atomicAdd(&A.sh_count[32 * (band + 1)], n);
-    atomicAdd(&A.sh_count[0], n);
+// Positional spawn output: the shadow ray of source i goes to sh_out[i],
+// sh_valid[i] says whether it exists; one atomic per wave for the total.
+__device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
+                                             bool flag, size_t i,
+                                             const float* pos, const float* wi) {
+  if (active) {
+    A.sh_valid[i] = flag ? 1 : 0;
+    if (flag) {
+      float4* op = reinterpret_cast<float4*>(A.sh_out + i);
+      op[0] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
+      op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
+    }
   }
-  base = __builtin_amdgcn_readfirstlane(base);
-  if (flag) {
-    const size_t k = size_t(band) * band_size(A.M) + base +
-        uint32_t(__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))));
-    float4* op = reinterpret_cast<float4*>(A.sh_out + k);
-    op[0] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
-    op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
-    if (A.sh_src) A.sh_src[k] = int32_t(i);
+  if (A.sh_count) {
+    const unsigned long long bal = __ballot(flag);
+    if (bal && (threadIdx.x & 63) == 0) atomicAdd(A.sh_count, uint32_t(__popcll(bal)));
   }
 }
 
@@ -701,15 +693,12 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   __shared__ int32_t stack[kStack * kBlock];
   __shared__ float sbox[6 * 64 * W];
   __shared__ float4 stl[4 * 64 * W];
-  // rays of band q: [q*S, q*S + n_q); n_q = S (clipped to M) unless the input
-  // is a spawn layout (n_q from its counter block) or a device count prefix
-  const size_t M = A.M;
-  const size_t S = band_size(M);
-  size_t dense = M;
-  if (A.d_count && !A.seg_in) {
+  size_t M = A.M;
+  if (A.d_count) {  // ray count produced on the device
     const size_t dc = *A.d_count;
-    dense = dc < M ? dc : M;
+    M = dc < M ? dc : M;
   }
+  const size_t S = band_size(M);
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
   __syncthreads();
@@ -718,30 +707,22 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   bool flag = false;
   float pos[3], wi[3];
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
-  auto band_end = [&](uint32_t q) -> size_t {
-    const size_t b = size_t(q) * S;
-    if (A.seg_in) {
-      const size_t n = A.d_count[32 * (q + 1)];
-      return b + (n < S ? n : S);
-    }
-    const size_t e = b + S;
-    return e < dense ? e : dense;
-  };
+  const int lane = threadIdx.x & 63;
   if (!kPersist) {
     const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-    const uint32_t q = uint32_t(i / S);
-    if (q < 8 && i < band_end(q))
+    const bool act = i < M && (!A.valid || A.valid[i]);
+    if (act)
       scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
                                       pos, wi);
-    if (SPAWN) append_shadow(A, flag, i, q, pos, wi);
-  } else {
+    if (SPAWN) store_shadow(A, i < M, flag, i, pos, wi);
+  } else if (!A.valid) {
+    // dense input: waves dequeue kChunk-ray chunks of their XCD's band first
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
-    const int lane = threadIdx.x & 63;
     const uint32_t home = xcc_id() & 7u;
     for (uint32_t k = 0; k < 8; ++k) {
       const uint32_t q = (home + k) & 7u;
       const size_t begin = size_t(q) * S;
-      const size_t end = band_end(q);
+      const size_t end = begin + S < M ? begin + S : M;
       if (begin >= end) continue;
       // the next chunk is dequeued before the current one is traced, so the
       // atomic's latency overlaps the traversal
@@ -757,10 +738,55 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
           if (i < end)
             scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit,
                                             flag, pos, wi);
-          if (SPAWN) append_shadow(A, flag, i, q, pos, wi);
+          if (SPAWN) store_shadow(A, i < end, flag, i, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
       }
+    }
+  } else {
+    // masked input: each wave scans 64-slot chunks of the bands, re-packs the
+    // valid slots (ballot + prefix) into a 128-entry LDS ring and traces them
+    // 64 at a time -- full waves, near-source order.
+    __shared__ uint32_t ring[kBlock / 64][128];
+    uint32_t* rg = ring[threadIdx.x >> 6];
+    uint32_t head = 0, tail = 0;  // wave-uniform
+    uint32_t k = 0;
+    const uint32_t home = xcc_id() & 7u;
+    for (;;) {
+      while (tail - head < 64 && k < 8) {
+        const uint32_t q = (home + k) & 7u;
+        const size_t begin = size_t(q) * S;
+        const size_t end = begin + S < M ? begin + S : M;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&A.heads[32 * q], 64u);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (begin + base >= end) {
+          ++k;
+          continue;
+        }
+        const size_t i = begin + base + lane;
+        const bool v = i < end && A.valid[i];
+        const unsigned long long bal = __ballot(v);
+        const uint32_t below =
+            uint32_t(__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))));
+        if (v) rg[(tail + below) & 127u] = uint32_t(i);
+        tail += uint32_t(__popcll(bal));
+      }
+      const uint32_t avail = tail - head;
+      if (avail == 0) break;
+      const uint32_t take = avail < 64 ? avail : 64;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (uint32_t(lane) < take) {
+        const size_t i = rg[(head + lane) & 127u];
+        scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
+                                        pos, wi);
+      }
+      head += take;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // slots are reused only after they were read
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   if (COUNT) {
@@ -951,10 +977,10 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, 8 * 32 * sizeof(uint32_t), s);
-  if (e == hipSuccess && SPAWN)
-    e = hipMemsetAsync(a.sh_count, 0, kSpawnWords * sizeof(uint32_t), s);
+  if (e == hipSuccess && SPAWN && a.sh_count)
+    e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
-  const unsigned g = kPersist ? unsigned(grid) : grid_for(8 * band_size(a.M));
+  const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
   k_scene<W, ANY, COUNT, SPAWN><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
@@ -977,14 +1003,15 @@ static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
                                uint8_t* occ, unsigned long long* counters,
                                uint32_t* heads, const float* shade10 = nullptr,
                                spray_rt_ray* sh_out = nullptr,
-                               int32_t* sh_src = nullptr,
-                               uint32_t* sh_count = nullptr, bool seg_in = false) {
+                               uint8_t* sh_valid = nullptr,
+                               uint32_t* sh_count = nullptr,
+                               const uint8_t* valid = nullptr) {
   if (M == 0) {
-    if (sh_count) return hipMemsetAsync(sh_count, 0, kSpawnWords * sizeof(uint32_t), s);
+    if (sh_count) return hipMemsetAsync(sh_count, 0, sizeof(uint32_t), s);
     return hipSuccess;
   }
   SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M, d_count, hits,
-              occ, counters, heads, ShadePt{}, sh_out, sh_src, sh_count, seg_in};
+              occ, counters, heads, ShadePt{}, sh_out, sh_valid, sh_count, valid};
   if (shade10) {
     for (int k = 0; k < 3; ++k) {
       a.shade.lp[k] = shade10[k];
@@ -1017,18 +1044,16 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                             M, d_count, nullptr, occluded, counters, heads);
 }
 
-hipError_t launch_scene_occluded_spawned(hipStream_t s, const SlotDesc* slots,
-                                         const int* dom2slot, const float* boxes,
-                                         int ndom, const BvhNode* tlas, int ntlas,
-                                         const spray_rt_ray* rays, size_t M_src,
-                                         const uint32_t* spawn_counts,
-                                         uint8_t* occluded, uint32_t* heads) {
-  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
-                            M_src, spawn_counts, nullptr, occluded, nullptr, heads,
-                            nullptr, nullptr, nullptr, nullptr, true);
+hipError_t launch_scene_occluded_masked(hipStream_t s, const SlotDesc* slots,
+                                       const int* dom2slot, const float* boxes,
+                                       int ndom, const BvhNode* tlas, int ntlas,
+                                       const spray_rt_ray* rays, size_t M,
+                                       const uint8_t* valid, uint8_t* occluded,
+                                       unsigned long long* counters, uint32_t* heads) {
+  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M,
+                            nullptr, nullptr, occluded, counters, heads, nullptr,
+                            nullptr, nullptr, nullptr, valid);
 }
-
-size_t spawn_band_size(size_t M) { return band_size(M); }
 
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
                                      const int* dom2slot, const float* boxes,
@@ -1036,10 +1061,10 @@ hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
                                      const spray_rt_ray* rays, size_t M,
                                      spray_rt_hit* hits, uint32_t* heads,
                                      const float* shade10, spray_rt_ray* out_rays,
-                                     int32_t* out_src, uint32_t* d_count) {
+                                     uint8_t* out_valid, uint32_t* d_count) {
   return launch_scene<false>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
                              M, nullptr, hits, nullptr, nullptr, heads, shade10,
-                             out_rays, out_src, d_count);
+                             out_rays, out_valid, d_count);
 }
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,

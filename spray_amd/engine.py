@@ -199,32 +199,24 @@ class RtContext:
                     "occluded_scene")
         return occ
 
-    @staticmethod
-    def spawn_band(M):
-        return lib().spray_rt_spawn_band(int(M))
-
-    @staticmethod
-    def spawn_capacity(M):
-        return lib().spray_rt_spawn_capacity(int(M))
-
-    def occluded_scene_spawned(self, rays, M_src, d_counts, occ):
-        """Any hit over rays in the spawn layout of M_src source rays."""
+    def occluded_scene_masked(self, rays, valid, occ):
+        """Any hit over the rays with valid[i] != 0 (device buffers)."""
+        n = _nbytes(rays) // 32
         a, k1 = _addr(rays)
-        b, k2 = _addr(d_counts)
+        b, k2 = _addr(valid)
         c, k3 = _addr(occ)
-        self._check(lib().spray_rt_occluded_scene_spawned(self.h, a, int(M_src), b, c),
-                    "occluded_scene_spawned")
+        self._check(lib().spray_rt_occluded_scene_masked(self.h, a, n, b, c),
+                    "occluded_scene_masked")
 
-    def intersect_scene_spawn_pt(self, rays, hits, shade, out_rays, out_src, d_count):
-        """Closest hit + fused PT shadow spawn in the spawn layout (device
-        buffers; d_count = uint32[288] counter block)."""
+    def intersect_scene_spawn_pt(self, rays, hits, shade, out_rays, out_valid, d_count=None):
+        """Closest hit + fused positional PT shadow spawn (device buffers)."""
         n = _nbytes(rays) // 32
         shade = np.ascontiguousarray(shade, np.float32)
         assert shade.size == 10
         a, k1 = _addr(rays)
         b, k2 = _addr(hits)
         c, k3 = _addr(out_rays)
-        d, k4 = _addr(out_src)
+        d, k4 = _addr(out_valid)
         e, k5 = _addr(d_count)
         self._check(lib().spray_rt_intersect_scene_spawn_pt(self.h, a, n, b, shade.ctypes.data,
                                                             c, d, e), "intersect_scene_spawn_pt")

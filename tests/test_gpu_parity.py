@@ -354,48 +354,55 @@ def test_two_domain_example(spray, oracle):
 
 
 def test_fused_spawn_matches_oracle(spray, oracle, scene64):
-    """intersect_scene_spawn_pt: same hits, and the same SET of shadow rays
-    as the oracle / the deterministic spawn, in the banded spawn layout;
-    occluded_scene_spawned over that layout."""
+    """intersect_scene_spawn_pt: same hits and exactly the oracle's shadow
+    rays at their source positions; occluded_scene_masked over them."""
     import torch
     sc, osc, doms, lights = scene64
     _, org, d, _ = bench_tile(oracle, (320, 400, 384, 64), 8)
     n = len(org)
-    cap = sc.rt.spawn_capacity(n)
-    S = sc.rt.spawn_band(n)
-    assert cap == 8 * S >= n and S % 128 == 0
     rays = torch.from_numpy(spray.make_rays(org, d).view(np.uint8)).cuda()
     hits = torch.zeros(n * 48, dtype=torch.uint8, device="cuda")
     shade = np.array([0, 500, 1000, 1, 1, 1, 0.4, 0.4, 0.4, 10.0], np.float32)
-    srays = torch.zeros(cap * 32, dtype=torch.uint8, device="cuda")
-    src = torch.full((cap,), -1, dtype=torch.int32, device="cuda")
-    cnts = torch.full((288,), 777, dtype=torch.int32, device="cuda")
-    sc.rt.intersect_scene_spawn_pt(rays, hits, shade, srays, src, cnts)
-    occ = torch.full((cap,), 9, dtype=torch.uint8, device="cuda")
-    sc.rt.occluded_scene_spawned(srays, n, cnts, occ)
+    srays = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    valid = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    cnt = torch.full((1,), 123, dtype=torch.int32, device="cuda")
+    sc.rt.intersect_scene_spawn_pt(rays, hits, shade, srays, valid, cnt)
+    occ = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+    sc.rt.occluded_scene_masked(srays, valid, occ)
     sc.rt.sync()
-    c = cnts.cpu().numpy()
-    bands = [int(c[32 * (q + 1)]) for q in range(8)]
-    assert int(c[0]) == sum(bands)
     oh, _ = osc.intersect(org, d)
     compare_hits(hits.cpu().numpy().view(spray.HIT_DTYPE), oh)
     so, sd, osrc = oracle.spawn_shadows_pt(org, d, oh, lights[0]["pos"], lights[0]["rad"],
                                            [0.4, 0.4, 0.4], 10.0)
-    sr_all = srays.cpu().numpy().view(spray.RAY_DTYPE)
-    src_all = src.cpu().numpy()
-    occ_all = occ.cpu().numpy()
-    idx = np.concatenate([np.arange(q * S, q * S + bands[q]) for q in range(8)])
-    g_src = src_all[idx]
-    # every spawned ray sits in the band of its source
-    assert np.array_equal(g_src // S, idx // S)
-    order = np.argsort(g_src)
-    assert np.array_equal(g_src[order], osrc)
-    sr = sr_all[idx][order]
+    v = valid.cpu().numpy()
+    assert set(np.unique(v)) <= {0, 1}
+    assert np.array_equal(np.nonzero(v)[0], osrc) and int(cnt.item()) == len(osrc)
+    sr = srays.cpu().numpy().view(spray.RAY_DTYPE)[osrc]
     assert np.array_equal(sr["org"].view(np.uint32), so.view(np.uint32))
     assert np.array_equal(sr["dir"].view(np.uint32), sd.view(np.uint32))
     oocc, _ = osc.occluded(so, sd)
-    assert np.array_equal(occ_all[idx][order], oocc)
-    # positions outside the bands are untouched
-    mask = np.ones(cap, bool)
-    mask[idx] = False
-    assert (occ_all[mask] == 9).all() and (src_all[mask] == -1).all()
+    o = occ.cpu().numpy()
+    assert np.array_equal(o[osrc], oocc)
+    assert (o[v == 0] == 9).all()  # only valid rays are written
+
+
+def test_masked_occlusion_sparse_patterns(spray, oracle, scene64):
+    """In-wave compaction with adversarial masks: all, none, every 63rd, one
+    isolated ray, random 5%."""
+    import torch
+    sc, osc, _, _ = scene64
+    _, org, d, _ = bench_tile(oracle, (400, 500, 256, 16), 8)
+    n = len(org)
+    rays = torch.from_numpy(spray.make_rays(org, d).view(np.uint8)).cuda()
+    ref, _ = osc.occluded(org, d)
+    rng = np.random.default_rng(11)
+    for mask in [np.ones(n, np.uint8), np.zeros(n, np.uint8),
+                 (np.arange(n) % 63 == 5).astype(np.uint8),
+                 (np.arange(n) == n // 2).astype(np.uint8),
+                 (rng.uniform(size=n) < 0.05).astype(np.uint8)]:
+        occ = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+        sc.rt.occluded_scene_masked(rays, torch.from_numpy(mask).cuda(), occ)
+        sc.rt.sync()
+        o = occ.cpu().numpy()
+        assert np.array_equal(o[mask == 1], ref[mask == 1])
+        assert (o[mask == 0] == 9).all()
