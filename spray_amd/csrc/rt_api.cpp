@@ -68,6 +68,8 @@ struct spray_rt_ctx {
   size_t stage3_cap = 0;
   uint32_t* d_block_counts = nullptr;
   uint32_t* d_heads = nullptr;  // work-queue heads of the persistent launches
+  void* d_sel = nullptr;        // selected indices + count + select scratch
+  size_t sel_cap = 0;
   size_t block_cap = 0;
   std::string err;
 };
@@ -253,7 +255,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
   }
   void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
-                  c->d_block_counts, c->d_heads};
+                  c->d_block_counts, c->d_heads, c->d_sel};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -638,11 +640,22 @@ int spray_rt_occluded_scene_masked(spray_rt_ctx_t c, const spray_rt_ray* rays,
   int r = scene_common(c, rays, M, occ);
   if (r) return r;
   if (M == 0) return SPRAY_RT_OK;
+  if (M > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "M > 2^32");
   if (!valid || !is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(valid))
     return fail(c, SPRAY_RT_ERR_ARG, "masked occlusion needs device buffers");
-  HIPCHK(c, launch_scene_occluded_masked(stream_of(c), c->d_slots, c->d_dom2slot,
-                                         c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
-                                         M, valid, occ, nullptr, c->d_heads));
+  hipStream_t s = stream_of(c);
+  size_t temp = 0;
+  HIPCHK(c, launch_select_flagged(s, valid, M, nullptr, nullptr, nullptr, &temp));
+  const size_t b_idx = align256(M * sizeof(uint32_t));
+  r = ensure(c, &c->d_sel, &c->sel_cap, b_idx + 256 + temp);
+  if (r) return r;
+  char* base = static_cast<char*>(c->d_sel);
+  uint32_t* idx = reinterpret_cast<uint32_t*>(base);
+  uint32_t* num = reinterpret_cast<uint32_t*>(base + b_idx);
+  HIPCHK(c, launch_select_flagged(s, valid, M, idx, num, base + b_idx + 256, &temp));
+  HIPCHK(c, launch_scene_occluded_indexed(s, c->d_slots, c->d_dom2slot, c->d_boxes,
+                                          c->ndom, c->d_tlas, c->ntlas, rays, M, idx,
+                                          num, occ, nullptr, c->d_heads));
   return SPRAY_RT_OK;
 }
 

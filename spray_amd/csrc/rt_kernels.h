@@ -44,14 +44,19 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
 // Closest hit with the PT shadow-ray spawn fused into the epilogue,
 // positional: out_rays[i] / out_valid[i] for source ray i; *d_count (may be
 // null) = number spawned, zeroed by the launcher.
-// Any hit over the rays with valid[i] != 0 (in-wave compaction); occluded[i]
-// written for those rays only.
-hipError_t launch_scene_occluded_masked(hipStream_t s, const SlotDesc* slots,
-                                       const int* dom2slot, const float* boxes,
-                                       int ndom, const BvhNode* tlas, int ntlas,
-                                       const spray_rt_ray* rays, size_t M,
-                                       const uint8_t* valid, uint8_t* occluded,
-                                       unsigned long long* counters, uint32_t* heads);
+// idx_out[0..*d_num) = ascending i with flags[i] != 0 (hipCUB select;
+// temp == nullptr: *temp_bytes <- required scratch size).
+hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
+                                 uint32_t* idx_out, uint32_t* d_num, void* temp,
+                                 size_t* temp_bytes);
+// Any hit over rays idx[0..*d_num) (d_num <= max_n), occluded[idx[j]] written.
+hipError_t launch_scene_occluded_indexed(hipStream_t s, const SlotDesc* slots,
+                                        const int* dom2slot, const float* boxes,
+                                        int ndom, const BvhNode* tlas, int ntlas,
+                                        const spray_rt_ray* rays, size_t max_n,
+                                        const uint32_t* idx, const uint32_t* d_num,
+                                        uint8_t* occluded,
+                                        unsigned long long* counters, uint32_t* heads);
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
                                      const int* dom2slot, const float* boxes,
                                      int ndom, const BvhNode* tlas, int ntlas,

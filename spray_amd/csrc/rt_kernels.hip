@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <hipcub/block/block_scan.hpp>
+#include <hipcub/device/device_select.hpp>
+#include <hipcub/iterator/counting_input_iterator.hpp>
 
 #include <climits>
 #include <cstdint>
@@ -488,8 +490,8 @@ struct SceneArgs {
   spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
   uint8_t* sh_valid;     // [M] 1 if source i spawned a shadow ray
   uint32_t* sh_count;    // optional total
-  // masked input (any hit): trace only rays with valid[i] != 0
-  const uint8_t* valid;
+  // indexed input: slot j traces ray idx[j] (e.g. a selected sparse subset)
+  const uint32_t* idx;
 };
 
 // Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): the unit of
@@ -708,15 +710,16 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
   float pos[3], wi[3];
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
   const int lane = threadIdx.x & 63;
+  const uint32_t* __restrict__ idx = A.idx;
   if (!kPersist) {
-    const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-    const bool act = i < M && (!A.valid || A.valid[i]);
-    if (act)
+    const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+    const size_t i = (idx && j < M) ? idx[j] : j;
+    if (j < M)
       scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
                                       pos, wi);
-    if (SPAWN) store_shadow(A, i < M, flag, i, pos, wi);
-  } else if (!A.valid) {
-    // dense input: waves dequeue kChunk-ray chunks of their XCD's band first
+    if (SPAWN) store_shadow(A, j < M, flag, i, pos, wi);
+  } else {
+    // waves dequeue kChunk-slot chunks of their XCD's band first
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     const uint32_t home = xcc_id() & 7u;
     for (uint32_t k = 0; k < 8; ++k) {
@@ -733,60 +736,16 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
         uint32_t next = 0;
         if (lane == 0) next = atomicAdd(&A.heads[32 * q], kChunk);
         for (uint32_t c = 0; c < kChunk; c += 64) {
-          const size_t i = begin + base + c + lane;
+          const size_t j = begin + base + c + lane;
+          const size_t i = (idx && j < end) ? idx[j] : j;
           flag = false;
-          if (i < end)
+          if (j < end)
             scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit,
                                             flag, pos, wi);
-          if (SPAWN) store_shadow(A, i < end, flag, i, pos, wi);
+          if (SPAWN) store_shadow(A, j < end, flag, i, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
       }
-    }
-  } else {
-    // masked input: each wave scans 64-slot chunks of the bands, re-packs the
-    // valid slots (ballot + prefix) into a 128-entry LDS ring and traces them
-    // 64 at a time -- full waves, near-source order.
-    __shared__ uint32_t ring[kBlock / 64][128];
-    uint32_t* rg = ring[threadIdx.x >> 6];
-    uint32_t head = 0, tail = 0;  // wave-uniform
-    uint32_t k = 0;
-    const uint32_t home = xcc_id() & 7u;
-    for (;;) {
-      while (tail - head < 64 && k < 8) {
-        const uint32_t q = (home + k) & 7u;
-        const size_t begin = size_t(q) * S;
-        const size_t end = begin + S < M ? begin + S : M;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&A.heads[32 * q], 64u);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (begin + base >= end) {
-          ++k;
-          continue;
-        }
-        const size_t i = begin + base + lane;
-        const bool v = i < end && A.valid[i];
-        const unsigned long long bal = __ballot(v);
-        const uint32_t below =
-            uint32_t(__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))));
-        if (v) rg[(tail + below) & 127u] = uint32_t(i);
-        tail += uint32_t(__popcll(bal));
-      }
-      const uint32_t avail = tail - head;
-      if (avail == 0) break;
-      const uint32_t take = avail < 64 ? avail : 64;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (uint32_t(lane) < take) {
-        const size_t i = rg[(head + lane) & 127u];
-        scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
-                                        pos, wi);
-      }
-      head += take;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // slots are reused only after they were read
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   if (COUNT) {
@@ -1005,13 +964,13 @@ static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
                                spray_rt_ray* sh_out = nullptr,
                                uint8_t* sh_valid = nullptr,
                                uint32_t* sh_count = nullptr,
-                               const uint8_t* valid = nullptr) {
+                               const uint32_t* idx = nullptr) {
   if (M == 0) {
     if (sh_count) return hipMemsetAsync(sh_count, 0, sizeof(uint32_t), s);
     return hipSuccess;
   }
   SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M, d_count, hits,
-              occ, counters, heads, ShadePt{}, sh_out, sh_valid, sh_count, valid};
+              occ, counters, heads, ShadePt{}, sh_out, sh_valid, sh_count, idx};
   if (shade10) {
     for (int k = 0; k < 3; ++k) {
       a.shade.lp[k] = shade10[k];
@@ -1044,15 +1003,24 @@ hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
                             M, d_count, nullptr, occluded, counters, heads);
 }
 
-hipError_t launch_scene_occluded_masked(hipStream_t s, const SlotDesc* slots,
-                                       const int* dom2slot, const float* boxes,
-                                       int ndom, const BvhNode* tlas, int ntlas,
-                                       const spray_rt_ray* rays, size_t M,
-                                       const uint8_t* valid, uint8_t* occluded,
-                                       unsigned long long* counters, uint32_t* heads) {
-  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M,
-                            nullptr, nullptr, occluded, counters, heads, nullptr,
-                            nullptr, nullptr, nullptr, valid);
+hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
+                                 uint32_t* idx_out, uint32_t* d_num, void* temp,
+                                 size_t* temp_bytes) {
+  return hipcub::DeviceSelect::Flagged(temp, *temp_bytes,
+                                       hipcub::CountingInputIterator<uint32_t>(0u),
+                                       flags, idx_out, d_num, int(M), s);
+}
+
+hipError_t launch_scene_occluded_indexed(hipStream_t s, const SlotDesc* slots,
+                                        const int* dom2slot, const float* boxes,
+                                        int ndom, const BvhNode* tlas, int ntlas,
+                                        const spray_rt_ray* rays, size_t max_n,
+                                        const uint32_t* idx, const uint32_t* d_num,
+                                        uint8_t* occluded,
+                                        unsigned long long* counters, uint32_t* heads) {
+  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays, max_n,
+                            d_num, nullptr, occluded, counters, heads, nullptr,
+                            nullptr, nullptr, nullptr, idx);
 }
 
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
