@@ -40,9 +40,12 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// Work distribution of the scene kernels (measured, profiles/): persistent
-// waves dequeuing chunks from per-XCD band queues (closest hit 128 rays, any
-// hit 64).  SPRAY_PERSIST_*=0 selects a plain one-ray-per-lane grid.
+// Work distribution of the scene kernels (measured, profiles/): closest hit
+// = persistent waves dequeuing 128-ray chunks from per-XCD band queues
+// (1.02 -> 0.71 ms: no block-coupled wave lifetimes, band-local L2); any hit
+// = one ray per lane over a plain grid (short waves: the persistent tail
+// costs more than it saves, 0.43 vs 0.48 ms).  SPRAY_PERSIST_*/SPRAY_CHUNK_*
+// select the other forms in diagnostic builds.
 #ifndef SPRAY_CHUNK_CH
 #define SPRAY_CHUNK_CH 128
 #endif
@@ -53,7 +56,7 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
 #define SPRAY_PERSIST_CH 1
 #endif
 #ifndef SPRAY_PERSIST_AH
-#define SPRAY_PERSIST_AH 1
+#define SPRAY_PERSIST_AH 0
 #endif
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 1 = domain mask
