@@ -53,6 +53,7 @@ struct spray_rt_ctx {
   int* d_dom2slot = nullptr;
   BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
   int ntlas = 0;
+  int tlas_depth = 0;
   std::vector<int> dom2slot;
   bool dom_dirty = true;
   // segment tables
@@ -423,6 +424,7 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   c->d_dom2slot = nullptr;
   c->d_tlas = nullptr;
   c->ntlas = 0;
+  c->tlas_depth = 0;
   c->ndom = ndomains;
   c->dom2slot.assign(ndomains, -1);
   c->dom_dirty = true;
@@ -440,6 +442,7 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
     HIPCHK(c, hipMemcpy(c->d_tlas, tlas.data(), tlas.size() * sizeof(BvhNode),
                         hipMemcpyHostToDevice));
     c->ntlas = int(tlas.size());
+    c->tlas_depth = depth;
   }
   return SPRAY_RT_OK;
 }
@@ -536,6 +539,16 @@ static int scene_common(spray_rt_ctx* c, const void* rays, size_t M,
   return prepare(c);
 }
 
+// The kernels' view of the resident scene; max_depth picks the traversal
+// stack size (the LDS footprint, hence the occupancy) of the launch.
+static SceneView view(const spray_rt_ctx* c) {
+  int depth = c->tlas_depth;
+  for (const SlotHost& sh : c->slots)
+    if (sh.dmem) depth = std::max(depth, sh.depth);
+  return SceneView{c->d_slots, c->d_dom2slot, c->d_boxes, c->ndom,
+                   c->d_tlas,  c->ntlas,      c->d_heads, depth};
+}
+
 // counters: optional device uint64[3] (nodes, tris, visits); exported for the
 // canonical-count tests and the bench's byte accounting cross-check.
 extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
@@ -547,9 +560,7 @@ extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
   if (M == 0) return SPRAY_RT_OK;
   hipStream_t s = stream_of(c);
   if (is_device_ptr(rays)) {
-    HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                     c->ndom, c->d_tlas, c->ntlas, rays, M, hits,
-                                     d_counters, c->d_heads));
+    HIPCHK(c, launch_scene_intersect(s, view(c), rays, M, hits, d_counters));
     return SPRAY_RT_OK;
   }
   r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
@@ -558,11 +569,8 @@ extern "C" int spray_rt_intersect_scene_counted(spray_rt_ctx_t c,
   if (r) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, M * sizeof(spray_rt_ray),
                            hipMemcpyHostToDevice, s));
-  HIPCHK(c, launch_scene_intersect(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                   c->ndom, c->d_tlas, c->ntlas,
-                                   static_cast<spray_rt_ray*>(c->d_stage),
-                                   M, static_cast<spray_rt_hit*>(c->d_stage2),
-                                   d_counters, c->d_heads));
+  HIPCHK(c, launch_scene_intersect(s, view(c), static_cast<spray_rt_ray*>(c->d_stage), M,
+                                   static_cast<spray_rt_hit*>(c->d_stage2), d_counters));
   HIPCHK(c, hipMemcpyAsync(hits, c->d_stage2, M * sizeof(spray_rt_hit),
                            hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
@@ -578,9 +586,7 @@ extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
   if (M == 0) return SPRAY_RT_OK;
   hipStream_t s = stream_of(c);
   if (is_device_ptr(rays)) {
-    HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                    c->ndom, c->d_tlas, c->ntlas, rays, M, nullptr,
-                                    occ, d_counters, c->d_heads));
+    HIPCHK(c, launch_scene_occluded(s, view(c), rays, M, nullptr, occ, d_counters));
     return SPRAY_RT_OK;
   }
   r = ensure(c, &c->d_stage, &c->stage_cap, M * sizeof(spray_rt_ray));
@@ -589,11 +595,8 @@ extern "C" int spray_rt_occluded_scene_counted(spray_rt_ctx_t c,
   if (r) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_stage, rays, M * sizeof(spray_rt_ray),
                            hipMemcpyHostToDevice, s));
-  HIPCHK(c, launch_scene_occluded(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                  c->ndom, c->d_tlas, c->ntlas,
-                                  static_cast<spray_rt_ray*>(c->d_stage),
-                                  M, nullptr, static_cast<uint8_t*>(c->d_stage2),
-                                  d_counters, c->d_heads));
+  HIPCHK(c, launch_scene_occluded(s, view(c), static_cast<spray_rt_ray*>(c->d_stage), M,
+                                  nullptr, static_cast<uint8_t*>(c->d_stage2), d_counters));
   HIPCHK(c, hipMemcpyAsync(occ, c->d_stage2, M, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return SPRAY_RT_OK;
@@ -610,10 +613,8 @@ extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
   if (max_rays == 0) return SPRAY_RT_OK;
   if (!is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(d_count))
     return fail(c, SPRAY_RT_ERR_ARG, "devcount variant needs device buffers");
-  HIPCHK(c, launch_scene_occluded(stream_of(c), c->d_slots, c->d_dom2slot,
-                                  c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
-                                  max_rays, d_count,
-                                  occ, d_counters, c->d_heads));
+  HIPCHK(c, launch_scene_occluded(stream_of(c), view(c), rays, max_rays, d_count, occ,
+                                  d_counters));
   return SPRAY_RT_OK;
 }
 
@@ -628,10 +629,8 @@ int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t c, const spray_rt_ray* rays
       (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(out_rays) ||
              !is_device_ptr(out_valid))))
     return fail(c, SPRAY_RT_ERR_ARG, "fused spawn needs device buffers");
-  HIPCHK(c, launch_scene_intersect_pt(stream_of(c), c->d_slots, c->d_dom2slot,
-                                      c->d_boxes, c->ndom, c->d_tlas, c->ntlas, rays,
-                                      M, hits, c->d_heads, shade, out_rays, out_valid,
-                                      d_count));
+  HIPCHK(c, launch_scene_intersect_pt(stream_of(c), view(c), rays, M, hits, shade,
+                                      out_rays, out_valid, d_count));
   return SPRAY_RT_OK;
 }
 
@@ -653,9 +652,7 @@ int spray_rt_occluded_scene_masked(spray_rt_ctx_t c, const spray_rt_ray* rays,
   uint32_t* idx = reinterpret_cast<uint32_t*>(base);
   uint32_t* num = reinterpret_cast<uint32_t*>(base + b_idx);
   HIPCHK(c, launch_select_flagged(s, valid, M, idx, num, base + b_idx + 256, &temp));
-  HIPCHK(c, launch_scene_occluded_indexed(s, c->d_slots, c->d_dom2slot, c->d_boxes,
-                                          c->ndom, c->d_tlas, c->ntlas, rays, M, idx,
-                                          num, occ, nullptr, c->d_heads));
+  HIPCHK(c, launch_scene_occluded_indexed(s, view(c), rays, M, idx, num, occ, nullptr));
   return SPRAY_RT_OK;
 }
 

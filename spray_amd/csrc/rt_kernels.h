@@ -24,46 +24,48 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
                           int* ids, float* ts, int* counts, int maxhits);
 
 // Fused scene path: domain list + per-domain traversal + epilogue.
-// heads: device scratch of 8*32 uint32 (per-XCD work-queue heads, zeroed by
-// the launcher with a memset on the same stream).
-// counters (optional, device uint64[3]: nodes, tris, visits) enable the
+// The resident scene as the kernels see it (all device pointers).
+struct SceneView {
+  const SlotDesc* slots;
+  const int* dom2slot;
+  const float* boxes;  // [ndom][6]
+  int ndom;
+  const BvhNode* tlas;  // top-level tree over the domain boxes
+  int ntlas;
+  uint32_t* heads;  // 8*32 uint32 work-queue heads, zeroed by every launch
+  int max_depth;    // max tree depth over resident slots and the top-level tree
+};
+
+// counters (optional, device uint64[3]: nodes, tris, visits) select the
 // counting variant used to verify the canonical traversal.
-hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
-                                  const int* dom2slot, const float* boxes,
-                                  int ndom, const BvhNode* tlas, int ntlas,
+hipError_t launch_scene_intersect(hipStream_t s, const SceneView& v,
                                   const spray_rt_ray* rays, size_t M,
-                                  spray_rt_hit* hits,
-                                  unsigned long long* counters, uint32_t* heads);
-hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
-                                 const int* dom2slot, const float* boxes,
-                                 int ndom, const BvhNode* tlas, int ntlas,
+                                  spray_rt_hit* hits, unsigned long long* counters);
+// d_count (optional, device): the launch covers min(*d_count, M) rays.
+hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
                                  const spray_rt_ray* rays, size_t M,
                                  const uint32_t* d_count, uint8_t* occluded,
-                                 unsigned long long* counters, uint32_t* heads);
+                                 unsigned long long* counters);
 
-// Closest hit with the PT shadow-ray spawn fused into the epilogue,
-// positional: out_rays[i] / out_valid[i] for source ray i; *d_count (may be
-// null) = number spawned, zeroed by the launcher.
 // idx_out[0..*d_num) = ascending i with flags[i] != 0 (hipCUB select;
 // temp == nullptr: *temp_bytes <- required scratch size).
 hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
                                  uint32_t* idx_out, uint32_t* d_num, void* temp,
                                  size_t* temp_bytes);
 // Any hit over rays idx[0..*d_num) (d_num <= max_n), occluded[idx[j]] written.
-hipError_t launch_scene_occluded_indexed(hipStream_t s, const SlotDesc* slots,
-                                        const int* dom2slot, const float* boxes,
-                                        int ndom, const BvhNode* tlas, int ntlas,
+hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
                                         const spray_rt_ray* rays, size_t max_n,
                                         const uint32_t* idx, const uint32_t* d_num,
                                         uint8_t* occluded,
-                                        unsigned long long* counters, uint32_t* heads);
-hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
-                                     const int* dom2slot, const float* boxes,
-                                     int ndom, const BvhNode* tlas, int ntlas,
+                                        unsigned long long* counters);
+// Closest hit with the PT shadow-ray spawn fused into the epilogue,
+// positional: out_rays[i] / out_valid[i] for source ray i; *d_count (may be
+// null) = number spawned, zeroed by the launcher.
+hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
                                      const spray_rt_ray* rays, size_t M,
-                                     spray_rt_hit* hits, uint32_t* heads,
-                                     const float* shade10, spray_rt_ray* out_rays,
-                                     uint8_t* out_valid, uint32_t* d_count);
+                                     spray_rt_hit* hits, const float* shade10,
+                                     spray_rt_ray* out_rays, uint8_t* out_valid,
+                                     uint32_t* d_count);
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                int spp, int tx, int ty, int tw, int th,

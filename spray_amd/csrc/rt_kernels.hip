@@ -61,6 +61,14 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 1 = domain mask
 // only, 2 = mask + ordered domain selection, no BVH traversal.
+// Minimum resident waves per SIMD the register allocator must allow (the
+// second __launch_bounds__ operand); 1 = unconstrained.
+#ifndef SPRAY_WAVES_CH
+#define SPRAY_WAVES_CH 1
+#endif
+#ifndef SPRAY_WAVES_AH
+#define SPRAY_WAVES_AH 1
+#endif
 #ifndef SPRAY_DIAG_MODE
 #define SPRAY_DIAG_MODE 0
 #endif
@@ -180,9 +188,9 @@ __device__ __forceinline__ bool aabb_ref(const float* box, const DRay& r,
 // BVH2 traversal of one slot (canonical order, see oracle.c traverse())
 // ---------------------------------------------------------------------------
 struct Best {
-  float t, u, v;
+  float t;
   uint32_t prim;  // PLY face index (tie-break key)
-  uint32_t leaf;  // leaf-order triangle index (Ng lookup)
+  uint32_t leaf;  // leaf-order triangle index (u, v, Ng are re-derived from it)
 };
 
 // ANY = occlusion (returns true at the first hit with t <= tfar_any).
@@ -193,6 +201,8 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
                                            float tnear, float tfar_any,
                                            Best& best, int32_t* stk,
                                            unsigned& nnode, unsigned& ntri) {
+  // u, v of the winner are not carried through the traversal (2 VGPRs less at
+  // the occupancy-limiting point): hit_uv() recomputes them bit-identically.
   const void* nodes = s.nodes;
   const void* tris = s.tris;
   const GAS uint32_t* __restrict__ prims = gptr(s.prims);
@@ -240,8 +250,6 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
             const uint32_t pid = prims[p];
             if (t < best.t || (t == best.t && pid < best.prim)) {
               best.t = t;
-              best.u = u;
-              best.v = v;
               best.prim = pid;
               best.leaf = p;
             }
@@ -262,6 +270,18 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
     cur = next;
   }
   return false;
+}
+
+// u, v (and Ng) of the accepted triangle: the same tri_test on the same
+// operands, hence the same bits as during the traversal.
+__device__ __forceinline__ float4 hit_uv(const SlotDesc& s, const Ray& r,
+                                         float tnear, uint32_t leaf, float& u,
+                                         float& v) {
+  const float4 a = ld4(s.tris, 3 * size_t(leaf)), b = ld4(s.tris, 3 * size_t(leaf) + 1),
+               c = ld4(s.tris, 3 * size_t(leaf) + 2);
+  float t;
+  tri_test(r, tnear, a, b, c, t, u, v);
+  return c;
 }
 
 // TriMeshBuffer::updateIntersection (src/render/trimesh_buffer.cc:328-360).
@@ -329,15 +349,16 @@ __global__ __launch_bounds__(kBlock) void k_rtc_intersect(
   const float* f = reinterpret_cast<const float*>(rec);
   const Ray r = make_ray(f[0], f[1], f[2], f[4], f[5], f[6]);
   const float tnear = f[8];
-  Best best{f[9], 0.f, 0.f, 0xFFFFFFFFu, 0u};
+  Best best{f[9], 0xFFFFFFFFu, 0u};
   unsigned a = 0, b = 0;
   if (s.nnodes)
     trace_slot<false, false>(s, r, tnear, 0.f, best, stack + threadIdx.x, a, b);
   if (best.prim == 0xFFFFFFFFu) return;  // miss: record untouched
-  const float4 c = ld4(s.tris, 3 * size_t(best.leaf) + 2);
+  float hu, hv;
+  const float4 c = hit_uv(s, r, tnear, best.leaf, hu, hv);
   uint32_t color;
   float nsx, nsy, nsz;
-  epilogue(s, best.prim, best.u, best.v, color, nsx, nsy, nsz);
+  epilogue(s, best.prim, hu, hv, color, nsx, nsy, nsz);
   float* o = reinterpret_cast<float*>(rec);
   uint32_t* ou = reinterpret_cast<uint32_t*>(rec);
   o[9] = best.t;          // tfar
@@ -345,8 +366,8 @@ __global__ __launch_bounds__(kBlock) void k_rtc_intersect(
   o[13] = c.z;
   o[14] = c.w;
   ou[15] = color;         // color (offset 60)
-  o[16] = best.u;
-  o[17] = best.v;
+  o[16] = hu;
+  o[17] = hv;
   ou[18] = 0u;            // geomID (one mesh per slot)
   ou[19] = best.prim;     // primID
   o[21] = nsx;            // Ns (offset 84)
@@ -366,7 +387,7 @@ __global__ __launch_bounds__(kBlock) void k_rtc_occluded(
   char* rec = rays + i * stride;
   const float* f = reinterpret_cast<const float*>(rec);
   const Ray r = make_ray(f[0], f[1], f[2], f[4], f[5], f[6]);
-  Best best{0.f, 0.f, 0.f, 0u, 0u};
+  Best best{0.f, 0u, 0u};
   unsigned a = 0, b = 0;
   if (s.nnodes &&
       trace_slot<true, false>(s, r, f[8], f[9], best, stack + threadIdx.x, a, b))
@@ -505,24 +526,25 @@ __device__ __host__ __forceinline__ size_t band_size(size_t M) {
 
 template <int W, bool ANY, bool COUNT, bool SPAWN>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
-                                          const float* sbox, const float4* stl,
-                                          int32_t* stk, unsigned& nnode,
-                                          unsigned& ntri, unsigned& nvisit,
-                                          bool& spawn, float* pos, float* wi) {
+                                          const float4* stl, int32_t* stk,
+                                          unsigned& nnode, unsigned& ntri,
+                                          unsigned& nvisit, bool& spawn, float* pos,
+                                          float* wi) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
+  const GAS float* __restrict__ boxes = gptr(A.boxes);
   const int ntlas = A.ntlas;
   spray_rt_hit* __restrict__ hits = A.hits;
   uint8_t* __restrict__ occ = A.occ;
   {
     const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
     const float4 o4 = rp[0], d4 = rp[1];
-    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
     if (ntlas > 0) {
+      const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
       int sp = 0;
       int32_t cur = 0;
       for (;;) {
@@ -566,28 +588,43 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
       else occ[i] = uint8_t(pc);
       return;
     }
-    Best best{ANY ? 0.f : d4.w, 0.f, 0.f, 0xFFFFFFFFu, 0u};
+    // Closest hit keeps (t, prim, leaf) of the running winner in place.  A
+    // later domain may only win with a strictly smaller t (the earlier
+    // entry of the sorted domain list wins ties): its traversal starts with
+    // the tie-break key at 0, and leaf at a sentinel tells whether it won.
+    Best best{ANY ? 0.f : d4.w, 0xFFFFFFFFu, 0xFFFFFFFFu};
     int best_dom = -1;
     bool occluded = false;
     for (;;) {
       float st = kInf;
       int sb = -1;
+      bool any_left = false;
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        uint64_t bits = m[w];
-        while (bits) {
-          const int j = __ffsll((long long)bits) - 1;
-          bits &= bits - 1;
-          const int b = 64 * w + j;
-          float tm;
-          aabb_ref(sbox + 6 * b, dr, tm);
-          if (sb < 0 || tm < st) {
-            st = tm;
-            sb = b;
+      for (int w = 0; w < W; ++w) any_left |= m[w] != 0;
+      if (!any_left) break;
+      {
+        // the reference's domain ray (division-based inverse), rebuilt per
+        // selection: keeping it live through trace_slot costs occupancy
+        float dx = r.dx, dy = r.dy, dz = r.dz;
+        asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+        const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          uint64_t bits = m[w];
+          while (bits) {
+            const int j = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            const int b = 64 * w + j;
+            float tm;
+            const GAS float* bx = boxes + 6 * b;
+            aabb_ref6(bx[0], bx[1], bx[2], bx[3], bx[4], bx[5], dr, tm);
+            if (sb < 0 || tm < st) {
+              st = tm;
+              sb = b;
+            }
           }
         }
       }
-      if (sb < 0) break;
 #pragma unroll
       for (int w = 0; w < W; ++w)
         if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
@@ -607,12 +644,15 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
           break;
         }
       } else {
-        Best local = best;
-        if (best_dom >= 0) local.prim = 0u;  // strictly nearer from now on
-        trace_slot<false, COUNT>(s, r, o4.w, 0.f, local, stk, nnode, ntri);
-        if (local.t < best.t || (best_dom < 0 && local.prim != 0xFFFFFFFFu)) {
-          best = local;
+        const uint32_t keep_prim = best.prim, keep_leaf = best.leaf;
+        if (best_dom >= 0) best.prim = 0u;  // strictly nearer from now on
+        best.leaf = 0xFFFFFFFFu;
+        trace_slot<false, COUNT>(s, r, o4.w, 0.f, best, stk, nnode, ntri);
+        if (best.leaf != 0xFFFFFFFFu) {
           best_dom = sb;
+        } else {
+          best.prim = keep_prim;
+          best.leaf = keep_leaf;
         }
       }
     }
@@ -629,11 +669,12 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         h1 = h2 = h0;
       } else {
         const SlotDesc s = slots[dom2slot[best_dom]];
-        const float4 c = ld4(s.tris, 3 * size_t(best.leaf) + 2);
+        float hu, hv;
+        const float4 c = hit_uv(s, r, o4.w, best.leaf, hu, hv);
         uint32_t color;
         float nsx, nsy, nsz;
-        epilogue(s, best.prim, best.u, best.v, color, nsx, nsy, nsz);
-        h0 = make_float4(best.t, best.u, best.v, __uint_as_float(best.prim));
+        epilogue(s, best.prim, hu, hv, color, nsx, nsy, nsz);
+        h0 = make_float4(best.t, hu, hv, __uint_as_float(best.prim));
         h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
         h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
       }
@@ -693,10 +734,14 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
   }
 }
 
-template <int W, bool ANY, bool COUNT, bool SPAWN>
-__global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
-  __shared__ int32_t stack[kStack * kBlock];
-  __shared__ float sbox[6 * 64 * W];
+// STK: traversal-stack entries per lane, >= the depth of every resident
+// slot tree and of the top-level tree (a node at depth k has at most k
+// pending siblings).  LDS = STK KiB + 4 KiB per 64 domains, so STK 16 lets 8
+// blocks (32 waves) share a CU where 24 allowed 5.
+template <int W, bool ANY, bool COUNT, bool SPAWN, int STK>
+__global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void k_scene(
+    SceneArgs A) {
+  __shared__ int32_t stack[STK * kBlock];
   __shared__ float4 stl[4 * 64 * W];
   size_t M = A.M;
   if (A.d_count) {  // ray count produced on the device
@@ -704,7 +749,6 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
     M = dc < M ? dc : M;
   }
   const size_t S = band_size(M);
-  for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
   __syncthreads();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
@@ -718,8 +762,8 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
     if (j < M)
-      scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit, flag,
-                                      pos, wi);
+      scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, stk, nnode, ntri, nvisit, flag, pos,
+                                      wi);
     if (SPAWN) store_shadow(A, j < M, flag, i, pos, wi);
   } else {
     // waves dequeue kChunk-slot chunks of their XCD's band first
@@ -743,8 +787,8 @@ __global__ __launch_bounds__(kBlock) void k_scene(SceneArgs A) {
           const size_t i = (idx && j < end) ? idx[j] : j;
           flag = false;
           if (j < end)
-            scene_ray<W, ANY, COUNT, SPAWN>(A, i, sbox, stl, stk, nnode, ntri, nvisit,
-                                            flag, pos, wi);
+            scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, stk, nnode, ntri, nvisit, flag,
+                                            pos, wi);
           if (SPAWN) store_shadow(A, j < end, flag, i, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
@@ -925,16 +969,19 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
   return hipGetLastError();
 }
 
-template <int W, bool ANY, bool COUNT, bool SPAWN>
+template <int W, bool ANY, bool COUNT, bool SPAWN, int STK>
 static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
   if (kPersist && !grid) {
     int dev = 0, cus = 0, per_cu = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scene<W, ANY, COUNT, SPAWN>,
-                                                 kBlock, 0);
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess)
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, k_scene<W, ANY, COUNT, SPAWN, STK>, kBlock, 0);
+    if (e != hipSuccess) return e;
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
   hipError_t e = hipSuccess;
@@ -943,67 +990,60 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
-  k_scene<W, ANY, COUNT, SPAWN><<<g, kBlock, 0, s>>>(a);
+  k_scene<W, ANY, COUNT, SPAWN, STK><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
+template <int W, bool ANY, bool SPAWN, int STK>
+static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a) {
+  return a.counters ? launch_scene_t<W, ANY, true, SPAWN, STK>(s, a)
+                    : launch_scene_t<W, ANY, false, SPAWN, STK>(s, a);
+}
+
 template <bool ANY, bool SPAWN>
-static hipError_t launch_scene_w(hipStream_t s, const SceneArgs& a, int ndom) {
-  if (ndom <= 64)
-    return a.counters ? launch_scene_t<1, ANY, true, SPAWN>(s, a)
-                      : launch_scene_t<1, ANY, false, SPAWN>(s, a);
-  return a.counters ? launch_scene_t<4, ANY, true, SPAWN>(s, a)
-                    : launch_scene_t<4, ANY, false, SPAWN>(s, a);
+static hipError_t launch_scene_w(hipStream_t s, const SceneArgs& a, int max_depth) {
+  if (max_depth > kStack) return hipErrorInvalidValue;
+  if (a.ndom <= 64)
+    return max_depth <= 16 ? launch_scene_c<1, ANY, SPAWN, 16>(s, a)
+                           : launch_scene_c<1, ANY, SPAWN, kStack>(s, a);
+  return max_depth <= 16 ? launch_scene_c<4, ANY, SPAWN, 16>(s, a)
+                         : launch_scene_c<4, ANY, SPAWN, kStack>(s, a);
 }
 
-template <bool ANY>
-static hipError_t launch_scene(hipStream_t s, const SlotDesc* slots,
-                               const int* dom2slot, const float* boxes,
-                               int ndom, const BvhNode* tlas, int ntlas,
-                               const spray_rt_ray* rays, size_t M,
-                               const uint32_t* d_count, spray_rt_hit* hits,
-                               uint8_t* occ, unsigned long long* counters,
-                               uint32_t* heads, const float* shade10 = nullptr,
-                               spray_rt_ray* sh_out = nullptr,
-                               uint8_t* sh_valid = nullptr,
-                               uint32_t* sh_count = nullptr,
-                               const uint32_t* idx = nullptr) {
-  if (M == 0) {
-    if (sh_count) return hipMemsetAsync(sh_count, 0, sizeof(uint32_t), s);
-    return hipSuccess;
-  }
-  SceneArgs a{slots, dom2slot, boxes, ndom, tlas, ntlas, rays, M, d_count, hits,
-              occ, counters, heads, ShadePt{}, sh_out, sh_valid, sh_count, idx};
-  if (shade10) {
-    for (int k = 0; k < 3; ++k) {
-      a.shade.lp[k] = shade10[k];
-      a.shade.lr[k] = shade10[3 + k];
-      a.shade.ks[k] = shade10[6 + k];
-    }
-    a.shade.shininess = shade10[9];
-    return launch_scene_w<ANY, true>(s, a, ndom);
-  }
-  return launch_scene_w<ANY, false>(s, a, ndom);
+static SceneArgs scene_args(const SceneView& v, const spray_rt_ray* rays, size_t M) {
+  SceneArgs a{};
+  a.slots = v.slots;
+  a.dom2slot = v.dom2slot;
+  a.boxes = v.boxes;
+  a.ndom = v.ndom;
+  a.tlas = v.tlas;
+  a.ntlas = v.ntlas;
+  a.heads = v.heads;
+  a.rays = rays;
+  a.M = M;
+  return a;
 }
 
-hipError_t launch_scene_intersect(hipStream_t s, const SlotDesc* slots,
-                                  const int* dom2slot, const float* boxes,
-                                  int ndom, const BvhNode* tlas, int ntlas,
+hipError_t launch_scene_intersect(hipStream_t s, const SceneView& v,
                                   const spray_rt_ray* rays, size_t M,
-                                  spray_rt_hit* hits,
-                                  unsigned long long* counters, uint32_t* heads) {
-  return launch_scene<false>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
-                             M, nullptr, hits, nullptr, counters, heads);
+                                  spray_rt_hit* hits, unsigned long long* counters) {
+  if (M == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.hits = hits;
+  a.counters = counters;
+  return launch_scene_w<false, false>(s, a, v.max_depth);
 }
 
-hipError_t launch_scene_occluded(hipStream_t s, const SlotDesc* slots,
-                                 const int* dom2slot, const float* boxes,
-                                 int ndom, const BvhNode* tlas, int ntlas,
+hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
                                  const spray_rt_ray* rays, size_t M,
                                  const uint32_t* d_count, uint8_t* occluded,
-                                 unsigned long long* counters, uint32_t* heads) {
-  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
-                            M, d_count, nullptr, occluded, counters, heads);
+                                 unsigned long long* counters) {
+  if (M == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.d_count = d_count;
+  a.occ = occluded;
+  a.counters = counters;
+  return launch_scene_w<true, false>(s, a, v.max_depth);
 }
 
 hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
@@ -1014,28 +1054,38 @@ hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
                                        flags, idx_out, d_num, int(M), s);
 }
 
-hipError_t launch_scene_occluded_indexed(hipStream_t s, const SlotDesc* slots,
-                                        const int* dom2slot, const float* boxes,
-                                        int ndom, const BvhNode* tlas, int ntlas,
+hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
                                         const spray_rt_ray* rays, size_t max_n,
                                         const uint32_t* idx, const uint32_t* d_num,
                                         uint8_t* occluded,
-                                        unsigned long long* counters, uint32_t* heads) {
-  return launch_scene<true>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays, max_n,
-                            d_num, nullptr, occluded, counters, heads, nullptr,
-                            nullptr, nullptr, nullptr, idx);
+                                        unsigned long long* counters) {
+  if (max_n == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, max_n);
+  a.idx = idx;
+  a.d_count = d_num;
+  a.occ = occluded;
+  a.counters = counters;
+  return launch_scene_w<true, false>(s, a, v.max_depth);
 }
 
-hipError_t launch_scene_intersect_pt(hipStream_t s, const SlotDesc* slots,
-                                     const int* dom2slot, const float* boxes,
-                                     int ndom, const BvhNode* tlas, int ntlas,
+hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
                                      const spray_rt_ray* rays, size_t M,
-                                     spray_rt_hit* hits, uint32_t* heads,
-                                     const float* shade10, spray_rt_ray* out_rays,
-                                     uint8_t* out_valid, uint32_t* d_count) {
-  return launch_scene<false>(s, slots, dom2slot, boxes, ndom, tlas, ntlas, rays,
-                             M, nullptr, hits, nullptr, nullptr, heads, shade10,
-                             out_rays, out_valid, d_count);
+                                     spray_rt_hit* hits, const float* shade10,
+                                     spray_rt_ray* out_rays, uint8_t* out_valid,
+                                     uint32_t* d_count) {
+  if (M == 0) return d_count ? hipMemsetAsync(d_count, 0, sizeof(uint32_t), s) : hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.hits = hits;
+  for (int k = 0; k < 3; ++k) {
+    a.shade.lp[k] = shade10[k];
+    a.shade.lr[k] = shade10[3 + k];
+    a.shade.ks[k] = shade10[6 + k];
+  }
+  a.shade.shininess = shade10[9];
+  a.sh_out = out_rays;
+  a.sh_valid = out_valid;
+  a.sh_count = d_count;
+  return launch_scene_w<false, true>(s, a, v.max_depth);
 }
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
