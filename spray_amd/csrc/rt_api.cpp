@@ -51,6 +51,7 @@ struct spray_rt_ctx {
   int ndom = 0;
   float* d_boxes = nullptr;
   int* d_dom2slot = nullptr;
+  DomTrav* d_domtrav = nullptr;  // per-domain traversal descriptors
   BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
   int ntlas = 0;
   int tlas_depth = 0;
@@ -127,6 +128,7 @@ int prepare(spray_rt_ctx* c) {
   hipStream_t s = stream_of(c);
   for (SlotHost& sh : c->slots)
     if (sh.ready) HIPCHK(c, hipStreamWaitEvent(s, sh.ready, 0));
+  const bool trav_dirty = c->slots_dirty || c->dom_dirty;
   if (c->slots_dirty) {
     size_t n = std::max<size_t>(c->slots.size(), 1);
     if (c->d_slots_cap < n) {
@@ -147,6 +149,23 @@ int prepare(spray_rt_ctx* c) {
                              c->ndom * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(c, hipStreamSynchronize(s));
     c->dom_dirty = false;
+  }
+  if (trav_dirty && c->ndom > 0) {
+    std::vector<DomTrav> t(c->ndom);
+    for (int d = 0; d < c->ndom; ++d) {
+      const int slot = c->dom2slot[d];
+      t[d] = DomTrav{nullptr, 0, 0};
+      if (slot < 0 || size_t(slot) >= c->slots.size()) continue;
+      const SlotDesc& sd = c->slots[slot].desc;
+      if (!sd.nnodes) continue;
+      const char* base = reinterpret_cast<const char*>(sd.nodes);
+      t[d].nodes = sd.nodes;
+      t[d].tri_off = uint32_t(reinterpret_cast<const char*>(sd.tris) - base);
+      t[d].prim_off = uint32_t(reinterpret_cast<const char*>(sd.prims) - base);
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_domtrav, t.data(), c->ndom * sizeof(DomTrav),
+                             hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamSynchronize(s));
   }
   return SPRAY_RT_OK;
 }
@@ -254,7 +273,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
     if (s.ready) (void)hipEventDestroy(s.ready);
     if (s.pinned) (void)hipHostFree(s.pinned);
   }
-  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_tlas, c->d_seg_slot,
+  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_domtrav, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
                   c->d_block_counts, c->d_heads, c->d_sel};
   for (void* b : bufs)
@@ -419,9 +438,11 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   HIPCHK(c, hipStreamSynchronize(stream_of(c)));
   if (c->d_boxes) HIPCHK(c, hipFree(c->d_boxes));
   if (c->d_dom2slot) HIPCHK(c, hipFree(c->d_dom2slot));
+  if (c->d_domtrav) HIPCHK(c, hipFree(c->d_domtrav));
   if (c->d_tlas) HIPCHK(c, hipFree(c->d_tlas));
   c->d_boxes = nullptr;
   c->d_dom2slot = nullptr;
+  c->d_domtrav = nullptr;
   c->d_tlas = nullptr;
   c->ntlas = 0;
   c->tlas_depth = 0;
@@ -431,6 +452,7 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   if (ndomains == 0) return SPRAY_RT_OK;
   HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_boxes), 6 * ndomains * sizeof(float)));
   HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_dom2slot), ndomains * sizeof(int)));
+  HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_domtrav), ndomains * sizeof(DomTrav)));
   HIPCHK(c, hipMemcpy(c->d_boxes, boxes, 6 * ndomains * sizeof(float),
                       hipMemcpyHostToDevice));
   std::vector<BvhNode> tlas;
@@ -535,7 +557,7 @@ static int scene_common(spray_rt_ctx* c, const void* rays, size_t M,
   if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->d_heads)
-    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), 8 * 32 * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), kQueues * 32 * sizeof(uint32_t)));
   return prepare(c);
 }
 
@@ -545,8 +567,8 @@ static SceneView view(const spray_rt_ctx* c) {
   int depth = c->tlas_depth;
   for (const SlotHost& sh : c->slots)
     if (sh.dmem) depth = std::max(depth, sh.depth);
-  return SceneView{c->d_slots, c->d_dom2slot, c->d_boxes, c->ndom,
-                   c->d_tlas,  c->ntlas,      c->d_heads, depth};
+  return SceneView{c->d_slots, c->d_dom2slot, c->d_domtrav, c->d_boxes, c->ndom,
+                   c->d_tlas,  c->ntlas,      c->d_heads,   depth};
 }
 
 // counters: optional device uint64[3] (nodes, tris, visits); exported for the

@@ -55,4 +55,18 @@ struct alignas(16) SlotDesc {
   uint32_t pad;
 };
 
+// Per-domain traversal descriptor of the scene path (16 B, staged in LDS by
+// the scene kernels): tris / prims live at byte offsets from the slot's
+// nodes; nodes == nullptr marks a domain that is not resident (or empty).
+struct alignas(16) DomTrav {
+  const BvhNode* nodes;
+  uint32_t tri_off;
+  uint32_t prim_off;
+};
+static_assert(sizeof(DomTrav) == 16, "DomTrav must be 16 B");
+
+// Persistent scene launches: kQueues work queues (kQueues / 8 per XCD), head
+// counters 32 words apart.
+constexpr int kQueues = 64;
+
 }  // namespace spray_rt

@@ -28,11 +28,12 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 struct SceneView {
   const SlotDesc* slots;
   const int* dom2slot;
-  const float* boxes;  // [ndom][6]
+  const DomTrav* domtrav;  // [ndom]
+  const float* boxes;      // [ndom][6]
   int ndom;
   const BvhNode* tlas;  // top-level tree over the domain boxes
   int ntlas;
-  uint32_t* heads;  // 8*32 uint32 work-queue heads, zeroed by every launch
+  uint32_t* heads;  // kQueues*32 uint32 work-queue heads, zeroed by every launch
   int max_depth;    // max tree depth over resident slots and the top-level tree
 };
 

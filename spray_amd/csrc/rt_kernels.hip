@@ -59,12 +59,13 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
 #define SPRAY_PERSIST_AH 0
 #endif
 
-// Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 1 = domain mask
+// Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 3 = ray in, 4 B out
+// (no domain tree), 4 = mask with the fast slab test, 1 = domain mask
 // only, 2 = mask + ordered domain selection, no BVH traversal.
 // Minimum resident waves per SIMD the register allocator must allow (the
 // second __launch_bounds__ operand); 1 = unconstrained.
 #ifndef SPRAY_WAVES_CH
-#define SPRAY_WAVES_CH 1
+#define SPRAY_WAVES_CH 6
 #endif
 #ifndef SPRAY_WAVES_AH
 #define SPRAY_WAVES_AH 1
@@ -197,15 +198,14 @@ struct Best {
 // Closest hit: keeps the lexicographic minimum of (t, prim) starting from
 // best; a candidate with t == best.t wins only with a smaller face index.
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
+__device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
+                                           const uint32_t* prims_, const Ray& r,
                                            float tnear, float tfar_any,
                                            Best& best, int32_t* stk,
                                            unsigned& nnode, unsigned& ntri) {
   // u, v of the winner are not carried through the traversal (2 VGPRs less at
   // the occupancy-limiting point): hit_uv() recomputes them bit-identically.
-  const void* nodes = s.nodes;
-  const void* tris = s.tris;
-  const GAS uint32_t* __restrict__ prims = gptr(s.prims);
+  const GAS uint32_t* __restrict__ prims = gptr(prims_);
   int sp = 0;
   int32_t cur = 0;
   for (;;) {
@@ -270,6 +270,15 @@ __device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
     cur = next;
   }
   return false;
+}
+
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
+                                           float tnear, float tfar_any,
+                                           Best& best, int32_t* stk,
+                                           unsigned& nnode, unsigned& ntri) {
+  return trace_tree<ANY, COUNT>(s.nodes, s.tris, s.prims, r, tnear, tfar_any, best,
+                                stk, nnode, ntri);
 }
 
 // u, v (and Ng) of the accepted triangle: the same tri_test on the same
@@ -498,6 +507,7 @@ __device__ __forceinline__ bool shadow_pt(const spray_rt_ray& ray,
 struct SceneArgs {
   const SlotDesc* slots;
   const int* dom2slot;
+  const DomTrav* domtrav;
   const float* boxes;
   int ndom;
   const BvhNode* tlas;
@@ -508,7 +518,7 @@ struct SceneArgs {
   spray_rt_hit* hits;
   uint8_t* occ;
   unsigned long long* counters;
-  uint32_t* heads;  // 8 queue heads, 32 words apart (persistent launch)
+  uint32_t* heads;  // kQueues queue heads, 32 words apart (persistent launch)
   // fused PT shadow spawn (closest hit): positional output
   ShadePt shade;
   spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
@@ -518,21 +528,22 @@ struct SceneArgs {
   const uint32_t* idx;
 };
 
-// Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): the unit of
-// XCD affinity of the persistent launches.
+// Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): one work
+// queue of the persistent launches; bands 8x .. 8x+7 (a contiguous eighth of
+// the rays) are the home queues of XCD x.
 __device__ __host__ __forceinline__ size_t band_size(size_t M) {
-  return (((M + 7) / 8) + 63) / 64 * 64;
+  return (((M + kQueues - 1) / kQueues) + 63) / 64 * 64;
 }
 
 template <int W, bool ANY, bool COUNT, bool SPAWN>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
-                                          const float4* stl, int32_t* stk,
+                                          const float4* stl, const float* sbox,
+                                          const float4* sdom, int32_t* stk,
                                           unsigned& nnode, unsigned& ntri,
                                           unsigned& nvisit, bool& spawn, float* pos,
                                           float* wi) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
-  const GAS float* __restrict__ boxes = gptr(A.boxes);
   const int ntlas = A.ntlas;
   spray_rt_hit* __restrict__ hits = A.hits;
   uint8_t* __restrict__ occ = A.occ;
@@ -543,7 +554,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
-    if (ntlas > 0) {
+    if (ntlas > 0 && SPRAY_DIAG_MODE != 3) {
       const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
       int sp = 0;
       int32_t cur = 0;
@@ -552,9 +563,14 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                      e = stl[4 * cur + 3];
         const int32_t cl = __float_as_int(e.x), cr = __float_as_int(e.y);
         float tm;
-        const bool hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
-        const bool hr =
-            cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+        bool hl, hr;
+        if (SPRAY_DIAG_MODE == 4) {  // diagnostic: fast slab instead of exact
+          hl = slab(r, a.x, a.y, a.z, a.w, b.x, b.y, 0.f, kInf, tm);
+          hr = cr != INT_MIN && slab(r, b.z, b.w, c.x, c.y, c.z, c.w, 0.f, kInf, tm);
+        } else {
+          hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
+          hr = cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+        }
         int32_t next = kNone;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -580,7 +596,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         cur = next;
       }
     }
-    if (SPRAY_DIAG_MODE == 1) {  // diagnostic: domain mask only
+    if (SPRAY_DIAG_MODE == 1 || SPRAY_DIAG_MODE >= 3) {  // diagnostic: mask only
       uint32_t pc = 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) pc += __popcll(m[w]);
@@ -616,8 +632,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
             bits &= bits - 1;
             const int b = 64 * w + j;
             float tm;
-            const GAS float* bx = boxes + 6 * b;
-            aabb_ref6(bx[0], bx[1], bx[2], bx[3], bx[4], bx[5], dr, tm);
+            aabb_ref(sbox + 6 * b, dr, tm);
             if (sb < 0 || tm < st) {
               st = tm;
               sb = b;
@@ -628,10 +643,12 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
 #pragma unroll
       for (int w = 0; w < W; ++w)
         if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
-      const int slot = dom2slot[sb];
-      if (slot < 0) continue;
-      const SlotDesc s = slots[slot];
-      if (!s.nnodes) continue;
+      const float4 dt = sdom[sb];
+      const char* nodes = reinterpret_cast<const char*>(
+          (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
+      if (!nodes) continue;  // not resident here (or empty)
+      const void* tris = nodes + __float_as_uint(dt.z);
+      const uint32_t* prims = reinterpret_cast<const uint32_t*>(nodes + __float_as_uint(dt.w));
       if (COUNT) ++nvisit;
       if (SPRAY_DIAG_MODE == 2) {  // diagnostic: no traversal
         best.prim = sb;
@@ -639,7 +656,8 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         continue;
       }
       if (ANY) {
-        if (trace_slot<true, COUNT>(s, r, o4.w, d4.w, best, stk, nnode, ntri)) {
+        if (trace_tree<true, COUNT>(nodes, tris, prims, r, o4.w, d4.w, best, stk, nnode,
+                                    ntri)) {
           occluded = true;
           break;
         }
@@ -647,7 +665,8 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         const uint32_t keep_prim = best.prim, keep_leaf = best.leaf;
         if (best_dom >= 0) best.prim = 0u;  // strictly nearer from now on
         best.leaf = 0xFFFFFFFFu;
-        trace_slot<false, COUNT>(s, r, o4.w, 0.f, best, stk, nnode, ntri);
+        trace_tree<false, COUNT>(nodes, tris, prims, r, o4.w, 0.f, best, stk, nnode,
+                                 ntri);
         if (best.leaf != 0xFFFFFFFFu) {
           best_dom = sb;
         } else {
@@ -709,12 +728,15 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 
-// Persistent launch: each wave dequeues 64-ray chunks.  Queue q owns the
-// contiguous ray range [q*M/8, (q+1)*M/8) -- an image band -- and is drained
-// first by the waves of XCD q (L2 locality: an XCD's L2 holds the BVH nodes of
-// its band); a wave whose queue is empty steals from the others.  No wave
-// waits on another: every wave exits once all eight queues are drained.
-// The heads are zeroed by a memset node before every launch.
+// Persistent launch: each wave dequeues kChunk-ray chunks from kQueues
+// queues, each owning a contiguous band of the rays.  XCD x's waves start on
+// its eight bands (an eighth of the image: its L2 holds the BVH nodes of that
+// region), spread over them by block index so that no head counter sees more
+// than 1/kQueues of the dequeues (same-address atomics serialise in L2), and
+// then steal -- first within the XCD, then from the others.  A drained queue
+// is recognised by a plain load of its head, so the end of the launch costs
+// no atomics.  No wave waits on another.  The heads are zeroed by a memset
+// before every launch.
 // Positional spawn output: the shadow ray of source i goes to sh_out[i],
 // sh_valid[i] says whether it exists; one atomic per wave for the total.
 __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
@@ -742,7 +764,9 @@ template <int W, bool ANY, bool COUNT, bool SPAWN, int STK>
 __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void k_scene(
     SceneArgs A) {
   __shared__ int32_t stack[STK * kBlock];
-  __shared__ float4 stl[4 * 64 * W];
+  __shared__ float4 stl[4 * 64 * W];   // top-level tree
+  __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
+  __shared__ float4 sdom[64 * W];      // DomTrav per domain
   size_t M = A.M;
   if (A.d_count) {  // ray count produced on the device
     const size_t dc = *A.d_count;
@@ -750,6 +774,8 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
   }
   const size_t S = band_size(M);
   for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
+  for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
+  for (int k = threadIdx.x; k < A.ndom; k += kBlock) sdom[k] = ld4(A.domtrav, k);
   __syncthreads();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
   int32_t* stk = stack + threadIdx.x;
@@ -762,33 +788,38 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
     if (j < M)
-      scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, stk, nnode, ntri, nvisit, flag, pos,
-                                      wi);
+      scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, sbox, sdom, stk, nnode, ntri, nvisit,
+                                      flag, pos, wi);
     if (SPAWN) store_shadow(A, j < M, flag, i, pos, wi);
   } else {
-    // waves dequeue kChunk-slot chunks of their XCD's band first
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
-    const uint32_t home = xcc_id() & 7u;
-    for (uint32_t k = 0; k < 8; ++k) {
-      const uint32_t q = (home + k) & 7u;
+    constexpr uint32_t kPerXcd = kQueues / 8;
+    const uint32_t xcd = xcc_id() & 7u;
+    const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
+    for (uint32_t k = 0; k < uint32_t(kQueues); ++k) {
+      const uint32_t q = ((xcd + k / kPerXcd) & 7u) * kPerXcd + (sub + k) % kPerXcd;
       const size_t begin = size_t(q) * S;
       const size_t end = begin + S < M ? begin + S : M;
       if (begin >= end) continue;
-      // the next chunk is dequeued before the current one is traced, so the
-      // atomic's latency overlaps the traversal
+      uint32_t* head = &A.heads[32 * q];
       uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&A.heads[32 * q], kChunk);
+      if (lane == 0) {
+        base = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (begin + base < end) base = atomicAdd(head, kChunk);
+      }
       base = __builtin_amdgcn_readfirstlane(base);
       while (begin + base < end) {
+        // the next chunk is dequeued before this one is traced: the atomic's
+        // latency overlaps the traversal
         uint32_t next = 0;
-        if (lane == 0) next = atomicAdd(&A.heads[32 * q], kChunk);
+        if (lane == 0) next = atomicAdd(head, kChunk);
         for (uint32_t c = 0; c < kChunk; c += 64) {
           const size_t j = begin + base + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
           flag = false;
           if (j < end)
-            scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, stk, nnode, ntri, nvisit, flag,
-                                            pos, wi);
+            scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, sbox, sdom, stk, nnode, ntri,
+                                            nvisit, flag, pos, wi);
           if (SPAWN) store_shadow(A, j < end, flag, i, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
@@ -985,7 +1016,7 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
   hipError_t e = hipSuccess;
-  if (kPersist) e = hipMemsetAsync(a.heads, 0, 8 * 32 * sizeof(uint32_t), s);
+  if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
   if (e == hipSuccess && SPAWN && a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
@@ -1014,6 +1045,7 @@ static SceneArgs scene_args(const SceneView& v, const spray_rt_ray* rays, size_t
   SceneArgs a{};
   a.slots = v.slots;
   a.dom2slot = v.dom2slot;
+  a.domtrav = v.domtrav;
   a.boxes = v.boxes;
   a.ndom = v.ndom;
   a.tlas = v.tlas;
