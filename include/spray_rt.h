@@ -191,9 +191,9 @@ int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t ctx, const spray_rt_ray* ra
                                       const float shade[10], spray_rt_ray* out_rays,
                                       uint8_t* out_valid, uint32_t* d_count);
 /* Any hit over the rays i < M with valid[i] != 0 (e.g. the positional spawn
- * output): occluded[i] is written for those rays only.  The kernel re-packs
- * the sparse valid rays into full wavefronts (ballot + prefix into an LDS
- * ring) in near-source order.  Device buffers only. */
+ * output): occluded[i] is written for those rays only.  The valid rays are
+ * first compacted into an ascending index list (device select), so the
+ * traversal runs on full wavefronts in source order.  Device buffers only. */
 int spray_rt_occluded_scene_masked(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                                    size_t M, const uint8_t* valid,
                                    uint8_t* occluded);
@@ -205,6 +205,28 @@ int spray_rt_occluded_scene_devcount(spray_rt_ctx_t ctx, const spray_rt_ray* ray
                                      uint8_t* occluded,
                                      unsigned long long* d_counters);
 
+/* ---- in-situ (domain-sharded, one rank per GPU) ---- */
+/* Domain -> rank map of the partition (InsituPartition::rank,
+ * src/render/data_partition.h:48-56): owner[ndomains] host array, ranks in
+ * [0, 64), -1 = nobody.  Reset by spray_rt_domain_bounds. */
+int spray_rt_set_owners(spray_rt_ctx_t ctx, const int* owner);
+/* Routing of a ray batch (insitu::Isector::intersect,
+ * src/insitu/insitu_isector.h:164-224, speculative: every domain on the
+ * list): rank_mask[i] = OR of (1 << owner[d]) over the domains d whose box
+ * the ray enters.  Device buffers only. */
+int spray_rt_route(spray_rt_ctx_t ctx, const spray_rt_ray* rays, size_t M,
+                   uint64_t* rank_mask);
+/* Closest hit over the RESIDENT domains of each ray's list (mapped slots;
+ * the others are skipped) plus the composite key that orders hits the way
+ * the sequential walk of the whole list does:
+ *   keys[i] = (bits(t) << 32) | (list position << 16) | domain,
+ *   0x7FFFFFFFFFFFFFFF on a miss.
+ * The minimum key over all ranks (VBuf tbuf compositing,
+ * src/insitu/insitu_vbuf.h:74-152) identifies the hit of the full scene.
+ * Device buffers only. */
+int spray_rt_intersect_scene_keyed(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                   size_t M, spray_rt_hit* hits, uint64_t* keys);
+
 /* ---- ray sources on the device (caller side of the hot path) ---- */
 /* cam[14] = pos[3], lowerleft[3], wvec[3], hvec[3], image_w, image_h
  * (Camera::init, src/render/camera.h:128-166).  ooc::Tracer::genMultiEyes
@@ -214,6 +236,14 @@ int spray_rt_occluded_scene_devcount(spray_rt_ctx_t ctx, const spray_rt_ray* ray
 int spray_rt_eye_rays_ooc(spray_rt_ctx_t ctx, const float cam[14], int image_w,
                           int spp, int tx, int ty, int tw, int th,
                           spray_rt_ray* rays, int32_t* pixid, int32_t* samid);
+/* insitu::genMultiSampleEyeRays / genSingleSampleEyeRays
+ * (src/insitu/insitu_ray.h:103-182): the stripe (tx,ty,tw,th) of blocking
+ * tile (bx,by,bw,bh), jitter seeded by (pixid, sample); samid = the
+ * blocking-tile-local sample id.  All device pointers. */
+int spray_rt_eye_rays_insitu(spray_rt_ctx_t ctx, const float cam[14], int image_w,
+                             int spp, int bx, int by, int bw, int bh, int tx, int ty,
+                             int tw, int th, spray_rt_ray* rays, int32_t* pixid,
+                             int32_t* samid);
 /* Point-light shadow rays of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-171)
  * for every hit: compacted into out_rays/out_src (source ray index); the
  * number written goes to *d_count (device int, zeroed by the call).

@@ -958,6 +958,15 @@ int or_scene_set_domain(or_scene* s, int id, const float* v, size_t nv,
   return 0;
 }
 
+/* A domain of the partition that another rank owns: its box takes part in
+ * the domain lists (every rank builds the same lists), its mesh is absent. */
+int or_scene_set_box(or_scene* s, int id, const float box[6]) {
+  if (id < 0 || id >= s->ndom) return -1;
+  memcpy(s->d[id].box, box, 6 * sizeof(float));
+  memcpy(s->boxes + 6 * id, box, 6 * sizeof(float));
+  return 0;
+}
+
 /* TriMeshBuffer::updateIntersection, src/render/trimesh_buffer.cc:328-360:
  * color channels (uint) * float weights, summed w,u,v order, truncated;
  * Ns from unnormalised vertex normals. */

@@ -132,6 +132,7 @@ void or_scene_free(or_scene*);
 int or_scene_set_domain(or_scene*, int id, const float* v, size_t nv,
                         const uint32_t* f, size_t nf, const uint32_t* colors,
                         const float* normals, const float box[6]);
+int or_scene_set_box(or_scene* s, int id, const float box[6]);
 /* Closest hit over every domain the ray's sorted domain list holds
  * (ooc_isector.h:126-145 enqueues the ray to all of them; ooc_vbuf.cc:54-112
  * keeps the nearest), ties -> earlier list entry.  nthreads<=0: all. */

@@ -104,6 +104,7 @@ def _declare(L):
         "or_scene_create": (P, [C.c_int]),
         "or_scene_free": (None, [P]),
         "or_scene_set_domain": (C.c_int, [P, C.c_int, P, SZ, P, SZ, P, P, P]),
+        "or_scene_set_box": (C.c_int, [P, C.c_int, P]),
         "or_scene_intersect": (None, [P, P, P, SZ, P, P, C.c_int]),
         "or_scene_occluded": (None, [P, P, P, SZ, P, P, C.c_int]),
         "or_spawn_shadows_pt": (SZ, [P, P, P, SZ, P, P, P, C.c_float, P, P, P]),
@@ -480,6 +481,10 @@ class Scene:
                                       _p(u32(colors)), _p(f32(normals)), _p(f32(box)))
         assert r == 0
 
+    def set_box(self, i, box):
+        """A domain owned elsewhere: listed by the domain query, no mesh."""
+        assert lib().or_scene_set_box(self.h, i, _p(f32(box))) == 0
+
     def intersect(self, org, d, nthreads=0):
         n = len(org)
         hits = np.zeros(n, HIT_DTYPE)
@@ -497,12 +502,16 @@ class Scene:
         return o, c.as_dict()
 
 
-def load_scene(spray_path, ply_path=None):
-    """Parse a .spray file and build the whole-scene oracle."""
+def load_scene(spray_path, ply_path=None, only=None):
+    """Parse a .spray file and build the whole-scene oracle; ``only``: the
+    domain ids whose meshes are resident (the others keep just their box)."""
     domains, lights = parse_spray(spray_path, ply_path)
     sc = Scene(len(domains))
     cache = {}
     for d in domains:
+        if only is not None and d["id"] not in only:
+            sc.set_box(d["id"], d["world_bound"])
+            continue
         key = (d["file"], d["transform"].tobytes())
         if key not in cache:
             cache[key] = load_domain_mesh(d)

@@ -63,6 +63,10 @@ SIGNATURES = {
     "spray_rt_intersect_scene_spawn_pt": (I, [P, P, SZ, P, P, P, P, P]),
     "spray_rt_occluded_scene_masked": (I, [P, P, SZ, P, P]),
     "spray_rt_eye_rays_ooc": (I, [P, P, I, I, I, I, I, I, P, P, P]),
+    "spray_rt_eye_rays_insitu": (I, [P, P, I, I, I, I, I, I, I, I, I, I, P, P, P]),
+    "spray_rt_set_owners": (I, [P, P]),
+    "spray_rt_route": (I, [P, P, SZ, P]),
+    "spray_rt_intersect_scene_keyed": (I, [P, P, SZ, P, P]),
     "spray_rt_spawn_shadows_pt": (I, [P, P, P, SZ, P, P, P, P]),
     # spray_scene.h
     "spray_scene_create": (I, [C.c_char_p, C.c_char_p, I, I, P, C.c_char_p, SZ]),

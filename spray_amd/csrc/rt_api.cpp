@@ -52,6 +52,7 @@ struct spray_rt_ctx {
   float* d_boxes = nullptr;
   int* d_dom2slot = nullptr;
   DomTrav* d_domtrav = nullptr;  // per-domain traversal descriptors
+  int* d_owner = nullptr;        // in-situ domain -> rank map
   BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
   int ntlas = 0;
   int tlas_depth = 0;
@@ -273,7 +274,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
     if (s.ready) (void)hipEventDestroy(s.ready);
     if (s.pinned) (void)hipHostFree(s.pinned);
   }
-  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_domtrav, c->d_tlas, c->d_seg_slot,
+  void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_domtrav, c->d_owner, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
                   c->d_block_counts, c->d_heads, c->d_sel};
   for (void* b : bufs)
@@ -439,10 +440,12 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   if (c->d_boxes) HIPCHK(c, hipFree(c->d_boxes));
   if (c->d_dom2slot) HIPCHK(c, hipFree(c->d_dom2slot));
   if (c->d_domtrav) HIPCHK(c, hipFree(c->d_domtrav));
+  if (c->d_owner) HIPCHK(c, hipFree(c->d_owner));
   if (c->d_tlas) HIPCHK(c, hipFree(c->d_tlas));
   c->d_boxes = nullptr;
   c->d_dom2slot = nullptr;
   c->d_domtrav = nullptr;
+  c->d_owner = nullptr;
   c->d_tlas = nullptr;
   c->ntlas = 0;
   c->tlas_depth = 0;
@@ -686,6 +689,63 @@ int spray_rt_intersect_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
 int spray_rt_occluded_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
                             size_t M, uint8_t* occluded) {
   return spray_rt_occluded_scene_counted(c, rays, M, occluded, nullptr);
+}
+
+int spray_rt_set_owners(spray_rt_ctx_t c, const int* owner) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (c->ndom <= 0) return fail(c, SPRAY_RT_ERR_STATE, "no domain bounds set");
+  if (!owner) return fail(c, SPRAY_RT_ERR_ARG, "null owner map");
+  for (int d = 0; d < c->ndom; ++d)
+    if (owner[d] < -1 || owner[d] >= 64)
+      return fail(c, SPRAY_RT_ERR_ARG, "owner[%d] = %d out of [-1, 64)", d, owner[d]);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->d_owner)
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_owner), c->ndom * sizeof(int)));
+  hipStream_t s = stream_of(c);
+  HIPCHK(c, hipMemcpyAsync(c->d_owner, owner, c->ndom * sizeof(int), hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_route(spray_rt_ctx_t c, const spray_rt_ray* rays, size_t M,
+                   uint64_t* rank_mask) {
+  int r = scene_common(c, rays, M, rank_mask);
+  if (r) return r;
+  if (!c->d_owner) return fail(c, SPRAY_RT_ERR_STATE, "no owner map set");
+  if (M == 0) return SPRAY_RT_OK;
+  if (!is_device_ptr(rays) || !is_device_ptr(rank_mask))
+    return fail(c, SPRAY_RT_ERR_ARG, "route needs device buffers");
+  HIPCHK(c, launch_route(stream_of(c), view(c), c->d_owner, rays, M, rank_mask));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_intersect_scene_keyed(spray_rt_ctx_t c, const spray_rt_ray* rays, size_t M,
+                                   spray_rt_hit* hits, uint64_t* keys) {
+  int r = scene_common(c, rays, M, hits);
+  if (r) return r;
+  if (M == 0) return SPRAY_RT_OK;
+  if (!keys || !is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(keys))
+    return fail(c, SPRAY_RT_ERR_ARG, "keyed intersect needs device buffers");
+  HIPCHK(c, launch_scene_intersect_keyed(stream_of(c), view(c), rays, M, hits, keys));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_eye_rays_insitu(spray_rt_ctx_t c, const float cam[14], int image_w, int spp,
+                             int bx, int by, int bw, int bh, int tx, int ty, int tw, int th,
+                             spray_rt_ray* rays, int32_t* pixid, int32_t* samid) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (!cam || spp <= 0 || tw < 0 || th < 0 || bw <= 0 || bh <= 0)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad eye-ray arguments");
+  if (tw && th && (tx < bx || ty < by || tx + tw > bx + bw || ty + th > by + bh))
+    return fail(c, SPRAY_RT_ERR_ARG, "stripe outside its blocking tile");
+  if (size_t(tw) * th * spp == 0) return SPRAY_RT_OK;
+  if (!is_device_ptr(rays) || (pixid && !is_device_ptr(pixid)) ||
+      (samid && !is_device_ptr(samid)))
+    return fail(c, SPRAY_RT_ERR_ARG, "eye-ray buffers must be device memory");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, launch_eye_rays_insitu(stream_of(c), cam, image_w, spp, bx, by, bw, tx, ty, tw,
+                                   th, rays, pixid, samid));
+  return SPRAY_RT_OK;
 }
 
 int spray_rt_eye_rays_ooc(spray_rt_ctx_t c, const float cam[14], int image_w,

@@ -68,6 +68,21 @@ hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
                                      spray_rt_ray* out_rays, uint8_t* out_valid,
                                      uint32_t* d_count);
 
+// Closest hit + composite key per ray for in-situ compositing:
+// (t bits << 32) | (position in the ray's sorted domain list << 16) | domain,
+// 0x7FFF...F on a miss (non-resident domains are skipped but counted).
+hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
+                                        const spray_rt_ray* rays, size_t M,
+                                        spray_rt_hit* hits, uint64_t* keys);
+// out[i] = OR over the ray's domain list of (1 << owner[domain]); owner < 0:
+// unowned.  owner: device int[ndom], ranks < 64.
+hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,
+                        const spray_rt_ray* rays, size_t M, uint64_t* out);
+hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w,
+                                  int spp, int bx, int by, int bw, int tx, int ty,
+                                  int tw, int th, spray_rt_ray* rays, int32_t* pixid,
+                                  int32_t* samid);
+
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                int spp, int tx, int ty, int tw, int th,
                                spray_rt_ray* rays, int32_t* pixid,

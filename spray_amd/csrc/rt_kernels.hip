@@ -60,7 +60,7 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
 #endif
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 3 = ray in, 4 B out
-// (no domain tree), 4 = mask with the fast slab test, 1 = domain mask
+// (no domain tree), 1 = domain mask
 // only, 2 = mask + ordered domain selection, no BVH traversal.
 // Minimum resident waves per SIMD the register allocator must allow (the
 // second __launch_bounds__ operand); 1 = unconstrained.
@@ -526,7 +526,14 @@ struct SceneArgs {
   uint32_t* sh_count;    // optional total
   // indexed input: slot j traces ray idx[j] (e.g. a selected sparse subset)
   const uint32_t* idx;
+  // kEpiKeys: composite key per ray
+  uint64_t* keys;
 };
+
+// Closest-hit epilogue variants of the scene kernels.
+constexpr int kEpiNone = 0;   // hit records only
+constexpr int kEpiSpawn = 1;  // + fused PT shadow spawn (positional)
+constexpr int kEpiKeys = 2;   // + 64-bit composite key (t, list position, domain)
 
 // Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): one work
 // queue of the persistent launches; bands 8x .. 8x+7 (a contiguous eighth of
@@ -535,7 +542,53 @@ __device__ __host__ __forceinline__ size_t band_size(size_t M) {
   return (((M + kQueues - 1) / kQueues) + 63) / 64 * 64;
 }
 
-template <int W, bool ANY, bool COUNT, bool SPAWN>
+// Domain list of one ray as a bitmask: WbvhEmbree::intersect
+// (src/render/wbvh_embree.cc:126-148) over the top-level tree staged in LDS.
+// Every node test is the reference's intersectAabb (exact ops) on exact union
+// boxes, so the mask equals the brute-force list over all domain boxes.
+template <int W>
+__device__ __forceinline__ void tlas_mask(const float4* stl, int ntlas, int32_t* stk,
+                                          float4 o4, float4 d4, uint64_t* m) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  if (ntlas <= 0) return;
+  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const float4 a = stl[4 * cur], b = stl[4 * cur + 1], c = stl[4 * cur + 2],
+                 e = stl[4 * cur + 3];
+    const int32_t cl = __float_as_int(e.x), cr = __float_as_int(e.y);
+    float tm;
+    const bool hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
+    const bool hr = cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+    int32_t next = kNone;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int32_t ch = k == 0 ? cl : cr;
+      if (!(k == 0 ? hl : hr)) continue;
+      if (ch < 0) {
+        const int d = int(~uint32_t(ch) >> 2);
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (w == (d >> 6)) m[w] |= 1ull << (d & 63);
+      } else if (next == kNone) {
+        next = ch;
+      } else {
+        stk[sp * kBlock] = ch;
+        ++sp;
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = stk[sp * kBlock];
+    }
+    cur = next;
+  }
+}
+
+template <int W, bool ANY, bool COUNT, int EPI>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                           const float4* stl, const float* sbox,
                                           const float4* sdom, int32_t* stk,
@@ -554,48 +607,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
-    if (ntlas > 0 && SPRAY_DIAG_MODE != 3) {
-      const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-      int sp = 0;
-      int32_t cur = 0;
-      for (;;) {
-        const float4 a = stl[4 * cur], b = stl[4 * cur + 1], c = stl[4 * cur + 2],
-                     e = stl[4 * cur + 3];
-        const int32_t cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-        float tm;
-        bool hl, hr;
-        if (SPRAY_DIAG_MODE == 4) {  // diagnostic: fast slab instead of exact
-          hl = slab(r, a.x, a.y, a.z, a.w, b.x, b.y, 0.f, kInf, tm);
-          hr = cr != INT_MIN && slab(r, b.z, b.w, c.x, c.y, c.z, c.w, 0.f, kInf, tm);
-        } else {
-          hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
-          hr = cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
-        }
-        int32_t next = kNone;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int32_t ch = k == 0 ? cl : cr;
-          if (!(k == 0 ? hl : hr)) continue;
-          if (ch < 0) {
-            const int d = int(~uint32_t(ch) >> 2);
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-              if (w == (d >> 6)) m[w] |= 1ull << (d & 63);
-          } else if (next == kNone) {
-            next = ch;
-          } else {
-            stk[sp * kBlock] = ch;
-            ++sp;
-          }
-        }
-        if (next == kNone) {
-          if (sp == 0) break;
-          --sp;
-          next = stk[sp * kBlock];
-        }
-        cur = next;
-      }
-    }
+    if (SPRAY_DIAG_MODE != 3) tlas_mask<W>(stl, ntlas, stk, o4, d4, m);
     if (SPRAY_DIAG_MODE == 1 || SPRAY_DIAG_MODE >= 3) {  // diagnostic: mask only
       uint32_t pc = 0;
 #pragma unroll
@@ -610,6 +622,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     // the tie-break key at 0, and leaf at a sentinel tells whether it won.
     Best best{ANY ? 0.f : d4.w, 0xFFFFFFFFu, 0xFFFFFFFFu};
     int best_dom = -1;
+    uint32_t it = 0, best_it = 0;  // list positions (kEpiKeys only)
     bool occluded = false;
     for (;;) {
       float st = kInf;
@@ -643,6 +656,8 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
 #pragma unroll
       for (int w = 0; w < W; ++w)
         if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
+      const uint32_t pos_sb = it;
+      if (EPI == kEpiKeys) ++it;
       const float4 dt = sdom[sb];
       const char* nodes = reinterpret_cast<const char*>(
           (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
@@ -669,6 +684,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                  ntri);
         if (best.leaf != 0xFFFFFFFFu) {
           best_dom = sb;
+          if (EPI == kEpiKeys) best_it = pos_sb;
         } else {
           best.prim = keep_prim;
           best.leaf = keep_leaf;
@@ -701,7 +717,15 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
       hp[0] = h0;
       hp[1] = h1;
       hp[2] = h2;
-      if (SPAWN && best_dom >= 0) {
+      if (EPI == kEpiKeys) {
+        // in-situ compositing key: the order of the sequential domain walk
+        // (t, then the earlier entry of the sorted domain list), unique per
+        // domain; misses sort last
+        A.keys[i] = best_dom < 0 ? 0x7FFFFFFFFFFFFFFFull
+                                 : (uint64_t(__float_as_uint(best.t)) << 32) |
+                                       (uint64_t(best_it) << 16) | uint64_t(best_dom);
+      }
+      if (EPI == kEpiSpawn && best_dom >= 0) {
         spray_rt_hit h;
         h.t = h0.x;
         h.color = __float_as_uint(h1.w);
@@ -760,7 +784,7 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
 // slot tree and of the top-level tree (a node at depth k has at most k
 // pending siblings).  LDS = STK KiB + 4 KiB per 64 domains, so STK 16 lets 8
 // blocks (32 waves) share a CU where 24 allowed 5.
-template <int W, bool ANY, bool COUNT, bool SPAWN, int STK>
+template <int W, bool ANY, bool COUNT, int EPI, int STK>
 __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void k_scene(
     SceneArgs A) {
   __shared__ int32_t stack[STK * kBlock];
@@ -788,9 +812,9 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
     if (j < M)
-      scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, sbox, sdom, stk, nnode, ntri, nvisit,
+      scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, nnode, ntri, nvisit,
                                       flag, pos, wi);
-    if (SPAWN) store_shadow(A, j < M, flag, i, pos, wi);
+    if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     constexpr uint32_t kPerXcd = kQueues / 8;
@@ -818,9 +842,9 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
           const size_t i = (idx && j < end) ? idx[j] : j;
           flag = false;
           if (j < end)
-            scene_ray<W, ANY, COUNT, SPAWN>(A, i, stl, sbox, sdom, stk, nnode, ntri,
+            scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, nnode, ntri,
                                             nvisit, flag, pos, wi);
-          if (SPAWN) store_shadow(A, j < end, flag, i, pos, wi);
+          if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
       }
@@ -831,6 +855,40 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
     atomicAdd(&A.counters[1], (unsigned long long)ntri);
     atomicAdd(&A.counters[2], (unsigned long long)nvisit);
   }
+}
+
+// In-situ routing (insitu::Isector::intersect, src/insitu/insitu_isector.h:
+// 164-224, + InsituPartition::rank, src/render/data_partition.h:48-56): the
+// set of ranks owning a domain on the ray's list, as a bitmask.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tlas,
+                                                  int ntlas, const int* __restrict__ owner,
+                                                  int ndom, const spray_rt_ray* __restrict__ rays,
+                                                  size_t M, uint64_t* __restrict__ out) {
+  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ float4 stl[4 * 64 * W];
+  __shared__ int sown[64 * W];
+  for (int k = threadIdx.x; k < 4 * ntlas; k += kBlock) stl[k] = ld4(tlas, k);
+  for (int k = threadIdx.x; k < ndom; k += kBlock) sown[k] = owner[k];
+  __syncthreads();
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= M) return;
+  const float4* rp = reinterpret_cast<const float4*>(rays + i);
+  const float4 o4 = rp[0], d4 = rp[1];
+  uint64_t m[W];
+  tlas_mask<W>(stl, ntlas, stack + threadIdx.x, o4, d4, m);
+  uint64_t ranks = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t bits = m[w];
+    while (bits) {
+      const int j = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      const int o = sown[64 * w + j];
+      if (o >= 0) ranks |= 1ull << o;
+    }
+  }
+  out[i] = ranks;
 }
 
 // ---------------------------------------------------------------------------
@@ -895,6 +953,44 @@ __global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
   if (pixid) pixid[bufid] = y * image_w + x;
   if (samid) samid[bufid] = int32_t(bufid);
   (void)s;
+}
+
+// insitu::genMultiSampleEyeRays / genSingleSampleEyeRays (src/insitu/
+// insitu_ray.h:103-182): stripe (tx, ty, tw, th) of blocking tile
+// (bx, by, bw, bh); jitter seeded by (pixid, s); samid = blocking-tile-local
+// sample id (the VBuf index).
+__global__ __launch_bounds__(kBlock) void k_eye_rays_insitu(
+    Cam cam, int image_w, int spp, int bx, int by, int bw, int tx, int ty, int tw,
+    int th, spray_rt_ray* __restrict__ rays, int32_t* __restrict__ pixid,
+    int32_t* __restrict__ samid) {
+  const size_t bufid = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const size_t n = size_t(tw) * th * spp;
+  if (bufid >= n) return;
+  const int s = int(bufid % spp);
+  const int p = int(bufid / spp);
+  const int x = tx + p % tw, y = ty + p / tw;
+  const int pid = image_w * y + x;
+  float fx = float(x), fy = float(y);
+  if (spp > 1) {
+    uint32_t st = mm_fin(mm_mix(mm_mix(0u, uint32_t(pid)), uint32_t(s)));
+    fx = float(x) + sampler_1d(st);
+    fy = float(y) + sampler_1d(st);
+  }
+  const float* c = cam.p;
+  const float u = fx / c[12], v = fy / c[13];
+  float dx = ((c[3] + c[6] * u) + c[9] * v) - c[0];
+  float dy = ((c[4] + c[7] * u) + c[10] * v) - c[1];
+  float dz = ((c[5] + c[8] * u) + c[11] * v) - c[2];
+  const float inv = 1.0f / sqrtf((dx * dx + dy * dy) + dz * dz);
+  dx = dx * inv;
+  dy = dy * inv;
+  dz = dz * inv;
+  float4* rp = reinterpret_cast<float4*>(rays + bufid);
+  rp[0] = make_float4(c[0], c[1], c[2], kRayEpsilon);
+  rp[1] = make_float4(dx, dy, dz, kInf);
+  if (pixid) pixid[bufid] = pid;
+  if (samid)
+    samid[bufid] = spp > 1 ? (bw * (y - by) + (x - bx)) * spp + s : bw * (y - by) + (x - bx);
 }
 
 __device__ __forceinline__ uint32_t block_prefix(bool flag, uint32_t& total) {
@@ -1000,7 +1096,7 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
   return hipGetLastError();
 }
 
-template <int W, bool ANY, bool COUNT, bool SPAWN, int STK>
+template <int W, bool ANY, bool COUNT, int EPI, int STK>
 static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
@@ -1011,34 +1107,34 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
       e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, k_scene<W, ANY, COUNT, SPAWN, STK>, kBlock, 0);
+          &per_cu, k_scene<W, ANY, COUNT, EPI, STK>, kBlock, 0);
     if (e != hipSuccess) return e;
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
-  if (e == hipSuccess && SPAWN && a.sh_count)
+  if (e == hipSuccess && EPI == kEpiSpawn && a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
-  k_scene<W, ANY, COUNT, SPAWN, STK><<<g, kBlock, 0, s>>>(a);
+  k_scene<W, ANY, COUNT, EPI, STK><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
-template <int W, bool ANY, bool SPAWN, int STK>
+template <int W, bool ANY, int EPI, int STK>
 static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a) {
-  return a.counters ? launch_scene_t<W, ANY, true, SPAWN, STK>(s, a)
-                    : launch_scene_t<W, ANY, false, SPAWN, STK>(s, a);
+  return a.counters ? launch_scene_t<W, ANY, true, EPI, STK>(s, a)
+                    : launch_scene_t<W, ANY, false, EPI, STK>(s, a);
 }
 
-template <bool ANY, bool SPAWN>
+template <bool ANY, int EPI>
 static hipError_t launch_scene_w(hipStream_t s, const SceneArgs& a, int max_depth) {
   if (max_depth > kStack) return hipErrorInvalidValue;
   if (a.ndom <= 64)
-    return max_depth <= 16 ? launch_scene_c<1, ANY, SPAWN, 16>(s, a)
-                           : launch_scene_c<1, ANY, SPAWN, kStack>(s, a);
-  return max_depth <= 16 ? launch_scene_c<4, ANY, SPAWN, 16>(s, a)
-                         : launch_scene_c<4, ANY, SPAWN, kStack>(s, a);
+    return max_depth <= 16 ? launch_scene_c<1, ANY, EPI, 16>(s, a)
+                           : launch_scene_c<1, ANY, EPI, kStack>(s, a);
+  return max_depth <= 16 ? launch_scene_c<4, ANY, EPI, 16>(s, a)
+                         : launch_scene_c<4, ANY, EPI, kStack>(s, a);
 }
 
 static SceneArgs scene_args(const SceneView& v, const spray_rt_ray* rays, size_t M) {
@@ -1063,7 +1159,7 @@ hipError_t launch_scene_intersect(hipStream_t s, const SceneView& v,
   SceneArgs a = scene_args(v, rays, M);
   a.hits = hits;
   a.counters = counters;
-  return launch_scene_w<false, false>(s, a, v.max_depth);
+  return launch_scene_w<false, kEpiNone>(s, a, v.max_depth);
 }
 
 hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
@@ -1075,7 +1171,7 @@ hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
   a.d_count = d_count;
   a.occ = occluded;
   a.counters = counters;
-  return launch_scene_w<true, false>(s, a, v.max_depth);
+  return launch_scene_w<true, kEpiNone>(s, a, v.max_depth);
 }
 
 hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
@@ -1097,7 +1193,7 @@ hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
   a.d_count = d_num;
   a.occ = occluded;
   a.counters = counters;
-  return launch_scene_w<true, false>(s, a, v.max_depth);
+  return launch_scene_w<true, kEpiNone>(s, a, v.max_depth);
 }
 
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
@@ -1117,7 +1213,40 @@ hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
   a.sh_out = out_rays;
   a.sh_valid = out_valid;
   a.sh_count = d_count;
-  return launch_scene_w<false, true>(s, a, v.max_depth);
+  return launch_scene_w<false, kEpiSpawn>(s, a, v.max_depth);
+}
+
+hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
+                                        const spray_rt_ray* rays, size_t M,
+                                        spray_rt_hit* hits, uint64_t* keys) {
+  if (M == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.hits = hits;
+  a.keys = keys;
+  return launch_scene_w<false, kEpiKeys>(s, a, v.max_depth);
+}
+
+hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,
+                        const spray_rt_ray* rays, size_t M, uint64_t* out) {
+  if (M == 0) return hipSuccess;
+  if (v.ndom <= 64)
+    k_route<1><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, M, out);
+  else
+    k_route<4><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, M, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w,
+                                  int spp, int bx, int by, int bw, int tx, int ty,
+                                  int tw, int th, spray_rt_ray* rays, int32_t* pixid,
+                                  int32_t* samid) {
+  const size_t n = size_t(tw) * th * spp;
+  if (n == 0) return hipSuccess;
+  Cam c;
+  for (int k = 0; k < 14; ++k) c.p[k] = cam14[k];
+  k_eye_rays_insitu<<<grid_for(n), kBlock, 0, s>>>(c, image_w, spp, bx, by, bw, tx, ty,
+                                                   tw, th, rays, pixid, samid);
+  return hipGetLastError();
 }
 
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,

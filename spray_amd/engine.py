@@ -15,7 +15,8 @@ import numpy as np
 from ._native import (HIT_DTYPE, INVALID_ID, RAY_DTYPE, RTC_ISECT_DTYPE,
                       SprayRtError, lib)
 
-__all__ = ["RtContext", "Scene", "camera_init", "make_rays", "RAY_DTYPE",
+__all__ = ["RtContext", "Scene", "camera_init", "make_rays", "host_parse_scene",
+           "host_domain_mesh", "RAY_DTYPE",
            "HIT_DTYPE", "RTC_ISECT_DTYPE", "INVALID_ID", "SprayRtError"]
 
 
@@ -62,6 +63,43 @@ def make_rays(org, dir, tnear=0.001, tfar=np.inf):
     r["tnear"] = tnear
     r["tfar"] = tfar
     return r
+
+
+def host_parse_scene(desc, ply_path=""):
+    """Scene file -> (boxes [n,6], lights [nl,7]) without touching the GPU
+    (spray_host_parse_scene)."""
+    nd, nl = C.c_int(), C.c_int()
+    err = C.create_string_buffer(1024)
+    if lib().spray_host_parse_scene(desc.encode(), (ply_path or "").encode(), C.byref(nd),
+                                    C.byref(nl), None, None, None, err, 1024) != 0:
+        raise SprayRtError("parse %s: %s" % (desc, err.value.decode()))
+    boxes = np.zeros((nd.value, 6), np.float32)
+    xf = np.zeros((nd.value, 16), np.float32)
+    lights = np.zeros((nl.value, 7), np.float32)
+    if lib().spray_host_parse_scene(desc.encode(), (ply_path or "").encode(), C.byref(nd),
+                                    C.byref(nl), boxes.ctypes.data, xf.ctypes.data,
+                                    lights.ctypes.data, err, 1024) != 0:
+        raise SprayRtError("parse %s: %s" % (desc, err.value.decode()))
+    return boxes, lights
+
+
+def host_domain_mesh(desc, ply_path, domain_id):
+    """TriMeshBuffer::load of one domain on the host -> (verts, faces,
+    colors, normals)."""
+    nv, nf = C.c_size_t(), C.c_size_t()
+    L = lib()
+    if L.spray_host_domain_mesh(desc.encode(), (ply_path or "").encode(), int(domain_id),
+                                C.byref(nv), C.byref(nf), None, None, None, None) != 0:
+        raise SprayRtError("domain %d of %s failed to load" % (domain_id, desc))
+    v = np.zeros((nv.value, 3), np.float32)
+    f = np.zeros((nf.value, 3), np.uint32)
+    c = np.zeros(nv.value, np.uint32)
+    n = np.zeros((nv.value, 3), np.float32)
+    if L.spray_host_domain_mesh(desc.encode(), (ply_path or "").encode(), int(domain_id),
+                                C.byref(nv), C.byref(nf), v.ctypes.data, f.ctypes.data,
+                                c.ctypes.data, n.ctypes.data) != 0:
+        raise SprayRtError("domain %d of %s failed to load" % (domain_id, desc))
+    return v, f, c, n
 
 
 class RtContext:
@@ -228,6 +266,41 @@ class RtContext:
         e, k4 = _addr(counters)
         self._check(lib().spray_rt_occluded_scene_devcount(self.h, a, int(max_rays), b, c, e),
                     "occluded_scene_devcount")
+
+    # ---- in-situ (domain-sharded) ----
+    def set_owners(self, owner):
+        """Domain -> rank map (InsituPartition::rank), host int array."""
+        o = np.ascontiguousarray(owner, np.int32)
+        self._check(lib().spray_rt_set_owners(self.h, o.ctypes.data), "set_owners")
+
+    def route(self, rays, rank_mask):
+        """rank_mask[i] (uint64 / int64 device tensor) = ranks owning a domain
+        on ray i's list."""
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        b, k2 = _addr(rank_mask)
+        self._check(lib().spray_rt_route(self.h, a, n, b), "route")
+
+    def intersect_scene_keyed(self, rays, hits, keys):
+        """Closest hit over the resident domains + composite key (device)."""
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        c, k3 = _addr(keys)
+        self._check(lib().spray_rt_intersect_scene_keyed(self.h, a, n, b, c),
+                    "intersect_scene_keyed")
+
+    def eye_rays_insitu(self, cam, image_w, spp, block, stripe, rays, pixid=None,
+                        samid=None):
+        cam = np.ascontiguousarray(cam, np.float32)
+        bx, by, bw, bh = block
+        tx, ty, tw, th = stripe
+        a, k1 = _addr(rays)
+        b, k2 = _addr(pixid)
+        c, k3 = _addr(samid)
+        self._check(lib().spray_rt_eye_rays_insitu(self.h, cam.ctypes.data, int(image_w),
+                                                   int(spp), bx, by, bw, bh, tx, ty, tw, th,
+                                                   a, b, c), "eye_rays_insitu")
 
     # ---- device ray sources ----
     def eye_rays_ooc(self, cam, image_w, spp, tile, rays, pixid=None, samid=None):

@@ -1,0 +1,302 @@
+"""In-situ (domain-sharded) tracing across ranks, one rank per GPU.
+
+The reference's in-situ mode (src/insitu/) keeps every domain resident on
+exactly one MPI rank and moves rays to the data:
+
+* ``InsituPartition::partition`` (src/render/data_partition.h:59-137): domain
+  centroids Morton-coded, sorted, dealt out in contiguous shares;
+* ``TileList`` / ``makeHorizontalStripe`` (src/render/tile.cc:159-212): each
+  rank generates the eye rays of one horizontal stripe of every blocking
+  tile;
+* ``Isector::intersect`` (src/insitu/insitu_isector.h:164-224): every ray is
+  queued, speculatively, to every domain on its sorted domain list, and the
+  queues of remote domains travel to their owners (insitu_comm.inl:28-101,
+  MPI Isend/Iprobe/Recv);
+* ``VBuf::compositeTbuf`` / ``compositeObuf`` (src/insitu/insitu_vbuf.h:
+  74-152): the per-sample nearest t is reduced with MPI_Allreduce(MIN), and
+  only the rank whose local hit equals it shades the sample and spawns its
+  shadow ray; occlusion bits are reduced with MPI_Allreduce(MAX).
+
+Here the queues become bulk exchanges over RCCL (torch.distributed "nccl"):
+a count all-to-all, then one all-to-all of 32-B rays + 4-B sample ids per
+bounce.  The tbuf is a 64-bit composite key (t, position in the ray's sorted
+domain list, domain), reduced with MIN: the winner is then unique and equal
+to the sequential walk of the whole list (spray_rt_intersect_scene_keyed),
+where the reference leaves exact t ties to MPI's reduction order.
+
+The protocol runs on torch tensors; the local work (routing, keyed closest
+hit, shadow spawn, any hit) is a pluggable ``local`` object -- on a GPU the
+HIP engine (:class:`GpuLocal`).  Collectives with the "gloo" backend stage
+device tensors through host memory (tests; the product runs "nccl").
+"""
+from __future__ import annotations
+
+import numpy as np
+
+__all__ = ["morton_code", "morton_partition", "horizontal_stripe", "Comm", "GpuLocal",
+           "InsituTracer", "MISS_KEY", "setup_rank_context"]
+
+MISS_KEY = 0x7FFFFFFFFFFFFFFF
+
+
+# ---------------------------------------------------------------------------
+# partition and stripes
+# ---------------------------------------------------------------------------
+def _expand_bits(v):
+    """Morton::expandBits (src/render/morton.h:44-50), uint32 arithmetic."""
+    v = np.uint32(v)
+    with np.errstate(over="ignore"):
+        v = (v * np.uint32(0x00010001)) & np.uint32(0xFF0000FF)
+        v = (v * np.uint32(0x00000101)) & np.uint32(0x0F00F00F)
+        v = (v * np.uint32(0x00000011)) & np.uint32(0xC30C30C3)
+        v = (v * np.uint32(0x00000005)) & np.uint32(0x49249249)
+    return v
+
+
+def morton_code(x, y, z):
+    """Morton::compute (src/render/morton.h:32-41): 30-bit code of a point in
+    the unit cube, float32 clamping as the reference."""
+    f = np.float32
+    c = []
+    for a in (x, y, z):
+        a = f(min(max(f(a) * f(1024.0), f(0.0)), f(1023.0)))
+        c.append(_expand_bits(int(a)))
+    with np.errstate(over="ignore"):
+        return int((c[0] * np.uint32(4) + c[1] * np.uint32(2) + c[2]) & np.uint32(0xFFFFFFFF))
+
+
+def morton_partition(boxes, scene_bound, nranks):
+    """InsituPartition::partition with GROUP_CLOSE_DOMAINS
+    (src/render/data_partition.h:59-137) -> owner rank per domain.
+
+    boxes [n, 6] (lo, hi) world bounds in domain-id order, scene_bound [6].
+    Codes are sorted by (code, domain id): std::sort leaves equal codes in an
+    unspecified order, the domain id makes the map deterministic.  As in the
+    reference, shares = n // nranks (0 when n < nranks: every domain then
+    stays on rank 0) and the rank counter wraps."""
+    f = np.float32
+    boxes = np.asarray(boxes, f).reshape(-1, 6)
+    sb = np.asarray(scene_bound, f).reshape(6)
+    n = len(boxes)
+    if nranks <= 0:
+        raise ValueError("nranks must be > 0")
+    diag = sb[3:] - sb[:3]
+    scale = (f(1.0) / diag).astype(f)
+    mn = (sb[:3] * scale).astype(f)
+    off = (f(0.0) - mn).astype(f)
+    codes = []
+    for i in range(n):
+        center = ((boxes[i, :3] + boxes[i, 3:]) * f(0.5)).astype(f)  # Aabb::getCenter
+        c = (center * scale + off).astype(f)
+        codes.append((morton_code(c[0], c[1], c[2]), i))
+    codes.sort()
+    owner = np.zeros(n, np.int32)
+    shares = n // nranks
+    rank, s = 0, 0
+    for _, dom in codes:
+        owner[dom] = rank
+        s += 1
+        if s == shares:
+            s = 0
+            rank += 1
+            if rank == nranks:
+                rank = 0
+    return owner
+
+
+def horizontal_stripe(nranks, rank, tile):
+    """makeHorizontalStripe (src/render/tile.cc:187-209): tile = (x, y, w, h)
+    -> this rank's stripe (x, y, w, h); w = h = 0 when empty."""
+    x, y, w, h = tile
+    hh = max(h // nranks, 1)
+    oy = y + rank * hh
+    yend = y + h
+    if oy >= yend:
+        return (0, oy, 0, 0)
+    oh = yend - oy if (oy + hh > yend or rank == nranks - 1) else hh
+    return (x, oy, w, oh)
+
+
+# ---------------------------------------------------------------------------
+# collectives
+# ---------------------------------------------------------------------------
+class Comm:
+    """The rank group.  world == 1 makes every collective a no-op; "gloo"
+    stages device tensors through host memory."""
+
+    def __init__(self, dist=None, group=None):
+        self.dist = dist
+        self.group = group
+        if dist is not None and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+            self.staged = dist.get_backend(group) == "gloo"
+        else:
+            self.rank, self.world, self.staged = 0, 1, False
+
+    def _host(self, t):
+        return t.cpu() if (self.staged and t.is_cuda) else t
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        if self.world == 1:
+            out.copy_(inp)
+            return out
+        o, i = self._host(out), self._host(inp)
+        self.dist.all_to_all_single(o, i, out_splits, in_splits, group=self.group)
+        if o is not out:
+            out.copy_(o)
+        return out
+
+    def all_reduce(self, t, op):
+        if self.world == 1:
+            return t
+        h = self._host(t)
+        self.dist.all_reduce(h, op=op, group=self.group)
+        if h is not t:
+            t.copy_(h)
+        return t
+
+    def op(self, name):
+        return getattr(self.dist.ReduceOp, name) if self.dist is not None else None
+
+
+# ---------------------------------------------------------------------------
+# local work on one GPU
+# ---------------------------------------------------------------------------
+class GpuLocal:
+    """Local work of one rank through the HIP engine (device tensors).
+    Rays are float32 [n, 8] (org, tnear, dir, tfar), hits float32 [n, 12]
+    (spray_rt_hit), keys / rank masks int64 [n]."""
+
+    def __init__(self, rt, device, stream=None):
+        import torch
+        self.torch = torch
+        self.rt = rt
+        self.device = device
+        # the engine enqueues on torch's stream: the protocol's torch ops and
+        # the kernels stay ordered without host synchronisation
+        rt.set_stream(stream if stream is not None else torch.cuda.current_stream(device))
+
+    def route(self, rays):
+        m = self.torch.empty(rays.shape[0], dtype=self.torch.int64, device=self.device)
+        if rays.shape[0]:
+            self.rt.route(rays, m)
+        return m
+
+    def intersect_keyed(self, rays):
+        n = rays.shape[0]
+        hits = self.torch.empty((n, 12), dtype=self.torch.float32, device=self.device)
+        keys = self.torch.empty(n, dtype=self.torch.int64, device=self.device)
+        if n:
+            self.rt.intersect_scene_keyed(rays, hits, keys)
+        return hits, keys
+
+    def spawn_pt(self, rays, hits, shade):
+        t = self.torch
+        n = rays.shape[0]
+        out = t.empty((max(n, 1), 8), dtype=t.float32, device=self.device)
+        src = t.empty(max(n, 1), dtype=t.int32, device=self.device)
+        cnt = t.zeros(1, dtype=t.int32, device=self.device)
+        if n:
+            self.rt.spawn_shadows_pt(rays, hits, n, shade, out, src, cnt)
+        k = int(cnt.item()) if n else 0
+        return out[:k], src[:k].long()
+
+    def occluded(self, rays):
+        t = self.torch
+        occ = t.zeros(rays.shape[0], dtype=t.uint8, device=self.device)
+        if rays.shape[0]:
+            self.rt.occluded_scene(rays, occ)
+        return occ
+
+
+def setup_rank_context(rt, desc, ply_path, owner, rank):
+    """Loads the domains ``owner`` assigns to ``rank`` into slots 0..k-1 of
+    the engine context and installs the full domain box set and owner map
+    (every rank computes the same domain lists)."""
+    from .engine import host_domain_mesh, host_parse_scene
+    boxes, _ = host_parse_scene(desc, ply_path)
+    rt.domain_bounds(boxes)
+    mine = [d for d in range(len(boxes)) if owner[d] == rank]
+    for slot, d in enumerate(mine):
+        v, f, c, n = host_domain_mesh(desc, ply_path, d)
+        rt.upload_domain(slot, v, f, c, n)
+        rt.map_domain(d, slot)
+    rt.set_owners(owner)
+    return mine
+
+
+# ---------------------------------------------------------------------------
+# the per-tile protocol
+# ---------------------------------------------------------------------------
+class InsituTracer:
+    """One bounce (primary closest hit + point-light shadow rays) of a
+    blocking tile, distributed by domain ownership."""
+
+    def __init__(self, local, comm):
+        import torch
+        self.torch = torch
+        self.local = local
+        self.comm = comm
+
+    def exchange(self, mask, payloads):
+        """Sends row i of every payload to each rank whose bit is set in
+        mask[i] (speculative queues, insitu_comm.inl:28-101): returns the
+        received payloads, grouped by source rank in the sender's order."""
+        t = self.torch
+        W = self.comm.world
+        n = mask.shape[0]
+        if n:
+            bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
+            sel = ((mask.unsqueeze(0) >> bit) & 1).bool()  # [W, n], dest-major
+            dest, idx = sel.nonzero(as_tuple=True)
+        else:
+            dest = t.zeros(0, dtype=t.int64, device=mask.device)
+            idx = dest
+        send = t.bincount(dest, minlength=W).to(t.int64)
+        recv = t.empty_like(send)
+        self.comm.all_to_all(recv, send, None, None)
+        sc, rc = send.tolist(), recv.tolist()
+        outs = []
+        for p in payloads:
+            s = p.index_select(0, idx)
+            r = p.new_empty((sum(rc),) + tuple(p.shape[1:]))
+            self.comm.all_to_all(r, s, rc, sc)
+            outs.append(r)
+        return outs
+
+    def trace_tile(self, rays, samid, nsamples, shade):
+        """rays float32 [n, 8] of this rank's stripe, samid int32/int64 [n]
+        (blocking-tile sample ids < nsamples).
+
+        Returns a dict: ``samid`` / ``hits`` of the samples whose nearest hit
+        lies in this rank's domains, ``shadow_samid`` of the shadow rays
+        this rank spawned, ``obuf`` (uint8 [nsamples], global occlusion) and
+        ``n_shadow`` (shadow rays spawned on all ranks)."""
+        t = self.torch
+        L, C = self.local, self.comm
+        samid = samid.to(t.int64)
+        # primary: route, exchange, local closest hit with composite keys
+        rrays, rsam = self.exchange(L.route(rays), [rays, samid])
+        hits, keys = L.intersect_keyed(rrays)
+        tbuf = t.full((nsamples,), MISS_KEY, dtype=t.int64, device=keys.device)
+        if keys.numel():
+            tbuf.scatter_reduce_(0, rsam, keys, "amin")
+        C.all_reduce(tbuf, C.op("MIN"))
+        win = (keys == tbuf.index_select(0, rsam)) & (keys != MISS_KEY)
+        # only the winner shades: the others' hits are masked as misses
+        hw = hits.clone()
+        hw.view(t.int32)[:, 11].masked_fill_(~win, -1)  # spray_rt_hit.domain
+        srays, src = L.spawn_pt(rrays, hw, shade)
+        ssam = rsam.index_select(0, src)
+        # shadow rays: route, exchange, local any hit, OR over ranks
+        rs, rssam = self.exchange(L.route(srays), [srays, ssam])
+        occ = L.occluded(rs)
+        obuf = t.zeros(nsamples, dtype=t.uint8, device=occ.device)
+        if occ.numel():
+            obuf.scatter_reduce_(0, rssam, occ, "amax")
+        C.all_reduce(obuf, C.op("MAX"))
+        nsh = t.tensor([srays.shape[0]], dtype=t.int64, device=occ.device)
+        C.all_reduce(nsh, C.op("SUM"))
+        return {"samid": rsam[win], "hits": hits[win], "shadow_samid": ssam,
+                "obuf": obuf, "n_shadow": int(nsh.item())}
