@@ -15,6 +15,11 @@ sampler (ooc::Tracer::genMultiEyes over its 8 blocking tiles of 1024x128).
 Multi-GPU (torchrun, one process per GPU): every rank traces its own frame
 (frame replicas, weak scaling); barrier + max over ranks around the K timed
 steps.  Rank 0 prints one JSON line.
+
+With more than one rank (or --insitu 1) the line also carries "insitu":
+configs[2], the same frame traced with the domains sharded 64/N per GPU
+(Morton partition) and the rays moving to their domains' owners over RCCL
+all-to-all (spray_amd/insitu.py) -- strong scaling of one frame.
 """
 from __future__ import annotations
 
@@ -85,6 +90,58 @@ def cpu_baseline(target_s=10.0):
                       "%.1f s traversal+spawn" % (reps, n, threads, dt)}
 
 
+def run_insitu(args, dist, world, rank, local, cam):
+    """configs[2]: one frame, domains sharded by the reference's Morton
+    partition, eye rays of this rank's horizontal stripe (one blocking tile =
+    the frame), rays exchanged to their domains' owners; timed like the main
+    measurement (barrier + max over ranks)."""
+    import torch
+    import spray_amd
+    from spray_amd import insitu
+    from spray_amd.engine import host_parse_scene
+    dev = torch.device("cuda", local)
+    boxes, _ = host_parse_scene(SCENE, SCENES)
+    bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
+    owner = insitu.morton_partition(boxes, bound, world)
+    rt = spray_amd.RtContext(local)
+    insitu.setup_rank_context(rt, SCENE, SCENES, owner, rank)
+    comm = insitu.Comm(dist if world > 1 else None)
+    tr = insitu.InsituTracer(insitu.GpuLocal(rt, dev), comm)
+    stripe = insitu.horizontal_stripe(world, rank, (0, 0, W, H))
+    n = stripe[2] * stripe[3] * SPP
+    rays = torch.empty((n, 8), dtype=torch.float32, device=dev)
+    sam = torch.empty(n, dtype=torch.int32, device=dev)
+    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, None, sam)
+    torch.cuda.synchronize()
+    res = None
+    for _ in range(args.warmup):
+        res = tr.trace_tile(rays, sam, SHADE)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = tr.trace_tile(rays, sam, SHADE)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    rays_step = res["n_rays"] + res["n_shadow"]
+    rt.close()
+    return {"value": round(rays_step * args.steps / el / 1e6, 3), "unit": "Mrays/s",
+            "ms_per_step": round(el / args.steps * 1e3, 4), "scaling": "strong",
+            "rays_per_step": rays_step, "primary_rays": res["n_rays"],
+            "shadow_rays": res["n_shadow"],
+            "config": "configs[2]: 64 domains, %d per GPU (Morton partition), 1024x1024x8spp "
+                      "frame in %d horizontal stripes, speculative ray exchange over "
+                      "RCCL all-to-all" % (int(np.bincount(owner, minlength=world)[rank]),
+                                            world)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +150,8 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--insitu", type=int, default=-1,
+                    help="also measure configs[2] (default: when more than one rank)")
     args = ap.parse_args()
 
     import torch
@@ -221,6 +280,8 @@ def main():
                        "occluded_achieved_GBs": round(ah_gbs, 1)},
         "canonical_counts": gpu_counts,
     }
+    if args.insitu == 1 or (args.insitu < 0 and world > 1):
+        out["insitu"] = run_insitu(args, dist, world, rank, local, cam)
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

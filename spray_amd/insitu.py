@@ -124,7 +124,7 @@ class Comm:
     """The rank group.  world == 1 makes every collective a no-op; "gloo"
     stages device tensors through host memory."""
 
-    def __init__(self, dist=None, group=None):
+    def __init__(self, dist=None, group=None, always=False):
         self.dist = dist
         self.group = group
         if dist is not None and dist.is_initialized():
@@ -133,12 +133,14 @@ class Comm:
             self.staged = dist.get_backend(group) == "gloo"
         else:
             self.rank, self.world, self.staged = 0, 1, False
+        # always: issue the collectives even for one rank (exercises RCCL)
+        self.skip = self.world == 1 and not (always and dist is not None)
 
     def _host(self, t):
         return t.cpu() if (self.staged and t.is_cuda) else t
 
     def all_to_all(self, out, inp, out_splits, in_splits):
-        if self.world == 1:
+        if self.skip:
             out.copy_(inp)
             return out
         o, i = self._host(out), self._host(inp)
@@ -148,7 +150,7 @@ class Comm:
         return out
 
     def all_reduce(self, t, op):
-        if self.world == 1:
+        if self.skip:
             return t
         h = self._host(t)
         self.dist.all_reduce(h, op=op, group=self.group)
@@ -229,9 +231,58 @@ def setup_rank_context(rt, desc, ply_path, owner, rank):
 # ---------------------------------------------------------------------------
 # the per-tile protocol
 # ---------------------------------------------------------------------------
+class Exchange:
+    """One routed exchange: row i of a ray batch goes to every rank whose bit
+    is set in mask[i].  ``forward`` moves per-ray payloads to the owners
+    (grouped by source rank, in the sender's order); ``backward`` returns
+    per-copy results to the sender, in the order the copies were sent."""
+
+    def __init__(self, comm, mask):
+        import torch as t
+        W = comm.world
+        self.comm = comm
+        n = mask.shape[0]
+        if n:
+            bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
+            sel = ((mask.unsqueeze(0) >> bit) & 1).bool()  # [W, n], dest-major
+            dest, self.idx = sel.nonzero(as_tuple=True)
+        else:
+            dest = t.zeros(0, dtype=t.int64, device=mask.device)
+            self.idx = dest
+        send = t.bincount(dest, minlength=W).to(t.int64)
+        recv = t.empty_like(send)
+        comm.all_to_all(recv, send, None, None)  # the count phase
+        self.sc, self.rc = send.tolist(), recv.tolist()
+        self.n_sent, self.n_recv = sum(self.sc), sum(self.rc)
+
+    def forward(self, payload):
+        """payload: per-ray rows [n, ...] of the sender's batch."""
+        s = payload.index_select(0, self.idx)
+        if self.comm.skip:
+            return s
+        r = payload.new_empty((self.n_recv,) + tuple(payload.shape[1:]))
+        return self.comm.all_to_all(r, s, self.rc, self.sc)
+
+    def backward(self, result):
+        """result: per received copy [n_recv, ...] -> per sent copy."""
+        if self.comm.skip:
+            return result
+        r = result.new_empty((self.n_sent,) + tuple(result.shape[1:]))
+        return self.comm.all_to_all(r, result.contiguous(), self.sc, self.rc)
+
+
 class InsituTracer:
     """One bounce (primary closest hit + point-light shadow rays) of a
-    blocking tile, distributed by domain ownership."""
+    blocking tile, distributed by domain ownership.
+
+    Compositing happens per ray copy instead of over a whole-tile buffer:
+    the owners' keys travel back to the ray's sender (reverse all-to-all),
+    the sender's minimum travels out again, and the one owner whose key
+    equals it shades the sample and spawns its shadow ray; the shadow ray's
+    occlusion bits come back to that rank and are OR-ed there.  This is the
+    tbuf MIN / obuf MAX compositing of VBuf (insitu_vbuf.h:74-152) at the
+    cost of 8 B (keys) and 1 B (occlusion) per remote copy, instead of
+    all-reduces over every sample of the tile."""
 
     def __init__(self, local, comm):
         import torch
@@ -239,64 +290,39 @@ class InsituTracer:
         self.local = local
         self.comm = comm
 
-    def exchange(self, mask, payloads):
-        """Sends row i of every payload to each rank whose bit is set in
-        mask[i] (speculative queues, insitu_comm.inl:28-101): returns the
-        received payloads, grouped by source rank in the sender's order."""
-        t = self.torch
-        W = self.comm.world
-        n = mask.shape[0]
-        if n:
-            bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
-            sel = ((mask.unsqueeze(0) >> bit) & 1).bool()  # [W, n], dest-major
-            dest, idx = sel.nonzero(as_tuple=True)
-        else:
-            dest = t.zeros(0, dtype=t.int64, device=mask.device)
-            idx = dest
-        send = t.bincount(dest, minlength=W).to(t.int64)
-        recv = t.empty_like(send)
-        self.comm.all_to_all(recv, send, None, None)
-        sc, rc = send.tolist(), recv.tolist()
-        outs = []
-        for p in payloads:
-            s = p.index_select(0, idx)
-            r = p.new_empty((sum(rc),) + tuple(p.shape[1:]))
-            self.comm.all_to_all(r, s, rc, sc)
-            outs.append(r)
-        return outs
-
-    def trace_tile(self, rays, samid, nsamples, shade):
-        """rays float32 [n, 8] of this rank's stripe, samid int32/int64 [n]
-        (blocking-tile sample ids < nsamples).
+    def trace_tile(self, rays, samid, shade):
+        """rays float32 [n, 8] of this rank's stripe, samid [n] (blocking-
+        tile sample ids).
 
         Returns a dict: ``samid`` / ``hits`` of the samples whose nearest hit
-        lies in this rank's domains, ``shadow_samid`` of the shadow rays
-        this rank spawned, ``obuf`` (uint8 [nsamples], global occlusion) and
-        ``n_shadow`` (shadow rays spawned on all ranks)."""
+        lies in this rank's domains (this rank shades them), ``shadow_samid``
+        / ``shadow_occ`` of the shadow rays it spawned, and the job totals
+        ``n_rays`` and ``n_shadow``."""
         t = self.torch
         L, C = self.local, self.comm
         samid = samid.to(t.int64)
-        # primary: route, exchange, local closest hit with composite keys
-        rrays, rsam = self.exchange(L.route(rays), [rays, samid])
+        n = rays.shape[0]
+        # primary rays to the owners of their domains, keyed closest hit there
+        ex = Exchange(C, L.route(rays))
+        rrays, rsam = ex.forward(rays), ex.forward(samid)
         hits, keys = L.intersect_keyed(rrays)
-        tbuf = t.full((nsamples,), MISS_KEY, dtype=t.int64, device=keys.device)
-        if keys.numel():
-            tbuf.scatter_reduce_(0, rsam, keys, "amin")
-        C.all_reduce(tbuf, C.op("MIN"))
-        win = (keys == tbuf.index_select(0, rsam)) & (keys != MISS_KEY)
-        # only the winner shades: the others' hits are masked as misses
-        hw = hits.clone()
-        hw.view(t.int32)[:, 11].masked_fill_(~win, -1)  # spray_rt_hit.domain
-        srays, src = L.spawn_pt(rrays, hw, shade)
-        ssam = rsam.index_select(0, src)
-        # shadow rays: route, exchange, local any hit, OR over ranks
-        rs, rssam = self.exchange(L.route(srays), [srays, ssam])
-        occ = L.occluded(rs)
-        obuf = t.zeros(nsamples, dtype=t.uint8, device=occ.device)
-        if occ.numel():
-            obuf.scatter_reduce_(0, rssam, occ, "amax")
-        C.all_reduce(obuf, C.op("MAX"))
-        nsh = t.tensor([srays.shape[0]], dtype=t.int64, device=occ.device)
-        C.all_reduce(nsh, C.op("SUM"))
-        return {"samid": rsam[win], "hits": hits[win], "shadow_samid": ssam,
-                "obuf": obuf, "n_shadow": int(nsh.item())}
+        # composite: minimum key per ray at its sender, back to the owners
+        best = t.full((n,), MISS_KEY, dtype=t.int64, device=rays.device)
+        if ex.n_sent:
+            best.scatter_reduce_(0, ex.idx, ex.backward(keys), "amin")
+        win = (keys == ex.forward(best)) & (keys != MISS_KEY)
+        out_hits = hits[win]
+        # only the winner shades: the others' hits become misses
+        hits.view(t.int32)[:, 11].masked_fill_(~win, -1)  # spray_rt_hit.domain
+        srays, src = L.spawn_pt(rrays, hits, shade)
+        # shadow rays to the owners of their domains, any hit, OR at the spawner
+        sx = Exchange(C, L.route(srays))
+        occ = L.occluded(sx.forward(srays))
+        socc = t.zeros(srays.shape[0], dtype=t.uint8, device=rays.device)
+        if sx.n_sent:
+            socc.scatter_reduce_(0, sx.idx, sx.backward(occ), "amax")
+        tot = t.tensor([n, srays.shape[0]], dtype=t.int64, device=rays.device)
+        C.all_reduce(tot, C.op("SUM"))
+        return {"samid": rsam[win], "hits": out_hits,
+                "shadow_samid": rsam.index_select(0, src), "shadow_occ": socc,
+                "n_rays": int(tot[0]), "n_shadow": int(tot[1])}

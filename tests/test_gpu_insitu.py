@@ -93,16 +93,46 @@ def test_insitu_world1_matches_whole_scene(spray, oracle):
     org, d, _, sam = oracle.eye_rays_insitu(cam, H.IMG, H.SPP, H.TILE, H.TILE)
     tr = insitu.InsituTracer(insitu.GpuLocal(rt, torch.device("cuda")), insitu.Comm())
     n = len(org)
-    res = tr.trace_tile(_dev_rays(org, d), torch.from_numpy(sam).cuda(), n, H.SHADE)
+    res = tr.trace_tile(_dev_rays(org, d), torch.from_numpy(sam).cuda(), H.SHADE)
     hit_ref, occ_ref, nsh = H.full_reference(oracle, cam, H.TILE, H.SPP)
     got = np.zeros(n, oracle.HIT_DTYPE)
     got[res["samid"].cpu().numpy()] = res["hits"].cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1)
     hit = hit_ref["domain"] >= 0
     assert len(res["samid"]) == hit.sum()
     assert got[hit].tobytes() == hit_ref[hit].tobytes()
-    assert res["n_shadow"] == nsh
-    assert (res["obuf"].cpu().numpy() == occ_ref).all()
+    assert res["n_shadow"] == nsh and res["n_rays"] == n
+    ss = res["shadow_samid"].cpu().numpy()
+    assert len(ss) == nsh and (res["shadow_occ"].cpu().numpy() == occ_ref[ss]).all()
     rt.close()
+
+
+def test_insitu_over_rccl_one_rank(spray, oracle):
+    """The protocol's collectives through RCCL ("nccl", world_size 1, every
+    all-to-all / all-reduce issued): same result as the whole scene."""
+    import torch.distributed as dist
+    from spray_amd import insitu
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rt = _full_ctx(spray)
+        cam = H.bench_camera(oracle)
+        org, d, _, sam = oracle.eye_rays_insitu(cam, H.IMG, H.SPP, H.TILE, H.TILE)
+        tr = insitu.InsituTracer(insitu.GpuLocal(rt, torch.device("cuda")),
+                                 insitu.Comm(dist, always=True))
+        res = tr.trace_tile(_dev_rays(org, d), torch.from_numpy(sam).cuda(), H.SHADE)
+        hit_ref, occ_ref, nsh = H.full_reference(oracle, cam, H.TILE, H.SPP)
+        hit = hit_ref["domain"] >= 0
+        got = np.zeros(len(org), oracle.HIT_DTYPE)
+        got[res["samid"].cpu().numpy()] = (res["hits"].cpu().numpy()
+                                           .view(oracle.HIT_DTYPE).reshape(-1))
+        assert len(res["samid"]) == hit.sum()
+        assert got[hit].tobytes() == hit_ref[hit].tobytes()
+        ss = res["shadow_samid"].cpu().numpy()
+        assert res["n_shadow"] == nsh and (res["shadow_occ"].cpu().numpy() == occ_ref[ss]).all()
+        rt.close()
+    finally:
+        dist.destroy_process_group()
 
 
 def _free_port():
@@ -139,10 +169,12 @@ def _gpu_rank_main(rank, world, port, out):
         rt.eye_rays_insitu(cam, Hh.IMG, Hh.SPP, Hh.TILE, stripe, rays, None, sam)
         rt.sync()
         tr = insitu.InsituTracer(insitu.GpuLocal(rt, torch.device("cuda")), insitu.Comm(dist))
-        res = tr.trace_tile(rays, sam, Hh.TILE[2] * Hh.TILE[3] * Hh.SPP, Hh.SHADE)
+        res = tr.trace_tile(rays, sam, Hh.SHADE)
         np.savez(os.path.join(out, "r%d.npz" % rank), samid=res["samid"].cpu().numpy(),
-                 hits=res["hits"].cpu().numpy(), obuf=res["obuf"].cpu().numpy(),
-                 n_shadow=res["n_shadow"], n_rays=n)
+                 hits=res["hits"].cpu().numpy(),
+                 shadow_samid=res["shadow_samid"].cpu().numpy(),
+                 shadow_occ=res["shadow_occ"].cpu().numpy(), n_shadow=res["n_shadow"],
+                 n_rays=n)
         rt.close()
     finally:
         dist.destroy_process_group()
@@ -165,7 +197,7 @@ def test_insitu_two_ranks_on_gpu(oracle):
         got[r["samid"]] = r["hits"].view(oracle.HIT_DTYPE).reshape(-1)
         seen[r["samid"]] += 1
         assert int(r["n_shadow"]) == nsh
-        assert (r["obuf"] == occ_ref).all()
+        assert (r["shadow_occ"] == occ_ref[r["shadow_samid"]]).all()
         assert len(r["samid"]) > 100
     hit = hit_ref["domain"] >= 0
     assert (seen[hit] == 1).all() and (seen[~hit] == 0).all()

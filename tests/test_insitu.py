@@ -87,11 +87,11 @@ def _rank_main(rank, world, port, out):
         stripe = insitu.horizontal_stripe(world, rank, H.TILE)
         org, d, pix, sam = po.eye_rays_insitu(cam, H.IMG, H.SPP, H.TILE, stripe)
         tr = insitu.InsituTracer(local, insitu.Comm(dist))
-        nsamples = H.TILE[2] * H.TILE[3] * H.SPP
-        res = tr.trace_tile(H.rays_tensor(org, d), torch.from_numpy(sam), nsamples, H.SHADE)
+        res = tr.trace_tile(H.rays_tensor(org, d), torch.from_numpy(sam), H.SHADE)
         np.savez(os.path.join(out, "r%d.npz" % rank), samid=res["samid"].numpy(),
                  hits=res["hits"].numpy(), shadow_samid=res["shadow_samid"].numpy(),
-                 obuf=res["obuf"].numpy(), n_shadow=res["n_shadow"], n_rays=len(org))
+                 shadow_occ=res["shadow_occ"].numpy(), n_shadow=res["n_shadow"],
+                 n_total=res["n_rays"], n_rays=len(org))
     finally:
         dist.destroy_process_group()
 
@@ -124,8 +124,10 @@ def test_insitu_protocol_gloo(oracle, world):
     assert (seen[hit] == 1).all() and (seen[~hit] == 0).all()  # one winner per hit
     assert got[hit].tobytes() == hit_ref[hit].tobytes()
     for r in res:
-        assert int(r["n_shadow"]) == nsh_ref
-        assert (r["obuf"] == occ_ref).all()
+        assert int(r["n_shadow"]) == nsh_ref and int(r["n_total"]) == n
+        assert (r["shadow_occ"] == occ_ref[r["shadow_samid"]]).all()
+        # a rank spawns shadow rays exactly for the samples it won
+        assert set(r["shadow_samid"].tolist()) <= set(r["samid"].tolist())
     sh = np.concatenate([r["shadow_samid"] for r in res])
     assert len(sh) == nsh_ref and len(set(sh.tolist())) == nsh_ref
     assert 0 < occ_ref.sum() < nsh_ref
