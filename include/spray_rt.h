@@ -227,6 +227,32 @@ int spray_rt_route(spray_rt_ctx_t ctx, const spray_rt_ray* rays, size_t M,
 int spray_rt_intersect_scene_keyed(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                                    size_t M, spray_rt_hit* hits, uint64_t* keys);
 
+/* ---- out-of-core (streamed domains, config 4) ---- */
+/* An LRU cache of cache_slots domain images in HBM, fed from pinned host
+ * memory (LruCache::load, src/render/lru_cache.cc:65-171; Scene::load,
+ * src/render/scene.inl:161-187).  Uses the context's domain boxes
+ * (spray_rt_domain_bounds first), stream and device. */
+typedef struct spray_rt_ooc* spray_rt_ooc_t;
+int spray_rt_ooc_create(spray_rt_ctx_t ctx, int cache_slots, spray_rt_ooc_t* out);
+int spray_rt_ooc_destroy(spray_rt_ooc_t ooc);
+/* TriMeshBuffer::load (trimesh_buffer.cc:117-169) once per domain: the BVH
+ * image is built here and kept in pinned host memory. */
+int spray_rt_ooc_set_domain(spray_rt_ooc_t ooc, int domain, const float* verts_xyz,
+                            size_t nverts, const uint32_t* faces, size_t nfaces,
+                            const uint32_t* colors_rgb, const float* vnormals);
+/* Closest hit of a device ray batch over every domain of each ray's list,
+ * the domains streamed through the cache in ascending id order (queues
+ * built on the device, one drain launch per domain).  Same hit records as
+ * spray_rt_intersect_scene.  Device buffers only. */
+int spray_rt_ooc_intersect(spray_rt_ooc_t ooc, const spray_rt_ray* rays, size_t M,
+                           spray_rt_hit* hits);
+/* Any hit of the rays with valid[i] != 0 (valid may be NULL), domains in
+ * descending order; occluded[i] written for those rays.  Device buffers. */
+int spray_rt_ooc_occluded(spray_rt_ooc_t ooc, const spray_rt_ray* rays, size_t M,
+                          const uint8_t* valid, uint8_t* occluded);
+/* out[4] = cache loads (misses), cache hits, bytes uploaded, drain launches */
+int spray_rt_ooc_stats(spray_rt_ooc_t ooc, unsigned long long out[4]);
+
 /* ---- ray sources on the device (caller side of the hot path) ---- */
 /* cam[14] = pos[3], lowerleft[3], wvec[3], hvec[3], image_w, image_h
  * (Camera::init, src/render/camera.h:128-166).  ooc::Tracer::genMultiEyes

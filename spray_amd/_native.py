@@ -65,6 +65,12 @@ SIGNATURES = {
     "spray_rt_eye_rays_ooc": (I, [P, P, I, I, I, I, I, I, P, P, P]),
     "spray_rt_eye_rays_insitu": (I, [P, P, I, I, I, I, I, I, I, I, I, I, P, P, P]),
     "spray_rt_set_owners": (I, [P, P]),
+    "spray_rt_ooc_create": (I, [P, I, P]),
+    "spray_rt_ooc_destroy": (I, [P]),
+    "spray_rt_ooc_set_domain": (I, [P, I, P, SZ, P, SZ, P, P]),
+    "spray_rt_ooc_intersect": (I, [P, P, SZ, P]),
+    "spray_rt_ooc_occluded": (I, [P, P, SZ, P, P]),
+    "spray_rt_ooc_stats": (I, [P, P]),
     "spray_rt_route": (I, [P, P, SZ, P]),
     "spray_rt_intersect_scene_keyed": (I, [P, P, SZ, P, P]),
     "spray_rt_spawn_shadows_pt": (I, [P, P, P, SZ, P, P, P, P]),

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -16,68 +17,16 @@
 
 #include "bvh_build.h"
 #include "rt_common.h"
+#include "rt_ctx.h"
 #include "rt_kernels.h"
 #include "spray_rt.h"
 
 using namespace spray_rt;
 
-namespace {
+using namespace spray_rt::detail;
 
-struct SlotHost {
-  void* dmem = nullptr;  // one allocation: nodes|tris|prims|faces|colors|normals
-  size_t bytes = 0;
-  SlotDesc desc{};
-  int depth = 0;
-  hipEvent_t ready = nullptr;  // async upload completion
-  void* pinned = nullptr;      // staging for async uploads
-  size_t pinned_bytes = 0;
-};
-
-size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
-
-}  // namespace
-
-struct spray_rt_ctx {
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t user_stream = nullptr;
-  bool user_stream_set = false;
-  hipStream_t upload_stream = nullptr;
-  std::vector<SlotHost> slots;
-  SlotDesc* d_slots = nullptr;
-  size_t d_slots_cap = 0;
-  bool slots_dirty = true;
-  // scene path
-  int ndom = 0;
-  float* d_boxes = nullptr;
-  int* d_dom2slot = nullptr;
-  DomTrav* d_domtrav = nullptr;  // per-domain traversal descriptors
-  int* d_owner = nullptr;        // in-situ domain -> rank map
-  BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
-  int ntlas = 0;
-  int tlas_depth = 0;
-  std::vector<int> dom2slot;
-  bool dom_dirty = true;
-  // segment tables
-  int* d_seg_slot = nullptr;
-  size_t* d_seg_off = nullptr;
-  size_t seg_cap = 0;
-  // host-pointer staging
-  void* d_stage = nullptr;
-  size_t stage_cap = 0;
-  void* d_stage2 = nullptr;
-  size_t stage2_cap = 0;
-  void* d_stage3 = nullptr;
-  size_t stage3_cap = 0;
-  uint32_t* d_block_counts = nullptr;
-  uint32_t* d_heads = nullptr;  // work-queue heads of the persistent launches
-  void* d_sel = nullptr;        // selected indices + count + select scratch
-  size_t sel_cap = 0;
-  size_t block_cap = 0;
-  std::string err;
-};
-
-namespace {
+namespace spray_rt {
+namespace detail {
 
 int fail(spray_rt_ctx* c, int code, const char* fmt, ...) {
   char buf[512];
@@ -88,14 +37,6 @@ int fail(spray_rt_ctx* c, int code, const char* fmt, ...) {
   if (c) c->err = buf;
   return code;
 }
-
-#define HIPCHK(ctx, expr)                                                   \
-  do {                                                                      \
-    hipError_t _e = (expr);                                                 \
-    if (_e != hipSuccess)                                                   \
-      return fail(ctx, SPRAY_RT_ERR_HIP, "%s: %s", #expr,                   \
-                  hipGetErrorString(_e));                                   \
-  } while (0)
 
 hipStream_t stream_of(spray_rt_ctx* c) {
   return c->user_stream_set ? c->user_stream : c->own_stream;
@@ -122,6 +63,60 @@ int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes) {
   *cap = want;
   return SPRAY_RT_OK;
 }
+
+bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
+                      size_t nfaces, const uint32_t* colors, const float* normals,
+                      SlotImage* out) {
+  BvhImage img;
+  if (!build_bvh(verts, nverts, faces, nfaces, &img)) return false;
+  const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
+  const size_t b_tris = align256(img.tris.size() * sizeof(float));
+  const size_t b_prims = align256(img.prims.size() * sizeof(uint32_t));
+  const size_t b_faces = align256(3 * nfaces * sizeof(uint32_t));
+  const size_t b_colors = colors ? align256(nverts * sizeof(uint32_t)) : 0;
+  const size_t b_normals = normals ? align256(3 * nverts * sizeof(float)) : 0;
+  out->bytes.assign(
+      std::max<size_t>(256, b_nodes + b_tris + b_prims + b_faces + b_colors + b_normals), 0);
+  char* host = out->bytes.data();
+  size_t off = 0;
+  auto put = [&](const void* src, size_t n, size_t padded) {
+    if (n) std::memcpy(host + off, src, n);
+    size_t o = off;
+    off += padded;
+    return o;
+  };
+  out->o_nodes = put(img.nodes.data(), img.nodes.size() * sizeof(BvhNode), b_nodes);
+  out->o_tris = put(img.tris.data(), img.tris.size() * sizeof(float), b_tris);
+  out->o_prims = put(img.prims.data(), img.prims.size() * sizeof(uint32_t), b_prims);
+  out->o_faces = put(faces, 3 * nfaces * sizeof(uint32_t), b_faces);
+  out->o_colors = colors ? put(colors, nverts * sizeof(uint32_t), b_colors) : SIZE_MAX;
+  out->o_normals = normals ? put(normals, 3 * nverts * sizeof(float), b_normals) : SIZE_MAX;
+  out->nnodes = uint32_t(img.nodes.size());
+  out->ntris = uint32_t(img.prims.size());
+  out->nverts = uint32_t(nverts);
+  out->depth = img.depth;
+  return true;
+}
+
+SlotDesc SlotImage::desc_at(const void* base) const {
+  const char* d = static_cast<const char*>(base);
+  SlotDesc s{};
+  s.nodes = reinterpret_cast<const BvhNode*>(d + o_nodes);
+  s.tris = reinterpret_cast<const float*>(d + o_tris);
+  s.prims = reinterpret_cast<const uint32_t*>(d + o_prims);
+  s.faces = reinterpret_cast<const uint32_t*>(d + o_faces);
+  s.colors = o_colors == SIZE_MAX ? nullptr : reinterpret_cast<const uint32_t*>(d + o_colors);
+  s.normals = o_normals == SIZE_MAX ? nullptr : reinterpret_cast<const float*>(d + o_normals);
+  s.ntris = ntris;
+  s.nverts = nverts;
+  s.nnodes = nnodes;
+  return s;
+}
+
+}  // namespace detail
+}  // namespace spray_rt
+
+namespace {
 
 // Makes pending async uploads visible to the compute stream and pushes the
 // slot table / domain map when they changed.
@@ -311,8 +306,8 @@ int spray_rt_domain_upload(spray_rt_ctx_t c, int slot, const float* verts,
     return fail(c, SPRAY_RT_ERR_ARG, "bad slot %d", slot);
   if ((nverts && !verts) || (nfaces && !faces))
     return fail(c, SPRAY_RT_ERR_ARG, "null mesh arrays");
-  BvhImage img;
-  if (!build_bvh(verts, nverts, faces, nfaces, &img))
+  SlotImage img;
+  if (!build_slot_image(verts, nverts, faces, nfaces, colors, normals, &img))
     return fail(c, SPRAY_RT_ERR_ARG, "face index out of range or mesh too large");
   if (size_t(slot) >= c->slots.size()) c->slots.resize(slot + 1);
   SlotHost& sh = c->slots[slot];
@@ -320,15 +315,7 @@ int spray_rt_domain_upload(spray_rt_ctx_t c, int slot, const float* verts,
   // the previous image may still be read by queued work
   HIPCHK(c, hipStreamSynchronize(stream_of(c)));
   if (sh.ready) HIPCHK(c, hipEventSynchronize(sh.ready));
-
-  const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
-  const size_t b_tris = align256(img.tris.size() * sizeof(float));
-  const size_t b_prims = align256(img.prims.size() * sizeof(uint32_t));
-  const size_t b_faces = align256(3 * nfaces * sizeof(uint32_t));
-  const size_t b_colors = colors ? align256(nverts * sizeof(uint32_t)) : 0;
-  const size_t b_normals = normals ? align256(3 * nverts * sizeof(float)) : 0;
-  const size_t total =
-      std::max<size_t>(256, b_nodes + b_tris + b_prims + b_faces + b_colors + b_normals);
+  const size_t total = img.bytes.size();
   if (sh.bytes < total) {
     if (sh.dmem) HIPCHK(c, hipFree(sh.dmem));
     sh.dmem = nullptr;
@@ -336,52 +323,22 @@ int spray_rt_domain_upload(spray_rt_ctx_t c, int slot, const float* verts,
     HIPCHK(c, hipMalloc(&sh.dmem, total));
     sh.bytes = total;
   }
-  // host image of the slot (pinned when async)
-  std::vector<char> tmp;
-  char* host;
-  if (async) {
+  char* d = static_cast<char*>(sh.dmem);
+  if (async) {  // staged through pinned memory, completion tracked by an event
     if (sh.pinned_bytes < total) {
       if (sh.pinned) HIPCHK(c, hipHostFree(sh.pinned));
       sh.pinned = nullptr;
       HIPCHK(c, hipHostMalloc(&sh.pinned, total, hipHostMallocDefault));
       sh.pinned_bytes = total;
     }
-    host = static_cast<char*>(sh.pinned);
-  } else {
-    tmp.resize(total);
-    host = tmp.data();
-  }
-  size_t off = 0;
-  auto put = [&](const void* src, size_t n, size_t padded) {
-    if (n) std::memcpy(host + off, src, n);
-    size_t o = off;
-    off += padded;
-    return o;
-  };
-  const size_t o_nodes = put(img.nodes.data(), img.nodes.size() * sizeof(BvhNode), b_nodes);
-  const size_t o_tris = put(img.tris.data(), img.tris.size() * sizeof(float), b_tris);
-  const size_t o_prims = put(img.prims.data(), img.prims.size() * sizeof(uint32_t), b_prims);
-  const size_t o_faces = put(faces, 3 * nfaces * sizeof(uint32_t), b_faces);
-  const size_t o_colors = colors ? put(colors, nverts * sizeof(uint32_t), b_colors) : 0;
-  const size_t o_normals = normals ? put(normals, 3 * nverts * sizeof(float), b_normals) : 0;
-  char* d = static_cast<char*>(sh.dmem);
-  if (async) {
+    std::memcpy(sh.pinned, img.bytes.data(), total);
     if (!sh.ready) HIPCHK(c, hipEventCreateWithFlags(&sh.ready, hipEventDisableTiming));
-    HIPCHK(c, hipMemcpyAsync(d, host, off, hipMemcpyHostToDevice, c->upload_stream));
+    HIPCHK(c, hipMemcpyAsync(d, sh.pinned, total, hipMemcpyHostToDevice, c->upload_stream));
     HIPCHK(c, hipEventRecord(sh.ready, c->upload_stream));
   } else {
-    HIPCHK(c, hipMemcpy(d, host, off, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d, img.bytes.data(), total, hipMemcpyHostToDevice));
   }
-  SlotDesc& desc = sh.desc;
-  desc.nodes = reinterpret_cast<const BvhNode*>(d + o_nodes);
-  desc.tris = reinterpret_cast<const float*>(d + o_tris);
-  desc.prims = reinterpret_cast<const uint32_t*>(d + o_prims);
-  desc.faces = reinterpret_cast<const uint32_t*>(d + o_faces);
-  desc.colors = colors ? reinterpret_cast<const uint32_t*>(d + o_colors) : nullptr;
-  desc.normals = normals ? reinterpret_cast<const float*>(d + o_normals) : nullptr;
-  desc.ntris = uint32_t(img.prims.size());
-  desc.nverts = uint32_t(nverts);
-  desc.nnodes = uint32_t(img.nodes.size());
+  sh.desc = img.desc_at(d);
   sh.depth = img.depth;
   c->slots_dirty = true;
   return SPRAY_RT_OK;

@@ -1,0 +1,114 @@
+// rt_ctx.h -- the engine context behind spray_rt_ctx_t and the internal
+// helpers shared by the C ABI translation units (rt_api.cpp, ooc.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rt_common.h"
+#include "spray_rt.h"
+
+namespace spray_rt {
+namespace detail {
+
+struct SlotHost {
+  void* dmem = nullptr;  // one allocation: nodes|tris|prims|faces|colors|normals
+  size_t bytes = 0;
+  SlotDesc desc{};
+  int depth = 0;
+  hipEvent_t ready = nullptr;  // async upload completion
+  void* pinned = nullptr;      // staging for async uploads
+  size_t pinned_bytes = 0;
+};
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace detail
+}  // namespace spray_rt
+
+struct spray_rt_ctx {
+  using SlotHost = spray_rt::detail::SlotHost;
+  using SlotDesc = spray_rt::SlotDesc;
+  using DomTrav = spray_rt::DomTrav;
+  using BvhNode = spray_rt::BvhNode;
+
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t user_stream = nullptr;
+  bool user_stream_set = false;
+  hipStream_t upload_stream = nullptr;
+  std::vector<SlotHost> slots;
+  SlotDesc* d_slots = nullptr;
+  size_t d_slots_cap = 0;
+  bool slots_dirty = true;
+  // scene path
+  int ndom = 0;
+  float* d_boxes = nullptr;
+  int* d_dom2slot = nullptr;
+  DomTrav* d_domtrav = nullptr;  // per-domain traversal descriptors
+  int* d_owner = nullptr;        // in-situ domain -> rank map
+  BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
+  int ntlas = 0;
+  int tlas_depth = 0;
+  std::vector<int> dom2slot;
+  bool dom_dirty = true;
+  // segment tables
+  int* d_seg_slot = nullptr;
+  size_t* d_seg_off = nullptr;
+  size_t seg_cap = 0;
+  // host-pointer staging
+  void* d_stage = nullptr;
+  size_t stage_cap = 0;
+  void* d_stage2 = nullptr;
+  size_t stage2_cap = 0;
+  void* d_stage3 = nullptr;
+  size_t stage3_cap = 0;
+  uint32_t* d_block_counts = nullptr;
+  uint32_t* d_heads = nullptr;  // work-queue heads of the persistent launches
+  void* d_sel = nullptr;        // selected indices + count + select scratch
+  size_t sel_cap = 0;
+  size_t block_cap = 0;
+  std::string err;
+};
+
+namespace spray_rt {
+namespace detail {
+
+// Device image of one domain, packed on the host: BVH2 nodes | triangle
+// records | leaf->face map | faces | colors | normals, 256-B aligned (the
+// HBM slot layout of rt_common.h).
+struct SlotImage {
+  std::vector<char> bytes;
+  size_t o_nodes = 0, o_tris = 0, o_prims = 0, o_faces = 0;
+  size_t o_colors = SIZE_MAX, o_normals = SIZE_MAX;  // SIZE_MAX: absent
+  uint32_t nnodes = 0, ntris = 0, nverts = 0;
+  int depth = 0;
+  // descriptor of the image once copied to device address base
+  SlotDesc desc_at(const void* base) const;
+};
+// Builds the canonical BVH2 (bvh_build.h) and packs the image; false on
+// invalid face indices.
+bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
+                      size_t nfaces, const uint32_t* colors, const float* normals,
+                      SlotImage* out);
+
+// Records a message in the context; returns code.
+int fail(spray_rt_ctx* c, int code, const char* fmt, ...);
+hipStream_t stream_of(spray_rt_ctx* c);
+bool is_device_ptr(const void* p);
+// grows *buf to at least bytes (device memory)
+int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes);
+
+}  // namespace detail
+}  // namespace spray_rt
+
+#define HIPCHK(ctx, expr)                                                   \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess)                                                   \
+      return ::spray_rt::detail::fail(ctx, SPRAY_RT_ERR_HIP, "%s: %s", #expr, \
+                                      hipGetErrorString(_e));               \
+  } while (0)

@@ -1,0 +1,399 @@
+// rt_device.h -- device-side building blocks shared by the gfx950 kernels
+// (rt_kernels.hip, ooc_kernels.hip): ray / box / triangle tests, BVH2
+// traversal of one domain tree, the updateIntersection epilogue, the
+// top-level domain mask and the point-light shadow spawn.
+//
+// Every translation unit is compiled with -ffp-contract=off: each fused
+// multiply-add here is an explicit fmaf(), so t/u/v/Ng are bit-identical to
+// the CPU oracle (oracle/oracle.c) and across kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "rt_common.h"
+#include "rt_kernels.h"
+#include "spray_rt.h"
+
+namespace spray_rt {
+namespace {
+
+constexpr float kInf = __builtin_inff();
+constexpr int32_t kNone = INT_MAX;
+
+inline unsigned grid_for(size_t M) { return unsigned((M + kBlock - 1) / kBlock); }
+
+// Pointers read out of the slot table are generic; re-qualify them as global
+// so the loads are global_load_* (not flat_*, which also ticks lgkmcnt).
+#define GAS __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const GAS T* gptr(const T* p) {
+  return (const GAS T*)(p);
+}
+typedef float v4f __attribute__((ext_vector_type(4)));
+// 16-B global load of element i of a float4 array
+__device__ __forceinline__ float4 ld4(const void* base, size_t i) {
+  const v4f v = reinterpret_cast<const GAS v4f*>(gptr(base))[i];
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// ---------------------------------------------------------------------------
+// ray / box / triangle primitives
+// ---------------------------------------------------------------------------
+struct Ray {
+  float ox, oy, oz;
+  float dx, dy, dz;
+  float ix, iy, iz;     // 1/d with |d| clamped at kDirClamp (culling only)
+  float oix, oiy, oiz;  // o * inv
+};
+
+__device__ __forceinline__ float clamp_dir(float d) {
+  return fabsf(d) < kDirClamp ? copysignf(kDirClamp, d) : d;
+}
+
+__device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx,
+                                        float dy, float dz) {
+  Ray r;
+  r.ox = ox; r.oy = oy; r.oz = oz;
+  r.dx = dx; r.dy = dy; r.dz = dz;
+  r.ix = 1.0f / clamp_dir(dx);
+  r.iy = 1.0f / clamp_dir(dy);
+  r.iz = 1.0f / clamp_dir(dz);
+  r.oix = ox * r.ix;
+  r.oiy = oy * r.iy;
+  r.oiz = oz * r.iz;
+  return r;
+}
+
+// Conservative slab test of a (padded) node box against [tnear, tfar].
+__device__ __forceinline__ bool slab(const Ray& r, float lx, float ly, float lz,
+                                     float hx, float hy, float hz, float tnear,
+                                     float tfar, float& tenter) {
+  float t0x = fmaf(lx, r.ix, -r.oix), t1x = fmaf(hx, r.ix, -r.oix);
+  float t0y = fmaf(ly, r.iy, -r.oiy), t1y = fmaf(hy, r.iy, -r.oiy);
+  float t0z = fmaf(lz, r.iz, -r.oiz), t1z = fmaf(hz, r.iz, -r.oiz);
+  float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)),
+                     fmaxf(fminf(t0z, t1z), tnear));
+  float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)),
+                     fminf(fmaxf(t0z, t1z), tfar * kTfarSlack));
+  tenter = tmin;
+  return tmin <= tmax;
+}
+
+// Embree 2.17 MoellerTrumboreIntersector1 restated (e1 = v0-v1, e2 = v2-v0,
+// Ng = e1 x e2; edge tests scaled by |den|); t, u, v by IEEE division.
+// Record: a = v0.xyz e1.x | b = e1.yz e2.xy | c = e2.z Ng.xyz
+__device__ __forceinline__ bool tri_test(const Ray& r, float tnear, float4 a,
+                                         float4 b, float4 c, float& t,
+                                         float& u, float& v) {
+  const float cx = a.x - r.ox, cy = a.y - r.oy, cz = a.z - r.oz;
+  const float rx = fmaf(r.dy, cz, -(r.dz * cy));
+  const float ry = fmaf(r.dz, cx, -(r.dx * cz));
+  const float rz = fmaf(r.dx, cy, -(r.dy * cx));
+  const float den = fmaf(c.w, r.dz, fmaf(c.z, r.dy, c.y * r.dx));
+  const float absden = fabsf(den);
+  float U = fmaf(rz, c.x, fmaf(ry, b.w, rx * b.z));  // R . e2
+  float V = fmaf(rz, b.y, fmaf(ry, b.x, rx * a.w));  // R . e1
+  float T = fmaf(c.w, cz, fmaf(c.z, cy, c.y * cx));  // Ng . C
+  if (den < 0.0f) {
+    U = -U;
+    V = -V;
+    T = -T;
+  }
+  if (!(den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= absden)) return false;
+  const float tt = T / absden;
+  if (!(tt > tnear)) return false;
+  t = tt;
+  u = U / absden;
+  v = V / absden;
+  return true;
+}
+
+// Reference domain-box test: intersectAabb (src/render/aabb.h:139-169) with
+// t0 = SPRAY_RAY_EPSILON, t1 = +inf (RTCRayExt::reset, rays.h:149-169).  The
+// exact float ops of the reference (division-based inverse, sub then mul).
+struct DRay {
+  float ox, oy, oz, ix, iy, iz;
+};
+__device__ __forceinline__ DRay make_dray(float ox, float oy, float oz,
+                                          float dx, float dy, float dz) {
+  DRay r;
+  r.ox = ox; r.oy = oy; r.oz = oz;
+  r.ix = 1.0f / dx;
+  r.iy = 1.0f / dy;
+  r.iz = 1.0f / dz;
+  return r;
+}
+__device__ __forceinline__ bool aabb_ref6(float lx, float ly, float lz, float hx,
+                                          float hy, float hz, const DRay& r,
+                                          float& tmin_out) {
+  const bool sx = r.ix < 0.0f, sy = r.iy < 0.0f, sz = r.iz < 0.0f;
+  float tmin = ((sx ? hx : lx) - r.ox) * r.ix;
+  float tmax = ((sx ? lx : hx) - r.ox) * r.ix;
+  const float tymin = ((sy ? hy : ly) - r.oy) * r.iy;
+  const float tymax = ((sy ? ly : hy) - r.oy) * r.iy;
+  if ((tmin > tymax) || (tymin > tmax)) return false;
+  if (tymin > tmin) tmin = tymin;
+  if (tymax < tmax) tmax = tymax;
+  const float tzmin = ((sz ? hz : lz) - r.oz) * r.iz;
+  const float tzmax = ((sz ? lz : hz) - r.oz) * r.iz;
+  if ((tmin > tzmax) || (tzmin > tmax)) return false;
+  if (tzmin > tmin) tmin = tzmin;
+  if (tzmax < tmax) tmax = tzmax;
+  tmin_out = tmin;
+  return (tmin < kInf) && (tmax > kRayEpsilon);
+}
+__device__ __forceinline__ bool aabb_ref(const float* box, const DRay& r,
+                                         float& tmin_out) {
+  return aabb_ref6(box[0], box[1], box[2], box[3], box[4], box[5], r, tmin_out);
+}
+
+// ---------------------------------------------------------------------------
+// BVH2 traversal of one slot (canonical order, see oracle.c traverse())
+// ---------------------------------------------------------------------------
+struct Best {
+  float t;
+  uint32_t prim;  // PLY face index (tie-break key)
+  uint32_t leaf;  // leaf-order triangle index (u, v, Ng are re-derived from it)
+};
+
+// ANY = occlusion (returns true at the first hit with t <= tfar_any).
+// Closest hit: keeps the lexicographic minimum of (t, prim) starting from
+// best; a candidate with t == best.t wins only with a smaller face index.
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
+                                           const uint32_t* prims_, const Ray& r,
+                                           float tnear, float tfar_any,
+                                           Best& best, int32_t* stk,
+                                           unsigned& nnode, unsigned& ntri) {
+  // u, v of the winner are not carried through the traversal (2 VGPRs less at
+  // the occupancy-limiting point): hit_uv() recomputes them bit-identically.
+  const GAS uint32_t* __restrict__ prims = gptr(prims_);
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const size_t nb = 4 * size_t(cur);
+    const float4 n0 = ld4(nodes, nb), n1 = ld4(nodes, nb + 1), n2 = ld4(nodes, nb + 2),
+                 n3 = ld4(nodes, nb + 3);
+    if (COUNT) ++nnode;
+    const float tcut = ANY ? tfar_any : best.t;
+    float tl, tr;
+    const bool hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tcut, tl);
+    const bool hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tcut, tr);
+    int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+    bool h0 = hl, h1 = hr;
+    if (hl && hr && tr < tl) {
+      const int32_t x = c0;
+      c0 = c1;
+      c1 = x;
+    } else if (!hl && hr) {
+      c0 = c1;
+      h0 = true;
+      h1 = false;
+    }
+    int32_t next = kNone;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int32_t c = k == 0 ? c0 : c1;
+      const bool h = k == 0 ? h0 : h1;
+      if (!h) continue;
+      if (c < 0) {
+        const uint32_t enc = ~uint32_t(c);
+        const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
+        for (uint32_t q = 0; q < cnt; ++q) {
+          const uint32_t p = first + q;
+          const float4 a = ld4(tris, 3 * size_t(p)), b = ld4(tris, 3 * size_t(p) + 1),
+                       cc = ld4(tris, 3 * size_t(p) + 2);
+          if (COUNT) ++ntri;
+          float t, u, v;
+          if (!tri_test(r, tnear, a, b, cc, t, u, v)) continue;
+          if (ANY) {
+            if (t <= tfar_any) return true;
+          } else {
+            const uint32_t pid = prims[p];
+            if (t < best.t || (t == best.t && pid < best.prim)) {
+              best.t = t;
+              best.prim = pid;
+              best.leaf = p;
+            }
+          }
+        }
+      } else if (next == kNone) {
+        next = c;
+      } else {
+        stk[sp * kBlock] = c;
+        ++sp;
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = stk[sp * kBlock];
+    }
+    cur = next;
+  }
+  return false;
+}
+
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool trace_slot(const SlotDesc& s, const Ray& r,
+                                           float tnear, float tfar_any,
+                                           Best& best, int32_t* stk,
+                                           unsigned& nnode, unsigned& ntri) {
+  return trace_tree<ANY, COUNT>(s.nodes, s.tris, s.prims, r, tnear, tfar_any, best,
+                                stk, nnode, ntri);
+}
+
+// u, v (and Ng) of the accepted triangle: the same tri_test on the same
+// operands, hence the same bits as during the traversal.
+__device__ __forceinline__ float4 hit_uv(const SlotDesc& s, const Ray& r,
+                                         float tnear, uint32_t leaf, float& u,
+                                         float& v) {
+  const float4 a = ld4(s.tris, 3 * size_t(leaf)), b = ld4(s.tris, 3 * size_t(leaf) + 1),
+               c = ld4(s.tris, 3 * size_t(leaf) + 2);
+  float t;
+  tri_test(r, tnear, a, b, c, t, u, v);
+  return c;
+}
+
+// TriMeshBuffer::updateIntersection (src/render/trimesh_buffer.cc:328-360).
+__device__ __forceinline__ void epilogue(const SlotDesc& s, uint32_t prim,
+                                         float u, float v, uint32_t& color,
+                                         float& nsx, float& nsy, float& nsz) {
+  const GAS uint32_t* faces = gptr(s.faces);
+  const uint32_t f0 = faces[3 * prim], f1 = faces[3 * prim + 1],
+                 f2 = faces[3 * prim + 2];
+  const float w = 1.f - u - v;
+  if (s.colors) {
+    const GAS uint32_t* colors = gptr(s.colors);
+    const uint32_t c0 = colors[f0], c1 = colors[f1], c2 = colors[f2];
+    uint32_t ch[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int sh = 16 - 8 * k;
+      const float a = float((c0 >> sh) & 0xffu), b = float((c1 >> sh) & 0xffu),
+                  c = float((c2 >> sh) & 0xffu);
+      ch[k] = uint32_t((a * w + b * u) + c * v);
+    }
+    color = (ch[0] << 16) | (ch[1] << 8) | ch[2];
+  } else {
+    color = 0;
+  }
+  if (s.normals) {
+    const GAS float* n0 = gptr(s.normals) + 3 * f0;
+    const GAS float* n1 = gptr(s.normals) + 3 * f1;
+    const GAS float* n2 = gptr(s.normals) + 3 * f2;
+    nsx = (n0[0] * w + n1[0] * u) + n2[0] * v;
+    nsy = (n0[1] * w + n1[1] * u) + n2[1] * v;
+    nsz = (n0[2] * w + n1[2] * u) + n2[2] * v;
+  } else {
+    nsx = nsy = nsz = 0.0f;
+  }
+}
+
+// Domain list of one ray as a bitmask: WbvhEmbree::intersect
+// (src/render/wbvh_embree.cc:126-148) over the top-level tree staged in LDS.
+// Every node test is the reference's intersectAabb (exact ops) on exact union
+// boxes, so the mask equals the brute-force list over all domain boxes.
+template <int W>
+__device__ __forceinline__ void tlas_mask(const float4* stl, int ntlas, int32_t* stk,
+                                          float4 o4, float4 d4, uint64_t* m) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  if (ntlas <= 0) return;
+  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const float4 a = stl[4 * cur], b = stl[4 * cur + 1], c = stl[4 * cur + 2],
+                 e = stl[4 * cur + 3];
+    const int32_t cl = __float_as_int(e.x), cr = __float_as_int(e.y);
+    float tm;
+    const bool hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
+    const bool hr = cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+    int32_t next = kNone;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int32_t ch = k == 0 ? cl : cr;
+      if (!(k == 0 ? hl : hr)) continue;
+      if (ch < 0) {
+        const int d = int(~uint32_t(ch) >> 2);
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (w == (d >> 6)) m[w] |= 1ull << (d & 63);
+      } else if (next == kNone) {
+        next = ch;
+      } else {
+        stk[sp * kBlock] = ch;
+        ++sp;
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = stk[sp * kBlock];
+    }
+    cur = next;
+  }
+}
+
+// ooc::ShaderPt point-light branch for camera rays (ooc_shader_pt.h:93-171,
+// blinnPhong reflection.h:202-214, hasPositive utils/math.h:76-78).
+struct ShadePt {
+  float lp[3], lr[3], ks[3], shininess;
+};
+
+__device__ __forceinline__ bool shadow_pt(const spray_rt_ray& ray,
+                                          const spray_rt_hit& h,
+                                          const ShadePt& sh, float pos[3],
+                                          float wi[3]) {
+  if (h.domain < 0) return false;
+  const float* o = ray.org;
+  const float* d = ray.dir;
+  pos[0] = d[0] * h.t + o[0];
+  pos[1] = d[1] * h.t + o[1];
+  pos[2] = d[2] * h.t + o[2];
+  const float kd[3] = {
+      float(double((h.color >> 16) & 0xffu) * 0.00392156862745098),
+      float(double((h.color >> 8) & 0xffu) * 0.00392156862745098),
+      float(double(h.color & 0xffu) * 0.00392156862745098)};
+  const float wo[3] = {-d[0], -d[1], -d[2]};
+  const float cos_i = (wo[0] * h.ns[0] + wo[1] * h.ns[1]) + wo[2] * h.ns[2];
+  float n[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  if (!(cos_i > 0.0f)) {
+    n[0] = -n[0];
+    n[1] = -n[1];
+    n[2] = -n[2];
+  }
+  float inv = 1.0f / sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);
+  n[0] *= inv;
+  n[1] *= inv;
+  n[2] *= inv;
+  float l[3] = {sh.lp[0] - pos[0], sh.lp[1] - pos[1], sh.lp[2] - pos[2]};
+  inv = 1.0f / sqrtf((l[0] * l[0] + l[1] * l[1]) + l[2] * l[2]);
+  wi[0] = l[0] * inv;
+  wi[1] = l[1] * inv;
+  wi[2] = l[2] * inv;
+  float ct = (n[0] * wi[0] + n[1] * wi[1]) + n[2] * wi[2];
+  ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
+  float hh[3] = {wi[0] + wo[0], wi[1] + wo[1], wi[2] + wo[2]};
+  inv = 1.0f / sqrtf((hh[0] * hh[0] + hh[1] * hh[1]) + hh[2] * hh[2]);
+  hh[0] *= inv;
+  hh[1] *= inv;
+  hh[2] *= inv;
+  float ndh = (n[0] * hh[0] + n[1] * hh[1]) + n[2] * hh[2];
+  ndh = ndh < 0.0f ? 0.0f : (ndh > 1.0f ? 1.0f : ndh);
+  const float pw = powf(ndh, sh.shininess);
+  bool pos_any = false;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float cs = sh.ks[k] * pw, cd = kd[k] * ct;
+    if ((sh.lr[k] * (cd + cs)) * 1.0f > 0.0f) pos_any = true;
+  }
+  return pos_any;
+}
+
+}  // namespace
+}  // namespace spray_rt

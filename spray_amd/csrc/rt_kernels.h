@@ -96,4 +96,48 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
                            int32_t* out_src, uint32_t* d_count,
                            uint32_t* block_counts);
 
+// ---- out-of-core path (ooc_kernels.hip) ----
+// One resident domain as its drain launch sees it.
+struct OocDomain {
+  const void* nodes;
+  const void* tris;
+  const uint32_t* prims;
+  const uint32_t* faces;
+  const uint32_t* colors;
+  const float* normals;
+  float box[6];  // world box (the reference's domain-list test)
+  int domain;
+};
+
+// Device scratch of the queue build (sized by the caller).
+struct OocScratch {
+  uint64_t* masks;   // [M * W]
+  uint32_t* npairs;  // [M + 1]
+  uint32_t* poff;    // [M + 1]
+  uint16_t* key_in;  // [pair_cap]
+  uint16_t* key_out;
+  uint32_t* val_in;
+  uint32_t* val_out;  // the queues: ray ids grouped by domain, ascending
+  uint32_t* first;    // [ndom + 1]
+  void* temp;
+  size_t temp_bytes;
+  size_t pair_cap;
+  uint32_t npair;
+};
+
+// Builds the per-domain ray queues of a batch (rays with valid[i] == 0 are
+// skipped; valid may be null) and copies first[0..ndom] to h_first (host):
+// domain d's queue is val_out[first[d] .. first[d+1]).  Returns
+// hipErrorOutOfMemory (q.npair = needed) when pair_cap is too small.
+hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int ndom,
+                             const spray_rt_ray* rays, const uint8_t* valid, size_t M,
+                             OocScratch& q, uint32_t* h_first);
+size_t ooc_temp_bytes(size_t M, size_t pairs);
+hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* tie, size_t M);
+hipError_t launch_ooc_ch(hipStream_t s, const OocDomain& D, const spray_rt_ray* rays,
+                         const uint32_t* idx, uint32_t n, spray_rt_hit* hits, uint64_t* tie);
+hipError_t launch_ooc_ah(hipStream_t s, const OocDomain& D, const spray_rt_ray* rays,
+                         const uint32_t* idx, uint32_t n, uint8_t* occ);
+hipError_t launch_ooc_clear_occ(hipStream_t s, const uint8_t* valid, uint8_t* occ, size_t M);
+
 }  // namespace spray_rt

@@ -15,7 +15,8 @@ import numpy as np
 from ._native import (HIT_DTYPE, INVALID_ID, RAY_DTYPE, RTC_ISECT_DTYPE,
                       SprayRtError, lib)
 
-__all__ = ["RtContext", "Scene", "camera_init", "make_rays", "host_parse_scene",
+__all__ = ["RtContext", "Scene", "OocCache", "ooc_scene", "camera_init", "make_rays",
+           "host_parse_scene",
            "host_domain_mesh", "RAY_DTYPE",
            "HIT_DTYPE", "RTC_ISECT_DTYPE", "INVALID_ID", "SprayRtError"]
 
@@ -323,6 +324,67 @@ class RtContext:
         e, k5 = _addr(d_count)
         self._check(lib().spray_rt_spawn_shadows_pt(self.h, a, b, int(n), shade.ctypes.data,
                                                     c, d, e), "spawn_shadows_pt")
+
+
+class OocCache:
+    """Out-of-core domains (spray_rt_ooc_*): every domain image in pinned host
+    memory, ``cache_slots`` of them resident in HBM at a time (LruCache)."""
+
+    def __init__(self, rt, cache_slots):
+        self.rt = rt
+        h = C.c_void_p()
+        rt._check(lib().spray_rt_ooc_create(rt.h, int(cache_slots), C.byref(h)), "ooc_create")
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().spray_rt_ooc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_domain(self, domain_id, verts, faces, colors=None, normals=None):
+        v = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
+        f = np.ascontiguousarray(faces, np.uint32).reshape(-1, 3)
+        c = None if colors is None else np.ascontiguousarray(colors, np.uint32)
+        n = None if normals is None else np.ascontiguousarray(normals, np.float32)
+        self.rt._check(lib().spray_rt_ooc_set_domain(
+            self.h, int(domain_id), v.ctypes.data, len(v), f.ctypes.data, len(f),
+            None if c is None else c.ctypes.data, None if n is None else n.ctypes.data),
+            "ooc_set_domain")
+
+    def intersect(self, rays, hits):
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        self.rt._check(lib().spray_rt_ooc_intersect(self.h, a, n, b), "ooc_intersect")
+
+    def occluded(self, rays, valid, occ):
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        b, k2 = _addr(valid)
+        c, k3 = _addr(occ)
+        self.rt._check(lib().spray_rt_ooc_occluded(self.h, a, n, b, c), "ooc_occluded")
+
+    def stats(self):
+        out = (C.c_ulonglong * 4)()
+        self.rt._check(lib().spray_rt_ooc_stats(self.h, out), "ooc_stats")
+        return {"loads": out[0], "hits": out[1], "bytes": out[2], "drains": out[3]}
+
+
+def ooc_scene(desc, ply_path, cache_slots, device=0):
+    """RtContext + OocCache over every domain of a scene file."""
+    rt = RtContext(device)
+    boxes, _ = host_parse_scene(desc, ply_path)
+    rt.domain_bounds(boxes)
+    oc = OocCache(rt, cache_slots)
+    for d in range(len(boxes)):
+        oc.set_domain(d, *host_domain_mesh(desc, ply_path, d))
+    return rt, oc
 
 
 class Scene:

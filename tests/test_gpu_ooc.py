@@ -1,0 +1,135 @@
+"""GPU parity of the out-of-core path (spray_rt_ooc_*: LRU cache of domain
+images streamed from pinned host memory, per-domain drain launches) against
+the whole-scene oracle, plus its cache accounting and the cross-domain tie
+rule (the earlier entry of the sorted domain list wins an equal t)."""
+import numpy as np
+import pytest
+import torch
+
+import insitu_helpers as H
+from conftest import SCENES, WAVELETS64, random_rays
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def spray():
+    import spray_amd
+    return spray_amd
+
+
+def batch(oracle):
+    cam = H.bench_camera(oracle)
+    org, d, _, _ = oracle.eye_rays_insitu(cam, H.IMG, H.SPP, H.TILE, H.TILE)
+    rng = np.random.default_rng(11)
+    o2, d2 = random_rays(rng, 6000, np.array([30, 29, 30], np.float32), 60.0)
+    # origins inside domain boxes: negative box entry t, several domains
+    o3 = rng.uniform([-10, -10, -10], [70, 68, 70], size=(3000, 3)).astype(np.float32)
+    d3 = rng.normal(size=(3000, 3)).astype(np.float32)
+    d3 /= np.linalg.norm(d3, axis=1, keepdims=True)
+    return (np.concatenate([org, o2, o3]).astype(np.float32),
+            np.concatenate([d, d2, d3]).astype(np.float32))
+
+
+@pytest.mark.parametrize("slots", [1, 4, 64])
+def test_ooc_matches_whole_scene(spray, oracle, slots):
+    org, d = batch(oracle)
+    sc, _, _ = oracle.load_scene(WAVELETS64, SCENES)
+    ref, _ = sc.intersect(org, d)
+    so, sd, src = oracle.spawn_shadows_pt(org, d, ref, H.SHADE[0:3], H.SHADE[3:6],
+                                          H.SHADE[6:9], H.SHADE[9])
+    ref_occ, _ = sc.occluded(so, sd)
+
+    rt, oc = spray.engine.ooc_scene(WAVELETS64, SCENES, slots)
+    rays = H.rays_tensor(org, d).cuda()
+    hits = torch.empty((len(org), 12), dtype=torch.float32, device="cuda")
+    oc.intersect(rays, hits)
+    rt.sync()
+    got = hits.cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1)
+    assert (got["domain"] >= 0).sum() > 5000
+    assert got.tobytes() == ref.tobytes()
+
+    # positional shadow batch: valid where a shadow ray was spawned
+    srays = torch.zeros((len(org), 8), dtype=torch.float32, device="cuda")
+    srays[torch.from_numpy(src).long().cuda()] = H.rays_tensor(so, sd).cuda()
+    valid = torch.zeros(len(org), dtype=torch.uint8, device="cuda")
+    valid[torch.from_numpy(src).long().cuda()] = 1
+    occ = torch.full((len(org),), 7, dtype=torch.uint8, device="cuda")
+    oc.occluded(srays, valid, occ)
+    rt.sync()
+    o = occ.cpu().numpy()
+    assert (o[src] == ref_occ).all()
+    untouched = np.ones(len(org), bool)
+    untouched[src] = False
+    assert (o[untouched] == 7).all()
+    st = oc.stats()
+    assert st["drains"] > 0 and st["bytes"] > 0
+    if slots == 64:
+        assert st["loads"] <= 64  # every domain uploaded at most once
+    else:
+        assert st["loads"] > 64 - slots  # streamed
+    oc.close()
+    rt.close()
+
+
+def test_ooc_lru_reuse_between_passes(spray, oracle):
+    """Closest hit drains ascending, any hit descending: the domains the
+    first pass left resident are cache hits of the second."""
+    org, d = batch(oracle)
+    rt, oc = spray.engine.ooc_scene(WAVELETS64, SCENES, 4)
+    rays = H.rays_tensor(org, d).cuda()
+    hits = torch.empty((len(org), 12), dtype=torch.float32, device="cuda")
+    oc.intersect(rays, hits)
+    a = oc.stats()
+    assert a["hits"] == 0 and a["loads"] == a["drains"]
+    occ = torch.empty(len(org), dtype=torch.uint8, device="cuda")
+    oc.occluded(rays, None, occ)
+    b = oc.stats()
+    assert b["hits"] - a["hits"] >= 3
+    rt.sync()
+    oc.close()
+    rt.close()
+
+
+def test_cross_domain_tie_goes_to_earlier_list_entry(spray, oracle):
+    """Two domains holding the same mesh (same box): every hit is an exact
+    t tie across domains; the sequential walk keeps domain 0 (equal box
+    entry t, smaller id) -- in the scene kernel, the keyed kernel and the
+    out-of-core merge alike."""
+    v, f, c = oracle.load_ply(SCENES + "/wavelet.ply")
+    n = np.zeros_like(v)
+    oracle.lib().or_compute_normals(oracle._p(v), len(v), oracle._p(f), len(f), oracle._p(n))
+    box = np.concatenate([v.min(0), v.max(0)]).astype(np.float32)
+    boxes = np.stack([box, box])
+    rng = np.random.default_rng(3)
+    org, d = random_rays(rng, 20000, (box[:3] + box[3:]) / 2, 25.0)
+    sc = oracle.Scene(2)
+    sc.set_domain(0, v, f, c, n, box)
+    sc.set_domain(1, v, f, c, n, box)
+    ref, _ = sc.intersect(org, d)
+    hit = ref["domain"] >= 0
+    assert hit.sum() > 1000 and (ref["domain"][hit] == 0).all()
+
+    rt = spray.RtContext(0)
+    rt.domain_bounds(boxes)
+    for k in range(2):
+        rt.upload_domain(k, v, f, c, n)
+        rt.map_domain(k, k)
+    rays = H.rays_tensor(org, d).cuda()
+    h1 = torch.empty((len(org), 12), dtype=torch.float32, device="cuda")
+    rt.intersect_scene(rays, h1)
+    h2 = torch.empty_like(h1)
+    keys = torch.empty(len(org), dtype=torch.int64, device="cuda")
+    rt.intersect_scene_keyed(rays, h2, keys)
+    oc = spray.OocCache(rt, 1)
+    for k in (1, 0):  # also set in reverse order
+        oc.set_domain(k, v, f, c, n)
+    h3 = torch.empty_like(h1)
+    oc.intersect(rays, h3)
+    rt.sync()
+    for h in (h1, h2, h3):
+        assert h.cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1).tobytes() == ref.tobytes()
+    k = keys.cpu().numpy()
+    assert ((k[hit] & 0xFFFF) == 0).all() and ((k[hit] >> 16 & 0xFFFF) == 0).all()
+    oc.close()
+    rt.close()
