@@ -19,7 +19,9 @@ steps.  Rank 0 prints one JSON line.
 With more than one rank (or --insitu 1) the line also carries "insitu":
 configs[2], the same frame traced with the domains sharded 64/N per GPU
 (Morton partition) and the rays moving to their domains' owners over RCCL
-all-to-all (spray_amd/insitu.py) -- strong scaling of one frame.
+all-to-all (spray_amd/insitu.py) -- strong scaling of one frame.  On one
+rank it carries "ooc": configs[3], the same frame with a 4-slot HBM cache of
+domain images streamed from pinned host memory (spray_rt_ooc_*).
 """
 from __future__ import annotations
 
@@ -142,6 +144,54 @@ def run_insitu(args, dist, world, rank, local, cam):
                                             world)}
 
 
+def run_ooc(args, rt_main, prim, n_prim, slots=4):
+    """configs[3]: the same frame with at most `slots` domains resident in HBM
+    (spray_rt_ooc_*): closest hit with the domains streamed through the LRU
+    cache in ascending order, PT shadow spawn (compacted), any hit with the
+    domains in descending order.  The H2D copies of the domain images are
+    inside the timed region."""
+    import torch
+    import spray_amd
+    dev = prim.device
+    rt, oc = spray_amd.ooc_scene(SCENE, SCENES, slots, device=dev.index or 0)
+    rt.set_stream(torch.cuda.current_stream(dev))
+    hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
+    shadow = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
+    src = torch.empty(n_prim, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    occ = torch.empty(n_prim, dtype=torch.uint8, device=dev)
+
+    def frame():
+        oc.intersect(prim, hits)
+        rt.spawn_shadows_pt(prim, hits, n_prim, SHADE, shadow, src, cnt)
+        ns = int(cnt.item())
+        oc.occluded(shadow[:ns * 32], None, occ[:ns])
+        return ns
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+    s0 = oc.stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ns = frame()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    s1 = oc.stats()
+    k = args.steps
+    out = {"value": round((n_prim + ns) * k / el / 1e6, 3), "unit": "Mrays/s",
+           "ms_per_step": round(el / k * 1e3, 4), "cache_slots": slots,
+           "loads_per_step": (s1["loads"] - s0["loads"]) / k,
+           "hits_per_step": (s1["hits"] - s0["hits"]) / k,
+           "h2d_MB_per_step": round((s1["bytes"] - s0["bytes"]) / k / 1e6, 2),
+           "rays_per_step": n_prim + ns,
+           "config": "configs[3]: 64 domains, %d-slot HBM LRU cache, images streamed from "
+                     "pinned host memory (H2D inside the timed region)" % slots}
+    oc.close()
+    rt.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +202,8 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--insitu", type=int, default=-1,
                     help="also measure configs[2] (default: when more than one rank)")
+    ap.add_argument("--ooc", type=int, default=-1,
+                    help="also measure configs[3] (default: on one rank)")
     args = ap.parse_args()
 
     import torch
@@ -280,6 +332,8 @@ def main():
                        "occluded_achieved_GBs": round(ah_gbs, 1)},
         "canonical_counts": gpu_counts,
     }
+    if args.ooc == 1 or (args.ooc < 0 and world == 1):
+        out["ooc"] = run_ooc(args, rt, prim, n_prim)
     if args.insitu == 1 or (args.insitu < 0 and world > 1):
         out["insitu"] = run_insitu(args, dist, world, rank, local, cam)
     if rank == 0 and world == 1 and args.cpu_baseline:
