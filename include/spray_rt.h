@@ -280,6 +280,16 @@ int spray_rt_spawn_shadows_pt(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                               const float shade[10], spray_rt_ray* out_rays,
                               int32_t* out_src, uint32_t* d_count);
 
+/* Ambient-occlusion rays of ooc::ShaderAo (src/ooc/ooc_shader_ao.h:
+ * 120-146): nsamples cosine-weighted hemisphere directions per hit, sample l
+ * of pixel p seeded by p * (l + 1) (pixid[i] = the ray's pixel), compacted
+ * into out_rays/out_src in (source ray, sample) order; *d_count = number
+ * written.  out_rays must hold M * nsamples rays.  Device buffers only. */
+int spray_rt_spawn_shadows_ao(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                              const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                              int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
+                              uint32_t* d_count);
+
 #ifdef __cplusplus
 }
 #endif

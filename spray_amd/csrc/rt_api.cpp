@@ -741,4 +741,26 @@ int spray_rt_spawn_shadows_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
   return SPRAY_RT_OK;
 }
 
+int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                              const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                              int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
+                              uint32_t* d_count) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (!d_count || nsamples <= 0 || nsamples > 1024)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad AO arguments");
+  if (M * size_t(nsamples) > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "too many rays");
+  if (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(pixid) ||
+            !is_device_ptr(out_rays) || !is_device_ptr(d_count)))
+    return fail(c, SPRAY_RT_ERR_ARG, "spawn buffers must be device memory");
+  HIPCHK(c, hipSetDevice(c->device));
+  size_t nb = (M + kBlock - 1) / kBlock + 1;
+  void* bc = c->d_block_counts;
+  int r = ensure(c, &bc, &c->block_cap, nb * sizeof(uint32_t));
+  if (r) return r;
+  c->d_block_counts = static_cast<uint32_t*>(bc);
+  HIPCHK(c, launch_spawn_ao(stream_of(c), rays, hits, pixid, M, nsamples, out_rays, out_src,
+                            d_count, c->d_block_counts));
+  return SPRAY_RT_OK;
+}
+
 }  // extern "C"

@@ -96,6 +96,13 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
                            int32_t* out_src, uint32_t* d_count,
                            uint32_t* block_counts);
 
+// Ambient-occlusion rays of ooc::ShaderAo, nsamples per hit, compacted in
+// (source ray, sample) order; block_counts as launch_spawn_pt.
+hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
+                           const int32_t* pixid, size_t M, int nsamples,
+                           spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
+                           uint32_t* block_counts);
+
 // ---- out-of-core path (ooc_kernels.hip) ----
 // One resident domain as its drain launch sees it.
 struct OocDomain {

@@ -688,6 +688,151 @@ __global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
   }
 }
 
+// ooc::ShaderAo (src/ooc/ooc_shader_ao.h:120-146): nsamples cosine-weighted
+// hemisphere directions per hit (DiffuseBsdf::sampleRandom, reflection.h:
+// 245-249; getCosineHemisphereSample, sampler.cc:54-60; ConcentricDisk-
+// Sampling, sampler.h:49-92; localToWorld, sampler.h:101-110), seeded by
+// pixid * (l + 1).  Sample l of hit i is emitted when its radiance weight
+// is positive.  Operation order as the oracle (glm); cosf/sinf are the
+// device's, so directions agree with the host to a few ulps.
+struct AoOut {
+  float o[3], w[3];
+  bool ok;
+};
+__device__ __forceinline__ float gdot3(const float* a, const float* b) {
+  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
+__device__ __forceinline__ void gnorm3(float* a) {
+  const float inv = 1.0f / sqrtf(gdot3(a, a));
+  a[0] *= inv;
+  a[1] *= inv;
+  a[2] *= inv;
+}
+__device__ __forceinline__ AoOut ao_sample(const spray_rt_ray& ray, const spray_rt_hit& h,
+                                           int32_t pixid, int l, int nsamples) {
+  AoOut r;
+  r.ok = false;
+  if (h.domain < 0) return r;
+  const float* o = ray.org;
+  const float* d = ray.dir;
+  r.o[0] = d[0] * h.t + o[0];
+  r.o[1] = d[1] * h.t + o[1];
+  r.o[2] = d[2] * h.t + o[2];
+  const float kd[3] = {float(double((h.color >> 16) & 0xffu) * 0.00392156862745098),
+                       float(double((h.color >> 8) & 0xffu) * 0.00392156862745098),
+                       float(double(h.color & 0xffu) * 0.00392156862745098)};
+  const float wo[3] = {-d[0], -d[1], -d[2]};
+  float N[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  if (!(gdot3(wo, N) > 0.0f)) {
+    N[0] = -N[0];
+    N[1] = -N[1];
+    N[2] = -N[2];
+  }
+  gnorm3(N);
+  const float ao_w = 1.0f / float(nsamples);
+  uint32_t st = mm_fin(mm_mix(0u, uint32_t(pixid * (l + 1))));
+  const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+  const float sx = 2 * u1 - 1, sy = 2 * u2 - 1;
+  float dx, dy;
+  if (sx == 0.0f && sy == 0.0f) {
+    dx = 0.0f;
+    dy = 0.0f;
+  } else {
+    float rr, th;
+    if (sx >= -sy) {
+      if (sx > sy) {
+        rr = sx;
+        th = sy > 0.0f ? sy / rr : 8.0f + sy / rr;
+      } else {
+        rr = sy;
+        th = 2.0f - sx / rr;
+      }
+    } else {
+      if (sx <= sy) {
+        rr = -sx;
+        th = 4.0f - sy / rr;
+      } else {
+        rr = -sy;
+        th = 6.0f + sx / rr;
+      }
+    }
+    th *= 3.14159265358979323846f / 4.f;
+    dx = rr * cosf(th);
+    dy = rr * sinf(th);
+  }
+  float lv[3] = {dx, dy, sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy))};
+  gnorm3(lv);
+  float dx0[3] = {0.f, N[2], -N[1]}, dx1[3] = {-N[2], 0.f, N[0]};
+  float ax[3];
+  const float* pick = gdot3(dx0, dx0) > gdot3(dx1, dx1) ? dx0 : dx1;
+  ax[0] = pick[0];
+  ax[1] = pick[1];
+  ax[2] = pick[2];
+  gnorm3(ax);
+  float ay[3] = {N[1] * ax[2] - ax[1] * N[2], N[2] * ax[0] - ax[2] * N[0],
+                 N[0] * ax[1] - ax[0] * N[1]};
+  gnorm3(ay);
+  r.w[0] = (ax[0] * lv[0] + ay[0] * lv[1]) + N[0] * lv[2];
+  r.w[1] = (ax[1] * lv[0] + ay[1] * lv[1]) + N[1] * lv[2];
+  r.w[2] = (ax[2] * lv[0] + ay[2] * lv[1]) + N[2] * lv[2];
+  gnorm3(r.w);
+  const float pdf = lv[2] * 0.3183098861837907f;
+  float ct = gdot3(N, r.w);
+  ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (kd[k] * (0.3183098861837907f * ct * ao_w / pdf) > 0.0f) r.ok = true;
+  return r;
+}
+
+__device__ __forceinline__ uint32_t ao_count(const spray_rt_ray* rays, const spray_rt_hit* hits,
+                                             const int32_t* pixid, size_t i, int ns) {
+  const spray_rt_hit h = hits[i];
+  if (h.domain < 0) return 0;
+  const spray_rt_ray r = rays[i];
+  uint32_t c = 0;
+  for (int l = 0; l < ns; ++l) c += ao_sample(r, h, pixid[i], l, ns).ok ? 1u : 0u;
+  return c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spawn_ao_count(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
+    const int32_t* __restrict__ pixid, size_t M, int ns, uint32_t* __restrict__ block_counts) {
+  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
+  __shared__ typename Scan::TempStorage tmp;
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const uint32_t c = i < M ? ao_count(rays, hits, pixid, i, ns) : 0u;
+  uint32_t ex, total;
+  Scan(tmp).ExclusiveSum(c, ex, total);
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spawn_ao_write(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
+    const int32_t* __restrict__ pixid, size_t M, int ns,
+    const uint32_t* __restrict__ block_offsets, spray_rt_ray* __restrict__ out,
+    int32_t* __restrict__ src) {
+  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
+  __shared__ typename Scan::TempStorage tmp;
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const uint32_t c = i < M ? ao_count(rays, hits, pixid, i, ns) : 0u;
+  uint32_t k, total;
+  Scan(tmp).ExclusiveSum(c, k, total);
+  if (!c) return;
+  k += block_offsets[blockIdx.x];
+  const spray_rt_hit h = hits[i];
+  const spray_rt_ray r = rays[i];
+  for (int l = 0; l < ns; ++l) {
+    const AoOut a = ao_sample(r, h, pixid[i], l, ns);
+    if (!a.ok) continue;
+    float4* op = reinterpret_cast<float4*>(out + k);
+    op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
+    op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
+    if (src) src[k] = int32_t(i);
+    ++k;
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -903,6 +1048,19 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
   k_spawn_pt_count<<<g, kBlock, 0, s>>>(rays, hits, M, sh, block_counts);
   k_scan_blocks<<<1, 1024, 0, s>>>(block_counts, g, d_count);
   k_spawn_pt_write<<<g, kBlock, 0, s>>>(rays, hits, M, sh, block_counts,
+                                        out_rays, out_src);
+  return hipGetLastError();
+}
+
+hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
+                           const int32_t* pixid, size_t M, int nsamples,
+                           spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
+                           uint32_t* block_counts) {
+  if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+  const unsigned g = grid_for(M);
+  k_spawn_ao_count<<<g, kBlock, 0, s>>>(rays, hits, pixid, M, nsamples, block_counts);
+  k_scan_blocks<<<1, 1024, 0, s>>>(block_counts, g, d_count);
+  k_spawn_ao_write<<<g, kBlock, 0, s>>>(rays, hits, pixid, M, nsamples, block_counts,
                                         out_rays, out_src);
   return hipGetLastError();
 }

@@ -314,6 +314,17 @@ class RtContext:
                                                 int(spp), tx, ty, tw, th, a, b, c),
                     "eye_rays_ooc")
 
+    def spawn_shadows_ao(self, rays, hits, pixid, n, nsamples, out_rays, out_src, d_count):
+        """ooc::ShaderAo rays (nsamples per hit), compacted (device)."""
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        p, k3 = _addr(pixid)
+        c, k4 = _addr(out_rays)
+        d, k5 = _addr(out_src)
+        e, k6 = _addr(d_count)
+        self._check(lib().spray_rt_spawn_shadows_ao(self.h, a, b, p, int(n), int(nsamples),
+                                                    c, d, e), "spawn_shadows_ao")
+
     def spawn_shadows_pt(self, rays, hits, n, shade, out_rays, out_src, d_count):
         shade = np.ascontiguousarray(shade, np.float32)
         assert shade.size == 10

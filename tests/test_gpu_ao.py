@@ -1,0 +1,56 @@
+"""GPU ambient-occlusion rays (ooc::ShaderAo, 16 per hit) against the oracle:
+same (source, sample) sequence and origins, directions within 1e-5 (device
+cosf/sinf vs libm), and any-hit of the device's rays bit-identical to the
+oracle's on the same rays."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import BENCH_CAMERA, SCENES, WAVELETS64
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ao16_spawn_and_occlusion(oracle):
+    import spray_amd
+    c = BENCH_CAMERA
+    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 1024, 1024)
+    tile = (384, 448, 128, 32)
+    org, d, pix, _ = oracle.eye_rays_ooc(cam, 1024, 2, tile)
+    sc, _, _ = oracle.load_scene(WAVELETS64, SCENES)
+    hits, _ = sc.intersect(org, d)
+    so, sd, src = oracle.spawn_shadows_ao(org, d, pix, hits, 16)
+    assert len(so) > 16 * 1000
+
+    scene = spray_amd.Scene(WAVELETS64, SCENES)
+    rt = scene.rt
+    n = len(org)
+    rays = torch.zeros((n, 8), dtype=torch.float32)
+    rays[:, 0:3] = torch.from_numpy(org)
+    rays[:, 3] = 0.001
+    rays[:, 4:7] = torch.from_numpy(d)
+    rays[:, 7] = float("inf")
+    rays = rays.cuda()
+    h = torch.empty((n, 12), dtype=torch.float32, device="cuda")
+    rt.intersect_scene(rays, h)
+    pixid = torch.from_numpy(pix).cuda()
+    out = torch.empty((n * 16, 8), dtype=torch.float32, device="cuda")
+    osrc = torch.empty(n * 16, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rt.spawn_shadows_ao(rays, h, pixid, n, 16, out, osrc, cnt)
+    rt.sync()
+    m = int(cnt.item())
+    assert h.cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1).tobytes() == hits.tobytes()
+    assert m == len(so)
+    assert (osrc[:m].cpu().numpy() == src).all()
+    g = out[:m].cpu().numpy()
+    assert g[:, 0:3].tobytes() == np.ascontiguousarray(so).tobytes()
+    assert np.abs(g[:, 4:7] - sd).max() < 1e-5
+    assert (g[:, 3] == np.float32(0.001)).all() and np.isinf(g[:, 7]).all()
+    occ = torch.empty(m, dtype=torch.uint8, device="cuda")
+    rt.occluded_scene(out[:m].contiguous(), occ)
+    rt.sync()
+    ref, _ = sc.occluded(np.ascontiguousarray(g[:, 0:3]), np.ascontiguousarray(g[:, 4:7]))
+    o = occ.cpu().numpy()
+    assert (o == ref).all() and 0 < o.sum() < m
+    scene.close()
