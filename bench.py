@@ -21,7 +21,9 @@ configs[2], the same frame traced with the domains sharded 64/N per GPU
 (Morton partition) and the rays moving to their domains' owners over RCCL
 all-to-all (spray_amd/insitu.py) -- strong scaling of one frame.  On one
 rank it carries "ooc": configs[3], the same frame with a 4-slot HBM cache of
-domain images streamed from pinned host memory (spray_rt_ooc_*).
+domain images streamed from pinned host memory (spray_rt_ooc_*).  "ao" is the
+configs[4] workload per GPU: primary rays + 16 ambient-occlusion rays per hit
+spawned on the device.
 """
 from __future__ import annotations
 
@@ -144,6 +146,47 @@ def run_insitu(args, dist, world, rank, local, cam):
                                             world)}
 
 
+def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
+    """configs[4] per GPU: closest hit of the frame, ooc::ShaderAo spawn of 16
+    rays per hit on the device, any hit of all of them (count stays on the
+    device).  Frame replicas across ranks, timed like the main line."""
+    import torch
+    dev = prim.device
+    hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
+    ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
+    src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
+
+    def frame():
+        rt.intersect_scene(prim, hits)
+        rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt)
+        rt.occluded_scene_devcount(ao, n_prim * nsamples, cnt, occ)
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    n_ao = int(cnt.item())
+    return {"value": round((n_prim + n_ao) * world * args.steps / el / 1e6, 3),
+            "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+            "scaling": "weak", "rays_per_step": n_prim + n_ao, "ao_rays": n_ao,
+            "config": "configs[4] workload per GPU: 64 domains resident, primary + "
+                      "AO-%d rays per hit (frame replicas x%d)" % (nsamples, world)}
+
+
 def run_ooc(args, rt_main, prim, n_prim, slots=4):
     """configs[3]: the same frame with at most `slots` domains resident in HBM
     (spray_rt_ooc_*): closest hit with the domains streamed through the LRU
@@ -204,6 +247,7 @@ def main():
                     help="also measure configs[2] (default: when more than one rank)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
+    ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
     args = ap.parse_args()
 
     import torch
@@ -229,8 +273,10 @@ def main():
     n_prim = W * H * SPP
     per_tile = W * TILE_H * SPP
     prim = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
+    pixid = torch.empty(n_prim, dtype=torch.int32, device=dev)
     for k, t in enumerate(tiles()):
-        rt.eye_rays_ooc(cam, W, SPP, t, prim[k * per_tile * 32:(k + 1) * per_tile * 32])
+        rt.eye_rays_ooc(cam, W, SPP, t, prim[k * per_tile * 32:(k + 1) * per_tile * 32],
+                        pixid[k * per_tile:(k + 1) * per_tile])
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
     shadow = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim, dtype=torch.int32, device=dev)
@@ -332,6 +378,8 @@ def main():
                        "occluded_achieved_GBs": round(ah_gbs, 1)},
         "canonical_counts": gpu_counts,
     }
+    if args.ao:
+        out["ao"] = run_ao(args, dist, world, rt, prim, pixid, n_prim)
     if args.ooc == 1 or (args.ooc < 0 and world == 1):
         out["ooc"] = run_ooc(args, rt, prim, n_prim)
     if args.insitu == 1 or (args.insitu < 0 and world > 1):
