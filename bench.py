@@ -158,6 +158,8 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
 
+    rt.set_coherence(rt.RAYS_INCOHERENT)  # hemisphere rays: one walk per lane
+
     def frame():
         rt.intersect_scene(prim, hits)
         rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt)
@@ -180,6 +182,7 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e.item())
     n_ao = int(cnt.item())
+    rt.set_coherence(rt.RAYS_ADAPTIVE)
     return {"value": round((n_prim + n_ao) * world * args.steps / el / 1e6, 3),
             "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
             "scaling": "weak", "rays_per_step": n_prim + n_ao, "ao_rays": n_ao,
@@ -305,6 +308,8 @@ def main():
             counts_src = "oracle fixture tests/golden/workload_counts.json (== gpu counting build)"
         else:
             counts_src = "gpu counting build (MISMATCH vs oracle fixture)"
+
+    rt.set_coherence(rt.RAYS_COHERENT)  # camera rays and point-light shadow rays
 
     def step(ev=None):
         # closest hit with the PT shadow spawn fused into its epilogue, then

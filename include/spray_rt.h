@@ -205,6 +205,18 @@ int spray_rt_occluded_scene_devcount(spray_rt_ctx_t ctx, const spray_rt_ray* ray
                                      uint8_t* occluded,
                                      unsigned long long* d_counters);
 
+/* ---- traversal form of the any-hit scene launches ---- */
+/* Closest-hit scene launches walk each domain tree as a wave-wide packet
+ * (one scalar fetch per node per wave).  Any-hit launches follow this
+ * setting: COHERENT = packets (camera / point-light shadow rays), INCOHERENT
+ * = one walk per lane (hemisphere-sampled AO rays), ADAPTIVE (default) =
+ * per wave, packets when every direction is within ~8 degrees of the
+ * wave's first.  Results are identical in every mode. */
+#define SPRAY_RT_RAYS_ADAPTIVE 0
+#define SPRAY_RT_RAYS_COHERENT 1
+#define SPRAY_RT_RAYS_INCOHERENT 2
+int spray_rt_set_coherence(spray_rt_ctx_t ctx, int mode);
+
 /* ---- in-situ (domain-sharded, one rank per GPU) ---- */
 /* Domain -> rank map of the partition (InsituPartition::rank,
  * src/render/data_partition.h:48-56): owner[ndomains] host array, ranks in

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
     const BvhNode* __restrict__ tlas, int ntlas, const spray_rt_ray* __restrict__ rays,
     const uint8_t* __restrict__ valid, size_t M, uint64_t* __restrict__ masks,
     uint32_t* __restrict__ npairs) {
-  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ int32_t wstack[(kBlock / 64) * kStack];
   __shared__ float4 stl[4 * 64 * W];
   for (int k = threadIdx.x; k < 4 * ntlas; k += kBlock) stl[k] = ld4(tlas, k);
   __syncthreads();
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
   for (int w = 0; w < W; ++w) m[w] = 0;
   if (!valid || valid[i]) {
     const float4* rp = reinterpret_cast<const float4*>(rays + i);
-    tlas_mask<W>(stl, ntlas, stack + threadIdx.x, rp[0], rp[1], m);
+    tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, rp[0], rp[1], m);
   }
   uint32_t n = 0;
 #pragma unroll

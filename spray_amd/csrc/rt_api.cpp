@@ -528,7 +528,7 @@ static SceneView view(const spray_rt_ctx* c) {
   for (const SlotHost& sh : c->slots)
     if (sh.dmem) depth = std::max(depth, sh.depth);
   return SceneView{c->d_slots, c->d_dom2slot, c->d_domtrav, c->d_boxes, c->ndom,
-                   c->d_tlas,  c->ntlas,      c->d_heads,   depth};
+                   c->d_tlas,  c->ntlas,      c->d_heads,   depth,        c->coherence};
 }
 
 // counters: optional device uint64[3] (nodes, tris, visits); exported for the
@@ -646,6 +646,15 @@ int spray_rt_intersect_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
 int spray_rt_occluded_scene(spray_rt_ctx_t c, const spray_rt_ray* rays,
                             size_t M, uint8_t* occluded) {
   return spray_rt_occluded_scene_counted(c, rays, M, occluded, nullptr);
+}
+
+int spray_rt_set_coherence(spray_rt_ctx_t c, int mode) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (mode != SPRAY_RT_RAYS_ADAPTIVE && mode != SPRAY_RT_RAYS_COHERENT &&
+      mode != SPRAY_RT_RAYS_INCOHERENT)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad coherence mode %d", mode);
+  c->coherence = mode;
+  return SPRAY_RT_OK;
 }
 
 int spray_rt_set_owners(spray_rt_ctx_t c, const int* owner) {

@@ -53,6 +53,7 @@ struct spray_rt_ctx {
   BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
   int ntlas = 0;
   int tlas_depth = 0;
+  int coherence = SPRAY_RT_RAYS_ADAPTIVE;
   std::vector<int> dom2slot;
   bool dom_dirty = true;
   // segment tables

@@ -39,6 +39,59 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Node / triangle fetch.  When every active lane of the wave fetches the same
+// record (coherent rays walking the same path), one scalar load brings it
+// through the scalar data cache and it is broadcast for free; otherwise each
+// lane loads its own 16-B pieces through the vector memory path (whose data
+// return is what the traversal saturates: TD ~80 % busy, profiles/).
+#ifndef SPRAY_SCALAR_UNIFORM
+#define SPRAY_SCALAR_UNIFORM 0
+#endif
+#define CAS __attribute__((address_space(4)))
+__device__ __forceinline__ bool wave_uniform_addr(const void* p, uint64_t& u) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+  u = (uint64_t(hi) << 32) | lo;
+  return __ballot(a != u) == 0;
+}
+__device__ __forceinline__ void ld_node(const void* nodes, size_t nb, float4& n0, float4& n1,
+                                        float4& n2, float4& n3) {
+  if (SPRAY_SCALAR_UNIFORM) {
+    uint64_t u;
+    if (wave_uniform_addr(static_cast<const float4*>(nodes) + nb, u)) {
+      const CAS v4f* q = reinterpret_cast<const CAS v4f*>(u);
+      const v4f x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+      n0 = make_float4(x0.x, x0.y, x0.z, x0.w);
+      n1 = make_float4(x1.x, x1.y, x1.z, x1.w);
+      n2 = make_float4(x2.x, x2.y, x2.z, x2.w);
+      n3 = make_float4(x3.x, x3.y, x3.z, x3.w);
+      return;
+    }
+  }
+  n0 = ld4(nodes, nb);
+  n1 = ld4(nodes, nb + 1);
+  n2 = ld4(nodes, nb + 2);
+  n3 = ld4(nodes, nb + 3);
+}
+__device__ __forceinline__ void ld_tri(const void* tris, uint32_t p, float4& a, float4& b,
+                                       float4& c) {
+  if (SPRAY_SCALAR_UNIFORM) {
+    uint64_t u;
+    if (wave_uniform_addr(static_cast<const float4*>(tris) + 3 * size_t(p), u)) {
+      const CAS v4f* q = reinterpret_cast<const CAS v4f*>(u);
+      const v4f x0 = q[0], x1 = q[1], x2 = q[2];
+      a = make_float4(x0.x, x0.y, x0.z, x0.w);
+      b = make_float4(x1.x, x1.y, x1.z, x1.w);
+      c = make_float4(x2.x, x2.y, x2.z, x2.w);
+      return;
+    }
+  }
+  a = ld4(tris, 3 * size_t(p));
+  b = ld4(tris, 3 * size_t(p) + 1);
+  c = ld4(tris, 3 * size_t(p) + 2);
+}
+
 // ---------------------------------------------------------------------------
 // ray / box / triangle primitives
 // ---------------------------------------------------------------------------
@@ -175,8 +228,8 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
   int32_t cur = 0;
   for (;;) {
     const size_t nb = 4 * size_t(cur);
-    const float4 n0 = ld4(nodes, nb), n1 = ld4(nodes, nb + 1), n2 = ld4(nodes, nb + 2),
-                 n3 = ld4(nodes, nb + 3);
+    float4 n0, n1, n2, n3;
+    ld_node(nodes, nb, n0, n1, n2, n3);
     if (COUNT) ++nnode;
     const float tcut = ANY ? tfar_any : best.t;
     float tl, tr;
@@ -204,8 +257,8 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
         const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
         for (uint32_t q = 0; q < cnt; ++q) {
           const uint32_t p = first + q;
-          const float4 a = ld4(tris, 3 * size_t(p)), b = ld4(tris, 3 * size_t(p) + 1),
-                       cc = ld4(tris, 3 * size_t(p) + 2);
+          float4 a, b, cc;
+          ld_tri(tris, p, a, b, cc);
           if (COUNT) ++ntri;
           float t, u, v;
           if (!tri_test(r, tnear, a, b, cc, t, u, v)) continue;
@@ -235,6 +288,87 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
     cur = next;
   }
   return false;
+}
+
+// Packet traversal of one domain tree by the whole wave.  The tree pointers
+// and the walk (current node, stack) are wave-uniform: nodes and triangles
+// come through scalar loads (one fetch per wave, broadcast), and a child is
+// visited when the exact-per-lane slab test of any participating lane (act)
+// accepts it, nearer side first by majority.  Each lane keeps its own
+// result with the same winner rule as trace_tree, and since a lane only
+// ever skips boxes its own conservative test rejected, the per-lane results
+// are those of the per-lane walk.  ANY: a lane that finds an occluder sets
+// hit and leaves the packet; the walk ends when no lane participates.
+// wstk: kStack entries of LDS per wave.
+template <bool ANY>
+__device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tris_u,
+                                                  uint64_t prims_u, const Ray& r,
+                                                  float tnear, float tfar_any, Best& best,
+                                                  bool& act, bool& hit, int32_t* wstk) {
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const CAS v4f* q = reinterpret_cast<const CAS v4f*>(nodes_u) + 4 * cur;
+    const v4f n0 = q[0], n1 = q[1], n2 = q[2], n3 = q[3];
+    const float tcut = ANY ? tfar_any : best.t;
+    float tl = 0.f, tr = 0.f;
+    const bool hl = act && slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tcut, tl);
+    const bool hr = act && slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tcut, tr);
+    const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(n3.x));
+    const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(n3.y));
+    const uint64_t bl = __ballot(hl), br = __ballot(hr);
+    const uint64_t vl = __ballot(hl && (!hr || tl <= tr));
+    const uint64_t vr = __ballot(hr && (!hl || tr < tl));
+    const bool lf = __popcll(vl) >= __popcll(vr);
+    int32_t next = kNone;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bool left = (k == 0) == lf;
+      const int32_t c = left ? cl : cr;
+      if (!(left ? bl : br)) continue;
+      if (c < 0) {
+        const bool h = left ? hl : hr;
+        const uint32_t enc = ~uint32_t(c);
+        const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
+        for (uint32_t qq = 0; qq < cnt; ++qq) {
+          const uint32_t p = first + qq;
+          const CAS v4f* tq = reinterpret_cast<const CAS v4f*>(tris_u) + 3 * size_t(p);
+          const v4f x0 = tq[0], x1 = tq[1], x2 = tq[2];
+          if (!h) continue;
+          float t, u, v;
+          if (!tri_test(r, tnear, make_float4(x0.x, x0.y, x0.z, x0.w),
+                        make_float4(x1.x, x1.y, x1.z, x1.w),
+                        make_float4(x2.x, x2.y, x2.z, x2.w), t, u, v))
+            continue;
+          if (ANY) {
+            if (t <= tfar_any) {
+              hit = true;
+              act = false;
+            }
+          } else {
+            const uint32_t pid = reinterpret_cast<const CAS uint32_t*>(prims_u)[p];
+            if (t < best.t || (t == best.t && pid < best.prim)) {
+              best.t = t;
+              best.prim = pid;
+              best.leaf = p;
+            }
+          }
+        }
+        if (ANY && __ballot(act) == 0) return;
+      } else if (next == kNone) {
+        next = c;
+      } else {
+        wstk[sp] = c;
+        ++sp;
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = __builtin_amdgcn_readfirstlane(wstk[sp]);
+    }
+    cur = next;
+  }
 }
 
 template <bool ANY, bool COUNT>
@@ -334,6 +468,65 @@ __device__ __forceinline__ void tlas_mask(const float4* stl, int ntlas, int32_t*
       if (sp == 0) break;
       --sp;
       next = stk[sp * kBlock];
+    }
+    cur = next;
+  }
+}
+
+// The same mask, traversed once per wave: every active lane evaluates the
+// exact test at each node the wave visits, and a child is visited when any
+// lane's test accepts it (ballot).  A lane that rejects a box rejects every
+// box inside it (monotone ops on exact unions), so each lane's bits are
+// exactly its own domain list.  Control flow and the stack (wstk, kStack
+// entries of LDS per wave) are wave-uniform: no per-lane stack traffic and
+// no divergence -- neighbouring rays share nearly all of their top-level
+// path.
+template <int W>
+__device__ __forceinline__ void tlas_mask_wave(const float4* stl, int ntlas, int32_t* wstk,
+                                               float4 o4, float4 d4, uint64_t* m) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  if (ntlas <= 0) return;
+  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const float4 a = stl[4 * cur], b = stl[4 * cur + 1], c = stl[4 * cur + 2],
+                 e = stl[4 * cur + 3];
+    const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(e.x));
+    const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(e.y));
+    float tm;
+    const bool hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
+    const bool hr = cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+    const bool al = __ballot(hl) != 0, ar = __ballot(hr) != 0;
+    int32_t next = kNone;
+    if (cl < 0) {
+      const int d = int(~uint32_t(cl) >> 2);
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        if (hl && w == (d >> 6)) m[w] |= 1ull << (d & 63);
+    } else if (al) {
+      next = cl;
+    }
+    if (cr < 0) {
+      if (cr != INT_MIN) {
+        const int d = int(~uint32_t(cr) >> 2);
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (hr && w == (d >> 6)) m[w] |= 1ull << (d & 63);
+      }
+    } else if (ar) {
+      if (next == kNone) {
+        next = cr;
+      } else {
+        wstk[sp] = cr;
+        ++sp;
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = __builtin_amdgcn_readfirstlane(wstk[sp]);
     }
     cur = next;
   }

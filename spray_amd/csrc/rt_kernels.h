@@ -35,6 +35,7 @@ struct SceneView {
   int ntlas;
   uint32_t* heads;  // kQueues*32 uint32 work-queue heads, zeroed by every launch
   int max_depth;    // max tree depth over resident slots and the top-level tree
+  int coherence;    // SPRAY_RT_RAYS_* of the any-hit launches
 };
 
 // counters (optional, device uint64[3]: nodes, tris, visits) select the

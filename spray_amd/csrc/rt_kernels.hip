@@ -215,7 +215,7 @@ __device__ __host__ __forceinline__ size_t band_size(size_t M) {
 template <int W, bool ANY, bool COUNT, int EPI>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                           const float4* stl, const float* sbox,
-                                          const float4* sdom, int32_t* stk,
+                                          const float4* sdom, int32_t* stk, int32_t* wstk,
                                           unsigned& nnode, unsigned& ntri,
                                           unsigned& nvisit, bool& spawn, float* pos,
                                           float* wi) {
@@ -231,13 +231,20 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
-    if (SPRAY_DIAG_MODE != 3) tlas_mask<W>(stl, ntlas, stk, o4, d4, m);
+    if (SPRAY_DIAG_MODE != 3) tlas_mask_wave<W>(stl, ntlas, wstk, o4, d4, m);
     if (SPRAY_DIAG_MODE == 1 || SPRAY_DIAG_MODE >= 3) {  // diagnostic: mask only
       uint32_t pc = 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) pc += __popcll(m[w]);
-      if (!ANY) hits[i].prim = pc;
-      else occ[i] = uint8_t(pc);
+      if (!ANY) {  // a whole 48-B record, as the real epilogue writes
+        float4* hp = reinterpret_cast<float4*>(hits + i);
+        const float4 h = make_float4(0.f, 0.f, 0.f, __uint_as_float(pc));
+        hp[0] = h;
+        hp[1] = h;
+        hp[2] = h;
+      } else {
+        occ[i] = uint8_t(pc);
+      }
       return;
     }
     // Closest hit keeps (t, prim, leaf) of the running winner in place.  A
@@ -370,6 +377,206 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   }
 }
 
+// A wave's rays are coherent when every direction is within ~8 degrees of
+// the first valid lane's (camera rays of neighbouring pixels, shadow rays
+// toward one point light); hemisphere-sampled AO rays are not, and walk
+// per lane.
+__device__ __forceinline__ bool wave_coherent(const SceneArgs& A, size_t i, bool valid) {
+  float dx = 0.f, dy = 0.f, dz = 0.f;
+  if (valid) {
+    const float4 d4 = reinterpret_cast<const float4*>(A.rays + i)[1];
+    dx = d4.x;
+    dy = d4.y;
+    dz = d4.z;
+  }
+  const uint64_t vb = __ballot(valid);
+  if (!vb) return true;
+  const int lead = __ffsll((long long)vb) - 1;
+  const float lx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), lead));
+  const float ly = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), lead));
+  const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), lead));
+  const float c = (dx * lx + dy * ly) + dz * lz;
+  return __ballot(valid && !(c >= 0.99f)) == 0;
+}
+
+// The fast (non-counting) form of scene_ray, run by the whole wave: rays of
+// lanes with valid == false only take part in the collective steps.  The
+// wave walks the union of its lanes' domain lists, one domain at a time --
+// the nearest remaining domain of the first lane that still has one -- and
+// traverses each domain tree as a packet (trace_tree_packet).  Lanes meet
+// their domains out of list order, so a lane's running hit is replaced by a
+// nearer t, or by an equal t of an earlier list entry (smaller (box entry
+// t, id)); that is exactly the sequential walk's result.
+template <int W, bool ANY, int EPI>
+__device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, bool valid,
+                                                 const float4* stl, const float* sbox,
+                                                 const float4* sdom, int32_t* wstk,
+                                                 bool& spawn, float* pos, float* wi) {
+  const SlotDesc* __restrict__ slots = A.slots;
+  const int* __restrict__ dom2slot = A.dom2slot;
+  const int lane = threadIdx.x & 63;
+  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+  if (valid) {
+    const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
+    o4 = rp[0];
+    d4 = rp[1];
+  }
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  uint64_t m[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, o4, d4, m);
+  uint64_t m0[EPI == kEpiKeys ? W : 1];
+  if (EPI == kEpiKeys) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) m0[w] = m[w];
+  }
+  Best best{ANY ? 0.f : d4.w, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  int best_dom = -1;
+  bool occluded = false;
+  for (;;) {
+    bool has = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) has |= m[w] != 0;
+    const uint64_t hb = __ballot(has);
+    if (!hb) break;
+    const int lead = __ffsll((long long)hb) - 1;
+    int sb = 0;
+    if (lane == lead) {  // the lead lane's nearest remaining domain
+      float dx = r.dx, dy = r.dy, dz = r.dz;
+      asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+      const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
+      float st = kInf;
+      sb = -1;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t bits = m[w];
+        while (bits) {
+          const int j = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          const int b = 64 * w + j;
+          float tm;
+          aabb_ref(sbox + 6 * b, dr, tm);
+          if (sb < 0 || tm < st) {
+            st = tm;
+            sb = b;
+          }
+        }
+      }
+    }
+    const int d = __builtin_amdgcn_readlane(sb, lead);
+    bool act = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (w == (d >> 6)) {
+        act = (m[w] >> (d & 63)) & 1ull;
+        m[w] &= ~(1ull << (d & 63));
+      }
+    if (ANY) act = act && !occluded;
+    if (!__ballot(act)) continue;
+    const float4 dt = sdom[d];
+    const uint32_t nlo = __builtin_amdgcn_readfirstlane(__float_as_uint(dt.x));
+    const uint32_t nhi = __builtin_amdgcn_readfirstlane(__float_as_uint(dt.y));
+    const uint64_t nodes = (uint64_t(nhi) << 32) | nlo;
+    if (!nodes) continue;  // not resident here (or empty)
+    const uint64_t tris = nodes + __builtin_amdgcn_readfirstlane(__float_as_uint(dt.z));
+    const uint64_t prims = nodes + __builtin_amdgcn_readfirstlane(__float_as_uint(dt.w));
+    if (ANY) {
+      bool hit = false;
+      trace_tree_packet<true>(nodes, tris, prims, r, o4.w, d4.w, best, act, hit, wstk);
+      if (hit) {
+        occluded = true;
+#pragma unroll
+        for (int w = 0; w < W; ++w) m[w] = 0;
+      }
+    } else {
+      Best loc{best_dom < 0 ? d4.w : best.t, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      bool hit = false;
+      trace_tree_packet<false>(nodes, tris, prims, r, o4.w, 0.f, loc, act, hit, wstk);
+      if (loc.leaf != 0xFFFFFFFFu) {
+        bool take = best_dom < 0 || loc.t < best.t;
+        if (!take && loc.t == best.t) {  // exact tie: the earlier list entry
+          const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+          float tmd, tme;
+          aabb_ref(sbox + 6 * d, dr, tmd);
+          aabb_ref(sbox + 6 * best_dom, dr, tme);
+          take = tmd < tme || (tmd == tme && d < best_dom);
+        }
+        if (take) {
+          best = loc;
+          best_dom = d;
+        }
+      }
+    }
+  }
+  if (!valid) return;
+  if (ANY) {
+    A.occ[i] = occluded ? 1 : 0;
+    return;
+  }
+  float4 h0, h1, h2;
+  if (best_dom < 0) {
+    h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+    h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    h2 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  } else {
+    const SlotDesc s = slots[dom2slot[best_dom]];
+    float hu, hv;
+    const float4 c = hit_uv(s, r, o4.w, best.leaf, hu, hv);
+    uint32_t color;
+    float nsx, nsy, nsz;
+    epilogue(s, best.prim, hu, hv, color, nsx, nsy, nsz);
+    h0 = make_float4(best.t, hu, hv, __uint_as_float(best.prim));
+    h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
+    h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
+  }
+  float4* hp = reinterpret_cast<float4*>(A.hits + i);
+  hp[0] = h0;
+  hp[1] = h1;
+  hp[2] = h2;
+  if (EPI == kEpiKeys) {
+    uint64_t key = 0x7FFFFFFFFFFFFFFFull;
+    if (best_dom >= 0) {  // position of best_dom in the ray's sorted list
+      const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+      float tb;
+      aabb_ref(sbox + 6 * best_dom, dr, tb);
+      uint32_t p = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t bits = m0[w];
+        while (bits) {
+          const int j = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          const int b = 64 * w + j;
+          float tm;
+          aabb_ref(sbox + 6 * b, dr, tm);
+          if (tm < tb || (tm == tb && b < best_dom)) ++p;
+        }
+      }
+      key = (uint64_t(__float_as_uint(best.t)) << 32) | (uint64_t(p) << 16) |
+            uint64_t(best_dom);
+    }
+    A.keys[i] = key;
+  }
+  if (EPI == kEpiSpawn && best_dom >= 0) {
+    spray_rt_hit h;
+    h.t = h0.x;
+    h.color = __float_as_uint(h1.w);
+    h.ns[0] = h2.x;
+    h.ns[1] = h2.y;
+    h.ns[2] = h2.z;
+    h.domain = best_dom;
+    spray_rt_ray ray;
+    ray.org[0] = o4.x;
+    ray.org[1] = o4.y;
+    ray.org[2] = o4.z;
+    ray.dir[0] = d4.x;
+    ray.dir[1] = d4.y;
+    ray.dir[2] = d4.z;
+    spawn = shadow_pt(ray, h, A.shade, pos, wi);
+  }
+}
+
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
@@ -408,13 +615,22 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
 // slot tree and of the top-level tree (a node at depth k has at most k
 // pending siblings).  LDS = STK KiB + 4 KiB per 64 domains, so STK 16 lets 8
 // blocks (32 waves) share a CU where 24 allowed 5.
-template <int W, bool ANY, bool COUNT, int EPI, int STK>
+// TRAV: 0 per-lane walk, 1 packet walk, 2 packet walk for coherent waves
+// and per-lane for the others (any-hit only; the counting variants always
+// walk per lane, the canonical order the counts are defined on).
+template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void k_scene(
     SceneArgs A) {
-  __shared__ int32_t stack[STK * kBlock];
+  // packet form for the non-counting kernels; any-hit waves fall back to
+  // the per-lane walk when their rays are not coherent (AO hemispheres)
+  constexpr bool kPacket = TRAV != 0 && !COUNT && SPRAY_DIAG_MODE == 0;
+  constexpr bool kAdaptive = kPacket && TRAV == 2;
+  constexpr bool kLaneStack = !kPacket || kAdaptive;
+  __shared__ int32_t stack[(kLaneStack ? STK : 1) * kBlock];
   __shared__ float4 stl[4 * 64 * W];   // top-level tree
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
+  __shared__ int32_t wstack[(kBlock / 64) * kStack];  // top-level stacks, one per wave
   size_t M = A.M;
   if (A.d_count) {  // ray count produced on the device
     const size_t dc = *A.d_count;
@@ -427,6 +643,7 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
   __syncthreads();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
   int32_t* stk = stack + threadIdx.x;
+  int32_t* wstk = wstack + (threadIdx.x >> 6) * kStack;
   bool flag = false;
   float pos[3], wi[3];
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
@@ -435,9 +652,11 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
   if (!kPersist) {
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
-    if (j < M)
-      scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, nnode, ntri, nvisit,
-                                      flag, pos, wi);
+    if (kPacket && (!kAdaptive || wave_coherent(A, i, j < M)))
+      scene_ray_packet<W, ANY, EPI>(A, i, j < M, stl, sbox, sdom, wstk, flag, pos, wi);
+    else if (j < M)
+      scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
+                                      nvisit, flag, pos, wi);
     if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
@@ -465,9 +684,12 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
           const size_t j = begin + base + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
           flag = false;
-          if (j < end)
-            scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, nnode, ntri,
-                                            nvisit, flag, pos, wi);
+          if (kPacket && (!kAdaptive || wave_coherent(A, i, j < end)))
+            scene_ray_packet<W, ANY, EPI>(A, i, j < end, stl, sbox, sdom, wstk, flag, pos,
+                                          wi);
+          else if (j < end)
+            scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode,
+                                            ntri, nvisit, flag, pos, wi);
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
         }
         base = __builtin_amdgcn_readfirstlane(next);
@@ -489,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
                                                   int ntlas, const int* __restrict__ owner,
                                                   int ndom, const spray_rt_ray* __restrict__ rays,
                                                   size_t M, uint64_t* __restrict__ out) {
-  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ int32_t wstack[(kBlock / 64) * kStack];
   __shared__ float4 stl[4 * 64 * W];
   __shared__ int sown[64 * W];
   for (int k = threadIdx.x; k < 4 * ntlas; k += kBlock) stl[k] = ld4(tlas, k);
@@ -500,7 +722,7 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
   const float4* rp = reinterpret_cast<const float4*>(rays + i);
   const float4 o4 = rp[0], d4 = rp[1];
   uint64_t m[W];
-  tlas_mask<W>(stl, ntlas, stack + threadIdx.x, o4, d4, m);
+  tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, o4, d4, m);
   uint64_t ranks = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) {
@@ -865,7 +1087,7 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
   return hipGetLastError();
 }
 
-template <int W, bool ANY, bool COUNT, int EPI, int STK>
+template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
@@ -876,7 +1098,7 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
       e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, k_scene<W, ANY, COUNT, EPI, STK>, kBlock, 0);
+          &per_cu, k_scene<W, ANY, COUNT, EPI, STK, TRAV>, kBlock, 0);
     if (e != hipSuccess) return e;
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
@@ -886,24 +1108,34 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
-  k_scene<W, ANY, COUNT, EPI, STK><<<g, kBlock, 0, s>>>(a);
+  k_scene<W, ANY, COUNT, EPI, STK, TRAV><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
+// counting variants walk per lane; closest hit walks packets; any hit
+// follows the context's ray-coherence setting
 template <int W, bool ANY, int EPI, int STK>
-static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a) {
-  return a.counters ? launch_scene_t<W, ANY, true, EPI, STK>(s, a)
-                    : launch_scene_t<W, ANY, false, EPI, STK>(s, a);
+static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherence) {
+  if (a.counters) return launch_scene_t<W, ANY, true, EPI, STK, 0>(s, a);
+  if (!ANY) return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
+  switch (coherence) {
+    case SPRAY_RT_RAYS_COHERENT:
+      return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
+    case SPRAY_RT_RAYS_INCOHERENT:
+      return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
+    default:
+      return launch_scene_t<W, ANY, false, EPI, STK, 2>(s, a);
+  }
 }
 
 template <bool ANY, int EPI>
-static hipError_t launch_scene_w(hipStream_t s, const SceneArgs& a, int max_depth) {
-  if (max_depth > kStack) return hipErrorInvalidValue;
+static hipError_t launch_scene_w(hipStream_t s, const SceneArgs& a, const SceneView& v) {
+  if (v.max_depth > kStack) return hipErrorInvalidValue;
   if (a.ndom <= 64)
-    return max_depth <= 16 ? launch_scene_c<1, ANY, EPI, 16>(s, a)
-                           : launch_scene_c<1, ANY, EPI, kStack>(s, a);
-  return max_depth <= 16 ? launch_scene_c<4, ANY, EPI, 16>(s, a)
-                         : launch_scene_c<4, ANY, EPI, kStack>(s, a);
+    return v.max_depth <= 16 ? launch_scene_c<1, ANY, EPI, 16>(s, a, v.coherence)
+                             : launch_scene_c<1, ANY, EPI, kStack>(s, a, v.coherence);
+  return v.max_depth <= 16 ? launch_scene_c<4, ANY, EPI, 16>(s, a, v.coherence)
+                           : launch_scene_c<4, ANY, EPI, kStack>(s, a, v.coherence);
 }
 
 static SceneArgs scene_args(const SceneView& v, const spray_rt_ray* rays, size_t M) {
@@ -928,7 +1160,7 @@ hipError_t launch_scene_intersect(hipStream_t s, const SceneView& v,
   SceneArgs a = scene_args(v, rays, M);
   a.hits = hits;
   a.counters = counters;
-  return launch_scene_w<false, kEpiNone>(s, a, v.max_depth);
+  return launch_scene_w<false, kEpiNone>(s, a, v);
 }
 
 hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
@@ -940,7 +1172,7 @@ hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
   a.d_count = d_count;
   a.occ = occluded;
   a.counters = counters;
-  return launch_scene_w<true, kEpiNone>(s, a, v.max_depth);
+  return launch_scene_w<true, kEpiNone>(s, a, v);
 }
 
 hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
@@ -962,7 +1194,7 @@ hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
   a.d_count = d_num;
   a.occ = occluded;
   a.counters = counters;
-  return launch_scene_w<true, kEpiNone>(s, a, v.max_depth);
+  return launch_scene_w<true, kEpiNone>(s, a, v);
 }
 
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
@@ -982,7 +1214,7 @@ hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
   a.sh_out = out_rays;
   a.sh_valid = out_valid;
   a.sh_count = d_count;
-  return launch_scene_w<false, kEpiSpawn>(s, a, v.max_depth);
+  return launch_scene_w<false, kEpiSpawn>(s, a, v);
 }
 
 hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
@@ -992,7 +1224,7 @@ hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
   SceneArgs a = scene_args(v, rays, M);
   a.hits = hits;
   a.keys = keys;
-  return launch_scene_w<false, kEpiKeys>(s, a, v.max_depth);
+  return launch_scene_w<false, kEpiKeys>(s, a, v);
 }
 
 hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,

@@ -143,6 +143,12 @@ class RtContext:
     def sync(self):
         self._check(lib().spray_rt_sync(self.h), "sync")
 
+    RAYS_ADAPTIVE, RAYS_COHERENT, RAYS_INCOHERENT = 0, 1, 2
+
+    def set_coherence(self, mode):
+        """Traversal form of the any-hit launches (results are identical)."""
+        self._check(lib().spray_rt_set_coherence(self.h, int(mode)), "set_coherence")
+
     # ---- domains ----
     def upload_domain(self, slot, verts, faces, colors=None, normals=None, async_=False):
         v = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)

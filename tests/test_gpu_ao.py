@@ -47,10 +47,13 @@ def test_ao16_spawn_and_occlusion(oracle):
     assert g[:, 0:3].tobytes() == np.ascontiguousarray(so).tobytes()
     assert np.abs(g[:, 4:7] - sd).max() < 1e-5
     assert (g[:, 3] == np.float32(0.001)).all() and np.isinf(g[:, 7]).all()
-    occ = torch.empty(m, dtype=torch.uint8, device="cuda")
-    rt.occluded_scene(out[:m].contiguous(), occ)
-    rt.sync()
     ref, _ = sc.occluded(np.ascontiguousarray(g[:, 0:3]), np.ascontiguousarray(g[:, 4:7]))
-    o = occ.cpu().numpy()
-    assert (o == ref).all() and 0 < o.sum() < m
+    # every traversal form (packet, per lane, per-wave choice) gives the same bits
+    for mode in (rt.RAYS_ADAPTIVE, rt.RAYS_COHERENT, rt.RAYS_INCOHERENT):
+        rt.set_coherence(mode)
+        occ = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+        rt.occluded_scene(out[:m].contiguous(), occ)
+        rt.sync()
+        o = occ.cpu().numpy()
+        assert (o == ref).all() and 0 < o.sum() < m
     scene.close()
