@@ -39,7 +39,8 @@ namespace {
 #define SPRAY_PERSIST_AH 0
 #endif
 
-// Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): 3 = ray in, 4 B out
+// Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): packet form: 5 = no
+// tree walks, 6 = top-level mask only; per-lane form: 3 = ray in, record out
 // (no domain tree), 1 = domain mask
 // only, 2 = mask + ordered domain selection, no BVH traversal.
 // Minimum resident waves per SIMD the register allocator must allow (the
@@ -435,6 +436,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   int best_dom = -1;
   bool occluded = false;
   for (;;) {
+    if (SPRAY_DIAG_MODE == 6) break;  // diagnostic: top-level mask only
     bool has = false;
 #pragma unroll
     for (int w = 0; w < W; ++w) has |= m[w] != 0;
@@ -442,10 +444,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     if (!hb) break;
     const int lead = __ffsll((long long)hb) - 1;
     int sb = 0;
-    if (lane == lead) {  // the lead lane's nearest remaining domain
-      float dx = r.dx, dy = r.dy, dz = r.dz;
-      asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
-      const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
+    if (lane == lead) {
+      // the lead lane's nearest remaining domain by the fast slab entry
+      // distance: the order only steers culling, the merge below is exact
       float st = kInf;
       sb = -1;
 #pragma unroll
@@ -455,8 +456,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
           const int j = __ffsll((long long)bits) - 1;
           bits &= bits - 1;
           const int b = 64 * w + j;
+          const float* bx = sbox + 6 * b;
           float tm;
-          aabb_ref(sbox + 6 * b, dr, tm);
+          slab(r, bx[0], bx[1], bx[2], bx[3], bx[4], bx[5], -kInf, kInf, tm);
           if (sb < 0 || tm < st) {
             st = tm;
             sb = b;
@@ -481,6 +483,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     if (!nodes) continue;  // not resident here (or empty)
     const uint64_t tris = nodes + __builtin_amdgcn_readfirstlane(__float_as_uint(dt.z));
     const uint64_t prims = nodes + __builtin_amdgcn_readfirstlane(__float_as_uint(dt.w));
+    if (SPRAY_DIAG_MODE == 5) continue;  // diagnostic: no tree walks
     if (ANY) {
       bool hit = false;
       trace_tree_packet<true>(nodes, tris, prims, r, o4.w, d4.w, best, act, hit, wstk);
@@ -623,7 +626,8 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
     SceneArgs A) {
   // packet form for the non-counting kernels; any-hit waves fall back to
   // the per-lane walk when their rays are not coherent (AO hemispheres)
-  constexpr bool kPacket = TRAV != 0 && !COUNT && SPRAY_DIAG_MODE == 0;
+  constexpr bool kPacket =
+      TRAV != 0 && !COUNT && (SPRAY_DIAG_MODE == 0 || SPRAY_DIAG_MODE >= 5);
   constexpr bool kAdaptive = kPacket && TRAV == 2;
   constexpr bool kLaneStack = !kPacket || kAdaptive;
   __shared__ int32_t stack[(kLaneStack ? STK : 1) * kBlock];
