@@ -25,6 +25,12 @@ using namespace spray_rt;
 
 using namespace spray_rt::detail;
 
+// Masked any hit: 0 = traced in place under the mask, 1 = compacted first
+// into an ascending index list (hipCUB select) -- diagnostic builds compare.
+#ifndef SPRAY_MASKED_SELECT
+#define SPRAY_MASKED_SELECT 1
+#endif
+
 namespace spray_rt {
 namespace detail {
 
@@ -625,6 +631,10 @@ int spray_rt_occluded_scene_masked(spray_rt_ctx_t c, const spray_rt_ray* rays,
   if (!valid || !is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(valid))
     return fail(c, SPRAY_RT_ERR_ARG, "masked occlusion needs device buffers");
   hipStream_t s = stream_of(c);
+  if (!SPRAY_MASKED_SELECT) {
+    HIPCHK(c, launch_scene_occluded_masked(s, view(c), rays, M, valid, occ));
+    return SPRAY_RT_OK;
+  }
   size_t temp = 0;
   HIPCHK(c, launch_select_flagged(s, valid, M, nullptr, nullptr, nullptr, &temp));
   const size_t b_idx = align256(M * sizeof(uint32_t));

@@ -49,11 +49,16 @@ hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
                                  const uint32_t* d_count, uint8_t* occluded,
                                  unsigned long long* counters);
 
-// idx_out[0..*d_num) = ascending i with flags[i] != 0 (hipCUB select;
-// temp == nullptr: *temp_bytes <- required scratch size).
+// idx_out[0..*d_num) = ascending i with flags[i] != 0 (tile count, scan,
+// ordered write; temp == nullptr: *temp_bytes <- required scratch size).
 hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
                                  uint32_t* idx_out, uint32_t* d_num, void* temp,
                                  size_t* temp_bytes);
+// Any hit over the rays i < M with valid[i] != 0, in place (no compaction:
+// a packet wave walks the union of its valid lanes' paths).
+hipError_t launch_scene_occluded_masked(hipStream_t s, const SceneView& v,
+                                       const spray_rt_ray* rays, size_t M,
+                                       const uint8_t* valid, uint8_t* occluded);
 // Any hit over rays idx[0..*d_num) (d_num <= max_n), occluded[idx[j]] written.
 hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
                                         const spray_rt_ray* rays, size_t max_n,

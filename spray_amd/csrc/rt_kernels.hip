@@ -8,9 +8,8 @@
 // other kernel here -- VBuf compares t with == (ooc_vbuf.cc:41-52).
 #include <hip/hip_runtime.h>
 
+#include <hipcub/block/block_reduce.hpp>
 #include <hipcub/block/block_scan.hpp>
-#include <hipcub/device/device_select.hpp>
-#include <hipcub/iterator/counting_input_iterator.hpp>
 
 #include <climits>
 #include <cstdint>
@@ -199,6 +198,9 @@ struct SceneArgs {
   const uint32_t* idx;
   // kEpiKeys: composite key per ray
   uint64_t* keys;
+  // positional mask: only rays with valid[i] != 0 are traced (occ / hits of
+  // the others untouched)
+  const uint8_t* valid;
 };
 
 // Closest-hit epilogue variants of the scene kernels.
@@ -656,9 +658,10 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
   if (!kPersist) {
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
-    if (kPacket && (!kAdaptive || wave_coherent(A, i, j < M)))
-      scene_ray_packet<W, ANY, EPI>(A, i, j < M, stl, sbox, sdom, wstk, flag, pos, wi);
-    else if (j < M)
+    const bool ok = j < M && (!A.valid || A.valid[i]);
+    if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
+      scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+    else if (ok)
       scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
     if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
@@ -687,11 +690,11 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
         for (uint32_t c = 0; c < kChunk; c += 64) {
           const size_t j = begin + base + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
+          const bool ok = j < end && (!A.valid || A.valid[i]);
           flag = false;
-          if (kPacket && (!kAdaptive || wave_coherent(A, i, j < end)))
-            scene_ray_packet<W, ANY, EPI>(A, i, j < end, stl, sbox, sdom, wstk, flag, pos,
-                                          wi);
-          else if (j < end)
+          if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
+            scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+          else if (ok)
             scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
@@ -894,6 +897,62 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ c,
     __syncthreads();
   }
   if (threadIdx.x == 0) *d_count = run;
+}
+
+// Ordered selection of the flagged positions (the masked any hit's index
+// list): tiles of kSelTile flags, 16 per thread through one 16-B load;
+// count -> scan of the tile counts -> ordered write.
+constexpr int kSelPer = 16;
+constexpr int kSelTile = kBlock * kSelPer;
+
+__device__ __forceinline__ uint32_t flags16(const uint8_t* f, size_t M, size_t base,
+                                            uint32_t& mask) {
+  // bit k of mask = flags[base + k] != 0
+  mask = 0;
+  if (base + kSelPer <= M && (reinterpret_cast<uintptr_t>(f + base) & 15) == 0) {
+    const uint4 v = *reinterpret_cast<const uint4*>(f + base);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((w[q] >> (8 * b)) & 0xffu) mask |= 1u << (4 * q + b);
+  } else {
+    for (int k = 0; k < kSelPer; ++k)
+      if (base + k < M && f[base + k]) mask |= 1u << k;
+  }
+  return __popc(mask);
+}
+
+__global__ __launch_bounds__(kBlock) void k_select_count(const uint8_t* __restrict__ f,
+                                                         size_t M,
+                                                         uint32_t* __restrict__ tile_counts) {
+  using Reduce = hipcub::BlockReduce<uint32_t, kBlock>;
+  __shared__ typename Reduce::TempStorage tmp;
+  uint32_t mask;
+  const size_t base = size_t(blockIdx.x) * kSelTile + size_t(threadIdx.x) * kSelPer;
+  const uint32_t c = base < M ? flags16(f, M, base, mask) : 0u;
+  const uint32_t total = Reduce(tmp).Sum(c);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_select_write(const uint8_t* __restrict__ f,
+                                                         size_t M,
+                                                         const uint32_t* __restrict__ tile_off,
+                                                         uint32_t* __restrict__ out) {
+  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
+  __shared__ typename Scan::TempStorage tmp;
+  uint32_t mask = 0;
+  const size_t base = size_t(blockIdx.x) * kSelTile + size_t(threadIdx.x) * kSelPer;
+  const uint32_t c = base < M ? flags16(f, M, base, mask) : 0u;
+  uint32_t k, total;
+  Scan(tmp).ExclusiveSum(c, k, total);
+  k += tile_off[blockIdx.x];
+  while (mask) {
+    const int b = __ffs(mask) - 1;
+    mask &= mask - 1;
+    out[k++] = uint32_t(base + b);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
@@ -1182,9 +1241,27 @@ hipError_t launch_scene_occluded(hipStream_t s, const SceneView& v,
 hipError_t launch_select_flagged(hipStream_t s, const uint8_t* flags, size_t M,
                                  uint32_t* idx_out, uint32_t* d_num, void* temp,
                                  size_t* temp_bytes) {
-  return hipcub::DeviceSelect::Flagged(temp, *temp_bytes,
-                                       hipcub::CountingInputIterator<uint32_t>(0u),
-                                       flags, idx_out, d_num, int(M), s);
+  const size_t tiles = (M + kSelTile - 1) / kSelTile;
+  if (!temp) {
+    *temp_bytes = (tiles + 1) * sizeof(uint32_t);
+    return hipSuccess;
+  }
+  if (M == 0) return hipMemsetAsync(d_num, 0, sizeof(uint32_t), s);
+  uint32_t* tc = static_cast<uint32_t*>(temp);
+  k_select_count<<<unsigned(tiles), kBlock, 0, s>>>(flags, M, tc);
+  k_scan_blocks<<<1, 1024, 0, s>>>(tc, uint32_t(tiles), d_num);
+  k_select_write<<<unsigned(tiles), kBlock, 0, s>>>(flags, M, tc, idx_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_scene_occluded_masked(hipStream_t s, const SceneView& v,
+                                       const spray_rt_ray* rays, size_t M,
+                                       const uint8_t* valid, uint8_t* occluded) {
+  if (M == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.valid = valid;
+  a.occ = occluded;
+  return launch_scene_w<true, kEpiNone>(s, a, v);
 }
 
 hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
