@@ -15,8 +15,8 @@ step() {  # name, timeout, cmd...
 step pytest_gpu 900 python -m pytest tests -m gpu -q -rA
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
-step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0
-step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0
-step prof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0
-step prof_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2" -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0
+step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0
+step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --ao 0 --ooc 0
+step prof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --ao 0 --ooc 0
+step prof_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2" -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --ao 0 --ooc 0
 echo done

@@ -26,11 +26,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
+    name = name.replace("spray_rt::(anonymous namespace)::", "").replace("void ", "")
     if "k_scene<" in name:
-        t = name[name.index("k_scene<"):name.index(">") + 1]
-        return t
-    n = name.split("(")[0]
-    return n.replace("void ", "").replace("spray_rt::(anonymous namespace)::", "")[:60]
+        return name[name.index("k_scene<"):name.index(">") + 1]
+    return name.split("(")[0][:60]
 
 
 def pmc(path):
@@ -52,10 +51,10 @@ def main(src, tag):
     write = pmc(os.path.join(src, "pmc_write"))
     l2 = pmc(os.path.join(src, "pmc_l2"))
     lines = ["# rocprofv3 summary, %s" % tag, "",
-             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 "
-             "--warmup 2 --cpu-baseline 0` (trace), and separate `--pmc FETCH_SIZE`, "
+             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 20 "
+             "--warmup 3 --cpu-baseline 0` (trace), and separate `--pmc FETCH_SIZE`, "
              "`--pmc WRITE_SIZE`, `--pmc TCC_HIT_sum TCC_MISS_sum` passes of "
-             "`bench.py --steps 3 --warmup 1` (scripts/gpu_profile.sh).", "",
+             "`bench.py --steps 3 --warmup 1 --cpu-baseline 0 --ao 0 --ooc 0` (scripts/gpu_profile.sh).", "",
              "| kernel | calls | avg us | FETCH_SIZE KiB | read bytes (x2 corr.) | "
              "WRITE_SIZE KiB | L2 hit |", "|---|---|---|---|---|---|---|"]
     traffic = {}
@@ -75,7 +74,7 @@ def main(src, tag):
                           "bytes_lower": fs * 1024 + ws * 1024,
                           "bytes_corrected": 2 * fs * 1024 + ws * 1024,
                           "avg_us": float(r["AverageNs"]) / 1e3}
-    ch = [v for k, v in traffic.items() if k.startswith("k_scene<1, false, false, true>")]
+    ch = [v for k, v in traffic.items() if k.startswith("k_scene<1, false, false, 1,")]
     out = {"source": src, "round": tag, "per_kernel": traffic}
     if ch:
         out["scene_intersect_bytes_per_launch"] = ch[0]["bytes_corrected"]

@@ -105,28 +105,39 @@ __global__ __launch_bounds__(kBlock) void k_ooc_init(spray_rt_hit* __restrict__ 
 // Closest hit of the rays queued to one resident domain, merged into the
 // running result of each ray: nearer t wins; an equal t goes to the earlier
 // entry of the ray's domain list (smaller (box entry t, id)).
+// The queue of one domain holds its rays in ascending ray order --
+// neighbouring pixels -- so each wave walks the tree as a packet
+// (trace_tree_packet: one scalar fetch per node per wave).
 __global__ __launch_bounds__(kBlock) void k_ooc_ch(OocDomain D,
                                                    const spray_rt_ray* __restrict__ rays,
                                                    const uint32_t* __restrict__ idx,
                                                    uint32_t n, spray_rt_hit* __restrict__ hits,
                                                    uint64_t* __restrict__ tie) {
-  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ int32_t wstack[(kBlock / 64) * kStack];
   const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t i = idx[j];
-  const float4* rp = reinterpret_cast<const float4*>(rays + i);
-  const float4 o4 = rp[0], d4 = rp[1];
+  if (blockIdx.x * kBlock + (threadIdx.x & ~63u) >= n) return;  // whole wave idle
+  const bool valid = j < n;
+  const uint32_t i = valid ? idx[j] : 0u;
+  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+  float4 h0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+  if (valid) {
+    const float4* rp = reinterpret_cast<const float4*>(rays + i);
+    o4 = rp[0];
+    d4 = rp[1];
+    h0 = reinterpret_cast<const float4*>(hits + i)[0];
+  }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   float4* hp = reinterpret_cast<float4*>(hits + i);
-  const float4 h0 = hp[0];
   const bool have = __float_as_uint(h0.w) != 0xFFFFFFFFu;
   const float tcur = have ? h0.x : d4.w;
   // the domain's own nearest hit with t <= tcur (ties at tcur included)
   Best best{tcur, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  unsigned a = 0, b = 0;
-  trace_tree<false, false>(D.nodes, D.tris, D.prims, r, o4.w, 0.f, best, stack + threadIdx.x,
-                           a, b);
-  if (best.leaf == 0xFFFFFFFFu) return;
+  bool act = valid, hit = false;
+  trace_tree_packet<false>(reinterpret_cast<uint64_t>(D.nodes),
+                           reinterpret_cast<uint64_t>(D.tris),
+                           reinterpret_cast<uint64_t>(D.prims), r, o4.w, 0.f, best, act, hit,
+                           wstack + (threadIdx.x >> 6) * kStack);
+  if (!valid || best.leaf == 0xFFFFFFFFu) return;
   const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   float tm;
   aabb_ref(D.box, dr, tm);
@@ -153,19 +164,26 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ah(OocDomain D,
                                                    const spray_rt_ray* __restrict__ rays,
                                                    const uint32_t* __restrict__ idx,
                                                    uint32_t n, uint8_t* __restrict__ occ) {
-  __shared__ int32_t stack[kStack * kBlock];
+  __shared__ int32_t wstack[(kBlock / 64) * kStack];
   const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t i = idx[j];
-  if (occ[i]) return;  // occluded by an earlier domain
-  const float4* rp = reinterpret_cast<const float4*>(rays + i);
-  const float4 o4 = rp[0], d4 = rp[1];
+  if (blockIdx.x * kBlock + (threadIdx.x & ~63u) >= n) return;  // whole wave idle
+  const uint32_t i = j < n ? idx[j] : 0u;
+  const bool valid = j < n && !occ[i];  // else occluded by an earlier domain
+  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+  if (valid) {
+    const float4* rp = reinterpret_cast<const float4*>(rays + i);
+    o4 = rp[0];
+    d4 = rp[1];
+  }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   Best best{0.f, 0u, 0u};
-  unsigned a = 0, b = 0;
-  if (trace_tree<true, false>(D.nodes, D.tris, D.prims, r, o4.w, d4.w, best,
-                              stack + threadIdx.x, a, b))
-    occ[i] = 1;
+  bool act = valid, hit = false;
+  if (__ballot(act))
+    trace_tree_packet<true>(reinterpret_cast<uint64_t>(D.nodes),
+                            reinterpret_cast<uint64_t>(D.tris),
+                            reinterpret_cast<uint64_t>(D.prims), r, o4.w, d4.w, best, act, hit,
+                            wstack + (threadIdx.x >> 6) * kStack);
+  if (hit) occ[i] = 1;
 }
 
 __global__ __launch_bounds__(kBlock) void k_ooc_clear_occ(const uint8_t* __restrict__ valid,
