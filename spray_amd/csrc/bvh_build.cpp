@@ -48,17 +48,19 @@ int ceil_log2(size_t x) {
   return l;
 }
 
-// Conservative padding of a finite child box (culling only).
-void pad(float lo[3], float hi[3]) {
+// Conservative padding of a finite child box (culling only): each bound
+// moves out by rel x max(|lo|, |hi|, extent).
+void pad_rel(float lo[3], float hi[3], float rel) {
   if (!(std::isfinite(lo[0]) && std::isfinite(hi[0]))) return;
   for (int j = 0; j < 3; ++j) {
     float e = hi[j] - lo[j];
     float m = std::fmax(std::fmax(std::fabs(lo[j]), std::fabs(hi[j])), e);
-    float p = m * kBoxPad;
+    float p = m * rel;
     lo[j] = lo[j] - p;
     hi[j] = hi[j] + p;
   }
 }
+void pad(float lo[3], float hi[3]) { pad_rel(lo, hi, kBoxPad); }
 
 class Builder {
  public:
@@ -298,10 +300,18 @@ bool build_domain_tree(const float* boxes, size_t n, std::vector<BvhNode>* out,
   BvhImage img;
   Builder b(boxes, n, 1, &img);
   b.run();
-  // leaves hold one box each: rewrite ~((first << 2) | 0) as ~(id << 2)
+  // leaves hold one box each: rewrite ~((first << 2) | 0) as ~(id << 2).
+  // Internal children get a padded box: the packet walk tests them with the
+  // fast (fma) slab, a superset of the exact test with this margin; leaf
+  // boxes stay exact -- they decide the mask.
   for (BvhNode& nd : img.nodes) {
-    for (int32_t* ref : {&nd.left, &nd.right}) {
-      if (*ref >= 0 || *ref == kNoChild) continue;
+    for (int side = 0; side < 2; ++side) {
+      int32_t* ref = side ? &nd.right : &nd.left;
+      if (*ref >= 0) {
+        pad_rel(side ? nd.r_lo : nd.l_lo, side ? nd.r_hi : nd.l_hi, kTopPad);
+        continue;
+      }
+      if (*ref == kNoChild) continue;
       uint32_t first = ~uint32_t(*ref) >> 2;
       *ref = ~int32_t(img.prims[first] << 2);
     }

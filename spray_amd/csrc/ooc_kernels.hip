@@ -42,7 +42,9 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
   for (int w = 0; w < W; ++w) m[w] = 0;
   if (!valid || valid[i]) {
     const float4* rp = reinterpret_cast<const float4*>(rays + i);
-    tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, rp[0], rp[1], m);
+    const float4 o4 = rp[0], d4 = rp[1];
+    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
   }
   uint32_t n = 0;
 #pragma unroll

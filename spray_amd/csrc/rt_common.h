@@ -26,6 +26,7 @@ constexpr float kRayEpsilon = 0.001f;  // SPRAY_RAY_EPSILON, render/spray.h:46
 // it is conservative; tests/ check BVH == brute force bit-exactly).
 constexpr float kTfarSlack = 1.0000153f;  // 1 + 2^-16
 constexpr float kBoxPad = 1e-6f;          // relative node-box padding
+constexpr float kTopPad = 1e-5f;          // internal boxes of the domain tree
 constexpr float kDirClamp = 1e-20f;       // |d| floor for the inverse dir
 
 // 64-B BVH2 node: left box, right box, child refs.  ref >= 0: internal node

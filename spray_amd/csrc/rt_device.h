@@ -481,9 +481,13 @@ __device__ __forceinline__ void tlas_mask(const float4* stl, int ntlas, int32_t*
 // entries of LDS per wave) are wave-uniform: no per-lane stack traffic and
 // no divergence -- neighbouring rays share nearly all of their top-level
 // path.
+// Internal children carry padded boxes (build_domain_tree) and are tested
+// with the fast slab -- a superset of the exact test -- leaf children with
+// the reference's exact intersectAabb, which alone sets a lane's bit.
 template <int W>
 __device__ __forceinline__ void tlas_mask_wave(const float4* stl, int ntlas, int32_t* wstk,
-                                               float4 o4, float4 d4, uint64_t* m) {
+                                               const Ray& r, float4 o4, float4 d4,
+                                               uint64_t* m) {
 #pragma unroll
   for (int w = 0; w < W; ++w) m[w] = 0;
   if (ntlas <= 0) return;
@@ -496,8 +500,11 @@ __device__ __forceinline__ void tlas_mask_wave(const float4* stl, int ntlas, int
     const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(e.x));
     const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(e.y));
     float tm;
-    const bool hl = aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm);
-    const bool hr = cr != INT_MIN && aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm);
+    const bool hl = cl < 0 ? aabb_ref6(a.x, a.y, a.z, a.w, b.x, b.y, dr, tm)
+                           : slab(r, a.x, a.y, a.z, a.w, b.x, b.y, 0.f, kInf, tm);
+    const bool hr = cr == INT_MIN ? false
+                    : cr < 0      ? aabb_ref6(b.z, b.w, c.x, c.y, c.z, c.w, dr, tm)
+                                  : slab(r, b.z, b.w, c.x, c.y, c.z, c.w, 0.f, kInf, tm);
     const bool al = __ballot(hl) != 0, ar = __ballot(hr) != 0;
     int32_t next = kNone;
     if (cl < 0) {

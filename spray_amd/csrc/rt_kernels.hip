@@ -234,7 +234,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
-    if (SPRAY_DIAG_MODE != 3) tlas_mask_wave<W>(stl, ntlas, wstk, o4, d4, m);
+    if (SPRAY_DIAG_MODE != 3) tlas_mask_wave<W>(stl, ntlas, wstk, r, o4, d4, m);
     if (SPRAY_DIAG_MODE == 1 || SPRAY_DIAG_MODE >= 3) {  // diagnostic: mask only
       uint32_t pc = 0;
 #pragma unroll
@@ -428,7 +428,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   uint64_t m[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) m[w] = 0;
-  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, o4, d4, m);
+  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
   uint64_t m0[EPI == kEpiKeys ? W : 1];
   if (EPI == kEpiKeys) {
 #pragma unroll
@@ -729,7 +729,8 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
   const float4* rp = reinterpret_cast<const float4*>(rays + i);
   const float4 o4 = rp[0], d4 = rp[1];
   uint64_t m[W];
-  tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, o4, d4, m);
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
   uint64_t ranks = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) {

@@ -202,3 +202,60 @@ def test_insitu_two_ranks_on_gpu(oracle):
     hit = hit_ref["domain"] >= 0
     assert (seen[hit] == 1).all() and (seen[~hit] == 0).all()
     assert got[hit].tobytes() == hit_ref[hit].tobytes()
+
+
+def test_domain_mask_exact_on_box_boundaries(spray, oracle):
+    """The top-level walk (fast slab on padded internal boxes, exact
+    intersectAabb on the leaves) yields exactly the brute-force domain list:
+    with owner[d] = d the routing mask IS the domain mask.  Rays aimed at box
+    corners, edge midpoints and face centres (shared by neighbouring
+    domains), from outside, from inside, and axis-parallel."""
+    from spray_amd import insitu
+    from test_insitu import scene_boxes
+    boxes, bound = scene_boxes()
+    rng = np.random.default_rng(17)
+    pts = []
+    for b in boxes:
+        lo, hi = b[:3], b[3:]
+        c = (lo + hi) / 2
+        for k in range(8):  # corners
+            pts.append(np.where([(k >> a) & 1 for a in range(3)], hi, lo))
+        for a in range(3):  # face centres
+            for v in (lo[a], hi[a]):
+                p = c.copy()
+                p[a] = v
+                pts.append(p)
+    pts = np.array(pts, np.float32)
+    n = len(pts)
+    org = np.concatenate([
+        rng.uniform(-40, 110, size=(n, 3)),                   # outside / anywhere
+        pts + rng.normal(scale=3.0, size=(n, 3)),              # near the target
+        np.repeat(((bound[:3] + bound[3:]) / 2)[None], n, 0),  # from the centre
+    ]).astype(np.float32)
+    tgt = np.concatenate([pts, pts, pts])
+    d = (tgt - org).astype(np.float32)
+    nrm = np.linalg.norm(d, axis=1)
+    keep = nrm > 0
+    org, d = org[keep], d[keep] / nrm[keep, None]
+    # axis-parallel rays grazing box faces
+    m = 2000
+    ax = rng.integers(0, 3, m)
+    o2 = pts[rng.integers(0, n, m)].copy()
+    d2 = np.zeros((m, 3), np.float32)
+    d2[np.arange(m), ax] = rng.choice([-1.0, 1.0], m)
+    o2[np.arange(m), ax] += -d2[np.arange(m), ax] * 150.0
+    org = np.concatenate([org, o2]).astype(np.float32)
+    d = np.concatenate([d, d2]).astype(np.float32)
+    rt = spray.RtContext(0)
+    rt.domain_bounds(boxes)
+    rt.set_owners(np.arange(len(boxes), dtype=np.int32))
+    loc = insitu.GpuLocal(rt, torch.device("cuda"))
+    mask = loc.route(H.rays_tensor(org, d).cuda()).cpu().numpy().view(np.uint64)
+    ids, _, cnt, _ = oracle.domain_query(org, d, boxes, len(boxes))
+    ref = np.zeros(len(org), np.uint64)
+    for i in range(len(org)):
+        for k in range(cnt[i]):
+            ref[i] |= np.uint64(1) << np.uint64(ids[i, k])
+    assert (mask == ref).all(), np.nonzero(mask != ref)[0][:10]
+    assert (cnt >= 4).sum() > 100
+    rt.close()
