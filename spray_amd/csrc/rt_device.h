@@ -48,6 +48,11 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
 #define SPRAY_SCALAR_UNIFORM 0
 #endif
 #define CAS __attribute__((address_space(4)))
+// Packet walk child order: 1 = majority vote of the lanes, 0 = the first
+// lane entering both children.
+#ifndef SPRAY_PACKET_VOTE
+#define SPRAY_PACKET_VOTE 0
+#endif
 __device__ __forceinline__ bool wave_uniform_addr(const void* p, uint64_t& u) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
@@ -317,9 +322,16 @@ __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tri
     const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(n3.x));
     const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(n3.y));
     const uint64_t bl = __ballot(hl), br = __ballot(hr);
+#if SPRAY_PACKET_VOTE
     const uint64_t vl = __ballot(hl && (!hr || tl <= tr));
     const uint64_t vr = __ballot(hr && (!hl || tr < tl));
     const bool lf = __popcll(vl) >= __popcll(vr);
+#else
+    // near side of the first lane that enters both children
+    const uint64_t both = bl & br;
+    const bool lf = both ? __builtin_amdgcn_readlane(int(tl <= tr), __ffsll((long long)both) - 1) != 0
+                         : true;
+#endif
     int32_t next = kNone;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {

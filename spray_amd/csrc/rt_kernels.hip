@@ -39,7 +39,7 @@ namespace {
 #endif
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): packet form: 5 = no
-// tree walks, 6 = top-level mask only; per-lane form: 3 = ray in, record out
+// tree walks, 6 = top-level mask only, 7 = no epilogue / spawn; per-lane form: 3 = ray in, record out
 // (no domain tree), 1 = domain mask
 // only, 2 = mask + ordered domain selection, no BVH traversal.
 // Minimum resident waves per SIMD the register allocator must allow (the
@@ -524,6 +524,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
     h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     h2 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  } else if (SPRAY_DIAG_MODE == 7) {  // diagnostic: no epilogue, no spawn
+    h0 = make_float4(best.t, 0.f, 0.f, __uint_as_float(best.prim));
+    h1 = h2 = h0;
   } else {
     const SlotDesc s = slots[dom2slot[best_dom]];
     float hu, hv;
@@ -563,7 +566,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     }
     A.keys[i] = key;
   }
-  if (EPI == kEpiSpawn && best_dom >= 0) {
+  if (EPI == kEpiSpawn && best_dom >= 0 && SPRAY_DIAG_MODE != 7) {
     spray_rt_hit h;
     h.t = h0.x;
     h.color = __float_as_uint(h1.w);
