@@ -305,22 +305,25 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
 // are those of the per-lane walk.  ANY: a lane that finds an occluder sets
 // hit and leaves the packet; the walk ends when no lane participates.
 // wstk: kStack entries of LDS per wave.
+typedef float v16f __attribute__((ext_vector_type(16)));
+
 template <bool ANY>
 __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tris_u,
                                                   uint64_t prims_u, const Ray& r,
                                                   float tnear, float tfar_any, Best& best,
                                                   bool& act, bool& hit, int32_t* wstk) {
+  const CAS v16f* nodes = reinterpret_cast<const CAS v16f*>(nodes_u);
   int sp = 0;
   int32_t cur = 0;
   for (;;) {
-    const CAS v4f* q = reinterpret_cast<const CAS v4f*>(nodes_u) + 4 * cur;
-    const v4f n0 = q[0], n1 = q[1], n2 = q[2], n3 = q[3];
+    // the whole 64-B node in one scalar fetch (one round trip per step)
+    const v16f n = nodes[cur];
     const float tcut = ANY ? tfar_any : best.t;
     float tl = 0.f, tr = 0.f;
-    const bool hl = act && slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tcut, tl);
-    const bool hr = act && slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tcut, tr);
-    const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(n3.x));
-    const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(n3.y));
+    const bool hl = slab(r, n[0], n[1], n[2], n[3], n[4], n[5], tnear, tcut, tl) && act;
+    const bool hr = slab(r, n[6], n[7], n[8], n[9], n[10], n[11], tnear, tcut, tr) && act;
+    const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(n[12]));
+    const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(n[13]));
     const uint64_t bl = __ballot(hl), br = __ballot(hr);
 #if SPRAY_PACKET_VOTE
     const uint64_t vl = __ballot(hl && (!hr || tl <= tr));
@@ -342,16 +345,26 @@ __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tri
         const bool h = left ? hl : hr;
         const uint32_t enc = ~uint32_t(c);
         const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
-        for (uint32_t qq = 0; qq < cnt; ++qq) {
-          const uint32_t p = first + qq;
-          const CAS v4f* tq = reinterpret_cast<const CAS v4f*>(tris_u) + 3 * size_t(p);
-          const v4f x0 = tq[0], x1 = tq[1], x2 = tq[2];
+        // the leaf's (up to four) 48-B triangles in three scalar fetches
+        const CAS v16f* tq = reinterpret_cast<const CAS v16f*>(tris_u + 48ull * first);
+        const v16f t0 = tq[0], t1 = tq[1], t2 = tq[2];
+        const float tv[48] = {t0[0], t0[1], t0[2],  t0[3],  t0[4],  t0[5],  t0[6],  t0[7],
+                              t0[8], t0[9], t0[10], t0[11], t0[12], t0[13], t0[14], t0[15],
+                              t1[0], t1[1], t1[2],  t1[3],  t1[4],  t1[5],  t1[6],  t1[7],
+                              t1[8], t1[9], t1[10], t1[11], t1[12], t1[13], t1[14], t1[15],
+                              t2[0], t2[1], t2[2],  t2[3],  t2[4],  t2[5],  t2[6],  t2[7],
+                              t2[8], t2[9], t2[10], t2[11], t2[12], t2[13], t2[14], t2[15]};
+#pragma unroll
+        for (uint32_t qq = 0; qq < 4; ++qq) {
+          if (qq >= cnt) break;
           if (!h) continue;
+          const float* x = tv + 12 * qq;
           float t, u, v;
-          if (!tri_test(r, tnear, make_float4(x0.x, x0.y, x0.z, x0.w),
-                        make_float4(x1.x, x1.y, x1.z, x1.w),
-                        make_float4(x2.x, x2.y, x2.z, x2.w), t, u, v))
+          if (!tri_test(r, tnear, make_float4(x[0], x[1], x[2], x[3]),
+                        make_float4(x[4], x[5], x[6], x[7]),
+                        make_float4(x[8], x[9], x[10], x[11]), t, u, v))
             continue;
+          const uint32_t p = first + qq;
           if (ANY) {
             if (t <= tfar_any) {
               hit = true;
