@@ -228,6 +228,10 @@ int spray_rt_set_owners(spray_rt_ctx_t ctx, const int* owner);
  * the ray enters.  Device buffers only. */
 int spray_rt_route(spray_rt_ctx_t ctx, const spray_rt_ray* rays, size_t M,
                    uint64_t* rank_mask);
+/* Exchange packing: dst[j] = src[idx[j]] for rows of 4, 8, 16, 32 (a ray)
+ * or 48 (a hit record) bytes; idx int64.  Device buffers only. */
+int spray_rt_gather_rows(spray_rt_ctx_t ctx, const void* src, size_t row_bytes,
+                         const int64_t* idx, size_t n, void* dst);
 /* Closest hit over the RESIDENT domains of each ray's list (mapped slots;
  * the others are skipped) plus the composite key that orders hits the way
  * the sequential walk of the whole list does:

@@ -667,6 +667,22 @@ int spray_rt_set_coherence(spray_rt_ctx_t c, int mode) {
   return SPRAY_RT_OK;
 }
 
+int spray_rt_gather_rows(spray_rt_ctx_t c, const void* src, size_t row_bytes,
+                         const int64_t* idx, size_t n, void* dst) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (row_bytes != 4 && row_bytes != 8 && row_bytes != 16 && row_bytes != 32 &&
+      row_bytes != 48)
+    return fail(c, SPRAY_RT_ERR_ARG, "row size %zu not supported", row_bytes);
+  if (n == 0) return SPRAY_RT_OK;
+  if (!is_device_ptr(src) || !is_device_ptr(idx) || !is_device_ptr(dst))
+    return fail(c, SPRAY_RT_ERR_ARG, "gather needs device buffers");
+  if (row_bytes % 16 == 0 &&
+      ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15))
+    return fail(c, SPRAY_RT_ERR_ARG, "16-B rows need 16-B aligned buffers");
+  HIPCHK(c, launch_gather_rows(stream_of(c), src, row_bytes, idx, n, dst));
+  return SPRAY_RT_OK;
+}
+
 int spray_rt_set_owners(spray_rt_ctx_t c, const int* owner) {
   if (!c) return SPRAY_RT_ERR_ARG;
   if (c->ndom <= 0) return fail(c, SPRAY_RT_ERR_STATE, "no domain bounds set");

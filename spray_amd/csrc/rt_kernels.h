@@ -89,6 +89,11 @@ hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w
                                   int tw, int th, spray_rt_ray* rays, int32_t* pixid,
                                   int32_t* samid);
 
+// dst[j] = src[idx[j]], rows of 4, 8, 16, 32 or 48 bytes (16-B aligned
+// buffers for the 16-B multiples).
+hipError_t launch_gather_rows(hipStream_t s, const void* src, size_t row_bytes,
+                              const int64_t* idx, size_t n, void* dst);
+
 hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                int spp, int tx, int ty, int tw, int th,
                                spray_rt_ray* rays, int32_t* pixid,

@@ -903,6 +903,26 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ c,
   if (threadIdx.x == 0) *d_count = run;
 }
 
+// Row gather dst[j] = src[idx[j]] for rows of 4 / 8 / 16 / 32 / 48 bytes
+// (the in-situ exchange packing); 16-B rows move as one 16-B load/store.
+template <int WORDS>
+__global__ __launch_bounds__(kBlock) void k_gather_rows(const uint32_t* __restrict__ src,
+                                                        const int64_t* __restrict__ idx,
+                                                        size_t n, uint32_t* __restrict__ dst) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t i = size_t(idx[j]);
+  if (WORDS % 4 == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + i * WORDS);
+    uint4* d4 = reinterpret_cast<uint4*>(dst + j * WORDS);
+#pragma unroll
+    for (int k = 0; k < WORDS / 4; ++k) d4[k] = s4[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < WORDS; ++k) dst[j * WORDS + k] = src[i * WORDS + k];
+  }
+}
+
 // Ordered selection of the flagged positions (the masked any hit's index
 // list): tiles of kSelTile flags, 16 per thread through one 16-B load;
 // count -> scan of the tile counts -> ordered write.
@@ -1332,6 +1352,22 @@ hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w
   for (int k = 0; k < 14; ++k) c.p[k] = cam14[k];
   k_eye_rays_insitu<<<grid_for(n), kBlock, 0, s>>>(c, image_w, spp, bx, by, bw, tx, ty,
                                                    tw, th, rays, pixid, samid);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(hipStream_t s, const void* src, size_t row_bytes,
+                              const int64_t* idx, size_t n, void* dst) {
+  if (n == 0) return hipSuccess;
+  const uint32_t* a = static_cast<const uint32_t*>(src);
+  uint32_t* b = static_cast<uint32_t*>(dst);
+  switch (row_bytes) {
+    case 4: k_gather_rows<1><<<grid_for(n), kBlock, 0, s>>>(a, idx, n, b); break;
+    case 8: k_gather_rows<2><<<grid_for(n), kBlock, 0, s>>>(a, idx, n, b); break;
+    case 16: k_gather_rows<4><<<grid_for(n), kBlock, 0, s>>>(a, idx, n, b); break;
+    case 32: k_gather_rows<8><<<grid_for(n), kBlock, 0, s>>>(a, idx, n, b); break;
+    case 48: k_gather_rows<12><<<grid_for(n), kBlock, 0, s>>>(a, idx, n, b); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -288,6 +288,15 @@ class RtContext:
         b, k2 = _addr(rank_mask)
         self._check(lib().spray_rt_route(self.h, a, n, b), "route")
 
+    def gather_rows(self, src, idx, dst):
+        """dst[j] = src[idx[j]] (device tensors, rows of 4/8/16/32/48 B)."""
+        n = idx.numel()
+        row = _nbytes(src) // src.shape[0] if src.shape[0] else 4
+        a, k1 = _addr(src)
+        b, k2 = _addr(idx)
+        c, k3 = _addr(dst)
+        self._check(lib().spray_rt_gather_rows(self.h, a, row, b, n, c), "gather_rows")
+
     def intersect_scene_keyed(self, rays, hits, keys):
         """Closest hit over the resident domains + composite key (device)."""
         n = _nbytes(rays) // 32

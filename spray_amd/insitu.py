@@ -204,6 +204,11 @@ class GpuLocal:
         k = int(cnt.item()) if n else 0
         return out[:k], src[:k].long()
 
+    def gather(self, src, idx, dst):
+        """Exchange packing through the engine (torch's row gather is several
+        times slower for 32- and 48-byte rows)."""
+        self.rt.gather_rows(src, idx, dst)
+
     def occluded(self, rays):
         t = self.torch
         occ = t.zeros(rays.shape[0], dtype=t.uint8, device=self.device)
@@ -237,10 +242,11 @@ class Exchange:
     (grouped by source rank, in the sender's order); ``backward`` returns
     per-copy results to the sender, in the order the copies were sent."""
 
-    def __init__(self, comm, mask):
+    def __init__(self, comm, mask, gather=None):
         import torch as t
         W = comm.world
         self.comm = comm
+        self.gather = gather
         n = mask.shape[0]
         if n:
             bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
@@ -257,7 +263,11 @@ class Exchange:
 
     def forward(self, payload):
         """payload: per-ray rows [n, ...] of the sender's batch."""
-        s = payload.index_select(0, self.idx)
+        if self.gather is not None and payload.is_cuda:
+            s = payload.new_empty((self.idx.numel(),) + tuple(payload.shape[1:]))
+            self.gather(payload, self.idx, s)
+        else:
+            s = payload.index_select(0, self.idx)
         if self.comm.skip:
             return s
         r = payload.new_empty((self.n_recv,) + tuple(payload.shape[1:]))
@@ -300,10 +310,11 @@ class InsituTracer:
         ``n_rays`` and ``n_shadow``."""
         t = self.torch
         L, C = self.local, self.comm
-        samid = samid.to(t.int64)
+        samid = samid.to(t.int32)
         n = rays.shape[0]
         # primary rays to the owners of their domains, keyed closest hit there
-        ex = Exchange(C, L.route(rays))
+        gather = getattr(L, "gather", None)
+        ex = Exchange(C, L.route(rays), gather)
         rrays, rsam = ex.forward(rays), ex.forward(samid)
         hits, keys = L.intersect_keyed(rrays)
         # composite: minimum key per ray at its sender, back to the owners
@@ -316,13 +327,13 @@ class InsituTracer:
         hits.view(t.int32)[:, 11].masked_fill_(~win, -1)  # spray_rt_hit.domain
         srays, src = L.spawn_pt(rrays, hits, shade)
         # shadow rays to the owners of their domains, any hit, OR at the spawner
-        sx = Exchange(C, L.route(srays))
+        sx = Exchange(C, L.route(srays), gather)
         occ = L.occluded(sx.forward(srays))
         socc = t.zeros(srays.shape[0], dtype=t.uint8, device=rays.device)
         if sx.n_sent:
             socc.scatter_reduce_(0, sx.idx, sx.backward(occ), "amax")
         tot = t.tensor([n, srays.shape[0]], dtype=t.int64, device=rays.device)
         C.all_reduce(tot, C.op("SUM"))
-        return {"samid": rsam[win], "hits": out_hits,
-                "shadow_samid": rsam.index_select(0, src), "shadow_occ": socc,
+        return {"samid": rsam[win].long(), "hits": out_hits,
+                "shadow_samid": rsam.index_select(0, src).long(), "shadow_occ": socc,
                 "n_rays": int(tot[0]), "n_shadow": int(tot[1])}
