@@ -228,6 +228,13 @@ int spray_rt_set_owners(spray_rt_ctx_t ctx, const int* owner);
  * the ray enters.  Device buffers only. */
 int spray_rt_route(spray_rt_ctx_t ctx, const spray_rt_ray* rays, size_t M,
                    uint64_t* rank_mask);
+/* Exchange plan of a routed batch (the per-destination queues of
+ * insitu_comm.inl, built at once): idx = for d = 0..world-1 the ascending
+ * indices i with bit d of rank_mask[i], concatenated; starts[0..world] =
+ * the list bounds (int64).  idx == NULL computes the bounds only (starts
+ * [world] = the capacity idx needs).  Device buffers only. */
+int spray_rt_exchange_plan(spray_rt_ctx_t ctx, const uint64_t* rank_mask, size_t n,
+                           int world, int64_t* idx, int64_t* starts);
 /* Exchange packing: dst[j] = src[idx[j]] for rows of 4, 8, 16, 32 (a ray)
  * or 48 (a hit record) bytes; idx int64.  Device buffers only. */
 int spray_rt_gather_rows(spray_rt_ctx_t ctx, const void* src, size_t row_bytes,

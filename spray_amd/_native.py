@@ -66,6 +66,7 @@ SIGNATURES = {
     "spray_rt_eye_rays_insitu": (I, [P, P, I, I, I, I, I, I, I, I, I, I, P, P, P]),
     "spray_rt_set_owners": (I, [P, P]),
     "spray_rt_gather_rows": (I, [P, P, SZ, P, SZ, P]),
+    "spray_rt_exchange_plan": (I, [P, P, SZ, I, P, P]),
     "spray_rt_set_coherence": (I, [P, I]),
     "spray_rt_spawn_shadows_ao": (I, [P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_ooc_create": (I, [P, I, P]),

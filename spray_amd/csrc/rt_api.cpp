@@ -667,6 +667,21 @@ int spray_rt_set_coherence(spray_rt_ctx_t c, int mode) {
   return SPRAY_RT_OK;
 }
 
+int spray_rt_exchange_plan(spray_rt_ctx_t c, const uint64_t* rank_mask, size_t n,
+                           int world, int64_t* idx, int64_t* starts) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (world <= 0 || world > 64) return fail(c, SPRAY_RT_ERR_ARG, "world must be in [1, 64]");
+  if (n > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "n > 2^32");
+  if (!is_device_ptr(starts) || (n && !is_device_ptr(rank_mask)) ||
+      (idx && !is_device_ptr(idx)))
+    return fail(c, SPRAY_RT_ERR_ARG, "exchange plan needs device buffers");
+  HIPCHK(c, hipSetDevice(c->device));
+  int r = ensure(c, &c->d_sel, &c->sel_cap, plan_temp_bytes(n, world));
+  if (r) return r;
+  HIPCHK(c, launch_plan(stream_of(c), rank_mask, n, world, idx, starts, c->d_sel));
+  return SPRAY_RT_OK;
+}
+
 int spray_rt_gather_rows(spray_rt_ctx_t c, const void* src, size_t row_bytes,
                          const int64_t* idx, size_t n, void* dst) {
   if (!c) return SPRAY_RT_ERR_ARG;

@@ -89,6 +89,13 @@ hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w
                                   int tw, int th, spray_rt_ray* rays, int32_t* pixid,
                                   int32_t* samid);
 
+// Exchange plan: idx = for d in 0..world-1 the ascending i with bit d of
+// masks[i] (concatenated); starts[0..world] = list bounds (device int64).
+// idx == nullptr: bounds only (size the list first).
+// temp: plan_temp_bytes(n, world) bytes of device scratch.
+size_t plan_temp_bytes(size_t n, int world);
+hipError_t launch_plan(hipStream_t s, const uint64_t* masks, size_t n, int world,
+                       int64_t* idx, int64_t* starts, void* temp);
 // dst[j] = src[idx[j]], rows of 4, 8, 16, 32 or 48 bytes (16-B aligned
 // buffers for the 16-B multiples).
 hipError_t launch_gather_rows(hipStream_t s, const void* src, size_t row_bytes,

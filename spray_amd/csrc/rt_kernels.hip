@@ -903,6 +903,63 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ c,
   if (threadIdx.x == 0) *d_count = run;
 }
 
+constexpr int kSelPer = 16;  // flags / masks per thread of the selection kernels
+constexpr int kSelTile = kBlock * kSelPer;
+
+// Exchange plan of a routed batch: for every destination rank d, the
+// ascending indices of the rays whose mask has bit d, concatenated in rank
+// order.  Tiles of kSelTile rays x ranks: count -> one exclusive scan over
+// the [rank][tile] counts (rank-major, so the concatenation falls out) ->
+// ordered write.
+__device__ __forceinline__ uint32_t mask_bits16(const uint64_t* m, size_t n, size_t base,
+                                                int d, uint32_t& bits) {
+  bits = 0;
+#pragma unroll
+  for (int k = 0; k < kSelPer; ++k)
+    if (base + k < n && ((m[base + k] >> d) & 1ull)) bits |= 1u << k;
+  return __popc(bits);
+}
+
+__global__ __launch_bounds__(kBlock) void k_plan_count(const uint64_t* __restrict__ m,
+                                                       size_t n, uint32_t* __restrict__ tc) {
+  using Reduce = hipcub::BlockReduce<uint32_t, kBlock>;
+  __shared__ typename Reduce::TempStorage tmp;
+  const int d = blockIdx.y;
+  uint32_t bits;
+  const size_t base = size_t(blockIdx.x) * kSelTile + size_t(threadIdx.x) * kSelPer;
+  const uint32_t c = base < n ? mask_bits16(m, n, base, d, bits) : 0u;
+  const uint32_t total = Reduce(tmp).Sum(c);
+  if (threadIdx.x == 0) tc[size_t(d) * gridDim.x + blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_plan_write(const uint64_t* __restrict__ m,
+                                                       size_t n, const uint32_t* __restrict__ tc,
+                                                       int64_t* __restrict__ idx) {
+  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
+  __shared__ typename Scan::TempStorage tmp;
+  const int d = blockIdx.y;
+  uint32_t bits = 0;
+  const size_t base = size_t(blockIdx.x) * kSelTile + size_t(threadIdx.x) * kSelPer;
+  const uint32_t c = base < n ? mask_bits16(m, n, base, d, bits) : 0u;
+  uint32_t k, total;
+  Scan(tmp).ExclusiveSum(c, k, total);
+  k += tc[size_t(d) * gridDim.x + blockIdx.x];
+  while (bits) {
+    const int b = __ffs(bits) - 1;
+    bits &= bits - 1;
+    idx[k++] = int64_t(base + b);
+  }
+}
+
+// starts[d] = first position of rank d's list (d <= world: starts[world] = total)
+__global__ void k_plan_bounds(const uint32_t* __restrict__ tc, uint32_t tiles, int world,
+                              const uint32_t* __restrict__ total,
+                              int64_t* __restrict__ starts) {
+  const int d = threadIdx.x;
+  if (d < world) starts[d] = tc[size_t(d) * tiles];
+  if (d == world) starts[d] = *total;
+}
+
 // Row gather dst[j] = src[idx[j]] for rows of 4 / 8 / 16 / 32 / 48 bytes
 // (the in-situ exchange packing); 16-B rows move as one 16-B load/store.
 template <int WORDS>
@@ -926,8 +983,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(const uint32_t* __restri
 // Ordered selection of the flagged positions (the masked any hit's index
 // list): tiles of kSelTile flags, 16 per thread through one 16-B load;
 // count -> scan of the tile counts -> ordered write.
-constexpr int kSelPer = 16;
-constexpr int kSelTile = kBlock * kSelPer;
 
 __device__ __forceinline__ uint32_t flags16(const uint8_t* f, size_t M, size_t base,
                                             uint32_t& mask) {
@@ -1352,6 +1407,28 @@ hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w
   for (int k = 0; k < 14; ++k) c.p[k] = cam14[k];
   k_eye_rays_insitu<<<grid_for(n), kBlock, 0, s>>>(c, image_w, spp, bx, by, bw, tx, ty,
                                                    tw, th, rays, pixid, samid);
+  return hipGetLastError();
+}
+
+size_t plan_temp_bytes(size_t n, int world) {
+  const size_t tiles = (n + kSelTile - 1) / kSelTile;
+  return (tiles * size_t(world) + 2) * sizeof(uint32_t);
+}
+
+hipError_t launch_plan(hipStream_t s, const uint64_t* masks, size_t n, int world,
+                       int64_t* idx, int64_t* starts, void* temp) {
+  const size_t tiles = (n + kSelTile - 1) / kSelTile;
+  uint32_t* tc = static_cast<uint32_t*>(temp);
+  uint32_t* total = tc + tiles * size_t(world) + 1;
+  if (n == 0 || world <= 0) {
+    hipError_t e = hipMemsetAsync(starts, 0, (world + 1) * sizeof(int64_t), s);
+    return e;
+  }
+  const dim3 g{unsigned(tiles), unsigned(world), 1u};
+  k_plan_count<<<g, kBlock, 0, s>>>(masks, n, tc);
+  k_scan_blocks<<<1, 1024, 0, s>>>(tc, uint32_t(tiles * world), total);
+  if (idx) k_plan_write<<<g, kBlock, 0, s>>>(masks, n, tc, idx);
+  k_plan_bounds<<<1, 128, 0, s>>>(tc, uint32_t(tiles), world, total, starts);
   return hipGetLastError();
 }
 

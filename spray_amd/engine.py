@@ -288,6 +288,16 @@ class RtContext:
         b, k2 = _addr(rank_mask)
         self._check(lib().spray_rt_route(self.h, a, n, b), "route")
 
+    def exchange_plan(self, rank_mask, world, idx, starts):
+        """idx = per destination rank the ascending ray indices (device int64;
+        None: bounds only); starts [world + 1] int64."""
+        n = rank_mask.numel()
+        a, k1 = _addr(rank_mask)
+        b, k2 = _addr(idx)
+        c, k3 = _addr(starts)
+        self._check(lib().spray_rt_exchange_plan(self.h, a, n, int(world), b, c),
+                    "exchange_plan")
+
     def gather_rows(self, src, idx, dst):
         """dst[j] = src[idx[j]] (device tensors, rows of 4/8/16/32/48 B)."""
         n = idx.numel()

@@ -204,6 +204,17 @@ class GpuLocal:
         k = int(cnt.item()) if n else 0
         return out[:k], src[:k].long()
 
+    def plan(self, mask, world):
+        """Per-destination ascending ray lists of a routed batch (device):
+        bounds first (one host read sizes the list), then the lists."""
+        t = self.torch
+        starts = t.empty(world + 1, dtype=t.int64, device=self.device)
+        self.rt.exchange_plan(mask, world, None, starts)
+        total = int(starts[-1])
+        idx = t.empty(max(total, 1), dtype=t.int64, device=self.device)
+        self.rt.exchange_plan(mask, world, idx, starts)
+        return idx[:total], starts
+
     def gather(self, src, idx, dst):
         """Exchange packing through the engine (torch's row gather is several
         times slower for 32- and 48-byte rows)."""
@@ -242,20 +253,25 @@ class Exchange:
     (grouped by source rank, in the sender's order); ``backward`` returns
     per-copy results to the sender, in the order the copies were sent."""
 
-    def __init__(self, comm, mask, gather=None):
+    def __init__(self, comm, mask, gather=None, plan=None):
         import torch as t
         W = comm.world
         self.comm = comm
         self.gather = gather
         n = mask.shape[0]
-        if n:
-            bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
-            sel = ((mask.unsqueeze(0) >> bit) & 1).bool()  # [W, n], dest-major
-            dest, self.idx = sel.nonzero(as_tuple=True)
+        if plan is not None and mask.is_cuda:
+            # device plan: per-rank lists + bounds in four small kernels
+            self.idx, starts = plan(mask, W)
+            send = starts[1:] - starts[:-1]
         else:
-            dest = t.zeros(0, dtype=t.int64, device=mask.device)
-            self.idx = dest
-        send = t.bincount(dest, minlength=W).to(t.int64)
+            if n:
+                bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
+                sel = ((mask.unsqueeze(0) >> bit) & 1).bool()  # [W, n], dest-major
+                dest, self.idx = sel.nonzero(as_tuple=True)
+            else:
+                dest = t.zeros(0, dtype=t.int64, device=mask.device)
+                self.idx = dest
+            send = t.bincount(dest, minlength=W).to(t.int64)
         recv = t.empty_like(send)
         comm.all_to_all(recv, send, None, None)  # the count phase
         self.sc, self.rc = send.tolist(), recv.tolist()
@@ -313,8 +329,8 @@ class InsituTracer:
         samid = samid.to(t.int32)
         n = rays.shape[0]
         # primary rays to the owners of their domains, keyed closest hit there
-        gather = getattr(L, "gather", None)
-        ex = Exchange(C, L.route(rays), gather)
+        gather, plan = getattr(L, "gather", None), getattr(L, "plan", None)
+        ex = Exchange(C, L.route(rays), gather, plan)
         rrays, rsam = ex.forward(rays), ex.forward(samid)
         hits, keys = L.intersect_keyed(rrays)
         # composite: minimum key per ray at its sender, back to the owners
@@ -327,7 +343,7 @@ class InsituTracer:
         hits.view(t.int32)[:, 11].masked_fill_(~win, -1)  # spray_rt_hit.domain
         srays, src = L.spawn_pt(rrays, hits, shade)
         # shadow rays to the owners of their domains, any hit, OR at the spawner
-        sx = Exchange(C, L.route(srays), gather)
+        sx = Exchange(C, L.route(srays), gather, plan)
         occ = L.occluded(sx.forward(srays))
         socc = t.zeros(srays.shape[0], dtype=t.uint8, device=rays.device)
         if sx.n_sent:
