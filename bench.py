@@ -190,6 +190,46 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
                       "AO-%d rays per hit (frame replicas x%d)" % (nsamples, world)}
 
 
+def run_frame(args, dist, world, rt, cam, lights):
+    """The whole ooc-mode frame of configs[1] on the device (spray_amd/frame.py):
+    the reference's tile schedule (8 tiles of 1024x128 at 1M samples per
+    rank), per tile eye rays -> closest hit -> ooc::ShaderPt -> any hit of the
+    shadows -> film into the HDR image; frame replicas across ranks."""
+    import torch
+    import spray_amd
+    sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
+                                     lights=lights)
+    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(SCENE))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    _, (nrad, nsh) = spray_amd.frame.render_frame(rt, sh, cam, W, H, SPP, image=image)
+    for _ in range(args.warmup):
+        spray_amd.frame.render_frame(rt, sh, cam, W, H, SPP, image=image, stats=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        spray_amd.frame.render_frame(rt, sh, cam, W, H, SPP, image=image, stats=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    rt.frame_stats(reset=True)
+    img = image.view(-1, 4)[:, :3]
+    return {"value": round((nrad + nsh) * world * args.steps / el / 1e6, 3),
+            "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+            "scaling": "weak", "rays_per_step": nrad + nsh, "radiance_rays": nrad,
+            "shadow_rays": nsh, "image_mean": round(float(img.mean()), 6),
+            "config": "configs[1] as a whole frame: 8 tiles of 1024x128x8spp, eye rays + "
+                      "closest hit + PT shading + any hit + film on the device, bounces=1 "
+                      "(frame replicas x%d)" % world}
+
+
 def run_ooc(args, rt_main, prim, n_prim, slots=4):
     """configs[3]: the same frame with at most `slots` domains resident in HBM
     (spray_rt_ooc_*): closest hit with the domains streamed through the LRU
@@ -251,6 +291,8 @@ def main():
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
+    ap.add_argument("--frame", type=int, default=1,
+                    help="also measure the whole device frame (shading + film)")
     args = ap.parse_args()
 
     import torch
@@ -385,6 +427,9 @@ def main():
     }
     if args.ao:
         out["ao"] = run_ao(args, dist, world, rt, prim, pixid, n_prim)
+    if args.frame:
+        _, lights = spray_amd.engine.host_parse_scene(SCENE, SCENES)
+        out["frame"] = run_frame(args, dist, world, rt, cam, lights)
     if args.ooc == 1 or (args.ooc < 0 and world == 1):
         out["ooc"] = run_ooc(args, rt, prim, n_prim)
     if args.insitu == 1 or (args.insitu < 0 and world > 1):

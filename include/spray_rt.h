@@ -60,6 +60,7 @@ extern "C" {
 #define SPRAY_RT_ERR_STATE (-3)
 #define SPRAY_RT_ERR_NOMEM (-4)
 #define SPRAY_RT_ERR_LIMIT (-5)
+#define SPRAY_RT_ERR_UNSUPPORTED (-6) /* a case the reference aborts on */
 
 #define SPRAY_RT_INVALID_ID 0xFFFFFFFFu
 #define SPRAY_RT_MAX_SCENE_DOMAINS 256
@@ -312,6 +313,101 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                               const spray_rt_hit* hits, const int32_t* pixid, size_t M,
                               int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
                               uint32_t* d_count);
+
+/* ---- frames: path shading, film, tiles (callers of the hot path) ---- */
+/* The shading pass of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-227) /
+ * ooc::ShaderAo (src/ooc/ooc_shader_ao.h:92-197), the retire-to-image step
+ * (ooc_tcontext.inl:123-135 + HdrImage::add, src/display/image.h:90-99), the
+ * blocking-tile list (src/render/tile.cc:52-200) and the PPM writer
+ * (image.h:167-204), so a whole ooc-mode frame runs on the device. */
+#define SPRAY_RT_SHADER_PT 0
+#define SPRAY_RT_SHADER_AO 1
+#define SPRAY_RT_LIGHT_POINT 0      /* PointLight, src/render/light.h:38-62 */
+#define SPRAY_RT_LIGHT_HEMISPHERE 1 /* DiffuseHemisphereLight, light.h:64-90 */
+#define SPRAY_RT_BSDF_DIFFUSE 0     /* reflection.h:234-262 */
+#define SPRAY_RT_BSDF_MIRROR 1      /* reflection.h:264-287 */
+#define SPRAY_RT_BSDF_GLASS 2       /* p = eta_exterior, eta_interior; :292-330 */
+#define SPRAY_RT_BSDF_TRANSMISSION 3 /* p = eta_exterior, eta_interior; :335-364 */
+#define SPRAY_RT_MAX_LIGHTS 8
+
+typedef struct spray_rt_light {
+  int32_t type;
+  float pos[3];      /* point lights */
+  float radiance[3];
+} spray_rt_light;
+
+typedef struct spray_rt_bsdf {
+  int32_t type;
+  float p[3];
+} spray_rt_bsdf;
+
+/* Shader configuration (spray::Config: bounces, ao_samples, ks, shininess;
+ * the scene's lights). */
+typedef struct spray_rt_shader {
+  int32_t shader;   /* SPRAY_RT_SHADER_* */
+  int32_t bounces;  /* >= 1 */
+  int32_t samples;  /* AO rays per hit / samples per area light */
+  int32_t nlights;  /* <= SPRAY_RT_MAX_LIGHTS */
+  float ks[3];
+  float shininess;
+  spray_rt_light lights[SPRAY_RT_MAX_LIGHTS];
+} spray_rt_shader;
+
+/* Per-domain BSDFs (Scene::getBsdf(domain), scene_loader.cc:88-130), host
+ * array of n entries; domains without an entry are diffuse. */
+int spray_rt_set_bsdfs(spray_rt_ctx_t ctx, int n, const spray_rt_bsdf* bsdfs);
+/* Shadow rays one path slot can spawn per shading pass (the slot stride of
+ * the shadow buffers). */
+int spray_rt_shadow_slots(const spray_rt_shader* shader);
+/* Closest hit of the rays with valid[i] != 0 (device buffers); hits of the
+ * other rays are left as they were. */
+int spray_rt_intersect_scene_masked(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                    size_t M, const uint8_t* valid, spray_rt_hit* hits);
+/* One shading pass over M positional path slots at bounce `bounce` (0 =
+ * camera rays).  In: rays[i] (the ray that produced hits[i]), w[i] = path
+ * weight (float4, xyz), valid[i].  Out: shadow k of slot i at
+ * i*ns + k (ns = spray_rt_shadow_slots) in shadows / sw (float4) /
+ * svalid; the next radiance ray in rays[i], w[i], valid[i].  d_stats
+ * (device uint64[4], may be NULL) += {cases the reference aborts on (they
+ * are skipped), shadow rays spawned, next radiance rays, live slots shaded}.
+ * pixid seeds the AO sampler, samid the PT samplers.  Device buffers. */
+int spray_rt_shade(spray_rt_ctx_t ctx, const spray_rt_shader* shader, int bounce,
+                   spray_rt_ray* rays, const spray_rt_hit* hits, float* w,
+                   uint8_t* valid, const int32_t* pixid, const int32_t* samid, size_t M,
+                   spray_rt_ray* shadows, float* sw, uint8_t* svalid,
+                   unsigned long long* d_stats);
+/* image_rgba[pixid] += scale * sw for every unoccluded shadow of the M
+ * slots (pixel groups of spp consecutive slots, ns shadows each); float +=
+ * double product, in slot then shadow order.  Device buffers. */
+int spray_rt_film(spray_rt_ctx_t ctx, float* image_rgba, const int32_t* pixid, size_t M,
+                  int spp, int ns, const float* sw, const uint8_t* svalid,
+                  const uint8_t* occluded, double scale);
+/* One tile of an ooc-mode frame on the device, enqueued on the context's
+ * stream (no host synchronisation): eye rays (genMultiEyes), then per
+ * bounce closest hit -> shade -> any hit of the shadows -> film.
+ * image_rgba: device float[image_w*image_h*4]. */
+int spray_rt_render_tile(spray_rt_ctx_t ctx, const spray_rt_shader* shader,
+                         const float cam[14], int image_w, int spp, int tx, int ty, int tw,
+                         int th, float* image_rgba);
+/* Totals of the tiles rendered since the last reset (synchronises the
+ * stream): out[3] = radiance rays traced, shadow rays traced, shading cases
+ * the reference aborts on (skipped here).  Returns SPRAY_RT_ERR_UNSUPPORTED
+ * when out[2] > 0. */
+int spray_rt_frame_stats(spray_rt_ctx_t ctx, unsigned long long out[3], int reset);
+/* This rank's tiles of the image, tiles[cap][4] = x, y, w, h; *n = count
+ * (tiles = NULL, cap = 0: count only).
+ *  SPRAY_RT_TILES_IMAGE (ooc mode, ImageScheduleTileList::init, tile.cc:
+ *    317-391): the rank's vertical stripe (makeVerticalStripe) cut into
+ *    horizontal tiles of at most max_samples_per_rank samples;
+ *  SPRAY_RT_TILES_BLOCKING (in-situ mode, TileList::init, tile.cc:52-182):
+ *    square-ish blocking tiles of the image, each cut to the rank's
+ *    horizontal stripe (makeHorizontalStripe; empty stripes w = h = 0). */
+#define SPRAY_RT_TILES_IMAGE 0
+#define SPRAY_RT_TILES_BLOCKING 1
+int spray_rt_tile_list(int schedule, int image_w, int image_h, int spp, int nranks, int rank,
+                       long long max_samples_per_rank, int* tiles, int cap, int* n);
+/* HdrImage::writePpm (image.h:167-204): P3, max 1023, bottom row first. */
+int spray_rt_write_ppm(const char* path, const float* rgba_host, int w, int h);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,12 @@ int spray_host_parse_scene(const char* desc, const char* ply_path,
                            int* ndomains, int* nlights, float* boxes,
                            float* transforms, float* lights, char* err,
                            size_t errlen);
+/* Host-only: the domains' materials (SceneLoader::parseMaterial,
+ * src/io/scene_loader.cc:88-130) as spray_rt_bsdf records (diffuse/mirror:
+ * p = albedo/reflectance; glass/transmission: p = eta_a, eta_b).  NULL
+ * bsdfs -> count only. */
+int spray_host_scene_bsdfs(const char* desc, int* ndomains, spray_rt_bsdf* bsdfs, char* err,
+                           size_t errlen);
 /* Host-only: TriMeshBuffer::load for domain `id` (PLY, transform, normals).
  * NULL arrays -> sizes only. */
 int spray_host_domain_mesh(const char* desc, const char* ply_path, int id,

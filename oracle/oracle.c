@@ -1153,26 +1153,62 @@ size_t or_spawn_shadows_pt(const float* org, const float* dir,
   return m;
 }
 
+/* getCosineHemisphereSample (render/sampler.cc:54-60): ConcentricDiskSampling
+ * (sampler.h:49-92; theta *= SPRAY_PI / 4.f is a double product, M_PI being
+ * a double), cosineHemisphereSample (sampler.h:112-120), localToWorld
+ * (sampler.h:101-110), cosineHemispherePdf (sampler.h:126-128).  glm calls
+ * cosf/sinf; here cos/sin are evaluated in double and rounded once, which
+ * the GPU path reproduces bit for bit (the two may differ from glibc's cosf
+ * by an ulp on rare arguments). */
+static void cosine_hemisphere(float u1, float u2, f3 N, f3* wi, float* pdf) {
+  float sx = 2 * u1 - 1, sy = 2 * u2 - 1, rr, th, dx, dy;
+  if (sx == 0.0f && sy == 0.0f) {
+    dx = 0.0f; dy = 0.0f;
+  } else {
+    if (sx >= -sy) {
+      if (sx > sy) { rr = sx; th = sy > 0.0f ? sy / rr : 8.0f + sy / rr; }
+      else { rr = sy; th = 2.0f - sx / rr; }
+    } else {
+      if (sx <= sy) { rr = -sx; th = 4.0f - sy / rr; }
+      else { rr = -sy; th = 6.0f + sx / rr; }
+    }
+    th = (float)((double)th * (3.14159265358979323846 / 4.0));
+    dx = rr * (float)cos((double)th);
+    dy = rr * (float)sin((double)th);
+  }
+  f3 lv = mk3(dx, dy, sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy)));
+  lv = gnorm(lv);
+  f3 dx0 = mk3(0, N.z, -N.y), dx1 = mk3(-N.z, 0, N.x);
+  f3 ax = gnorm(gdot(dx0, dx0) > gdot(dx1, dx1) ? dx0 : dx1);
+  f3 ay = gnorm(gcross(N, ax));
+  f3 w = mk3((ax.x * lv.x + ay.x * lv.y) + N.x * lv.z,
+             (ax.y * lv.x + ay.y * lv.y) + N.y * lv.z,
+             (ax.z * lv.x + ay.z * lv.y) + N.z * lv.z);
+  *wi = gnorm(w);
+  *pdf = lv.z * 0.3183098861837907f;
+}
+
+static inline f3 unpack_rgb(uint32_t c) {
+  /* util::unpack(uint32, vec3&): channel * SPRAY_1_OVER_255 (a double) */
+  return mk3((float)((double)((c >> 16) & 0xff) * 0.00392156862745098),
+             (float)((double)((c >> 8) & 0xff) * 0.00392156862745098),
+             (float)((double)(c & 0xff) * 0.00392156862745098));
+}
+
 /* ooc::ShaderAo, src/ooc/ooc_shader_ao.h:120-146 with DiffuseBsdf::
- * sampleRandom (reflection.h:245-249), getCosineHemisphereSample
- * (sampler.cc:54-60), ConcentricDiskSampling (sampler.h:49-92) and
- * localToWorld (sampler.h:101-110).  Uses libm cos/sin: the GPU path agrees
- * to a few ulps, not bit-exactly. */
+ * sampleRandom (reflection.h:245-249) and cosine_hemisphere above. */
 size_t or_spawn_shadows_ao(const float* org, const float* dir,
                            const int32_t* pixid, const or_hit* hits, size_t n,
                            int nsamples, float* sorg, float* sdir,
                            int32_t* src) {
   size_t m = 0;
-  const float PI = 3.14159265358979323846f;
   for (size_t i = 0; i < n; ++i) {
     const or_hit* h = hits + i;
     if (h->domain < 0) continue;
     const float* o = org + 3 * i;
     const float* d = dir + 3 * i;
     f3 pos = mk3(d[0] * h->t + o[0], d[1] * h->t + o[1], d[2] * h->t + o[2]);
-    f3 kd = mk3((float)((double)((h->color >> 16) & 0xff) * 0.00392156862745098),
-                (float)((double)((h->color >> 8) & 0xff) * 0.00392156862745098),
-                (float)((double)(h->color & 0xff) * 0.00392156862745098));
+    f3 kd = unpack_rgb(h->color);
     f3 normal = mk3(h->ns[0], h->ns[1], h->ns[2]);
     f3 wo = mk3(-d[0], -d[1], -d[2]);
     float cos_i = gdot(wo, normal);
@@ -1182,31 +1218,9 @@ size_t or_spawn_shadows_ao(const float* org, const float* dir,
     for (int l = 0; l < nsamples; ++l) {
       uint32_t st = or_sampler_init1(pixid[i] * (l + 1));
       float u1 = or_sampler_get1d(&st), u2 = or_sampler_get1d(&st);
-      float sx = 2 * u1 - 1, sy = 2 * u2 - 1, rr, th, dx, dy;
-      if (sx == 0.0f && sy == 0.0f) {
-        dx = 0.0f; dy = 0.0f;
-      } else {
-        if (sx >= -sy) {
-          if (sx > sy) { rr = sx; th = sy > 0.0f ? sy / rr : 8.0f + sy / rr; }
-          else { rr = sy; th = 2.0f - sx / rr; }
-        } else {
-          if (sx <= sy) { rr = -sx; th = 4.0f - sy / rr; }
-          else { rr = -sy; th = 6.0f + sx / rr; }
-        }
-        th *= PI / 4.f;
-        dx = rr * cosf(th);
-        dy = rr * sinf(th);
-      }
-      f3 lv = mk3(dx, dy, sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy)));
-      lv = gnorm(lv);
-      f3 dx0 = mk3(0, N.z, -N.y), dx1 = mk3(-N.z, 0, N.x);
-      f3 ax = gnorm(gdot(dx0, dx0) > gdot(dx1, dx1) ? dx0 : dx1);
-      f3 ay = gnorm(gcross(N, ax));
-      f3 w = mk3((ax.x * lv.x + ay.x * lv.y) + N.x * lv.z,
-                 (ax.y * lv.x + ay.y * lv.y) + N.y * lv.z,
-                 (ax.z * lv.x + ay.z * lv.y) + N.z * lv.z);
-      w = gnorm(w);
-      float pdf = lv.z * 0.3183098861837907f;
+      f3 w;
+      float pdf;
+      cosine_hemisphere(u1, u2, N, &w, &pdf);
       float costheta = clampf(gdot(N, w), 0.0f, 1.0f);
       float kdv[3] = {kd.x, kd.y, kd.z};
       int pos_any = 0;
@@ -1222,4 +1236,227 @@ size_t or_spawn_shadows_ao(const float* org, const float* dir,
     }
   }
   return m;
+}
+
+/* ------------------------------------------------------------------ */
+/* path shading + film (callers of the hot path) */
+/* ------------------------------------------------------------------ */
+
+int or_shadow_slots(const or_shader* P) {
+  if (P->shader == OR_SHADER_AO) return P->samples;
+  int k = 0;
+  for (int l = 0; l < P->nlights; ++l)
+    k += P->lights[l].type == OR_LIGHT_HEMISPHERE ? P->samples : 1;
+  return k;
+}
+
+static inline int has_pos(f3 v) { return v.x > 0.0f || v.y > 0.0f || v.z > 0.0f; }
+
+/* blinnPhong, render/reflection.h:202-214 (glm::pow rounded once from
+ * double, as cos/sin above) */
+static f3 blinn_phong(float costheta, f3 kd, const float ks[3], float shin, f3 li,
+                      f3 wi, f3 n, f3 wo) {
+  f3 hh = gnorm(add3(wi, wo));
+  float ndh = clampf(gdot(n, hh), 0.0f, 1.0f);
+  float pw = (float)pow((double)ndh, (double)shin);
+  return mk3(li.x * (kd.x * costheta + ks[0] * pw), li.y * (kd.y * costheta + ks[1] * pw),
+             li.z * (kd.z * costheta + ks[2] * pw));
+}
+
+/* FrDielectric / Refract, reflection.h:134-172 */
+static float fr_dielectric(float cosI, float etaI, float etaT, f3 wo, f3 nff, f3* wt) {
+  float sin2I = fmaxf(0.0f, 1.0f - (cosI * cosI));
+  float eta = etaI / etaT;
+  float sin2T = eta * eta * sin2I;
+  if (sin2T >= 1.0f) return 1.0f;
+  float cosT = sqrtf(1.0f - sin2T);
+  float rparl = ((etaT * cosI) - (etaI * cosT)) / ((etaT * cosI) + (etaI * cosT));
+  float rperp = ((etaI * cosI) - (etaT * cosT)) / ((etaI * cosI) + (etaT * cosT));
+  float fr = (rparl * rparl + rperp * rperp) / 2.0f;
+  float a = eta * cosI - cosT;
+  *wt = mk3((eta * -wo.x) + (nff.x * a), (eta * -wo.y) + (nff.y * a), (eta * -wo.z) + (nff.z * a));
+  return fr;
+}
+static int refract_(float cosI, float etaI, float etaT, f3 wo, f3 nff, f3* wt) {
+  float sin2I = fmaxf(0.0f, 1.0f - (cosI * cosI));
+  float eta = etaI / etaT;
+  float sin2T = eta * eta * sin2I;
+  if (sin2T >= 1.0f) return 0;
+  float cosT = sqrtf(1.0f - sin2T);
+  float a = eta * cosI - cosT;
+  *wt = mk3((eta * -wo.x) + (nff.x * a), (eta * -wo.y) + (nff.y * a), (eta * -wo.z) + (nff.z * a));
+  return 1;
+}
+
+/* One shading pass of ooc::ShaderPt (ooc_shader_pt.h:93-227) or
+ * ooc::ShaderAo (ooc_shader_ao.h:92-197) over n positional path slots at
+ * bounce `bounce` (0 = camera rays; next_actual_depth = bounce + 1 since
+ * this restatement resolves every hit exactly, with no speculative
+ * history).  Slot i's shadow k lands at i*nshadow + k; its next radiance
+ * ray replaces (org, dir) i with valid[i] = 1.  Returns the number of
+ * cases the reference aborts on (glass with both reflection and
+ * transmission, ooc_shader_pt.h:206-207; AO on a delta BSDF,
+ * reflection.h:268-271), which are skipped. */
+int or_shade(const or_shader* P, const or_bsdf* bsdf, int nbsdf, int bounce,
+             float* org, float* dir, const or_hit* hits, float* w, uint8_t* valid,
+             const int32_t* pixid, const int32_t* samid, size_t n, float* sorg,
+             float* sdir, float* sw, uint8_t* svalid) {
+  const int ns = or_shadow_slots(P);
+  const int nad = bounce + 1;
+  int bad = 0;
+  for (size_t i = 0; i < n; ++i) {
+    for (int k = 0; k < ns; ++k) svalid[i * ns + k] = 0;
+    if (!valid[i]) continue;
+    valid[i] = 0;
+    const or_hit* h = hits + i;
+    if (h->domain < 0) continue;
+    const float* o = org + 3 * i;
+    const float* d = dir + 3 * i;
+    f3 pos = mk3(d[0] * h->t + o[0], d[1] * h->t + o[1], d[2] * h->t + o[2]);
+    f3 kd = unpack_rgb(h->color);
+    f3 normal = mk3(h->ns[0], h->ns[1], h->ns[2]);
+    f3 wo = mk3(-d[0], -d[1], -d[2]);
+    f3 Lin = mk3(w[3 * i], w[3 * i + 1], w[3 * i + 2]);
+    float cos_i = gdot(wo, normal);
+    int entering = cos_i > 0.0f;
+    f3 nff = gnorm(entering ? normal : mk3(-normal.x, -normal.y, -normal.z));
+    int bt = (h->domain < nbsdf && bsdf) ? bsdf[h->domain].type : OR_BSDF_DIFFUSE;
+    int delta = bt != OR_BSDF_DIFFUSE;
+    f3 wi;
+    float pdf;
+#define EMIT(k, L)                                                         \
+  do {                                                                     \
+    size_t j_ = i * ns + (k);                                              \
+    sorg[3 * j_] = pos.x; sorg[3 * j_ + 1] = pos.y; sorg[3 * j_ + 2] = pos.z; \
+    sdir[3 * j_] = wi.x; sdir[3 * j_ + 1] = wi.y; sdir[3 * j_ + 2] = wi.z;  \
+    sw[3 * j_] = (L).x; sw[3 * j_ + 1] = (L).y; sw[3 * j_ + 2] = (L).z;     \
+    svalid[j_] = 1;                                                        \
+  } while (0)
+    if (P->shader == OR_SHADER_AO) {
+      if (delta) {
+        ++bad;
+      } else {
+        const float ao_w = 1.0f / (float)P->samples;
+        for (int l = 0; l < P->samples; ++l) {
+          uint32_t st = or_sampler_init1(pixid[i] * (l + 1));
+          float u1 = or_sampler_get1d(&st), u2 = or_sampler_get1d(&st);
+          cosine_hemisphere(u1, u2, nff, &wi, &pdf);
+          float ct = clampf(gdot(nff, wi), 0.0f, 1.0f);
+          float s = 0.3183098861837907f * ct * ao_w / pdf;
+          f3 L = mk3((Lin.x * kd.x) * s, (Lin.y * kd.y) * s, (Lin.z * kd.z) * s);
+          if (has_pos(L)) EMIT(l, L);
+        }
+      }
+    } else if (!delta) {
+      uint32_t st = or_sampler_init1(samid[i] * nad);
+      int k = 0;
+      for (int l = 0; l < P->nlights; ++l) {
+        const or_light* lt = P->lights + l;
+        f3 li = mk3(lt->radiance[0], lt->radiance[1], lt->radiance[2]);
+        if (lt->type == OR_LIGHT_HEMISPHERE) {
+          for (int s = 0; s < P->samples; ++s, ++k) {
+            float u1 = or_sampler_get1d(&st), u2 = or_sampler_get1d(&st);
+            cosine_hemisphere(u1, u2, nff, &wi, &pdf);
+            if (pdf > 0.0f) {
+              float ct = clampf(gdot(nff, wi), 0.0f, 1.0f);
+              f3 bp = blinn_phong(ct, kd, P->ks, P->shininess, li, wi, nff, wo);
+              float sc = 1.0f / (pdf * (float)P->samples);
+              f3 L = mk3((Lin.x * bp.x) * sc, (Lin.y * bp.y) * sc, (Lin.z * bp.z) * sc);
+              if (has_pos(L)) EMIT(k, L);
+            }
+          }
+        } else {
+          wi = gnorm(sub3(mk3(lt->pos[0], lt->pos[1], lt->pos[2]), pos));
+          pdf = 1.0f;
+          float ct = clampf(gdot(nff, wi), 0.0f, 1.0f);
+          f3 bp = blinn_phong(ct, kd, P->ks, P->shininess, li, wi, nff, wo);
+          float sc = 1.0f / pdf;
+          f3 L = mk3((Lin.x * bp.x) * sc, (Lin.y * bp.y) * sc, (Lin.z * bp.z) * sc);
+          if (has_pos(L)) EMIT(k, L);
+          ++k;
+        }
+      }
+    }
+#undef EMIT
+    if (nad >= P->bounces) continue;
+    f3 won = gnorm(wo);
+    f3 nw = mk3(0, 0, 0);
+    int emit = 0;
+    if (delta) {
+      if (cos_i != 0.0f) {
+        float c = clampf(cos_i, -1.0f, 1.0f);
+        float ac = fabsf(c);
+        if (!entering) c = ac;
+        int refl = 0, trans = 0;
+        float fr = 0.0f;
+        f3 wt = mk3(0, 0, 0);
+        const float* bp = bsdf[h->domain].p;
+        if (bt == OR_BSDF_MIRROR) {
+          fr = 1.0f; refl = 1;
+        } else if (bt == OR_BSDF_GLASS) {
+          float eI = entering ? bp[0] : bp[1], eT = entering ? bp[1] : bp[0];
+          fr = fr_dielectric(c, eI, eT, won, nff, &wt);
+          if (fr == 1.0f) refl = 1;
+          else if (fr == 0.0f) trans = 1;
+          else { refl = 1; trans = 1; }
+        } else { /* transmission */
+          float eI = entering ? bp[0] : bp[1], eT = entering ? bp[1] : bp[0];
+          if (refract_(c, eI, eT, won, nff, &wt)) { trans = 1; fr = 0.0f; }
+          else { refl = 1; fr = 1.0f; }
+        }
+        if (refl && trans) {
+          ++bad;
+        } else if (refl) {
+          float s2 = 2.0f * gdot(won, nff);
+          wi = gnorm(mk3(-won.x + s2 * nff.x, -won.y + s2 * nff.y, -won.z + s2 * nff.z));
+          float s = fr / ac;
+          nw = mk3(Lin.x * s, Lin.y * s, Lin.z * s);
+          emit = has_pos(nw);
+        } else if (trans) {
+          wi = gnorm(wt);
+          float s = (1.0f - fr) / ac;
+          nw = mk3(Lin.x * s, Lin.y * s, Lin.z * s);
+          emit = has_pos(nw);
+        }
+      }
+    } else {
+      uint32_t st = or_sampler_init1(samid[i] * nad);
+      float u1 = or_sampler_get1d(&st), u2 = or_sampler_get1d(&st);
+      cosine_hemisphere(u1, u2, nff, &wi, &pdf);
+      float ct = clampf(gdot(nff, wi), 0.0f, 1.0f);
+      nw = mk3((((Lin.x * kd.x) * 0.3183098861837907f) * ct) / pdf,
+               (((Lin.y * kd.y) * 0.3183098861837907f) * ct) / pdf,
+               (((Lin.z * kd.z) * 0.3183098861837907f) * ct) / pdf);
+      emit = has_pos(nw);
+    }
+    if (emit) {
+      org[3 * i] = pos.x; org[3 * i + 1] = pos.y; org[3 * i + 2] = pos.z;
+      dir[3 * i] = wi.x; dir[3 * i + 1] = wi.y; dir[3 * i + 2] = wi.z;
+      w[3 * i] = nw.x; w[3 * i + 1] = nw.y; w[3 * i + 2] = nw.z;
+      valid[i] = 1;
+    }
+  }
+  return bad;
+}
+
+/* TContext::retire (ooc_tcontext.inl:123-135) + HdrImage::add(pixid, rgb,
+ * double scale) (display/image.h:90-99): every unoccluded shadow adds
+ * scale * w to its pixel (float += double product).  Slots come in pixel
+ * groups of spp (the eye-ray layout); within a pixel the adds run in slot
+ * order then shadow order -- the reference's order is that of its OpenMP
+ * retire loop, which this fixes. */
+void or_film(float* image, const int32_t* pixid, size_t n, int spp, int nshadow,
+             const float* sw, const uint8_t* svalid, const uint8_t* occ,
+             double scale) {
+  (void)spp;
+  for (size_t i = 0; i < n; ++i) {
+    float* px = image + 4 * (size_t)pixid[i];
+    for (int k = 0; k < nshadow; ++k) {
+      size_t j = i * nshadow + k;
+      if (!svalid[j] || occ[j]) continue;
+      px[0] = (float)((double)px[0] + scale * (double)sw[3 * j]);
+      px[1] = (float)((double)px[1] + scale * (double)sw[3 * j + 1]);
+      px[2] = (float)((double)px[2] + scale * (double)sw[3 * j + 2]);
+    }
+  }
 }

@@ -155,6 +155,44 @@ size_t or_spawn_shadows_ao(const float* org, const float* dir,
                            int nsamples, float* sorg, float* sdir,
                            int32_t* src_index_out);
 
+/* ---- path shading + film (ooc::ShaderPt / ShaderAo, TContext::retire) ---- */
+#define OR_SHADER_PT 0
+#define OR_SHADER_AO 1
+#define OR_LIGHT_POINT 0      /* PointLight, render/light.h:38-62 */
+#define OR_LIGHT_HEMISPHERE 1 /* DiffuseHemisphereLight, light.h:64-90 */
+#define OR_BSDF_DIFFUSE 0
+#define OR_BSDF_MIRROR 1
+#define OR_BSDF_GLASS 2        /* p = eta_exterior, eta_interior */
+#define OR_BSDF_TRANSMISSION 3 /* p = eta_exterior, eta_interior */
+#define OR_MAX_LIGHTS 8
+typedef struct or_light {
+  int32_t type;
+  float pos[3];
+  float radiance[3];
+} or_light;
+typedef struct or_bsdf {
+  int32_t type;
+  float p[3];
+} or_bsdf;
+typedef struct or_shader {
+  int32_t shader;  /* OR_SHADER_* */
+  int32_t bounces; /* cfg.bounces */
+  int32_t samples; /* cfg.ao_samples */
+  int32_t nlights;
+  float ks[3];
+  float shininess;
+  or_light lights[OR_MAX_LIGHTS];
+} or_shader;
+int or_shadow_slots(const or_shader* P);
+/* w[n][3] path weights, sw[n*nshadow][3]; see oracle.c */
+int or_shade(const or_shader* P, const or_bsdf* bsdf, int nbsdf, int bounce,
+             float* org, float* dir, const or_hit* hits, float* w, uint8_t* valid,
+             const int32_t* pixid, const int32_t* samid, size_t n, float* sorg,
+             float* sdir, float* sw, uint8_t* svalid);
+void or_film(float* image_rgba, const int32_t* pixid, size_t n, int spp, int nshadow,
+             const float* sw, const uint8_t* svalid, const uint8_t* occ,
+             double scale);
+
 #ifdef __cplusplus
 }
 #endif

@@ -109,6 +109,9 @@ def _declare(L):
         "or_scene_occluded": (None, [P, P, P, SZ, P, P, C.c_int]),
         "or_spawn_shadows_pt": (SZ, [P, P, P, SZ, P, P, P, C.c_float, P, P, P]),
         "or_spawn_shadows_ao": (SZ, [P, P, P, P, SZ, C.c_int, P, P, P]),
+        "or_shadow_slots": (C.c_int, [P]),
+        "or_shade": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, SZ, P, P, P, P]),
+        "or_film": (None, [P, P, SZ, C.c_int, C.c_int, P, P, P, C.c_double]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -540,3 +543,176 @@ def spawn_shadows_ao(org, d, pixid, hits, nsamples):
                                   _p(np.ascontiguousarray(pixid, np.int32)), _p(hits),
                                   n, int(nsamples), _p(so), _p(sd), _p(src))
     return so[:m].copy(), sd[:m].copy(), src[:m].copy()
+
+
+# ---------------------------------------------------------------------------
+# frames: path shading, film, tiles (ooc::ShaderPt / ShaderAo, TContext::
+# retire, TileList) -- the CPU restatement the frame-layer tests check
+# ---------------------------------------------------------------------------
+SHADER_PT, SHADER_AO = 0, 1
+LIGHT_POINT, LIGHT_HEMISPHERE = 0, 1
+BSDF = {"diffuse": 0, "mirror": 1, "glass": 2, "transmission": 3}
+
+
+class OrLight(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pos", C.c_float * 3), ("radiance", C.c_float * 3)]
+
+
+class OrBsdf(C.Structure):
+    _fields_ = [("type", C.c_int32), ("p", C.c_float * 3)]
+
+
+class OrShader(C.Structure):
+    _fields_ = [("shader", C.c_int32), ("bounces", C.c_int32), ("samples", C.c_int32),
+                ("nlights", C.c_int32), ("ks", C.c_float * 3), ("shininess", C.c_float),
+                ("lights", OrLight * 8)]
+
+
+def shader(kind="pt", bounces=1, samples=1, ks=(0.4, 0.4, 0.4), shininess=10.0, lights=()):
+    """lights: rows (type, x, y, z, r, g, b)."""
+    s = OrShader()
+    s.shader = SHADER_AO if kind == "ao" else SHADER_PT
+    s.bounces, s.samples, s.nlights = int(bounces), int(samples), len(lights)
+    for k in range(3):
+        s.ks[k] = float(ks[k])
+    s.shininess = float(shininess)
+    for i, l in enumerate(lights):
+        s.lights[i].type = int(l[0])
+        for k in range(3):
+            s.lights[i].pos[k] = float(l[1 + k])
+            s.lights[i].radiance[k] = float(l[4 + k])
+    return s
+
+
+def scene_lights(lights):
+    """parse_spray lights -> rows (type, x, y, z, r, g, b)."""
+    rows = []
+    for l in lights:
+        if l["type"] == "point":
+            rows.append((LIGHT_POINT, *l["pos"], *l["rad"]))
+        else:
+            rows.append((LIGHT_HEMISPHERE, 0, 0, 0, *l["rad"]))
+    return rows
+
+
+def scene_bsdfs(domains):
+    """SceneLoader::parseMaterial (scene_loader.cc:88-130) -> (type, p0, p1, p2)."""
+    out = []
+    for d in domains:
+        t = d["mtl"]
+        if not t:
+            raise ValueError("domain %d has no material" % d["id"])
+        if t[0] not in BSDF:
+            raise ValueError("unknown material type " + t[0])
+        want = 4 if t[0] in ("diffuse", "mirror") else 3
+        if len(t) != want:
+            raise ValueError("wrong number of material parameters")
+        p = [float(x) for x in t[1:]] + [0.0] * (4 - want)
+        out.append((BSDF[t[0]], *[np.float32(x) for x in p]))
+    return out
+
+
+def _bsdf_array(bsdfs):
+    arr = (OrBsdf * max(len(bsdfs), 1))()
+    for i, b in enumerate(bsdfs):
+        arr[i].type = int(b[0])
+        for k in range(3):
+            arr[i].p[k] = float(b[1 + k])
+    return arr
+
+
+def shadow_slots(sh):
+    return lib().or_shadow_slots(C.byref(sh))
+
+
+def shade(sh, bsdfs, bounce, org, d, hits, w, valid, pixid, samid):
+    """One shading pass; org/d/w/valid updated in place (next rays).
+    Returns (sorg, sdir, sw, svalid, aborts)."""
+    n = len(org)
+    ns = shadow_slots(sh)
+    so = np.zeros((n * ns, 3), np.float32)
+    sd = np.zeros((n * ns, 3), np.float32)
+    sw = np.zeros((n * ns, 3), np.float32)
+    sv = np.zeros(n * ns, np.uint8)
+    arr = _bsdf_array(bsdfs)
+    for a in (org, d, w, valid):
+        assert a.flags["C_CONTIGUOUS"]
+    bad = lib().or_shade(C.byref(sh), C.addressof(arr), len(bsdfs), int(bounce), _p(org),
+                         _p(d), _p(hits), _p(w), _p(valid),
+                         _p(np.ascontiguousarray(pixid, np.int32)),
+                         _p(np.ascontiguousarray(samid, np.int32)), n, _p(so), _p(sd),
+                         _p(sw), _p(sv))
+    return so, sd, sw, sv, bad
+
+
+def film(image, pixid, spp, ns, sw, svalid, occ, scale):
+    assert image.dtype == np.float32 and image.flags["C_CONTIGUOUS"]
+    lib().or_film(_p(image), _p(np.ascontiguousarray(pixid, np.int32)), len(pixid), int(spp),
+                  int(ns), _p(f32(sw)), _p(np.ascontiguousarray(svalid, np.uint8)),
+                  _p(np.ascontiguousarray(occ, np.uint8)), float(scale))
+
+
+def tile_list(image_w, image_h, spp, nranks=1, rank=0, max_samples_per_rank=1024 * 1024,
+              schedule="image"):
+    """"image": ImageScheduleTileList::init + makeVerticalStripe
+    (src/render/tile.cc:208-230, 317-391); "blocking": BlockingTileList::init
+    + TileList::init + makeHorizontalStripe (tile.cc:52-206)."""
+    if schedule == "image":
+        sw = max(image_w // nranks, 1)
+        sx = rank * sw
+        if sx >= image_w:
+            return []
+        vw = image_w - sx if (sx + sw > image_w or rank == nranks - 1) else sw
+        est = (vw * image_h * spp + max_samples_per_rank - 1) // max_samples_per_rank
+        th = image_h // est
+        assert th > 0
+        return [(sx, y, vw, min(th, image_h - y)) for y in range(0, image_h, th)]
+    total = image_w * image_h * spp
+    per_cluster = max_samples_per_rank * nranks
+    ntiles = (total + per_cluster - 1) // per_cluster
+    n1 = int(math.ceil(math.sqrt(float(ntiles))))
+    assert 0 < n1 <= image_w and n1 <= image_h
+    tw, th = image_w // n1, image_h // n1
+    out = []
+    for y in range(0, image_h, th):
+        for x in range(0, image_w, tw):
+            w, h = min(tw, image_w - x), min(th, image_h - y)
+            assert w * h * spp <= per_cluster
+            sh = max(h // nranks, 1)
+            sy = y + rank * sh
+            if sy >= y + h:
+                out.append((0, sy, 0, 0))
+            else:
+                hh = (y + h - sy) if (sy + sh > y + h or rank == nranks - 1) else sh
+                out.append((x, sy, w, hh))
+    return out
+
+
+def render_tile(scene, sh, bsdfs, cam, image_w, spp, tile, image):
+    """One tile of an ooc-mode frame (ooc::Tracer::trace with exact
+    resolution): eye rays, then per bounce closest hit of the live slots ->
+    shade -> any hit of the shadows -> film.  Returns (radiance rays,
+    shadow rays, aborts)."""
+    org, d, pix, sam = eye_rays_ooc(cam, image_w, spp, tile)
+    n = len(org)
+    w = np.ones((n, 3), np.float32)
+    valid = np.ones(n, np.uint8)
+    hits = np.zeros(n, HIT_DTYPE)
+    ns = shadow_slots(sh)
+    nrad, nsh, bad = 0, 0, 0
+    for b in range(sh.bounces):
+        live = np.flatnonzero(valid)
+        nrad += len(live)
+        if len(live):
+            h, _ = scene.intersect(org[live], d[live])
+            hits[live] = h
+        so, sd, sw, sv, k = shade(sh, bsdfs, b, org, d, hits, w, valid, pix, sam)
+        bad += k
+        occ = np.zeros(n * ns, np.uint8)
+        sel = np.flatnonzero(sv)
+        nsh += len(sel)
+        if len(sel):
+            o, _ = scene.occluded(so[sel], sd[sel])
+            occ[sel] = o
+        film(image, pix, spp, ns, sw, sv, occ, 1.0 / spp)
+    return nrad, nsh, bad

@@ -7,6 +7,7 @@ binding.  There is no CPU fallback.
 """
 from .engine import (HIT_DTYPE, INVALID_ID, RAY_DTYPE, RTC_ISECT_DTYPE, OocCache,
                      RtContext, Scene, SprayRtError, camera_init, make_rays, ooc_scene)
+from . import frame
 
 __all__ = ["RtContext", "Scene", "OocCache", "ooc_scene", "SprayRtError", "camera_init",
-           "make_rays", "RAY_DTYPE", "HIT_DTYPE", "RTC_ISECT_DTYPE", "INVALID_ID"]
+           "make_rays", "RAY_DTYPE", "HIT_DTYPE", "RTC_ISECT_DTYPE", "INVALID_ID", "frame"]

@@ -33,6 +33,30 @@ assert RTC_ISECT_DTYPE.itemsize == 96
 
 INVALID_ID = 0xFFFFFFFF
 
+# frame-layer records (include/spray_rt.h)
+SHADER_PT, SHADER_AO = 0, 1
+LIGHT_POINT, LIGHT_HEMISPHERE = 0, 1
+BSDF_DIFFUSE, BSDF_MIRROR, BSDF_GLASS, BSDF_TRANSMISSION = 0, 1, 2, 3
+MAX_LIGHTS = 8
+
+
+class LightRec(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pos", C.c_float * 3), ("radiance", C.c_float * 3)]
+
+
+class BsdfRec(C.Structure):
+    _fields_ = [("type", C.c_int32), ("p", C.c_float * 3)]
+
+
+class ShaderRec(C.Structure):
+    _fields_ = [("shader", C.c_int32), ("bounces", C.c_int32), ("samples", C.c_int32),
+                ("nlights", C.c_int32), ("ks", C.c_float * 3), ("shininess", C.c_float),
+                ("lights", LightRec * MAX_LIGHTS)]
+
+
+assert C.sizeof(LightRec) == 28 and C.sizeof(BsdfRec) == 16
+assert C.sizeof(ShaderRec) == 32 + 28 * MAX_LIGHTS
+
 # every symbol the public headers declare: (restype, argtypes)
 P = C.c_void_p
 SZ = C.c_size_t
@@ -78,6 +102,15 @@ SIGNATURES = {
     "spray_rt_route": (I, [P, P, SZ, P]),
     "spray_rt_intersect_scene_keyed": (I, [P, P, SZ, P, P]),
     "spray_rt_spawn_shadows_pt": (I, [P, P, P, SZ, P, P, P, P]),
+    "spray_rt_set_bsdfs": (I, [P, I, P]),
+    "spray_rt_shadow_slots": (I, [P]),
+    "spray_rt_intersect_scene_masked": (I, [P, P, SZ, P, P]),
+    "spray_rt_shade": (I, [P, P, I, P, P, P, P, P, P, SZ, P, P, P, P]),
+    "spray_rt_film": (I, [P, P, P, SZ, I, I, P, P, P, C.c_double]),
+    "spray_rt_render_tile": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "spray_rt_frame_stats": (I, [P, P, I]),
+    "spray_rt_tile_list": (I, [I, I, I, I, I, I, C.c_longlong, P, I, P]),
+    "spray_rt_write_ppm": (I, [C.c_char_p, P, I, I]),
     # spray_scene.h
     "spray_scene_create": (I, [C.c_char_p, C.c_char_p, I, I, P, C.c_char_p, SZ]),
     "spray_scene_destroy": (I, [P]),
@@ -94,6 +127,7 @@ SIGNATURES = {
     "spray_camera_init": (I, [P, P, P, C.c_float, I, I, P]),
     "spray_scene_domain_mesh": (I, [P, I, P, P, P, P, P, P]),
     "spray_host_parse_scene": (I, [C.c_char_p, C.c_char_p, P, P, P, P, P, C.c_char_p, SZ]),
+    "spray_host_scene_bsdfs": (I, [C.c_char_p, P, P, C.c_char_p, SZ]),
     "spray_host_domain_mesh": (I, [C.c_char_p, C.c_char_p, I, P, P, P, P, P, P]),
 }
 

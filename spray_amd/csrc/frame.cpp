@@ -1,0 +1,313 @@
+// frame.cpp -- C ABI of the frame layer: per-domain BSDFs, the shading pass,
+// the film, whole-tile rendering on the device, the blocking-tile list and
+// the PPM writer.  The per-tile driver is the device form of
+// ooc::Tracer::trace (src/ooc/ooc_tracer.inl:184-234) with the exact
+// (non-speculative) resolution of every ray: eye rays -> per bounce
+// closest hit -> shade -> any hit of the shadows -> film.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "rt_ctx.h"
+#include "rt_kernels.h"
+#include "spray_rt.h"
+
+using namespace spray_rt;
+using namespace spray_rt::detail;
+
+namespace {
+
+bool shader_ok(const spray_rt_shader* P) {
+  if (!P || P->bounces < 1 || P->nlights < 0 || P->nlights > SPRAY_RT_MAX_LIGHTS) return false;
+  if (P->shader == SPRAY_RT_SHADER_AO) return P->samples >= 1;
+  if (P->shader != SPRAY_RT_SHADER_PT) return false;
+  for (int l = 0; l < P->nlights; ++l) {
+    const int t = P->lights[l].type;
+    if (t != SPRAY_RT_LIGHT_POINT && t != SPRAY_RT_LIGHT_HEMISPHERE) return false;
+    if (t == SPRAY_RT_LIGHT_HEMISPHERE && P->samples < 1) return false;
+  }
+  return true;
+}
+
+// carve consecutive 256-B aligned pieces out of one allocation
+struct Carve {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(size_t n) {
+    T* p = reinterpret_cast<T*>(base + off);
+    off += align256(n * sizeof(T));
+    return p;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int spray_rt_shadow_slots(const spray_rt_shader* P) {
+  if (!shader_ok(P)) return SPRAY_RT_ERR_ARG;
+  if (P->shader == SPRAY_RT_SHADER_AO) return P->samples;
+  int k = 0;
+  for (int l = 0; l < P->nlights; ++l)
+    k += P->lights[l].type == SPRAY_RT_LIGHT_HEMISPHERE ? P->samples : 1;
+  return k;
+}
+
+int spray_rt_set_bsdfs(spray_rt_ctx_t c, int n, const spray_rt_bsdf* bsdfs) {
+  if (!c || n < 0 || (n && !bsdfs)) return c ? fail(c, SPRAY_RT_ERR_ARG, "bad bsdf table") : SPRAY_RT_ERR_ARG;
+  for (int i = 0; i < n; ++i) {
+    const int t = bsdfs[i].type;
+    if (t < SPRAY_RT_BSDF_DIFFUSE || t > SPRAY_RT_BSDF_TRANSMISSION)
+      return fail(c, SPRAY_RT_ERR_ARG, "bsdf %d: unknown type %d", i, t);
+    if ((t == SPRAY_RT_BSDF_GLASS || t == SPRAY_RT_BSDF_TRANSMISSION) &&
+        !(bsdfs[i].p[0] > 0.f && bsdfs[i].p[1] > 0.f))
+      return fail(c, SPRAY_RT_ERR_ARG, "bsdf %d: refractive indices must be positive", i);
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));  // the table may be in use
+  if (c->d_bsdf) HIPCHK(c, hipFree(c->d_bsdf));
+  c->d_bsdf = nullptr;
+  c->nbsdf = 0;
+  if (n == 0) return SPRAY_RT_OK;
+  HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_bsdf), n * sizeof(spray_rt_bsdf)));
+  HIPCHK(c, hipMemcpy(c->d_bsdf, bsdfs, n * sizeof(spray_rt_bsdf), hipMemcpyHostToDevice));
+  c->nbsdf = n;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_intersect_scene_masked(spray_rt_ctx_t c, const spray_rt_ray* rays, size_t M,
+                                    const uint8_t* valid, spray_rt_hit* hits) {
+  int r = scene_common(c, rays, M, hits);
+  if (r) return r;
+  if (M == 0) return SPRAY_RT_OK;
+  if (M > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "M > 2^32");
+  if (!valid || !is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(valid))
+    return fail(c, SPRAY_RT_ERR_ARG, "masked closest hit needs device buffers");
+  hipStream_t s = stream_of(c);
+  size_t temp = 0;
+  HIPCHK(c, launch_select_flagged(s, valid, M, nullptr, nullptr, nullptr, &temp));
+  const size_t b_idx = align256(M * sizeof(uint32_t));
+  r = ensure(c, &c->d_sel, &c->sel_cap, b_idx + 256 + temp);
+  if (r) return r;
+  char* base = static_cast<char*>(c->d_sel);
+  uint32_t* idx = reinterpret_cast<uint32_t*>(base);
+  uint32_t* num = reinterpret_cast<uint32_t*>(base + b_idx);
+  HIPCHK(c, launch_select_flagged(s, valid, M, idx, num, base + b_idx + 256, &temp));
+  HIPCHK(c, launch_scene_intersect_indexed(s, view(c), rays, M, idx, num, hits));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_shade(spray_rt_ctx_t c, const spray_rt_shader* P, int bounce, spray_rt_ray* rays,
+                   const spray_rt_hit* hits, float* w, uint8_t* valid, const int32_t* pixid,
+                   const int32_t* samid, size_t M, spray_rt_ray* shadows, float* sw,
+                   uint8_t* svalid, unsigned long long* d_stats) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (!shader_ok(P) || bounce < 0) return fail(c, SPRAY_RT_ERR_ARG, "bad shader configuration");
+  if (M == 0) return SPRAY_RT_OK;
+  const int ns = spray_rt_shadow_slots(P);
+  const bool need_pix = P->shader == SPRAY_RT_SHADER_AO;
+  if (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(w) ||
+      !is_device_ptr(valid) || (need_pix && !is_device_ptr(pixid)) ||
+      (!need_pix && !is_device_ptr(samid)) || (ns && (!is_device_ptr(shadows) ||
+                                                      !is_device_ptr(sw) ||
+                                                      !is_device_ptr(svalid))) ||
+      (d_stats && !is_device_ptr(d_stats)))
+    return fail(c, SPRAY_RT_ERR_ARG, "shading buffers must be device memory");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, launch_shade(stream_of(c), *P, c->d_bsdf, c->nbsdf, bounce, ns, rays, hits, w, valid,
+                         pixid, samid, M, shadows, sw, svalid, d_stats));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_film(spray_rt_ctx_t c, float* image, const int32_t* pixid, size_t M, int spp,
+                  int ns, const float* sw, const uint8_t* svalid, const uint8_t* occ,
+                  double scale) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (spp <= 0 || ns < 0 || M % size_t(spp))
+    return fail(c, SPRAY_RT_ERR_ARG, "film: M must be a multiple of spp");
+  if (M == 0 || ns == 0) return SPRAY_RT_OK;
+  if (!is_device_ptr(image) || !is_device_ptr(pixid) || !is_device_ptr(sw) ||
+      !is_device_ptr(svalid) || !is_device_ptr(occ))
+    return fail(c, SPRAY_RT_ERR_ARG, "film buffers must be device memory");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, launch_film(stream_of(c), image, pixid, M, spp, ns, sw, svalid, occ, scale));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float cam[14],
+                         int image_w, int spp, int tx, int ty, int tw, int th, float* image) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (!shader_ok(P) || !cam || spp <= 0 || tw < 0 || th < 0 || image_w <= 0 || tx < 0 ||
+      ty < 0 || tx + tw > image_w || ty + th > int(cam[13]))
+    return fail(c, SPRAY_RT_ERR_ARG, "bad render arguments");
+  const size_t M = size_t(tw) * th * spp;
+  if (M == 0) return SPRAY_RT_OK;
+  const int ns = spray_rt_shadow_slots(P);
+  const size_t MS = M * size_t(ns);
+  if (M > 0xFFFFFFFFull || MS > 0xFFFFFFFFull)
+    return fail(c, SPRAY_RT_ERR_LIMIT, "tile too large (samples x shadow slots > 2^32)");
+  if (!is_device_ptr(image)) return fail(c, SPRAY_RT_ERR_ARG, "image must be device memory");
+  int r = scene_common(c, image, M, image);
+  if (r) return r;
+  const size_t bytes = align256(M * sizeof(spray_rt_ray)) + align256(M * sizeof(spray_rt_hit)) +
+                       align256(M * 16) + align256(M) + 2 * align256(M * 4) +
+                       align256(MS * sizeof(spray_rt_ray)) + align256(MS * 16) +
+                       2 * align256(MS);
+  r = ensure(c, &c->d_frame, &c->frame_cap, bytes);
+  if (r) return r;
+  hipStream_t s = stream_of(c);
+  if (!c->d_fstats) {
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_fstats), 4 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, 4 * sizeof(unsigned long long), s));
+  }
+  Carve cv{static_cast<char*>(c->d_frame)};
+  spray_rt_ray* rays = cv.take<spray_rt_ray>(M);
+  spray_rt_hit* hits = cv.take<spray_rt_hit>(M);
+  float* w = cv.take<float>(4 * M);
+  uint8_t* valid = cv.take<uint8_t>(M);
+  int32_t* pixid = cv.take<int32_t>(M);
+  int32_t* samid = cv.take<int32_t>(M);
+  spray_rt_ray* sh = cv.take<spray_rt_ray>(MS);
+  float* sw = cv.take<float>(4 * MS);
+  uint8_t* sv = cv.take<uint8_t>(MS);
+  uint8_t* occ = cv.take<uint8_t>(MS);
+  HIPCHK(c, launch_eye_rays_ooc(s, cam, image_w, spp, tx, ty, tw, th, rays, pixid, samid));
+  HIPCHK(c, launch_path_init(s, w, valid, M));
+  const double scale = 1.0 / double(spp);
+  const int user = c->coherence;
+  for (int b = 0; b < P->bounces; ++b) {
+    if (b == 0) {
+      // camera rays: coherent packets
+      c->coherence = SPRAY_RT_RAYS_COHERENT;
+      hipError_t e = launch_scene_intersect(s, view(c), rays, M, hits, nullptr);
+      c->coherence = user;
+      HIPCHK(c, e);
+    } else {
+      r = spray_rt_intersect_scene_masked(c, rays, M, valid, hits);
+      if (r) return r;
+    }
+    HIPCHK(c, launch_shade(s, *P, c->d_bsdf, c->nbsdf, b, ns, rays, hits, w, valid, pixid, samid,
+                           M, sh, sw, sv, c->d_fstats));
+    if (ns) {
+      r = spray_rt_occluded_scene_masked(c, sh, MS, sv, occ);
+      if (r) return r;
+      HIPCHK(c, launch_film(s, image, pixid, M, spp, ns, sw, sv, occ, scale));
+    }
+  }
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_frame_stats(spray_rt_ctx_t c, unsigned long long out[3], int reset) {
+  if (!c || !out) return SPRAY_RT_ERR_ARG;
+  out[0] = out[1] = out[2] = 0;
+  if (!c->d_fstats) return SPRAY_RT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = stream_of(c);
+  unsigned long long h[4];
+  HIPCHK(c, hipMemcpyAsync(h, c->d_fstats, sizeof(h), hipMemcpyDeviceToHost, s));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, sizeof(h), s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  out[0] = h[3];
+  out[1] = h[1];
+  out[2] = h[0];
+  if (h[0])
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED, "%llu shading cases the reference aborts on", h[0]);
+  return SPRAY_RT_OK;
+}
+
+// ImageScheduleTileList::init (tile.cc:317-391): this rank's vertical
+// stripe of the image (makeVerticalStripe, :208-230) cut into horizontal
+// tiles of at most max_samples_per_rank samples.
+static int image_schedule_tiles(int image_w, int image_h, int spp, int nranks, int rank,
+                                long long max_samples, int* tiles, int cap, int* n) {
+  const int sw = std::max(image_w / nranks, 1);
+  const int sx = rank * sw;
+  *n = 0;
+  if (sx >= image_w) return SPRAY_RT_OK;  // empty stripe: no tiles
+  const int vw = (sx + sw > image_w || rank == nranks - 1) ? image_w - sx : sw;
+  const long long samples = (long long)vw * image_h * spp;
+  const long long est = (samples + max_samples - 1) / max_samples;
+  if (est >= INT_MAX) return SPRAY_RT_ERR_LIMIT;
+  const int th = image_h / int(est);
+  if (th <= 0) return SPRAY_RT_ERR_LIMIT;  // the reference divides by zero here
+  *n = (image_h + th - 1) / th;
+  if (*n > cap) return tiles ? SPRAY_RT_ERR_LIMIT : SPRAY_RT_OK;
+  int k = 0;
+  for (int y = 0; y < image_h; y += th) {
+    int* t = tiles + 4 * k++;
+    t[0] = sx;
+    t[1] = y;
+    t[2] = vw;
+    t[3] = std::min(th, image_h - y);
+  }
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_tile_list(int schedule, int image_w, int image_h, int spp, int nranks, int rank,
+                       long long max_samples_per_rank, int* tiles, int cap, int* n) {
+  if (image_w <= 0 || image_h <= 0 || spp <= 0 || nranks <= 0 || rank < 0 || rank >= nranks ||
+      max_samples_per_rank <= 0 || !n || cap < 0 || (cap && !tiles))
+    return SPRAY_RT_ERR_ARG;
+  if (schedule == SPRAY_RT_TILES_IMAGE)
+    return image_schedule_tiles(image_w, image_h, spp, nranks, rank, max_samples_per_rank,
+                                tiles, cap, n);
+  if (schedule != SPRAY_RT_TILES_BLOCKING) return SPRAY_RT_ERR_ARG;
+  // BlockingTileList::init (tile.cc:52-153)
+  const long long total = (long long)image_w * image_h * spp;
+  const long long per_cluster = max_samples_per_rank * nranks;
+  const long long ntiles = (total + per_cluster - 1) / per_cluster;
+  const long long n1 = (long long)std::ceil(std::sqrt(double(ntiles)));
+  if (n1 <= 0 || n1 > image_w || n1 > image_h) return SPRAY_RT_ERR_LIMIT;
+  const int tw = int(image_w / n1), thh = int(image_h / n1);
+  const int nx = (image_w + tw - 1) / tw, ny = (image_h + thh - 1) / thh;
+  *n = nx * ny;
+  if (*n > cap) return tiles ? SPRAY_RT_ERR_LIMIT : SPRAY_RT_OK;
+  int k = 0;
+  for (int y = 0; y < image_h; y += thh) {
+    for (int x = 0; x < image_w; x += tw) {
+      const int w = std::min(tw, image_w - x), h = std::min(thh, image_h - y);
+      if ((long long)w * h * spp > per_cluster) return SPRAY_RT_ERR_LIMIT;  // CHECK_LE, :128
+      // makeHorizontalStripe (tile.cc:184-206)
+      const int sh = std::max(h / nranks, 1);
+      const int sy = y + rank * sh, yend = y + h;
+      int* t = tiles + 4 * k++;
+      if (sy >= yend) {
+        t[0] = 0; t[1] = sy; t[2] = 0; t[3] = 0;
+      } else {
+        t[0] = x;
+        t[1] = sy;
+        t[2] = w;
+        t[3] = (sy + sh > yend || rank == nranks - 1) ? yend - sy : sh;
+      }
+    }
+  }
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_write_ppm(const char* path, const float* rgba, int w, int h) {
+  if (!path || !rgba || w <= 0 || h <= 0) return SPRAY_RT_ERR_ARG;
+  FILE* f = std::fopen(path, "w");
+  if (!f) return SPRAY_RT_ERR_ARG;
+  std::fprintf(f, "P3\n%d %d\n1023\n", w, h);
+  for (int y = h - 1; y > -1; --y) {
+    for (int x = 0; x < w; ++x) {
+      const float* p = rgba + 4 * (size_t(y) * w + x);
+      unsigned v[3];
+      for (int k = 0; k < 3; ++k) {
+        // glm::clamp(c * 1023.f, 0, 1023) then (unsigned) truncation
+        const float t = p[k] * 1023.f;
+        const float cl = std::min(std::max(t, 0.0f), 1023.0f);
+        v[k] = unsigned(cl);
+      }
+      std::fprintf(f, "%u %u %u\n", v[0], v[1], v[2]);
+    }
+  }
+  return std::fclose(f) == 0 ? SPRAY_RT_OK : SPRAY_RT_ERR_ARG;
+}
+
+}  // extern "C"

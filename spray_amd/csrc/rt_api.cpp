@@ -242,6 +242,30 @@ int run_rtc(spray_rt_ctx* c, const int* slots, const size_t* offsets, int nseg,
 
 }  // namespace
 
+int spray_rt::detail::scene_common(spray_rt_ctx* c, const void* rays, size_t M,
+                                   const void* out) {
+  if (!c) return SPRAY_RT_ERR_ARG;
+  if (c->ndom <= 0) return fail(c, SPRAY_RT_ERR_STATE, "no domain bounds set");
+  if (c->ndom > SPRAY_RT_MAX_SCENE_DOMAINS)
+    return fail(c, SPRAY_RT_ERR_LIMIT, "scene path supports <= %d domains",
+                SPRAY_RT_MAX_SCENE_DOMAINS);
+  if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->d_heads)
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), kQueues * 32 * sizeof(uint32_t)));
+  return prepare(c);
+}
+
+// The kernels' view of the resident scene; max_depth picks the traversal
+// stack size (the LDS footprint, hence the occupancy) of the launch.
+SceneView spray_rt::detail::view(const spray_rt_ctx* c) {
+  int depth = c->tlas_depth;
+  for (const SlotHost& sh : c->slots)
+    if (sh.dmem) depth = std::max(depth, sh.depth);
+  return SceneView{c->d_slots, c->d_dom2slot, c->d_domtrav, c->d_boxes, c->ndom,
+                   c->d_tlas,  c->ntlas,      c->d_heads,   depth,        c->coherence};
+}
+
 extern "C" {
 
 int spray_rt_create(int hip_device, spray_rt_ctx_t* out) {
@@ -277,7 +301,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
   }
   void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_domtrav, c->d_owner, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
-                  c->d_block_counts, c->d_heads, c->d_sel};
+                  c->d_block_counts, c->d_heads, c->d_sel, c->d_bsdf, c->d_frame, c->d_fstats};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -511,30 +535,6 @@ int spray_rt_domains1M(spray_rt_ctx_t c, const float* org, const float* dir,
   HIPCHK(c, hipMemcpyAsync(counts, c->d_stage3, b_cnt, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return SPRAY_RT_OK;
-}
-
-static int scene_common(spray_rt_ctx* c, const void* rays, size_t M,
-                        const void* out) {
-  if (!c) return SPRAY_RT_ERR_ARG;
-  if (c->ndom <= 0) return fail(c, SPRAY_RT_ERR_STATE, "no domain bounds set");
-  if (c->ndom > SPRAY_RT_MAX_SCENE_DOMAINS)
-    return fail(c, SPRAY_RT_ERR_LIMIT, "scene path supports <= %d domains",
-                SPRAY_RT_MAX_SCENE_DOMAINS);
-  if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
-  HIPCHK(c, hipSetDevice(c->device));
-  if (!c->d_heads)
-    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), kQueues * 32 * sizeof(uint32_t)));
-  return prepare(c);
-}
-
-// The kernels' view of the resident scene; max_depth picks the traversal
-// stack size (the LDS footprint, hence the occupancy) of the launch.
-static SceneView view(const spray_rt_ctx* c) {
-  int depth = c->tlas_depth;
-  for (const SlotHost& sh : c->slots)
-    if (sh.dmem) depth = std::max(depth, sh.depth);
-  return SceneView{c->d_slots, c->d_dom2slot, c->d_domtrav, c->d_boxes, c->ndom,
-                   c->d_tlas,  c->ntlas,      c->d_heads,   depth,        c->coherence};
 }
 
 // counters: optional device uint64[3] (nodes, tris, visits); exported for the

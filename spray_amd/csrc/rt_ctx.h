@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "rt_common.h"
+#include "rt_kernels.h"
 #include "spray_rt.h"
 
 namespace spray_rt {
@@ -72,6 +73,12 @@ struct spray_rt_ctx {
   void* d_sel = nullptr;        // selected indices + count + select scratch
   size_t sel_cap = 0;
   size_t block_cap = 0;
+  // frame layer
+  spray_rt_bsdf* d_bsdf = nullptr;  // per-domain BSDFs (Scene::getBsdf)
+  int nbsdf = 0;
+  void* d_frame = nullptr;  // render_tile path buffers
+  size_t frame_cap = 0;
+  unsigned long long* d_fstats = nullptr;  // render_tile totals (shade stats)
   std::string err;
 };
 
@@ -102,6 +109,10 @@ hipStream_t stream_of(spray_rt_ctx* c);
 bool is_device_ptr(const void* p);
 // grows *buf to at least bytes (device memory)
 int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes);
+// scene-path entry checks + lazy rebuild of the device scene tables
+int scene_common(spray_rt_ctx* c, const void* rays, size_t M, const void* out);
+// the kernels' view of the resident scene (coherence = the context's)
+SceneView view(const spray_rt_ctx* c);
 
 }  // namespace detail
 }  // namespace spray_rt

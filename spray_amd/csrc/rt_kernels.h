@@ -165,4 +165,21 @@ hipError_t launch_ooc_ah(hipStream_t s, const OocDomain& D, const spray_rt_ray* 
                          const uint32_t* idx, uint32_t n, uint8_t* occ);
 hipError_t launch_ooc_clear_occ(hipStream_t s, const uint8_t* valid, uint8_t* occ, size_t M);
 
+// frame layer (frame_kernels.hip)
+hipError_t launch_shade(hipStream_t s, const spray_rt_shader& P, const spray_rt_bsdf* bsdfs,
+                        int nbsdf, int bounce, int ns, spray_rt_ray* rays,
+                        const spray_rt_hit* hits, float* w, uint8_t* valid,
+                        const int32_t* pixid, const int32_t* samid, size_t M,
+                        spray_rt_ray* shadows, float* sw, uint8_t* svalid,
+                        unsigned long long* stats);
+hipError_t launch_path_init(hipStream_t s, float* w, uint8_t* valid, size_t M);
+hipError_t launch_film(hipStream_t s, float* image, const int32_t* pixid, size_t M, int spp,
+                       int ns, const float* sw, const uint8_t* svalid, const uint8_t* occ,
+                       double scale);
+// closest hit of the rays idx[0 .. *d_num) (selected on the device)
+hipError_t launch_scene_intersect_indexed(hipStream_t s, const SceneView& v,
+                                          const spray_rt_ray* rays, size_t max_n,
+                                          const uint32_t* idx, const uint32_t* d_num,
+                                          spray_rt_hit* hits);
+
 }  // namespace spray_rt

@@ -15,6 +15,7 @@
 #include <cstdint>
 
 #include "rt_device.h"
+#include "shade_device.h"
 
 namespace spray_rt {
 namespace {
@@ -755,27 +756,6 @@ struct Cam {
   float p[14];
 };
 
-__device__ __forceinline__ uint32_t mm_mix(uint32_t hash, uint32_t k) {
-  k *= 0xcc9e2d51u;
-  k = (k << 15) | (k >> 17);
-  k *= 0x1b873593u;
-  hash ^= k;
-  hash = ((hash << 13) | (hash >> 19)) * 5u + 0xe6546b64u;
-  return hash;
-}
-__device__ __forceinline__ uint32_t mm_fin(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x85ebca6bu;
-  h ^= h >> 13;
-  h *= 0xc2b2ae35u;
-  h ^= h >> 16;
-  return h;
-}
-__device__ __forceinline__ float sampler_1d(uint32_t& s) {
-  s = s * 1664525u + 1013904223u;
-  return float(int32_t(s >> 1)) * 4.656612873077392578125e-10f;
-}
-
 // ooc::Tracer::genMultiEyes (src/ooc/ooc_tracer.inl:124-172) + Camera::
 // generateRay (camera.h:168-209), glm operand order.
 __global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
@@ -1057,21 +1037,12 @@ __global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
 // 245-249; getCosineHemisphereSample, sampler.cc:54-60; ConcentricDisk-
 // Sampling, sampler.h:49-92; localToWorld, sampler.h:101-110), seeded by
 // pixid * (l + 1).  Sample l of hit i is emitted when its radiance weight
-// is positive.  Operation order as the oracle (glm); cosf/sinf are the
-// device's, so directions agree with the host to a few ulps.
+// is positive.  Operation order as the oracle (glm), trig rounded once from
+// double (shade_device.h), so directions equal the host's bit for bit.
 struct AoOut {
   float o[3], w[3];
   bool ok;
 };
-__device__ __forceinline__ float gdot3(const float* a, const float* b) {
-  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
-}
-__device__ __forceinline__ void gnorm3(float* a) {
-  const float inv = 1.0f / sqrtf(gdot3(a, a));
-  a[0] *= inv;
-  a[1] *= inv;
-  a[2] *= inv;
-}
 __device__ __forceinline__ AoOut ao_sample(const spray_rt_ray& ray, const spray_rt_hit& h,
                                            int32_t pixid, int l, int nsamples) {
   AoOut r;
@@ -1094,53 +1065,10 @@ __device__ __forceinline__ AoOut ao_sample(const spray_rt_ray& ray, const spray_
   }
   gnorm3(N);
   const float ao_w = 1.0f / float(nsamples);
-  uint32_t st = mm_fin(mm_mix(0u, uint32_t(pixid * (l + 1))));
+  uint32_t st = sampler_init1(pixid * (l + 1));
   const float u1 = sampler_1d(st), u2 = sampler_1d(st);
-  const float sx = 2 * u1 - 1, sy = 2 * u2 - 1;
-  float dx, dy;
-  if (sx == 0.0f && sy == 0.0f) {
-    dx = 0.0f;
-    dy = 0.0f;
-  } else {
-    float rr, th;
-    if (sx >= -sy) {
-      if (sx > sy) {
-        rr = sx;
-        th = sy > 0.0f ? sy / rr : 8.0f + sy / rr;
-      } else {
-        rr = sy;
-        th = 2.0f - sx / rr;
-      }
-    } else {
-      if (sx <= sy) {
-        rr = -sx;
-        th = 4.0f - sy / rr;
-      } else {
-        rr = -sy;
-        th = 6.0f + sx / rr;
-      }
-    }
-    th *= 3.14159265358979323846f / 4.f;
-    dx = rr * cosf(th);
-    dy = rr * sinf(th);
-  }
-  float lv[3] = {dx, dy, sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy))};
-  gnorm3(lv);
-  float dx0[3] = {0.f, N[2], -N[1]}, dx1[3] = {-N[2], 0.f, N[0]};
-  float ax[3];
-  const float* pick = gdot3(dx0, dx0) > gdot3(dx1, dx1) ? dx0 : dx1;
-  ax[0] = pick[0];
-  ax[1] = pick[1];
-  ax[2] = pick[2];
-  gnorm3(ax);
-  float ay[3] = {N[1] * ax[2] - ax[1] * N[2], N[2] * ax[0] - ax[2] * N[0],
-                 N[0] * ax[1] - ax[0] * N[1]};
-  gnorm3(ay);
-  r.w[0] = (ax[0] * lv[0] + ay[0] * lv[1]) + N[0] * lv[2];
-  r.w[1] = (ax[1] * lv[0] + ay[1] * lv[1]) + N[1] * lv[2];
-  r.w[2] = (ax[2] * lv[0] + ay[2] * lv[1]) + N[2] * lv[2];
-  gnorm3(r.w);
-  const float pdf = lv[2] * 0.3183098861837907f;
+  float pdf;
+  cosine_hemisphere(u1, u2, N, r.w, pdf);
   float ct = gdot3(N, r.w);
   ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
 #pragma unroll
@@ -1254,19 +1182,24 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   return hipGetLastError();
 }
 
-// counting variants walk per lane; closest hit walks packets; any hit
-// follows the context's ray-coherence setting
+// counting variants walk per lane; the fused closest-hit forms walk
+// packets; plain closest hit and any hit follow the context's ray-coherence
+// setting
 template <int W, bool ANY, int EPI, int STK>
 static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherence) {
   if (a.counters) return launch_scene_t<W, ANY, true, EPI, STK, 0>(s, a);
-  if (!ANY) return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
-  switch (coherence) {
-    case SPRAY_RT_RAYS_COHERENT:
-      return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
-    case SPRAY_RT_RAYS_INCOHERENT:
-      return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
-    default:
-      return launch_scene_t<W, ANY, false, EPI, STK, 2>(s, a);
+  // the fused spawn / keyed closest-hit forms serve camera rays: packets
+  if constexpr (!ANY && EPI != kEpiNone) {
+    return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
+  } else {
+    switch (coherence) {
+      case SPRAY_RT_RAYS_COHERENT:
+        return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
+      case SPRAY_RT_RAYS_INCOHERENT:
+        return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
+      default:
+        return launch_scene_t<W, ANY, false, EPI, STK, 2>(s, a);
+    }
   }
 }
 
@@ -1355,6 +1288,18 @@ hipError_t launch_scene_occluded_indexed(hipStream_t s, const SceneView& v,
   a.occ = occluded;
   a.counters = counters;
   return launch_scene_w<true, kEpiNone>(s, a, v);
+}
+
+hipError_t launch_scene_intersect_indexed(hipStream_t s, const SceneView& v,
+                                          const spray_rt_ray* rays, size_t max_n,
+                                          const uint32_t* idx, const uint32_t* d_num,
+                                          spray_rt_hit* hits) {
+  if (max_n == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, max_n);
+  a.idx = idx;
+  a.d_count = d_num;
+  a.hits = hits;
+  return launch_scene_w<false, kEpiNone>(s, a, v);
 }
 
 hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,

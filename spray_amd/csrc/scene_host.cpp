@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -759,6 +760,42 @@ int spray_host_parse_scene(const char* desc, const char* ply_path,
       std::memcpy(lights + 7 * i + 1, ls[i].position, 12);
       std::memcpy(lights + 7 * i + 4, ls[i].radiance, 12);
     }
+  return SPRAY_RT_OK;
+}
+
+int spray_host_scene_bsdfs(const char* desc, int* ndomains, spray_rt_bsdf* bsdfs, char* err,
+                           size_t errlen) {
+  if (!desc || !ndomains) return SPRAY_RT_ERR_ARG;
+  std::vector<spray_amd::Domain> doms;
+  std::vector<spray_amd::Light> ls;
+  std::string e;
+  if (!spray_amd::load_scene_file(desc, "", &doms, &ls, &e)) {
+    if (err && errlen) std::snprintf(err, errlen, "%s", e.c_str());
+    return SPRAY_RT_ERR_ARG;
+  }
+  *ndomains = int(doms.size());
+  if (!bsdfs) return SPRAY_RT_OK;
+  // SceneLoader::parseMaterial (src/io/scene_loader.cc:88-130)
+  for (size_t i = 0; i < doms.size(); ++i) {
+    const std::vector<std::string>& t = doms[i].material;
+    spray_rt_bsdf& b = bsdfs[i];
+    b.type = SPRAY_RT_BSDF_DIFFUSE;
+    b.p[0] = b.p[1] = b.p[2] = 0.f;
+    auto bad = [&](const char* why) {
+      if (err && errlen) std::snprintf(err, errlen, "domain %zu: %s", i, why);
+      return SPRAY_RT_ERR_ARG;
+    };
+    if (t.empty()) return bad("no material (the reference's getBsdf would be null)");
+    const std::string& k = t[0];
+    const size_t want = (k == "diffuse" || k == "mirror") ? 4 : 3;
+    if (k == "diffuse") b.type = SPRAY_RT_BSDF_DIFFUSE;
+    else if (k == "mirror") b.type = SPRAY_RT_BSDF_MIRROR;
+    else if (k == "glass") b.type = SPRAY_RT_BSDF_GLASS;
+    else if (k == "transmission") b.type = SPRAY_RT_BSDF_TRANSMISSION;
+    else return bad("unknown material type");
+    if (t.size() != want) return bad("wrong number of material parameters");
+    for (size_t j = 1; j < want; ++j) b.p[j - 1] = float(std::atof(t[j].c_str()));
+  }
   return SPRAY_RT_OK;
 }
 

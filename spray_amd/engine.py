@@ -12,11 +12,11 @@ import ctypes as C
 
 import numpy as np
 
-from ._native import (HIT_DTYPE, INVALID_ID, RAY_DTYPE, RTC_ISECT_DTYPE,
+from ._native import (HIT_DTYPE, INVALID_ID, RAY_DTYPE, RTC_ISECT_DTYPE, BsdfRec,
                       SprayRtError, lib)
 
 __all__ = ["RtContext", "Scene", "OocCache", "ooc_scene", "camera_init", "make_rays",
-           "host_parse_scene",
+           "host_parse_scene", "host_scene_bsdfs",
            "host_domain_mesh", "RAY_DTYPE",
            "HIT_DTYPE", "RTC_ISECT_DTYPE", "INVALID_ID", "SprayRtError"]
 
@@ -82,6 +82,19 @@ def host_parse_scene(desc, ply_path=""):
                                     lights.ctypes.data, err, 1024) != 0:
         raise SprayRtError("parse %s: %s" % (desc, err.value.decode()))
     return boxes, lights
+
+
+def host_scene_bsdfs(desc):
+    """Scene file -> [(type, p0, p1, p2)] per domain (SceneLoader::parseMaterial)."""
+    nd = C.c_int()
+    err = C.create_string_buffer(1024)
+    L = lib()
+    if L.spray_host_scene_bsdfs(desc.encode(), C.byref(nd), None, err, 1024) != 0:
+        raise SprayRtError("parse %s: %s" % (desc, err.value.decode()))
+    arr = (BsdfRec * max(nd.value, 1))()
+    if L.spray_host_scene_bsdfs(desc.encode(), C.byref(nd), C.addressof(arr), err, 1024) != 0:
+        raise SprayRtError("materials of %s: %s" % (desc, err.value.decode()))
+    return [(arr[i].type, arr[i].p[0], arr[i].p[1], arr[i].p[2]) for i in range(nd.value)]
 
 
 def host_domain_mesh(desc, ply_path, domain_id):
@@ -349,6 +362,60 @@ class RtContext:
         e, k6 = _addr(d_count)
         self._check(lib().spray_rt_spawn_shadows_ao(self.h, a, b, p, int(n), int(nsamples),
                                                     c, d, e), "spawn_shadows_ao")
+
+    # ---- frame layer (shading, film, tiles) ----
+    def set_bsdfs(self, bsdfs):
+        """Per-domain BSDFs: a sequence of (type, p0, p1, p2) (Scene::getBsdf)."""
+        n = len(bsdfs)
+        arr = (BsdfRec * max(n, 1))()
+        for i, b in enumerate(bsdfs):
+            arr[i].type = int(b[0])
+            for k in range(3):
+                arr[i].p[k] = float(b[1 + k])
+        self._check(lib().spray_rt_set_bsdfs(self.h, n, C.addressof(arr) if n else None),
+                    "set_bsdfs")
+
+    def intersect_scene_masked(self, rays, valid, hits):
+        """Closest hit of the rays with valid[i] != 0 (device buffers)."""
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        b, k2 = _addr(valid)
+        c, k3 = _addr(hits)
+        self._check(lib().spray_rt_intersect_scene_masked(self.h, a, n, b, c),
+                    "intersect_scene_masked")
+
+    def shade(self, shader, bounce, rays, hits, w, valid, pixid, samid, shadows, sw, svalid,
+              stats=None):
+        """One ShaderPt / ShaderAo pass over positional path slots (device)."""
+        n = _nbytes(rays) // 32
+        ptrs = [_addr(x) for x in (rays, hits, w, valid, pixid, samid, shadows, sw, svalid,
+                                   stats)]
+        a = [p[0] for p in ptrs]
+        self._check(lib().spray_rt_shade(self.h, C.byref(shader), int(bounce), a[0], a[1], a[2],
+                                         a[3], a[4], a[5], n, a[6], a[7], a[8], a[9]), "shade")
+
+    def film(self, image, pixid, n, spp, ns, sw, svalid, occ, scale):
+        """image[pixid] += scale * unoccluded shadow weights (device)."""
+        ptrs = [_addr(x) for x in (image, pixid, sw, svalid, occ)]
+        a = [p[0] for p in ptrs]
+        self._check(lib().spray_rt_film(self.h, a[0], a[1], int(n), int(spp), int(ns), a[2],
+                                        a[3], a[4], float(scale)), "film")
+
+    def render_tile(self, shader, cam, image_w, spp, tile, image):
+        """One tile of an ooc-mode frame, enqueued on the context's stream."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        tx, ty, tw, th = (int(v) for v in tile)
+        a, k1 = _addr(image)
+        self._check(lib().spray_rt_render_tile(self.h, C.byref(shader), cam.ctypes.data,
+                                               int(image_w), int(spp), tx, ty, tw, th, a),
+                    "render_tile")
+
+    def frame_stats(self, reset=True):
+        """(radiance rays, shadow rays) traced by render_tile since the last
+        reset (synchronises); raises on shading cases the reference aborts on."""
+        out = (C.c_ulonglong * 3)()
+        self._check(lib().spray_rt_frame_stats(self.h, out, int(bool(reset))), "frame_stats")
+        return int(out[0]), int(out[1])
 
     def spawn_shadows_pt(self, rays, hits, n, shade, out_rays, out_src, d_count):
         shade = np.ascontiguousarray(shade, np.float32)
