@@ -56,7 +56,7 @@ struct spray_rt_ooc {
   OocScratch q{};
   size_t q_rays = 0;
   void* q_mem = nullptr;
-  uint64_t* tie = nullptr;
+  uint64_t* tie = nullptr;  // per-ray closest-hit key (kOocMissKey: none yet)
   size_t tie_cap = 0;
   std::vector<uint32_t> first;
 };
@@ -83,7 +83,9 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   const size_t b_k = align256(pairs * sizeof(uint16_t));
   const size_t b_v = align256(pairs * sizeof(uint32_t));
   const size_t b_first = align256(257 * sizeof(uint32_t));
-  const size_t total = b_masks + 2 * b_cnt + 2 * b_k + 2 * b_v + b_first + align256(temp);
+  const size_t b_pk = align256(pairs * sizeof(uint64_t));
+  const size_t total =
+      b_masks + 2 * b_cnt + 2 * b_k + 3 * b_v + b_pk + b_first + align256(temp);
   HIPCHK(c, hipMalloc(&o->q_mem, total));
   char* p = static_cast<char*>(o->q_mem);
   auto take = [&](size_t n) {
@@ -99,6 +101,8 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   o->q.val_in = reinterpret_cast<uint32_t*>(take(b_v));
   o->q.val_out = reinterpret_cast<uint32_t*>(take(b_v));
   o->q.first = reinterpret_cast<uint32_t*>(take(b_first));
+  o->q.pkey = reinterpret_cast<uint64_t*>(take(b_pk));
+  o->q.pleaf = reinterpret_cast<uint32_t*>(take(b_v));
   o->q.temp = take(align256(temp));
   o->q.temp_bytes = temp;
   o->q.pair_cap = pairs;
@@ -187,12 +191,28 @@ OocDomain domain_view(const spray_rt_ooc* o, int d, int k, const float* boxes) {
 
 // Drains every non-empty queue, ascending or descending domain order (a
 // closest-hit pass followed by a reversed any-hit pass reuses the domains
-// left resident by the first).
+// left resident by the first), max(1, slots / 2) resident domains per
+// launch: while one batch drains, the LRU victims of the next are the
+// previous batch's slots, so its uploads overlap the drain.
 template <typename Launch>
 int drain(spray_rt_ooc* o, bool reverse, const std::vector<float>& boxes, Launch launch) {
   spray_rt_ctx* c = o->ctx;
   hipStream_t s = stream_of(c);
   const int n = c->ndom;
+  const int per = std::max(1, std::min<int>(kOocBatch, int(o->slot.size()) / 2));
+  OocBatch B{};
+  int bslot[kOocBatch];
+  auto flush = [&]() -> int {
+    if (B.count == 0) return SPRAY_RT_OK;
+    HIPCHK(c, launch(s, B));
+    for (int k = 0; k < B.count; ++k) {
+      HIPCHK(c, hipEventRecord(o->slot[bslot[k]].released, s));
+      o->slot[bslot[k]].pending_release = true;
+    }
+    o->drains += B.count;  // domain queues drained
+    B.count = 0;
+    return SPRAY_RT_OK;
+  };
   for (int k = 0; k < n; ++k) {
     const int d = reverse ? n - 1 - k : k;
     const uint32_t b = o->first[d], e = o->first[d + 1];
@@ -200,12 +220,13 @@ int drain(spray_rt_ooc* o, bool reverse, const std::vector<float>& boxes, Launch
     int sl = -1;
     int r = acquire(o, d, &sl);
     if (r) return r;
-    HIPCHK(c, launch(s, domain_view(o, d, sl, boxes.data()), o->q.val_out + b, e - b));
-    HIPCHK(c, hipEventRecord(o->slot[sl].released, s));
-    o->slot[sl].pending_release = true;
-    ++o->drains;
+    B.d[B.count] = domain_view(o, d, sl, boxes.data());
+    B.begin[B.count] = b;
+    B.n[B.count] = e - b;
+    bslot[B.count] = sl;
+    if (++B.count == per && (r = flush())) return r;
   }
-  return SPRAY_RT_OK;
+  return flush();
 }
 
 int host_boxes(spray_rt_ooc* o, std::vector<float>* boxes) {
@@ -322,11 +343,12 @@ int spray_rt_ooc_intersect(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
   if ((r = host_boxes(o, &boxes))) return r;
   if ((r = build_queues(o, rays, nullptr, M))) return r;
   HIPCHK(c, launch_ooc_init(stream_of(c), hits, o->tie, M));
-  uint64_t* tie = o->tie;
-  return drain(o, false, boxes,
-               [&](hipStream_t s, const OocDomain& D, const uint32_t* idx, uint32_t n) {
-                 return launch_ooc_ch(s, D, rays, idx, n, hits, tie);
-               });
+  uint64_t* key = o->tie;
+  const int W = c->ndom <= 64 ? 1 : 4;
+  return drain(o, false, boxes, [&](hipStream_t s, const OocBatch& B) {
+    return launch_ooc_ch_batch(s, B, W, rays, o->q.val_out, o->q.masks, c->d_boxes, key,
+                               o->q.pkey, o->q.pleaf, hits);
+  });
 }
 
 int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
@@ -341,10 +363,9 @@ int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
   if ((r = host_boxes(o, &boxes))) return r;
   if ((r = build_queues(o, rays, valid, M))) return r;
   HIPCHK(c, launch_ooc_clear_occ(stream_of(c), valid, occluded, M));
-  return drain(o, true, boxes,
-               [&](hipStream_t s, const OocDomain& D, const uint32_t* idx, uint32_t n) {
-                 return launch_ooc_ah(s, D, rays, idx, n, occluded);
-               });
+  return drain(o, true, boxes, [&](hipStream_t s, const OocBatch& B) {
+    return launch_ooc_ah_batch(s, B, rays, o->q.val_out, occluded);
+  });
 }
 
 int spray_rt_ooc_stats(spray_rt_ooc_t o, unsigned long long out[4]) {

@@ -5,10 +5,10 @@
 // time (ooc_tcontext.inl:28-101) while the LRU cache streams the next ones
 // in (lru_cache.cc:65-171).  On the GPU the queues are built in bulk --
 // domain masks, (domain, ray) pairs, one stable radix sort -- and each
-// resident domain drains its queue in one launch.  A ray's closest hit is
-// combined across launches by the order of the sequential walk of its
-// domain list, (t, then (entry t of the domain box, domain id)), so the
-// result is the whole-scene one whatever the drain order.
+// batch of resident domains drains its queues in one launch.  A ray's
+// closest hit is combined across domains by the order of the sequential
+// walk of its domain list, (t, then the list position), so the result is
+// the whole-scene one whatever the drain order.
 #include <hip/hip_runtime.h>
 
 #include <hipcub/device/device_radix_sort.hpp>
@@ -19,12 +19,6 @@
 
 namespace spray_rt {
 namespace {
-
-// orderable bits of a float (total order, -0 < +0)
-__device__ __forceinline__ uint32_t ord_bits(float f) {
-  const uint32_t b = __float_as_uint(f);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
 
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_ooc_masks(
@@ -94,83 +88,161 @@ __global__ void k_ooc_bounds(const uint16_t* __restrict__ key, uint32_t n, int n
 }
 
 __global__ __launch_bounds__(kBlock) void k_ooc_init(spray_rt_hit* __restrict__ hits,
-                                                     uint64_t* __restrict__ tie, size_t M) {
+                                                     uint64_t* __restrict__ key, size_t M) {
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= M) return;
   float4* hp = reinterpret_cast<float4*>(hits + i);
   hp[0] = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
   hp[1] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
   hp[2] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-  tie[i] = ~0ull;
+  key[i] = kOocMissKey;
 }
 
-// Closest hit of the rays queued to one resident domain, merged into the
-// running result of each ray: nearer t wins; an equal t goes to the earlier
-// entry of the ray's domain list (smaller (box entry t, id)).
-// The queue of one domain holds its rays in ascending ray order --
-// neighbouring pixels -- so each wave walks the tree as a packet
-// (trace_tree_packet: one scalar fetch per node per wave).
-__global__ __launch_bounds__(kBlock) void k_ooc_ch(OocDomain D,
-                                                   const spray_rt_ray* __restrict__ rays,
-                                                   const uint32_t* __restrict__ idx,
-                                                   uint32_t n, spray_rt_hit* __restrict__ hits,
-                                                   uint64_t* __restrict__ tie) {
+// The pair handled by this lane of a batch launch: the waves of segment s
+// (one resident domain's queue) are wave0[s] .. wave0[s+1]-1, so a wave
+// always walks one domain tree.  Returns the segment, or -1 past the end.
+__device__ __forceinline__ int batch_pair(const OocBatch& B, uint32_t& pj, bool& valid) {
+  const uint32_t gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+  if (gw >= B.wave0[B.count]) return -1;
+  int s = 0;
+  while (s + 1 < B.count && B.wave0[s + 1] <= gw) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  const uint32_t j = (gw - B.wave0[s]) * 64 + (threadIdx.x & 63);
+  valid = j < B.n[s];
+  pj = B.begin[s] + (valid ? j : 0u);
+  return s;
+}
+
+// Position of domain `dom` in the ray's sorted domain list (ascending
+// (intersectAabb entry t, id), rays.h:71-79): the tie-break of the key.
+template <int W>
+__device__ __forceinline__ uint32_t list_pos(const uint64_t* m, const float* boxes, int dom,
+                                             const DRay& dr) {
+  float tb;
+  aabb_ref(boxes + 6 * dom, dr, tb);
+  uint32_t p = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t bits = m[w];
+    while (bits) {
+      const int j = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      const int b = 64 * w + j;
+      float tm;
+      aabb_ref(boxes + 6 * b, dr, tm);
+      if (tm < tb || (tm == tb && b < dom)) ++p;
+    }
+  }
+  return p;
+}
+
+// Closest hit of the rays queued to up to kOocBatch resident domains in one
+// launch.  Each (ray, domain) pair walks its domain tree as a packet (a
+// queue holds its rays in ascending order: neighbouring pixels) with the
+// ray's current best t as the cut, and a hit enters the ray's 64-bit key
+// (t bits | list position | domain) by atomicMin.  The key order is the
+// sequential walk's winner rule (nearer t, then the earlier list entry) and
+// keys are unique per (ray, domain), so the result is the same in any drain
+// order and any interleaving.  The pair's own key and winning triangle go
+// to pkey / pleaf for k_ooc_ch_resolve.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
+    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
+    const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
+    uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf) {
   __shared__ int32_t wstack[(kBlock / 64) * kStack];
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (blockIdx.x * kBlock + (threadIdx.x & ~63u) >= n) return;  // whole wave idle
-  const bool valid = j < n;
-  const uint32_t i = valid ? idx[j] : 0u;
+  uint32_t pj;
+  bool valid;
+  const int s = batch_pair(B, pj, valid);
+  if (s < 0) return;
+  const OocDomain& D = B.d[s];
+  const uint32_t i = valid ? idx[pj] : 0u;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  float4 h0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+  uint64_t k0 = kOocMissKey;
   if (valid) {
     const float4* rp = reinterpret_cast<const float4*>(rays + i);
     o4 = rp[0];
     d4 = rp[1];
-    h0 = reinterpret_cast<const float4*>(hits + i)[0];
+    k0 = __hip_atomic_load(key + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  float4* hp = reinterpret_cast<float4*>(hits + i);
-  const bool have = __float_as_uint(h0.w) != 0xFFFFFFFFu;
-  const float tcur = have ? h0.x : d4.w;
-  // the domain's own nearest hit with t <= tcur (ties at tcur included)
+  // the domain's own nearest hit with t <= the ray's best so far (ties at
+  // that t included: the list position decides them)
+  const float tcur = k0 == kOocMissKey ? d4.w : __uint_as_float(uint32_t(k0 >> 32));
   Best best{tcur, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool act = valid, hit = false;
   trace_tree_packet<false>(reinterpret_cast<uint64_t>(D.nodes),
                            reinterpret_cast<uint64_t>(D.tris),
                            reinterpret_cast<uint64_t>(D.prims), r, o4.w, 0.f, best, act, hit,
                            wstack + (threadIdx.x >> 6) * kStack);
-  if (!valid || best.leaf == 0xFFFFFFFFu) return;
-  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  float tm;
-  aabb_ref(D.box, dr, tm);
-  const uint64_t mine = (uint64_t(ord_bits(tm)) << 32) | uint32_t(D.domain);
-  if (have && !(best.t < tcur) && !(mine < tie[i])) return;
-  SlotDesc s{};
-  s.tris = static_cast<const float*>(D.tris);
-  s.faces = D.faces;
-  s.colors = D.colors;
-  s.normals = D.normals;
-  float hu, hv;
-  const float4 c = hit_uv(s, r, o4.w, best.leaf, hu, hv);
-  uint32_t color;
-  float nsx, nsy, nsz;
-  epilogue(s, best.prim, hu, hv, color, nsx, nsy, nsz);
-  hp[0] = make_float4(best.t, hu, hv, __uint_as_float(best.prim));
-  hp[1] = make_float4(c.y, c.z, c.w, __uint_as_float(color));
-  hp[2] = make_float4(nsx, nsy, nsz, __int_as_float(D.domain));
-  tie[i] = mine;
+  if (!valid) return;
+  uint64_t mine = kOocMissKey;
+  if (best.leaf != 0xFFFFFFFFu) {
+    uint64_t m[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
+    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    mine = (uint64_t(__float_as_uint(best.t)) << 32) |
+           (uint64_t(list_pos<W>(m, boxes, D.domain, dr)) << 16) | uint64_t(D.domain);
+    atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
+  }
+  pkey[pj] = mine;
+  pleaf[pj] = best.leaf;
 }
 
-// Any hit of the rays queued to one resident domain, OR-ed into occ.
-__global__ __launch_bounds__(kBlock) void k_ooc_ah(OocDomain D,
-                                                   const spray_rt_ray* __restrict__ rays,
-                                                   const uint32_t* __restrict__ idx,
-                                                   uint32_t n, uint8_t* __restrict__ occ) {
+// Hit records of the batch's winners: the one pair whose key equals its
+// ray's minimum runs updateIntersection (trimesh_buffer.cc:328-360) while
+// its domain is still resident.  A later batch with a smaller key rewrites
+// the record.
+__global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
+    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
+    const uint64_t* __restrict__ key, const uint64_t* __restrict__ pkey,
+    const uint32_t* __restrict__ pleaf, spray_rt_hit* __restrict__ hits) {
+  uint32_t pj;
+  bool valid;
+  const int s = batch_pair(B, pj, valid);
+  if (s < 0 || !valid) return;
+  const uint64_t mine = pkey[pj];
+  if (mine == kOocMissKey) return;
+  const uint32_t i = idx[pj];
+  if (key[i] != mine) return;
+  const OocDomain& D = B.d[s];
+  const float4* rp = reinterpret_cast<const float4*>(rays + i);
+  const float4 o4 = rp[0], d4 = rp[1];
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  SlotDesc sd{};
+  sd.tris = static_cast<const float*>(D.tris);
+  sd.faces = D.faces;
+  sd.colors = D.colors;
+  sd.normals = D.normals;
+  const uint32_t leaf = pleaf[pj];
+  const uint32_t prim = reinterpret_cast<const GAS uint32_t*>(gptr(D.prims))[leaf];
+  float hu, hv;
+  const float4 c = hit_uv(sd, r, o4.w, leaf, hu, hv);
+  uint32_t color;
+  float nsx, nsy, nsz;
+  epilogue(sd, prim, hu, hv, color, nsx, nsy, nsz);
+  float4* hp = reinterpret_cast<float4*>(hits + i);
+  hp[0] = make_float4(__uint_as_float(uint32_t(mine >> 32)), hu, hv, __uint_as_float(prim));
+  hp[1] = make_float4(c.y, c.z, c.w, __uint_as_float(color));
+  hp[2] = make_float4(nsx, nsy, nsz, __int_as_float(D.domain));
+}
+
+// Any hit of the rays queued to the batch's domains, OR-ed into occ (a ray
+// already occluded by an earlier batch is skipped; same-batch writers all
+// store 1).
+__global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(OocBatch B,
+                                                         const spray_rt_ray* __restrict__ rays,
+                                                         const uint32_t* __restrict__ idx,
+                                                         uint8_t* __restrict__ occ) {
   __shared__ int32_t wstack[(kBlock / 64) * kStack];
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (blockIdx.x * kBlock + (threadIdx.x & ~63u) >= n) return;  // whole wave idle
-  const uint32_t i = j < n ? idx[j] : 0u;
-  const bool valid = j < n && !occ[i];  // else occluded by an earlier domain
+  uint32_t pj;
+  bool ok;
+  const int s = batch_pair(B, pj, ok);
+  if (s < 0) return;
+  const OocDomain& D = B.d[s];
+  const uint32_t i = ok ? idx[pj] : 0u;
+  const bool valid = ok && !occ[i];
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
   if (valid) {
     const float4* rp = reinterpret_cast<const float4*>(rays + i);
@@ -250,23 +322,41 @@ size_t ooc_temp_bytes(size_t M, size_t pairs) {
   return a > b ? a : b;
 }
 
-hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* tie, size_t M) {
+hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* key, size_t M) {
   if (M == 0) return hipSuccess;
-  k_ooc_init<<<grid_for(M), kBlock, 0, s>>>(hits, tie, M);
+  k_ooc_init<<<grid_for(M), kBlock, 0, s>>>(hits, key, M);
   return hipGetLastError();
 }
 
-hipError_t launch_ooc_ch(hipStream_t s, const OocDomain& D, const spray_rt_ray* rays,
-                         const uint32_t* idx, uint32_t n, spray_rt_hit* hits, uint64_t* tie) {
-  if (n == 0) return hipSuccess;
-  k_ooc_ch<<<grid_for(n), kBlock, 0, s>>>(D, rays, idx, n, hits, tie);
+static unsigned batch_grid(OocBatch& B) {
+  B.wave0[0] = 0;
+  for (int k = 0; k < B.count; ++k) B.wave0[k + 1] = B.wave0[k] + (B.n[k] + 63) / 64;
+  return (B.wave0[B.count] + kBlock / 64 - 1) / (kBlock / 64);
+}
+
+hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
+                               const uint32_t* idx, const uint64_t* masks, const float* boxes,
+                               uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
+                               spray_rt_hit* hits) {
+  if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
+  const unsigned g = batch_grid(B);
+  if (g == 0) return hipSuccess;
+  if (W == 1)
+    k_ooc_ch_batch<1><<<g, kBlock, 0, s>>>(B, rays, idx, masks, boxes, key, pkey, pleaf);
+  else
+    k_ooc_ch_batch<4><<<g, kBlock, 0, s>>>(B, rays, idx, masks, boxes, key, pkey, pleaf);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, idx, key, pkey, pleaf, hits);
   return hipGetLastError();
 }
 
-hipError_t launch_ooc_ah(hipStream_t s, const OocDomain& D, const spray_rt_ray* rays,
-                         const uint32_t* idx, uint32_t n, uint8_t* occ) {
-  if (n == 0) return hipSuccess;
-  k_ooc_ah<<<grid_for(n), kBlock, 0, s>>>(D, rays, idx, n, occ);
+hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, const spray_rt_ray* rays,
+                               const uint32_t* idx, uint8_t* occ) {
+  if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
+  const unsigned g = batch_grid(B);
+  if (g == 0) return hipSuccess;
+  k_ooc_ah_batch<<<g, kBlock, 0, s>>>(B, rays, idx, occ);
   return hipGetLastError();
 }
 

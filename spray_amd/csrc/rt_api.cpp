@@ -803,9 +803,8 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
             !is_device_ptr(out_rays) || !is_device_ptr(d_count)))
     return fail(c, SPRAY_RT_ERR_ARG, "spawn buffers must be device memory");
   HIPCHK(c, hipSetDevice(c->device));
-  size_t nb = (M + kBlock - 1) / kBlock + 1;
   void* bc = c->d_block_counts;
-  int r = ensure(c, &bc, &c->block_cap, nb * sizeof(uint32_t));
+  int r = ensure(c, &bc, &c->block_cap, ao_scratch_bytes(M, nsamples));
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
   HIPCHK(c, launch_spawn_ao(stream_of(c), rays, hits, pixid, M, nsamples, out_rays, out_src,

@@ -295,6 +295,69 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
   return false;
 }
 
+// Any hit, one ray per lane, as a "while-while" walk with postponed leaves
+// (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
+// descending inner nodes until every active lane of the wave holds a leaf,
+// then the lanes test their leaves' triangles together.  Leaf tests (the
+// expensive, divergent part of the per-lane walk) then run with most lanes
+// active instead of one lane's leaf stalling the rest at every step.  The
+// result -- is there a hit with tnear < t <= tfar -- does not depend on the
+// visit order, and culling stays conservative, so it equals trace_tree's.
+// Leaves go through the per-lane stack like inner nodes; a visit still
+// pushes at most one entry, so the stack bound (tree depth) is unchanged.
+__device__ __forceinline__ bool occluded_tree_ww(const void* nodes, const void* tris,
+                                                 const Ray& r, float tnear, float tfar,
+                                                 int32_t* stk) {
+  int sp = 0;
+  int32_t cur = 0;       // next entry: inner node >= 0, leaf < 0, kNone = done
+  int32_t leaf = kNone;  // the parked leaf
+  for (;;) {
+    while (cur >= 0 && cur != kNone) {
+      float4 n0, n1, n2, n3;
+      ld_node(nodes, 4 * size_t(cur), n0, n1, n2, n3);
+      float tl, tr;
+      const bool hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tfar, tl);
+      const bool hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tfar, tr);
+      int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+      if (hl && hr && tr < tl) {
+        const int32_t x = c0;
+        c0 = c1;
+        c1 = x;
+      }
+      if (hl && hr) {
+        stk[sp * kBlock] = c1;
+        ++sp;
+        cur = c0;
+      } else if (hl || hr) {
+        cur = hl ? c0 : c1;
+      } else {
+        cur = sp ? stk[--sp * kBlock] : kNone;
+      }
+      if (cur < 0 && leaf == kNone) {  // park the leaf, keep descending
+        leaf = cur;
+        cur = sp ? stk[--sp * kBlock] : kNone;
+      }
+      if (__ballot(leaf == kNone) == 0) break;  // every active lane holds a leaf
+    }
+    while (leaf != kNone) {
+      const uint32_t enc = ~uint32_t(leaf);
+      const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
+      for (uint32_t q = 0; q < cnt; ++q) {
+        float4 a, b, c;
+        ld_tri(tris, first + q, a, b, c);
+        float t, u, v;
+        if (tri_test(r, tnear, a, b, c, t, u, v) && t <= tfar) return true;
+      }
+      leaf = kNone;
+      if (cur < 0) {  // the walk stopped on a second leaf
+        leaf = cur;
+        cur = sp ? stk[--sp * kBlock] : kNone;
+      }
+    }
+    if (cur == kNone) return false;
+  }
+}
+
 // Packet traversal of one domain tree by the whole wave.  The tree pointers
 // and the walk (current node, stack) are wave-uniform: nodes and triangles
 // come through scalar loads (one fetch per wave, broadcast), and a child is

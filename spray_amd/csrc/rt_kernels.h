@@ -115,11 +115,13 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
                            uint32_t* block_counts);
 
 // Ambient-occlusion rays of ooc::ShaderAo, nsamples per hit, compacted in
-// (source ray, sample) order; block_counts as launch_spawn_pt.
+// (source ray, sample) order; scratch: ao_scratch_bytes(M, nsamples) of
+// device memory (per-hit sample masks and tile totals).
 hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
-                           uint32_t* block_counts);
+                           void* scratch);
+size_t ao_scratch_bytes(size_t M, int nsamples);
 
 // ---- out-of-core path (ooc_kernels.hip) ----
 // One resident domain as its drain launch sees it.
@@ -144,6 +146,8 @@ struct OocScratch {
   uint32_t* val_in;
   uint32_t* val_out;  // the queues: ray ids grouped by domain, ascending
   uint32_t* first;    // [ndom + 1]
+  uint64_t* pkey;     // [pair_cap] closest-hit key of each (ray, domain) pair
+  uint32_t* pleaf;    // [pair_cap] its triangle (leaf order)
   void* temp;
   size_t temp_bytes;
   size_t pair_cap;
@@ -158,11 +162,27 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
                              const spray_rt_ray* rays, const uint8_t* valid, size_t M,
                              OocScratch& q, uint32_t* h_first);
 size_t ooc_temp_bytes(size_t M, size_t pairs);
-hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* tie, size_t M);
-hipError_t launch_ooc_ch(hipStream_t s, const OocDomain& D, const spray_rt_ray* rays,
-                         const uint32_t* idx, uint32_t n, spray_rt_hit* hits, uint64_t* tie);
-hipError_t launch_ooc_ah(hipStream_t s, const OocDomain& D, const spray_rt_ray* rays,
-                         const uint32_t* idx, uint32_t n, uint8_t* occ);
+// Per-ray closest-hit key of the ooc drains: t bits << 32 | position in the
+// ray's sorted domain list << 16 | domain; a miss is kOocMissKey.
+constexpr uint64_t kOocMissKey = ~0ull;
+constexpr int kOocBatch = 8;  // resident domains drained by one launch
+struct OocBatch {
+  OocDomain d[kOocBatch];
+  uint32_t begin[kOocBatch];  // queue of d[k]: idx[begin[k] .. begin[k] + n[k])
+  uint32_t n[kOocBatch];
+  uint32_t wave0[kOocBatch + 1];  // filled by the launcher
+  int count;
+};
+hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* key, size_t M);
+// Closest hit of a batch (traversal + key atomicMin, then the winners'
+// records); masks: the queue build's per-ray domain masks (W words), boxes
+// the domain boxes, pkey / pleaf scratch indexed like idx.
+hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
+                               const uint32_t* idx, const uint64_t* masks, const float* boxes,
+                               uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
+                               spray_rt_hit* hits);
+hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, const spray_rt_ray* rays,
+                               const uint32_t* idx, uint8_t* occ);
 hipError_t launch_ooc_clear_occ(hipStream_t s, const uint8_t* valid, uint8_t* occ, size_t M);
 
 // frame layer (frame_kernels.hip)

@@ -45,6 +45,11 @@ namespace {
 // only, 2 = mask + ordered domain selection, no BVH traversal.
 // Minimum resident waves per SIMD the register allocator must allow (the
 // second __launch_bounds__ operand); 1 = unconstrained.
+// Per-lane any hit: 1 = while-while walk with postponed leaves, 0 = the
+// canonical closest-child-first walk.
+#ifndef SPRAY_AH_WW
+#define SPRAY_AH_WW 1
+#endif
 #ifndef SPRAY_WAVES_CH
 #define SPRAY_WAVES_CH 6
 #endif
@@ -306,8 +311,13 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         continue;
       }
       if (ANY) {
-        if (trace_tree<true, COUNT>(nodes, tris, prims, r, o4.w, d4.w, best, stk, nnode,
-                                    ntri)) {
+        // the counting build walks in the canonical order the byte formula
+        // is defined on; the fast build postpones leaves (same result)
+        const bool o = (COUNT || SPRAY_AH_WW == 0)
+                           ? trace_tree<true, COUNT>(nodes, tris, prims, r, o4.w, d4.w, best,
+                                                     stk, nnode, ntri)
+                           : occluded_tree_ww(nodes, tris, r, o4.w, d4.w, stk);
+        if (o) {
           occluded = true;
           break;
         }
@@ -1077,52 +1087,164 @@ __device__ __forceinline__ AoOut ao_sample(const spray_rt_ray& ray, const spray_
   return r;
 }
 
-__device__ __forceinline__ uint32_t ao_count(const spray_rt_ray* rays, const spray_rt_hit* hits,
-                                             const int32_t* pixid, size_t i, int ns) {
-  const spray_rt_hit h = hits[i];
-  if (h.domain < 0) return 0;
-  const spray_rt_ray r = rays[i];
-  uint32_t c = 0;
-  for (int l = 0; l < ns; ++l) c += ao_sample(r, h, pixid[i], l, ns).ok ? 1u : 0u;
-  return c;
+// Whether sample l of a hit yields an AO ray -- ao_sample(...).ok, without
+// the trigonometry in the common case.  The concentric-disk radius is
+// rr = max(|sx|, |sy|); for rr < 0.999 the local direction has
+// lv.z >= 0.0447, so ct = N . w and pdf = lv.z / pi are positive and finite
+// and the weight kd * (ct / (pi * ns * pdf)) is positive exactly when a
+// colour channel is (kd >= 1/255, the factor is ~1/ns: no underflow) --
+// given a finite normalised N.  Otherwise the full sample decides.
+__device__ __forceinline__ bool ao_ok(const spray_rt_ray& ray, const spray_rt_hit& h,
+                                      int32_t pixid, int l, int nsamples) {
+  if (h.domain < 0) return false;
+  float N[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  gnorm3(N);
+  const bool nfin = isfinite(N[0]) && isfinite(N[1]) && isfinite(N[2]);
+  uint32_t st = sampler_init1(pixid * (l + 1));
+  const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+  const float rr = fmaxf(fabsf(2 * u1 - 1), fabsf(2 * u2 - 1));
+  if (nfin && rr < 0.999f) return (h.color & 0xFFFFFFu) != 0u;
+  return ao_sample(ray, h, pixid, l, nsamples).ok;
 }
+
+// One lane per (hit, sample) pair q = i * ns + l (32-bit: the API bounds
+// M * ns), kAoPer pairs per thread in block-strided rounds: each round
+// covers kBlock consecutive pairs, so the 32-B ray stores of a round are
+// contiguous and the lanes of one hit share its record loads.  Output order
+// is q ascending -- the reference's (hits in order, samples l = 0..ns-1):
+// count pass (ao_ok), one scan of the tile totals, write pass.
+#ifndef SPRAY_AO_DIAG
+#define SPRAY_AO_DIAG 0
+#endif
+constexpr int kAoPer = 16;
+constexpr int kAoTile = kBlock * kAoPer;
 
 __global__ __launch_bounds__(kBlock) void k_spawn_ao_count(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
-    const int32_t* __restrict__ pixid, size_t M, int ns, uint32_t* __restrict__ block_counts) {
-  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
-  __shared__ typename Scan::TempStorage tmp;
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  const uint32_t c = i < M ? ao_count(rays, hits, pixid, i, ns) : 0u;
-  uint32_t ex, total;
-  Scan(tmp).ExclusiveSum(c, ex, total);
-  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+    const int32_t* __restrict__ pixid, uint32_t npairs, uint32_t ns,
+    uint32_t* __restrict__ tile_counts) {
+  using Reduce = hipcub::BlockReduce<uint32_t, kBlock>;
+  __shared__ typename Reduce::TempStorage tmp;
+  const uint32_t base = blockIdx.x * uint32_t(kAoTile) + threadIdx.x;
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < kAoPer; ++r) {  // independent rounds: the loads overlap
+    const uint32_t q = base + uint32_t(r * kBlock);
+    const uint32_t i = q < npairs ? q / ns : 0u;
+    const spray_rt_hit h = hits[i];
+    if (q < npairs && h.domain >= 0 && ao_ok(rays[i], h, pixid[i], int(q - i * ns), int(ns)))
+      ++c;
+  }
+  const uint32_t total = Reduce(tmp).Sum(c);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
 }
 
+// Write pass: the ok flags of all rounds first (independent loads, one
+// barrier for the whole tile's prefix), then the samples and stores, with
+// no further synchronisation.
 __global__ __launch_bounds__(kBlock) void k_spawn_ao_write(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
-    const int32_t* __restrict__ pixid, size_t M, int ns,
-    const uint32_t* __restrict__ block_offsets, spray_rt_ray* __restrict__ out,
+    const int32_t* __restrict__ pixid, uint32_t npairs, uint32_t ns,
+    const uint32_t* __restrict__ tile_off, spray_rt_ray* __restrict__ out,
     int32_t* __restrict__ src) {
-  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
-  __shared__ typename Scan::TempStorage tmp;
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  const uint32_t c = i < M ? ao_count(rays, hits, pixid, i, ns) : 0u;
-  uint32_t k, total;
-  Scan(tmp).ExclusiveSum(c, k, total);
-  if (!c) return;
-  k += block_offsets[blockIdx.x];
-  const spray_rt_hit h = hits[i];
-  const spray_rt_ray r = rays[i];
-  for (int l = 0; l < ns; ++l) {
-    const AoOut a = ao_sample(r, h, pixid[i], l, ns);
-    if (!a.ok) continue;
+  __shared__ uint32_t wcnt[kAoPer][kBlock / 64];
+  __shared__ uint32_t spre[kAoPer][kBlock];  // each thread's output slot per round
+  const uint32_t base = blockIdx.x * uint32_t(kAoTile) + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  uint32_t okm = 0;
+#pragma unroll
+  for (int r = 0; r < kAoPer; ++r) {
+    const uint32_t q = base + uint32_t(r * kBlock);
+    const uint32_t i = q < npairs ? q / ns : 0u;
+    const spray_rt_hit h = hits[i];
+    const bool ok =
+        q < npairs && h.domain >= 0 && ao_ok(rays[i], h, pixid[i], int(q - i * ns), int(ns));
+    const unsigned long long bal = __ballot(ok);
+    spre[r][threadIdx.x] = __popcll(bal & below);
+    if (lane == 0) wcnt[r][wave] = __popcll(bal);
+    okm |= ok ? 1u << r : 0u;
+  }
+  __syncthreads();
+  uint32_t run = tile_off[blockIdx.x];
+#pragma unroll
+  for (int r = 0; r < kAoPer; ++r) {
+    uint32_t before = run;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      const uint32_t x = wcnt[r][w];
+      before += w < wave ? x : 0u;
+      run += x;
+    }
+    spre[r][threadIdx.x] += before;
+  }
+#pragma unroll 1
+  for (int r = 0; r < kAoPer; ++r) {
+    if (!((okm >> r) & 1u)) continue;
+    const uint32_t q = base + uint32_t(r * kBlock);
+    const uint32_t i = q / ns;
+    const uint32_t k = spre[r][threadIdx.x];
+#if SPRAY_AO_DIAG == 1  // diagnostic: stores only
+    AoOut a;
+    a.o[0] = a.o[1] = a.o[2] = float(i);
+    a.w[0] = a.w[1] = a.w[2] = float(q);
+#else
+    const AoOut a = ao_sample(rays[i], hits[i], pixid[i], int(q - i * ns), int(ns));
+#endif
+#if SPRAY_AO_DIAG == 2  // diagnostic: sampling only
+    if (a.w[0] != 12345.f) continue;
+#endif
     float4* op = reinterpret_cast<float4*>(out + k);
     op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
     op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
     if (src) src[k] = int32_t(i);
-    ++k;
   }
+}
+
+// ns <= 32: the ok flags per hit first (one thread per hit: the hit record,
+// the normalised N and the colour test once, then ns cheap sampler draws),
+// as a sample mask plus the hit's exclusive prefix within its tile of kBlock
+// hits; the write pass (one lane per pair, coalesced stores) then needs no
+// prefix work: slot = tile offset + prefix + popcount of the mask below l.
+__global__ __launch_bounds__(kBlock) void k_spawn_ao_hitmask(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
+    const int32_t* __restrict__ pixid, uint32_t M, uint32_t ns, uint2* __restrict__ meta,
+    uint32_t* __restrict__ tile_counts) {
+  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
+  __shared__ typename Scan::TempStorage tmp;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t mask = 0;
+  if (i < M) {
+    const spray_rt_hit h = hits[i];
+    if (h.domain >= 0) {
+      const spray_rt_ray r = rays[i];
+      const int32_t px = pixid[i];
+      for (uint32_t l = 0; l < ns; ++l)
+        if (ao_ok(r, h, px, int(l), int(ns))) mask |= 1u << l;
+    }
+  }
+  uint32_t pre, total;
+  Scan(tmp).ExclusiveSum(uint32_t(__popc(mask)), pre, total);
+  if (i < M) meta[i] = make_uint2(mask, pre);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spawn_ao_write_masked(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
+    const int32_t* __restrict__ pixid, uint32_t npairs, uint32_t ns,
+    const uint2* __restrict__ meta, const uint32_t* __restrict__ tile_off,
+    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src) {
+  const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= npairs) return;
+  const uint32_t i = q / ns, l = q - i * ns;
+  const uint2 m = meta[i];
+  if (!((m.x >> l) & 1u)) return;
+  const uint32_t k = tile_off[i / kBlock] + m.y + __popc(m.x & ((1u << l) - 1u));
+  const AoOut a = ao_sample(rays[i], hits[i], pixid[i], int(l), int(ns));
+  float4* op = reinterpret_cast<float4*>(out + k);
+  op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
+  op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
+  if (src) src[k] = int32_t(i);
 }
 
 }  // namespace
@@ -1430,14 +1552,33 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
 hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
-                           uint32_t* block_counts) {
+                           void* scratch) {
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
-  const unsigned g = grid_for(M);
-  k_spawn_ao_count<<<g, kBlock, 0, s>>>(rays, hits, pixid, M, nsamples, block_counts);
-  k_scan_blocks<<<1, 1024, 0, s>>>(block_counts, g, d_count);
-  k_spawn_ao_write<<<g, kBlock, 0, s>>>(rays, hits, pixid, M, nsamples, block_counts,
+  const uint32_t npairs = uint32_t(M * size_t(nsamples));
+  if (nsamples <= 32) {
+    const uint32_t g = uint32_t((M + kBlock - 1) / kBlock);
+    uint2* meta = static_cast<uint2*>(scratch);
+    uint32_t* tiles = reinterpret_cast<uint32_t*>(meta + M);
+    k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
+                                            uint32_t(nsamples), meta, tiles);
+    k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
+    k_spawn_ao_write_masked<<<(npairs + kBlock - 1) / kBlock, kBlock, 0, s>>>(
+        rays, hits, pixid, npairs, uint32_t(nsamples), meta, tiles, out_rays, out_src);
+    return hipGetLastError();
+  }
+  const uint32_t g = (npairs + kAoTile - 1) / kAoTile;
+  uint32_t* tiles = static_cast<uint32_t*>(scratch);
+  k_spawn_ao_count<<<g, kBlock, 0, s>>>(rays, hits, pixid, npairs, uint32_t(nsamples), tiles);
+  k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
+  k_spawn_ao_write<<<g, kBlock, 0, s>>>(rays, hits, pixid, npairs, uint32_t(nsamples), tiles,
                                         out_rays, out_src);
   return hipGetLastError();
+}
+
+size_t ao_scratch_bytes(size_t M, int nsamples) {
+  if (nsamples <= 32) return M * sizeof(uint2) + ((M + kBlock - 1) / kBlock + 1) * sizeof(uint32_t);
+  const size_t g = (M * size_t(nsamples) + kAoTile - 1) / kAoTile;
+  return (g + 1) * sizeof(uint32_t);
 }
 
 }  // namespace spray_rt

@@ -101,8 +101,11 @@ __device__ __forceinline__ void cosine_hemisphere(float u1, float u2, const floa
       }
     }
     th = float(double(th) * (kPi / 4.0));
-    dx = rr * cos_r(th);
-    dy = rr * sin_r(th);
+    // one shared argument reduction; the same values as cos() and sin()
+    double sd, cd;
+    sincos(double(th), &sd, &cd);
+    dx = rr * float(cd);
+    dy = rr * float(sd);
   }
   float lv[3] = {dx, dy, sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy))};
   gnorm3(lv);

@@ -11,7 +11,8 @@ from conftest import BENCH_CAMERA, SCENES, WAVELETS64
 pytestmark = pytest.mark.gpu
 
 
-def test_ao16_spawn_and_occlusion(oracle):
+@pytest.mark.parametrize("ns", [16, 5, 40])
+def test_ao16_spawn_and_occlusion(oracle, ns):
     import spray_amd
     c = BENCH_CAMERA
     cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 1024, 1024)
@@ -19,8 +20,8 @@ def test_ao16_spawn_and_occlusion(oracle):
     org, d, pix, _ = oracle.eye_rays_ooc(cam, 1024, 2, tile)
     sc, _, _ = oracle.load_scene(WAVELETS64, SCENES)
     hits, _ = sc.intersect(org, d)
-    so, sd, src = oracle.spawn_shadows_ao(org, d, pix, hits, 16)
-    assert len(so) > 16 * 1000
+    so, sd, src = oracle.spawn_shadows_ao(org, d, pix, hits, ns)
+    assert len(so) > ns * 1000
 
     scene = spray_amd.Scene(WAVELETS64, SCENES)
     rt = scene.rt
@@ -34,10 +35,10 @@ def test_ao16_spawn_and_occlusion(oracle):
     h = torch.empty((n, 12), dtype=torch.float32, device="cuda")
     rt.intersect_scene(rays, h)
     pixid = torch.from_numpy(pix).cuda()
-    out = torch.empty((n * 16, 8), dtype=torch.float32, device="cuda")
-    osrc = torch.empty(n * 16, dtype=torch.int32, device="cuda")
+    out = torch.empty((n * ns, 8), dtype=torch.float32, device="cuda")
+    osrc = torch.empty(n * ns, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
-    rt.spawn_shadows_ao(rays, h, pixid, n, 16, out, osrc, cnt)
+    rt.spawn_shadows_ao(rays, h, pixid, n, ns, out, osrc, cnt)
     rt.sync()
     m = int(cnt.item())
     assert h.cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1).tobytes() == hits.tobytes()
@@ -49,7 +50,8 @@ def test_ao16_spawn_and_occlusion(oracle):
     assert (g[:, 3] == np.float32(0.001)).all() and np.isinf(g[:, 7]).all()
     ref, _ = sc.occluded(np.ascontiguousarray(g[:, 0:3]), np.ascontiguousarray(g[:, 4:7]))
     # every traversal form (packet, per lane, per-wave choice) gives the same bits
-    for mode in (rt.RAYS_ADAPTIVE, rt.RAYS_COHERENT, rt.RAYS_INCOHERENT):
+    modes = (rt.RAYS_ADAPTIVE, rt.RAYS_COHERENT, rt.RAYS_INCOHERENT) if ns == 16 else ()
+    for mode in modes:
         rt.set_coherence(mode)
         occ = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
         rt.occluded_scene(out[:m].contiguous(), occ)

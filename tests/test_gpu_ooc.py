@@ -1,5 +1,5 @@
 """GPU parity of the out-of-core path (spray_rt_ooc_*: LRU cache of domain
-images streamed from pinned host memory, per-domain drain launches) against
+images streamed from pinned host memory, batched per-domain drains) against
 the whole-scene oracle, plus its cache accounting and the cross-domain tie
 rule (the earlier entry of the sorted domain list wins an equal t)."""
 import numpy as np
