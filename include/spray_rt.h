@@ -389,6 +389,15 @@ int spray_rt_film(spray_rt_ctx_t ctx, float* image_rgba, const int32_t* pixid, s
 int spray_rt_render_tile(spray_rt_ctx_t ctx, const spray_rt_shader* shader,
                          const float cam[14], int image_w, int spp, int tx, int ty, int tw,
                          int th, float* image_rgba);
+/* Several tiles (tiles[ntiles][4] = x, y, w, h) as one device batch: each
+ * tile's eye rays keep their tile-local seeds and every later pass is per
+ * sample slot or per pixel, so the image equals rendering the tiles one by
+ * one -- with one launch per pass instead of one per tile (the reference's
+ * 1M-samples-per-rank tile cap bounds host memory; 288 GB of HBM holds a
+ * whole 1024x1024x8 frame's buffers, ~1 GB, many times over). */
+int spray_rt_render_tiles(spray_rt_ctx_t ctx, const spray_rt_shader* shader,
+                          const float cam[14], int image_w, int spp, const int* tiles,
+                          int ntiles, float* image_rgba);
 /* Totals of the tiles rendered since the last reset (synchronises the
  * stream): out[3] = radiance rays traced, shadow rays traced, shading cases
  * the reference aborts on (skipped here).  Returns SPRAY_RT_ERR_UNSUPPORTED

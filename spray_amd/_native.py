@@ -108,6 +108,7 @@ SIGNATURES = {
     "spray_rt_shade": (I, [P, P, I, P, P, P, P, P, P, SZ, P, P, P, P]),
     "spray_rt_film": (I, [P, P, P, SZ, I, I, P, P, P, C.c_double]),
     "spray_rt_render_tile": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "spray_rt_render_tiles": (I, [P, P, P, I, I, P, I, P]),
     "spray_rt_frame_stats": (I, [P, P, I]),
     "spray_rt_tile_list": (I, [I, I, I, I, I, I, C.c_longlong, P, I, P]),
     "spray_rt_write_ppm": (I, [C.c_char_p, P, I, I]),

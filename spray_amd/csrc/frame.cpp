@@ -139,18 +139,24 @@ int spray_rt_film(spray_rt_ctx_t c, float* image, const int32_t* pixid, size_t M
   return SPRAY_RT_OK;
 }
 
-int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float cam[14],
-                         int image_w, int spp, int tx, int ty, int tw, int th, float* image) {
+int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const float cam[14],
+                          int image_w, int spp, const int* tiles, int ntiles, float* image) {
   if (!c) return SPRAY_RT_ERR_ARG;
-  if (!shader_ok(P) || !cam || spp <= 0 || tw < 0 || th < 0 || image_w <= 0 || tx < 0 ||
-      ty < 0 || tx + tw > image_w || ty + th > int(cam[13]))
+  if (!shader_ok(P) || !cam || spp <= 0 || image_w <= 0 || ntiles < 0 || (ntiles && !tiles))
     return fail(c, SPRAY_RT_ERR_ARG, "bad render arguments");
-  const size_t M = size_t(tw) * th * spp;
+  size_t M = 0;
+  for (int k = 0; k < ntiles; ++k) {
+    const int tx = tiles[4 * k], ty = tiles[4 * k + 1], tw = tiles[4 * k + 2],
+              th = tiles[4 * k + 3];
+    if (tw < 0 || th < 0 || tx < 0 || ty < 0 || tx + tw > image_w || ty + th > int(cam[13]))
+      return fail(c, SPRAY_RT_ERR_ARG, "bad tile %d", k);
+    M += size_t(tw) * th * spp;
+  }
   if (M == 0) return SPRAY_RT_OK;
   const int ns = spray_rt_shadow_slots(P);
   const size_t MS = M * size_t(ns);
   if (M > 0xFFFFFFFFull || MS > 0xFFFFFFFFull)
-    return fail(c, SPRAY_RT_ERR_LIMIT, "tile too large (samples x shadow slots > 2^32)");
+    return fail(c, SPRAY_RT_ERR_LIMIT, "batch too large (samples x shadow slots > 2^32)");
   if (!is_device_ptr(image)) return fail(c, SPRAY_RT_ERR_ARG, "image must be device memory");
   int r = scene_common(c, image, M, image);
   if (r) return r;
@@ -162,8 +168,9 @@ int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float
   if (r) return r;
   hipStream_t s = stream_of(c);
   if (!c->d_fstats) {
-    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_fstats), 4 * sizeof(unsigned long long)));
-    HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, 4 * sizeof(unsigned long long), s));
+    const size_t fb = 4 * kStatStripes * sizeof(unsigned long long);
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_fstats), fb));
+    HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, fb, s));
   }
   Carve cv{static_cast<char*>(c->d_frame)};
   spray_rt_ray* rays = cv.take<spray_rt_ray>(M);
@@ -176,7 +183,19 @@ int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float
   float* sw = cv.take<float>(4 * MS);
   uint8_t* sv = cv.take<uint8_t>(MS);
   uint8_t* occ = cv.take<uint8_t>(MS);
-  HIPCHK(c, launch_eye_rays_ooc(s, cam, image_w, spp, tx, ty, tw, th, rays, pixid, samid));
+  // each tile's eye rays (tile-local sampler seeds) at its offset; from
+  // here on every pass is per slot (or per pixel group of spp slots), so
+  // the batch gives each tile exactly its own-launch result
+  size_t off = 0;
+  for (int k = 0; k < ntiles; ++k) {
+    const int tx = tiles[4 * k], ty = tiles[4 * k + 1], tw = tiles[4 * k + 2],
+              th = tiles[4 * k + 3];
+    const size_t m = size_t(tw) * th * spp;
+    if (!m) continue;
+    HIPCHK(c, launch_eye_rays_ooc(s, cam, image_w, spp, tx, ty, tw, th, rays + off, pixid + off,
+                                  samid + off));
+    off += m;
+  }
   HIPCHK(c, launch_path_init(s, w, valid, M));
   const double scale = 1.0 / double(spp);
   const int user = c->coherence;
@@ -192,7 +211,7 @@ int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float
       if (r) return r;
     }
     HIPCHK(c, launch_shade(s, *P, c->d_bsdf, c->nbsdf, b, ns, rays, hits, w, valid, pixid, samid,
-                           M, sh, sw, sv, c->d_fstats));
+                           M, sh, sw, sv, c->d_fstats, kStatStripes));
     if (ns) {
       r = spray_rt_occluded_scene_masked(c, sh, MS, sv, occ);
       if (r) return r;
@@ -202,16 +221,24 @@ int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float
   return SPRAY_RT_OK;
 }
 
+int spray_rt_render_tile(spray_rt_ctx_t c, const spray_rt_shader* P, const float cam[14],
+                         int image_w, int spp, int tx, int ty, int tw, int th, float* image) {
+  const int t[4] = {tx, ty, tw, th};
+  return spray_rt_render_tiles(c, P, cam, image_w, spp, t, 1, image);
+}
+
 int spray_rt_frame_stats(spray_rt_ctx_t c, unsigned long long out[3], int reset) {
   if (!c || !out) return SPRAY_RT_ERR_ARG;
   out[0] = out[1] = out[2] = 0;
   if (!c->d_fstats) return SPRAY_RT_OK;
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = stream_of(c);
-  unsigned long long h[4];
-  HIPCHK(c, hipMemcpyAsync(h, c->d_fstats, sizeof(h), hipMemcpyDeviceToHost, s));
-  if (reset) HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, sizeof(h), s));
+  unsigned long long hs[4 * kStatStripes], h[4] = {0, 0, 0, 0};
+  HIPCHK(c, hipMemcpyAsync(hs, c->d_fstats, sizeof(hs), hipMemcpyDeviceToHost, s));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, sizeof(hs), s));
   HIPCHK(c, hipStreamSynchronize(s));
+  for (int k = 0; k < 4; ++k)
+    for (int x = 0; x < kStatStripes; ++x) h[k] += hs[k * kStatStripes + x];
   out[0] = h[3];
   out[1] = h[1];
   out[2] = h[0];

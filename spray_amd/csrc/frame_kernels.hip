@@ -229,12 +229,18 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 // stats[4] += {reference-abort cases, shadows spawned, next radiance rays,
 // live slots shaded (= radiance rays traced this bounce)}
+// stats: 4 counters, each striped over `stripes` words (counter k of block b
+// at stats[k * stripes + b % stripes]: same-address atomics serialise in L2,
+// one word per counter put a ~200 us floor under a 1M-slot launch); the
+// block sums first, one atomic per counter per block.
 __global__ __launch_bounds__(kBlock) void k_shade(
     spray_rt_shader P, const spray_rt_bsdf* __restrict__ bsdfs, int nbsdf, int bounce,
     int ns, spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
     float4* __restrict__ w, uint8_t* __restrict__ valid, const int32_t* __restrict__ pixid,
     const int32_t* __restrict__ samid, size_t M, spray_rt_ray* __restrict__ sh,
-    float4* __restrict__ sw, uint8_t* __restrict__ sv, unsigned long long* __restrict__ stats) {
+    float4* __restrict__ sw, uint8_t* __restrict__ sv, unsigned long long* __restrict__ stats,
+    int stripes) {
+  __shared__ uint32_t part[kBlock / 64][4];
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   ShadeCount cnt;
   if (i < M)
@@ -243,9 +249,17 @@ __global__ __launch_bounds__(kBlock) void k_shade(
   if (!stats) return;
   const uint32_t v[4] = {wave_sum(cnt.bad), wave_sum(cnt.shadows), wave_sum(cnt.next),
                          wave_sum(cnt.live)};
-  if ((threadIdx.x & 63) == 0)
-    for (int k = 0; k < 4; ++k)
-      if (v[k]) atomicAdd(stats + k, (unsigned long long)v[k]);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0)
+    for (int k = 0; k < 4; ++k) part[wave][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint32_t t = 0;
+    for (int x = 0; x < kBlock / 64; ++x) t += part[x][threadIdx.x];
+    if (t)
+      atomicAdd(stats + threadIdx.x * stripes + blockIdx.x % unsigned(stripes),
+                (unsigned long long)t);
+  }
 }
 
 // path weights (1, 1, 1) and all slots live: the camera rays of a tile
@@ -292,11 +306,12 @@ hipError_t launch_shade(hipStream_t s, const spray_rt_shader& P, const spray_rt_
                         const spray_rt_hit* hits, float* w, uint8_t* valid,
                         const int32_t* pixid, const int32_t* samid, size_t M,
                         spray_rt_ray* shadows, float* sw, uint8_t* svalid,
-                        unsigned long long* stats) {
+                        unsigned long long* stats, int stripes) {
   if (M == 0) return hipSuccess;
   k_shade<<<grid_for(M), kBlock, 0, s>>>(P, bsdfs, nbsdf, bounce, ns, rays, hits,
                                          reinterpret_cast<float4*>(w), valid, pixid, samid, M,
-                                         shadows, reinterpret_cast<float4*>(sw), svalid, stats);
+                                         shadows, reinterpret_cast<float4*>(sw), svalid, stats,
+                                         stripes < 1 ? 1 : stripes);
   return hipGetLastError();
 }
 

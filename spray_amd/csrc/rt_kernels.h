@@ -191,7 +191,8 @@ hipError_t launch_shade(hipStream_t s, const spray_rt_shader& P, const spray_rt_
                         const spray_rt_hit* hits, float* w, uint8_t* valid,
                         const int32_t* pixid, const int32_t* samid, size_t M,
                         spray_rt_ray* shadows, float* sw, uint8_t* svalid,
-                        unsigned long long* stats);
+                        unsigned long long* stats, int stripes = 1);
+constexpr int kStatStripes = 64;  // render_tile's striped shading counters
 hipError_t launch_path_init(hipStream_t s, float* w, uint8_t* valid, size_t M);
 hipError_t launch_film(hipStream_t s, float* image, const int32_t* pixid, size_t M, int spp,
                        int ns, const float* sw, const uint8_t* svalid, const uint8_t* occ,

@@ -410,6 +410,16 @@ class RtContext:
                                                int(image_w), int(spp), tx, ty, tw, th, a),
                     "render_tile")
 
+    def render_tiles(self, shader, cam, image_w, spp, tiles, image):
+        """Tiles [(x, y, w, h)] of an ooc-mode frame as one device batch
+        (the same image as render_tile per tile), enqueued on the stream."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        t = np.ascontiguousarray(np.asarray(tiles, np.int32).reshape(-1, 4))
+        a, k1 = _addr(image)
+        self._check(lib().spray_rt_render_tiles(self.h, C.byref(shader), cam.ctypes.data,
+                                                int(image_w), int(spp), t.ctypes.data,
+                                                len(t), a), "render_tiles")
+
     def frame_stats(self, reset=True):
         """(radiance rays, shadow rays) traced by render_tile since the last
         reset (synchronises); raises on shading cases the reference aborts on."""

@@ -4,7 +4,7 @@
 
 Per rank: the ooc tile schedule (``ImageScheduleTileList``, tile.cc:317-391:
 the rank's vertical stripe cut into horizontal tiles); per tile, on the device
-(``spray_rt_render_tile``): eye rays, then per bounce closest hit -> shading
+(``spray_rt_render_tile``, or all of them as one batch, ``spray_rt_render_tiles``): eye rays, then per bounce closest hit -> shading
 (``ooc::ShaderPt`` / ``ooc::ShaderAo``) -> any hit of the shadow rays ->
 film.  The ranks' images hold disjoint pixels, so the composite
 (``HdrImage::composite``, image.h:170-186, an MPI_Reduce SUM) is one
@@ -84,9 +84,11 @@ def tile_list(image_w, image_h, spp, nranks=1, rank=0, max_samples_per_rank=None
 
 
 def render_frame(rt, shader, cam, image_w, image_h, spp, nranks=1, rank=0,
-                 max_samples_per_rank=None, image=None, device="cuda", stats=True):
+                 max_samples_per_rank=None, image=None, device="cuda", stats=True, batch=True):
     """One frame of this rank's tiles into a device float32 [h*w*4] image
     (cleared first, HdrImage::clear), enqueued on the context's stream.
+    batch: all tiles as one device batch (spray_rt_render_tiles), else one
+    render_tile per tile -- the same image.
     Returns (image, (radiance rays, shadow rays)) -- with stats=False the
     call does not synchronise and the counts are None."""
     import torch
@@ -94,10 +96,13 @@ def render_frame(rt, shader, cam, image_w, image_h, spp, nranks=1, rank=0,
         image = torch.zeros(image_w * image_h * 4, dtype=torch.float32, device=device)
     else:
         image.zero_()
-    for t in tile_list(image_w, image_h, spp, nranks, rank, max_samples_per_rank, "image"):
-        if t[2] * t[3] == 0:
-            continue
-        rt.render_tile(shader, cam, image_w, spp, t, image)
+    tiles = [t for t in tile_list(image_w, image_h, spp, nranks, rank, max_samples_per_rank,
+                                  "image") if t[2] * t[3]]
+    if batch:
+        rt.render_tiles(shader, cam, image_w, spp, tiles, image)
+    else:
+        for t in tiles:
+            rt.render_tile(shader, cam, image_w, spp, t, image)
     return image, (rt.frame_stats() if stats else None)
 
 

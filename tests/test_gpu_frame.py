@@ -209,3 +209,29 @@ def test_render_frame_ranks_partition_and_ppm(spray, oracle, scene64, tmp_path):
     p = tmp_path / "f.ppm"
     spray.frame.write_ppm(p, total, w, h)
     assert p.read_text().startswith("P3\n64 64\n1023\n")
+
+
+@pytest.mark.parametrize("kind", ["pt", "ao"])
+def test_batched_tiles_equal_per_tile(spray, oracle, scene64, kind):
+    """spray_rt_render_tiles (all tiles as one device batch) gives the image
+    of render_tile per tile, bit for bit, and the same ray counts."""
+    sc, osc, doms, slights = scene64
+    w = h = 96
+    cam = camera(oracle, w, h)
+    rows = oracle.scene_lights(slights)
+    sc.rt.set_bsdfs(oracle.scene_bsdfs(doms))
+    sh_g = spray.frame.make_shader(kind, 2, 3, lights=rows)
+    tiles = [t for t in spray.frame.tile_list(w, h, 2, 1, 0, 4000) if t[2] * t[3]]
+    assert len(tiles) > 3
+    one = torch.zeros(w * h * 4, dtype=torch.float32, device="cuda")
+    sc.rt.frame_stats(reset=True)
+    for t in tiles:
+        sc.rt.render_tile(sh_g, cam, w, 2, t, one)
+    c1 = sc.rt.frame_stats(reset=True)
+    many = torch.zeros_like(one)
+    sc.rt.render_tiles(sh_g, cam, w, 2, tiles, many)
+    c2 = sc.rt.frame_stats(reset=True)
+    torch.cuda.synchronize()
+    assert c1 == c2 and c1[0] > 0
+    a, b = one.cpu().numpy(), many.cpu().numpy()
+    assert (a > 0).sum() > 1000 and a.tobytes() == b.tobytes()
