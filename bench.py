@@ -155,6 +155,7 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
     ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
+    order = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
 
@@ -162,8 +163,10 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
 
     def frame():
         rt.intersect_scene(prim, hits)
-        rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt)
-        rt.occluded_scene_devcount(ao, n_prim * nsamples, cnt, occ)
+        # the spp rays of a pixel share every sample direction (seed
+        # pixid * (l + 1)): traced sample-major, they sit on neighbouring lanes
+        rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order)
+        rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
 
     for _ in range(args.warmup):
         frame()
@@ -187,7 +190,8 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
             "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
             "scaling": "weak", "rays_per_step": n_prim + n_ao, "ao_rays": n_ao,
             "config": "configs[4] workload per GPU: 64 domains resident, primary + "
-                      "AO-%d rays per hit (frame replicas x%d)" % (nsamples, world)}
+                      "AO-%d rays per hit traced sample-major per pixel (frame replicas x%d)"
+                      % (nsamples, world)}
 
 
 def run_frame(args, dist, world, rt, cam, lights):

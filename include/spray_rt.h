@@ -205,6 +205,14 @@ int spray_rt_occluded_scene_devcount(spray_rt_ctx_t ctx, const spray_rt_ray* ray
                                      size_t max_rays, const uint32_t* d_count,
                                      uint8_t* occluded,
                                      unsigned long long* d_counters);
+/* Any hit of the rays order[j], j < *d_count (device count, <= max_rays),
+ * lanes taking them in that order; occluded[order[j]] is written.  The
+ * results equal the positional launch's -- only the grouping of rays into
+ * wavefronts changes (e.g. spray_rt_spawn_shadows_ao_ordered's order).
+ * Device buffers only. */
+int spray_rt_occluded_scene_order(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                  size_t max_rays, const uint32_t* order,
+                                  const uint32_t* d_count, uint8_t* occluded);
 
 /* ---- traversal form of the any-hit scene launches ---- */
 /* Closest-hit scene launches walk each domain tree as a wave-wide packet
@@ -313,6 +321,18 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                               const spray_rt_hit* hits, const int32_t* pixid, size_t M,
                               int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
                               uint32_t* d_count);
+/* The same rays, plus trace_order[0 .. *d_count) (device uint32, room for
+ * M * nsamples): a permutation of the written rays for
+ * spray_rt_occluded_scene_order.  The reference seeds sample l of every ray
+ * of a pixel with pixid * (l + 1), so the spp rays of one pixel draw the same
+ * hemisphere samples; within each aligned block of 8 source rays the order
+ * is sample-major (l, then ray), which puts rays of nearly the same origin
+ * and direction on neighbouring lanes.  (nsamples > 32: identity.) */
+int spray_rt_spawn_shadows_ao_ordered(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                      const spray_rt_hit* hits, const int32_t* pixid,
+                                      size_t M, int nsamples, spray_rt_ray* out_rays,
+                                      int32_t* out_src, uint32_t* d_count,
+                                      uint32_t* trace_order);
 
 /* ---- frames: path shading, film, tiles (callers of the hot path) ---- */
 /* The shading pass of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-227) /

@@ -93,6 +93,8 @@ SIGNATURES = {
     "spray_rt_exchange_plan": (I, [P, P, SZ, I, P, P]),
     "spray_rt_set_coherence": (I, [P, I]),
     "spray_rt_spawn_shadows_ao": (I, [P, P, P, P, SZ, I, P, P, P]),
+    "spray_rt_spawn_shadows_ao_ordered": (I, [P, P, P, P, SZ, I, P, P, P, P]),
+    "spray_rt_occluded_scene_order": (I, [P, P, SZ, P, P, P]),
     "spray_rt_ooc_create": (I, [P, I, P]),
     "spray_rt_ooc_destroy": (I, [P]),
     "spray_rt_ooc_set_domain": (I, [P, I, P, SZ, P, SZ, P, P]),

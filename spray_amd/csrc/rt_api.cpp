@@ -606,6 +606,21 @@ extern "C" int spray_rt_occluded_scene_devcount(spray_rt_ctx_t c,
   return SPRAY_RT_OK;
 }
 
+extern "C" int spray_rt_occluded_scene_order(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                                             size_t max_rays, const uint32_t* order,
+                                             const uint32_t* d_count, uint8_t* occ) {
+  int r = scene_common(c, rays, max_rays, occ);
+  if (r) return r;
+  if (max_rays == 0) return SPRAY_RT_OK;
+  if (max_rays > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "max_rays > 2^32");
+  if (!is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(order) ||
+      !is_device_ptr(d_count))
+    return fail(c, SPRAY_RT_ERR_ARG, "ordered occlusion needs device buffers");
+  HIPCHK(c, launch_scene_occluded_indexed(stream_of(c), view(c), rays, max_rays, order, d_count,
+                                          occ, nullptr));
+  return SPRAY_RT_OK;
+}
+
 int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                       size_t M, spray_rt_hit* hits,
                                       const float shade[10], spray_rt_ray* out_rays,
@@ -791,16 +806,17 @@ int spray_rt_spawn_shadows_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
   return SPRAY_RT_OK;
 }
 
-int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
-                              const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                              int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
-                              uint32_t* d_count) {
+int spray_rt_spawn_shadows_ao_ordered(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                                      const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                                      int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
+                                      uint32_t* d_count, uint32_t* trace_order) {
   if (!c) return SPRAY_RT_ERR_ARG;
   if (!d_count || nsamples <= 0 || nsamples > 1024)
     return fail(c, SPRAY_RT_ERR_ARG, "bad AO arguments");
   if (M * size_t(nsamples) > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "too many rays");
   if (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(pixid) ||
-            !is_device_ptr(out_rays) || !is_device_ptr(d_count)))
+            !is_device_ptr(out_rays) || !is_device_ptr(d_count) ||
+            (trace_order && !is_device_ptr(trace_order))))
     return fail(c, SPRAY_RT_ERR_ARG, "spawn buffers must be device memory");
   HIPCHK(c, hipSetDevice(c->device));
   void* bc = c->d_block_counts;
@@ -808,8 +824,16 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
   HIPCHK(c, launch_spawn_ao(stream_of(c), rays, hits, pixid, M, nsamples, out_rays, out_src,
-                            d_count, c->d_block_counts));
+                            d_count, c->d_block_counts, trace_order));
   return SPRAY_RT_OK;
+}
+
+int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                              const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                              int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
+                              uint32_t* d_count) {
+  return spray_rt_spawn_shadows_ao_ordered(c, rays, hits, pixid, M, nsamples, out_rays, out_src,
+                                           d_count, nullptr);
 }
 
 }  // extern "C"

@@ -1118,6 +1118,9 @@ __device__ __forceinline__ bool ao_ok(const spray_rt_ray& ray, const spray_rt_hi
 #endif
 constexpr int kAoPer = 16;
 constexpr int kAoTile = kBlock * kAoPer;
+// source rays per sample-major trace-order block (divides kBlock)
+constexpr uint32_t kAoGroup = 8;
+static_assert(kBlock % kAoGroup == 0, "trace-order blocks must not straddle tiles");
 
 __global__ __launch_bounds__(kBlock) void k_spawn_ao_count(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
@@ -1233,18 +1236,42 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write_masked(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
     const int32_t* __restrict__ pixid, uint32_t npairs, uint32_t ns,
     const uint2* __restrict__ meta, const uint32_t* __restrict__ tile_off,
-    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src) {
+    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src, uint32_t* __restrict__ order) {
   const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
   if (q >= npairs) return;
   const uint32_t i = q / ns, l = q - i * ns;
   const uint2 m = meta[i];
   if (!((m.x >> l) & 1u)) return;
-  const uint32_t k = tile_off[i / kBlock] + m.y + __popc(m.x & ((1u << l) - 1u));
+  const uint32_t below = (1u << l) - 1u;
+  const uint32_t k = tile_off[i / kBlock] + m.y + __popc(m.x & below);
   const AoOut a = ao_sample(rays[i], hits[i], pixid[i], int(l), int(ns));
   float4* op = reinterpret_cast<float4*>(out + k);
   op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
   op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
   if (src) src[k] = int32_t(i);
+  if (order) {
+    // Trace order: within each aligned block of kAoGroup source rays the
+    // block's AO rays sample-major -- (l, then ray).  The spp rays of a
+    // pixel share pixid, hence every sample's seed pixid * (l + 1): the
+    // rays of one sample leave nearly the same point in nearly the same
+    // direction and now sit on neighbouring lanes.  The block's rays occupy
+    // the same output range in both orders, so this is a permutation of
+    // [0, count).
+    const uint32_t M = npairs / ns;
+    const uint32_t i0 = i & ~(kAoGroup - 1u);
+    const uint32_t ie = i0 + kAoGroup < M ? i0 + kAoGroup : M;
+    uint32_t pos = tile_off[i0 / kBlock] + meta[i0].y;
+    for (uint32_t j = i0; j < ie; ++j) {
+      const uint32_t mj = meta[j].x;
+      pos += __popc(mj & below) + (j < i ? (mj >> l) & 1u : 0u);
+    }
+    order[pos] = k;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_iota(uint32_t* __restrict__ out, uint32_t n) {
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) out[j] = j;
 }
 
 }  // namespace
@@ -1552,7 +1579,7 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
 hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
-                           void* scratch) {
+                           void* scratch, uint32_t* order) {
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
   const uint32_t npairs = uint32_t(M * size_t(nsamples));
   if (nsamples <= 32) {
@@ -1563,7 +1590,7 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
                                             uint32_t(nsamples), meta, tiles);
     k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
     k_spawn_ao_write_masked<<<(npairs + kBlock - 1) / kBlock, kBlock, 0, s>>>(
-        rays, hits, pixid, npairs, uint32_t(nsamples), meta, tiles, out_rays, out_src);
+        rays, hits, pixid, npairs, uint32_t(nsamples), meta, tiles, out_rays, out_src, order);
     return hipGetLastError();
   }
   const uint32_t g = (npairs + kAoTile - 1) / kAoTile;
@@ -1572,6 +1599,8 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
   k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
   k_spawn_ao_write<<<g, kBlock, 0, s>>>(rays, hits, pixid, npairs, uint32_t(nsamples), tiles,
                                         out_rays, out_src);
+  // more samples than a mask holds: the trace order is the output order
+  if (order) k_iota<<<(npairs + kBlock - 1) / kBlock, kBlock, 0, s>>>(order, npairs);
   return hipGetLastError();
 }
 

@@ -352,16 +352,33 @@ class RtContext:
                                                 int(spp), tx, ty, tw, th, a, b, c),
                     "eye_rays_ooc")
 
-    def spawn_shadows_ao(self, rays, hits, pixid, n, nsamples, out_rays, out_src, d_count):
-        """ooc::ShaderAo rays (nsamples per hit), compacted (device)."""
+    def spawn_shadows_ao(self, rays, hits, pixid, n, nsamples, out_rays, out_src, d_count,
+                         order=None):
+        """ooc::ShaderAo rays (nsamples per hit), compacted (device); order
+        (optional, uint32/int32 device tensor): their sample-major trace order."""
         a, k1 = _addr(rays)
         b, k2 = _addr(hits)
         p, k3 = _addr(pixid)
         c, k4 = _addr(out_rays)
         d, k5 = _addr(out_src)
         e, k6 = _addr(d_count)
-        self._check(lib().spray_rt_spawn_shadows_ao(self.h, a, b, p, int(n), int(nsamples),
-                                                    c, d, e), "spawn_shadows_ao")
+        if order is None:
+            self._check(lib().spray_rt_spawn_shadows_ao(self.h, a, b, p, int(n), int(nsamples),
+                                                        c, d, e), "spawn_shadows_ao")
+            return
+        o, k7 = _addr(order)
+        self._check(lib().spray_rt_spawn_shadows_ao_ordered(self.h, a, b, p, int(n),
+                                                            int(nsamples), c, d, e, o),
+                    "spawn_shadows_ao_ordered")
+
+    def occluded_scene_order(self, rays, max_rays, order, d_count, occ):
+        """Any hit of rays order[j], j < *d_count; occ[order[j]] written (device)."""
+        a, k1 = _addr(rays)
+        o, k2 = _addr(order)
+        b, k3 = _addr(d_count)
+        c, k4 = _addr(occ)
+        self._check(lib().spray_rt_occluded_scene_order(self.h, a, int(max_rays), o, b, c),
+                    "occluded_scene_order")
 
     # ---- frame layer (shading, film, tiles) ----
     def set_bsdfs(self, bsdfs):

@@ -58,4 +58,35 @@ def test_ao16_spawn_and_occlusion(oracle, ns):
         rt.sync()
         o = occ.cpu().numpy()
         assert (o == ref).all() and 0 < o.sum() < m
+
+    # the sample-major trace order: same rays, a permutation of [0, m) that
+    # keeps each 8-ray block's range, and the same occlusion bits
+    out2 = torch.empty_like(out)
+    osrc2 = torch.empty_like(osrc)
+    cnt2 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    order = torch.full((n * ns,), -1, dtype=torch.int32, device="cuda")
+    rt.spawn_shadows_ao(rays, h, pixid, n, ns, out2, osrc2, cnt2, order=order)
+    rt.sync()
+    assert int(cnt2.item()) == m
+    assert out2[:m].cpu().numpy().tobytes() == out[:m].cpu().numpy().tobytes()
+    ordh = order[:m].cpu().numpy().astype(np.int64)
+    assert np.array_equal(np.sort(ordh), np.arange(m))
+    assert np.array_equal(src[ordh] // 8, src // 8)
+    if ns <= 32:
+        # blocks whose rays spawn all ns samples: (sample, ray) ascending
+        first = np.searchsorted(src, src)
+        rank = np.arange(m) - first
+        per = np.bincount(src, minlength=n)
+        full = np.array([(per[b * 8:b * 8 + 8] % ns == 0).all() for b in range(n // 8 + 1)])
+        sel = full[src[ordh] // 8]
+        key = (src[ordh] // 8) * 4096 + rank[ordh] * 8 + src[ordh] % 8
+        k = key[sel]
+        assert sel.sum() > m // 2 and (np.diff(k) > 0).all()
+    for mode in (rt.RAYS_ADAPTIVE, rt.RAYS_INCOHERENT):
+        rt.set_coherence(mode)
+        occ = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+        rt.occluded_scene_order(out2, m, order, cnt2, occ)
+        rt.sync()
+        assert (occ.cpu().numpy() == ref).all()
+    rt.set_coherence(rt.RAYS_ADAPTIVE)
     scene.close()
