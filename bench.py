@@ -159,13 +159,13 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
 
-    rt.set_coherence(rt.RAYS_INCOHERENT)  # hemisphere rays: one walk per lane
-
     def frame():
+        rt.set_coherence(rt.RAYS_COHERENT)  # camera rays: packets
         rt.intersect_scene(prim, hits)
         # the spp rays of a pixel share every sample direction (seed
         # pixid * (l + 1)): traced sample-major, they sit on neighbouring lanes
         rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order)
+        rt.set_coherence(rt.RAYS_INCOHERENT)  # hemisphere rays: one walk per lane
         rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
 
     for _ in range(args.warmup):
