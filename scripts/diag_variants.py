@@ -37,14 +37,14 @@ def run():
         if lib:
             env["SPRAY_RT_LIB"] = lib
         r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10",
-                            "--warmup", "2", "--cpu-baseline", "0"], env=env,
+                            "--warmup", "2", "--cpu-baseline", "0", "--frame", "0", "--ooc", "0"], env=env,
                            capture_output=True, text=True, timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
         if not line:
             print(name, "FAILED", r.returncode, r.stderr[-800:])
             continue
         j = json.loads(line[-1])
-        print("%-14s step %.4f ms  %s" % (name, j["ms_per_step"], json.dumps(j["kernels_ms"])),
+        print("%-14s step %.4f ms  ao %.4f ms  %s" % (name, j["ms_per_step"], j.get("ao", {}).get("ms_per_step", 0), json.dumps(j["kernels_ms"])),
               flush=True)
 
 

@@ -672,7 +672,8 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
   if (!kPersist) {
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
-    const bool ok = j < M && (!A.valid || A.valid[i]);
+    // an index list entry past the ray buffer is skipped, never read
+    const bool ok = j < M && i < A.M && (!A.valid || A.valid[i]);
     if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (ok)
@@ -704,7 +705,7 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void
         for (uint32_t c = 0; c < kChunk; c += 64) {
           const size_t j = begin + base + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
-          const bool ok = j < end && (!A.valid || A.valid[i]);
+          const bool ok = j < end && i < A.M && (!A.valid || A.valid[i]);
           flag = false;
           if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);

@@ -74,8 +74,8 @@ __device__ __forceinline__ void unpack_rgb(uint32_t c, float kd[3]) {
 // v.z = sqrt(max(0, 1 - x^2 - y^2)), normalize, localToWorld (mat3(dx, dy,
 // N) * v), normalize; pdf = v.z / pi.  theta *= SPRAY_PI / 4.f is a double
 // product (M_PI is a double).
-__device__ __forceinline__ void cosine_hemisphere(float u1, float u2, const float N[3],
-                                                  float wi[3], float& pdf) {
+// Split in two: the sample in the local frame (a function of u1, u2 only) ...
+__device__ __forceinline__ void hemisphere_local(float u1, float u2, float lv[3]) {
   const float sx = 2 * u1 - 1, sy = 2 * u2 - 1;
   float dx, dy;
   if (sx == 0.0f && sy == 0.0f) {
@@ -107,8 +107,15 @@ __device__ __forceinline__ void cosine_hemisphere(float u1, float u2, const floa
     dx = rr * float(cd);
     dy = rr * float(sd);
   }
-  float lv[3] = {dx, dy, sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy))};
+  lv[0] = dx;
+  lv[1] = dy;
+  lv[2] = sqrtf(fmaxf(0.f, (1.f - dx * dx) - dy * dy));
   gnorm3(lv);
+}
+
+// ... rotated into the frame of N (localToWorld), and its pdf.
+__device__ __forceinline__ void hemisphere_world(const float lv[3], const float N[3],
+                                                 float wi[3], float& pdf) {
   const float dx0[3] = {0.f, N[2], -N[1]}, dx1[3] = {-N[2], 0.f, N[0]};
   float ax[3];
   const float* pick = gdot3(dx0, dx0) > gdot3(dx1, dx1) ? dx0 : dx1;
@@ -124,6 +131,13 @@ __device__ __forceinline__ void cosine_hemisphere(float u1, float u2, const floa
   wi[2] = (ax[2] * lv[0] + ay[2] * lv[1]) + N[2] * lv[2];
   gnorm3(wi);
   pdf = lv[2] * kOneOverPi;
+}
+
+__device__ __forceinline__ void cosine_hemisphere(float u1, float u2, const float N[3],
+                                                  float wi[3], float& pdf) {
+  float lv[3];
+  hemisphere_local(u1, u2, lv);
+  hemisphere_world(lv, N, wi, pdf);
 }
 
 // blinnPhong (reflection.h:202-214): li * (kd * costheta + ks * pow(n.h, s))
