@@ -229,14 +229,6 @@ int drain(spray_rt_ooc* o, bool reverse, const std::vector<float>& boxes, Launch
   return flush();
 }
 
-int host_boxes(spray_rt_ooc* o, std::vector<float>* boxes) {
-  spray_rt_ctx* c = o->ctx;
-  boxes->resize(6 * size_t(c->ndom));
-  HIPCHK(c, hipMemcpy(boxes->data(), c->d_boxes, boxes->size() * sizeof(float),
-                      hipMemcpyDeviceToHost));
-  return SPRAY_RT_OK;
-}
-
 int check_batch(spray_rt_ooc* o, const void* rays, size_t M, const void* out) {
   if (!o) return SPRAY_RT_ERR_ARG;
   spray_rt_ctx* c = o->ctx;
@@ -339,8 +331,7 @@ int spray_rt_ooc_intersect(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
     HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&o->tie), M * sizeof(uint64_t)));
     o->tie_cap = M;
   }
-  std::vector<float> boxes;
-  if ((r = host_boxes(o, &boxes))) return r;
+  const std::vector<float>& boxes = c->h_boxes;
   if ((r = build_queues(o, rays, nullptr, M))) return r;
   HIPCHK(c, launch_ooc_init(stream_of(c), hits, o->tie, M));
   uint64_t* key = o->tie;
@@ -359,8 +350,7 @@ int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
   spray_rt_ctx* c = o->ctx;
   if (valid && !is_device_ptr(valid))
     return fail(c, SPRAY_RT_ERR_ARG, "valid must be device memory");
-  std::vector<float> boxes;
-  if ((r = host_boxes(o, &boxes))) return r;
+  const std::vector<float>& boxes = c->h_boxes;
   if ((r = build_queues(o, rays, valid, M))) return r;
   HIPCHK(c, launch_ooc_clear_occ(stream_of(c), valid, occluded, M));
   return drain(o, true, boxes, [&](hipStream_t s, const OocBatch& B) {

@@ -437,6 +437,7 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   c->ntlas = 0;
   c->tlas_depth = 0;
   c->ndom = ndomains;
+  c->h_boxes.assign(boxes, boxes + 6 * size_t(ndomains));
   c->dom2slot.assign(ndomains, -1);
   c->dom_dirty = true;
   if (ndomains == 0) return SPRAY_RT_OK;

@@ -48,6 +48,7 @@ struct spray_rt_ctx {
   // scene path
   int ndom = 0;
   float* d_boxes = nullptr;
+  std::vector<float> h_boxes;  // the same boxes on the host (ooc drain views)
   int* d_dom2slot = nullptr;
   DomTrav* d_domtrav = nullptr;  // per-domain traversal descriptors
   int* d_owner = nullptr;        // in-situ domain -> rank map
