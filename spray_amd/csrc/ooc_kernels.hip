@@ -312,13 +312,19 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
 }
 
 size_t ooc_temp_bytes(size_t M, size_t pairs) {
+  // size queries only; a failed query leaves 0, and the launch that needs the
+  // scratch then reports its error
   size_t a = 0, b = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, a, static_cast<uint32_t*>(nullptr),
-                                   static_cast<uint32_t*>(nullptr), int(M + 1));
-  hipcub::DeviceRadixSort::SortPairs(nullptr, b, static_cast<uint16_t*>(nullptr),
-                                     static_cast<uint16_t*>(nullptr),
-                                     static_cast<uint32_t*>(nullptr),
-                                     static_cast<uint32_t*>(nullptr), int(pairs), 0, 8);
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, a, static_cast<uint32_t*>(nullptr),
+                                       static_cast<uint32_t*>(nullptr),
+                                       int(M + 1)) != hipSuccess)
+    a = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, static_cast<uint16_t*>(nullptr),
+                                         static_cast<uint16_t*>(nullptr),
+                                         static_cast<uint32_t*>(nullptr),
+                                         static_cast<uint32_t*>(nullptr), int(pairs), 0,
+                                         8) != hipSuccess)
+    b = 0;
   return a > b ? a : b;
 }
 

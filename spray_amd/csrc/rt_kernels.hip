@@ -630,6 +630,9 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
   }
 }
 
+// The closest-hit register target (SPRAY_WAVES_CH) applies to the 16-entry
+// stack over <= 64 domains; the 24-entry stack and the 256-domain tables
+// are LDS-bound below it anyway.
 // STK: traversal-stack entries per lane, >= the depth of every resident
 // slot tree and of the top-level tree (a node at depth k has at most k
 // pending siblings).  LDS = STK KiB + 4 KiB per 64 domains, so STK 16 lets 8
@@ -638,7 +641,7 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
 // and per-lane for the others (any-hit only; the counting variants always
 // walk per lane, the canonical order the counts are defined on).
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
-__global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : SPRAY_WAVES_CH) void k_scene(
+__global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : (W == 1 && STK == 16 ? SPRAY_WAVES_CH : 1)) void k_scene(
     SceneArgs A) {
   // packet form for the non-counting kernels; any-hit waves fall back to
   // the per-lane walk when their rays are not coherent (AO hemispheres)
