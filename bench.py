@@ -1,14 +1,16 @@
 """Headline benchmark: Mrays/s (primary + shadow) on the 64-domain wavelets
 scene at 1024x1024, 8 spp (BASELINE.json, configs[1]).
 
-One step = one frame of the hot path over rays already resident in HBM:
+One step = one frame of the hot path over rays already resident in HBM,
+as ONE launch (spray_rt_intersect_scene_shadow_pt):
   1. closest hit of the 8,388,608 primary rays against every domain of their
-     sorted domain lists (spray_rt_intersect_scene: domain query + BVH2
-     traversal + updateIntersection epilogue, one launch),
-  2. point-light shadow-ray spawn of ooc::ShaderPt -- fused into the epilogue
-     of (1) (spray_rt_intersect_scene_spawn_pt: positional, with a valid flag),
-  3. any hit of the spawned shadow rays (spray_rt_occluded_scene_masked:
-     in-wave ballot compaction of the valid rays).
+     sorted domain lists (domain query + BVH2 traversal + updateIntersection
+     epilogue),
+  2. point-light shadow-ray spawn of ooc::ShaderPt in the epilogue of (1),
+  3. any hit of the spawned shadow rays: each wave queues its shadow rays in
+     LDS and traces them as 64-ray packets.
+The same work as two launches (spawn_pt, then select + any hit) is timed
+beside it ("unfused").
 Primary rays are generated once before timing by the reference's camera /
 sampler (ooc::Tracer::genMultiEyes over its 8 blocking tiles of 1024x128).
 
@@ -358,22 +360,26 @@ def main():
     rt.set_coherence(rt.RAYS_COHERENT)  # camera rays and point-light shadow rays
 
     def step(ev=None):
-        # closest hit with the PT shadow spawn fused into its epilogue, then
-        # any hit over the spawned rays (count stays on the device)
+        # closest hit + PT shadow spawn + the shadow rays' any hit, one launch
         if ev:
             ev[0].record(stream)
-        rt.intersect_scene_spawn_pt(prim, hits, SHADE, shadow, valid, nsh)
+        rt.intersect_scene_shadow_pt(prim, hits, SHADE, occ, valid, nsh)
         if ev:
             ev[1].record(stream)
-            ev[2].record(stream)
+
+    def step_unfused(ev):
+        # the same as two launches: closest hit with the fused positional
+        # spawn, then select + any hit of the spawned rays
+        ev[0].record(stream)
+        rt.intersect_scene_spawn_pt(prim, hits, SHADE, shadow, valid, nsh)
+        ev[1].record(stream)
         rt.occluded_scene_masked(shadow, valid, occ)
-        if ev:
-            ev[3].record(stream)
+        ev[2].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -389,17 +395,25 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     assert int(nsh.item()) == n_shadow
-
-    ch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    sp_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    ah_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    fused_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     ms_step = elapsed / args.steps * 1e3
     rays_step = n_prim + n_shadow
     value = rays_step * world * args.steps / elapsed / 1e6
 
+    # the two-launch form of the same step, for comparison (untimed by the
+    # step clock above)
+    uev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for k in range(args.steps):
+        step_unfused(uev[k])
+    torch.cuda.synchronize()
+    ch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in uev]))
+    ah_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in uev]))
+
     pc, sh = gpu_counts["primary"], gpu_counts["shadow"]
     ch_bytes = algorithmic_bytes(n_prim, pc["nodes"], pc["tris"], 32)
     ah_bytes = algorithmic_bytes(n_shadow, sh["nodes"], sh["tris"], 4)
+    fused_bytes = ch_bytes + ah_bytes
+    fused_gbs = fused_bytes / (fused_ms * 1e-3) / 1e9
     ch_gbs = ch_bytes / (ch_ms * 1e-3) / 1e9
     ah_gbs = ah_bytes / (ah_ms * 1e-3) / 1e9
     traffic = None
@@ -418,15 +432,17 @@ def main():
                                "resident per GPU (configs[1])",
                    "rays_per_step": rays_step, "primary_rays": n_prim, "shadow_rays": n_shadow,
                    "parallelism": "frame replicas x%d (weak)" % world},
-        "roofline": {"bound": "hbm", "achieved": round(ch_gbs, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ch_gbs / HBM_PEAK_GBS, 4),
+        "roofline": {"bound": "hbm", "achieved": round(fused_gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(fused_gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "k_scene<closest-hit, fused PT spawn> (primary)",
-                     "bytes_per_launch": ch_bytes, "avg_launch_ms": round(ch_ms, 4),
+                     "kernel": "k_scene<closest hit + PT spawn + shadow any hit> (one launch)",
+                     "bytes_per_launch": fused_bytes, "avg_launch_ms": round(fused_ms, 4),
                      "counts": counts_src},
-        "kernels_ms": {"intersect_scene_spawn_pt": round(ch_ms, 4),
-                       "occluded_scene": round(ah_ms, 4),
-                       "occluded_achieved_GBs": round(ah_gbs, 1)},
+        "kernels_ms": {"intersect_scene_shadow_pt": round(fused_ms, 4),
+                       "unfused": {"intersect_scene_spawn_pt": round(ch_ms, 4),
+                                   "occluded_scene_masked": round(ah_ms, 4),
+                                   "closest_hit_achieved_GBs": round(ch_gbs, 1),
+                                   "any_hit_achieved_GBs": round(ah_gbs, 1)}},
         "canonical_counts": gpu_counts,
     }
     if args.ao:

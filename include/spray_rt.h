@@ -191,6 +191,18 @@ int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t ctx, const spray_rt_ray* ra
                                       size_t M, spray_rt_hit* hits,
                                       const float shade[10], spray_rt_ray* out_rays,
                                       uint8_t* out_valid, uint32_t* d_count);
+/* Closest hit, PT shadow spawn and the shadow rays' any hit in ONE launch:
+ * hits[i] as spray_rt_intersect_scene; sh_valid[i] = 1 when ray i spawned a
+ * point-light shadow ray (as spray_rt_intersect_scene_spawn_pt's out_valid),
+ * occluded[i] = its any-hit result (written where sh_valid[i]), *d_count
+ * (optional, device) = number of shadow rays.  The shadow rays never leave
+ * the chip: each wave queues its spawned rays in LDS and traces them as
+ * 64-ray packets.  Results equal spawn_pt + occluded_scene_masked.  Device
+ * buffers only. */
+int spray_rt_intersect_scene_shadow_pt(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                       size_t M, spray_rt_hit* hits, const float shade[10],
+                                       uint8_t* occluded, uint8_t* sh_valid,
+                                       uint32_t* d_count);
 /* Any hit over the rays i < M with valid[i] != 0 (e.g. the positional spawn
  * output): occluded[i] is written for those rays only.  The valid rays are
  * first compacted into an ascending index list (device select), so the

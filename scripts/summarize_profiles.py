@@ -74,7 +74,10 @@ def main(src, tag):
                           "bytes_lower": fs * 1024 + ws * 1024,
                           "bytes_corrected": 2 * fs * 1024 + ws * 1024,
                           "avg_us": float(r["AverageNs"]) / 1e3}
-    ch = [v for k, v in traffic.items() if k.startswith("k_scene<1, false, false, 1,")]
+    # the bench step's launch: the fused closest hit + shadow any hit (EPI 3),
+    # else (older profiles) the closest hit with the fused spawn (EPI 1)
+    ch = [v for k, v in traffic.items() if k.startswith("k_scene<1, false, false, 3,")]
+    ch = ch or [v for k, v in traffic.items() if k.startswith("k_scene<1, false, false, 1,")]
     out = {"source": src, "round": tag, "per_kernel": traffic}
     if ch:
         out["scene_intersect_bytes_per_launch"] = ch[0]["bytes_corrected"]

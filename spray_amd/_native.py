@@ -86,6 +86,7 @@ SIGNATURES = {
     "spray_rt_occluded_scene_devcount": (I, [P, P, SZ, P, P, P]),
     "spray_rt_intersect_scene_spawn_pt": (I, [P, P, SZ, P, P, P, P, P]),
     "spray_rt_occluded_scene_masked": (I, [P, P, SZ, P, P]),
+    "spray_rt_intersect_scene_shadow_pt": (I, [P, P, SZ, P, P, P, P, P]),
     "spray_rt_eye_rays_ooc": (I, [P, P, I, I, I, I, I, I, P, P, P]),
     "spray_rt_eye_rays_insitu": (I, [P, P, I, I, I, I, I, I, I, I, I, I, P, P, P]),
     "spray_rt_set_owners": (I, [P, P]),

@@ -638,6 +638,23 @@ int spray_rt_intersect_scene_spawn_pt(spray_rt_ctx_t c, const spray_rt_ray* rays
   return SPRAY_RT_OK;
 }
 
+int spray_rt_intersect_scene_shadow_pt(spray_rt_ctx_t c, const spray_rt_ray* rays, size_t M,
+                                       spray_rt_hit* hits, const float shade[10],
+                                       uint8_t* occluded, uint8_t* sh_valid,
+                                       uint32_t* d_count) {
+  int r = scene_common(c, rays, M, hits);
+  if (r) return r;
+  if (!shade) return fail(c, SPRAY_RT_ERR_ARG, "null shade parameters");
+  if (M > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "M > 2^32");
+  if ((d_count && !is_device_ptr(d_count)) ||
+      (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(occluded) ||
+             !is_device_ptr(sh_valid))))
+    return fail(c, SPRAY_RT_ERR_ARG, "fused shadow tracing needs device buffers");
+  HIPCHK(c, launch_scene_intersect_shadow_pt(stream_of(c), view(c), rays, M, hits, shade,
+                                             occluded, sh_valid, d_count));
+  return SPRAY_RT_OK;
+}
+
 int spray_rt_occluded_scene_masked(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                    size_t M, const uint8_t* valid, uint8_t* occ) {
   int r = scene_common(c, rays, M, occ);

@@ -74,6 +74,15 @@ hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
                                      spray_rt_ray* out_rays, uint8_t* out_valid,
                                      uint32_t* d_count);
 
+// Closest hit, the fused PT shadow spawn and the shadow rays' any hit in one
+// launch: sh_valid[i] = source i spawned a shadow ray, occluded[i] (written
+// where sh_valid[i]) = it is blocked; *d_count (may be null) = shadow rays.
+hipError_t launch_scene_intersect_shadow_pt(hipStream_t s, const SceneView& v,
+                                            const spray_rt_ray* rays, size_t M,
+                                            spray_rt_hit* hits, const float* shade10,
+                                            uint8_t* occluded, uint8_t* sh_valid,
+                                            uint32_t* d_count);
+
 // Closest hit + composite key per ray for in-situ compositing:
 // (t bits << 32) | (position in the ray's sorted domain list << 16) | domain,
 // 0x7FFF...F on a miss (non-resident domains are skipped but counted).

@@ -53,6 +53,9 @@ namespace {
 #ifndef SPRAY_WAVES_CH
 #define SPRAY_WAVES_CH 6
 #endif
+#ifndef SPRAY_WAVES_SHADOW
+#define SPRAY_WAVES_SHADOW 6
+#endif
 #ifndef SPRAY_WAVES_AH
 #define SPRAY_WAVES_AH 1
 #endif
@@ -213,6 +216,7 @@ struct SceneArgs {
 constexpr int kEpiNone = 0;   // hit records only
 constexpr int kEpiSpawn = 1;  // + fused PT shadow spawn (positional)
 constexpr int kEpiKeys = 2;   // + 64-bit composite key (t, list position, domain)
+constexpr int kEpiShadow = 3; // + PT spawn and the shadow ray's any hit, same launch
 
 // Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): one work
 // queue of the persistent launches; bands 8x .. 8x+7 (a contiguous eighth of
@@ -421,16 +425,23 @@ __device__ __forceinline__ bool wave_coherent(const SceneArgs& A, size_t i, bool
 // their domains out of list order, so a lane's running hit is replaced by a
 // nearer t, or by an equal t of an earlier list entry (smaller (box entry
 // t, id)); that is exactly the sequential walk's result.
+// rin (optional): the lane's ray as org[3], dir[3] (a shadow ray queued in
+// LDS, tnear = SPRAY_RAY_EPSILON, tfar = +inf) instead of A.rays[i]; i is
+// then only the index its result is written at.
 template <int W, bool ANY, int EPI>
 __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, bool valid,
                                                  const float4* stl, const float* sbox,
                                                  const float4* sdom, int32_t* wstk,
-                                                 bool& spawn, float* pos, float* wi) {
+                                                 bool& spawn, float* pos, float* wi,
+                                                 const float* rin = nullptr) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int lane = threadIdx.x & 63;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  if (valid) {
+  if (valid && rin) {
+    o4 = make_float4(rin[0], rin[1], rin[2], kRayEpsilon);
+    d4 = make_float4(rin[3], rin[4], rin[5], kInf);
+  } else if (valid) {
     const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
     o4 = rp[0];
     d4 = rp[1];
@@ -577,7 +588,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     }
     A.keys[i] = key;
   }
-  if (EPI == kEpiSpawn && best_dom >= 0 && SPRAY_DIAG_MODE != 7) {
+  if ((EPI == kEpiSpawn || EPI == kEpiShadow) && best_dom >= 0 && SPRAY_DIAG_MODE != 7) {
     spray_rt_hit h;
     h.t = h0.x;
     h.color = __float_as_uint(h1.w);
@@ -633,6 +644,84 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
 // The closest-hit register target (SPRAY_WAVES_CH) applies to the 16-entry
 // stack over <= 64 domains; the 24-entry stack and the 256-domain tables
 // are LDS-bound below it anyway.
+// Fused shadow tracing (kEpiShadow): a per-wave LDS queue of the spawned
+// point-light shadow rays.  A wave's chunks append their shadow rays until
+// 64 are waiting, which then walk the scene as one any-hit packet -- right
+// after their primary rays, while the nodes those just visited are still in
+// the caches -- and the rest is traced when the wave runs out of work.
+// occ[i] / sh_valid[i] are positional by source ray, as the two-launch form
+// (spawn, select, any hit) writes them.
+constexpr uint32_t kShadowQ = 128;  // >= 63 waiting + 64 new
+struct ShadowQueue {
+  float* ray;     // [kShadowQ][6]: org, dir
+  uint32_t* src;  // [kShadowQ]: source ray index
+  uint32_t n;     // waiting (wave-uniform)
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int W>
+__device__ __forceinline__ void shadow_trace(const SceneArgs& A, const ShadowQueue& q,
+                                             uint32_t cnt, const float4* stl, const float* sbox,
+                                             const float4* sdom, int32_t* wstk) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool v = lane < cnt;
+  const size_t s = v ? q.src[lane] : 0;
+  bool f = false;
+  float p[3], w[3];
+  scene_ray_packet<W, true, kEpiNone>(A, s, v, stl, sbox, sdom, wstk, f, p, w, q.ray + 6 * lane);
+}
+
+template <int W>
+__device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, bool active,
+                                            bool flag, size_t i, const float* pos,
+                                            const float* wi, const float4* stl,
+                                            const float* sbox, const float4* sdom,
+                                            int32_t* wstk) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (active) A.sh_valid[i] = flag ? 1 : 0;
+  const unsigned long long bal = __ballot(flag);
+  if (!bal) return;
+  if (A.sh_count && lane == 0) atomicAdd(A.sh_count, uint32_t(__popcll(bal)));
+  if (flag) {
+    const uint32_t k = q.n + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
+    float* e = q.ray + 6 * k;
+    e[0] = pos[0];
+    e[1] = pos[1];
+    e[2] = pos[2];
+    e[3] = wi[0];
+    e[4] = wi[1];
+    e[5] = wi[2];
+    q.src[k] = uint32_t(i);
+  }
+  q.n += uint32_t(__popcll(bal));
+  if (q.n < 64) return;
+  wave_lds_sync();
+  shadow_trace<W>(A, q, 64, stl, sbox, sdom, wstk);
+  // the remainder (< 64) moves to the front
+  const uint32_t rest = q.n - 64;
+  const bool mv = lane < rest;
+  float e[6];
+  uint32_t si = 0;
+  if (mv) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e[k] = q.ray[6 * (64 + lane) + k];
+    si = q.src[64 + lane];
+  }
+  wave_lds_sync();
+  if (mv) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) q.ray[6 * lane + k] = e[k];
+    q.src[lane] = si;
+  }
+  wave_lds_sync();
+  q.n = rest;
+}
+
 // STK: traversal-stack entries per lane, >= the depth of every resident
 // slot tree and of the top-level tree (a node at depth k has at most k
 // pending siblings).  LDS = STK KiB + 4 KiB per 64 domains, so STK 16 lets 8
@@ -641,7 +730,11 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
 // and per-lane for the others (any-hit only; the counting variants always
 // walk per lane, the canonical order the counts are defined on).
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
-__global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : (W == 1 && STK == 16 ? SPRAY_WAVES_CH : 1)) void k_scene(
+__global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH
+                                     : (W == 1 && STK == 16
+                                            ? (EPI == kEpiShadow ? SPRAY_WAVES_SHADOW
+                                                                 : SPRAY_WAVES_CH)
+                                            : 1)) void k_scene(
     SceneArgs A) {
   // packet form for the non-counting kernels; any-hit waves fall back to
   // the per-lane walk when their rays are not coherent (AO hemispheres)
@@ -654,6 +747,11 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : (W == 1 && STK == 16
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
   __shared__ int32_t wstack[(kBlock / 64) * kStack];  // top-level stacks, one per wave
+  constexpr bool kShadow = EPI == kEpiShadow;
+  __shared__ float sq_ray[kShadow ? (kBlock / 64) * kShadowQ * 6 : 1];
+  __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
+  ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
+                 sq_src + (kShadow ? (threadIdx.x >> 6) * kShadowQ : 0), 0u};
   size_t M = A.M;
   if (A.d_count) {  // ray count produced on the device
     const size_t dc = *A.d_count;
@@ -683,6 +781,7 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : (W == 1 && STK == 16
       scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
     if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
+    if (kShadow) shadow_push<W>(A, sq, j < M, flag, i, pos, wi, stl, sbox, sdom, wstk);
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     constexpr uint32_t kPerXcd = kQueues / 8;
@@ -716,10 +815,16 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH : (W == 1 && STK == 16
             scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
+          if (kShadow)
+            shadow_push<W>(A, sq, j < end, flag, i, pos, wi, stl, sbox, sdom, wstk);
         }
         base = __builtin_amdgcn_readfirstlane(next);
       }
     }
+  }
+  if (kShadow && sq.n) {  // the wave's last shadow rays (fewer than 64)
+    wave_lds_sync();
+    shadow_trace<W>(A, sq, sq.n, stl, sbox, sdom, wstk);
   }
   if (COUNT) {
     atomicAdd(&A.counters[0], (unsigned long long)nnode);
@@ -1327,7 +1432,7 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
-  if (e == hipSuccess && EPI == kEpiSpawn && a.sh_count)
+  if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow) && a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
@@ -1473,6 +1578,26 @@ hipError_t launch_scene_intersect_pt(hipStream_t s, const SceneView& v,
   a.sh_valid = out_valid;
   a.sh_count = d_count;
   return launch_scene_w<false, kEpiSpawn>(s, a, v);
+}
+
+hipError_t launch_scene_intersect_shadow_pt(hipStream_t s, const SceneView& v,
+                                            const spray_rt_ray* rays, size_t M,
+                                            spray_rt_hit* hits, const float* shade10,
+                                            uint8_t* occluded, uint8_t* sh_valid,
+                                            uint32_t* d_count) {
+  if (M == 0) return d_count ? hipMemsetAsync(d_count, 0, sizeof(uint32_t), s) : hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.hits = hits;
+  for (int k = 0; k < 3; ++k) {
+    a.shade.lp[k] = shade10[k];
+    a.shade.lr[k] = shade10[3 + k];
+    a.shade.ks[k] = shade10[6 + k];
+  }
+  a.shade.shininess = shade10[9];
+  a.occ = occluded;
+  a.sh_valid = sh_valid;
+  a.sh_count = d_count;
+  return launch_scene_w<false, kEpiShadow>(s, a, v);
 }
 
 hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,

@@ -279,6 +279,21 @@ class RtContext:
         self._check(lib().spray_rt_intersect_scene_spawn_pt(self.h, a, n, b, shade.ctypes.data,
                                                             c, d, e), "intersect_scene_spawn_pt")
 
+    def intersect_scene_shadow_pt(self, rays, hits, shade, occ, sh_valid, d_count=None):
+        """Closest hit + PT shadow spawn + the shadows' any hit, one launch
+        (device buffers): sh_valid[i], occ[i] positional by source ray."""
+        n = _nbytes(rays) // 32
+        shade = np.ascontiguousarray(shade, np.float32)
+        assert shade.size == 10
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        c, k3 = _addr(occ)
+        d, k4 = _addr(sh_valid)
+        e, k5 = _addr(d_count)
+        self._check(lib().spray_rt_intersect_scene_shadow_pt(self.h, a, n, b, shade.ctypes.data,
+                                                             c, d, e),
+                    "intersect_scene_shadow_pt")
+
     def occluded_scene_devcount(self, rays, max_rays, d_count, occ, counters=None):
         a, k1 = _addr(rays)
         b, k2 = _addr(d_count)

@@ -406,3 +406,43 @@ def test_masked_occlusion_sparse_patterns(spray, oracle, scene64):
         o = occ.cpu().numpy()
         assert np.array_equal(o[mask == 1], ref[mask == 1])
         assert (o[mask == 0] == 9).all()
+
+
+@pytest.mark.parametrize("cut", [0, 37, 4000])
+def test_fused_shadow_trace_matches_two_launches(spray, oracle, scene64, cut):
+    """intersect_scene_shadow_pt (closest hit + spawn + the shadows' any hit,
+    one launch, per-wave LDS queues) equals spawn_pt + occluded_scene_masked
+    and the oracle, including ragged batch sizes and partial queues."""
+    import torch
+    sc, osc, doms, lights = scene64
+    _, org, d, _ = bench_tile(oracle, (320, 400, 384, 64), 8)
+    n = len(org) - cut
+    org, d = org[:n], d[:n]
+    rays = torch.from_numpy(spray.make_rays(org, d).view(np.uint8)).cuda()
+    shade = np.array([0, 500, 1000, 1, 1, 1, 0.4, 0.4, 0.4, 10.0], np.float32)
+    hits = torch.zeros(n * 48, dtype=torch.uint8, device="cuda")
+    occ = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+    sv = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    cnt = torch.full((1,), 123, dtype=torch.int32, device="cuda")
+    sc.rt.intersect_scene_shadow_pt(rays, hits, shade, occ, sv, cnt)
+    hits2 = torch.zeros_like(hits)
+    srays = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    valid = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    cnt2 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    sc.rt.intersect_scene_spawn_pt(rays, hits2, shade, srays, valid, cnt2)
+    occ2 = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+    sc.rt.occluded_scene_masked(srays, valid, occ2)
+    sc.rt.sync()
+    assert hits.cpu().numpy().tobytes() == hits2.cpu().numpy().tobytes()
+    v = sv.cpu().numpy()
+    assert np.array_equal(v, valid.cpu().numpy()) and set(np.unique(v)) <= {0, 1}
+    assert int(cnt.item()) == int(cnt2.item()) == int(v.sum()) > 1000
+    o = occ.cpu().numpy()
+    assert np.array_equal(o[v == 1], occ2.cpu().numpy()[v == 1])
+    assert (o[v == 0] == 9).all()
+    oh, _ = osc.intersect(org, d)
+    so, sd, osrc = oracle.spawn_shadows_pt(org, d, oh, lights[0]["pos"], lights[0]["rad"],
+                                           [0.4, 0.4, 0.4], 10.0)
+    oocc, _ = osc.occluded(so, sd)
+    assert np.array_equal(np.nonzero(v)[0], osrc) and np.array_equal(o[osrc], oocc)
+    assert 0 < oocc.sum() < len(oocc)
