@@ -212,6 +212,13 @@ struct SceneArgs {
   const uint8_t* valid;
 };
 
+// Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
+// rays and records streamed through a frame do not evict BVH nodes from L2
+// (measured: fused step 0.848 / 0.828 vs 0.868 / 0.843 ms on one box).
+#ifndef SPRAY_NT_IO
+#define SPRAY_NT_IO 1
+#endif
+
 // Closest-hit epilogue variants of the scene kernels.
 constexpr int kEpiNone = 0;   // hit records only
 constexpr int kEpiSpawn = 1;  // + fused PT shadow spawn (positional)
@@ -442,9 +449,17 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     o4 = make_float4(rin[0], rin[1], rin[2], kRayEpsilon);
     d4 = make_float4(rin[3], rin[4], rin[5], kInf);
   } else if (valid) {
-    const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
-    o4 = rp[0];
-    d4 = rp[1];
+    const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
+    v4f a, b;
+    if (SPRAY_NT_IO) {  // streamed once: keep L2 for the BVH
+      a = __builtin_nontemporal_load(rp);
+      b = __builtin_nontemporal_load(rp + 1);
+    } else {
+      a = rp[0];
+      b = rp[1];
+    }
+    o4 = make_float4(a.x, a.y, a.z, a.w);
+    d4 = make_float4(b.x, b.y, b.z, b.w);
   }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   uint64_t m[W];
@@ -560,10 +575,17 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
     h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
   }
-  float4* hp = reinterpret_cast<float4*>(A.hits + i);
-  hp[0] = h0;
-  hp[1] = h1;
-  hp[2] = h2;
+  if (SPRAY_NT_IO) {
+    v4f* hp = reinterpret_cast<v4f*>(A.hits + i);
+    __builtin_nontemporal_store(v4f{h0.x, h0.y, h0.z, h0.w}, hp);
+    __builtin_nontemporal_store(v4f{h1.x, h1.y, h1.z, h1.w}, hp + 1);
+    __builtin_nontemporal_store(v4f{h2.x, h2.y, h2.z, h2.w}, hp + 2);
+  } else {
+    float4* hp = reinterpret_cast<float4*>(A.hits + i);
+    hp[0] = h0;
+    hp[1] = h1;
+    hp[2] = h2;
+  }
   if (EPI == kEpiKeys) {
     uint64_t key = 0x7FFFFFFFFFFFFFFFull;
     if (best_dom >= 0) {  // position of best_dom in the ray's sorted list
