@@ -218,6 +218,11 @@ struct SceneArgs {
 #ifndef SPRAY_NT_IO
 #define SPRAY_NT_IO 1
 #endif
+// The same for the per-lane path's ray loads and the AO rays' stores
+// (measured: AO step 6.27 vs 6.41 ms).
+#ifndef SPRAY_NT_IO_LANE
+#define SPRAY_NT_IO_LANE 1
+#endif
 
 // Closest-hit epilogue variants of the scene kernels.
 constexpr int kEpiNone = 0;   // hit records only
@@ -245,8 +250,16 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   spray_rt_hit* __restrict__ hits = A.hits;
   uint8_t* __restrict__ occ = A.occ;
   {
-    const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
-    const float4 o4 = rp[0], d4 = rp[1];
+    const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
+    v4f a, b;
+    if (SPRAY_NT_IO_LANE) {
+      a = __builtin_nontemporal_load(rp);
+      b = __builtin_nontemporal_load(rp + 1);
+    } else {
+      a = rp[0];
+      b = rp[1];
+    }
+    const float4 o4 = make_float4(a.x, a.y, a.z, a.w), d4 = make_float4(b.x, b.y, b.z, b.w);
     const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     uint64_t m[W];
 #pragma unroll
@@ -1376,9 +1389,15 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write_masked(
   const uint32_t below = (1u << l) - 1u;
   const uint32_t k = tile_off[i / kBlock] + m.y + __popc(m.x & below);
   const AoOut a = ao_sample(rays[i], hits[i], pixid[i], int(l), int(ns));
-  float4* op = reinterpret_cast<float4*>(out + k);
-  op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
-  op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
+  if (SPRAY_NT_IO_LANE) {
+    v4f* op = reinterpret_cast<v4f*>(out + k);
+    __builtin_nontemporal_store(v4f{a.o[0], a.o[1], a.o[2], kRayEpsilon}, op);
+    __builtin_nontemporal_store(v4f{a.w[0], a.w[1], a.w[2], kInf}, op + 1);
+  } else {
+    float4* op = reinterpret_cast<float4*>(out + k);
+    op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
+    op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
+  }
   if (src) src[k] = int32_t(i);
   if (order) {
     // Trace order: within each aligned block of kAoGroup source rays the
