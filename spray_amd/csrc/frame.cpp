@@ -19,6 +19,12 @@
 using namespace spray_rt;
 using namespace spray_rt::detail;
 
+// 1: frames of camera rays lit by one point light take the fused launch
+// (fused_frame); 0: every frame takes the general bounce loop.
+#ifndef SPRAY_FRAME_FUSED
+#define SPRAY_FRAME_FUSED 1
+#endif
+
 namespace {
 
 bool shader_ok(const spray_rt_shader* P) {
@@ -44,6 +50,15 @@ struct Carve {
     return p;
   }
 };
+
+// A frame whose whole shading is the point-light term of camera rays (one
+// point light, diffuse surfaces, bounces = 1): its single bounce runs as one
+// fused launch (closest hit + shading + the shadow rays' any hit) and the
+// film.
+bool fused_frame(const spray_rt_ctx* c, const spray_rt_shader* P) {
+  return SPRAY_FRAME_FUSED && P->shader == SPRAY_RT_SHADER_PT && P->bounces == 1 &&
+         P->nlights == 1 && P->lights[0].type == SPRAY_RT_LIGHT_POINT && !c->bsdf_delta;
+}
 
 }  // namespace
 
@@ -73,6 +88,8 @@ int spray_rt_set_bsdfs(spray_rt_ctx_t c, int n, const spray_rt_bsdf* bsdfs) {
   if (c->d_bsdf) HIPCHK(c, hipFree(c->d_bsdf));
   c->d_bsdf = nullptr;
   c->nbsdf = 0;
+  c->bsdf_delta = false;
+  for (int i = 0; i < n; ++i) c->bsdf_delta |= bsdfs[i].type != SPRAY_RT_BSDF_DIFFUSE;
   if (n == 0) return SPRAY_RT_OK;
   HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_bsdf), n * sizeof(spray_rt_bsdf)));
   HIPCHK(c, hipMemcpy(c->d_bsdf, bsdfs, n * sizeof(spray_rt_bsdf), hipMemcpyHostToDevice));
@@ -163,7 +180,7 @@ int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const floa
   const size_t bytes = align256(M * sizeof(spray_rt_ray)) + align256(M * sizeof(spray_rt_hit)) +
                        align256(M * 16) + align256(M) + 2 * align256(M * 4) +
                        align256(MS * sizeof(spray_rt_ray)) + align256(MS * 16) +
-                       2 * align256(MS);
+                       2 * align256(MS) + align256(sizeof(uint32_t));
   r = ensure(c, &c->d_frame, &c->frame_cap, bytes);
   if (r) return r;
   hipStream_t s = stream_of(c);
@@ -173,6 +190,7 @@ int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const floa
     HIPCHK(c, hipMemsetAsync(c->d_fstats, 0, fb, s));
   }
   Carve cv{static_cast<char*>(c->d_frame)};
+  uint32_t* nshadow = cv.take<uint32_t>(1);
   spray_rt_ray* rays = cv.take<spray_rt_ray>(M);
   spray_rt_hit* hits = cv.take<spray_rt_hit>(M);
   float* w = cv.take<float>(4 * M);
@@ -196,8 +214,18 @@ int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const floa
                                   samid + off));
     off += m;
   }
-  HIPCHK(c, launch_path_init(s, w, valid, M));
   const double scale = 1.0 / double(spp);
+  if (fused_frame(c, P)) {
+    const spray_rt_light& lt = P->lights[0];
+    const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
+                               lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
+                               P->ks[2],       P->shininess};
+    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, M, hits, shade10, occ, sv, sw, nshadow));
+    HIPCHK(c, launch_frame_stats_add(s, c->d_fstats, kStatStripes, M, nshadow));
+    HIPCHK(c, launch_film(s, image, pixid, M, spp, ns, sw, sv, occ, scale));
+    return SPRAY_RT_OK;
+  }
+  HIPCHK(c, launch_path_init(s, w, valid, M));
   const int user = c->coherence;
   for (int b = 0; b < P->bounces; ++b) {
     if (b == 0) {

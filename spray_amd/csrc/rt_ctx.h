@@ -77,6 +77,7 @@ struct spray_rt_ctx {
   // frame layer
   spray_rt_bsdf* d_bsdf = nullptr;  // per-domain BSDFs (Scene::getBsdf)
   int nbsdf = 0;
+  bool bsdf_delta = false;  // some domain's BSDF is not diffuse
   void* d_frame = nullptr;  // render_tile path buffers
   size_t frame_cap = 0;
   unsigned long long* d_fstats = nullptr;  // render_tile totals (shade stats)

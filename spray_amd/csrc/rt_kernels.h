@@ -83,6 +83,17 @@ hipError_t launch_scene_intersect_shadow_pt(hipStream_t s, const SceneView& v,
                                             uint8_t* occluded, uint8_t* sh_valid,
                                             uint32_t* d_count);
 
+// The same for a frame's camera rays (one point light, diffuse surfaces,
+// bounces = 1): the spawn rule and light weight of the shading pass
+// (k_shade), the weight to sw[i] (float4) for the film.
+hipError_t launch_scene_frame_pt(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                 size_t M, spray_rt_hit* hits, const float* shade10,
+                                 uint8_t* occluded, uint8_t* sh_valid, float* sw,
+                                 uint32_t* d_count);
+// stats[live], stats[shadows] of the frame counters += M, *d_count
+hipError_t launch_frame_stats_add(hipStream_t s, unsigned long long* stats, int stripes,
+                                  size_t M, const uint32_t* d_count);
+
 // Closest hit + composite key per ray for in-situ compositing:
 // (t bits << 32) | (position in the ray's sorted domain list << 16) | domain,
 // 0x7FFF...F on a miss (non-resident domains are skipped but counted).

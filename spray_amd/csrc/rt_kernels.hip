@@ -203,6 +203,7 @@ struct SceneArgs {
   spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
   uint8_t* sh_valid;     // [M] 1 if source i spawned a shadow ray
   uint32_t* sh_count;    // optional total
+  float4* sw;            // kEpiShadowFrame: light weight of source i's shadow ray
   // indexed input: slot j traces ray idx[j] (e.g. a selected sparse subset)
   const uint32_t* idx;
   // kEpiKeys: composite key per ray
@@ -229,6 +230,10 @@ constexpr int kEpiNone = 0;   // hit records only
 constexpr int kEpiSpawn = 1;  // + fused PT shadow spawn (positional)
 constexpr int kEpiKeys = 2;   // + 64-bit composite key (t, list position, domain)
 constexpr int kEpiShadow = 3; // + PT spawn and the shadow ray's any hit, same launch
+// kEpiShadow for a frame's camera rays: the spawn rule and the light weight of
+// ooc::ShaderPt's shading pass (k_shade, one point light, path weight 1),
+// the weight written to sw[i] for the film
+constexpr int kEpiShadowFrame = 4;
 
 // Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): one work
 // queue of the persistent launches; bands 8x .. 8x+7 (a contiguous eighth of
@@ -623,6 +628,18 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     }
     A.keys[i] = key;
   }
+  if (EPI == kEpiShadowFrame && best_dom >= 0) {
+    spray_rt_hit h;
+    h.t = h0.x;
+    h.color = __float_as_uint(h1.w);
+    h.ns[0] = h2.x;
+    h.ns[1] = h2.y;
+    h.ns[2] = h2.z;
+    const float d3[3] = {d4.x, d4.y, d4.z}, o3[3] = {o4.x, o4.y, o4.z};
+    float L[3];
+    spawn = shade_pt_point(o3, d3, h, A.shade, pos, wi, L);
+    if (spawn) A.sw[i] = make_float4(L[0], L[1], L[2], 0.f);
+  }
   if ((EPI == kEpiSpawn || EPI == kEpiShadow) && best_dom >= 0 && SPRAY_DIAG_MODE != 7) {
     spray_rt_hit h;
     h.t = h0.x;
@@ -767,7 +784,7 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH
                                      : (W == 1 && STK == 16
-                                            ? (EPI == kEpiShadow ? SPRAY_WAVES_SHADOW
+                                            ? (EPI == kEpiShadow || EPI == kEpiShadowFrame ? SPRAY_WAVES_SHADOW
                                                                  : SPRAY_WAVES_CH)
                                             : 1)) void k_scene(
     SceneArgs A) {
@@ -782,7 +799,7 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
   __shared__ int32_t wstack[(kBlock / 64) * kStack];  // top-level stacks, one per wave
-  constexpr bool kShadow = EPI == kEpiShadow;
+  constexpr bool kShadow = EPI == kEpiShadow || EPI == kEpiShadowFrame;
   __shared__ float sq_ray[kShadow ? (kBlock / 64) * kShadowQ * 6 : 1];
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
   ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
@@ -1419,6 +1436,15 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write_masked(
   }
 }
 
+// frame counters of a fused bounce: live slots (= radiance rays) and shadows
+__global__ void k_frame_stats_add(unsigned long long* __restrict__ stats, int stripes, size_t M,
+                                  const uint32_t* __restrict__ d_count) {
+  if (threadIdx.x == 0) {
+    stats[3 * stripes] += (unsigned long long)M;
+    stats[1 * stripes] += (unsigned long long)*d_count;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_iota(uint32_t* __restrict__ out, uint32_t n) {
   const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
   if (j < n) out[j] = j;
@@ -1473,7 +1499,8 @@ static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
-  if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow) && a.sh_count)
+  if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) &&
+      a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
@@ -1639,6 +1666,32 @@ hipError_t launch_scene_intersect_shadow_pt(hipStream_t s, const SceneView& v,
   a.sh_valid = sh_valid;
   a.sh_count = d_count;
   return launch_scene_w<false, kEpiShadow>(s, a, v);
+}
+
+hipError_t launch_scene_frame_pt(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                 size_t M, spray_rt_hit* hits, const float* shade10,
+                                 uint8_t* occluded, uint8_t* sh_valid, float* sw,
+                                 uint32_t* d_count) {
+  if (M == 0) return d_count ? hipMemsetAsync(d_count, 0, sizeof(uint32_t), s) : hipSuccess;
+  SceneArgs a = scene_args(v, rays, M);
+  a.hits = hits;
+  for (int k = 0; k < 3; ++k) {
+    a.shade.lp[k] = shade10[k];
+    a.shade.lr[k] = shade10[3 + k];
+    a.shade.ks[k] = shade10[6 + k];
+  }
+  a.shade.shininess = shade10[9];
+  a.occ = occluded;
+  a.sh_valid = sh_valid;
+  a.sw = reinterpret_cast<float4*>(sw);
+  a.sh_count = d_count;
+  return launch_scene_w<false, kEpiShadowFrame>(s, a, v);
+}
+
+hipError_t launch_frame_stats_add(hipStream_t s, unsigned long long* stats, int stripes,
+                                  size_t M, const uint32_t* d_count) {
+  k_frame_stats_add<<<1, 64, 0, s>>>(stats, stripes, M, d_count);
+  return hipGetLastError();
 }
 
 hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,

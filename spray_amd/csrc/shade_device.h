@@ -158,5 +158,39 @@ __device__ __forceinline__ bool has_positive(const float v[3]) {
   return v[0] > 0.0f || v[1] > 0.0f || v[2] > 0.0f;
 }
 
+// ooc::ShaderPt's point-light term for a camera ray -- path weight (1,1,1),
+// one point light, a diffuse surface: the operations of the shading pass
+// (frame_kernels.hip, shade_slot) in the same order, so the weight and the
+// spawn rule are k_shade's bit for bit.  pos / wi: the shadow ray.
+__device__ __forceinline__ bool shade_pt_point(const float o[3], const float d[3],
+                                               const spray_rt_hit& h, const ShadePt& sh,
+                                               float pos[3], float wi[3], float L[3]) {
+  pos[0] = d[0] * h.t + o[0];
+  pos[1] = d[1] * h.t + o[1];
+  pos[2] = d[2] * h.t + o[2];
+  float kd[3];
+  unpack_rgb(h.color, kd);
+  const float wo[3] = {-d[0], -d[1], -d[2]};
+  const float cos_i = gdot3(wo, h.ns);
+  float nff[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  if (!(cos_i > 0.0f)) {
+    nff[0] = -nff[0];
+    nff[1] = -nff[1];
+    nff[2] = -nff[2];
+  }
+  gnorm3(nff);
+  wi[0] = sh.lp[0] - pos[0];
+  wi[1] = sh.lp[1] - pos[1];
+  wi[2] = sh.lp[2] - pos[2];
+  gnorm3(wi);
+  const float ct = gclamp01(gdot3(nff, wi));
+  float bp[3];
+  blinn_phong(ct, kd, sh.ks, sh.shininess, sh.lr, wi, nff, wo, bp);
+  const float sc = 1.0f / 1.0f;  // 1 / pdf of a point light
+#pragma unroll
+  for (int k = 0; k < 3; ++k) L[k] = (1.0f * bp[k]) * sc;
+  return has_positive(L);
+}
+
 }  // namespace
 }  // namespace spray_rt
