@@ -446,3 +446,45 @@ def test_fused_shadow_trace_matches_two_launches(spray, oracle, scene64, cut):
     oocc, _ = osc.occluded(so, sd)
     assert np.array_equal(np.nonzero(v)[0], osrc) and np.array_equal(o[osrc], oocc)
     assert 0 < oocc.sum() < len(oocc)
+
+
+def test_scene_more_than_64_domains(spray, oracle, tmp_path):
+    """A 5x5x4 grid of 100 domains (the 256-domain variants of the scene
+    kernels: four mask words, larger LDS tables): closest hit, any hit and the
+    fused shadow launch equal the oracle."""
+    import torch
+    lines = ["light point 0 500 1000 1 1 1", ""]
+    for i in range(5):
+        for j in range(4):
+            for k in range(5):
+                lines += ["domain", "file wavelet.ply", "mtl diffuse 1 1 1",
+                          "bound -10.000000 -10.000000 -10.000000 10.000000 9.324713 10.000000",
+                          "face 5480", "vertex 2840",
+                          "translate %f %f %f" % (20.0 * i, 19.324713 * j, 20.0 * k), ""]
+    desc = tmp_path / "wavelets100.spray"
+    desc.write_text("\n".join(lines))
+    sc = spray.Scene(str(desc), SCENES, cache_size=-1, device=0)
+    osc, doms, lights = oracle.load_scene(str(desc), SCENES)
+    assert len(doms) == 100
+    cam = oracle.camera_init([150.0, 120.0, 150.0], [40.0, 28.0, 40.0], [0, 1, 0], 60.0, 512, 512)
+    org, d, _, _ = oracle.eye_rays_ooc(cam, 512, 2, (128, 128, 256, 128))
+    n = len(org)
+    rays = torch.from_numpy(spray.make_rays(org, d).view(np.uint8)).cuda()
+    shade = np.array([0, 500, 1000, 1, 1, 1, 0.4, 0.4, 0.4, 10.0], np.float32)
+    hits = torch.zeros(n * 48, dtype=torch.uint8, device="cuda")
+    occ = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+    sv = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    sc.rt.intersect_scene_shadow_pt(rays, hits, shade, occ, sv, None)
+    sc.rt.sync()
+    oh, _ = osc.intersect(org, d)
+    assert (oh["domain"] >= 64).sum() > 1000
+    compare_hits(hits.cpu().numpy().view(spray.HIT_DTYPE), oh)
+    so, sd, osrc = oracle.spawn_shadows_pt(org, d, oh, lights[0]["pos"], lights[0]["rad"],
+                                           [0.4, 0.4, 0.4], 10.0)
+    oocc, _ = osc.occluded(so, sd)
+    v = sv.cpu().numpy()
+    assert np.array_equal(np.nonzero(v)[0], osrc)
+    assert np.array_equal(occ.cpu().numpy()[osrc], oocc) and 0 < oocc.sum() < len(oocc)
+    g = sc.rt.occluded_scene(spray.make_rays(so, sd))
+    assert np.array_equal(g, oocc)
+    sc.close()
