@@ -204,16 +204,7 @@ int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const floa
   // each tile's eye rays (tile-local sampler seeds) at its offset; from
   // here on every pass is per slot (or per pixel group of spp slots), so
   // the batch gives each tile exactly its own-launch result
-  size_t off = 0;
-  for (int k = 0; k < ntiles; ++k) {
-    const int tx = tiles[4 * k], ty = tiles[4 * k + 1], tw = tiles[4 * k + 2],
-              th = tiles[4 * k + 3];
-    const size_t m = size_t(tw) * th * spp;
-    if (!m) continue;
-    HIPCHK(c, launch_eye_rays_ooc(s, cam, image_w, spp, tx, ty, tw, th, rays + off, pixid + off,
-                                  samid + off));
-    off += m;
-  }
+  HIPCHK(c, launch_eye_rays_ooc_tiles(s, cam, image_w, spp, tiles, ntiles, rays, pixid, samid));
   const double scale = 1.0 / double(spp);
   if (fused_frame(c, P)) {
     const spray_rt_light& lt = P->lights[0];

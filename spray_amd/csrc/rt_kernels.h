@@ -126,6 +126,12 @@ hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
                                spray_rt_ray* rays, int32_t* pixid,
                                int32_t* samid);
 
+// The eye rays of ntiles tiles (x, y, w, h; host array) back to back, as
+// one launch_eye_rays_ooc per tile at its offset would write them.
+hipError_t launch_eye_rays_ooc_tiles(hipStream_t s, const float* cam14, int image_w, int spp,
+                                    const int* tiles, int ntiles, spray_rt_ray* rays,
+                                    int32_t* pixid, int32_t* samid);
+
 // Deterministic (ascending source index) compaction of PT shadow rays.
 // block_counts: device scratch of ceil(M/kBlock) + 1 uint32.
 hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,

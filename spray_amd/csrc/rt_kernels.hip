@@ -928,15 +928,11 @@ struct Cam {
 };
 
 // ooc::Tracer::genMultiEyes (src/ooc/ooc_tracer.inl:124-172) + Camera::
-// generateRay (camera.h:168-209), glm operand order.
-__global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
-    Cam cam, int image_w, int spp, int tx, int ty, int tw, int th,
-    spray_rt_ray* __restrict__ rays, int32_t* __restrict__ pixid,
-    int32_t* __restrict__ samid) {
-  const size_t bufid = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  const size_t n = size_t(tw) * th * spp;
-  if (bufid >= n) return;
-  const int s = int(bufid % spp);
+// generateRay (camera.h:168-209), glm operand order: ray `bufid` of tile
+// (tx, ty, tw), written at out[0] (pixid / samid optional).
+__device__ __forceinline__ void eye_ray_ooc(const Cam& cam, int image_w, int spp, int tx, int ty,
+                                            int tw, size_t bufid, spray_rt_ray* out,
+                                            int32_t* pixid, int32_t* samid) {
   const int p = int(bufid / spp);
   const int x0 = p % tw, y0 = p / tw;
   const int x = tx + x0, y = ty + y0;
@@ -955,12 +951,47 @@ __global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
   dx = dx * inv;
   dy = dy * inv;
   dz = dz * inv;
-  float4* rp = reinterpret_cast<float4*>(rays + bufid);
+  float4* rp = reinterpret_cast<float4*>(out);
   rp[0] = make_float4(c[0], c[1], c[2], kRayEpsilon);
   rp[1] = make_float4(dx, dy, dz, kInf);
-  if (pixid) pixid[bufid] = y * image_w + x;
-  if (samid) samid[bufid] = int32_t(bufid);
-  (void)s;
+  if (pixid) *pixid = y * image_w + x;
+  if (samid) *samid = int32_t(bufid);
+}
+
+__global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
+    Cam cam, int image_w, int spp, int tx, int ty, int tw, int th,
+    spray_rt_ray* __restrict__ rays, int32_t* __restrict__ pixid,
+    int32_t* __restrict__ samid) {
+  const size_t bufid = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const size_t n = size_t(tw) * th * spp;
+  if (bufid >= n) return;
+  eye_ray_ooc(cam, image_w, spp, tx, ty, tw, bufid, rays + bufid, pixid ? pixid + bufid : nullptr,
+              samid ? samid + bufid : nullptr);
+}
+
+// The eye rays of up to kEyeTiles tiles in one launch, tile k's at off[k]
+// (each with its tile-local seeds, as one launch per tile writes them).
+constexpr int kEyeTiles = 32;
+struct EyeTiles {
+  int n;
+  int t[kEyeTiles][4];
+  uint32_t off[kEyeTiles + 1];
+};
+__global__ __launch_bounds__(kBlock) void k_eye_rays_ooc_tiles(
+    Cam cam, int image_w, int spp, EyeTiles T, spray_rt_ray* __restrict__ rays,
+    int32_t* __restrict__ pixid, int32_t* __restrict__ samid) {
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= T.off[T.n]) return;
+  int lo = 0, hi = T.n - 1;  // the last tile with off <= j
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (T.off[mid] <= j)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  eye_ray_ooc(cam, image_w, spp, T.t[lo][0], T.t[lo][1], T.t[lo][2], j - T.off[lo], rays + j,
+              pixid ? pixid + j : nullptr, samid ? samid + j : nullptr);
 }
 
 // insitu::genMultiSampleEyeRays / genSingleSampleEyeRays (src/insitu/
@@ -1776,6 +1807,34 @@ hipError_t launch_eye_rays_ooc(hipStream_t s, const float* cam14, int image_w,
   k_eye_rays_ooc<<<grid_for(n), kBlock, 0, s>>>(c, image_w, spp, tx, ty, tw, th,
                                                 rays, pixid, samid);
   return hipGetLastError();
+}
+
+hipError_t launch_eye_rays_ooc_tiles(hipStream_t s, const float* cam14, int image_w, int spp,
+                                    const int* tiles, int ntiles, spray_rt_ray* rays,
+                                    int32_t* pixid, int32_t* samid) {
+  Cam c;
+  for (int k = 0; k < 14; ++k) c.p[k] = cam14[k];
+  size_t base = 0;
+  for (int k0 = 0; k0 < ntiles; k0 += kEyeTiles) {
+    EyeTiles T{};
+    T.n = ntiles - k0 < kEyeTiles ? ntiles - k0 : kEyeTiles;
+    uint32_t off = 0;
+    for (int k = 0; k < T.n; ++k) {
+      for (int q = 0; q < 4; ++q) T.t[k][q] = tiles[4 * (k0 + k) + q];
+      T.off[k] = off;
+      off += uint32_t(size_t(T.t[k][2]) * T.t[k][3] * spp);
+    }
+    T.off[T.n] = off;
+    if (off) {
+      k_eye_rays_ooc_tiles<<<(off + kBlock - 1) / kBlock, kBlock, 0, s>>>(
+          c, image_w, spp, T, rays + base, pixid ? pixid + base : nullptr,
+          samid ? samid + base : nullptr);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    base += off;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
