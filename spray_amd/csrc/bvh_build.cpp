@@ -321,4 +321,67 @@ bool build_domain_tree(const float* boxes, size_t n, std::vector<BvhNode>* out,
   return true;
 }
 
+bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
+                    std::vector<QNode>* out) {
+  out->assign(nodes.size(), QNode{});
+  *grid = QGrid{};
+  auto empty = [](const float* lo) { return lo[0] == kInf; };  // builder's never-hit box
+  // grid over the union of the finite child boxes, ~700 steps of margin
+  float lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
+  for (const BvhNode& n : nodes)
+    for (int side = 0; side < 2; ++side) {
+      const float* bl = side ? n.r_lo : n.l_lo;
+      const float* bh = side ? n.r_hi : n.l_hi;
+      if (empty(bl)) continue;
+      for (int j = 0; j < 3; ++j) {
+        if (!std::isfinite(bl[j]) || !std::isfinite(bh[j])) return false;
+        lo[j] = std::min(lo[j], bl[j]);
+        hi[j] = std::max(hi[j], bh[j]);
+      }
+    }
+  if (!(lo[0] <= hi[0])) {  // no finite box at all
+    for (int j = 0; j < 3; ++j) lo[j] = hi[j] = 0.f;
+  }
+  for (int j = 0; j < 3; ++j) {
+    double ext = double(hi[j]) - double(lo[j]);
+    if (!(ext > 0)) ext = std::max(std::fabs(double(lo[j])), 1.0) * 1e-3;
+    grid->scale[j] = float(ext / 64000.0);
+    grid->base[j] = float(double(lo[j]) - 700.0 * double(grid->scale[j]));
+    if (!std::isfinite(grid->base[j]) || !(grid->scale[j] > 0.f)) return false;
+  }
+  // decoded bound of grid coordinate q on axis j (the value the kernel's
+  // folded slab evaluates up to rounding, which the extra step covers)
+  auto dec = [&](int j, long q) {
+    return double(std::fma(float(q), grid->scale[j], grid->base[j]));
+  };
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const BvhNode& n = nodes[i];
+    QNode& o = (*out)[i];
+    o.left = n.left;
+    o.right = n.right;
+    for (int side = 0; side < 2; ++side) {
+      const float* bl = side ? n.r_lo : n.l_lo;
+      const float* bh = side ? n.r_hi : n.l_hi;
+      uint16_t* q = o.q + 6 * side;
+      for (int j = 0; j < 3; ++j) {
+        if (empty(bl)) {
+          q[j] = q[3 + j] = 0xFFFF;
+          continue;
+        }
+        const double s = grid->scale[j];
+        long ql = long(std::floor((double(bl[j]) - grid->base[j]) / s)) - 2;
+        while (ql > 0 && !(dec(j, ql) + s <= double(bl[j]))) --ql;
+        long qh = long(std::ceil((double(bh[j]) - grid->base[j]) / s)) + 2;
+        while (qh < 0xFFFF && !(dec(j, qh) - s >= double(bh[j]))) ++qh;
+        if (ql < 0 || qh > 0xFFFF || !(dec(j, ql) + s <= double(bl[j])) ||
+            !(dec(j, qh) - s >= double(bh[j])))
+          return false;
+        q[j] = uint16_t(ql);
+        q[3 + j] = uint16_t(qh);
+      }
+    }
+  }
+  return true;
+}
+
 }  // namespace spray_rt

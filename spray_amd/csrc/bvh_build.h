@@ -27,6 +27,13 @@ struct BvhImage {
 bool build_bvh(const float* verts, size_t nverts, const uint32_t* faces,
                size_t nfaces, BvhImage* out);
 
+// 16-bit quantized copy of a domain tree for the per-lane any-hit walk
+// (QNode, rt_common.h).  Every decoded child box fmaf(q, scale, base)
+// contains the padded fp32 box with one grid step to spare; false if a box
+// cannot be represented (non-finite finite-box bounds).
+bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
+                    std::vector<QNode>* out);
+
 // Top-level tree over domain boxes [n][6] (lo, hi): same builder, one domain
 // per leaf (ref ~(id << 2)), EXACT union boxes (no padding) so that the
 // reference's intersectAabb evaluated on a parent accepts whenever it accepts

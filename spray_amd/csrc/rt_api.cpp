@@ -72,9 +72,14 @@ int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes) {
 
 bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
                       size_t nfaces, const uint32_t* colors, const float* normals,
-                      SlotImage* out) {
+                      SlotImage* out, bool quantized) {
   BvhImage img;
   if (!build_bvh(verts, nverts, faces, nfaces, &img)) return false;
+  QGrid grid{};
+  std::vector<QNode> qn;
+  if (quantized && !img.nodes.empty() && !quantize_nodes(img.nodes, &grid, &qn)) return false;
+  // QGrid at nodes - 32, QNode i at nodes - 64 - 32 i (rt_common.h)
+  const size_t b_q = qn.empty() ? 0 : align256(sizeof(QGrid) + qn.size() * sizeof(QNode));
   const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
   const size_t b_tris = align256(img.tris.size() * sizeof(float));
   const size_t b_prims = align256(img.prims.size() * sizeof(uint32_t));
@@ -82,7 +87,7 @@ bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
   const size_t b_colors = colors ? align256(nverts * sizeof(uint32_t)) : 0;
   const size_t b_normals = normals ? align256(3 * nverts * sizeof(float)) : 0;
   out->bytes.assign(
-      std::max<size_t>(256, b_nodes + b_tris + b_prims + b_faces + b_colors + b_normals), 0);
+      std::max<size_t>(256, b_q + b_nodes + b_tris + b_prims + b_faces + b_colors + b_normals), 0);
   char* host = out->bytes.data();
   size_t off = 0;
   auto put = [&](const void* src, size_t n, size_t padded) {
@@ -91,6 +96,12 @@ bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
     off += padded;
     return o;
   };
+  if (b_q) {
+    std::memcpy(host + b_q - sizeof(QGrid), &grid, sizeof(QGrid));
+    for (size_t i = 0; i < qn.size(); ++i)
+      std::memcpy(host + b_q - sizeof(QGrid) - (i + 1) * sizeof(QNode), &qn[i], sizeof(QNode));
+    off = b_q;
+  }
   out->o_nodes = put(img.nodes.data(), img.nodes.size() * sizeof(BvhNode), b_nodes);
   out->o_tris = put(img.tris.data(), img.tris.size() * sizeof(float), b_tris);
   out->o_prims = put(img.prims.data(), img.prims.size() * sizeof(uint32_t), b_prims);

@@ -43,6 +43,29 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node must be 64 B");
 
+// 32-B quantized copy of a BvhNode for the per-lane any-hit walk (scene
+// slots only): both child boxes as 16-bit grid coordinates of the domain's
+// grid (base + q * scale per axis), rounded outward by at least one extra
+// grid step, so every decoded box contains the padded fp32 box and culling
+// stays conservative; an empty (+inf) box becomes the grid's far corner.
+// Placed in front of the fp32 nodes of the same slot:
+//   nodes - 32          : QGrid (base xyz, scale xyz)
+//   nodes - 64 - 32 * i : QNode i
+// so the scene descriptors (DomTrav) address them without another pointer.
+struct alignas(16) QNode {
+  uint16_t q[12];  // l_lo xyz, l_hi xyz, r_lo xyz, r_hi xyz
+  int32_t left;
+  int32_t right;
+};
+static_assert(sizeof(QNode) == 32, "quantized node must be 32 B");
+struct alignas(16) QGrid {
+  float base[3];
+  float pad0;
+  float scale[3];
+  float pad1;
+};
+static_assert(sizeof(QGrid) == 32, "grid header must be 32 B");
+
 struct alignas(16) SlotDesc {
   const BvhNode* nodes;
   const float* tris;        // 12 floats per triangle

@@ -87,9 +87,12 @@ struct spray_rt_ctx {
 namespace spray_rt {
 namespace detail {
 
-// Device image of one domain, packed on the host: BVH2 nodes | triangle
-// records | leaf->face map | faces | colors | normals, 256-B aligned (the
-// HBM slot layout of rt_common.h).
+// Device image of one domain, packed on the host: [quantized nodes + grid]
+// | BVH2 nodes | triangle records | leaf->face map | faces | colors |
+// normals, 256-B aligned (the HBM slot layout of rt_common.h).  The
+// quantized copy (QNode, in front of the nodes) is built for scene slots
+// only (quantized = true): the OOC drains do not read it, so its images
+// stream without it.
 struct SlotImage {
   std::vector<char> bytes;
   size_t o_nodes = 0, o_tris = 0, o_prims = 0, o_faces = 0;
@@ -100,10 +103,10 @@ struct SlotImage {
   SlotDesc desc_at(const void* base) const;
 };
 // Builds the canonical BVH2 (bvh_build.h) and packs the image; false on
-// invalid face indices.
+// invalid face indices or non-finite vertices of a quantized image.
 bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
                       size_t nfaces, const uint32_t* colors, const float* normals,
-                      SlotImage* out);
+                      SlotImage* out, bool quantized = true);
 
 // Records a message in the context; returns code.
 int fail(spray_rt_ctx* c, int code, const char* fmt, ...);

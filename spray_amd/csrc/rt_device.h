@@ -305,20 +305,57 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
 // visit order, and culling stays conservative, so it equals trace_tree's.
 // Leaves go through the per-lane stack like inner nodes; a visit still
 // pushes at most one entry, so the stack bound (tree depth) is unchanged.
+//
+// Q: walk the slot's 32-B quantized node copy (QNode, rt_common.h) instead of
+// the 64-B fp32 nodes -- half the bytes through the vector data path, which
+// bounds this walk.  The grid decode is folded into the ray's slab constants
+// (t = q * (scale / d) + (base - o) / d); the extra grid step every quantized
+// box carries covers the rounding, so culling stays conservative and the
+// result is the fp32 walk's.
+__device__ __forceinline__ float q_lo(float w) { return float(__float_as_uint(w) & 0xFFFFu); }
+__device__ __forceinline__ float q_hi(float w) { return float(__float_as_uint(w) >> 16); }
+
+template <bool Q>
 __device__ __forceinline__ bool occluded_tree_ww(const void* nodes, const void* tris,
-                                                 const Ray& r, float tnear, float tfar,
+                                                 const Ray& r0, float tnear, float tfar,
                                                  int32_t* stk) {
+  const char* nbytes = static_cast<const char*>(nodes);
+  Ray r = r0;
+  if (Q) {
+    const float4 base = ld4(nbytes - sizeof(QGrid), 0);
+    const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
+    r.oix = -fmaf(base.x, r0.ix, -r0.oix);
+    r.oiy = -fmaf(base.y, r0.iy, -r0.oiy);
+    r.oiz = -fmaf(base.z, r0.iz, -r0.oiz);
+    r.ix = scale.x * r0.ix;
+    r.iy = scale.y * r0.iy;
+    r.iz = scale.z * r0.iz;
+  }
   int sp = 0;
   int32_t cur = 0;       // next entry: inner node >= 0, leaf < 0, kNone = done
   int32_t leaf = kNone;  // the parked leaf
   for (;;) {
     while (cur >= 0 && cur != kNone) {
-      float4 n0, n1, n2, n3;
-      ld_node(nodes, 4 * size_t(cur), n0, n1, n2, n3);
       float tl, tr;
-      const bool hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tfar, tl);
-      const bool hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tfar, tr);
-      int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+      bool hl, hr;
+      int32_t c0, c1;
+      if (Q) {
+        const char* qp = nbytes - 2 * sizeof(QNode) - sizeof(QNode) * size_t(cur);
+        const float4 a = ld4(qp, 0), b = ld4(qp, 1);
+        hl = slab(r, q_lo(a.x), q_hi(a.x), q_lo(a.y), q_hi(a.y), q_lo(a.z), q_hi(a.z), tnear,
+                  tfar, tl);
+        hr = slab(r, q_lo(a.w), q_hi(a.w), q_lo(b.x), q_hi(b.x), q_lo(b.y), q_hi(b.y), tnear,
+                  tfar, tr);
+        c0 = __float_as_int(b.z);
+        c1 = __float_as_int(b.w);
+      } else {
+        float4 n0, n1, n2, n3;
+        ld_node(nodes, 4 * size_t(cur), n0, n1, n2, n3);
+        hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tfar, tl);
+        hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tfar, tr);
+        c0 = __float_as_int(n3.x);
+        c1 = __float_as_int(n3.y);
+      }
       if (hl && hr && tr < tl) {
         const int32_t x = c0;
         c0 = c1;

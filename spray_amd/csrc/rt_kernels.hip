@@ -50,6 +50,11 @@ namespace {
 #ifndef SPRAY_AH_WW
 #define SPRAY_AH_WW 1
 #endif
+// Per-lane while-while any hit over the 32-B quantized node copy (QNode) of
+// scene slots: 1 = quantized nodes, 0 = the fp32 nodes.
+#ifndef SPRAY_AH_QNODES
+#define SPRAY_AH_QNODES 1
+#endif
 #ifndef SPRAY_WAVES_CH
 #define SPRAY_WAVES_CH 6
 #endif
@@ -345,7 +350,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         const bool o = (COUNT || SPRAY_AH_WW == 0)
                            ? trace_tree<true, COUNT>(nodes, tris, prims, r, o4.w, d4.w, best,
                                                      stk, nnode, ntri)
-                           : occluded_tree_ww(nodes, tris, r, o4.w, d4.w, stk);
+                           : occluded_tree_ww<SPRAY_AH_QNODES != 0>(nodes, tris, r, o4.w, d4.w, stk);
         if (o) {
           occluded = true;
           break;
