@@ -715,14 +715,19 @@ void or_bvh_export(const or_bvh* b, float* nodes, uint32_t* order) {
 /* ------------------------------------------------------------------ */
 /* Slab test used for culling only (results never depend on it as long as it
  * is conservative): inverse direction with |d| < 1e-20 clamped to
- * +-1e-20, t = fmaf(bound, inv, -org*inv), hit iff
+ * +-1e-20, t = fmaf(bound, inv, -(org*inv +- ex)), hit iff
  *   max(tmin.x, tmin.y, tmin.z, tnear) <= min(tmax.x, tmax.y, tmax.z, tfar*(1+2^-16))
- * The (1+2^-16) widening and the box padding below keep grazing hits inside
- * (tests/ check BVH == brute force bit-exactly). */
+ * The rounding error of a plane's t is below 2^-24 (3 |org inv| + |bound
+ * inv|): the box padding below covers the bound part, and the per-axis
+ * offset ex = 2^-21 |org inv| (near planes use org*inv + ex, far planes
+ * org*inv - ex, by the sign of inv) the origin part -- rays from far away or
+ * at large coordinates.  The (1+2^-16) widening covers tfar.  (tests/ check
+ * BVH == brute force bit-exactly; spray_amd/csrc/rt_device.h, Ray, is the
+ * same arithmetic.) */
 #define OR_TFAR_SLACK 1.0000153f
 
 typedef struct {
-  float o[3], d[3], inv[3], oi[3];
+  float o[3], d[3], inv[3], ol[3], oh[3];
 } ray_pre;
 
 static inline void ray_prep(ray_pre* r, const float* o, const float* d) {
@@ -731,18 +736,21 @@ static inline void ray_prep(ray_pre* r, const float* o, const float* d) {
     r->d[j] = d[j];
     float dj = fabsf(d[j]) < 1e-20f ? copysignf(1e-20f, d[j]) : d[j];
     r->inv[j] = 1.0f / dj;
-    r->oi[j] = o[j] * r->inv[j];
+    float oi = o[j] * r->inv[j];
+    float s = copysignf(0x1p-21f * fabsf(oi), r->inv[j]);
+    r->ol[j] = oi + s;
+    r->oh[j] = oi - s;
   }
 }
 
 static inline int slab(const ray_pre* r, const float* lo, const float* hi,
                        float tnear, float tfar, float* tenter) {
-  float t0x = fmaf(lo[0], r->inv[0], -r->oi[0]);
-  float t1x = fmaf(hi[0], r->inv[0], -r->oi[0]);
-  float t0y = fmaf(lo[1], r->inv[1], -r->oi[1]);
-  float t1y = fmaf(hi[1], r->inv[1], -r->oi[1]);
-  float t0z = fmaf(lo[2], r->inv[2], -r->oi[2]);
-  float t1z = fmaf(hi[2], r->inv[2], -r->oi[2]);
+  float t0x = fmaf(lo[0], r->inv[0], -r->ol[0]);
+  float t1x = fmaf(hi[0], r->inv[0], -r->oh[0]);
+  float t0y = fmaf(lo[1], r->inv[1], -r->ol[1]);
+  float t1y = fmaf(hi[1], r->inv[1], -r->oh[1]);
+  float t0z = fmaf(lo[2], r->inv[2], -r->ol[2]);
+  float t1z = fmaf(hi[2], r->inv[2], -r->oh[2]);
   float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)),
                      fmaxf(fminf(t0z, t1z), tnear));
   float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)),

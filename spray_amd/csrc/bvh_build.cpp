@@ -345,7 +345,13 @@ bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
   for (int j = 0; j < 3; ++j) {
     double ext = double(hi[j]) - double(lo[j]);
     if (!(ext > 0)) ext = std::max(std::fabs(double(lo[j])), 1.0) * 1e-3;
-    grid->scale[j] = float(ext / 64000.0);
+    // The step never drops below 2^-19 of the axis' coordinate magnitude
+    // (>= 16 ulps): a flat or tiny domain far from the origin (a ground quad
+    // at y = -1, a wall at x = 5) then still has a base 700 steps below lo
+    // that fp32 can represent, and every bound has a representable step of
+    // margin.  Wider extents keep ext / 64000 (65535 steps cover ext + 1400).
+    const double mag = std::max(std::fabs(double(lo[j])), std::fabs(double(hi[j])));
+    grid->scale[j] = float(std::max(ext / 64000.0, std::ldexp(mag, -19)));
     grid->base[j] = float(double(lo[j]) - 700.0 * double(grid->scale[j]));
     if (!std::isfinite(grid->base[j]) || !(grid->scale[j] > 0.f)) return false;
   }

@@ -300,9 +300,9 @@ int spray_rt_ooc_set_domain(spray_rt_ooc_t o, int id, const float* verts, size_t
     return fail(c, SPRAY_RT_ERR_ARG, "null mesh arrays");
   HostDomain& hd = o->dom[id];
   SlotImage img;
-  if (!build_slot_image(verts, nverts, faces, nfaces, colors, normals, &img,
-                        /*quantized=*/false))
-    return fail(c, SPRAY_RT_ERR_ARG, "face index out of range or mesh too large");
+  if (const char* why = build_slot_image(verts, nverts, faces, nfaces, colors, normals, &img,
+                                         /*quantized=*/false))
+    return fail(c, SPRAY_RT_ERR_ARG, "ooc domain %d: %s", id, why);
   if (img.depth > kStack) return fail(c, SPRAY_RT_ERR_LIMIT, "tree deeper than the stack");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipDeviceSynchronize());  // a resident copy may still be read

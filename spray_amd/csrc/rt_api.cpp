@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdarg>
 #include <cstdio>
@@ -70,14 +71,19 @@ int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes) {
   return SPRAY_RT_OK;
 }
 
-bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
-                      size_t nfaces, const uint32_t* colors, const float* normals,
-                      SlotImage* out, bool quantized) {
+const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
+                             size_t nfaces, const uint32_t* colors, const float* normals,
+                             SlotImage* out, bool quantized) {
+  if (nfaces >= (size_t(1) << 29)) return "mesh too large (>= 2^29 faces)";
   BvhImage img;
-  if (!build_bvh(verts, nverts, faces, nfaces, &img)) return false;
+  if (!build_bvh(verts, nverts, faces, nfaces, &img)) return "face index out of range";
+  for (size_t i = 0; i < img.prims.size(); ++i)  // v0, e1, e2 of every referenced face
+    for (int k = 0; k < 9; ++k)
+      if (!std::isfinite(img.tris[12 * i + k])) return "non-finite vertex coordinate";
   QGrid grid{};
   std::vector<QNode> qn;
-  if (quantized && !img.nodes.empty() && !quantize_nodes(img.nodes, &grid, &qn)) return false;
+  if (quantized && !img.nodes.empty() && !quantize_nodes(img.nodes, &grid, &qn))
+    return "vertex coordinates beyond the range of the quantized node grid";
   // QGrid at nodes - 32, QNode i at nodes - 64 - 32 i (rt_common.h)
   const size_t b_q = qn.empty() ? 0 : align256(sizeof(QGrid) + qn.size() * sizeof(QNode));
   const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
@@ -112,7 +118,7 @@ bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
   out->ntris = uint32_t(img.prims.size());
   out->nverts = uint32_t(nverts);
   out->depth = img.depth;
-  return true;
+  return nullptr;
 }
 
 SlotDesc SlotImage::desc_at(const void* base) const {
@@ -348,8 +354,8 @@ int spray_rt_domain_upload(spray_rt_ctx_t c, int slot, const float* verts,
   if ((nverts && !verts) || (nfaces && !faces))
     return fail(c, SPRAY_RT_ERR_ARG, "null mesh arrays");
   SlotImage img;
-  if (!build_slot_image(verts, nverts, faces, nfaces, colors, normals, &img))
-    return fail(c, SPRAY_RT_ERR_ARG, "face index out of range or mesh too large");
+  if (const char* why = build_slot_image(verts, nverts, faces, nfaces, colors, normals, &img))
+    return fail(c, SPRAY_RT_ERR_ARG, "domain upload (slot %d): %s", slot, why);
   if (size_t(slot) >= c->slots.size()) c->slots.resize(slot + 1);
   SlotHost& sh = c->slots[slot];
   HIPCHK(c, hipSetDevice(c->device));
@@ -399,6 +405,23 @@ int spray_rt_bvh_build_host(const float* verts, size_t nverts,
   if (tris_out) std::memcpy(tris_out, img.tris.data(), img.tris.size() * sizeof(float));
   if (prims_out)
     std::memcpy(prims_out, img.prims.data(), img.prims.size() * sizeof(uint32_t));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_qnodes_host(const float* verts, size_t nverts, const uint32_t* faces,
+                         size_t nfaces, size_t* nnodes, float grid_out[6], void* qnodes_out) {
+  if ((nverts && !verts) || (nfaces && !faces)) return SPRAY_RT_ERR_ARG;
+  BvhImage img;
+  if (!build_bvh(verts, nverts, faces, nfaces, &img)) return SPRAY_RT_ERR_ARG;
+  QGrid grid{};
+  std::vector<QNode> qn;
+  if (!img.nodes.empty() && !quantize_nodes(img.nodes, &grid, &qn)) return SPRAY_RT_ERR_LIMIT;
+  if (nnodes) *nnodes = qn.size();
+  if (grid_out) {
+    std::memcpy(grid_out, grid.base, 12);
+    std::memcpy(grid_out + 3, grid.scale, 12);
+  }
+  if (qnodes_out) std::memcpy(qnodes_out, qn.data(), qn.size() * sizeof(QNode));
   return SPRAY_RT_OK;
 }
 

@@ -102,9 +102,11 @@ struct SlotImage {
   // descriptor of the image once copied to device address base
   SlotDesc desc_at(const void* base) const;
 };
-// Builds the canonical BVH2 (bvh_build.h) and packs the image; false on
-// invalid face indices or non-finite vertices of a quantized image.
-bool build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
+// Builds the canonical BVH2 (bvh_build.h) and packs the image.  Returns
+// nullptr on success, else what is wrong with the mesh (face index out of
+// range, too many faces, non-finite vertex, coordinates beyond the range of
+// the quantized node grid).
+const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* faces,
                       size_t nfaces, const uint32_t* colors, const float* normals,
                       SlotImage* out, bool quantized = true);
 

@@ -100,12 +100,28 @@ __device__ __forceinline__ void ld_tri(const void* tris, uint32_t p, float4& a, 
 // ---------------------------------------------------------------------------
 // ray / box / triangle primitives
 // ---------------------------------------------------------------------------
+// Culling arithmetic (slab tests only; results never depend on it while it
+// is conservative).  t of a plane is fmaf(bound, inv, -o * inv); its error is
+// below 2^-24 (3 |o inv| + |bound inv|).  The node boxes' padding (1e-6 of
+// the bound's magnitude, bvh_build.cpp) covers the |bound inv| part; the
+// |o inv| part -- origins far from a box, or far from the world origin --
+// is covered per ray: the near planes use o inv + ex, the far planes
+// o inv - ex (signs by the direction), ex = 2^-21 |o inv| per axis, so the
+// per-node cost is unchanged.  oracle.c evaluates the same operations.
 struct Ray {
   float ox, oy, oz;
   float dx, dy, dz;
   float ix, iy, iz;     // 1/d with |d| clamped at kDirClamp (culling only)
-  float oix, oiy, oiz;  // o * inv
+  float olx, oly, olz;  // lo-plane offsets: o * inv + sign(inv) ex
+  float ohx, ohy, ohz;  // hi-plane offsets: o * inv - sign(inv) ex
 };
+
+__device__ __forceinline__ void ray_axis(float o, float i, float& ol, float& oh) {
+  const float oi = o * i;
+  const float s = copysignf(0x1p-21f * fabsf(oi), i);
+  ol = oi + s;
+  oh = oi - s;
+}
 
 __device__ __forceinline__ float clamp_dir(float d) {
   return fabsf(d) < kDirClamp ? copysignf(kDirClamp, d) : d;
@@ -119,9 +135,9 @@ __device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx,
   r.ix = 1.0f / clamp_dir(dx);
   r.iy = 1.0f / clamp_dir(dy);
   r.iz = 1.0f / clamp_dir(dz);
-  r.oix = ox * r.ix;
-  r.oiy = oy * r.iy;
-  r.oiz = oz * r.iz;
+  ray_axis(ox, r.ix, r.olx, r.ohx);
+  ray_axis(oy, r.iy, r.oly, r.ohy);
+  ray_axis(oz, r.iz, r.olz, r.ohz);
   return r;
 }
 
@@ -129,9 +145,9 @@ __device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx,
 __device__ __forceinline__ bool slab(const Ray& r, float lx, float ly, float lz,
                                      float hx, float hy, float hz, float tnear,
                                      float tfar, float& tenter) {
-  float t0x = fmaf(lx, r.ix, -r.oix), t1x = fmaf(hx, r.ix, -r.oix);
-  float t0y = fmaf(ly, r.iy, -r.oiy), t1y = fmaf(hy, r.iy, -r.oiy);
-  float t0z = fmaf(lz, r.iz, -r.oiz), t1z = fmaf(hz, r.iz, -r.oiz);
+  float t0x = fmaf(lx, r.ix, -r.olx), t1x = fmaf(hx, r.ix, -r.ohx);
+  float t0y = fmaf(ly, r.iy, -r.oly), t1y = fmaf(hy, r.iy, -r.ohy);
+  float t0z = fmaf(lz, r.iz, -r.olz), t1z = fmaf(hz, r.iz, -r.ohz);
   float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)),
                      fmaxf(fminf(t0z, t1z), tnear));
   float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)),
@@ -312,24 +328,62 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
 // (t = q * (scale / d) + (base - o) / d); the extra grid step every quantized
 // box carries covers the rounding, so culling stays conservative and the
 // result is the fp32 walk's.
+//
+// Rounding of the folded form.  The fold (oix' = oix - base * ix, ix' =
+// scale * ix), the offsets and the slab's fmaf(q, ix', -oix') each round
+// once: the error of a plane's t is below 2^-24 (|oix| + 3 |oix'| +
+// 2 * 65536 |ix'|).  Far from the domain (|o - base| hundreds of domain
+// extents, or coordinates large against the extent) that outgrows the one
+// grid step of margin, so every plane moves outward in t by ex = 2^-20 *
+// (|oix| + |oix'| + 65536 |ix'|) per axis, folded into separate lo- and
+// hi-plane offsets like the fp32 walk's (Ray above).  The walk is then
+// conservative against its own decoded boxes, which contain the tight boxes,
+// so it finds every hit the fp32 walk finds (both equal brute force).
 __device__ __forceinline__ float q_lo(float w) { return float(__float_as_uint(w) & 0xFFFFu); }
 __device__ __forceinline__ float q_hi(float w) { return float(__float_as_uint(w) >> 16); }
 
+struct QRay {
+  float ix, iy, iz;     // scale * inv
+  float olx, oly, olz;  // lo-plane offsets
+  float ohx, ohy, ohz;  // hi-plane offsets
+};
+
+__device__ __forceinline__ void q_axis(float base, float scale, float ix, float oix, float& qix,
+                                       float& ol, float& oh) {
+  const float o = -fmaf(base, ix, -oix);
+  qix = scale * ix;
+  const float ex = 0x1p-20f * ((fabsf(oix) + fabsf(o)) + 65536.0f * fabsf(qix));
+  const float sx = copysignf(ex, ix);
+  ol = o + sx;  // lo plane: t - ex when ix > 0 (near), t + ex when ix < 0 (far)
+  oh = o - sx;
+}
+
+__device__ __forceinline__ bool slab_q(const QRay& r, float lx, float ly, float lz, float hx,
+                                       float hy, float hz, float tnear, float tfar,
+                                       float& tenter) {
+  float t0x = fmaf(lx, r.ix, -r.olx), t1x = fmaf(hx, r.ix, -r.ohx);
+  float t0y = fmaf(ly, r.iy, -r.oly), t1y = fmaf(hy, r.iy, -r.ohy);
+  float t0z = fmaf(lz, r.iz, -r.olz), t1z = fmaf(hz, r.iz, -r.ohz);
+  float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)),
+                     fmaxf(fminf(t0z, t1z), tnear));
+  float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)),
+                     fminf(fmaxf(t0z, t1z), tfar * kTfarSlack));
+  tenter = tmin;
+  return tmin <= tmax;
+}
+
 template <bool Q>
 __device__ __forceinline__ bool occluded_tree_ww(const void* nodes, const void* tris,
-                                                 const Ray& r0, float tnear, float tfar,
+                                                 const Ray& r, float tnear, float tfar,
                                                  int32_t* stk) {
   const char* nbytes = static_cast<const char*>(nodes);
-  Ray r = r0;
+  QRay qr;
   if (Q) {
     const float4 base = ld4(nbytes - sizeof(QGrid), 0);
     const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
-    r.oix = -fmaf(base.x, r0.ix, -r0.oix);
-    r.oiy = -fmaf(base.y, r0.iy, -r0.oiy);
-    r.oiz = -fmaf(base.z, r0.iz, -r0.oiz);
-    r.ix = scale.x * r0.ix;
-    r.iy = scale.y * r0.iy;
-    r.iz = scale.z * r0.iz;
+    q_axis(base.x, scale.x, r.ix, r.ox * r.ix, qr.ix, qr.olx, qr.ohx);
+    q_axis(base.y, scale.y, r.iy, r.oy * r.iy, qr.iy, qr.oly, qr.ohy);
+    q_axis(base.z, scale.z, r.iz, r.oz * r.iz, qr.iz, qr.olz, qr.ohz);
   }
   int sp = 0;
   int32_t cur = 0;       // next entry: inner node >= 0, leaf < 0, kNone = done
@@ -342,10 +396,10 @@ __device__ __forceinline__ bool occluded_tree_ww(const void* nodes, const void* 
       if (Q) {
         const char* qp = nbytes - 2 * sizeof(QNode) - sizeof(QNode) * size_t(cur);
         const float4 a = ld4(qp, 0), b = ld4(qp, 1);
-        hl = slab(r, q_lo(a.x), q_hi(a.x), q_lo(a.y), q_hi(a.y), q_lo(a.z), q_hi(a.z), tnear,
-                  tfar, tl);
-        hr = slab(r, q_lo(a.w), q_hi(a.w), q_lo(b.x), q_hi(b.x), q_lo(b.y), q_hi(b.y), tnear,
-                  tfar, tr);
+        hl = slab_q(qr, q_lo(a.x), q_hi(a.x), q_lo(a.y), q_hi(a.y), q_lo(a.z), q_hi(a.z),
+                    tnear, tfar, tl);
+        hr = slab_q(qr, q_lo(a.w), q_hi(a.w), q_lo(b.x), q_hi(b.x), q_lo(b.y), q_hi(b.y),
+                    tnear, tfar, tr);
         c0 = __float_as_int(b.z);
         c1 = __float_as_int(b.w);
       } else {

@@ -217,3 +217,74 @@ def test_face_index_validation(native):
     f = np.array([[0, 1, 3]], np.uint32)
     assert L.spray_rt_bvh_build_host(v.ctypes.data, 3, f.ctypes.data, 1, None, None, None,
                                      None, None) != 0
+
+
+QNODE_DTYPE = np.dtype([("q", "<u2", 12), ("left", "<i4"), ("right", "<i4")])
+
+
+def _qnodes(native, v, f):
+    L = native.lib()
+    nn = C.c_size_t()
+    grid = np.zeros(6, np.float32)
+    rc = L.spray_rt_qnodes_host(v.ctypes.data, len(v), f.ctypes.data, len(f), C.byref(nn),
+                                grid.ctypes.data, None)
+    assert rc == 0, rc
+    q = np.zeros(nn.value, QNODE_DTYPE)
+    assert L.spray_rt_qnodes_host(v.ctypes.data, len(v), f.ctypes.data, len(f), None, None,
+                                  q.ctypes.data) == 0
+    return q, grid
+
+
+def _quad(axis, value, lo=-1.0, hi=1.0):
+    """Two triangles spanning [lo, hi]^2 in the plane coordinate[axis] = value."""
+    o = [a for a in range(3) if a != axis]
+    v = np.zeros((4, 3), np.float32)
+    for k, (s, t) in enumerate([(lo, lo), (hi, lo), (hi, hi), (lo, hi)]):
+        v[k, axis] = value
+        v[k, o[0]], v[k, o[1]] = s, t
+    return v, np.array([[0, 1, 2], [0, 2, 3]], np.uint32)
+
+
+@pytest.mark.parametrize("case", ["ground_y-1", "wall_x5", "wall_z-1e3", "patch_1e4",
+                                  "ground_y0", "wavelet_far", "tilted"])
+def test_quantized_nodes_contain_fp32_boxes(native, oracle, case):
+    """flat / tiny domains away from the origin quantize
+    (the upload used to fail on them), and every decoded quantized child box
+    (base + q * scale, exact in float64) contains its padded fp32 box with at
+    least one grid step to spare -- the per-lane any hit's culling stays
+    conservative."""
+    rng = np.random.default_rng(3)
+    if case == "ground_y-1":
+        v, f = _quad(1, -1.0, -100, 100)
+    elif case == "wall_x5":
+        v, f = _quad(0, 5.0)
+    elif case == "wall_z-1e3":
+        v, f = _quad(2, -1000.0, -0.5, 0.25)
+    elif case == "patch_1e4":
+        v, f = _quad(1, 1e4, 1e4, 1e4 + 0.01)
+    elif case == "ground_y0":
+        v, f = _quad(1, 0.0)
+    elif case == "wavelet_far":
+        v, f, _ = oracle.load_ply(os.path.join(SCENES, "wavelet.ply"))
+        v = (v + np.float32(3.0e4)).astype(np.float32)
+    else:
+        v = rng.uniform(-1, 1, size=(30, 3)).astype(np.float32) + np.float32(7.0)
+        f = np.arange(30, dtype=np.uint32).reshape(-1, 3)
+    nodes, _, _, _ = _bvh(native, v, f)
+    q, grid = _qnodes(native, v, f)
+    assert len(q) == len(nodes)
+    base, scale = grid[:3].astype(np.float64), grid[3:].astype(np.float64)
+    assert np.isfinite(base).all() and (scale > 0).all()
+    assert np.array_equal(q["left"], nodes[:, 12].view(np.int32))
+    assert np.array_equal(q["right"], nodes[:, 13].view(np.int32))
+    for side in (0, 1):
+        lo32 = nodes[:, 6 * side:6 * side + 3].astype(np.float64)
+        hi32 = nodes[:, 6 * side + 3:6 * side + 6].astype(np.float64)
+        ql = q["q"][:, 6 * side:6 * side + 3].astype(np.float64)
+        qh = q["q"][:, 6 * side + 3:6 * side + 6].astype(np.float64)
+        live = np.isfinite(lo32).all(1)  # the builder's never-hit box stays 0xFFFF
+        assert (q["q"][~live, 6 * side:6 * side + 6] == 0xFFFF).all()
+        dlo = base + ql[live] * scale
+        dhi = base + qh[live] * scale
+        assert (dlo + scale <= lo32[live]).all()
+        assert (dhi - scale >= hi32[live]).all()

@@ -78,6 +78,38 @@ def test_bvh_equals_brute_force(oracle, wavelet, seed):
     assert cnt["nodes"] < len(org) * bvh.num_nodes / 10  # culling works
 
 
+@pytest.mark.parametrize("scale,shift", [(0.05, 0.0), (0.05, 1.0e4), (1.0, 3.0e4)])
+def test_bvh_equals_brute_force_far_origins(oracle, wavelet, scale, shift):
+    """Culling stays conservative for origins hundreds to thousands of domain
+    extents away and for domains at large coordinates (the per-ray origin
+    slack of the slab test, oracle.c ray_prep): rays aimed at vertices and
+    edge midpoints -- the triangles touching their leaf boxes' faces."""
+    v, f, _ = wavelet
+    v = (v * np.float32(scale) + np.float32(shift)).astype(np.float32)
+    ext = float((v.max(0) - v.min(0)).max())
+    rng = np.random.default_rng(17)
+    org, d = [], []
+    for k in (370.0, 2000.0, 9000.0):
+        fi = f[rng.integers(0, len(f), 2000)]
+        a, b = v[fi[:, 0]], v[fi[:, 1]]
+        w = rng.integers(0, 3, len(fi))[:, None]
+        tgt = np.where(w == 0, a, np.where(w == 1, (a + b) * np.float32(0.5), b)).astype(float)
+        u = rng.normal(size=(len(fi), 3))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        o = tgt + u * k * ext
+        dd = tgt - o
+        org.append(o.astype(np.float32))
+        d.append((dd / np.linalg.norm(dd, axis=1, keepdims=True)).astype(np.float32))
+    org, d = np.concatenate(org), np.concatenate(d)
+    tri = oracle.prep_tris(v, f)
+    bvh = oracle.Bvh(v, f)
+    t, _, _, p = oracle.brute_intersect(tri, org, d)
+    bt, _, _, bp, _ = bvh.intersect(org, d)
+    assert (p != INV).mean() > 0.3
+    assert np.array_equal(p, bp) and np.array_equal(t.view(np.uint32), bt.view(np.uint32))
+    assert np.array_equal(oracle.brute_occluded(tri, org, d), bvh.occluded(org, d)[0])
+
+
 def test_float64_checker_tolerance(oracle, wavelet):
     """North-star: hit t within 1e-4 relative (and the same primitive) of an
     exact evaluation, except flagged near-edge hits (the crack cases where
