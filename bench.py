@@ -14,18 +14,17 @@ beside it ("unfused").
 Primary rays are generated once before timing by the reference's camera /
 sampler (ooc::Tracer::genMultiEyes over its 8 blocking tiles of 1024x128).
 
-Multi-GPU (torchrun, one process per GPU): every rank traces its own frame
-(frame replicas, weak scaling); barrier + max over ranks around the K timed
-steps.  Rank 0 prints one JSON line.
-
-With more than one rank (or --insitu 1) the line also carries "insitu":
-configs[2], the same frame traced with the domains sharded 64/N per GPU
-(Morton partition) and the rays moving to their domains' owners over RCCL
-all-to-all (spray_amd/insitu.py) -- strong scaling of one frame.  On one
-rank it carries "ooc": configs[3], the same frame with a 4-slot HBM cache of
-domain images streamed from pinned host memory (spray_rt_ooc_*).  "ao" is the
-configs[4] workload per GPU: primary rays + 16 ambient-occlusion rays per hit
-spawned on the device.
+Multi-GPU (torchrun, one process per GPU): the headline becomes configs[2],
+the same frame traced with the domains sharded 64/N per GPU (Morton
+partition) and the rays moving to their domains' owners through the
+engine's in-situ tracer over RCCL (spray_rt_insitu_*) -- strong scaling of
+one frame; barrier + max over ranks around the K timed steps.  Every rank
+also times the whole-frame fused step on its own ("replicas", weak scaling).
+"ao" is configs[4]: AO-16 on the domain-sharded frame (N > 1) or the
+resident frame (N = 1).  At N = 1 the line carries "insitu" (the in-situ
+frame through a one-rank RCCL communicator) and "ooc": configs[3], the
+frame with a 4-slot HBM cache of domain images streamed from pinned host
+memory (spray_rt_ooc_*).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -96,56 +95,89 @@ def cpu_baseline(target_s=10.0):
                       "%.1f s traversal+spawn" % (reps, n, threads, dt)}
 
 
-def run_insitu(args, dist, world, rank, local, cam):
-    """configs[2]: one frame, domains sharded by the reference's Morton
-    partition, eye rays of this rank's horizontal stripe (one blocking tile =
-    the frame), rays exchanged to their domains' owners; timed like the main
-    measurement (barrier + max over ranks)."""
+def run_insitu(args, dist, world, rank, local, cam, kind="pt"):
+    """configs[2] (kind "pt": one bounce, the scene's point light) and
+    configs[4] (kind "ao": 16 AO rays per hit): one in-situ frame per step.
+    The domains are sharded by the reference's Morton partition (64/N per
+    GPU), each rank's eye rays are its horizontal stripe of the frame (one
+    blocking tile = the frame; HBM holds it), and the engine's in-situ tracer
+    (spray_rt_insitu_trace) moves the rays to their domains' owners with
+    count-first RCCL all-to-all-v exchanges, composites the hit keys, shades
+    at the winner, exchanges the shadow rays and films; the ranks' images are
+    composited by one RCCL reduce (HdrImage::composite).  Eye rays are made
+    once before timing (resident, like the main line).  RCCL is used at every
+    N, N = 1 included.  Timed like the main line (barrier + max over ranks)."""
     import torch
     import spray_amd
     from spray_amd import insitu
-    from spray_amd.engine import host_parse_scene
+    from spray_amd.engine import host_parse_scene, host_scene_bsdfs
     dev = torch.device("cuda", local)
-    boxes, _ = host_parse_scene(SCENE, SCENES)
+    boxes, lights = host_parse_scene(SCENE, SCENES)
     bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
     owner = insitu.morton_partition(boxes, bound, world)
     rt = spray_amd.RtContext(local)
     insitu.setup_rank_context(rt, SCENE, SCENES, owner, rank)
-    comm = insitu.Comm(dist if world > 1 else None)
-    tr = insitu.InsituTracer(insitu.GpuLocal(rt, dev), comm)
+    rt.set_bsdfs(host_scene_bsdfs(SCENE))
+    rt.set_stream(torch.cuda.current_stream(dev))
+    eng = insitu.InsituEngine(rt, world, rank, dist=dist if world > 1 else None,
+                              transport="rccl")
     stripe = insitu.horizontal_stripe(world, rank, (0, 0, W, H))
     n = stripe[2] * stripe[3] * SPP
-    rays = torch.empty((n, 8), dtype=torch.float32, device=dev)
-    sam = torch.empty(n, dtype=torch.int32, device=dev)
-    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, None, sam)
+    rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)[:n]
+    pix = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    sam = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, pix, sam)
+    if kind == "ao":
+        sh = spray_amd.frame.make_shader("ao", 1, 16, ks=SHADE[6:9], shininess=SHADE[9],
+                                         lights=lights)
+    else:
+        sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
+                                         lights=lights)
+    image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+
+    def frame():
+        image.zero_()
+        t = eng.trace(sh, rays, pix, sam, SPP, image)
+        eng.composite(image)
+        return t
+
+    tot = None
+    for _ in range(max(args.warmup, 1)):
+        tot = frame()
     torch.cuda.synchronize()
-    res = None
-    for _ in range(args.warmup):
-        res = tr.trace_tile(rays, sam, SHADE)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    s0 = eng.stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = tr.trace_tile(rays, sam, SHADE)
+        tot = frame()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    s1 = eng.stats()
     if world > 1:
         e = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e.item())
-    rays_step = res["n_rays"] + res["n_shadow"]
+    rays_step = tot[0] + tot[1]
+    k = args.steps
+    out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
+           "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
+           "rays_per_step": rays_step, "radiance_rays": tot[0], "shadow_rays": tot[1],
+           "rank0_MB_sent_per_step": round((s1["bytes_sent"] - s0["bytes_sent"]) / k / 1e6, 2),
+           "rank0_host_count_reads_per_step": (s1["host_count_reads"] -
+                                               s0["host_count_reads"]) / k,
+           "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
+           "config": "%s: 64 domains, %d per GPU (Morton partition), 1024x1024x8spp frame in "
+                     "%d horizontal stripes, %s, speculative ray exchange over RCCL "
+                     "all-to-all-v, image composite by RCCL reduce"
+                     % ("configs[4]" if kind == "ao" else "configs[2]",
+                        int(np.bincount(owner, minlength=world)[rank]), world,
+                        "AO-16 rays per hit" if kind == "ao" else "PT point-light shadows")}
+    eng.close()
     rt.close()
-    return {"value": round(rays_step * args.steps / el / 1e6, 3), "unit": "Mrays/s",
-            "ms_per_step": round(el / args.steps * 1e3, 4), "scaling": "strong",
-            "rays_per_step": rays_step, "primary_rays": res["n_rays"],
-            "shadow_rays": res["n_shadow"],
-            "config": "configs[2]: 64 domains, %d per GPU (Morton partition), 1024x1024x8spp "
-                      "frame in %d horizontal stripes, speculative ray exchange over "
-                      "RCCL all-to-all" % (int(np.bincount(owner, minlength=world)[rank]),
-                                            world)}
+    return out
 
 
 def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
@@ -292,8 +324,9 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--insitu", type=int, default=-1,
-                    help="also measure configs[2] (default: when more than one rank)")
+    ap.add_argument("--insitu", type=int, default=1,
+                    help="also measure configs[2] through the engine's RCCL in-situ tracer "
+                         "(always on with more than one rank: it is the headline there)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
@@ -426,12 +459,12 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (reference example mesh wavelet.ply x64, deterministic camera rays)",
         "config": {"workload": "wavelets64 1024x1024x8spp PT primary+shadow, all 64 domains "
                                "resident per GPU (configs[1])",
                    "rays_per_step": rays_step, "primary_rays": n_prim, "shadow_rays": n_shadow,
-                   "parallelism": "frame replicas x%d (weak)" % world},
+                   "parallelism": "one GPU, the whole frame"},
         "roofline": {"bound": "hbm", "achieved": round(fused_gbs, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(fused_gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
@@ -445,15 +478,30 @@ def main():
                                    "any_hit_achieved_GBs": round(ah_gbs, 1)}},
         "canonical_counts": gpu_counts,
     }
+    if args.insitu != 0 or world > 1:
+        out["insitu"] = run_insitu(args, dist, world, rank, local, cam)
+    if world > 1:
+        # configs[2] is the N > 1 headline: the frame split across the GPUs by
+        # domain (strong scaling); the frame replicas stay as a secondary key
+        ins = out["insitu"]
+        out["replicas"] = {"value": out["value"], "ms_per_step": out["ms_per_step"],
+                           "scaling": "weak",
+                           "config": "configs[1] frame replicas x%d (every GPU traces the "
+                                     "whole frame; no data-path collective)" % world}
+        out["value"], out["ms_per_step"] = ins["value"], ins["ms_per_step"]
+        out["config"] = {"workload": ins["config"], "rays_per_step": ins["rays_per_step"],
+                         "primary_rays": ins["radiance_rays"], "shadow_rays": ins["shadow_rays"],
+                         "parallelism": "domain-parallel in-situ x%d (strong)" % world}
     if args.ao:
-        out["ao"] = run_ao(args, dist, world, rt, prim, pixid, n_prim)
+        if world > 1:  # configs[4]: AO-16 on the domain-sharded frame
+            out["ao"] = run_insitu(args, dist, world, rank, local, cam, kind="ao")
+        else:
+            out["ao"] = run_ao(args, dist, world, rt, prim, pixid, n_prim)
     if args.frame:
         _, lights = spray_amd.engine.host_parse_scene(SCENE, SCENES)
         out["frame"] = run_frame(args, dist, world, rt, cam, lights)
     if args.ooc == 1 or (args.ooc < 0 and world == 1):
         out["ooc"] = run_ooc(args, rt, prim, n_prim)
-    if args.insitu == 1 or (args.insitu < 0 and world > 1):
-        out["insitu"] = run_insitu(args, dist, world, rank, local, cam)
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -457,6 +457,87 @@ int spray_rt_tile_list(int schedule, int image_w, int image_h, int spp, int nran
 /* HdrImage::writePpm (image.h:167-204): P3, max 1023, bottom row first. */
 int spray_rt_write_ppm(const char* path, const float* rgba_host, int w, int h);
 
+/* ---- in-situ frames: the domain-sharded tracer and its exchange ---- */
+/* The reference's in-situ mode (src/insitu/): every domain is resident on
+ * one rank, rays travel to the owners of the domains on their lists.  The
+ * whole per-bounce protocol runs in the engine on the context's stream:
+ *   route (Isector::intersect, insitu_isector.h:164-224) -> per-destination
+ *   lists -> count exchange -> ray exchange (Comm::run, insitu_comm.inl:
+ *   28-101; one grouped ncclSend/ncclRecv all-to-all-v instead of tagged
+ *   Isend/Iprobe/Recv) -> keyed closest hit at the owners -> keys back, min
+ *   at the ray's holder, the min forward (VBuf::compositeTbuf,
+ *   insitu_vbuf.h:109-129, per ray copy) -> the one owner whose key wins
+ *   shades (ShaderPt / ShaderAo, insitu_shader_*.h) -> its shadow rays are
+ *   routed and exchanged the same way, their occlusion bytes OR-ed back at
+ *   the spawner (compositeObuf) -> film (retireShadows) -> the spawned
+ *   radiance rays are the spawner's batch of the next bounce.
+ * Host round trips per bounce: three small count reads (no per-ray host
+ * work).  Collectives go through RCCL (the product: one communicator per
+ * in-situ context, spray_rt_insitu_unique_id on rank 0, broadcast by the
+ * caller) or, for tests and CPU-side debugging, through host callbacks
+ * (spray_rt_transport, buffers staged through host memory). */
+typedef struct spray_rt_insitu* spray_rt_insitu_t;
+
+/* Host-memory collectives of the rank group (every rank calls each one in
+ * the same order).  Return 0 on success. */
+typedef struct spray_rt_transport {
+  void* user;
+  /* send_bytes[r] bytes to rank r (consecutive in send), recv_bytes[r] from
+   * rank r (consecutive in recv) */
+  int (*alltoallv)(void* user, const void* send, const size_t* send_bytes, void* recv,
+                   const size_t* recv_bytes);
+  int (*allreduce_u64)(void* user, unsigned long long* data, size_t n); /* SUM, in place */
+  int (*reduce_f32)(void* user, float* data, size_t n, int root);       /* SUM to root */
+} spray_rt_transport;
+
+/* Optional per-sample record of a trace (tests, VBuf dumps): for every copy
+ * this rank shaded, its sample id, bounce, winning hit and the spawned /
+ * occluded bits of its shadow slots (slot k = bit k; <= 64 slots).
+ * Appended at *d_count (device, caller-zeroed) in no particular order; the
+ * arrays hold cap entries (device memory). */
+typedef struct spray_rt_insitu_rec {
+  int32_t* samid;
+  int32_t* bounce;
+  spray_rt_hit* hits;
+  unsigned long long* svalid;
+  unsigned long long* occluded;
+  size_t cap;
+  uint32_t* d_count;
+} spray_rt_insitu_rec;
+
+/* ncclGetUniqueId for the group's communicator (bytes >= 128). */
+int spray_rt_insitu_unique_id(void* id_out, size_t bytes);
+/* One in-situ context per rank on ctx (whose domain boxes, owner map
+ * (spray_rt_set_owners) and resident slots describe this rank's share).
+ * nccl_id != NULL: collectives over RCCL (ncclCommInitRank, blocks until
+ * every rank joined); else host != NULL: the given host collectives. */
+int spray_rt_insitu_create(spray_rt_ctx_t ctx, int world, int rank, const void* nccl_id,
+                           const spray_rt_transport* host, spray_rt_insitu_t* out);
+int spray_rt_insitu_destroy(spray_rt_insitu_t ins);
+/* InsituPartition::partition, GROUP_CLOSE_DOMAINS (src/render/
+ * data_partition.h:59-137): Morton codes of the domain-box centres in the
+ * scene bound, sorted by (code, id), dealt out in contiguous shares of
+ * ndomains / nranks.  Host only. */
+int spray_rt_insitu_partition(const float* boxes, int ndomains, const float scene_bound[6],
+                              int nranks, int* owner_out);
+/* This rank's part of a frame: rays[n] / pixid / samid are its eye rays
+ * (spray_rt_eye_rays_insitu of its stripe; samid = blocking-tile sample id),
+ * traced for shader->bounces bounces across the group; the contributions
+ * of the samples this rank shades are added to image_rgba (device float
+ * [w*h*4], scaled 1/spp).  totals (host, optional): the group's radiance
+ * rays, shadow rays and reference-abort cases (the same on every rank).
+ * rec (optional): see spray_rt_insitu_rec.  Device buffers only. */
+int spray_rt_insitu_trace(spray_rt_insitu_t ins, const spray_rt_shader* shader,
+                          const spray_rt_ray* rays, const int32_t* pixid, const int32_t* samid,
+                          size_t n, int spp, float* image_rgba, const spray_rt_insitu_rec* rec,
+                          unsigned long long totals[3]);
+/* HdrImage::composite (src/display/image.h:167-181): SUM of the ranks'
+ * images at rank 0 (device float[nfloats], in place). */
+int spray_rt_insitu_composite(spray_rt_insitu_t ins, float* image_rgba, size_t nfloats);
+/* out[6] = bytes sent to other ranks, bytes received, exchanges, host
+ * count reads, collectives issued, traces -- since creation. */
+int spray_rt_insitu_stats(spray_rt_insitu_t ins, unsigned long long out[6]);
+
 #ifdef __cplusplus
 }
 #endif

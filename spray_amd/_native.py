@@ -116,6 +116,13 @@ SIGNATURES = {
     "spray_rt_frame_stats": (I, [P, P, I]),
     "spray_rt_tile_list": (I, [I, I, I, I, I, I, C.c_longlong, P, I, P]),
     "spray_rt_write_ppm": (I, [C.c_char_p, P, I, I]),
+    "spray_rt_insitu_unique_id": (I, [P, SZ]),
+    "spray_rt_insitu_create": (I, [P, I, I, P, P, P]),
+    "spray_rt_insitu_destroy": (I, [P]),
+    "spray_rt_insitu_partition": (I, [P, I, P, I, P]),
+    "spray_rt_insitu_trace": (I, [P, P, P, P, P, SZ, I, P, P, P]),
+    "spray_rt_insitu_composite": (I, [P, P, SZ]),
+    "spray_rt_insitu_stats": (I, [P, P]),
     # spray_scene.h
     "spray_scene_create": (I, [C.c_char_p, C.c_char_p, I, I, P, C.c_char_p, SZ]),
     "spray_scene_destroy": (I, [P]),

@@ -21,10 +21,10 @@ LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libspray_rt.so")
 ARCH = os.environ.get("SPRAY_AMD_ARCH", "gfx950")
 
-SOURCES = ["rt_kernels.hip", "ooc_kernels.hip", "frame_kernels.hip", "rt_api.cpp", "ooc.cpp",
-           "frame.cpp", "bvh_build.cpp", "scene_host.cpp"]
+SOURCES = ["rt_kernels.hip", "ooc_kernels.hip", "frame_kernels.hip", "insitu_kernels.hip",
+           "rt_api.cpp", "ooc.cpp", "frame.cpp", "insitu.cpp", "bvh_build.cpp", "scene_host.cpp"]
 HEADERS = ["rt_common.h", "rt_device.h", "shade_device.h", "rt_kernels.h", "rt_ctx.h",
-           "bvh_build.h", "scene_host.h"]
+           "bvh_build.h", "scene_host.h", "insitu_kernels.h"]
 PUBLIC = [os.path.join(ROOT, "include", h) for h in ("spray_rt.h", "spray_scene.h")]
 
 
@@ -54,7 +54,7 @@ def build(force=False, verbose=False, defines=(), out=None):
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, *["-D" + d for d in defines],
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
+           *[os.path.join(CSRC, s) for s in SOURCES], "-ldl", "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

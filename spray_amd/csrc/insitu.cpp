@@ -1,0 +1,673 @@
+// insitu.cpp -- the in-situ (domain-sharded) tracer of one rank, with its
+// exchange, on the engine's stream: the device form of
+// insitu::MultiThreadTracer::traceInOmp (src/insitu/
+// insitu_multithread_tracer.inl:313-442) with the MPI queues of Comm::run
+// (insitu_comm.inl:28-101) and WorkStats::reduce (insitu_work_stats.cc:34-85)
+// replaced by count-first all-to-all-v exchanges over RCCL (or host
+// callbacks, spray_rt_transport).  See include/spray_rt.h for the protocol.
+//
+// Differences from the reference that do not change results: the owners
+// learn the composite minimum of each ray copy before shading (the
+// reference shades every local hit speculatively and discards the losers
+// at VBuf::compositeTbuf), and a fixed number of bounces replaces the
+// WorkStats termination test (no rays exist past shader->bounces).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "insitu_kernels.h"
+#include "rt_ctx.h"
+#include "rt_kernels.h"
+#include "spray_rt.h"
+
+using namespace spray_rt;
+using namespace spray_rt::detail;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// RCCL, resolved at run time: the copy already in the process (PyTorch's)
+// when there is one, else the system's librccl.so.1 -- one RCCL per process.
+// ---------------------------------------------------------------------------
+struct NcclApi {
+  bool ok = false;
+  std::string err;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*Reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int,
+                         ncclComm_t, hipStream_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+NcclApi& nccl() {
+  static NcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* name : {"librccl.so", "librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_NOLOAD))) break;
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      api.err = std::string("cannot load librccl: ") + dlerror();
+      return;
+    }
+    bool all = true;
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      all &= fn != nullptr;
+    };
+    sym(api.GetUniqueId, "ncclGetUniqueId");
+    sym(api.CommInitRank, "ncclCommInitRank");
+    sym(api.CommDestroy, "ncclCommDestroy");
+    sym(api.GroupStart, "ncclGroupStart");
+    sym(api.GroupEnd, "ncclGroupEnd");
+    sym(api.Send, "ncclSend");
+    sym(api.Recv, "ncclRecv");
+    sym(api.AllReduce, "ncclAllReduce");
+    sym(api.Reduce, "ncclReduce");
+    sym(api.GetErrorString, "ncclGetErrorString");
+    if (!all) {
+      api.err = "librccl lacks a required entry point";
+      return;
+    }
+    api.ok = true;
+  });
+  return api;
+}
+
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// transports
+// ---------------------------------------------------------------------------
+struct InsituTransport {
+  virtual ~InsituTransport() = default;
+  // per-peer counts: dev_send (device int64[world]) -> host send / recv
+  virtual int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+                     int64_t* h_recv) = 0;
+  // device buffers; byte counts per peer (host)
+  virtual int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+                        const size_t* rb) = 0;
+  virtual int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) = 0;
+  virtual int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) = 0;
+};
+
+struct spray_rt_insitu {
+  spray_rt_ctx* ctx = nullptr;
+  int world = 1, rank = 0;
+  std::unique_ptr<InsituTransport> tr;
+  // holder batch of the next bounce (double buffered)
+  DBuf hray[2], hw[2], hpix[2], hsam[2];
+  // routing / plan
+  DBuf mask, idx, starts, plan_tmp, dcnt;
+  // wire buffers
+  DBuf sendb, recvb;
+  // owner copies
+  DBuf oray, ow, opix, osam, ohit, okey, obest, owin, ovalid;
+  // holder side of the key composite
+  DBuf best, keyback;
+  // shadow slots of the shaded copies and their exchange
+  DBuf sray, ssw, ssv, socc, ssel, sgray, smask, sidx, sstarts, ashadow, aocc, sret;
+  DBuf nsel, sel_tmp, dnum, dstats, dtot;
+  unsigned long long* h_small = nullptr;  // pinned: counts, totals
+  unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
+};
+
+namespace {
+
+int grow(spray_rt_insitu* I, DBuf& b, size_t bytes) {
+  if (b.cap >= bytes) return SPRAY_RT_OK;
+  spray_rt_ctx* c = I->ctx;
+  if (b.p) {
+    HIPCHK(c, hipStreamSynchronize(stream_of(c)));  // queued work may still read it
+    HIPCHK(c, hipFree(b.p));
+  }
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t want = std::max<size_t>(align256(bytes + bytes / 8), 4096);
+  HIPCHK(c, hipMalloc(&b.p, want));
+  b.cap = want;
+  return SPRAY_RT_OK;
+}
+
+#define GROW(b, bytes)                          \
+  do {                                          \
+    int _r = grow(I, (b), (bytes));             \
+    if (_r) return _r;                          \
+  } while (0)
+#define CALL(expr)                              \
+  do {                                          \
+    int _r = (expr);                            \
+    if (_r) return _r;                          \
+  } while (0)
+
+// ---- RCCL ----
+struct RcclTransport : InsituTransport {
+  ncclComm_t comm = nullptr;
+  bool self_via_nccl = false;  // route self traffic through ncclSend/Recv (tests)
+
+  int chk(spray_rt_insitu* I, ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return SPRAY_RT_OK;
+    return fail(I->ctx, SPRAY_RT_ERR_HIP, "%s: %s", what, nccl().GetErrorString(r));
+  }
+  int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+             int64_t* h_recv) override {
+    const int W = I->world;
+    int64_t* dev_recv = const_cast<int64_t*>(dev_send) + 64;
+    std::vector<size_t> b(W, sizeof(int64_t));
+    CALL(alltoallv(I, dev_send, b.data(), dev_recv, b.data()));
+    hipStream_t s = stream_of(I->ctx);
+    HIPCHK(I->ctx, hipMemcpyAsync(I->h_small, dev_send, 128 * sizeof(int64_t),
+                                  hipMemcpyDeviceToHost, s));
+    HIPCHK(I->ctx, hipStreamSynchronize(s));
+    std::memcpy(h_send, I->h_small, W * sizeof(int64_t));
+    std::memcpy(h_recv, I->h_small + 64, W * sizeof(int64_t));
+    ++I->st[3];
+    return SPRAY_RT_OK;
+  }
+  int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+                const size_t* rb) override {
+    const NcclApi& N = nccl();
+    hipStream_t s = stream_of(I->ctx);
+    const char* sp = static_cast<const char*>(send);
+    char* rp = static_cast<char*>(recv);
+    size_t so = 0, ro = 0;
+    CALL(chk(I, N.GroupStart(), "ncclGroupStart"));
+    for (int r = 0; r < I->world; ++r) {
+      if (r == I->rank && !self_via_nccl) {
+        if (sb[r]) HIPCHK(I->ctx, hipMemcpyAsync(rp + ro, sp + so, sb[r], hipMemcpyDeviceToDevice, s));
+      } else {
+        if (sb[r]) CALL(chk(I, N.Send(sp + so, sb[r], ncclUint8, r, comm, s), "ncclSend"));
+        if (rb[r]) CALL(chk(I, N.Recv(rp + ro, rb[r], ncclUint8, r, comm, s), "ncclRecv"));
+      }
+      so += sb[r];
+      ro += rb[r];
+    }
+    CALL(chk(I, N.GroupEnd(), "ncclGroupEnd"));
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) override {
+    ++I->st[4];
+    return chk(I, nccl().AllReduce(dev, dev, n, ncclUint64, ncclSum, comm, stream_of(I->ctx)),
+               "ncclAllReduce");
+  }
+  int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) override {
+    ++I->st[4];
+    return chk(I, nccl().Reduce(dev, dev, n, ncclFloat32, ncclSum, root, comm, stream_of(I->ctx)),
+               "ncclReduce");
+  }
+  ~RcclTransport() override {
+    if (comm) nccl().CommDestroy(comm);
+  }
+};
+
+// ---- host callbacks (staged) ----
+struct HostTransport : InsituTransport {
+  spray_rt_transport cb{};
+  std::vector<char> hs, hr;
+
+  int sync(spray_rt_insitu* I) {
+    HIPCHK(I->ctx, hipStreamSynchronize(stream_of(I->ctx)));
+    return SPRAY_RT_OK;
+  }
+  int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+             int64_t* h_recv) override {
+    const int W = I->world;
+    HIPCHK(I->ctx, hipMemcpyAsync(h_send, dev_send, W * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                  stream_of(I->ctx)));
+    CALL(sync(I));
+    std::vector<size_t> b(W, sizeof(int64_t));
+    if (cb.alltoallv(cb.user, h_send, b.data(), h_recv, b.data()))
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: count exchange failed");
+    ++I->st[3];
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+                const size_t* rb) override {
+    const int W = I->world;
+    const size_t ts = std::accumulate(sb, sb + W, size_t(0));
+    const size_t trv = std::accumulate(rb, rb + W, size_t(0));
+    hs.resize(std::max<size_t>(ts, 1));
+    hr.resize(std::max<size_t>(trv, 1));
+    hipStream_t s = stream_of(I->ctx);
+    if (ts) HIPCHK(I->ctx, hipMemcpyAsync(hs.data(), send, ts, hipMemcpyDeviceToHost, s));
+    CALL(sync(I));
+    if (cb.alltoallv(cb.user, hs.data(), sb, hr.data(), rb))
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: all-to-all failed");
+    if (trv) HIPCHK(I->ctx, hipMemcpyAsync(recv, hr.data(), trv, hipMemcpyHostToDevice, s));
+    CALL(sync(I));  // hr is reused by the next call
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) override {
+    std::vector<unsigned long long> h(n);
+    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 8, hipMemcpyDeviceToHost, stream_of(I->ctx)));
+    CALL(sync(I));
+    if (cb.allreduce_u64(cb.user, h.data(), n))
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: all-reduce failed");
+    HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * 8, hipMemcpyHostToDevice, stream_of(I->ctx)));
+    CALL(sync(I));
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) override {
+    std::vector<float> h(n);
+    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 4, hipMemcpyDeviceToHost, stream_of(I->ctx)));
+    CALL(sync(I));
+    if (cb.reduce_f32(cb.user, h.data(), n, root))
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: reduce failed");
+    if (I->rank == root)
+      HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * 4, hipMemcpyHostToDevice, stream_of(I->ctx)));
+    CALL(sync(I));
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+};
+
+// One routed exchange: per-destination lists of a batch (route + plan), the
+// count exchange (one host read), the per-peer byte counts.
+struct Routed {
+  size_t total = 0;  // copies this rank sends (entries of idx)
+  size_t recv = 0;   // copies it receives
+  std::vector<int64_t> send_n, recv_n;
+  std::vector<size_t> bytes(size_t per, bool back) const {
+    const std::vector<int64_t>& v = back ? recv_n : send_n;
+    std::vector<size_t> b(v.size());
+    for (size_t r = 0; r < v.size(); ++r) b[r] = size_t(v[r]) * per;
+    return b;
+  }
+};
+
+int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf& mask, DBuf& idx,
+                    DBuf& starts, Routed* R) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  const int W = I->world;
+  GROW(mask, n * 8);
+  GROW(idx, n * size_t(W) * 8);
+  GROW(starts, (W + 1) * 8);
+  GROW(I->plan_tmp, plan_temp_bytes(n, W));
+  GROW(I->dcnt, 128 * 8);
+  if (n) HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, mask.as<uint64_t>()));
+  HIPCHK(c, launch_plan(s, mask.as<uint64_t>(), n, W, idx.as<int64_t>(), starts.as<int64_t>(),
+                        I->plan_tmp.p));
+  HIPCHK(c, launch_counts_from_starts(s, starts.as<int64_t>(), W, I->dcnt.as<int64_t>()));
+  R->send_n.assign(W, 0);
+  R->recv_n.assign(W, 0);
+  CALL(I->tr->counts(I, I->dcnt.as<int64_t>(), R->send_n.data(), R->recv_n.data()));
+  R->total = R->recv = 0;
+  for (int r = 0; r < W; ++r) {
+    if (R->send_n[r] < 0 || R->recv_n[r] < 0)
+      return fail(c, SPRAY_RT_ERR_STATE, "in-situ count exchange returned a negative count");
+    R->total += size_t(R->send_n[r]);
+    R->recv += size_t(R->recv_n[r]);
+  }
+  ++I->st[2];
+  return SPRAY_RT_OK;
+}
+
+int exchange(spray_rt_insitu* I, const Routed& R, size_t per, bool back, const void* send,
+             void* recv) {
+  const std::vector<size_t> sb = R.bytes(per, back), rb = R.bytes(per, !back);
+  for (int r = 0; r < I->world; ++r)
+    if (r != I->rank) {
+      I->st[0] += sb[r];
+      I->st[1] += rb[r];
+    }
+  return I->tr->alltoallv(I, send, sb.data(), recv, rb.data());
+}
+
+int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
+          const int32_t* pixid, const int32_t* samid, size_t n, int spp, float* image,
+          const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  const int ns = spray_rt_shadow_slots(P);
+  const double scale = 1.0 / double(spp);
+  GROW(I->dstats, 4 * 8);
+  GROW(I->dtot, 4 * 8);
+  GROW(I->dnum, 2 * 4);
+  HIPCHK(c, hipMemsetAsync(I->dstats.p, 0, 4 * 8, s));
+  // bounce 0: the caller's eye rays, path weights (1, 1, 1)
+  const spray_rt_ray* hr = rays;
+  const int32_t* hp = pixid;
+  const int32_t* hs = samid;
+  GROW(I->hw[0], n * 16);
+  HIPCHK(c, launch_weights_one(s, I->hw[0].as<float>(), n));
+  const float* hw = I->hw[0].as<float>();
+  size_t hn = n;
+  int cur = 0;
+  unsigned long long nrad = 0, nsh = 0;
+  for (int b = 0; b < P->bounces; ++b) {
+    nrad += hn;
+    // ---- radiance rays to the owners of their domains
+    Routed R;
+    CALL(route_and_count(I, hr, hn, I->mask, I->idx, I->starts, &R));
+    const size_t m = R.recv;
+    GROW(I->sendb, std::max(R.total * kRadRecBytes, R.total * 8));
+    GROW(I->recvb, m * kRadRecBytes);
+    HIPCHK(c, launch_pack_rad(s, hr, hw, hp, hs, I->idx.as<int64_t>(), R.total, I->sendb.p));
+    CALL(exchange(I, R, kRadRecBytes, false, I->sendb.p, I->recvb.p));
+    GROW(I->oray, m * 32);
+    GROW(I->ow, m * 16);
+    GROW(I->opix, m * 4);
+    GROW(I->osam, m * 4);
+    GROW(I->ohit, m * 48);
+    GROW(I->okey, m * 8);
+    GROW(I->obest, m * 8);
+    GROW(I->owin, m);
+    GROW(I->ovalid, m);
+    HIPCHK(c, launch_unpack_rad(s, I->recvb.p, m, I->oray.as<spray_rt_ray>(), I->ow.as<float>(),
+                                I->opix.as<int32_t>(), I->osam.as<int32_t>()));
+    if (m)
+      HIPCHK(c, launch_scene_intersect_keyed(s, view(c), I->oray.as<spray_rt_ray>(), m,
+                                             I->ohit.as<spray_rt_hit>(), I->okey.as<uint64_t>()));
+    // ---- keys back to the holder, minimum per ray, the minimum forward
+    GROW(I->keyback, R.total * 8);
+    GROW(I->best, hn * 8);
+    CALL(exchange(I, R, 8, true, I->okey.p, I->keyback.p));
+    HIPCHK(c, launch_fill_u64(s, I->best.as<uint64_t>(), hn, kInsituMissKey));
+    HIPCHK(c, launch_key_min(s, I->idx.as<int64_t>(), I->keyback.as<uint64_t>(), R.total,
+                             I->best.as<uint64_t>()));
+    if (R.total)
+      HIPCHK(c, launch_gather_rows(s, I->best.p, 8, I->idx.as<int64_t>(), R.total, I->sendb.p));
+    CALL(exchange(I, R, 8, false, I->sendb.p, I->obest.p));
+    HIPCHK(c, launch_winners(s, I->okey.as<uint64_t>(), I->obest.as<uint64_t>(), m,
+                             I->owin.as<uint8_t>()));
+    // ---- the winning owner shades (ShaderPt / ShaderAo at ray depth b)
+    const size_t MS = m * size_t(ns);
+    if (m > 0xFFFFFFFFull || MS > 0xFFFFFFFFull)
+      return fail(c, SPRAY_RT_ERR_LIMIT, "in-situ batch too large (copies x shadow slots > 2^32)");
+    GROW(I->sray, MS * 32);
+    GROW(I->ssw, MS * 16);
+    GROW(I->ssv, MS);
+    GROW(I->socc, MS);
+    if (m) HIPCHK(c, hipMemcpyAsync(I->ovalid.p, I->owin.p, m, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, launch_shade(s, *P, c->d_bsdf, c->nbsdf, b, ns, I->oray.as<spray_rt_ray>(),
+                           I->ohit.as<spray_rt_hit>(), I->ow.as<float>(), I->ovalid.as<uint8_t>(),
+                           I->opix.as<int32_t>(), I->osam.as<int32_t>(), m,
+                           I->sray.as<spray_rt_ray>(), I->ssw.as<float>(), I->ssv.as<uint8_t>(),
+                           I->dstats.as<unsigned long long>(), 1));
+    // ---- shadow slots and next radiance rays, compacted (one host read)
+    size_t t1 = 0, t2 = 0;
+    HIPCHK(c, launch_select_flagged(s, nullptr, MS, nullptr, nullptr, nullptr, &t1));
+    HIPCHK(c, launch_select_flagged(s, nullptr, m, nullptr, nullptr, nullptr, &t2));
+    GROW(I->sel_tmp, std::max(t1, t2));
+    GROW(I->ssel, MS * 4);
+    GROW(I->nsel, m * 4);
+    uint32_t* dnum = I->dnum.as<uint32_t>();
+    HIPCHK(c, launch_select_flagged(s, I->ssv.as<uint8_t>(), MS, I->ssel.as<uint32_t>(), dnum,
+                                    I->sel_tmp.p, &t1));
+    const bool more = b + 1 < P->bounces;
+    if (more)
+      HIPCHK(c, launch_select_flagged(s, I->ovalid.as<uint8_t>(), m, I->nsel.as<uint32_t>(),
+                                      dnum + 1, I->sel_tmp.p, &t2));
+    else
+      HIPCHK(c, hipMemsetAsync(dnum + 1, 0, 4, s));
+    HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    ++I->st[3];
+    uint32_t cnt2[2];
+    std::memcpy(cnt2, I->h_small, 8);
+    const size_t cs = cnt2[0], cn = cnt2[1];
+    nsh += cs;
+    // ---- shadow rays to the owners of their domains, occlusion OR-ed back
+    if (MS) HIPCHK(c, hipMemsetAsync(I->socc.p, 0, MS, s));
+    GROW(I->sgray, cs * 32);
+    HIPCHK(c, launch_gather_shadow(s, I->sray.as<spray_rt_ray>(), I->ssel.as<uint32_t>(), cs,
+                                   I->sgray.as<spray_rt_ray>()));
+    Routed S;
+    CALL(route_and_count(I, I->sgray.as<spray_rt_ray>(), cs, I->smask, I->sidx, I->sstarts, &S));
+    GROW(I->sendb, S.total * kShadowRecBytes);
+    GROW(I->recvb, S.recv * kShadowRecBytes);
+    HIPCHK(c, launch_pack_shadow(s, I->sray.as<spray_rt_ray>(), I->ssel.as<uint32_t>(),
+                                 I->sidx.as<int64_t>(), S.total, I->sendb.p));
+    CALL(exchange(I, S, kShadowRecBytes, false, I->sendb.p, I->recvb.p));
+    GROW(I->ashadow, S.recv * 32);
+    GROW(I->aocc, S.recv);
+    GROW(I->sret, S.total);
+    HIPCHK(c, launch_unpack_shadow(s, I->recvb.p, S.recv, I->ashadow.as<spray_rt_ray>()));
+    if (S.recv)
+      HIPCHK(c, launch_scene_occluded(s, view(c), I->ashadow.as<spray_rt_ray>(), S.recv, nullptr,
+                                      I->aocc.as<uint8_t>(), nullptr));
+    CALL(exchange(I, S, 1, true, I->aocc.p, I->sret.p));
+    HIPCHK(c, launch_occ_return(s, I->sidx.as<int64_t>(), I->sret.as<uint8_t>(), S.total,
+                                I->ssel.as<uint32_t>(), I->socc.as<uint8_t>()));
+    // ---- film of the copies this rank shaded
+    HIPCHK(c, launch_film_atomic(s, image, I->opix.as<int32_t>(), m, ns, I->ssw.as<float>(),
+                                 I->ssv.as<uint8_t>(), I->socc.as<uint8_t>(), scale));
+    if (rec)
+      HIPCHK(c, launch_record(s, I->owin.as<uint8_t>(), m, b, ns, I->osam.as<int32_t>(),
+                              I->ohit.as<spray_rt_hit>(), I->ssv.as<uint8_t>(),
+                              I->socc.as<uint8_t>(), *rec));
+    // ---- the spawned radiance rays: this rank's batch of the next bounce
+    if (more) {
+      const int nx = cur ^ 1;
+      GROW(I->hray[nx], cn * 32);
+      GROW(I->hw[nx], cn * 16);
+      GROW(I->hpix[nx], cn * 4);
+      GROW(I->hsam[nx], cn * 4);
+      HIPCHK(c, launch_gather_next(s, I->oray.as<spray_rt_ray>(), I->ow.as<float>(),
+                                   I->opix.as<int32_t>(), I->osam.as<int32_t>(),
+                                   I->nsel.as<uint32_t>(), cn, I->hray[nx].as<spray_rt_ray>(),
+                                   I->hw[nx].as<float>(), I->hpix[nx].as<int32_t>(),
+                                   I->hsam[nx].as<int32_t>()));
+      cur = nx;
+      hr = I->hray[cur].as<spray_rt_ray>();
+      hw = I->hw[cur].as<float>();
+      hp = I->hpix[cur].as<int32_t>();
+      hs = I->hsam[cur].as<int32_t>();
+      hn = cn;
+    }
+  }
+  // ---- the group's totals (WorkStats-like: one small all-reduce)
+  unsigned long long* ht = I->h_small + 8;
+  HIPCHK(c, hipMemcpyAsync(ht, I->dstats.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  const unsigned long long aborts = ht[0];
+  ht[0] = nrad;
+  ht[1] = nsh;
+  ht[2] = aborts;
+  HIPCHK(c, hipMemcpyAsync(I->dtot.p, ht, 3 * 8, hipMemcpyHostToDevice, s));
+  CALL(I->tr->allreduce_u64(I, I->dtot.as<unsigned long long>(), 3));
+  HIPCHK(c, hipMemcpyAsync(ht, I->dtot.p, 3 * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (totals)
+    for (int k = 0; k < 3; ++k) totals[k] = ht[k];
+  ++I->st[5];
+  if (ht[2])
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED, "%llu shading cases the reference aborts on", ht[2]);
+  return SPRAY_RT_OK;
+}
+
+void free_all(spray_rt_insitu* I) {
+  DBuf* all[] = {&I->hray[0], &I->hray[1], &I->hw[0], &I->hw[1], &I->hpix[0], &I->hpix[1],
+                 &I->hsam[0], &I->hsam[1], &I->mask, &I->idx, &I->starts, &I->plan_tmp,
+                 &I->dcnt, &I->sendb, &I->recvb, &I->oray, &I->ow, &I->opix, &I->osam,
+                 &I->ohit, &I->okey, &I->obest, &I->owin, &I->ovalid, &I->best, &I->keyback,
+                 &I->sray, &I->ssw, &I->ssv, &I->socc, &I->ssel, &I->sgray, &I->smask,
+                 &I->sidx, &I->sstarts, &I->ashadow, &I->aocc, &I->sret, &I->nsel,
+                 &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot};
+  for (DBuf* b : all)
+    if (b->p) (void)hipFree(b->p);
+  if (I->h_small) (void)hipHostFree(I->h_small);
+}
+
+// Morton::expandBits / compute (src/render/morton.h:32-50)
+uint32_t expand_bits(uint32_t v) {
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+uint32_t morton(float x, float y, float z) {
+  x = std::min(std::max(x * 1024.0f, 0.0f), 1023.0f);
+  y = std::min(std::max(y * 1024.0f, 0.0f), 1023.0f);
+  z = std::min(std::max(z * 1024.0f, 0.0f), 1023.0f);
+  return expand_bits(uint32_t(x)) * 4 + expand_bits(uint32_t(y)) * 2 + expand_bits(uint32_t(z));
+}
+
+}  // namespace
+
+extern "C" {
+
+int spray_rt_insitu_unique_id(void* id_out, size_t bytes) {
+  if (!id_out || bytes < sizeof(ncclUniqueId)) return SPRAY_RT_ERR_ARG;
+  const NcclApi& N = nccl();
+  if (!N.ok) return SPRAY_RT_ERR_UNSUPPORTED;
+  ncclUniqueId id;
+  if (N.GetUniqueId(&id) != ncclSuccess) return SPRAY_RT_ERR_HIP;
+  std::memcpy(id_out, &id, sizeof(id));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_create(spray_rt_ctx_t c, int world, int rank, const void* nccl_id,
+                           const spray_rt_transport* host, spray_rt_insitu_t* out) {
+  if (!c || !out) return SPRAY_RT_ERR_ARG;
+  *out = nullptr;
+  if (world < 1 || world > 64 || rank < 0 || rank >= world)
+    return fail(c, SPRAY_RT_ERR_ARG, "in-situ group: world %d rank %d (world in [1, 64])", world,
+                rank);
+  if (!nccl_id && (!host || !host->alltoallv || !host->allreduce_u64 || !host->reduce_f32))
+    return fail(c, SPRAY_RT_ERR_ARG, "in-situ group needs an RCCL id or host collectives");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::unique_ptr<spray_rt_insitu> I(new (std::nothrow) spray_rt_insitu);
+  if (!I) return SPRAY_RT_ERR_NOMEM;
+  I->ctx = c;
+  I->world = world;
+  I->rank = rank;
+  HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&I->h_small), 256 * 8, hipHostMallocDefault));
+  if (nccl_id) {
+    const NcclApi& N = nccl();
+    if (!N.ok) {
+      free_all(I.get());
+      return fail(c, SPRAY_RT_ERR_UNSUPPORTED, "RCCL unavailable: %s", N.err.c_str());
+    }
+    auto t = std::make_unique<RcclTransport>();
+    const char* self = std::getenv("SPRAY_INSITU_NCCL_SELF");
+    t->self_via_nccl = self && self[0] == '1';
+    ncclUniqueId id;
+    std::memcpy(&id, nccl_id, sizeof(id));
+    const ncclResult_t r = N.CommInitRank(&t->comm, world, id, rank);
+    if (r != ncclSuccess) {
+      free_all(I.get());
+      return fail(c, SPRAY_RT_ERR_HIP, "ncclCommInitRank: %s", N.GetErrorString(r));
+    }
+    I->tr = std::move(t);
+  } else {
+    auto t = std::make_unique<HostTransport>();
+    t->cb = *host;
+    I->tr = std::move(t);
+  }
+  *out = I.release();
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_destroy(spray_rt_insitu_t I) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  (void)hipSetDevice(I->ctx->device);
+  (void)hipStreamSynchronize(stream_of(I->ctx));
+  free_all(I);
+  delete I;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_partition(const float* boxes, int n, const float sb[6], int nranks,
+                              int* owner) {
+  if (!boxes || !sb || !owner || n < 0 || nranks <= 0) return SPRAY_RT_ERR_ARG;
+  // scale + offset of the unit-cube transform, evaluated as glm's
+  // trans * scale matrix applied to (c, 1): fl(fl(s * c) + off)
+  float scale[3], off[3];
+  for (int j = 0; j < 3; ++j) {
+    const float diag = sb[3 + j] - sb[j];
+    scale[j] = 1.0f / diag;
+    off[j] = 0.0f - sb[j] * scale[j];
+  }
+  std::vector<std::pair<uint32_t, int>> codes(n);
+  for (int i = 0; i < n; ++i) {
+    float cc[3];
+    for (int j = 0; j < 3; ++j) {
+      const float center = (boxes[6 * i + j] + boxes[6 * i + 3 + j]) * 0.5f;  // Aabb::getCenter
+      cc[j] = center * scale[j] + off[j];
+    }
+    codes[i] = {morton(cc[0], cc[1], cc[2]), i};
+  }
+  // std::sort by code leaves equal codes unordered; the id makes it total
+  std::sort(codes.begin(), codes.end());
+  const int shares = n / nranks;
+  int rank = 0, s = 0;
+  for (const auto& cd : codes) {
+    owner[cd.second] = rank;
+    if (++s == shares) {
+      s = 0;
+      if (++rank == nranks) rank = 0;
+    }
+  }
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_trace(spray_rt_insitu_t I, const spray_rt_shader* P, const spray_rt_ray* rays,
+                          const int32_t* pixid, const int32_t* samid, size_t n, int spp,
+                          float* image, const spray_rt_insitu_rec* rec,
+                          unsigned long long totals[3]) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = I->ctx;
+  if (spray_rt_shadow_slots(P) < 0 || spp <= 0)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad shader configuration");
+  if (rec && (spray_rt_shadow_slots(P) > 64 || !rec->d_count || !is_device_ptr(rec->d_count)))
+    return fail(c, SPRAY_RT_ERR_ARG, "records need <= 64 shadow slots and a device counter");
+  if (n > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "n > 2^32");
+  if (!image || !is_device_ptr(image) ||
+      (n && (!is_device_ptr(rays) || !is_device_ptr(pixid) || !is_device_ptr(samid))))
+    return fail(c, SPRAY_RT_ERR_ARG, "in-situ trace needs device buffers");
+  int r = scene_common(c, image, 1, image);
+  if (r) return r;
+  if (!c->d_owner) return fail(c, SPRAY_RT_ERR_STATE, "no owner map set");
+  return trace(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+}
+
+int spray_rt_insitu_composite(spray_rt_insitu_t I, float* image, size_t nfloats) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  if (!image || !is_device_ptr(image))
+    return fail(I->ctx, SPRAY_RT_ERR_ARG, "composite needs a device image");
+  HIPCHK(I->ctx, hipSetDevice(I->ctx->device));
+  if (I->world == 1) return SPRAY_RT_OK;
+  return I->tr->reduce_f32(I, image, nfloats, 0);
+}
+
+int spray_rt_insitu_stats(spray_rt_insitu_t I, unsigned long long out[6]) {
+  if (!I || !out) return SPRAY_RT_ERR_ARG;
+  for (int k = 0; k < 6; ++k) out[k] = I->st[k];
+  return SPRAY_RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// insitu_kernels.h -- launchers of the in-situ exchange kernels
+// (insitu_kernels.hip); the protocol that sequences them is insitu.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rt_kernels.h"
+#include "spray_rt.h"
+
+namespace spray_rt {
+
+constexpr uint64_t kInsituMissKey = 0x7FFFFFFFFFFFFFFFull;  // keyed closest hit: a miss
+constexpr size_t kRadRecBytes = 48;                         // org, dir, w, pixid, samid
+constexpr size_t kShadowRecBytes = 24;                      // org, dir
+
+// out[j] = radiance record of ray idx[j]
+hipError_t launch_pack_rad(hipStream_t s, const spray_rt_ray* rays, const float* w,
+                           const int32_t* pix, const int32_t* sam, const int64_t* idx, size_t n,
+                           void* out);
+hipError_t launch_unpack_rad(hipStream_t s, const void* in, size_t m, spray_rt_ray* rays,
+                             float* w, int32_t* pix, int32_t* sam);
+// out[j] = shadow record of slot sel[idx[j]]
+hipError_t launch_pack_shadow(hipStream_t s, const spray_rt_ray* slots, const uint32_t* sel,
+                              const int64_t* idx, size_t n, void* out);
+hipError_t launch_unpack_shadow(hipStream_t s, const void* in, size_t m, spray_rt_ray* rays);
+// out[j] = slots[sel[j]]
+hipError_t launch_gather_shadow(hipStream_t s, const spray_rt_ray* slots, const uint32_t* sel,
+                                size_t n, spray_rt_ray* out);
+// best[idx[j]] = min(best[idx[j]], keys[j]) over the returned keys
+hipError_t launch_key_min(hipStream_t s, const int64_t* idx, const uint64_t* keys, size_t n,
+                          uint64_t* best);
+hipError_t launch_fill_u64(hipStream_t s, uint64_t* p, size_t n, uint64_t v);
+// win[j] = key[j] is a hit and equals the composite minimum best[j]
+hipError_t launch_winners(hipStream_t s, const uint64_t* key, const uint64_t* best, size_t m,
+                          uint8_t* win);
+// occ[sel[idx[j]]] = 1 where ret[j]
+hipError_t launch_occ_return(hipStream_t s, const int64_t* idx, const uint8_t* ret, size_t n,
+                             const uint32_t* sel, uint8_t* occ);
+hipError_t launch_film_atomic(hipStream_t s, float* image, const int32_t* pix, size_t m, int ns,
+                              const float* sw, const uint8_t* sv, const uint8_t* occ,
+                              double scale);
+hipError_t launch_record(hipStream_t s, const uint8_t* win, size_t m, int bounce, int ns,
+                         const int32_t* sam, const spray_rt_hit* hits, const uint8_t* sv,
+                         const uint8_t* occ, const spray_rt_insitu_rec& rec);
+hipError_t launch_gather_next(hipStream_t s, const spray_rt_ray* rays, const float* w,
+                              const int32_t* pix, const int32_t* sam, const uint32_t* sel,
+                              size_t n, spray_rt_ray* orays, float* ow, int32_t* opix,
+                              int32_t* osam);
+hipError_t launch_weights_one(hipStream_t s, float* w, size_t n);
+// counts[r] = starts[r + 1] - starts[r], r < world (<= 64)
+hipError_t launch_counts_from_starts(hipStream_t s, const int64_t* starts, int world,
+                                     int64_t* counts);
+
+}  // namespace spray_rt

@@ -1,0 +1,288 @@
+// insitu_kernels.hip -- gfx950 kernels of the in-situ exchange (insitu.cpp):
+// packing rays into the wire records that travel between ranks, the
+// composite-key reduction (VBuf::compositeTbuf, src/insitu/insitu_vbuf.h:
+// 109-129, done per ray copy), the winner flags, the occlusion OR back at the
+// spawner (compositeObuf), the film of the shaded copies
+// (TContext::retireShadows + HdrImage::add, insitu_tcontext.inl:232-241) and
+// the next bounce's compaction.  All are HBM-bound streaming passes: one
+// thread per record, 16-B (or 8-B) accesses.
+#include <hip/hip_runtime.h>
+
+#include "insitu_kernels.h"
+#include "rt_device.h"
+
+namespace spray_rt {
+namespace {
+
+// 48-B radiance record: org, dir, path weight, pixel, sample.  tnear and
+// tfar are not sent: every radiance ray of the reference carries
+// SPRAY_RAY_EPSILON and +inf (RTCRayUtil::makeRadianceRay, rays.h:345-363).
+__global__ __launch_bounds__(kBlock) void k_pack_rad(const float4* __restrict__ rays,
+                                                     const float4* __restrict__ w,
+                                                     const int32_t* __restrict__ pix,
+                                                     const int32_t* __restrict__ sam,
+                                                     const int64_t* __restrict__ idx, size_t n,
+                                                     float4* __restrict__ out) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t i = size_t(idx[j]);
+  const float4 a = rays[2 * i], b = rays[2 * i + 1], c = w[i];
+  out[3 * j] = make_float4(a.x, a.y, a.z, b.x);
+  out[3 * j + 1] = make_float4(b.y, b.z, c.x, c.y);
+  out[3 * j + 2] = make_float4(c.z, __int_as_float(pix[i]), __int_as_float(sam[i]), 0.f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_rad(const float4* __restrict__ in, size_t m,
+                                                       float4* __restrict__ rays,
+                                                       float4* __restrict__ w,
+                                                       int32_t* __restrict__ pix,
+                                                       int32_t* __restrict__ sam) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= m) return;
+  const float4 a = in[3 * j], b = in[3 * j + 1], c = in[3 * j + 2];
+  rays[2 * j] = make_float4(a.x, a.y, a.z, kRayEpsilon);
+  rays[2 * j + 1] = make_float4(a.w, b.x, b.y, kInf);
+  w[j] = make_float4(b.z, b.w, c.x, 0.f);
+  pix[j] = __float_as_int(c.y);
+  sam[j] = __float_as_int(c.z);
+}
+
+// 24-B shadow record (org, dir; makeShadowRay, rays.h:389-423, sets
+// SPRAY_RAY_EPSILON / +inf too), taken from the spawner's slot sel[src[j]].
+__global__ __launch_bounds__(kBlock) void k_pack_shadow(const float4* __restrict__ sh,
+                                                        const uint32_t* __restrict__ sel,
+                                                        const int64_t* __restrict__ idx,
+                                                        size_t n, float* __restrict__ out) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t slot = sel[idx[j]];
+  const float4 a = sh[2 * slot], b = sh[2 * slot + 1];
+  float2* o = reinterpret_cast<float2*>(out + 6 * j);
+  o[0] = make_float2(a.x, a.y);
+  o[1] = make_float2(a.z, b.x);
+  o[2] = make_float2(b.y, b.z);
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_shadow(const float* __restrict__ in, size_t m,
+                                                          float4* __restrict__ rays) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= m) return;
+  const float2* p = reinterpret_cast<const float2*>(in + 6 * j);
+  const float2 a = p[0], b = p[1], c = p[2];
+  rays[2 * j] = make_float4(a.x, a.y, b.x, kRayEpsilon);
+  rays[2 * j + 1] = make_float4(b.y, c.x, c.y, kInf);
+}
+
+// the spawner's slot table of the compacted shadow rays: gathers the route
+// input (32-B rays) of slots sel[0..n)
+__global__ __launch_bounds__(kBlock) void k_gather_shadow(const float4* __restrict__ sh,
+                                                          const uint32_t* __restrict__ sel,
+                                                          size_t n, float4* __restrict__ out) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t slot = sel[j];
+  out[2 * j] = sh[2 * slot];
+  out[2 * j + 1] = sh[2 * slot + 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_key_min(const int64_t* __restrict__ idx,
+                                                    const unsigned long long* __restrict__ keys,
+                                                    size_t n,
+                                                    unsigned long long* __restrict__ best) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const unsigned long long k = keys[j];
+  if (k != kInsituMissKey) atomicMin(best + idx[j], k);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_u64(unsigned long long* __restrict__ p,
+                                                     size_t n, unsigned long long v) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j < n) p[j] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_winners(const unsigned long long* __restrict__ key,
+                                                    const unsigned long long* __restrict__ best,
+                                                    size_t m, uint8_t* __restrict__ win) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= m) return;
+  const unsigned long long k = key[j];
+  win[j] = (k != kInsituMissKey && k == best[j]) ? 1 : 0;
+}
+
+// obuf OR at the spawner: any owner that found an occluder marks the slot
+__global__ __launch_bounds__(kBlock) void k_occ_return(const int64_t* __restrict__ idx,
+                                                       const uint8_t* __restrict__ ret, size_t n,
+                                                       const uint32_t* __restrict__ sel,
+                                                       uint8_t* __restrict__ occ) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  if (ret[j]) occ[sel[idx[j]]] = 1;
+}
+
+// HdrImage::add of the unoccluded shadows of the copies this rank shaded
+// (one thread per copy, its ns slots in order; copies of one pixel may sit
+// on any rank, so the adds are atomic -- the reference's per-rank images are
+// summed by MPI_Reduce too, image.h:167-181)
+__global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ image,
+                                                        const int32_t* __restrict__ pix,
+                                                        size_t m, int ns,
+                                                        const float4* __restrict__ sw,
+                                                        const uint8_t* __restrict__ sv,
+                                                        const uint8_t* __restrict__ occ,
+                                                        double scale) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= m) return;
+  float* px = image + 4 * size_t(pix[i]);
+  for (int k = 0; k < ns; ++k) {
+    const size_t j = i * size_t(ns) + k;
+    if (!sv[j] || occ[j]) continue;
+    const float4 L = sw[j];
+    atomicAdd(px, float(scale * double(L.x)));
+    atomicAdd(px + 1, float(scale * double(L.y)));
+    atomicAdd(px + 2, float(scale * double(L.z)));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_record(const uint8_t* __restrict__ win, size_t m,
+                                                   int bounce, int ns,
+                                                   const int32_t* __restrict__ sam,
+                                                   const spray_rt_hit* __restrict__ hits,
+                                                   const uint8_t* __restrict__ sv,
+                                                   const uint8_t* __restrict__ occ,
+                                                   spray_rt_insitu_rec rec) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= m || !win[i]) return;
+  const uint32_t k = atomicAdd(rec.d_count, 1u);
+  if (k >= rec.cap) return;
+  unsigned long long v = 0, o = 0;
+  for (int s = 0; s < ns && s < 64; ++s) {
+    const size_t j = i * size_t(ns) + s;
+    if (sv[j]) v |= 1ull << s;
+    if (sv[j] && occ[j]) o |= 1ull << s;
+  }
+  rec.samid[k] = sam[i];
+  rec.bounce[k] = bounce;
+  rec.hits[k] = hits[i];
+  rec.svalid[k] = v;
+  rec.occluded[k] = o;
+}
+
+// the next bounce's holder arrays: rays / weights / pixel / sample of the
+// copies sel[0..n) that spawned a radiance ray
+__global__ __launch_bounds__(kBlock) void k_gather_next(const float4* __restrict__ rays,
+                                                        const float4* __restrict__ w,
+                                                        const int32_t* __restrict__ pix,
+                                                        const int32_t* __restrict__ sam,
+                                                        const uint32_t* __restrict__ sel,
+                                                        size_t n, float4* __restrict__ orays,
+                                                        float4* __restrict__ ow,
+                                                        int32_t* __restrict__ opix,
+                                                        int32_t* __restrict__ osam) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t i = sel[j];
+  orays[2 * j] = rays[2 * i];
+  orays[2 * j + 1] = rays[2 * i + 1];
+  ow[j] = w[i];
+  opix[j] = pix[i];
+  osam[j] = sam[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_weights_one(float4* __restrict__ w, size_t n) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j < n) w[j] = make_float4(1.f, 1.f, 1.f, 0.f);
+}
+
+}  // namespace
+
+#define LAUNCH(n, kern, ...)                                  \
+  do {                                                        \
+    if ((n) == 0) return hipSuccess;                          \
+    kern<<<grid_for(n), kBlock, 0, s>>>(__VA_ARGS__);         \
+    return hipGetLastError();                                 \
+  } while (0)
+
+hipError_t launch_pack_rad(hipStream_t s, const spray_rt_ray* rays, const float* w,
+                           const int32_t* pix, const int32_t* sam, const int64_t* idx, size_t n,
+                           void* out) {
+  LAUNCH(n, k_pack_rad, reinterpret_cast<const float4*>(rays),
+         reinterpret_cast<const float4*>(w), pix, sam, idx, n, static_cast<float4*>(out));
+}
+hipError_t launch_unpack_rad(hipStream_t s, const void* in, size_t m, spray_rt_ray* rays,
+                             float* w, int32_t* pix, int32_t* sam) {
+  LAUNCH(m, k_unpack_rad, static_cast<const float4*>(in), m, reinterpret_cast<float4*>(rays),
+         reinterpret_cast<float4*>(w), pix, sam);
+}
+hipError_t launch_pack_shadow(hipStream_t s, const spray_rt_ray* slots, const uint32_t* sel,
+                              const int64_t* idx, size_t n, void* out) {
+  LAUNCH(n, k_pack_shadow, reinterpret_cast<const float4*>(slots), sel, idx, n,
+         static_cast<float*>(out));
+}
+hipError_t launch_unpack_shadow(hipStream_t s, const void* in, size_t m, spray_rt_ray* rays) {
+  LAUNCH(m, k_unpack_shadow, static_cast<const float*>(in), m, reinterpret_cast<float4*>(rays));
+}
+hipError_t launch_gather_shadow(hipStream_t s, const spray_rt_ray* slots, const uint32_t* sel,
+                                size_t n, spray_rt_ray* out) {
+  LAUNCH(n, k_gather_shadow, reinterpret_cast<const float4*>(slots), sel, n,
+         reinterpret_cast<float4*>(out));
+}
+hipError_t launch_key_min(hipStream_t s, const int64_t* idx, const uint64_t* keys, size_t n,
+                          uint64_t* best) {
+  LAUNCH(n, k_key_min, idx, reinterpret_cast<const unsigned long long*>(keys), n,
+         reinterpret_cast<unsigned long long*>(best));
+}
+hipError_t launch_fill_u64(hipStream_t s, uint64_t* p, size_t n, uint64_t v) {
+  LAUNCH(n, k_fill_u64, reinterpret_cast<unsigned long long*>(p), n, (unsigned long long)v);
+}
+hipError_t launch_winners(hipStream_t s, const uint64_t* key, const uint64_t* best, size_t m,
+                          uint8_t* win) {
+  LAUNCH(m, k_winners, reinterpret_cast<const unsigned long long*>(key),
+         reinterpret_cast<const unsigned long long*>(best), m, win);
+}
+hipError_t launch_occ_return(hipStream_t s, const int64_t* idx, const uint8_t* ret, size_t n,
+                             const uint32_t* sel, uint8_t* occ) {
+  LAUNCH(n, k_occ_return, idx, ret, n, sel, occ);
+}
+hipError_t launch_film_atomic(hipStream_t s, float* image, const int32_t* pix, size_t m, int ns,
+                              const float* sw, const uint8_t* sv, const uint8_t* occ,
+                              double scale) {
+  if (ns == 0) return hipSuccess;
+  LAUNCH(m, k_film_atomic, image, pix, m, ns, reinterpret_cast<const float4*>(sw), sv, occ,
+         scale);
+}
+hipError_t launch_record(hipStream_t s, const uint8_t* win, size_t m, int bounce, int ns,
+                         const int32_t* sam, const spray_rt_hit* hits, const uint8_t* sv,
+                         const uint8_t* occ, const spray_rt_insitu_rec& rec) {
+  LAUNCH(m, k_record, win, m, bounce, ns, sam, hits, sv, occ, rec);
+}
+hipError_t launch_gather_next(hipStream_t s, const spray_rt_ray* rays, const float* w,
+                              const int32_t* pix, const int32_t* sam, const uint32_t* sel,
+                              size_t n, spray_rt_ray* orays, float* ow, int32_t* opix,
+                              int32_t* osam) {
+  LAUNCH(n, k_gather_next, reinterpret_cast<const float4*>(rays),
+         reinterpret_cast<const float4*>(w), pix, sam, sel, n, reinterpret_cast<float4*>(orays),
+         reinterpret_cast<float4*>(ow), opix, osam);
+}
+hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
+  LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
+}
+
+}  // namespace spray_rt
+
+namespace spray_rt {
+namespace {
+__global__ void k_counts_from_starts(const int64_t* __restrict__ starts, int world,
+                                     int64_t* __restrict__ counts) {
+  const int r = threadIdx.x;
+  if (r < world) counts[r] = starts[r + 1] - starts[r];
+}
+}  // namespace
+
+hipError_t launch_counts_from_starts(hipStream_t s, const int64_t* starts, int world,
+                                     int64_t* counts) {
+  k_counts_from_starts<<<1, 64, 0, s>>>(starts, world, counts);
+  return hipGetLastError();
+}
+
+}  // namespace spray_rt

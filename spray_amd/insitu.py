@@ -1,106 +1,53 @@
-"""In-situ (domain-sharded) tracing across ranks, one rank per GPU.
+"""In-situ (domain-sharded) frames across ranks, one rank per GPU: a thin
+caller of the engine's in-situ tracer (spray_rt_insitu_*, insitu.cpp).
 
 The reference's in-situ mode (src/insitu/) keeps every domain resident on
 exactly one MPI rank and moves rays to the data:
 
 * ``InsituPartition::partition`` (src/render/data_partition.h:59-137): domain
-  centroids Morton-coded, sorted, dealt out in contiguous shares;
+  centroids Morton-coded, sorted, dealt out in contiguous shares
+  (``morton_partition`` -> spray_rt_insitu_partition);
 * ``TileList`` / ``makeHorizontalStripe`` (src/render/tile.cc:159-212): each
   rank generates the eye rays of one horizontal stripe of every blocking
-  tile;
-* ``Isector::intersect`` (src/insitu/insitu_isector.h:164-224): every ray is
-  queued, speculatively, to every domain on its sorted domain list, and the
-  queues of remote domains travel to their owners (insitu_comm.inl:28-101,
-  MPI Isend/Iprobe/Recv);
-* ``VBuf::compositeTbuf`` / ``compositeObuf`` (src/insitu/insitu_vbuf.h:
-  74-152): the per-sample nearest t is reduced with MPI_Allreduce(MIN), and
-  only the rank whose local hit equals it shades the sample and spawns its
-  shadow ray; occlusion bits are reduced with MPI_Allreduce(MAX).
+  tile (``horizontal_stripe``, spray_rt_eye_rays_insitu);
+* the per-bounce exchange, compositing, shading and film run inside the
+  engine (``InsituEngine.trace``): route, count exchange, ray exchange
+  (grouped ncclSend / ncclRecv), keyed closest hit, key minimum, winner
+  shading, shadow exchange and occlusion OR, film; one reduce composites the
+  ranks' images (``InsituEngine.composite``).
 
-Here the queues become bulk exchanges over RCCL (torch.distributed "nccl"):
-a count all-to-all, then one all-to-all of 32-B rays + 4-B sample ids per
-bounce.  The tbuf is a 64-bit composite key (t, position in the ray's sorted
-domain list, domain), reduced with MIN: the winner is then unique and equal
-to the sequential walk of the whole list (spray_rt_intersect_scene_keyed),
-where the reference leaves exact t ties to MPI's reduction order.
-
-The protocol runs on torch tensors; the local work (routing, keyed closest
-hit, shadow spawn, any hit) is a pluggable ``local`` object -- on a GPU the
-HIP engine (:class:`GpuLocal`).  Collectives with the "gloo" backend stage
-device tensors through host memory (tests; the product runs "nccl").
+Collectives go through RCCL directly from the engine; the communicator's id
+is created on rank 0 and broadcast over ``torch.distributed`` once.  For tests
+a host transport drives the same protocol over any ``torch.distributed``
+group (e.g. "gloo" processes sharing one GPU), staging through host memory.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
-__all__ = ["morton_code", "morton_partition", "horizontal_stripe", "Comm", "GpuLocal",
-           "InsituTracer", "MISS_KEY", "setup_rank_context"]
+from ._native import SprayRtError, lib
+
+__all__ = ["morton_partition", "horizontal_stripe", "setup_rank_context", "InsituEngine",
+           "InsituRecords", "MISS_KEY"]
 
 MISS_KEY = 0x7FFFFFFFFFFFFFFF
 
 
-# ---------------------------------------------------------------------------
-# partition and stripes
-# ---------------------------------------------------------------------------
-def _expand_bits(v):
-    """Morton::expandBits (src/render/morton.h:44-50), uint32 arithmetic."""
-    v = np.uint32(v)
-    with np.errstate(over="ignore"):
-        v = (v * np.uint32(0x00010001)) & np.uint32(0xFF0000FF)
-        v = (v * np.uint32(0x00000101)) & np.uint32(0x0F00F00F)
-        v = (v * np.uint32(0x00000011)) & np.uint32(0xC30C30C3)
-        v = (v * np.uint32(0x00000005)) & np.uint32(0x49249249)
-    return v
-
-
-def morton_code(x, y, z):
-    """Morton::compute (src/render/morton.h:32-41): 30-bit code of a point in
-    the unit cube, float32 clamping as the reference."""
-    f = np.float32
-    c = []
-    for a in (x, y, z):
-        a = f(min(max(f(a) * f(1024.0), f(0.0)), f(1023.0)))
-        c.append(_expand_bits(int(a)))
-    with np.errstate(over="ignore"):
-        return int((c[0] * np.uint32(4) + c[1] * np.uint32(2) + c[2]) & np.uint32(0xFFFFFFFF))
-
-
 def morton_partition(boxes, scene_bound, nranks):
-    """InsituPartition::partition with GROUP_CLOSE_DOMAINS
-    (src/render/data_partition.h:59-137) -> owner rank per domain.
-
-    boxes [n, 6] (lo, hi) world bounds in domain-id order, scene_bound [6].
-    Codes are sorted by (code, domain id): std::sort leaves equal codes in an
-    unspecified order, the domain id makes the map deterministic.  As in the
-    reference, shares = n // nranks (0 when n < nranks: every domain then
-    stays on rank 0) and the rank counter wraps."""
-    f = np.float32
-    boxes = np.asarray(boxes, f).reshape(-1, 6)
-    sb = np.asarray(scene_bound, f).reshape(6)
-    n = len(boxes)
+    """Owner rank per domain (InsituPartition::partition, GROUP_CLOSE_DOMAINS):
+    spray_rt_insitu_partition.  boxes [n, 6] (lo, hi) world bounds in
+    domain-id order, scene_bound [6]."""
+    b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+    sb = np.ascontiguousarray(scene_bound, np.float32).reshape(6)
     if nranks <= 0:
         raise ValueError("nranks must be > 0")
-    diag = sb[3:] - sb[:3]
-    scale = (f(1.0) / diag).astype(f)
-    mn = (sb[:3] * scale).astype(f)
-    off = (f(0.0) - mn).astype(f)
-    codes = []
-    for i in range(n):
-        center = ((boxes[i, :3] + boxes[i, 3:]) * f(0.5)).astype(f)  # Aabb::getCenter
-        c = (center * scale + off).astype(f)
-        codes.append((morton_code(c[0], c[1], c[2]), i))
-    codes.sort()
-    owner = np.zeros(n, np.int32)
-    shares = n // nranks
-    rank, s = 0, 0
-    for _, dom in codes:
-        owner[dom] = rank
-        s += 1
-        if s == shares:
-            s = 0
-            rank += 1
-            if rank == nranks:
-                rank = 0
+    owner = np.zeros(len(b), np.int32)
+    rc = lib().spray_rt_insitu_partition(b.ctypes.data, len(b), sb.ctypes.data, int(nranks),
+                                         owner.ctypes.data)
+    if rc != 0:
+        raise SprayRtError("insitu_partition failed (%d)" % rc)
     return owner
 
 
@@ -115,117 +62,6 @@ def horizontal_stripe(nranks, rank, tile):
         return (0, oy, 0, 0)
     oh = yend - oy if (oy + hh > yend or rank == nranks - 1) else hh
     return (x, oy, w, oh)
-
-
-# ---------------------------------------------------------------------------
-# collectives
-# ---------------------------------------------------------------------------
-class Comm:
-    """The rank group.  world == 1 makes every collective a no-op; "gloo"
-    stages device tensors through host memory."""
-
-    def __init__(self, dist=None, group=None, always=False):
-        self.dist = dist
-        self.group = group
-        if dist is not None and dist.is_initialized():
-            self.rank = dist.get_rank(group)
-            self.world = dist.get_world_size(group)
-            self.staged = dist.get_backend(group) == "gloo"
-        else:
-            self.rank, self.world, self.staged = 0, 1, False
-        # always: issue the collectives even for one rank (exercises RCCL)
-        self.skip = self.world == 1 and not (always and dist is not None)
-
-    def _host(self, t):
-        return t.cpu() if (self.staged and t.is_cuda) else t
-
-    def all_to_all(self, out, inp, out_splits, in_splits):
-        if self.skip:
-            out.copy_(inp)
-            return out
-        o, i = self._host(out), self._host(inp)
-        self.dist.all_to_all_single(o, i, out_splits, in_splits, group=self.group)
-        if o is not out:
-            out.copy_(o)
-        return out
-
-    def all_reduce(self, t, op):
-        if self.skip:
-            return t
-        h = self._host(t)
-        self.dist.all_reduce(h, op=op, group=self.group)
-        if h is not t:
-            t.copy_(h)
-        return t
-
-    def op(self, name):
-        return getattr(self.dist.ReduceOp, name) if self.dist is not None else None
-
-
-# ---------------------------------------------------------------------------
-# local work on one GPU
-# ---------------------------------------------------------------------------
-class GpuLocal:
-    """Local work of one rank through the HIP engine (device tensors).
-    Rays are float32 [n, 8] (org, tnear, dir, tfar), hits float32 [n, 12]
-    (spray_rt_hit), keys / rank masks int64 [n]."""
-
-    def __init__(self, rt, device, stream=None):
-        import torch
-        self.torch = torch
-        self.rt = rt
-        self.device = device
-        # the engine enqueues on torch's stream: the protocol's torch ops and
-        # the kernels stay ordered without host synchronisation
-        rt.set_stream(stream if stream is not None else torch.cuda.current_stream(device))
-
-    def route(self, rays):
-        m = self.torch.empty(rays.shape[0], dtype=self.torch.int64, device=self.device)
-        if rays.shape[0]:
-            self.rt.route(rays, m)
-        return m
-
-    def intersect_keyed(self, rays):
-        n = rays.shape[0]
-        hits = self.torch.empty((n, 12), dtype=self.torch.float32, device=self.device)
-        keys = self.torch.empty(n, dtype=self.torch.int64, device=self.device)
-        if n:
-            self.rt.intersect_scene_keyed(rays, hits, keys)
-        return hits, keys
-
-    def spawn_pt(self, rays, hits, shade):
-        t = self.torch
-        n = rays.shape[0]
-        out = t.empty((max(n, 1), 8), dtype=t.float32, device=self.device)
-        src = t.empty(max(n, 1), dtype=t.int32, device=self.device)
-        cnt = t.zeros(1, dtype=t.int32, device=self.device)
-        if n:
-            self.rt.spawn_shadows_pt(rays, hits, n, shade, out, src, cnt)
-        k = int(cnt.item()) if n else 0
-        return out[:k], src[:k].long()
-
-    def plan(self, mask, world):
-        """Per-destination ascending ray lists of a routed batch (device):
-        bounds first (one host read sizes the list), then the lists."""
-        t = self.torch
-        starts = t.empty(world + 1, dtype=t.int64, device=self.device)
-        self.rt.exchange_plan(mask, world, None, starts)
-        total = int(starts[-1])
-        idx = t.empty(max(total, 1), dtype=t.int64, device=self.device)
-        self.rt.exchange_plan(mask, world, idx, starts)
-        return idx[:total], starts
-
-    def gather(self, src, idx, dst):
-        """Exchange packing through the engine (torch's row gather is several
-        times slower for 32- and 48-byte rows)."""
-        self.rt.gather_rows(src, idx, dst)
-
-    def occluded(self, rays):
-        t = self.torch
-        occ = t.zeros(rays.shape[0], dtype=t.uint8, device=self.device)
-        if rays.shape[0]:
-            self.rt.occluded_scene(rays, occ)
-        return occ
 
 
 def setup_rank_context(rt, desc, ply_path, owner, rank):
@@ -245,111 +81,203 @@ def setup_rank_context(rt, desc, ply_path, owner, rank):
 
 
 # ---------------------------------------------------------------------------
-# the per-tile protocol
+# engine bindings
 # ---------------------------------------------------------------------------
-class Exchange:
-    """One routed exchange: row i of a ray batch goes to every rank whose bit
-    is set in mask[i].  ``forward`` moves per-ray payloads to the owners
-    (grouped by source rank, in the sender's order); ``backward`` returns
-    per-copy results to the sender, in the order the copies were sent."""
-
-    def __init__(self, comm, mask, gather=None, plan=None):
-        import torch as t
-        W = comm.world
-        self.comm = comm
-        self.gather = gather
-        n = mask.shape[0]
-        if plan is not None and mask.is_cuda:
-            # device plan: per-rank lists + bounds in four small kernels
-            self.idx, starts = plan(mask, W)
-            send = starts[1:] - starts[:-1]
-        else:
-            if n:
-                bit = t.arange(W, device=mask.device, dtype=t.int64).unsqueeze(1)
-                sel = ((mask.unsqueeze(0) >> bit) & 1).bool()  # [W, n], dest-major
-                dest, self.idx = sel.nonzero(as_tuple=True)
-            else:
-                dest = t.zeros(0, dtype=t.int64, device=mask.device)
-                self.idx = dest
-            send = t.bincount(dest, minlength=W).to(t.int64)
-        recv = t.empty_like(send)
-        comm.all_to_all(recv, send, None, None)  # the count phase
-        self.sc, self.rc = send.tolist(), recv.tolist()
-        self.n_sent, self.n_recv = sum(self.sc), sum(self.rc)
-
-    def forward(self, payload):
-        """payload: per-ray rows [n, ...] of the sender's batch."""
-        if self.gather is not None and payload.is_cuda:
-            s = payload.new_empty((self.idx.numel(),) + tuple(payload.shape[1:]))
-            self.gather(payload, self.idx, s)
-        else:
-            s = payload.index_select(0, self.idx)
-        if self.comm.skip:
-            return s
-        r = payload.new_empty((self.n_recv,) + tuple(payload.shape[1:]))
-        return self.comm.all_to_all(r, s, self.rc, self.sc)
-
-    def backward(self, result):
-        """result: per received copy [n_recv, ...] -> per sent copy."""
-        if self.comm.skip:
-            return result
-        r = result.new_empty((self.n_sent,) + tuple(result.shape[1:]))
-        return self.comm.all_to_all(r, result.contiguous(), self.sc, self.rc)
+_A2A = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
+                   C.POINTER(C.c_size_t))
+_AR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+_RED = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int)
 
 
-class InsituTracer:
-    """One bounce (primary closest hit + point-light shadow rays) of a
-    blocking tile, distributed by domain ownership.
+class Transport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("alltoallv", _A2A), ("allreduce_u64", _AR),
+                ("reduce_f32", _RED)]
 
-    Compositing happens per ray copy instead of over a whole-tile buffer:
-    the owners' keys travel back to the ray's sender (reverse all-to-all),
-    the sender's minimum travels out again, and the one owner whose key
-    equals it shades the sample and spawns its shadow ray; the shadow ray's
-    occlusion bits come back to that rank and are OR-ed there.  This is the
-    tbuf MIN / obuf MAX compositing of VBuf (insitu_vbuf.h:74-152) at the
-    cost of 8 B (keys) and 1 B (occlusion) per remote copy, instead of
-    all-reduces over every sample of the tile."""
 
-    def __init__(self, local, comm):
+class RecStruct(C.Structure):
+    _fields_ = [("samid", C.c_void_p), ("bounce", C.c_void_p), ("hits", C.c_void_p),
+                ("svalid", C.c_void_p), ("occluded", C.c_void_p), ("cap", C.c_size_t),
+                ("d_count", C.c_void_p)]
+
+
+def _host_view(ptr, nbytes):
+    if nbytes == 0:
+        return np.zeros(0, np.uint8)
+    return np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(ptr))
+
+
+class _HostCollectives:
+    """spray_rt_transport over a torch.distributed group (host tensors)."""
+
+    def __init__(self, dist, group=None):
         import torch
-        self.torch = torch
-        self.local = local
-        self.comm = comm
+        self.torch, self.dist, self.group = torch, dist, group
+        self.world = dist.get_world_size(group)
 
-    def trace_tile(self, rays, samid, shade):
-        """rays float32 [n, 8] of this rank's stripe, samid [n] (blocking-
-        tile sample ids).
+        def a2a(user, send, sb, recv, rb):
+            try:
+                s = [int(sb[r]) for r in range(self.world)]
+                r = [int(rb[k]) for k in range(self.world)]
+                src = torch.from_numpy(_host_view(send, sum(s)).copy())
+                dst = torch.empty(sum(r), dtype=torch.uint8)
+                self.dist.all_to_all_single(dst, src, r, s, group=self.group)
+                if sum(r):
+                    _host_view(recv, sum(r))[:] = dst.numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the status
+                print("insitu host all-to-all failed:", e)
+                return 1
 
-        Returns a dict: ``samid`` / ``hits`` of the samples whose nearest hit
-        lies in this rank's domains (this rank shades them), ``shadow_samid``
-        / ``shadow_occ`` of the shadow rays it spawned, and the job totals
-        ``n_rays`` and ``n_shadow``."""
-        t = self.torch
-        L, C = self.local, self.comm
-        samid = samid.to(t.int32)
-        n = rays.shape[0]
-        # primary rays to the owners of their domains, keyed closest hit there
-        gather, plan = getattr(L, "gather", None), getattr(L, "plan", None)
-        ex = Exchange(C, L.route(rays), gather, plan)
-        rrays, rsam = ex.forward(rays), ex.forward(samid)
-        hits, keys = L.intersect_keyed(rrays)
-        # composite: minimum key per ray at its sender, back to the owners
-        best = t.full((n,), MISS_KEY, dtype=t.int64, device=rays.device)
-        if ex.n_sent:
-            best.scatter_reduce_(0, ex.idx, ex.backward(keys), "amin")
-        win = (keys == ex.forward(best)) & (keys != MISS_KEY)
-        out_hits = hits[win]
-        # only the winner shades: the others' hits become misses
-        hits.view(t.int32)[:, 11].masked_fill_(~win, -1)  # spray_rt_hit.domain
-        srays, src = L.spawn_pt(rrays, hits, shade)
-        # shadow rays to the owners of their domains, any hit, OR at the spawner
-        sx = Exchange(C, L.route(srays), gather, plan)
-        occ = L.occluded(sx.forward(srays))
-        socc = t.zeros(srays.shape[0], dtype=t.uint8, device=rays.device)
-        if sx.n_sent:
-            socc.scatter_reduce_(0, sx.idx, sx.backward(occ), "amax")
-        tot = t.tensor([n, srays.shape[0]], dtype=t.int64, device=rays.device)
-        C.all_reduce(tot, C.op("SUM"))
-        return {"samid": rsam[win].long(), "hits": out_hits,
-                "shadow_samid": rsam.index_select(0, src).long(), "shadow_occ": socc,
-                "n_rays": int(tot[0]), "n_shadow": int(tot[1])}
+        def ar(user, data, n):
+            try:
+                a = _host_view(data, 8 * n).view(np.int64)
+                t = torch.from_numpy(a.copy())
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+                a[:] = t.numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001
+                print("insitu host all-reduce failed:", e)
+                return 1
+
+        def red(user, data, n, root):
+            try:
+                a = _host_view(data, 4 * n).view(np.float32)
+                t = torch.from_numpy(a.copy())
+                self.dist.reduce(t, dst=root, op=self.dist.ReduceOp.SUM, group=self.group)
+                a[:] = t.numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001
+                print("insitu host reduce failed:", e)
+                return 1
+
+        self._cbs = (_A2A(a2a), _AR(ar), _RED(red))  # kept alive with the engine
+        self.struct = Transport(None, *self._cbs)
+
+
+class InsituRecords:
+    """Device buffers of spray_rt_insitu_rec: per shaded copy its sample id,
+    bounce, winning hit (float32 [cap, 12]) and shadow-slot bits."""
+
+    def __init__(self, cap, device="cuda"):
+        import torch
+        self.cap = int(cap)
+        self.samid = torch.zeros(cap, dtype=torch.int32, device=device)
+        self.bounce = torch.zeros(cap, dtype=torch.int32, device=device)
+        self.hits = torch.zeros((cap, 12), dtype=torch.float32, device=device)
+        self.svalid = torch.zeros(cap, dtype=torch.int64, device=device)
+        self.occluded = torch.zeros(cap, dtype=torch.int64, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.struct = RecStruct(self.samid.data_ptr(), self.bounce.data_ptr(),
+                                self.hits.data_ptr(), self.svalid.data_ptr(),
+                                self.occluded.data_ptr(), self.cap, self.count.data_ptr())
+
+    def numpy(self):
+        """Host copies of the written records, sorted by (bounce, samid)."""
+        n = int(self.count.item())
+        if n > self.cap:
+            raise SprayRtError("record buffer overflow: %d > %d" % (n, self.cap))
+        s = self.samid[:n].cpu().numpy()
+        b = self.bounce[:n].cpu().numpy()
+        o = np.lexsort((s, b))
+        return {"samid": s[o], "bounce": b[o], "hits": self.hits[:n].cpu().numpy()[o],
+                "svalid": self.svalid[:n].cpu().numpy().view(np.uint64)[o],
+                "occluded": self.occluded[:n].cpu().numpy().view(np.uint64)[o]}
+
+
+class InsituEngine:
+    """spray_rt_insitu_t of one rank.
+
+    transport="rccl" (the product): RCCL communicator from an id made on
+    rank 0 and broadcast over ``dist`` (world 1 needs no ``dist``).
+    transport="host": host-staged collectives over ``dist`` (tests)."""
+
+    def __init__(self, rt, world=1, rank=0, dist=None, transport="rccl", group=None):
+        import torch
+        self.rt, self.world, self.rank = rt, int(world), int(rank)
+        self._host = None
+        h = C.c_void_p()
+        L = lib()
+        if transport == "rccl":
+            uid = np.zeros(128, np.uint8)
+            if self.rank == 0:
+                rc = L.spray_rt_insitu_unique_id(uid.ctypes.data, 128)
+                if rc != 0:
+                    raise SprayRtError("spray_rt_insitu_unique_id failed (%d)" % rc)
+            if self.world > 1:
+                t = torch.from_numpy(uid)
+                if dist.get_backend(group) == "nccl":
+                    t = t.cuda()
+                dist.broadcast(t, src=0, group=group)
+                uid = np.ascontiguousarray(t.cpu().numpy())
+            rc = L.spray_rt_insitu_create(rt.h, self.world, self.rank, uid.ctypes.data, None,
+                                          C.byref(h))
+        elif transport == "host":
+            if self.world > 1 and dist is None:
+                raise ValueError("host transport needs a torch.distributed group")
+            self._host = _HostCollectives(dist, group) if dist is not None else None
+            if self._host is None:  # world 1 without a group: local no-op collectives
+                self._host = _LocalCollectives()
+            rc = L.spray_rt_insitu_create(rt.h, self.world, self.rank, None,
+                                          C.byref(self._host.struct), C.byref(h))
+        else:
+            raise ValueError("transport must be 'rccl' or 'host'")
+        rt._check(rc, "insitu_create")
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().spray_rt_insitu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def trace(self, shader, rays, pixid, samid, spp, image, records=None):
+        """This rank's eye rays (device: rays [n, 8] float32 or 32-B rows,
+        pixid / samid int32 [n]) through shader.bounces bounces; the shaded
+        samples' contributions go to image (device float32 [w*h*4]).
+        Returns the group's (radiance rays, shadow rays)."""
+        from .engine import _addr, _nbytes
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        p, k2 = _addr(pixid)
+        s, k3 = _addr(samid)
+        im, k4 = _addr(image)
+        tot = (C.c_ulonglong * 3)()
+        rec = C.byref(records.struct) if records is not None else None
+        rc = lib().spray_rt_insitu_trace(self.h, C.byref(shader), a, p, s, n, int(spp), im, rec,
+                                         C.byref(tot))
+        self.rt._check(rc, "insitu_trace")
+        return int(tot[0]), int(tot[1])
+
+    def composite(self, image):
+        """HdrImage::composite: SUM of the ranks' images at rank 0."""
+        from .engine import _addr
+        im, k = _addr(image)
+        rc = lib().spray_rt_insitu_composite(self.h, im, image.numel())
+        self.rt._check(rc, "insitu_composite")
+        return image
+
+    def stats(self):
+        out = (C.c_ulonglong * 6)()
+        lib().spray_rt_insitu_stats(self.h, C.byref(out))
+        keys = ("bytes_sent", "bytes_received", "exchanges", "host_count_reads",
+                "collectives", "traces")
+        return dict(zip(keys, (int(x) for x in out)))
+
+
+class _LocalCollectives:
+    """A one-rank group's collectives (identity), for the host transport."""
+
+    def __init__(self):
+        def a2a(user, send, sb, recv, rb):
+            n = int(sb[0])
+            if n:
+                C.memmove(recv, send, n)
+            return 0
+
+        self._cbs = (_A2A(a2a), _AR(lambda u, d, n: 0), _RED(lambda u, d, n, r: 0))
+        self.struct = Transport(None, *self._cbs)

@@ -101,3 +101,76 @@ def full_reference(po, cam, tile, spp, desc=WAVELETS64, ply=SCENES):
 def bench_camera(po):
     c = BENCH_CAMERA
     return po.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], IMG, IMG)
+
+
+# ---------------------------------------------------------------------------
+# whole-scene reference of an in-situ frame (multi-bounce, PT / AO)
+# ---------------------------------------------------------------------------
+def reference_frame(po, sh, bsdfs, cam, img_w, img_h, spp, block, desc=WAVELETS64, ply=SCENES):
+    """The frame the in-situ ranks compute together, on the whole-scene
+    oracle: eye rays of the whole blocking tile (insitu seeds), per bounce
+    closest hit -> shade -> any hit -> film.  Returns (records by
+    (bounce, samid) -> (hit bytes, svalid bits, occluded bits), image,
+    (radiance rays, shadow rays))."""
+    org, d, pix, sam = po.eye_rays_insitu(cam, img_w, spp, block, block)
+    sc, _, _ = po.load_scene(desc, ply)
+    n = len(org)
+    ns = po.shadow_slots(sh)
+    w = np.ones((n, 3), np.float32)
+    valid = np.ones(n, np.uint8)
+    hits = np.zeros(n, po.HIT_DTYPE)
+    image = np.zeros(img_w * img_h * 4, np.float32)
+    recs = {}
+    nrad = nsh = 0
+    for b in range(sh.bounces):
+        live = np.flatnonzero(valid)
+        nrad += len(live)
+        if len(live):
+            h, _ = sc.intersect(org[live], d[live])
+            hits[live] = h
+        shaded = live[hits["domain"][live] >= 0]
+        so, sd, sw, sv, _ = po.shade(sh, bsdfs, b, org, d, hits, w, valid, pix, sam)
+        occ = np.zeros(n * ns, np.uint8)
+        sel = np.flatnonzero(sv)
+        nsh += len(sel)
+        if len(sel):
+            occ[sel], _ = sc.occluded(so[sel], sd[sel])
+        po.film(image, pix, spp, ns, sw, sv, occ, 1.0 / spp)
+        for i in shaded:
+            bv = bo = 0
+            for k in range(ns):
+                if sv[i * ns + k]:
+                    bv |= 1 << k
+                    if occ[i * ns + k]:
+                        bo |= 1 << k
+            recs[(b, int(sam[i]))] = (hits[i].tobytes(), bv, bo)
+    return recs, image, (nrad, nsh)
+
+
+def records_dict(recs):
+    """Engine / restatement records -> {(bounce, samid): (hit bytes, bits, bits)};
+    raises on a duplicate (a sample shaded twice in one bounce)."""
+    out = {}
+    if isinstance(recs, dict):  # InsituRecords.numpy()
+        rows = zip(recs["bounce"], recs["samid"], recs["hits"], recs["svalid"], recs["occluded"])
+        rows = [(int(b), int(s), np.ascontiguousarray(h).tobytes(), int(v), int(o))
+                for b, s, h, v, o in rows]
+    else:
+        rows = recs
+    for b, s, h, v, o in rows:
+        assert (b, s) not in out, ("shaded twice", b, s)
+        out[(b, s)] = (h, v, o)
+    return out
+
+
+def compare_records(got, ref):
+    """Bit-exact per (bounce, sample): same set of shaded samples, same
+    winning hit bytes, same spawned and occluded shadow slots."""
+    assert set(got) == set(ref), (len(set(got) - set(ref)), len(set(ref) - set(got)))
+    bad = [k for k in ref if got[k] != ref[k]]
+    assert not bad, (len(bad), bad[:5])
+
+
+def insitu_shader(po, kind, bounces, samples, lights=None):
+    lights = [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)] if lights is None else lights
+    return po.shader(kind, bounces, samples, (0.4, 0.4, 0.4), 10.0, lights)

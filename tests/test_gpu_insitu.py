@@ -1,7 +1,10 @@
 """GPU parity of the in-situ (domain-sharded) path: device eye rays of a
-stripe, routing masks, composite keys, and the whole protocol through the
-HIP engine (spray_amd.insitu.GpuLocal) at world_size 1 and 2 (two processes
-sharing the box's one GPU over "gloo"), against the whole-scene oracle."""
+stripe, routing masks, composite keys, and the engine's whole protocol
+(spray_rt_insitu_trace: exchange, compositing, shading, film; configs[2]
+PT, configs[4] AO-16, multi-bounce PT) -- over RCCL at one rank and over the
+host transport with 2 and 8 processes sharing the box's one GPU -- against
+the whole-scene oracle: every shaded sample bit-exact, totals exact, the
+composited image within summation-order tolerance."""
 import os
 import socket
 import tempfile
@@ -18,15 +21,6 @@ pytestmark = pytest.mark.gpu
 
 def _dev_rays(org, d):
     return H.rays_tensor(org, d).cuda()
-
-
-def _full_ctx(spray, owner=None):
-    from spray_amd import insitu
-    rt = spray.RtContext(0)
-    if owner is None:
-        owner = np.zeros(64, np.int32)
-    insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, 0)
-    return rt
 
 
 @pytest.fixture(scope="module")
@@ -72,10 +66,13 @@ def test_route_and_keys_match_oracle(spray, oracle):
     ref = H.OracleLocal(oracle, owner, 0)
     rt = spray.RtContext(0)
     insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, 0)
-    loc = insitu.GpuLocal(rt, torch.device("cuda"))
     rays = _dev_rays(org, d)
-    m = loc.route(rays)
-    hits, keys = loc.intersect_keyed(rays)
+    n = len(org)
+    m = torch.empty(n, dtype=torch.int64, device="cuda")
+    rt.route(rays, m)
+    hits = torch.empty((n, 12), dtype=torch.float32, device="cuda")
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    rt.intersect_scene_keyed(rays, hits, keys)
     torch.cuda.synchronize()
     cpu_rays = H.rays_tensor(org, d)
     assert (m.cpu() == ref.route(cpu_rays)).all()
@@ -86,55 +83,6 @@ def test_route_and_keys_match_oracle(spray, oracle):
     rt.close()
 
 
-def test_insitu_world1_matches_whole_scene(spray, oracle):
-    from spray_amd import insitu
-    rt = _full_ctx(spray)
-    cam = H.bench_camera(oracle)
-    org, d, _, sam = oracle.eye_rays_insitu(cam, H.IMG, H.SPP, H.TILE, H.TILE)
-    tr = insitu.InsituTracer(insitu.GpuLocal(rt, torch.device("cuda")), insitu.Comm())
-    n = len(org)
-    res = tr.trace_tile(_dev_rays(org, d), torch.from_numpy(sam).cuda(), H.SHADE)
-    hit_ref, occ_ref, nsh = H.full_reference(oracle, cam, H.TILE, H.SPP)
-    got = np.zeros(n, oracle.HIT_DTYPE)
-    got[res["samid"].cpu().numpy()] = res["hits"].cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1)
-    hit = hit_ref["domain"] >= 0
-    assert len(res["samid"]) == hit.sum()
-    assert got[hit].tobytes() == hit_ref[hit].tobytes()
-    assert res["n_shadow"] == nsh and res["n_rays"] == n
-    ss = res["shadow_samid"].cpu().numpy()
-    assert len(ss) == nsh and (res["shadow_occ"].cpu().numpy() == occ_ref[ss]).all()
-    rt.close()
-
-
-def test_insitu_over_rccl_one_rank(spray, oracle):
-    """The protocol's collectives through RCCL ("nccl", world_size 1, every
-    all-to-all / all-reduce issued): same result as the whole scene."""
-    import torch.distributed as dist
-    from spray_amd import insitu
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
-    dist.init_process_group("nccl", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
-    try:
-        rt = _full_ctx(spray)
-        cam = H.bench_camera(oracle)
-        org, d, _, sam = oracle.eye_rays_insitu(cam, H.IMG, H.SPP, H.TILE, H.TILE)
-        tr = insitu.InsituTracer(insitu.GpuLocal(rt, torch.device("cuda")),
-                                 insitu.Comm(dist, always=True))
-        res = tr.trace_tile(_dev_rays(org, d), torch.from_numpy(sam).cuda(), H.SHADE)
-        hit_ref, occ_ref, nsh = H.full_reference(oracle, cam, H.TILE, H.SPP)
-        hit = hit_ref["domain"] >= 0
-        got = np.zeros(len(org), oracle.HIT_DTYPE)
-        got[res["samid"].cpu().numpy()] = (res["hits"].cpu().numpy()
-                                           .view(oracle.HIT_DTYPE).reshape(-1))
-        assert len(res["samid"]) == hit.sum()
-        assert got[hit].tobytes() == hit_ref[hit].tobytes()
-        ss = res["shadow_samid"].cpu().numpy()
-        assert res["n_shadow"] == nsh and (res["shadow_occ"].cpu().numpy() == occ_ref[ss]).all()
-        rt.close()
-    finally:
-        dist.destroy_process_group()
-
-
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -143,65 +91,129 @@ def _free_port():
     return p
 
 
-def _gpu_rank_main(rank, world, port, out):
+CASES = {  # name: (shader kind, bounces, samples, image size, spp)
+    "pt1": ("pt", 1, 1, 128, 2),
+    "ao16": ("ao", 1, 16, 64, 2),
+    "pt3": ("pt", 3, 2, 96, 2),
+}
+LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)]}
+
+
+def _engine_rank(rank, world, case, transport, dist=None):
+    """One rank's engine frame of CASES[case]: returns (records, totals, image)."""
+    import spray_amd
+    from spray_amd import insitu
+    from oracle import pyoracle as po
+    from test_insitu import scene_boxes
+    kind, bounces, samples, img, spp = CASES[case]
+    boxes, bound = scene_boxes()
+    owner = insitu.morton_partition(boxes, bound, world)
+    rt = spray_amd.RtContext(0)
+    insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
+    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
+    rt.set_stream(torch.cuda.current_stream())
+    c = H.BENCH_CAMERA
+    cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    block = (0, 0, img, img)
+    stripe = insitu.horizontal_stripe(world, rank, block)
+    n = stripe[2] * stripe[3] * spp
+    rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device="cuda")[:n]
+    pix = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
+    sam = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
+    rt.eye_rays_insitu(cam, img, spp, block, stripe, rays, pix, sam)
+    lights = LIGHTS.get(case, [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)])
+    sh = spray_amd.frame.make_shader(kind, bounces, samples, lights=lights)
+    eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport=transport)
+    recs = insitu.InsituRecords(img * img * spp * bounces + 16)
+    image = torch.zeros(img * img * 4, dtype=torch.float32, device="cuda")
+    tot = eng.trace(sh, rays, pix, sam, spp, image, recs)
+    # a second trace reuses the engine's buffers: same totals, image doubles
+    tot2 = eng.trace(sh, rays, pix, sam, spp, image)
+    assert tot2 == tot
+    image.mul_(0.5)
+    st = eng.stats()
+    out = (recs.numpy(), tot, image.cpu().numpy(), st)
+    eng.close()
+    rt.close()
+    return out
+
+
+def _reference(oracle, case):
+    kind, bounces, samples, img, spp = CASES[case]
+    c = H.BENCH_CAMERA
+    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    _, doms, _ = oracle.load_scene(WAVELETS64, SCENES)
+    sh = H.insitu_shader(oracle, kind, bounces, samples, LIGHTS.get(case))
+    return H.reference_frame(oracle, sh, oracle.scene_bsdfs(doms), cam, img, img, spp,
+                             (0, 0, img, img))
+
+
+def _check(oracle, case, results):
+    ref, ref_img, ref_tot = _reference(oracle, case)
+    merged = []
+    for recs, tot, _, _ in results:
+        assert tot == ref_tot
+        d = H.records_dict(recs)
+        merged += [(b, s) + v for (b, s), v in d.items()]
+    H.compare_records(H.records_dict(merged), ref)
+    total = np.sum([r[2] for r in results], axis=0)
+    assert (ref_img > 0).sum() > 500
+    np.testing.assert_allclose(total, ref_img, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", ["pt1", "ao16", "pt3"])
+def test_engine_one_rank_rccl(oracle, case):
+    """The product transport (RCCL communicator of one rank): every
+    all-reduce / reduce through RCCL, the self exchange through
+    ncclSend / ncclRecv (SPRAY_INSITU_NCCL_SELF=1)."""
+    os.environ["SPRAY_INSITU_NCCL_SELF"] = "1"
+    try:
+        res = _engine_rank(0, 1, case, "rccl")
+    finally:
+        del os.environ["SPRAY_INSITU_NCCL_SELF"]
+    _check(oracle, case, [res])
+    assert res[3]["collectives"] > 0 and res[3]["traces"] == 2
+
+
+def test_engine_one_rank_host(oracle):
+    _check(oracle, "pt1", [_engine_rank(0, 1, "pt1", "host")])
+
+
+def _gpu_rank_main(rank, world, port, out, case):
+    import pickle
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
     sys.path.insert(0, os.path.dirname(here))
     import torch.distributed as dist
-    import spray_amd
-    from spray_amd import insitu
-    from oracle import pyoracle as po
-    import insitu_helpers as Hh
-    from test_insitu import scene_boxes
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        boxes, bound = scene_boxes()
-        owner = insitu.morton_partition(boxes, bound, world)
-        rt = spray_amd.RtContext(0)
-        insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
-        cam = Hh.bench_camera(po)
-        stripe = insitu.horizontal_stripe(world, rank, Hh.TILE)
-        n = stripe[2] * stripe[3] * Hh.SPP
-        rays = torch.empty((n, 8), dtype=torch.float32, device="cuda")
-        sam = torch.empty(n, dtype=torch.int32, device="cuda")
-        rt.eye_rays_insitu(cam, Hh.IMG, Hh.SPP, Hh.TILE, stripe, rays, None, sam)
-        rt.sync()
-        tr = insitu.InsituTracer(insitu.GpuLocal(rt, torch.device("cuda")), insitu.Comm(dist))
-        res = tr.trace_tile(rays, sam, Hh.SHADE)
-        np.savez(os.path.join(out, "r%d.npz" % rank), samid=res["samid"].cpu().numpy(),
-                 hits=res["hits"].cpu().numpy(),
-                 shadow_samid=res["shadow_samid"].cpu().numpy(),
-                 shadow_occ=res["shadow_occ"].cpu().numpy(), n_shadow=res["n_shadow"],
-                 n_rays=n)
-        rt.close()
+        res = _engine_rank(rank, world, case, "host", dist)
+        with open(os.path.join(out, "r%d.pkl" % rank), "wb") as fh:
+            pickle.dump(res, fh)
     finally:
         dist.destroy_process_group()
 
 
-def test_insitu_two_ranks_on_gpu(oracle):
-    """Two processes, 32 domains each, exchanging rays: the HIP route /
-    keyed / spawn / any-hit kernels under the real protocol."""
-    world = 2
+@pytest.mark.parametrize("world,case", [(2, "pt1"), (8, "pt1"), (8, "ao16"), (8, "pt3")])
+def test_engine_ranks_on_gpu(oracle, world, case):
+    """world processes sharing the box's one GPU, each an engine rank with
+    its 64/world domains (configs[2]: 8 per rank at world 8), exchanging
+    through the host transport over "gloo": every kernel and every step of
+    the engine's protocol runs; RCCL itself is covered by the one-rank test
+    (one GPU cannot hold an RCCL group of several ranks)."""
+    import pickle
     with tempfile.TemporaryDirectory() as out:
-        torch.multiprocessing.spawn(_gpu_rank_main, args=(world, _free_port(), out),
+        torch.multiprocessing.spawn(_gpu_rank_main, args=(world, _free_port(), out, case),
                                     nprocs=world)
-        res = [np.load(os.path.join(out, "r%d.npz" % r)) for r in range(world)]
-    hit_ref, occ_ref, nsh = H.full_reference(oracle, H.bench_camera(oracle), H.TILE, H.SPP)
-    n = len(hit_ref)
-    assert sum(int(r["n_rays"]) for r in res) == n
-    got = np.zeros(n, oracle.HIT_DTYPE)
-    seen = np.zeros(n, np.int32)
-    for r in res:
-        got[r["samid"]] = r["hits"].view(oracle.HIT_DTYPE).reshape(-1)
-        seen[r["samid"]] += 1
-        assert int(r["n_shadow"]) == nsh
-        assert (r["shadow_occ"] == occ_ref[r["shadow_samid"]]).all()
-        assert len(r["samid"]) > 100
-    hit = hit_ref["domain"] >= 0
-    assert (seen[hit] == 1).all() and (seen[~hit] == 0).all()
-    assert got[hit].tobytes() == hit_ref[hit].tobytes()
+        res = []
+        for r in range(world):
+            with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
+                res.append(pickle.load(fh))
+    _check(oracle, case, res)
+    assert sum(len(r[0]["samid"]) > 50 for r in res) >= max(2, world // 2)
+    assert all(r[3]["bytes_sent"] > 0 for r in res if len(r[0]["samid"]))
 
 
 def test_domain_mask_exact_on_box_boundaries(spray, oracle):
@@ -249,8 +261,10 @@ def test_domain_mask_exact_on_box_boundaries(spray, oracle):
     rt = spray.RtContext(0)
     rt.domain_bounds(boxes)
     rt.set_owners(np.arange(len(boxes), dtype=np.int32))
-    loc = insitu.GpuLocal(rt, torch.device("cuda"))
-    mask = loc.route(H.rays_tensor(org, d).cuda()).cpu().numpy().view(np.uint64)
+    mk = torch.empty(len(org), dtype=torch.int64, device="cuda")
+    rt.route(H.rays_tensor(org, d).cuda(), mk)
+    rt.sync()
+    mask = mk.cpu().numpy().view(np.uint64)
     ids, _, cnt, _ = oracle.domain_query(org, d, boxes, len(boxes))
     ref = np.zeros(len(org), np.uint64)
     for i in range(len(org)):
