@@ -49,7 +49,11 @@ W = H = 1024
 SPP = 8
 TILE_H = 128  # ImageScheduleTileList: 1M samples per rank -> 8 tiles of 1024x128
 SHADE = [0.0, 500.0, 1000.0, 1.0, 1.0, 1.0, 0.4, 0.4, 0.4, 10.0]  # light, --blinn
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+HBM_PEAK_GBS = 8000.0
+# SPRAY_BENCH_REHEARSE=1: rehearse the N > 1 code path on a one-GPU box (all
+# ranks share GPU 0; torch.distributed "gloo"; in-situ exchanges through the
+# engine's host transport instead of RCCL).  Never used for measurements.
+REHEARSE = os.environ.get("SPRAY_BENCH_REHEARSE") == "1"  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
 def tiles():
@@ -57,8 +61,66 @@ def tiles():
 
 
 def algorithmic_bytes(n_rays, nodes, tris, out_bytes):
-    """sum_rays (32 + out) + sum_visits (64 N_node + 48 N_tri)."""
+    """sum_rays (32 + out) + sum_visits (64 N_node + 48 N_tri).
+    A work index of the per-ray traversal, not traffic: the packet walk
+    fetches a node once per wave, and the scene stays in L2 / MALL."""
     return n_rays * (32 + out_bytes) + 64 * nodes + 48 * tris
+
+
+# the dominant kernels' names in the rocprofv3 summaries (profiles/)
+KERNEL_FUSED = "k_scene<1, false, false, 3, 16, 1>"  # closest hit + PT spawn + shadow any hit
+KERNEL_AO = "k_scene<1, true, false, 0, 16, 0>"      # per-lane any hit (AO rays)
+PMC = os.path.join(ROOT, "profiles", "pmc_counters.json")
+
+
+def scene_bytes(sc, rt):
+    """Bytes of the resident scene image a launch has to read at least once:
+    per domain the BVH2 nodes (64 B), triangle records (48 B), leaf map (4 B),
+    faces (12 B), colors (4 B / vertex) and normals (12 B / vertex)."""
+    total = 0
+    for d in range(sc.getNumDomains()):
+        i = rt.slot_info(sc.load(d))
+        v, f, _, _ = sc.domain_mesh(d)
+        total += 64 * i["nodes"] + 52 * i["tris"] + 12 * len(f) + 16 * len(v)
+    return total
+
+
+def roofline(kernel, launch_s, compulsory, index_bytes, index_note):
+    """The roofline object of one kernel.  achieved = its compulsory
+    (algorithmic) HBM bytes per launch -- rays in, results out, the scene
+    image once -- over the launch time measured here; traffic = the HBM bytes
+    its PMC pass measured (profiles/pmc_counters.json, labelled with the
+    round it comes from), and the other ceilings from the same profile."""
+    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "achieved": round(compulsory / launch_s / 1e9, 1),
+           "frac": round(compulsory / launch_s / 1e9 / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_launch": compulsory, "avg_launch_ms": round(launch_s * 1e3, 4),
+           "kernel": kernel, "traffic": None,
+           "index_8d": {"bytes_per_launch": index_bytes,
+                        "GB_s": round(index_bytes / launch_s / 1e9, 1), "note": index_note}}
+    if os.path.exists(PMC):
+        try:
+            pm = json.load(open(PMC))
+            dv = pm["kernels"][kernel]["derived"]
+        except (KeyError, ValueError):
+            return out
+        t = dv.get("traffic_bytes")
+        out["traffic"] = round(t) if t else None
+        out["traffic_source"] = ("profiles/pmc_counters.json (%s): 2 x FETCH_SIZE + WRITE_SIZE "
+                                 "of this kernel, separate --pmc passes" % pm.get("round"))
+        if t:
+            out["traffic_frac"] = round(t / launch_s / 1e9 / HBM_PEAK_GBS, 4)
+        ceil = {}
+        if "l2_request_bytes" in dv:
+            ceil["l2"] = {"request_bytes": round(dv["l2_request_bytes"]),
+                          "frac": round(dv["l2_request_bytes"] / launch_s / 34.5e12, 4),
+                          "peak_GBs": 34500.0, "l2_hit": round(dv.get("l2_hit", 0), 4)}
+        for k in ("valu_issue", "salu_issue", "valu_lane_util", "scalar_cache_hit", "ta_busy",
+                  "wait_any_frac"):
+            if k in dv:
+                ceil[k] = round(dv[k], 4)
+        out["ceilings"] = ceil
+    return out
 
 
 def cpu_baseline(target_s=10.0):
@@ -88,8 +150,17 @@ def cpu_baseline(target_s=10.0):
             n += b
         reps += 1
     y0, rows = 0, H
+    try:  # the reference's Embree path is the baseline only if Embree exists
+        import subprocess
+        ld = subprocess.run(["ldconfig", "-p"], capture_output=True, text=True, timeout=20).stdout
+        hits = [l.strip() for l in ld.splitlines() if "embree" in l.lower()]
+        probe = ("ldconfig -p on this host lists %s" % "; ".join(hits)) if hits else \
+            "ldconfig -p on this host lists no libembree: the reference's Embree path cannot run, " \
+            "the oracle port is the baseline"
+    except Exception as e:  # noqa: BLE001
+        probe = "ldconfig probe failed: %s" % e
     return {"value": round(n / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "embree_probe": probe,
             "sample": "%d x the full 1024x1024x8spp frame (8 tiles of 1024x128): %d "
                       "primary+shadow rays, oracle/oracle.c (C, OpenMP, %d threads), "
                       "%.1f s traversal+spawn" % (reps, n, threads, dt)}
@@ -120,7 +191,7 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt"):
     rt.set_bsdfs(host_scene_bsdfs(SCENE))
     rt.set_stream(torch.cuda.current_stream(dev))
     eng = insitu.InsituEngine(rt, world, rank, dist=dist if world > 1 else None,
-                              transport="rccl")
+                              transport="host" if REHEARSE else "rccl")
     stripe = insitu.horizontal_stripe(world, rank, (0, 0, W, H))
     n = stripe[2] * stripe[3] * SPP
     rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)[:n]
@@ -180,12 +251,15 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt"):
     return out
 
 
-def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
-    """configs[4] per GPU: closest hit of the frame, ooc::ShaderAo spawn of 16
-    rays per hit on the device, any hit of all of them (count stays on the
-    device).  Frame replicas across ranks, timed like the main line."""
+def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
+    """configs[4] workload on one GPU (all 64 domains resident): closest hit
+    of the frame, ooc::ShaderAo spawn of 16 rays per hit on the device, any
+    hit of all of them (count stays on the device).  The AO any hit is the
+    kernel with the most GPU time in the bench; its launch is timed with HIP
+    events for its roofline object."""
     import torch
     dev = prim.device
+    stream = torch.cuda.current_stream(dev)
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
     ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
@@ -193,23 +267,28 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
 
-    def frame():
+    def frame(ev=None):
         rt.set_coherence(rt.RAYS_COHERENT)  # camera rays: packets
         rt.intersect_scene(prim, hits)
         # the spp rays of a pixel share every sample direction (seed
         # pixid * (l + 1)): traced sample-major, they sit on neighbouring lanes
         rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order)
         rt.set_coherence(rt.RAYS_INCOHERENT)  # hemisphere rays: one walk per lane
+        if ev:
+            ev[0].record(stream)
         rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
+        if ev:
+            ev[1].record(stream)
 
     for _ in range(args.warmup):
         frame()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        frame()
+    for k in range(args.steps):
+        frame(evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -219,13 +298,25 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, nsamples=16):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e.item())
     n_ao = int(cnt.item())
+    ah_s = float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e-3
+    # canonical counts of the AO rays (counting build, outside the timing)
+    ctr = torch.zeros(3, dtype=torch.int64, device=dev)
+    rt.occluded_scene(ao[:n_ao * 32], occ[:n_ao], counters=ctr)
+    torch.cuda.synchronize()
+    idx = algorithmic_bytes(n_ao, int(ctr[0]), int(ctr[1]), 4)
+    # compulsory bytes: 32-B rays + 4-B trace order in, 1 B out, the scene once
+    comp = n_ao * (32 + 4 + 1) + sbytes
     rt.set_coherence(rt.RAYS_ADAPTIVE)
     return {"value": round((n_prim + n_ao) * world * args.steps / el / 1e6, 3),
             "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
             "scaling": "weak", "rays_per_step": n_prim + n_ao, "ao_rays": n_ao,
-            "config": "configs[4] workload per GPU: 64 domains resident, primary + "
-                      "AO-%d rays per hit traced sample-major per pixel (frame replicas x%d)"
-                      % (nsamples, world)}
+            "canonical_counts": {"nodes": int(ctr[0]), "tris": int(ctr[1]),
+                                 "visits": int(ctr[2]), "rays": n_ao},
+            "roofline": roofline(KERNEL_AO, ah_s, comp, idx,
+                                 "SURVEY 8(d) per-ray bytes over the AO rays' canonical counts "
+                                 "(counting build of this run)"),
+            "config": "configs[4] workload on one GPU: 64 domains resident, primary + "
+                      "AO-%d rays per hit traced sample-major per pixel" % nsamples}
 
 
 def run_frame(args, dist, world, rt, cam, lights):
@@ -323,7 +414,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--insitu", type=int, default=1,
                     help="also measure configs[2] through the engine's RCCL in-situ tracer "
                          "(always on with more than one rank: it is the headline there)")
@@ -340,9 +430,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if REHEARSE:  # every rank on GPU 0, "gloo" + the engine's host transport
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if REHEARSE:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import spray_amd
     sc = spray_amd.Scene(SCENE, SCENES, cache_size=-1, device=local)
@@ -446,16 +541,11 @@ def main():
     ch_bytes = algorithmic_bytes(n_prim, pc["nodes"], pc["tris"], 32)
     ah_bytes = algorithmic_bytes(n_shadow, sh["nodes"], sh["tris"], 4)
     fused_bytes = ch_bytes + ah_bytes
-    fused_gbs = fused_bytes / (fused_ms * 1e-3) / 1e9
-    ch_gbs = ch_bytes / (ch_ms * 1e-3) / 1e9
-    ah_gbs = ah_bytes / (ah_ms * 1e-3) / 1e9
-    traffic = None
-    if args.traffic and os.path.exists(args.traffic):
-        try:
-            traffic = json.load(open(args.traffic)).get("scene_intersect_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    sbytes = scene_bytes(sc, rt)
+    # compulsory bytes of the fused launch: 32-B rays in, 48-B records + the
+    # shadow valid / occluded bytes out (the shadow rays never leave the chip),
+    # the scene image once
+    fused_compulsory = n_prim * (32 + 48 + 1 + 1) + sbytes
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -465,17 +555,13 @@ def main():
                                "resident per GPU (configs[1])",
                    "rays_per_step": rays_step, "primary_rays": n_prim, "shadow_rays": n_shadow,
                    "parallelism": "one GPU, the whole frame"},
-        "roofline": {"bound": "hbm", "achieved": round(fused_gbs, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(fused_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "kernel": "k_scene<closest hit + PT spawn + shadow any hit> (one launch)",
-                     "bytes_per_launch": fused_bytes, "avg_launch_ms": round(fused_ms, 4),
-                     "counts": counts_src},
+        "roofline": roofline(KERNEL_FUSED, fused_ms * 1e-3, fused_compulsory, fused_bytes,
+                             "SURVEY 8(d) per-ray node/triangle bytes over the canonical counts "
+                             "(%s); a work index, not traffic (one node fetch per wave, scene "
+                             "in L2/MALL)" % counts_src),
         "kernels_ms": {"intersect_scene_shadow_pt": round(fused_ms, 4),
                        "unfused": {"intersect_scene_spawn_pt": round(ch_ms, 4),
-                                   "occluded_scene_masked": round(ah_ms, 4),
-                                   "closest_hit_achieved_GBs": round(ch_gbs, 1),
-                                   "any_hit_achieved_GBs": round(ah_gbs, 1)}},
+                                   "occluded_scene_masked": round(ah_ms, 4)}},
         "canonical_counts": gpu_counts,
     }
     if args.insitu != 0 or world > 1:
@@ -496,7 +582,7 @@ def main():
         if world > 1:  # configs[4]: AO-16 on the domain-sharded frame
             out["ao"] = run_insitu(args, dist, world, rank, local, cam, kind="ao")
         else:
-            out["ao"] = run_ao(args, dist, world, rt, prim, pixid, n_prim)
+            out["ao"] = run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes)
     if args.frame:
         _, lights = spray_amd.engine.host_parse_scene(SCENE, SCENES)
         out["frame"] = run_frame(args, dist, world, rt, cam, lights)
