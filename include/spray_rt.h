@@ -42,7 +42,9 @@
  *    geomID becomes 0 on a hit / occlusion and is otherwise left as the
  *    caller set it (0xFFFFFFFF); instID is never touched; color (byte
  *    offset 60) and Ns (offset 84) are filled by the fused epilogue.
- *  - One context per GPU; a context is driven by one host thread at a time.
+ *  - One context per GPU; a context is driven by one host thread at a time,
+ *    except through lanes (spray_rt_lane_*): one lane per host thread, run
+ *    concurrently.
  */
 #ifndef SPRAY_RT_H_
 #define SPRAY_RT_H_
@@ -173,6 +175,27 @@ int spray_rt_occluded_segments(spray_rt_ctx_t ctx, const int* slots,
  * counts[M] (truncated at maxhits). */
 int spray_rt_domains1M(spray_rt_ctx_t ctx, const float* org, const float* dir,
                        size_t M, int* ids, float* ts, int* counts, int maxhits);
+
+/* ---- lanes: concurrent per-thread submission (Scene's const queries) ---- */
+/* The reference calls Scene::intersect / occluded / intersectDomains from
+ * every OpenMP thread at once against the loaded domain
+ * (src/ooc/ooc_pcontext.h:144-157, ooc_tcontext.inl:28-100).  A lane is one
+ * host thread's private stream + staging: calls on different lanes of one
+ * context may run concurrently; one lane is driven by one thread at a time.
+ * They read the context's slot and domain tables, which must not change
+ * while lanes run (the reference loads domains inside omp single between
+ * barriers).  Host or device ray buffers; the call returns with the results
+ * in place (host) or completed on the lane's stream (device). */
+typedef struct spray_rt_lane* spray_rt_lane_t;
+int spray_rt_lane_create(spray_rt_ctx_t ctx, spray_rt_lane_t* out);
+int spray_rt_lane_destroy(spray_rt_lane_t lane);
+const char* spray_rt_lane_last_error(spray_rt_lane_t lane);
+int spray_rt_lane_intersect1M(spray_rt_lane_t lane, int slot, void* rays, size_t M,
+                              size_t stride);
+int spray_rt_lane_occluded1M(spray_rt_lane_t lane, int slot, void* rays, size_t M,
+                             size_t stride);
+int spray_rt_lane_domains1M(spray_rt_lane_t lane, const float* org, const float* dir, size_t M,
+                            int* ids, float* ts, int* counts, int maxhits);
 
 /* ---- fused scene path (all listed domains in one launch) ---- */
 int spray_rt_intersect_scene(spray_rt_ctx_t ctx, const spray_rt_ray* rays,

@@ -116,6 +116,12 @@ SIGNATURES = {
     "spray_rt_frame_stats": (I, [P, P, I]),
     "spray_rt_tile_list": (I, [I, I, I, I, I, I, C.c_longlong, P, I, P]),
     "spray_rt_write_ppm": (I, [C.c_char_p, P, I, I]),
+    "spray_rt_lane_create": (I, [P, P]),
+    "spray_rt_lane_destroy": (I, [P]),
+    "spray_rt_lane_last_error": (C.c_char_p, [P]),
+    "spray_rt_lane_intersect1M": (I, [P, I, P, SZ, SZ]),
+    "spray_rt_lane_occluded1M": (I, [P, I, P, SZ, SZ]),
+    "spray_rt_lane_domains1M": (I, [P, P, P, SZ, P, P, P, I]),
     "spray_rt_insitu_unique_id": (I, [P, SZ]),
     "spray_rt_insitu_create": (I, [P, I, I, P, P, P]),
     "spray_rt_insitu_destroy": (I, [P]),

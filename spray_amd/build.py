@@ -64,5 +64,24 @@ def build(force=False, verbose=False, defines=(), out=None):
     return target
 
 
+TEST_SRC = os.path.join(ROOT, "tests", "cpp", "scene_adapter_test.cpp")
+TEST_BIN = os.path.join(ROOT, "tests", "cpp", "_build", "scene_adapter_test")
+
+
+def build_tests():
+    """The C++ caller test of the SceneT drop-in (include/spray_scene.hpp):
+    links the engine and the CPU oracle (test infrastructure)."""
+    os.makedirs(os.path.dirname(TEST_BIN), exist_ok=True)
+    cmd = ["g++", "-O2", "-std=c++17", "-fopenmp", "-Wall", "-I" + os.path.join(ROOT, "include"),
+           "-I" + os.path.join(ROOT, "oracle"), TEST_SRC, "-L" + LIBDIR, "-lspray_rt",
+           "-L" + os.path.join(ROOT, "oracle", "_build"), "-loracle",
+           "-Wl,-rpath,$ORIGIN/../../../spray_amd/lib:$ORIGIN/../../../oracle/_build",
+           "-o", TEST_BIN]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("scene adapter test build failed:\n" + r.stdout + r.stderr)
+    return TEST_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

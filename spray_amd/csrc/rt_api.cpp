@@ -531,6 +531,164 @@ int spray_rt_occluded_segments(spray_rt_ctx_t c, const int* slots,
   return run_rtc(c, slots, offsets, nseg, rays, stride, launch_rtc_occluded);
 }
 
+}  // extern "C"
+
+// ---- lanes --------------------------------------------------------------
+namespace {
+int lane_fail(spray_rt_lane* L, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  L->err = buf;
+  return code;
+}
+#define LCHK(L, expr)                                                                  \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return lane_fail(L, SPRAY_RT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_e));   \
+  } while (0)
+
+int lane_buf(spray_rt_lane* L, size_t bytes) {
+  if (L->cap >= bytes) return SPRAY_RT_OK;
+  if (L->d_buf) LCHK(L, hipFree(L->d_buf));
+  L->d_buf = nullptr;
+  L->cap = 0;
+  const size_t want = std::max<size_t>(bytes, size_t(1) << 16);
+  LCHK(L, hipMalloc(&L->d_buf, want));
+  L->cap = want;
+  return SPRAY_RT_OK;
+}
+
+// the context's tables, rebuilt under its lock when a load made them stale
+int lane_tables(spray_rt_lane* L) {
+  spray_rt_ctx* c = L->ctx;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->slots_dirty && !c->dom_dirty) return SPRAY_RT_OK;
+  const int r = prepare(c);
+  if (r) return lane_fail(L, r, "%s", c->err.c_str());
+  return SPRAY_RT_OK;
+}
+
+template <typename Launch>
+int lane_rtc(spray_rt_lane* L, int slot, void* rays, size_t M, size_t stride, Launch launch) {
+  if (!L) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = L->ctx;
+  if (stride < 80 || (stride & 3)) return lane_fail(L, SPRAY_RT_ERR_ARG, "bad stride %zu", stride);
+  if (M == 0) return SPRAY_RT_OK;
+  if (!rays) return lane_fail(L, SPRAY_RT_ERR_ARG, "null ray buffer");
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (slot < 0 || size_t(slot) >= c->slots.size() || !c->slots[slot].dmem)
+      return lane_fail(L, SPRAY_RT_ERR_ARG, "slot %d is not loaded", slot);
+  }
+  LCHK(L, hipSetDevice(c->device));
+  int r = lane_tables(L);
+  if (r) return r;
+  const size_t off[2] = {0, M};
+  LCHK(L, hipMemcpyAsync(L->d_seg_slot, &slot, sizeof(int), hipMemcpyHostToDevice, L->stream));
+  LCHK(L, hipMemcpyAsync(L->d_seg_off, off, sizeof(off), hipMemcpyHostToDevice, L->stream));
+  if (is_device_ptr(rays)) {
+    LCHK(L, launch(L->stream, c->d_slots, L->d_seg_slot, L->d_seg_off, 1, static_cast<char*>(rays),
+                   stride, M));
+    LCHK(L, hipStreamSynchronize(L->stream));
+    return SPRAY_RT_OK;
+  }
+  const size_t bytes = M * stride;
+  r = lane_buf(L, bytes);
+  if (r) return r;
+  LCHK(L, hipMemcpyAsync(L->d_buf, rays, bytes, hipMemcpyHostToDevice, L->stream));
+  LCHK(L, launch(L->stream, c->d_slots, L->d_seg_slot, L->d_seg_off, 1,
+                 static_cast<char*>(L->d_buf), stride, M));
+  LCHK(L, hipMemcpyAsync(rays, L->d_buf, bytes, hipMemcpyDeviceToHost, L->stream));
+  LCHK(L, hipStreamSynchronize(L->stream));
+  return SPRAY_RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int spray_rt_lane_create(spray_rt_ctx_t c, spray_rt_lane_t* out) {
+  if (!c || !out) return SPRAY_RT_ERR_ARG;
+  *out = nullptr;
+  HIPCHK(c, hipSetDevice(c->device));
+  spray_rt_lane* L = new (std::nothrow) spray_rt_lane;
+  if (!L) return SPRAY_RT_ERR_NOMEM;
+  L->ctx = c;
+  if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&L->d_seg_slot), 256) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&L->d_seg_off), 256) != hipSuccess) {
+    spray_rt_lane_destroy(L);
+    return fail(c, SPRAY_RT_ERR_HIP, "lane creation failed");
+  }
+  *out = L;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_lane_destroy(spray_rt_lane_t L) {
+  if (!L) return SPRAY_RT_ERR_ARG;
+  (void)hipSetDevice(L->ctx->device);
+  if (L->stream) (void)hipStreamSynchronize(L->stream);
+  if (L->d_buf) (void)hipFree(L->d_buf);
+  if (L->d_seg_slot) (void)hipFree(L->d_seg_slot);
+  if (L->d_seg_off) (void)hipFree(L->d_seg_off);
+  if (L->stream) (void)hipStreamDestroy(L->stream);
+  delete L;
+  return SPRAY_RT_OK;
+}
+
+const char* spray_rt_lane_last_error(spray_rt_lane_t L) {
+  return L ? L->err.c_str() : "null lane";
+}
+
+int spray_rt_lane_intersect1M(spray_rt_lane_t L, int slot, void* rays, size_t M, size_t stride) {
+  return lane_rtc(L, slot, rays, M, stride, launch_rtc_intersect);
+}
+
+int spray_rt_lane_occluded1M(spray_rt_lane_t L, int slot, void* rays, size_t M, size_t stride) {
+  return lane_rtc(L, slot, rays, M, stride, launch_rtc_occluded);
+}
+
+int spray_rt_lane_domains1M(spray_rt_lane_t L, const float* org, const float* dir, size_t M,
+                            int* ids, float* ts, int* counts, int maxhits) {
+  if (!L) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = L->ctx;
+  if (maxhits <= 0) return lane_fail(L, SPRAY_RT_ERR_ARG, "maxhits must be > 0");
+  if (c->ndom == 0) return lane_fail(L, SPRAY_RT_ERR_STATE, "no domain bounds set");
+  if (M == 0) return SPRAY_RT_OK;
+  if (!org || !dir || !ids || !ts || !counts) return lane_fail(L, SPRAY_RT_ERR_ARG, "null buffer");
+  LCHK(L, hipSetDevice(c->device));
+  int r = lane_tables(L);
+  if (r) return r;
+  if (is_device_ptr(org)) {
+    LCHK(L, launch_domains(L->stream, c->d_boxes, c->ndom, org, dir, M, ids, ts, counts, maxhits));
+    LCHK(L, hipStreamSynchronize(L->stream));
+    return SPRAY_RT_OK;
+  }
+  const size_t b_in = align256(3 * M * sizeof(float));
+  const size_t b_ids = align256(M * maxhits * sizeof(int));
+  const size_t b_cnt = align256(M * sizeof(int));
+  r = lane_buf(L, 2 * b_in + 2 * b_ids + b_cnt);
+  if (r) return r;
+  char* b = static_cast<char*>(L->d_buf);
+  float* d_org = reinterpret_cast<float*>(b);
+  float* d_dir = reinterpret_cast<float*>(b + b_in);
+  int* d_ids = reinterpret_cast<int*>(b + 2 * b_in);
+  float* d_ts = reinterpret_cast<float*>(b + 2 * b_in + b_ids);
+  int* d_cnt = reinterpret_cast<int*>(b + 2 * b_in + 2 * b_ids);
+  LCHK(L, hipMemcpyAsync(d_org, org, 3 * M * sizeof(float), hipMemcpyHostToDevice, L->stream));
+  LCHK(L, hipMemcpyAsync(d_dir, dir, 3 * M * sizeof(float), hipMemcpyHostToDevice, L->stream));
+  LCHK(L, launch_domains(L->stream, c->d_boxes, c->ndom, d_org, d_dir, M, d_ids, d_ts, d_cnt,
+                         maxhits));
+  LCHK(L, hipMemcpyAsync(ids, d_ids, M * maxhits * sizeof(int), hipMemcpyDeviceToHost, L->stream));
+  LCHK(L, hipMemcpyAsync(ts, d_ts, M * maxhits * sizeof(float), hipMemcpyDeviceToHost, L->stream));
+  LCHK(L, hipMemcpyAsync(counts, d_cnt, M * sizeof(int), hipMemcpyDeviceToHost, L->stream));
+  LCHK(L, hipStreamSynchronize(L->stream));
+  return SPRAY_RT_OK;
+}
+
 int spray_rt_domains1M(spray_rt_ctx_t c, const float* org, const float* dir,
                        size_t M, int* ids, float* ts, int* counts, int maxhits) {
   if (!c) return SPRAY_RT_ERR_ARG;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -81,6 +82,20 @@ struct spray_rt_ctx {
   void* d_frame = nullptr;  // render_tile path buffers
   size_t frame_cap = 0;
   unsigned long long* d_fstats = nullptr;  // render_tile totals (shade stats)
+  std::string err;
+  std::mutex mu;  // lanes: the lazy table rebuild (prepare) runs under it
+};
+
+// A per-host-thread submission lane of a context (spray_rt_lane_*): its own
+// stream, staging buffers and one-segment table, so concurrent threads never
+// share mutable state; they only read the context's device tables.
+struct spray_rt_lane {
+  spray_rt_ctx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  void* d_buf = nullptr;
+  size_t cap = 0;
+  int* d_seg_slot = nullptr;
+  size_t* d_seg_off = nullptr;
   std::string err;
 };
 

@@ -288,3 +288,20 @@ def test_quantized_nodes_contain_fp32_boxes(native, oracle, case):
         dhi = base + qh[live] * scale
         assert (dlo + scale <= lo32[live]).all()
         assert (dhi - scale >= hi32[live]).all()
+
+
+def test_scene_adapter_header_compiles():
+    """include/spray_scene.hpp (the SceneT drop-in) is self-contained C++17
+    over the C ABI: it compiles on its own, and the C++ caller test
+    (tests/cpp/scene_adapter_test.cpp) builds against it."""
+    import subprocess
+    inc = os.path.join(ROOT, "include")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I" + inc,
+                        "-x", "c++", "-"], input='#include "spray_scene.hpp"\n'
+                       "template class spray_amd::Scene<>;\nint main() { return 0; }\n",
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    src = os.path.join(ROOT, "tests", "cpp", "scene_adapter_test.cpp")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-fopenmp", "-Wall", "-I" + inc,
+                        "-I" + os.path.join(ROOT, "oracle"), src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
