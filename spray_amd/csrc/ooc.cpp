@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -38,9 +40,7 @@ struct CacheSlot {
   size_t bytes = 0;
   int domain = -1;
   uint64_t used = 0;                // LRU stamp
-  hipEvent_t ready = nullptr;       // upload done (upload stream)
-  hipEvent_t released = nullptr;    // last drain using it done (compute stream)
-  bool pending_release = false;
+  int released = -1;                // launch ring entry of its last drain, -1 none
 };
 
 }  // namespace
@@ -50,6 +50,7 @@ struct spray_rt_ooc {
   std::vector<HostDomain> dom;
   std::vector<CacheSlot> slot;
   hipStream_t up = nullptr;
+  hipEvent_t up_done = nullptr;  // a batch's uploads done (upload stream)
   uint64_t clock = 0;
   unsigned long long loads = 0, hits = 0, bytes = 0, drains = 0;
   // queue scratch
@@ -59,6 +60,18 @@ struct spray_rt_ooc {
   uint64_t* tie = nullptr;  // per-ray closest-hit key (kOocMissKey: none yet)
   size_t tie_cap = 0;
   std::vector<uint32_t> first;
+  std::vector<unsigned long long> score;  // DomainStats scores of the last queue build
+  // drain launches: one event per launch in a ring (slot reuse, error
+  // checks), the live-count snapshot the kernels publish (OocSnapshot:
+  // pinned, device-mapped, [0..255] counts, [256] sequence), the any-hit
+  // last-block counter
+  static constexpr int kRing = 16;
+  hipEvent_t launch_ev[kRing] = {};
+  unsigned long long launches = 0;
+  unsigned long long* snap = nullptr;
+  uint32_t gen = 0;
+  uint32_t* done = nullptr;  // any-hit last-block counter
+  unsigned long long skipped = 0;
 };
 
 namespace {
@@ -77,15 +90,17 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   M = std::max(M, o->q_rays);
   pairs = std::max(pairs, o->q.pair_cap);
   free_scratch(o);
-  const size_t temp = ooc_temp_bytes(M, pairs);
+  const size_t rblk = (M + kBlock - 1) / kBlock;  // ray blocks
+  const size_t nblk = rblk * size_t(64 * W);
+  const size_t nchk = (rblk + kOocChunk - 1) / kOocChunk * size_t(64 * W);
   const size_t b_masks = align256(M * W * sizeof(uint64_t));
-  const size_t b_cnt = align256((M + 1) * sizeof(uint32_t));
-  const size_t b_k = align256(pairs * sizeof(uint16_t));
   const size_t b_v = align256(pairs * sizeof(uint32_t));
-  const size_t b_first = align256(257 * sizeof(uint32_t));
   const size_t b_pk = align256(pairs * sizeof(uint64_t));
-  const size_t total =
-      b_masks + 2 * b_cnt + 2 * b_k + 3 * b_v + b_pk + b_first + align256(temp);
+  const size_t b_blk = align256(nblk * sizeof(uint32_t));
+  const size_t b_dom = align256(257 * sizeof(uint32_t));
+  const size_t b_score = align256(256 * sizeof(unsigned long long));
+  const size_t b_ch = align256(nchk * sizeof(uint32_t));
+  const size_t total = b_masks + 2 * b_v + b_pk + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score;
   HIPCHK(c, hipMalloc(&o->q_mem, total));
   char* p = static_cast<char*>(o->q_mem);
   auto take = [&](size_t n) {
@@ -94,48 +109,53 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
     return r;
   };
   o->q.masks = reinterpret_cast<uint64_t*>(take(b_masks));
-  o->q.npairs = reinterpret_cast<uint32_t*>(take(b_cnt));
-  o->q.poff = reinterpret_cast<uint32_t*>(take(b_cnt));
-  o->q.key_in = reinterpret_cast<uint16_t*>(take(b_k));
-  o->q.key_out = reinterpret_cast<uint16_t*>(take(b_k));
-  o->q.val_in = reinterpret_cast<uint32_t*>(take(b_v));
-  o->q.val_out = reinterpret_cast<uint32_t*>(take(b_v));
-  o->q.first = reinterpret_cast<uint32_t*>(take(b_first));
-  o->q.pkey = reinterpret_cast<uint64_t*>(take(b_pk));
+  o->q.val = reinterpret_cast<uint32_t*>(take(b_v));
   o->q.pleaf = reinterpret_cast<uint32_t*>(take(b_v));
-  o->q.temp = take(align256(temp));
-  o->q.temp_bytes = temp;
+  o->q.pkey = reinterpret_cast<uint64_t*>(take(b_pk));
+  o->q.bc = reinterpret_cast<uint32_t*>(take(b_blk));
+  o->q.sb = reinterpret_cast<uint32_t*>(take(b_blk));
+  o->q.off = reinterpret_cast<uint32_t*>(take(b_blk));
+  o->q.first = reinterpret_cast<uint32_t*>(take(b_dom));
+  o->q.live = reinterpret_cast<uint32_t*>(take(b_dom));
+  o->q.csum = reinterpret_cast<uint32_t*>(take(b_ch));
+  o->q.cw = reinterpret_cast<uint32_t*>(take(b_ch));
+  o->q.score = reinterpret_cast<unsigned long long*>(take(b_score));
+  o->q.block_cap = nblk;
+  o->q.chunk_cap = nchk;
   o->q.pair_cap = pairs;
   o->q_rays = M;
   return SPRAY_RT_OK;
 }
 
 // Queues of a ray batch: o->first[d] .. o->first[d+1] index q.val_out.
-int build_queues(spray_rt_ooc* o, const spray_rt_ray* rays, const uint8_t* valid, size_t M) {
+// key_init / occ_clear: the pass's per-ray results to reset (may be null).
+int build_queues(spray_rt_ooc* o, const spray_rt_ray* rays, const uint8_t* valid, size_t M,
+                 uint64_t* key_init, uint8_t* occ_clear) {
   spray_rt_ctx* c = o->ctx;
   const int W = c->ndom <= 64 ? 1 : 4;
   int r = size_scratch(o, M, std::max<size_t>(M * 2, 1 << 16), W);
   if (r) return r;
   o->first.assign(c->ndom + 1, 0);
+  o->score.assign(c->ndom, 0);
   hipStream_t s = stream_of(c);
-  hipError_t e = launch_ooc_queues(s, c->d_tlas, c->ntlas, c->ndom, rays, valid, M, o->q,
-                                   o->first.data());
+  hipError_t e = launch_ooc_queues(s, c->d_tlas, c->ntlas, c->ndom, c->d_boxes, rays, valid, M,
+                                   o->q, key_init, occ_clear, o->first.data(), o->score.data());
   if (e == hipErrorOutOfMemory) {  // more pairs than guessed: grow, redo
     (void)hipGetLastError();
     r = size_scratch(o, M, o->q.npair, W);
     if (r) return r;
-    e = launch_ooc_queues(s, c->d_tlas, c->ntlas, c->ndom, rays, valid, M, o->q,
-                          o->first.data());
+    e = launch_ooc_queues(s, c->d_tlas, c->ntlas, c->ndom, c->d_boxes, rays, valid, M, o->q,
+                          key_init, occ_clear, o->first.data(), o->score.data());
   }
   HIPCHK(c, e);
   return SPRAY_RT_OK;
 }
 
-// Makes domain d resident (LruCache::load) and returns its slot; the compute
-// stream is made to wait for the upload.
-int acquire(spray_rt_ooc* o, int d, int* out) {
+// Makes domain d resident (LruCache::load) and returns its slot.  A miss
+// queues the upload on the upload stream after the slot's last drain;
+// *uploaded tells the caller to make the compute stream wait for it.
+int acquire(spray_rt_ooc* o, int d, int* out, bool* uploaded) {
   spray_rt_ctx* c = o->ctx;
-  hipStream_t s = stream_of(c);
   int best = -1;
   for (size_t k = 0; k < o->slot.size(); ++k)
     if (o->slot[k].domain == d) best = int(k);
@@ -154,22 +174,21 @@ int acquire(spray_rt_ooc* o, int d, int* out) {
     const HostDomain& hd = o->dom[d];
     const size_t n = hd.nbytes;
     if (cs.bytes < n) {  // grow: wait for the slot's readers, reallocate
-      if (cs.pending_release) HIPCHK(c, hipEventSynchronize(cs.released));
+      if (cs.released >= 0) HIPCHK(c, hipEventSynchronize(o->launch_ev[cs.released]));
       if (cs.dmem) HIPCHK(c, hipFree(cs.dmem));
       cs.dmem = nullptr;
       HIPCHK(c, hipMalloc(&cs.dmem, n));
       cs.bytes = n;
     }
-    if (cs.pending_release) HIPCHK(c, hipStreamWaitEvent(o->up, cs.released, 0));
+    // a ring entry re-recorded by a later launch only makes this wait longer
+    if (cs.released >= 0) HIPCHK(c, hipStreamWaitEvent(o->up, o->launch_ev[cs.released], 0));
     HIPCHK(c, hipMemcpyAsync(cs.dmem, hd.pinned, n, hipMemcpyHostToDevice, o->up));
-    HIPCHK(c, hipEventRecord(cs.ready, o->up));
     cs.domain = d;
     ++o->loads;
     o->bytes += n;
+    *uploaded = true;
   }
-  CacheSlot& cs = o->slot[best];
-  cs.used = ++o->clock;
-  HIPCHK(c, hipStreamWaitEvent(s, cs.ready, 0));
+  o->slot[best].used = ++o->clock;
   *out = best;
   return SPRAY_RT_OK;
 }
@@ -189,44 +208,117 @@ OocDomain domain_view(const spray_rt_ooc* o, int d, int k, const float* boxes) {
   return D;
 }
 
-// Drains every non-empty queue, ascending or descending domain order (a
-// closest-hit pass followed by a reversed any-hit pass reuses the domains
-// left resident by the first), max(1, slots / 2) resident domains per
-// launch: while one batch drains, the LRU victims of the next are the
+// Drains the queues in the reference's DomainStats order
+// (ooc_pcontext.h:128-132: rstats_.schedule(), highest score first;
+// ooc_domain_stats.cc:60-111), the any-hit pass starting with the domains
+// the closest-hit pass left resident.  max(1, slots / 2) resident domains
+// per launch: while one batch drains, the LRU victims of the next are the
 // previous batch's slots, so its uploads overlap the drain.
+//
+// A queue with no live pair left (q.live, see k_ooc_ch_batch: every queued
+// ray already has a hit nearer than the domain's entry t, or is occluded) is
+// skipped, domain load included -- the reference filters the same rays out
+// of the queue when it drains it (filterRqs / filterSqs,
+// ooc_tcontext.inl:138-170) and the sweep visits domains near the camera
+// first, so most far domains die this way.  Each launch publishes its
+// counts to pinned host memory from the device (OocSnapshot); before
+// choosing batch k + 1 the host waits for launch k - 1's snapshot, which
+// has landed by the time launch k runs, so the compute stream always holds
+// the next launch.  Counts only fall, so a queue seen dead is dead for
+// certain and results equal draining everything.  (A second compute stream
+// alternating batches measured no faster with the 4-slot cache of
+// configs[3]: at most two batches' domains are resident at once.)
 template <typename Launch>
-int drain(spray_rt_ooc* o, bool reverse, const std::vector<float>& boxes, Launch launch) {
+int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch launch) {
   spray_rt_ctx* c = o->ctx;
   hipStream_t s = stream_of(c);
   const int n = c->ndom;
   const int per = std::max(1, std::min<int>(kOocBatch, int(o->slot.size()) / 2));
-  OocBatch B{};
-  int bslot[kOocBatch];
-  auto flush = [&]() -> int {
-    if (B.count == 0) return SPRAY_RT_OK;
-    HIPCHK(c, launch(s, B));
-    for (int k = 0; k < B.count; ++k) {
-      HIPCHK(c, hipEventRecord(o->slot[bslot[k]].released, s));
-      o->slot[bslot[k]].pending_release = true;
+  std::vector<int> order;
+  std::vector<uint32_t> live(n, 0);
+  for (int d = 0; d < n; ++d) {
+    live[d] = o->first[d + 1] - o->first[d];
+    if (live[d] && o->dom[d].set && o->dom[d].img.nnodes) order.push_back(d);
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return o->score[a] > o->score[b];  // ties: ascending id
+  });
+  if (any_hit)  // reuse what the closest-hit pass left resident
+    std::stable_partition(order.begin(), order.end(), [&](int d) {
+      for (const CacheSlot& cs : o->slot)
+        if (cs.domain == d) return true;
+      return false;
+    });
+  OocSnapshot S{o->snap, o->snap + 256, ++o->gen, 0};
+  volatile unsigned long long* snap = o->snap;
+  const unsigned long long g = (unsigned long long)S.gen << 32;
+  // waits for launch `k` of this pass (0-based) to publish (or complete),
+  // then folds the newest counts in
+  auto absorb = [&](uint32_t k, int ring) -> int {
+    for (unsigned spins = 0; snap[256] < g + k + 1; ++spins) {
+      if ((spins & 1023) == 1023) {  // also watch the launch itself (errors)
+        const hipError_t e = hipEventQuery(o->launch_ev[ring]);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) HIPCHK(c, e);
+      }
     }
-    o->drains += B.count;  // domain queues drained
-    B.count = 0;
+    for (int d = 0; d < n; ++d) {
+      const unsigned long long v = snap[d];
+      if ((v >> 32) == S.gen) live[d] = std::min(live[d], uint32_t(v));
+    }
     return SPRAY_RT_OK;
   };
-  for (int k = 0; k < n; ++k) {
-    const int d = reverse ? n - 1 - k : k;
-    const uint32_t b = o->first[d], e = o->first[d + 1];
-    if (e <= b || !o->dom[d].set || !o->dom[d].img.nnodes) continue;
-    int sl = -1;
-    int r = acquire(o, d, &sl);
-    if (r) return r;
-    B.d[B.count] = domain_view(o, d, sl, boxes.data());
-    B.begin[B.count] = b;
-    B.n[B.count] = e - b;
-    bslot[B.count] = sl;
-    if (++B.count == per && (r = flush())) return r;
+  std::vector<char> done(n, 0);
+  int r = SPRAY_RT_OK, prev_ring = -1;
+  static const bool trace = std::getenv("SPRAY_OOC_TRACE") != nullptr;  // schedule log
+  if (trace)
+    std::fprintf(stderr, "ooc pass %s: %zu queues, %u pairs\n", any_hit ? "any" : "closest",
+                 order.size(), o->first[n]);
+  for (;;) {
+    // the next batch: the first `per` undone queues not known dead
+    OocBatch B{};
+    int bslot[kOocBatch];
+    bool uploaded = false;
+    for (int d : order) {
+      if (done[d]) continue;
+      if (live[d] == 0) {
+        done[d] = 1;
+        ++o->skipped;
+        continue;
+      }
+      int sl = -1;
+      if ((r = acquire(o, d, &sl, &uploaded))) return r;
+      B.d[B.count] = domain_view(o, d, sl, boxes.data());
+      B.begin[B.count] = o->first[d];
+      B.n[B.count] = o->first[d + 1] - o->first[d];
+      bslot[B.count] = sl;
+      if (++B.count == per) break;
+    }
+    if (B.count == 0) break;
+    const int ring = int(o->launches++ % spray_rt_ooc::kRing);
+    if (uploaded) {  // one wait for all of the batch's uploads
+      HIPCHK(c, hipEventRecord(o->up_done, o->up));
+      HIPCHK(c, hipStreamWaitEvent(s, o->up_done, 0));
+    }
+    if (trace) {
+      std::fprintf(stderr, "  launch %u:", S.launch);
+      for (int k = 0; k < B.count; ++k)
+        std::fprintf(stderr, " d%d q%u live%u score%llu", B.d[k].domain, B.n[k],
+                     live[B.d[k].domain], o->score[B.d[k].domain]);
+      std::fprintf(stderr, "%s\n", uploaded ? " (upload)" : "");
+    }
+    HIPCHK(c, launch(s, B, S));
+    HIPCHK(c, hipEventRecord(o->launch_ev[ring], s));
+    for (int k = 0; k < B.count; ++k) {
+      done[B.d[k].domain] = 1;
+      o->slot[bslot[k]].released = ring;
+    }
+    o->drains += B.count;
+    if (S.launch > 0 && (r = absorb(S.launch - 1, prev_ring))) return r;
+    ++S.launch;
+    prev_ring = ring;
   }
-  return flush();
+  return SPRAY_RT_OK;
 }
 
 int check_batch(spray_rt_ooc* o, const void* rays, size_t M, const void* out) {
@@ -260,10 +352,15 @@ int spray_rt_ooc_create(spray_rt_ctx_t c, int cache_slots, spray_rt_ooc_t* out) 
   o->dom.resize(c->ndom);
   o->slot.resize(cache_slots);
   hipError_t e = hipStreamCreateWithFlags(&o->up, hipStreamNonBlocking);
-  for (CacheSlot& s : o->slot) {
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ready, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.released, hipEventDisableTiming);
-  }
+  if (e == hipSuccess)  // fine-grained: device stores reach the host while kernels run
+    e = hipHostMalloc(reinterpret_cast<void**>(&o->snap), 257 * sizeof(unsigned long long),
+                      hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) std::memset(o->snap, 0, 257 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&o->done), sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(o->done, 0, sizeof(uint32_t));
+  for (int k = 0; k < spray_rt_ooc::kRing && e == hipSuccess; ++k)
+    e = hipEventCreateWithFlags(&o->launch_ev[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&o->up_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     spray_rt_ooc_destroy(o);
     return fail(c, SPRAY_RT_ERR_HIP, "ooc setup: %s", hipGetErrorString(e));
@@ -278,13 +375,16 @@ int spray_rt_ooc_destroy(spray_rt_ooc_t o) {
   (void)hipDeviceSynchronize();
   for (CacheSlot& s : o->slot) {
     if (s.dmem) (void)hipFree(s.dmem);
-    if (s.ready) (void)hipEventDestroy(s.ready);
-    if (s.released) (void)hipEventDestroy(s.released);
   }
   for (HostDomain& d : o->dom)
     if (d.pinned) (void)hipHostFree(d.pinned);
   free_scratch(o);
   if (o->tie) (void)hipFree(o->tie);
+  if (o->snap) (void)hipHostFree(o->snap);
+  if (o->up_done) (void)hipEventDestroy(o->up_done);
+  if (o->done) (void)hipFree(o->done);
+  for (hipEvent_t ev : o->launch_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (o->up) (void)hipStreamDestroy(o->up);
   delete o;
   return SPRAY_RT_OK;
@@ -333,14 +433,15 @@ int spray_rt_ooc_intersect(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
     o->tie_cap = M;
   }
   const std::vector<float>& boxes = c->h_boxes;
-  if ((r = build_queues(o, rays, nullptr, M))) return r;
-  HIPCHK(c, launch_ooc_init(stream_of(c), hits, o->tie, M));
   uint64_t* key = o->tie;
+  if ((r = build_queues(o, rays, nullptr, M, key, nullptr))) return r;
   const int W = c->ndom <= 64 ? 1 : 4;
-  return drain(o, false, boxes, [&](hipStream_t s, const OocBatch& B) {
-    return launch_ooc_ch_batch(s, B, W, rays, o->q.val_out, o->q.masks, c->d_boxes, key,
-                               o->q.pkey, o->q.pleaf, hits);
+  r = drain(o, false, boxes, [&](hipStream_t s, const OocBatch& B, const OocSnapshot& S) {
+    return launch_ooc_ch_batch(s, B, W, rays, o->q, c->d_boxes, key, hits, S);
   });
+  if (r) return r;
+  HIPCHK(c, launch_ooc_finish(stream_of(c), key, hits, M));
+  return SPRAY_RT_OK;
 }
 
 int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
@@ -352,10 +453,10 @@ int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
   if (valid && !is_device_ptr(valid))
     return fail(c, SPRAY_RT_ERR_ARG, "valid must be device memory");
   const std::vector<float>& boxes = c->h_boxes;
-  if ((r = build_queues(o, rays, valid, M))) return r;
-  HIPCHK(c, launch_ooc_clear_occ(stream_of(c), valid, occluded, M));
-  return drain(o, true, boxes, [&](hipStream_t s, const OocBatch& B) {
-    return launch_ooc_ah_batch(s, B, rays, o->q.val_out, occluded);
+  if ((r = build_queues(o, rays, valid, M, nullptr, occluded))) return r;
+  const int W = c->ndom <= 64 ? 1 : 4;
+  return drain(o, true, boxes, [&](hipStream_t s, const OocBatch& B, const OocSnapshot& S) {
+    return launch_ooc_ah_batch(s, B, W, rays, o->q, occluded, o->done, S);
   });
 }
 

@@ -3,16 +3,14 @@
 // The reference's ooc tracer queues every ray to every domain on its sorted
 // domain list (ooc_isector.h:116-174) and drains one resident domain at a
 // time (ooc_tcontext.inl:28-101) while the LRU cache streams the next ones
-// in (lru_cache.cc:65-171).  On the GPU the queues are built in bulk --
-// domain masks, (domain, ray) pairs, one stable radix sort -- and each
-// batch of resident domains drains its queues in one launch.  A ray's
-// closest hit is combined across domains by the order of the sequential
-// walk of its domain list, (t, then the list position), so the result is
-// the whole-scene one whatever the drain order.
+// in (lru_cache.cc:65-171).  On the GPU the queues are built in bulk -- one
+// pass over the rays computes the domain lists, the queue lengths and the
+// DomainStats scores, a one-block scan places the queues, a second pass
+// scatters the ray ids -- and each batch of resident domains drains its
+// queues in one launch.  A ray's closest hit is combined across domains by
+// the order of the sequential walk of its domain list, (t, then the list
+// position), so the result is the whole-scene one whatever the drain order.
 #include <hip/hip_runtime.h>
-
-#include <hipcub/device/device_radix_sort.hpp>
-#include <hipcub/device/device_scan.hpp>
 
 #include "rt_device.h"
 #include "rt_kernels.h"
@@ -20,82 +18,327 @@
 namespace spray_rt {
 namespace {
 
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_ooc_masks(
-    const BvhNode* __restrict__ tlas, int ntlas, const spray_rt_ray* __restrict__ rays,
-    const uint8_t* __restrict__ valid, size_t M, uint64_t* __restrict__ masks,
-    uint32_t* __restrict__ npairs) {
-  __shared__ int32_t wstack[(kBlock / 64) * kStack];
-  __shared__ float4 stl[4 * 64 * W];
-  for (int k = threadIdx.x; k < 4 * ntlas; k += kBlock) stl[k] = ld4(tlas, k);
-  __syncthreads();
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= M) return;
-  uint64_t m[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) m[w] = 0;
-  if (!valid || valid[i]) {
-    const float4* rp = reinterpret_cast<const float4*>(rays + i);
-    const float4 o4 = rp[0], d4 = rp[1];
-    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-    tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+  for (int off = 32; off > 0; off >>= 1) {
+    lo |= __shfl_xor(lo, off);
+    hi |= __shfl_xor(hi, off);
   }
-  uint32_t n = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    masks[i * W + w] = m[w];
-    n += __popcll(m[w]);
-  }
-  npairs[i] = n;
+  return (uint64_t(hi) << 32) | lo;
 }
 
-// (domain, ray) pair j of ray i at off[i] + k, in ascending domain order
+__device__ __forceinline__ uint64_t lanes_below() {
+  const uint32_t l = threadIdx.x & 63;
+  return l ? (~0ull >> (64 - l)) : 0ull;
+}
+
+// Position of domain `dom` (entry t `tb`) in the ray's sorted domain list
+// (ascending (intersectAabb entry t, id), rays.h:71-79): the tie-break of
+// the key and the DomainStats weight.
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_ooc_pairs(const uint64_t* __restrict__ masks,
-                                                      const uint32_t* __restrict__ off,
-                                                      size_t M, uint16_t* __restrict__ key,
-                                                      uint32_t* __restrict__ val) {
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= M) return;
-  uint32_t o = off[i];
+__device__ __forceinline__ uint32_t list_pos(const uint64_t* m, const float* boxes, int dom,
+                                             float tb, const DRay& dr) {
+  uint32_t p = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) {
-    uint64_t bits = masks[i * W + w];
+    uint64_t bits = m[w];
     while (bits) {
       const int j = __ffsll((long long)bits) - 1;
       bits &= bits - 1;
-      key[o] = uint16_t(64 * w + j);
-      val[o] = uint32_t(i);
-      ++o;
+      const int b = 64 * w + j;
+      float tm;
+      aabb_ref(boxes + 6 * b, dr, tm);
+      if (tm < tb || (tm == tb && b < dom)) ++p;
     }
   }
+  return p;
 }
 
-// queue bounds: first[d] = first position of domain d in the sorted keys
-__global__ void k_ooc_bounds(const uint16_t* __restrict__ key, uint32_t n, int ndom,
-                             uint32_t* __restrict__ first) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d > ndom) return;
-  uint32_t lo = 0, hi = n;  // lower_bound(d)
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (int(key[mid]) < d)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  first[d] = lo;
-}
+// Confirmed domains a lane keeps in LDS for its list positions (longer
+// lists recompute positions from the mask).
+constexpr int kLaneList = 8;
 
-__global__ __launch_bounds__(kBlock) void k_ooc_init(spray_rt_hit* __restrict__ hits,
-                                                     uint64_t* __restrict__ key, size_t M) {
+// Pass 1 over the rays.  The ray's domain list (ooc_isector.h:116-174: the
+// domains whose box intersectAabb hits): the conservative top-level walk,
+// each candidate then confirmed by the reference's box test (boxes staged
+// in LDS).  Per block and domain: queued pairs (bc) and DomainStats::
+// increment weights (sb; ooc_domain_stats.cc:60-111: SPRAY_RAY_DOMAIN_
+// LIST_SIZE - list position, 1 past the list), summed in LDS, then stored
+// block-major ([block * ndom + d], one coalesced row per block).  Also
+// resets the per-ray results of the pass.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_ooc_masks(
+    const BvhNode* __restrict__ tlas, int ntlas, const float* __restrict__ boxes, int ndom,
+    const spray_rt_ray* __restrict__ rays, const uint8_t* __restrict__ valid, size_t M,
+    uint64_t* __restrict__ masks, uint64_t* __restrict__ key_init,
+    uint8_t* __restrict__ occ_clear, uint32_t* __restrict__ bc, uint32_t* __restrict__ sb) {
+  __shared__ int32_t wstack[kWaves * kStack];
+  __shared__ float4 stl[4 * 64 * W];
+  __shared__ float sbox[6 * 64 * W];
+  __shared__ uint32_t cnt[64 * W], sc[64 * W];
+  __shared__ float lte[kLaneList][kBlock];
+  __shared__ int lid[kLaneList][kBlock];
+  for (int q = threadIdx.x; q < 4 * ntlas; q += kBlock) stl[q] = ld4(tlas, q);
+  for (int q = threadIdx.x; q < 6 * ndom; q += kBlock) sbox[q] = boxes[q];
+  for (int q = threadIdx.x; q < 64 * W; q += kBlock) cnt[q] = sc[q] = 0;
+  __syncthreads();
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= M) return;
-  float4* hp = reinterpret_cast<float4*>(hits + i);
-  hp[0] = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
-  hp[1] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
-  hp[2] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-  key[i] = kOocMissKey;
+  const bool in = i < M;
+  const bool live = in && (!valid || valid[i]);
+  uint64_t m[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+  if (live) {
+    const float4* rp = reinterpret_cast<const float4*>(rays + i);
+    o4 = rp[0];
+    d4 = rp[1];
+    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
+  }
+  // confirm; the confirmed entry t's go to the lane's LDS list
+  uint32_t k = 0;
+  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  if (live) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint64_t bits = m[w];
+      while (bits) {
+        const int j = __ffsll((long long)bits) - 1;
+        bits &= bits - 1;
+        float te;
+        if (aabb_ref(sbox + 6 * (64 * w + j), dr, te)) {
+          if (k < kLaneList) {
+            lte[k][threadIdx.x] = te;
+            lid[k][threadIdx.x] = 64 * w + j;
+          }
+          ++k;
+        } else {
+          m[w] &= ~(1ull << j);
+        }
+      }
+    }
+  }
+  // list position of each confirmed domain = its rank by (entry t, id); the
+  // weight goes into the entry's upper half
+  if (k <= kLaneList)
+    for (uint32_t a = 0; a < k; ++a) {
+      const float ta = lte[a][threadIdx.x];
+      const int da = lid[a][threadIdx.x] & 0xFFFF;
+      uint32_t pos = 0;
+      for (uint32_t b = 0; b < k; ++b) {
+        const float tb = lte[b][threadIdx.x];
+        pos += (tb < ta || (tb == ta && (lid[b][threadIdx.x] & 0xFFFF) < da)) ? 1u : 0u;
+      }
+      lid[a][threadIdx.x] = da | int((pos < kDomainListSize ? kDomainListSize - pos : 1u) << 16);
+    }
+  // per domain of the wave: pairs and weights summed over the wave first
+  // (a wave's rays mostly share domains: same-address LDS atomics serialise)
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t u = wave_or64(m[w]);
+    while (u) {
+      const int j = __ffsll((long long)u) - 1;
+      u &= u - 1;
+      const int dom = 64 * w + j;
+      const bool has = (m[w] >> j) & 1;
+      uint32_t add = 0;
+      if (has) {
+        if (k <= kLaneList) {
+          for (uint32_t a = 0; a < k; ++a) {
+            const int e = lid[a][threadIdx.x];
+            if ((e & 0xFFFF) == dom) add = uint32_t(e) >> 16;
+          }
+        } else {  // long list: the position from the mask
+          float te;
+          aabb_ref(sbox + 6 * dom, dr, te);
+          const uint32_t pos = list_pos<W>(m, sbox, dom, te, dr);
+          add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
+        }
+      }
+      const uint32_t n = uint32_t(__popcll(__ballot(has)));
+      for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o);
+      if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&cnt[dom], n);
+        atomicAdd(&sc[dom], add);
+      }
+    }
+  }
+  if (in) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) masks[i * W + w] = m[w];
+    if (key_init) key_init[i] = kOocMissKey;
+    if (occ_clear && live) occ_clear[i] = 0;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < ndom; q += kBlock) {
+    bc[size_t(blockIdx.x) * ndom + q] = cnt[q];
+    sb[size_t(blockIdx.x) * ndom + q] = sc[q];
+  }
+}
+
+// The per-block counts of one domain form a column of bc; columns are cut
+// into chunks of kOocChunk ray blocks, one 1024-thread block per (domain,
+// chunk).  Pass a: chunk sums of counts and DomainStats weights; pass b:
+// each chunk's exclusive scan from the sum of the chunks before it (off,
+// domain-major: a ray block's place in its queue); then one block folds
+// the chunk sums into queue lengths, scores and queue starts.
+constexpr int kScanBlock = 1024;
+
+
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int w = 0; w < kScanBlock / 64; ++w) t += red[w];
+  return t;
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_ooc_chunk_sums(
+    const uint32_t* __restrict__ bc, const uint32_t* __restrict__ sb, uint32_t nb, int ndom,
+    uint32_t* __restrict__ csum, uint32_t* __restrict__ cw) {
+  __shared__ uint32_t red[2][kScanBlock / 64];
+  const int d = blockIdx.x, c = blockIdx.y;
+  uint32_t v = 0, w = 0;
+  const uint32_t end = nb < (c + 1) * kOocChunk ? nb : (c + 1) * kOocChunk;
+  for (uint32_t b = c * kOocChunk + threadIdx.x; b < end; b += kScanBlock) {
+    v += bc[size_t(b) * ndom + d];
+    w += sb[size_t(b) * ndom + d];
+  }
+  const uint32_t tv = block_sum_u32(v, red[0]);
+  const uint32_t tw = block_sum_u32(w, red[1]);
+  if (threadIdx.x == 0) {
+    csum[size_t(d) * gridDim.y + c] = tv;
+    cw[size_t(d) * gridDim.y + c] = tw;
+  }
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_ooc_chunk_scan(
+    const uint32_t* __restrict__ bc, const uint32_t* __restrict__ csum, uint32_t nb, int ndom,
+    uint32_t* __restrict__ off) {
+  constexpr int kW = kScanBlock / 64;
+  __shared__ uint32_t wsum[kW];
+  __shared__ uint32_t carry;
+  const int d = blockIdx.x, c = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int q = 0; q < c; ++q) t += csum[size_t(d) * gridDim.y + q];
+    carry = t;
+  }
+  __syncthreads();
+  const uint32_t end = nb < (c + 1) * kOocChunk ? nb : (c + 1) * kOocChunk;
+  for (uint32_t b0 = c * kOocChunk; b0 < end; b0 += kScanBlock) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < end ? bc[size_t(b) * ndom + d] : 0u;
+    uint32_t incl = v;  // inclusive scan within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(incl, o);
+      if (lane >= o) incl += x;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = carry;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    if (b < end) off[size_t(d) * nb + b] = before + incl - v;
+    __syncthreads();
+    if (threadIdx.x == kScanBlock - 1) carry = before + incl;
+    __syncthreads();
+  }
+}
+
+// Queue bounds (one block): lengths and scores from the chunk sums, first =
+// their exclusive scan; every pair starts live.
+__global__ __launch_bounds__(256) void k_ooc_first(const uint32_t* __restrict__ csum,
+                                                   const uint32_t* __restrict__ cw, int nch,
+                                                   int ndom, uint32_t* __restrict__ first,
+                                                   uint32_t* __restrict__ live,
+                                                   unsigned long long* __restrict__ score) {
+  __shared__ uint32_t sh[256];
+  const int t = threadIdx.x;
+  uint32_t v = 0;
+  if (t < ndom) {
+    unsigned long long w = 0;
+    for (int q = 0; q < nch; ++q) {
+      v += csum[size_t(t) * nch + q];
+      w += cw[size_t(t) * nch + q];
+    }
+    score[t] = w;
+  }
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint32_t x = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  if (t < ndom) {
+    first[t] = sh[t] - v;
+    live[t] = v;
+  }
+  if (t == ndom - 1) first[ndom] = sh[t];
+}
+
+// Pass 2: ray i's id into the queue of every domain on its list, at its
+// block's scanned offset plus its rank among the block's rays of that
+// domain: every queue holds its rays in ascending order (packets of
+// neighbouring rays), the same order every run.  Positions past cap are
+// dropped (the host sees the total and grows).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_ooc_scatter(
+    const uint64_t* __restrict__ masks, size_t M, const uint32_t* __restrict__ first,
+    const uint32_t* __restrict__ off, uint32_t* __restrict__ val, size_t cap) {
+  __shared__ uint32_t wc[kWaves][64 * W];
+  for (int k = threadIdx.x; k < kWaves * 64 * W; k += kBlock) (&wc[0][0])[k] = 0;
+  __syncthreads();
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int wave = threadIdx.x >> 6;
+  uint64_t m[W], u[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    m[w] = i < M ? masks[i * W + w] : 0ull;
+    u[w] = wave_or64(m[w]);
+  }
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t bits = u[w];
+    while (bits) {
+      const int j = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      const uint64_t b = __ballot((m[w] >> j) & 1);
+      if ((threadIdx.x & 63) == 0) wc[wave][64 * w + j] = uint32_t(__popcll(b));
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 64 * W; k += kBlock) {  // exclusive over the waves
+    uint32_t run = 0;
+    for (int v = 0; v < kWaves; ++v) {
+      const uint32_t c = wc[v][k];
+      wc[v][k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t bits = u[w];
+    while (bits) {
+      const int j = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      const bool has = (m[w] >> j) & 1;
+      const uint64_t b = __ballot(has);
+      if (has) {
+        const int dom = 64 * w + j;
+        const size_t pos = size_t(first[dom]) + off[size_t(dom) * gridDim.x + blockIdx.x] +
+                           wc[wave][dom] + uint32_t(__popcll(b & lanes_below()));
+        if (pos < cap) val[pos] = uint32_t(i);
+      }
+    }
+  }
 }
 
 // The pair handled by this lane of a batch launch: the waves of segment s
@@ -113,49 +356,66 @@ __device__ __forceinline__ int batch_pair(const OocBatch& B, uint32_t& pj, bool&
   return s;
 }
 
-// Position of domain `dom` in the ray's sorted domain list (ascending
-// (intersectAabb entry t, id), rays.h:71-79): the tie-break of the key.
+// Liveness bookkeeping of the drains: live[d] counts the pairs of domain d's
+// queue that can still change a result -- closest hit: the domain's entry t
+// is not beyond the ray's best t (filterRqs, ooc_tcontext.inl:147: tdom <=
+// the ray's t); any hit: the ray is not occluded yet (filterSqs, :165).  It
+// starts at the queue length; a ray whose best t drops from `to` to `tn`
+// kills exactly its pairs with entry t in (tn, to], and a ray's first
+// occlusion kills all of its pairs, so each pair is counted down once.  Per
+// block the deaths are summed in LDS, one global atomic per domain.
 template <int W>
-__device__ __forceinline__ uint32_t list_pos(const uint64_t* m, const float* boxes, int dom,
-                                             const DRay& dr) {
-  float tb;
-  aabb_ref(boxes + 6 * dom, dr, tb);
-  uint32_t p = 0;
+__device__ __forceinline__ void count_deaths(const uint64_t* m, const float* boxes,
+                                             const DRay& dr, float tn, float to,
+                                             uint32_t* dead) {
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     uint64_t bits = m[w];
     while (bits) {
       const int j = __ffsll((long long)bits) - 1;
       bits &= bits - 1;
-      const int b = 64 * w + j;
-      float tm;
-      aabb_ref(boxes + 6 * b, dr, tm);
-      if (tm < tb || (tm == tb && b < dom)) ++p;
+      float te;
+      if (aabb_ref(boxes + 6 * (64 * w + j), dr, te) && te > tn && !(te > to))
+        atomicAdd(dead + 64 * w + j, 1u);
     }
   }
-  return p;
+}
+
+template <int W>
+__device__ __forceinline__ void flush_deaths(const uint32_t* dead, uint32_t* live) {
+  __syncthreads();
+  for (int k = threadIdx.x; k < 64 * W; k += kBlock)
+    if (dead[k]) atomicSub(live + k, dead[k]);
+}
+
+// The live counts to the host (OocSnapshot): values, then the sequence
+// number with system-scope release.  One block; every live atomic of the
+// launch is complete.
+__device__ __forceinline__ void write_snapshot(const uint32_t* live, const OocSnapshot& S,
+                                               int ndom) {
+  const unsigned long long g = (unsigned long long)S.gen << 32;
+  for (int k = threadIdx.x; k < ndom; k += blockDim.x)
+    S.snap[k] = g | __hip_atomic_load(live + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(S.seq, g | (S.launch + 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Closest hit of the rays queued to up to kOocBatch resident domains in one
-// launch.  Each (ray, domain) pair walks its domain tree as a packet (a
-// queue holds its rays in ascending order: neighbouring pixels) with the
-// ray's current best t as the cut, and a hit enters the ray's 64-bit key
-// (t bits | list position | domain) by atomicMin.  The key order is the
-// sequential walk's winner rule (nearer t, then the earlier list entry) and
-// keys are unique per (ray, domain), so the result is the same in any drain
-// order and any interleaving.  The pair's own key and winning triangle go
-// to pkey / pleaf for k_ooc_ch_resolve.
+// launch.  Each live (ray, domain) pair walks its domain tree as a packet (a
+// queue holds neighbouring rays) with the ray's current best t as the cut,
+// and a hit enters the ray's 64-bit key (t bits | list position | domain) by
+// atomicMin.  The key order is the sequential walk's winner rule (nearer t,
+// then the earlier list entry) and keys are unique per (ray, domain), so the
+// result is the same in any drain order and any interleaving.  The pair's
+// own key and winning triangle go to pkey / pleaf for k_ooc_ch_resolve.
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
-    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
-    const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
-    uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf) {
-  __shared__ int32_t wstack[(kBlock / 64) * kStack];
-  uint32_t pj;
-  bool valid;
-  const int s = batch_pair(B, pj, valid);
-  if (s < 0) return;
-  const OocDomain& D = B.d[s];
+__device__ __forceinline__ void ch_pair(const OocDomain& D, uint32_t pj, bool valid,
+                                        const spray_rt_ray* rays, const uint32_t* idx,
+                                        const uint64_t* masks, const float* boxes,
+                                        uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
+                                        int32_t* stack, uint32_t* dead) {
   const uint32_t i = valid ? idx[pj] : 0u;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
   uint64_t k0 = kOocMissKey;
@@ -166,38 +426,68 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
     k0 = __hip_atomic_load(key + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   // the domain's own nearest hit with t <= the ray's best so far (ties at
-  // that t included: the list position decides them)
+  // that t included: the list position decides them); a pair whose domain
+  // starts beyond that t is dead and does not walk
   const float tcur = k0 == kOocMissKey ? d4.w : __uint_as_float(uint32_t(k0 >> 32));
+  float te = 0.f;
+  aabb_ref(boxes + 6 * D.domain, dr, te);
   Best best{tcur, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  bool act = valid, hit = false;
-  trace_tree_packet<false>(reinterpret_cast<uint64_t>(D.nodes),
-                           reinterpret_cast<uint64_t>(D.tris),
-                           reinterpret_cast<uint64_t>(D.prims), r, o4.w, 0.f, best, act, hit,
-                           wstack + (threadIdx.x >> 6) * kStack);
+  bool act = valid && !(te > tcur), hit = false;
+  if (__ballot(act))
+    trace_tree_packet<false>(reinterpret_cast<uint64_t>(D.nodes),
+                             reinterpret_cast<uint64_t>(D.tris),
+                             reinterpret_cast<uint64_t>(D.prims), r, o4.w, 0.f, best, act, hit,
+                             stack);
   if (!valid) return;
   uint64_t mine = kOocMissKey;
   if (best.leaf != 0xFFFFFFFFu) {
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
-    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
     mine = (uint64_t(__float_as_uint(best.t)) << 32) |
-           (uint64_t(list_pos<W>(m, boxes, D.domain, dr)) << 16) | uint64_t(D.domain);
-    atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
+           (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
+    const uint64_t old =
+        atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
+    if (mine < old) {
+      const float to = old == kOocMissKey ? kInf : __uint_as_float(uint32_t(old >> 32));
+      if (best.t < to) count_deaths<W>(m, boxes, dr, best.t, to, dead);
+    }
   }
   pkey[pj] = mine;
   pleaf[pj] = best.leaf;
 }
 
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
+    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
+    const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
+    uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf,
+    uint32_t* __restrict__ live) {
+  __shared__ int32_t wstack[kWaves * kStack];
+  __shared__ uint32_t dead[64 * W];
+  for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
+  __syncthreads();
+  uint32_t pj;
+  bool valid;
+  const int s = batch_pair(B, pj, valid);
+  if (s >= 0)
+    ch_pair<W>(B.d[s], pj, valid, rays, idx, masks, boxes, key, pkey, pleaf,
+               wstack + (threadIdx.x >> 6) * kStack, dead);
+  flush_deaths<W>(dead, live);
+}
+
 // Hit records of the batch's winners: the one pair whose key equals its
 // ray's minimum runs updateIntersection (trimesh_buffer.cc:328-360) while
 // its domain is still resident.  A later batch with a smaller key rewrites
-// the record.
+// the record.  Block 0 first publishes the batch's live counts.
 __global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ key, const uint64_t* __restrict__ pkey,
-    const uint32_t* __restrict__ pleaf, spray_rt_hit* __restrict__ hits) {
+    const uint32_t* __restrict__ pleaf, spray_rt_hit* __restrict__ hits,
+    const uint32_t* __restrict__ live, OocSnapshot S, int ndom) {
+  if (blockIdx.x == 0) write_snapshot(live, S, ndom);
   uint32_t pj;
   bool valid;
   const int s = batch_pair(B, pj, valid);
@@ -228,147 +518,165 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
   hp[2] = make_float4(nsx, nsy, nsz, __int_as_float(D.domain));
 }
 
+// Miss records of the rays whose key is still kOocMissKey after the last
+// batch (every other record was written by its winner's resolve); one lane
+// per 16-byte quarter of a record, so a wave stores whole lines.
+__global__ __launch_bounds__(kBlock) void k_ooc_finish(const uint64_t* __restrict__ key,
+                                                       spray_rt_hit* __restrict__ hits,
+                                                       size_t M) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const size_t i = j / 3;
+  if (i >= M || key[i] != kOocMissKey) return;
+  const int part = int(j - 3 * i);
+  const float4 v = part == 0   ? make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu))
+                   : part == 1 ? make_float4(0.f, 0.f, 0.f, __uint_as_float(0u))
+                               : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  reinterpret_cast<float4*>(hits)[j] = v;
+}
+
 // Any hit of the rays queued to the batch's domains, OR-ed into occ (a ray
-// already occluded by an earlier batch is skipped; same-batch writers all
-// store 1).
-__global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(OocBatch B,
-                                                         const spray_rt_ray* __restrict__ rays,
-                                                         const uint32_t* __restrict__ idx,
-                                                         uint8_t* __restrict__ occ) {
-  __shared__ int32_t wstack[(kBlock / 64) * kStack];
+// already occluded by an earlier batch is skipped).  Shadow rays diverge, so
+// each lane walks its own ray (occluded_tree_ww: while-while with postponed
+// leaves, the in-core any-hit walk) rather than the packet.  The OR is an
+// atomic on the byte's word so that exactly one writer sees the ray's first
+// occlusion and counts its pairs dead.
+template <int W>
+__device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok,
+                                        const spray_rt_ray* rays, const uint32_t* idx,
+                                        const uint64_t* masks, uint8_t* occ, int32_t* stk,
+                                        uint32_t* dead) {
+  const uint32_t i = ok ? idx[pj] : 0u;
+  if (!ok || occ[i]) return;
+  const float4* rp = reinterpret_cast<const float4*>(rays + i);
+  const float4 o4 = rp[0], d4 = rp[1];
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  if (!occluded_tree_ww<false>(D.nodes, D.tris, r, o4.w, d4.w, stk)) return;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(occ + i);
+  const uint32_t sh = 8u * uint32_t(a & 3u);
+  const uint32_t was = atomicOr(reinterpret_cast<uint32_t*>(a & ~uintptr_t(3)), 1u << sh);
+  if ((was >> sh) & 0xFFu) return;  // another writer was first
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t bits = masks[size_t(i) * W + w];
+    while (bits) {
+      const int j = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      atomicAdd(dead + 64 * w + j, 1u);
+    }
+  }
+}
+
+// The last block to finish (done counter) publishes the live counts and
+// rearms the counter for the next launch.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(
+    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
+    const uint64_t* __restrict__ masks, uint8_t* __restrict__ occ,
+    uint32_t* __restrict__ live, uint32_t* __restrict__ done, OocSnapshot S, int ndom) {
+  __shared__ int32_t stack[kStack * kBlock];  // per-lane stacks, lane-interleaved
+  __shared__ uint32_t dead[64 * W];
+  __shared__ bool last;
+  for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
+  __syncthreads();
   uint32_t pj;
   bool ok;
   const int s = batch_pair(B, pj, ok);
-  if (s < 0) return;
-  const OocDomain& D = B.d[s];
-  const uint32_t i = ok ? idx[pj] : 0u;
-  const bool valid = ok && !occ[i];
-  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  if (valid) {
-    const float4* rp = reinterpret_cast<const float4*>(rays + i);
-    o4 = rp[0];
-    d4 = rp[1];
-  }
-  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  Best best{0.f, 0u, 0u};
-  bool act = valid, hit = false;
-  if (__ballot(act))
-    trace_tree_packet<true>(reinterpret_cast<uint64_t>(D.nodes),
-                            reinterpret_cast<uint64_t>(D.tris),
-                            reinterpret_cast<uint64_t>(D.prims), r, o4.w, d4.w, best, act, hit,
-                            wstack + (threadIdx.x >> 6) * kStack);
-  if (hit) occ[i] = 1;
-}
-
-__global__ __launch_bounds__(kBlock) void k_ooc_clear_occ(const uint8_t* __restrict__ valid,
-                                                          uint8_t* __restrict__ occ, size_t M) {
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i < M && (!valid || valid[i])) occ[i] = 0;
+  if (s >= 0)
+    ah_pair<W>(B.d[s], pj, ok, rays, idx, masks, occ, stack + threadIdx.x, dead);
+  flush_deaths<W>(dead, live);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  write_snapshot(live, S, ndom);
+  if (threadIdx.x == 0) *done = 0;
 }
 
 }  // namespace
 
 hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int ndom,
-                             const spray_rt_ray* rays, const uint8_t* valid, size_t M,
-                             OocScratch& q, uint32_t* h_first) {
-  if (ndom <= 0 || ndom > 256 || M > 0xFFFFFFFFull) return hipErrorInvalidValue;
+                             const float* boxes, const spray_rt_ray* rays, const uint8_t* valid,
+                             size_t M, OocScratch& q, uint64_t* key_init, uint8_t* occ_clear,
+                             uint32_t* h_first, unsigned long long* h_score) {
+  if (ndom <= 0 || ndom > 256 || M == 0 || M > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const int W = ndom <= 64 ? 1 : 4;
   const unsigned g = grid_for(M);
-  hipError_t e0 = hipMemsetAsync(q.npairs + M, 0, sizeof(uint32_t), s);
-  if (e0 != hipSuccess) return e0;
+  const size_t n = size_t(ndom) * g;
+  if (n > q.block_cap) return hipErrorInvalidValue;  // the caller sizes for M
   if (W == 1)
-    k_ooc_masks<1><<<g, kBlock, 0, s>>>(tlas, ntlas, rays, valid, M, q.masks, q.npairs);
+    k_ooc_masks<1><<<g, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, q.masks,
+                                        key_init, occ_clear, q.bc, q.sb);
   else
-    k_ooc_masks<4><<<g, kBlock, 0, s>>>(tlas, ntlas, rays, valid, M, q.masks, q.npairs);
+    k_ooc_masks<4><<<g, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, q.masks,
+                                        key_init, occ_clear, q.bc, q.sb);
+  const unsigned nch = (g + kOocChunk - 1) / kOocChunk;
+  if (size_t(ndom) * nch > q.chunk_cap) return hipErrorInvalidValue;  // the caller sizes for M
+  k_ooc_chunk_sums<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.sb, g, ndom, q.csum, q.cw);
+  k_ooc_chunk_scan<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.csum, g, ndom, q.off);
+  k_ooc_first<<<1, 256, 0, s>>>(q.csum, q.cw, int(nch), ndom, q.first, q.live, q.score);
+  if (W == 1)
+    k_ooc_scatter<1><<<g, kBlock, 0, s>>>(q.masks, M, q.first, q.off, q.val, q.pair_cap);
+  else
+    k_ooc_scatter<4><<<g, kBlock, 0, s>>>(q.masks, M, q.first, q.off, q.val, q.pair_cap);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // pair offsets: exclusive scan of the per-ray counts (+ total at [M])
-  size_t tb = q.temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(q.temp, tb, q.npairs, q.poff, int(M + 1), s);
-  if (e != hipSuccess) return e;
-  uint32_t total = 0;
-  e = hipMemcpyAsync(&total, q.poff + M, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  e = hipMemcpyAsync(h_first, q.first, (ndom + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h_score, q.score, ndom * sizeof(unsigned long long),
+                       hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return e;
-  q.npair = total;
-  if (total > q.pair_cap) return hipErrorOutOfMemory;  // caller grows and retries
-  if (total) {
-    if (W == 1)
-      k_ooc_pairs<1><<<g, kBlock, 0, s>>>(q.masks, q.poff, M, q.key_in, q.val_in);
-    else
-      k_ooc_pairs<4><<<g, kBlock, 0, s>>>(q.masks, q.poff, M, q.key_in, q.val_in);
-    int end_bit = 1;
-    while ((1 << end_bit) < ndom) ++end_bit;
-    tb = q.temp_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(q.temp, tb, q.key_in, q.key_out, q.val_in,
-                                           q.val_out, int(total), 0, end_bit, s);
-    if (e != hipSuccess) return e;
-  }
-  k_ooc_bounds<<<(ndom + 1 + 63) / 64, 64, 0, s>>>(q.key_out, total, ndom, q.first);
-  e = hipMemcpyAsync(h_first, q.first, (ndom + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                     s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  return e;
-}
-
-size_t ooc_temp_bytes(size_t M, size_t pairs) {
-  // size queries only; a failed query leaves 0, and the launch that needs the
-  // scratch then reports its error
-  size_t a = 0, b = 0;
-  if (hipcub::DeviceScan::ExclusiveSum(nullptr, a, static_cast<uint32_t*>(nullptr),
-                                       static_cast<uint32_t*>(nullptr),
-                                       int(M + 1)) != hipSuccess)
-    a = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, static_cast<uint16_t*>(nullptr),
-                                         static_cast<uint16_t*>(nullptr),
-                                         static_cast<uint32_t*>(nullptr),
-                                         static_cast<uint32_t*>(nullptr), int(pairs), 0,
-                                         8) != hipSuccess)
-    b = 0;
-  return a > b ? a : b;
-}
-
-hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* key, size_t M) {
-  if (M == 0) return hipSuccess;
-  k_ooc_init<<<grid_for(M), kBlock, 0, s>>>(hits, key, M);
-  return hipGetLastError();
+  q.npair = h_first[ndom];
+  return q.npair > q.pair_cap ? hipErrorOutOfMemory : hipSuccess;  // caller grows, redoes
 }
 
 static unsigned batch_grid(OocBatch& B) {
   B.wave0[0] = 0;
   for (int k = 0; k < B.count; ++k) B.wave0[k + 1] = B.wave0[k] + (B.n[k] + 63) / 64;
-  return (B.wave0[B.count] + kBlock / 64 - 1) / (kBlock / 64);
+  return (B.wave0[B.count] + kWaves - 1) / kWaves;
 }
 
 hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
-                               const uint32_t* idx, const uint64_t* masks, const float* boxes,
-                               uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
-                               spray_rt_hit* hits) {
+                               const OocScratch& q, const float* boxes, uint64_t* key,
+                               spray_rt_hit* hits, OocSnapshot snap) {
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
-  const unsigned g = batch_grid(B);
-  if (g == 0) return hipSuccess;
+  const int ndom = 64 * W;
+  unsigned g = batch_grid(B);
+  if (g == 0) g = 1;  // the resolve publishes even when empty
   if (W == 1)
-    k_ooc_ch_batch<1><<<g, kBlock, 0, s>>>(B, rays, idx, masks, boxes, key, pkey, pleaf);
+    k_ooc_ch_batch<1><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
+                                           q.pleaf, q.live);
   else
-    k_ooc_ch_batch<4><<<g, kBlock, 0, s>>>(B, rays, idx, masks, boxes, key, pkey, pleaf);
+    k_ooc_ch_batch<4><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
+                                           q.pleaf, q.live);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, idx, key, pkey, pleaf, hits);
+  k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, q.val, key, q.pkey, q.pleaf, hits, q.live,
+                                        snap, ndom);
   return hipGetLastError();
 }
 
-hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, const spray_rt_ray* rays,
-                               const uint32_t* idx, uint8_t* occ) {
-  if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
-  const unsigned g = batch_grid(B);
-  if (g == 0) return hipSuccess;
-  k_ooc_ah_batch<<<g, kBlock, 0, s>>>(B, rays, idx, occ);
-  return hipGetLastError();
-}
-
-hipError_t launch_ooc_clear_occ(hipStream_t s, const uint8_t* valid, uint8_t* occ, size_t M) {
+hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* hits, size_t M) {
   if (M == 0) return hipSuccess;
-  k_ooc_clear_occ<<<grid_for(M), kBlock, 0, s>>>(valid, occ, M);
+  k_ooc_finish<<<grid_for(3 * M), kBlock, 0, s>>>(key, hits, M);
+  return hipGetLastError();
+}
+
+hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
+                               const OocScratch& q, uint8_t* occ, uint32_t* done,
+                               OocSnapshot snap) {
+  if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
+  const int ndom = 64 * W;
+  unsigned g = batch_grid(B);
+  if (g == 0) g = 1;  // the last block publishes even when empty
+  if (W == 1)
+    k_ooc_ah_batch<1><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap,
+                                           ndom);
+  else
+    k_ooc_ah_batch<4><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap,
+                                           ndom);
   return hipGetLastError();
 }
 

@@ -22,6 +22,7 @@ constexpr int kBins = 32;          // SAH bins per axis
 constexpr int kMaxDepth = 24;      // builder guarantees depth <= kMaxDepth
 constexpr int kStack = 24;         // per-lane traversal stack (LDS), >= kMaxDepth
 constexpr float kRayEpsilon = 0.001f;  // SPRAY_RAY_EPSILON, render/spray.h:46
+constexpr unsigned kDomainListSize = 16;  // SPRAY_RAY_DOMAIN_LIST_SIZE, src/CMakeLists.txt:32-35
 // Culling slack of the slab test (results never depend on culling as long as
 // it is conservative; tests/ check BVH == brute force bit-exactly).
 constexpr float kTfarSlack = 1.0000153f;  // 1 + 2^-16

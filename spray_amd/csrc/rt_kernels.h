@@ -166,30 +166,49 @@ struct OocDomain {
 
 // Device scratch of the queue build (sized by the caller).
 struct OocScratch {
-  uint64_t* masks;   // [M * W]
-  uint32_t* npairs;  // [M + 1]
-  uint32_t* poff;    // [M + 1]
-  uint16_t* key_in;  // [pair_cap]
-  uint16_t* key_out;
-  uint32_t* val_in;
-  uint32_t* val_out;  // the queues: ray ids grouped by domain, ascending
-  uint32_t* first;    // [ndom + 1]
-  uint64_t* pkey;     // [pair_cap] closest-hit key of each (ray, domain) pair
-  uint32_t* pleaf;    // [pair_cap] its triangle (leaf order)
-  void* temp;
-  size_t temp_bytes;
+  uint64_t* masks;            // [M * W] per-ray domain list
+  uint32_t* val;              // [pair_cap] the queues: ray ids grouped by domain
+  uint32_t* first;            // [257] queue bounds
+  uint32_t* bc;               // [block_cap] pairs per (ray block, domain), block-major
+  uint32_t* sb;               // [block_cap] DomainStats weight per (ray block, domain)
+  uint32_t* off;              // [block_cap] a block's offset in its queue, domain-major
+  uint32_t* csum;             // [chunk_cap] pairs per (domain, chunk of ray blocks)
+  uint32_t* cw;               // [chunk_cap] DomainStats weight per (domain, chunk)
+  unsigned long long* score;  // [256] DomainStats score per domain
+  uint32_t* live;             // [256] live pairs per queue (see k_ooc_ch_batch)
+  uint64_t* pkey;             // [pair_cap] closest-hit key of each (ray, domain) pair
+  uint32_t* pleaf;            // [pair_cap] its triangle (leaf order)
+  size_t block_cap;           // >= ndom * ray blocks
+  size_t chunk_cap;           // >= ndom * ceil(ray blocks / kOocChunk)
   size_t pair_cap;
   uint32_t npair;
 };
 
+// Host-visible liveness snapshot (pinned, device-mapped): the kernels that
+// end a drain launch store snap[d] = gen << 32 | q.live[d] and then
+// seq = gen << 32 | launch number + 1.
+struct OocSnapshot {
+  unsigned long long* snap;  // [256]
+  unsigned long long* seq;   // [1]
+  uint32_t gen;
+  uint32_t launch;
+};
+
 // Builds the per-domain ray queues of a batch (rays with valid[i] == 0 are
-// skipped; valid may be null) and copies first[0..ndom] to h_first (host):
-// domain d's queue is val_out[first[d] .. first[d+1]).  Returns
-// hipErrorOutOfMemory (q.npair = needed) when pair_cap is too small.
+// skipped; valid may be null) in one pass over the rays: domain lists,
+// per-domain counts and DomainStats scores (ooc_domain_stats.cc:60-111: sum
+// over queued pairs of SPRAY_RAY_DOMAIN_LIST_SIZE - list position), queue
+// bounds, then a scatter of the ray ids (ascending within each block of
+// rays).  key_init (closest hit: the per-ray keys, set to kOocMissKey) and
+// occ_clear (any hit: the valid rays' flags, set to 0) may be null.
+// Copies first[0..ndom] to h_first and the scores to h_score; q.live[d]
+// starts at the queue lengths.  Returns hipErrorOutOfMemory (q.npair =
+// needed) when pair_cap is too small.
 hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int ndom,
-                             const spray_rt_ray* rays, const uint8_t* valid, size_t M,
-                             OocScratch& q, uint32_t* h_first);
-size_t ooc_temp_bytes(size_t M, size_t pairs);
+                             const float* boxes, const spray_rt_ray* rays, const uint8_t* valid,
+                             size_t M, OocScratch& q, uint64_t* key_init, uint8_t* occ_clear,
+                             uint32_t* h_first, unsigned long long* h_score);
+constexpr uint32_t kOocChunk = 4096;  // ray blocks per chunk of the queue-offset scan
 // Per-ray closest-hit key of the ooc drains: t bits << 32 | position in the
 // ray's sorted domain list << 16 | domain; a miss is kOocMissKey.
 constexpr uint64_t kOocMissKey = ~0ull;
@@ -201,18 +220,19 @@ struct OocBatch {
   uint32_t wave0[kOocBatch + 1];  // filled by the launcher
   int count;
 };
-hipError_t launch_ooc_init(hipStream_t s, spray_rt_hit* hits, uint64_t* key, size_t M);
 // Closest hit of a batch (traversal + key atomicMin, then the winners'
-// records); masks: the queue build's per-ray domain masks (W words), boxes
-// the domain boxes, pkey / pleaf scratch indexed like idx.
+// records) over the queues of q; boxes the domain boxes.  Pairs whose ray
+// gets a nearer hit are counted off q.live; the snapshot follows.
 hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
-                               const uint32_t* idx, const uint64_t* masks, const float* boxes,
-                               uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
-                               spray_rt_hit* hits);
-hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, const spray_rt_ray* rays,
-                               const uint32_t* idx, uint8_t* occ);
-hipError_t launch_ooc_clear_occ(hipStream_t s, const uint8_t* valid, uint8_t* occ, size_t M);
-
+                               const OocScratch& q, const float* boxes, uint64_t* key,
+                               spray_rt_hit* hits, OocSnapshot snap);
+// Miss records of the rays no batch hit (after the last closest-hit batch).
+hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* hits, size_t M);
+// Any hit of a batch; the pairs of newly occluded rays are counted off
+// q.live; the snapshot follows.  done: a device counter, 0 between launches.
+hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
+                               const OocScratch& q, uint8_t* occ, uint32_t* done,
+                               OocSnapshot snap);
 // frame layer (frame_kernels.hip)
 hipError_t launch_shade(hipStream_t s, const spray_rt_shader& P, const spray_rt_bsdf* bsdfs,
                         int nbsdf, int bounce, int ns, spray_rt_ray* rays,
