@@ -263,7 +263,8 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
     ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
-    order = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
+    traced = bool(args.ao_traced)
+    order = None if traced else torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
 
@@ -271,8 +272,10 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
         rt.set_coherence(rt.RAYS_COHERENT)  # camera rays: packets
         rt.intersect_scene(prim, hits)
         # the spp rays of a pixel share every sample direction (seed
-        # pixid * (l + 1)): traced sample-major, they sit on neighbouring lanes
-        rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order)
+        # pixid * (l + 1)): traced sample-major, they sit on neighbouring
+        # lanes -- written in that order (traced), or permuted through order
+        rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order,
+                            traced=traced)
         rt.set_coherence(rt.RAYS_INCOHERENT)  # hemisphere rays: one walk per lane
         if ev:
             ev[0].record(stream)
@@ -304,8 +307,8 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     rt.occluded_scene(ao[:n_ao * 32], occ[:n_ao], counters=ctr)
     torch.cuda.synchronize()
     idx = algorithmic_bytes(n_ao, int(ctr[0]), int(ctr[1]), 4)
-    # compulsory bytes: 32-B rays + 4-B trace order in, 1 B out, the scene once
-    comp = n_ao * (32 + 4 + 1) + sbytes
+    # compulsory bytes: 32-B rays (+ 4-B trace order) in, 1 B out, the scene once
+    comp = n_ao * (32 + (0 if traced else 4) + 1) + sbytes
     rt.set_coherence(rt.RAYS_ADAPTIVE)
     return {"value": round((n_prim + n_ao) * world * args.steps / el / 1e6, 3),
             "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -420,6 +423,8 @@ def main():
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
+    ap.add_argument("--ao-traced", type=int, default=1,
+                    help="AO rays spawned in their trace order (0: compacted + order permutation)")
     ap.add_argument("--frame", type=int, default=1,
                     help="also measure the whole device frame (shading + film)")
     args = ap.parse_args()

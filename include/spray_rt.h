@@ -248,7 +248,8 @@ int spray_rt_occluded_scene_devcount(spray_rt_ctx_t ctx, const spray_rt_ray* ray
                                      uint8_t* occluded,
                                      unsigned long long* d_counters);
 /* Any hit of the rays order[j], j < *d_count (device count, <= max_rays),
- * lanes taking them in that order; occluded[order[j]] is written.  The
+ * lanes taking them in that order; occluded[order[j]] is written (order =
+ * NULL: the identity, rays 0 .. *d_count - 1).  The
  * results equal the positional launch's -- only the grouping of rays into
  * wavefronts changes (e.g. spray_rt_spawn_shadows_ao_ordered's order).
  * Device buffers only. */
@@ -375,6 +376,14 @@ int spray_rt_spawn_shadows_ao_ordered(spray_rt_ctx_t ctx, const spray_rt_ray* ra
                                       size_t M, int nsamples, spray_rt_ray* out_rays,
                                       int32_t* out_src, uint32_t* d_count,
                                       uint32_t* trace_order);
+/* The same rays written directly in that trace order (out_rays[k] and
+ * out_src[k] for k < *d_count: a permutation of spray_rt_spawn_shadows_ao's
+ * output), for spray_rt_occluded_scene_order with order = NULL: the any-hit
+ * lanes then read rays and write occlusion flags contiguously. */
+int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                     const spray_rt_hit* hits, const int32_t* pixid,
+                                     size_t M, int nsamples, spray_rt_ray* out_rays,
+                                     int32_t* out_src, uint32_t* d_count);
 
 /* ---- frames: path shading, film, tiles (callers of the hot path) ---- */
 /* The shading pass of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-227) /

@@ -806,7 +806,7 @@ extern "C" int spray_rt_occluded_scene_order(spray_rt_ctx_t c, const spray_rt_ra
   if (r) return r;
   if (max_rays == 0) return SPRAY_RT_OK;
   if (max_rays > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "max_rays > 2^32");
-  if (!is_device_ptr(rays) || !is_device_ptr(occ) || !is_device_ptr(order) ||
+  if (!is_device_ptr(rays) || !is_device_ptr(occ) || (order && !is_device_ptr(order)) ||
       !is_device_ptr(d_count))
     return fail(c, SPRAY_RT_ERR_ARG, "ordered occlusion needs device buffers");
   HIPCHK(c, launch_scene_occluded_indexed(stream_of(c), view(c), rays, max_rays, order, d_count,
@@ -1016,10 +1016,10 @@ int spray_rt_spawn_shadows_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
   return SPRAY_RT_OK;
 }
 
-int spray_rt_spawn_shadows_ao_ordered(spray_rt_ctx_t c, const spray_rt_ray* rays,
-                                      const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                      int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
-                                      uint32_t* d_count, uint32_t* trace_order) {
+namespace {
+int spawn_ao(spray_rt_ctx_t c, const spray_rt_ray* rays, const spray_rt_hit* hits,
+             const int32_t* pixid, size_t M, int nsamples, spray_rt_ray* out_rays,
+             int32_t* out_src, uint32_t* d_count, uint32_t* trace_order, bool traced) {
   if (!c) return SPRAY_RT_ERR_ARG;
   if (!d_count || nsamples <= 0 || nsamples > 1024)
     return fail(c, SPRAY_RT_ERR_ARG, "bad AO arguments");
@@ -1034,16 +1034,31 @@ int spray_rt_spawn_shadows_ao_ordered(spray_rt_ctx_t c, const spray_rt_ray* rays
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
   HIPCHK(c, launch_spawn_ao(stream_of(c), rays, hits, pixid, M, nsamples, out_rays, out_src,
-                            d_count, c->d_block_counts, trace_order));
+                            d_count, c->d_block_counts, trace_order, traced));
   return SPRAY_RT_OK;
+}
+}  // namespace
+
+int spray_rt_spawn_shadows_ao_ordered(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                                      const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                                      int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
+                                      uint32_t* d_count, uint32_t* trace_order) {
+  return spawn_ao(c, rays, hits, pixid, M, nsamples, out_rays, out_src, d_count, trace_order,
+                  false);
 }
 
 int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
                               const spray_rt_hit* hits, const int32_t* pixid, size_t M,
                               int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
                               uint32_t* d_count) {
-  return spray_rt_spawn_shadows_ao_ordered(c, rays, hits, pixid, M, nsamples, out_rays, out_src,
-                                           d_count, nullptr);
+  return spawn_ao(c, rays, hits, pixid, M, nsamples, out_rays, out_src, d_count, nullptr, false);
+}
+
+int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t c, const spray_rt_ray* rays,
+                                     const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                                     int nsamples, spray_rt_ray* out_rays, int32_t* out_src,
+                                     uint32_t* d_count) {
+  return spawn_ao(c, rays, hits, pixid, M, nsamples, out_rays, out_src, d_count, nullptr, true);
 }
 
 }  // extern "C"

@@ -145,10 +145,11 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
 // device memory (per-hit sample masks and tile totals).  order (optional,
 // M * nsamples uint32): a trace order of the written rays, sample-major
 // within aligned blocks of 8 source rays (the spp rays of a pixel).
+// traced: the rays and sources are written in that trace order instead.
 hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
-                           void* scratch, uint32_t* order = nullptr);
+                           void* scratch, uint32_t* order = nullptr, bool traced = false);
 size_t ao_scratch_bytes(size_t M, int nsamples);
 
 // ---- out-of-core path (ooc_kernels.hip) ----

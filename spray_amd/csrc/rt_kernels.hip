@@ -23,14 +23,16 @@ namespace {
 // Work distribution of the scene kernels (measured, profiles/): closest hit
 // = persistent waves dequeuing 128-ray chunks from per-XCD band queues
 // (1.02 -> 0.71 ms: no block-coupled wave lifetimes, band-local L2); any hit
-// = one ray per lane over a plain grid (short waves: the persistent tail
-// costs more than it saves, 0.43 vs 0.48 ms).  SPRAY_PERSIST_*/SPRAY_CHUNK_*
-// select the other forms in diagnostic builds.
+// = one ray per lane over a plain grid for batches below kPersistAhRays
+// (shadow batches: the persistent tail costs more than it saves, 0.27 vs
+// 0.33 ms), persistent above it (AO-16 batches, 36.6 M rays: 6.23 -> 5.71 ms
+// per AO step).  SPRAY_PERSIST_*/SPRAY_CHUNK_* select the other forms in
+// diagnostic builds.
 #ifndef SPRAY_CHUNK_CH
 #define SPRAY_CHUNK_CH 128
 #endif
 #ifndef SPRAY_CHUNK_AH
-#define SPRAY_CHUNK_AH 64
+#define SPRAY_CHUNK_AH 128
 #endif
 #ifndef SPRAY_PERSIST_CH
 #define SPRAY_PERSIST_CH 1
@@ -38,6 +40,7 @@ namespace {
 #ifndef SPRAY_PERSIST_AH
 #define SPRAY_PERSIST_AH 0
 #endif
+constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this large persist
 
 // Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): packet form: 5 = no
 // tree walks, 6 = top-level mask only, 7 = no epilogue / spawn; per-lane form: 3 = ray in, record out
@@ -203,6 +206,7 @@ struct SceneArgs {
   uint8_t* occ;
   unsigned long long* counters;
   uint32_t* heads;  // kQueues queue heads, 32 words apart (persistent launch)
+  int persist;      // any hit: persistent waves (set by the launcher)
   // fused PT shadow spawn (closest hit): positional output
   ShadePt shade;
   spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
@@ -824,10 +828,10 @@ __global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH
   int32_t* wstk = wstack + (threadIdx.x >> 6) * kStack;
   bool flag = false;
   float pos[3], wi[3];
-  constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
+  const bool persist = ANY ? (SPRAY_PERSIST_AH != 0 || A.persist != 0) : SPRAY_PERSIST_CH != 0;
   const int lane = threadIdx.x & 63;
   const uint32_t* __restrict__ idx = A.idx;
-  if (!kPersist) {
+  if (!persist) {
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
     // an index list entry past the ray buffer is skipped, never read
@@ -1429,46 +1433,118 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_hitmask(
   if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kBlock) void k_spawn_ao_write_masked(
+// The write pass, one thread per hit: its set samples in order, each at
+// its compaction slot k (ascending from the hit's prefix) and its trace
+// position (the masks of the hit's aligned group of kAoGroup neighbours,
+// taken from the group's lanes: the group's rays of samples below l, then
+// the group's earlier rays of sample l).  traced: the ray and its source
+// go to the trace position, where the lanes of one sample write
+// neighbouring slots; else to k, with order[pos] = k.
+//
+// The work of ao_sample, split by what it depends on: the hit's origin,
+// normal and tangent frame once per hit; the local hemisphere sample
+// (sampler seed pixid * (l + 1) -> concentric disk, the double sincos) once
+// per (pixel, sample) -- the group's lanes compute samples l = me, me + 8,
+// ... of the group leader's pixel and pass them round; a lane of another
+// pixel draws its own -- and the rotation per (hit, sample).  The same
+// operations on the same values as ao_sample, so the same bits.
+__global__ __launch_bounds__(kBlock) void k_spawn_ao_write_hits(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
-    const int32_t* __restrict__ pixid, uint32_t npairs, uint32_t ns,
+    const int32_t* __restrict__ pixid, uint32_t M, uint32_t ns,
     const uint2* __restrict__ meta, const uint32_t* __restrict__ tile_off,
-    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src, uint32_t* __restrict__ order) {
-  const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
-  if (q >= npairs) return;
-  const uint32_t i = q / ns, l = q - i * ns;
-  const uint2 m = meta[i];
-  if (!((m.x >> l) & 1u)) return;
-  const uint32_t below = (1u << l) - 1u;
-  const uint32_t k = tile_off[i / kBlock] + m.y + __popc(m.x & below);
-  const AoOut a = ao_sample(rays[i], hits[i], pixid[i], int(l), int(ns));
-  if (SPRAY_NT_IO_LANE) {
-    v4f* op = reinterpret_cast<v4f*>(out + k);
-    __builtin_nontemporal_store(v4f{a.o[0], a.o[1], a.o[2], kRayEpsilon}, op);
-    __builtin_nontemporal_store(v4f{a.w[0], a.w[1], a.w[2], kInf}, op + 1);
-  } else {
-    float4* op = reinterpret_cast<float4*>(out + k);
-    op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
-    op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
-  }
-  if (src) src[k] = int32_t(i);
-  if (order) {
-    // Trace order: within each aligned block of kAoGroup source rays the
-    // block's AO rays sample-major -- (l, then ray).  The spp rays of a
-    // pixel share pixid, hence every sample's seed pixid * (l + 1): the
-    // rays of one sample leave nearly the same point in nearly the same
-    // direction and now sit on neighbouring lanes.  The block's rays occupy
-    // the same output range in both orders, so this is a permutation of
-    // [0, count).
-    const uint32_t M = npairs / ns;
-    const uint32_t i0 = i & ~(kAoGroup - 1u);
-    const uint32_t ie = i0 + kAoGroup < M ? i0 + kAoGroup : M;
-    uint32_t pos = tile_off[i0 / kBlock] + meta[i0].y;
-    for (uint32_t j = i0; j < ie; ++j) {
-      const uint32_t mj = meta[j].x;
-      pos += __popc(mj & below) + (j < i ? (mj >> l) & 1u : 0u);
+    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src, uint32_t* __restrict__ order,
+    int traced) {
+  static_assert(kBlock % kAoGroup == 0 && 64 % kAoGroup == 0, "groups stay inside a wave");
+  constexpr int kPer = 32 / int(kAoGroup);  // local samples per lane (ns <= 32)
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const bool in = i < M;
+  const uint2 m = in ? meta[i] : make_uint2(0u, 0u);
+  const int lane = threadIdx.x & 63, g0 = lane & ~int(kAoGroup - 1), me = lane - g0;
+  uint32_t gm[kAoGroup];
+#pragma unroll
+  for (int t = 0; t < int(kAoGroup); ++t) gm[t] = __shfl(m.x, g0 + t);
+  const uint32_t tile = in ? tile_off[blockIdx.x] : 0u;
+  const uint32_t gpos = tile + __shfl(m.y, g0);
+  const int32_t px = in ? pixid[i] : 0;
+  const int32_t lead = __shfl(px, g0);
+  if (__ballot(m.x != 0) == 0) return;  // the whole wave spawns nothing
+  // the group leader's local samples l = me + kAoGroup * c (those some lane
+  // of the group spawns)
+  uint32_t gor = 0;
+#pragma unroll
+  for (int t = 0; t < int(kAoGroup); ++t) gor |= gm[t];
+  float lvs[kPer][3];
+#pragma unroll
+  for (int c = 0; c < kPer; ++c) {
+    const uint32_t l = uint32_t(me + int(kAoGroup) * c);
+    lvs[c][0] = lvs[c][1] = lvs[c][2] = 0.f;
+    if (l < ns && ((gor >> l) & 1u)) {
+      uint32_t st = sampler_init1(lead * int32_t(l + 1));
+      const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+      hemisphere_local(u1, u2, lvs[c]);
     }
-    order[pos] = k;
+  }
+  // per hit (ao_sample's prologue)
+  float o[3] = {0.f, 0.f, 0.f}, N[3] = {0.f, 0.f, 1.f}, ax[3] = {1.f, 0.f, 0.f},
+        ay[3] = {0.f, 1.f, 0.f};
+  if (m.x) {
+    const spray_rt_ray r = rays[i];
+    const spray_rt_hit h = hits[i];
+    o[0] = r.dir[0] * h.t + r.org[0];
+    o[1] = r.dir[1] * h.t + r.org[1];
+    o[2] = r.dir[2] * h.t + r.org[2];
+    const float wo[3] = {-r.dir[0], -r.dir[1], -r.dir[2]};
+    N[0] = h.ns[0];
+    N[1] = h.ns[1];
+    N[2] = h.ns[2];
+    if (!(gdot3(wo, N) > 0.0f)) {
+      N[0] = -N[0];
+      N[1] = -N[1];
+      N[2] = -N[2];
+    }
+    gnorm3(N);
+    hemisphere_frame(N, ax, ay);
+  }
+  uint32_t k = tile + m.y, run = 0;
+#pragma unroll
+  for (int c = 0; c < kPer; ++c) {
+    for (int q = 0; q < int(kAoGroup); ++q) {
+      const uint32_t l = uint32_t(int(kAoGroup) * c + q);
+      if (l >= ns) break;  // uniform
+      float lv[3] = {__shfl(lvs[c][0], g0 + q), __shfl(lvs[c][1], g0 + q),
+                     __shfl(lvs[c][2], g0 + q)};
+      uint32_t col = 0, before = 0;
+#pragma unroll
+      for (int t = 0; t < int(kAoGroup); ++t) {
+        const uint32_t b = (gm[t] >> l) & 1u;
+        col += b;
+        before += t < me ? b : 0u;
+      }
+      if ((m.x >> l) & 1u) {
+        if (px != lead) {  // another pixel than the group's leader
+          uint32_t st = sampler_init1(px * int32_t(l + 1));
+          const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+          hemisphere_local(u1, u2, lv);
+        }
+        float w[3], pdf;
+        hemisphere_apply(lv, N, ax, ay, w, pdf);
+        const uint32_t pos = gpos + run + before;
+        const uint32_t dst = traced ? pos : k;
+        if (order && !traced) order[pos] = k;
+        ++k;
+        if (SPRAY_NT_IO_LANE) {
+          v4f* op = reinterpret_cast<v4f*>(out + dst);
+          __builtin_nontemporal_store(v4f{o[0], o[1], o[2], kRayEpsilon}, op);
+          __builtin_nontemporal_store(v4f{w[0], w[1], w[2], kInf}, op + 1);
+        } else {
+          float4* op = reinterpret_cast<float4*>(out + dst);
+          op[0] = make_float4(o[0], o[1], o[2], kRayEpsilon);
+          op[1] = make_float4(w[0], w[1], w[2], kInf);
+        }
+        if (src) src[dst] = int32_t(i);
+      }
+      run += col;
+    }
   }
 }
 
@@ -1519,8 +1595,10 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 }
 
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
-static hipError_t launch_scene_t(hipStream_t s, const SceneArgs& a) {
-  constexpr bool kPersist = ANY ? SPRAY_PERSIST_AH : SPRAY_PERSIST_CH;
+static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
+  const bool kPersist =
+      ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays) : SPRAY_PERSIST_CH != 0;
+  a.persist = kPersist ? 1 : 0;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
   if (kPersist && !grid) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -1866,7 +1944,7 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
 hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_rt_hit* hits,
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
-                           void* scratch, uint32_t* order) {
+                           void* scratch, uint32_t* order, bool traced) {
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
   const uint32_t npairs = uint32_t(M * size_t(nsamples));
   if (nsamples <= 32) {
@@ -1876,8 +1954,9 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
     k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
                                             uint32_t(nsamples), meta, tiles);
     k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
-    k_spawn_ao_write_masked<<<(npairs + kBlock - 1) / kBlock, kBlock, 0, s>>>(
-        rays, hits, pixid, npairs, uint32_t(nsamples), meta, tiles, out_rays, out_src, order);
+    k_spawn_ao_write_hits<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
+                                               uint32_t(nsamples), meta, tiles, out_rays,
+                                               out_src, order, traced ? 1 : 0);
     return hipGetLastError();
   }
   const uint32_t g = (npairs + kAoTile - 1) / kAoTile;

@@ -113,24 +113,37 @@ __device__ __forceinline__ void hemisphere_local(float u1, float u2, float lv[3]
   gnorm3(lv);
 }
 
-// ... rotated into the frame of N (localToWorld), and its pdf.
-__device__ __forceinline__ void hemisphere_world(const float lv[3], const float N[3],
-                                                 float wi[3], float& pdf) {
+// ... rotated into the frame of N (localToWorld), and its pdf.  The frame
+// (ax, ay) depends on N only: callers with many samples per normal build it
+// once.
+__device__ __forceinline__ void hemisphere_frame(const float N[3], float ax[3], float ay[3]) {
   const float dx0[3] = {0.f, N[2], -N[1]}, dx1[3] = {-N[2], 0.f, N[0]};
-  float ax[3];
   const float* pick = gdot3(dx0, dx0) > gdot3(dx1, dx1) ? dx0 : dx1;
   ax[0] = pick[0];
   ax[1] = pick[1];
   ax[2] = pick[2];
   gnorm3(ax);
-  float ay[3] = {N[1] * ax[2] - ax[1] * N[2], N[2] * ax[0] - ax[2] * N[0],
-                 N[0] * ax[1] - ax[0] * N[1]};
+  ay[0] = N[1] * ax[2] - ax[1] * N[2];
+  ay[1] = N[2] * ax[0] - ax[2] * N[0];
+  ay[2] = N[0] * ax[1] - ax[0] * N[1];
   gnorm3(ay);
+}
+
+__device__ __forceinline__ void hemisphere_apply(const float lv[3], const float N[3],
+                                                 const float ax[3], const float ay[3],
+                                                 float wi[3], float& pdf) {
   wi[0] = (ax[0] * lv[0] + ay[0] * lv[1]) + N[0] * lv[2];
   wi[1] = (ax[1] * lv[0] + ay[1] * lv[1]) + N[1] * lv[2];
   wi[2] = (ax[2] * lv[0] + ay[2] * lv[1]) + N[2] * lv[2];
   gnorm3(wi);
   pdf = lv[2] * kOneOverPi;
+}
+
+__device__ __forceinline__ void hemisphere_world(const float lv[3], const float N[3],
+                                                 float wi[3], float& pdf) {
+  float ax[3], ay[3];
+  hemisphere_frame(N, ax, ay);
+  hemisphere_apply(lv, N, ax, ay, wi, pdf);
 }
 
 __device__ __forceinline__ void cosine_hemisphere(float u1, float u2, const float N[3],

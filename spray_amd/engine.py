@@ -368,15 +368,23 @@ class RtContext:
                     "eye_rays_ooc")
 
     def spawn_shadows_ao(self, rays, hits, pixid, n, nsamples, out_rays, out_src, d_count,
-                         order=None):
+                         order=None, traced=False):
         """ooc::ShaderAo rays (nsamples per hit), compacted (device); order
-        (optional, uint32/int32 device tensor): their sample-major trace order."""
+        (optional, uint32/int32 device tensor): their sample-major trace order;
+        traced: the rays written in that trace order instead."""
         a, k1 = _addr(rays)
         b, k2 = _addr(hits)
         p, k3 = _addr(pixid)
         c, k4 = _addr(out_rays)
         d, k5 = _addr(out_src)
         e, k6 = _addr(d_count)
+        if traced:
+            if order is not None:
+                raise ValueError("traced spawn writes no order")
+            self._check(lib().spray_rt_spawn_shadows_ao_traced(self.h, a, b, p, int(n),
+                                                               int(nsamples), c, d, e),
+                        "spawn_shadows_ao_traced")
+            return
         if order is None:
             self._check(lib().spray_rt_spawn_shadows_ao(self.h, a, b, p, int(n), int(nsamples),
                                                         c, d, e), "spawn_shadows_ao")
@@ -387,9 +395,10 @@ class RtContext:
                     "spawn_shadows_ao_ordered")
 
     def occluded_scene_order(self, rays, max_rays, order, d_count, occ):
-        """Any hit of rays order[j], j < *d_count; occ[order[j]] written (device)."""
+        """Any hit of rays order[j], j < *d_count; occ[order[j]] written (device;
+        order None: rays 0 .. *d_count - 1)."""
         a, k1 = _addr(rays)
-        o, k2 = _addr(order)
+        o, k2 = _addr(order) if order is not None else (None, None)
         b, k3 = _addr(d_count)
         c, k4 = _addr(occ)
         self._check(lib().spray_rt_occluded_scene_order(self.h, a, int(max_rays), o, b, c),

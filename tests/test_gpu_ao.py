@@ -1,7 +1,9 @@
 """GPU ambient-occlusion rays (ooc::ShaderAo, 16 per hit) against the oracle:
 same (source, sample) sequence, origins and directions bit for bit (both
 sides round the hemisphere sample's sin / cos once from double, DESIGN.md
-section 4), and any hit of the device's rays bit-identical to the oracle's."""
+section 4), and any hit of the device's rays bit-identical to the oracle's,
+in compaction order, through the trace-order permutation, written in trace
+order (traced), and through the persistent any-hit form."""
 import numpy as np
 import pytest
 import torch
@@ -88,5 +90,32 @@ def test_ao16_spawn_and_occlusion(oracle, ns):
         rt.occluded_scene_order(out2, m, order, cnt2, occ)
         rt.sync()
         assert (occ.cpu().numpy() == ref).all()
+
+    # traced: the same rays written in that order -- out3[k] = out[order[k]]
+    out3 = torch.empty_like(out)
+    osrc3 = torch.empty_like(osrc)
+    cnt3 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rt.spawn_shadows_ao(rays, h, pixid, n, ns, out3, osrc3, cnt3, traced=True)
+    rt.sync()
+    assert int(cnt3.item()) == m
+    assert out3[:m].cpu().numpy().tobytes() == out[:m].cpu().numpy()[ordh].tobytes()
+    assert (osrc3[:m].cpu().numpy() == src[ordh]).all()
+    rt.set_coherence(rt.RAYS_INCOHERENT)
+    occ = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+    rt.occluded_scene_order(out3, m, None, cnt3, occ)
+    rt.sync()
+    assert (occ.cpu().numpy() == ref[ordh]).all()
+    if ns == 16:
+        # a batch of >= 16 Mi rays capacity runs the persistent any-hit form
+        # (kPersistAhRays); the device count bounds it to the m written rays
+        cap = 16 << 20
+        big = torch.empty((cap, 8), dtype=torch.float32, device="cuda")
+        big[:m] = out3[:m]
+        occb = torch.full((cap,), 9, dtype=torch.uint8, device="cuda")
+        rt.occluded_scene_order(big, cap, None, cnt3, occb)
+        rt.sync()
+        ob = occb.cpu().numpy()
+        assert (ob[:m] == ref[ordh]).all() and (ob[m:] == 9).all()
+        del big, occb
     rt.set_coherence(rt.RAYS_ADAPTIVE)
     scene.close()
