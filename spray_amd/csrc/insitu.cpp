@@ -112,10 +112,14 @@ struct InsituTransport {
   virtual int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
                      int64_t* h_recv) = 0;
   // device buffers; byte counts per peer (host)
+  // skip_self: the rank's own segment is not moved (its offsets still count)
   virtual int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
-                        const size_t* rb) = 0;
+                        const size_t* rb, bool skip_self = false) = 0;
   virtual int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) = 0;
   virtual int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) = 0;
+  // copies a rank sends itself may skip the wire (the owner gathers them
+  // straight from the holder's arrays)
+  virtual bool self_direct() const { return true; }
 };
 
 struct spray_rt_insitu {
@@ -181,7 +185,7 @@ struct RcclTransport : InsituTransport {
     const int W = I->world;
     int64_t* dev_recv = const_cast<int64_t*>(dev_send) + 64;
     std::vector<size_t> b(W, sizeof(int64_t));
-    CALL(alltoallv(I, dev_send, b.data(), dev_recv, b.data()));
+    CALL(alltoallv(I, dev_send, b.data(), dev_recv, b.data(), false));
     hipStream_t s = stream_of(I->ctx);
     HIPCHK(I->ctx, hipMemcpyAsync(I->h_small, dev_send, 128 * sizeof(int64_t),
                                   hipMemcpyDeviceToHost, s));
@@ -192,7 +196,7 @@ struct RcclTransport : InsituTransport {
     return SPRAY_RT_OK;
   }
   int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
-                const size_t* rb) override {
+                const size_t* rb, bool skip_self) override {
     const NcclApi& N = nccl();
     hipStream_t s = stream_of(I->ctx);
     const char* sp = static_cast<const char*>(send);
@@ -201,7 +205,8 @@ struct RcclTransport : InsituTransport {
     CALL(chk(I, N.GroupStart(), "ncclGroupStart"));
     for (int r = 0; r < I->world; ++r) {
       if (r == I->rank && !self_via_nccl) {
-        if (sb[r]) HIPCHK(I->ctx, hipMemcpyAsync(rp + ro, sp + so, sb[r], hipMemcpyDeviceToDevice, s));
+        if (sb[r] && !skip_self)
+          HIPCHK(I->ctx, hipMemcpyAsync(rp + ro, sp + so, sb[r], hipMemcpyDeviceToDevice, s));
       } else {
         if (sb[r]) CALL(chk(I, N.Send(sp + so, sb[r], ncclUint8, r, comm, s), "ncclSend"));
         if (rb[r]) CALL(chk(I, N.Recv(rp + ro, rb[r], ncclUint8, r, comm, s), "ncclRecv"));
@@ -223,6 +228,7 @@ struct RcclTransport : InsituTransport {
     return chk(I, nccl().Reduce(dev, dev, n, ncclFloat32, ncclSum, root, comm, stream_of(I->ctx)),
                "ncclReduce");
   }
+  bool self_direct() const override { return !self_via_nccl; }
   ~RcclTransport() override {
     if (comm) nccl().CommDestroy(comm);
   }
@@ -251,7 +257,7 @@ struct HostTransport : InsituTransport {
     return SPRAY_RT_OK;
   }
   int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
-                const size_t* rb) override {
+                const size_t* rb, bool) override {  // the self segment travels (unused)
     const int W = I->world;
     const size_t ts = std::accumulate(sb, sb + W, size_t(0));
     const size_t trv = std::accumulate(rb, rb + W, size_t(0));
@@ -297,6 +303,7 @@ struct HostTransport : InsituTransport {
 struct Routed {
   size_t total = 0;  // copies this rank sends (entries of idx)
   size_t recv = 0;   // copies it receives
+  size_t self_n = 0, self_send = 0, self_recv = 0;  // its own copies, their offsets
   std::vector<int64_t> send_n, recv_n;
   std::vector<size_t> bytes(size_t per, bool back) const {
     const std::vector<int64_t>& v = back ? recv_n : send_n;
@@ -327,6 +334,11 @@ int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf
   for (int r = 0; r < W; ++r) {
     if (R->send_n[r] < 0 || R->recv_n[r] < 0)
       return fail(c, SPRAY_RT_ERR_STATE, "in-situ count exchange returned a negative count");
+    if (r == I->rank) {
+      R->self_n = size_t(R->send_n[r]);
+      R->self_send = R->total;
+      R->self_recv = R->recv;
+    }
     R->total += size_t(R->send_n[r]);
     R->recv += size_t(R->recv_n[r]);
   }
@@ -335,14 +347,14 @@ int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf
 }
 
 int exchange(spray_rt_insitu* I, const Routed& R, size_t per, bool back, const void* send,
-             void* recv) {
+             void* recv, bool skip_self = false) {
   const std::vector<size_t> sb = R.bytes(per, back), rb = R.bytes(per, !back);
   for (int r = 0; r < I->world; ++r)
     if (r != I->rank) {
       I->st[0] += sb[r];
       I->st[1] += rb[r];
     }
-  return I->tr->alltoallv(I, send, sb.data(), recv, rb.data());
+  return I->tr->alltoallv(I, send, sb.data(), recv, rb.data(), skip_self);
 }
 
 int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
@@ -374,8 +386,17 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     const size_t m = R.recv;
     GROW(I->sendb, std::max(R.total * kRadRecBytes, R.total * 8));
     GROW(I->recvb, m * kRadRecBytes);
-    HIPCHK(c, launch_pack_rad(s, hr, hw, hp, hs, I->idx.as<int64_t>(), R.total, I->sendb.p));
-    CALL(exchange(I, R, kRadRecBytes, false, I->sendb.p, I->recvb.p));
+    // the rank's own copies skip the wire: the owner side gathers them from
+    // the holder arrays (same records, same positions)
+    const bool direct = I->tr->self_direct() && R.self_n;
+    const size_t ps = direct ? R.self_send : R.total, pe = direct ? R.self_send + R.self_n : R.total;
+    const size_t us = direct ? R.self_recv : m, ue = direct ? R.self_recv + R.self_n : m;
+    char* sbp = static_cast<char*>(I->sendb.p);
+    char* rbp = static_cast<char*>(I->recvb.p);
+    const int64_t* ix = I->idx.as<int64_t>();
+    HIPCHK(c, launch_pack_rad(s, hr, hw, hp, hs, ix, ps, sbp));
+    HIPCHK(c, launch_pack_rad(s, hr, hw, hp, hs, ix + pe, R.total - pe, sbp + pe * kRadRecBytes));
+    CALL(exchange(I, R, kRadRecBytes, false, I->sendb.p, I->recvb.p, direct));
     GROW(I->oray, m * 32);
     GROW(I->ow, m * 16);
     GROW(I->opix, m * 4);
@@ -385,8 +406,16 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     GROW(I->obest, m * 8);
     GROW(I->owin, m);
     GROW(I->ovalid, m);
-    HIPCHK(c, launch_unpack_rad(s, I->recvb.p, m, I->oray.as<spray_rt_ray>(), I->ow.as<float>(),
-                                I->opix.as<int32_t>(), I->osam.as<int32_t>()));
+    spray_rt_ray* oray = I->oray.as<spray_rt_ray>();
+    float* ow = I->ow.as<float>();
+    int32_t* opix = I->opix.as<int32_t>();
+    int32_t* osam = I->osam.as<int32_t>();
+    HIPCHK(c, launch_unpack_rad(s, rbp, us, oray, ow, opix, osam));
+    HIPCHK(c, launch_unpack_rad(s, rbp + ue * kRadRecBytes, m - ue, oray + ue, ow + 4 * ue,
+                                opix + ue, osam + ue));
+    if (direct)
+      HIPCHK(c, launch_gather_rad(s, hr, hw, hp, hs, ix + R.self_send, R.self_n, oray + us,
+                                  ow + 4 * us, opix + us, osam + us));
     if (m)
       HIPCHK(c, launch_scene_intersect_keyed(s, view(c), I->oray.as<spray_rt_ray>(), m,
                                              I->ohit.as<spray_rt_hit>(), I->okey.as<uint64_t>()));
@@ -448,13 +477,27 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     CALL(route_and_count(I, I->sgray.as<spray_rt_ray>(), cs, I->smask, I->sidx, I->sstarts, &S));
     GROW(I->sendb, S.total * kShadowRecBytes);
     GROW(I->recvb, S.recv * kShadowRecBytes);
-    HIPCHK(c, launch_pack_shadow(s, I->sray.as<spray_rt_ray>(), I->ssel.as<uint32_t>(),
-                                 I->sidx.as<int64_t>(), S.total, I->sendb.p));
-    CALL(exchange(I, S, kShadowRecBytes, false, I->sendb.p, I->recvb.p));
-    GROW(I->ashadow, S.recv * 32);
-    GROW(I->aocc, S.recv);
-    GROW(I->sret, S.total);
-    HIPCHK(c, launch_unpack_shadow(s, I->recvb.p, S.recv, I->ashadow.as<spray_rt_ray>()));
+    {
+      const bool sdir = I->tr->self_direct() && S.self_n;
+      const size_t a0 = sdir ? S.self_send : S.total, a1 = sdir ? S.self_send + S.self_n : S.total;
+      const size_t b0 = sdir ? S.self_recv : S.recv, b1 = sdir ? S.self_recv + S.self_n : S.recv;
+      const spray_rt_ray* sr = I->sray.as<spray_rt_ray>();
+      const uint32_t* ssel = I->ssel.as<uint32_t>();
+      const int64_t* six = I->sidx.as<int64_t>();
+      char* sbp = static_cast<char*>(I->sendb.p);
+      char* rbp = static_cast<char*>(I->recvb.p);
+      HIPCHK(c, launch_pack_shadow(s, sr, ssel, six, a0, sbp));
+      HIPCHK(c, launch_pack_shadow(s, sr, ssel, six + a1, S.total - a1, sbp + a1 * kShadowRecBytes));
+      CALL(exchange(I, S, kShadowRecBytes, false, I->sendb.p, I->recvb.p, sdir));
+      GROW(I->ashadow, S.recv * 32);
+      GROW(I->aocc, S.recv);
+      GROW(I->sret, S.total);
+      spray_rt_ray* ash = I->ashadow.as<spray_rt_ray>();
+      HIPCHK(c, launch_unpack_shadow(s, rbp, b0, ash));
+      HIPCHK(c, launch_unpack_shadow(s, rbp + b1 * kShadowRecBytes, S.recv - b1, ash + b1));
+      if (sdir)
+        HIPCHK(c, launch_gather_shadow_self(s, sr, ssel, six + S.self_send, S.self_n, ash + b0));
+    }
     if (S.recv)
       HIPCHK(c, launch_scene_occluded(s, view(c), I->ashadow.as<spray_rt_ray>(), S.recv, nullptr,
                                       I->aocc.as<uint8_t>(), nullptr));

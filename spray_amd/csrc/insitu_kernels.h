@@ -28,6 +28,14 @@ hipError_t launch_unpack_shadow(hipStream_t s, const void* in, size_t m, spray_r
 // out[j] = slots[sel[j]]
 hipError_t launch_gather_shadow(hipStream_t s, const spray_rt_ray* slots, const uint32_t* sel,
                                 size_t n, spray_rt_ray* out);
+// the rank's own copies without the wire: orays[j] etc. = holder record idx[j]
+// as k_unpack_rad leaves it; out[j] = shadow slot sel[idx[j]] as k_unpack_shadow
+hipError_t launch_gather_rad(hipStream_t s, const spray_rt_ray* rays, const float* w,
+                             const int32_t* pix, const int32_t* sam, const int64_t* idx, size_t n,
+                             spray_rt_ray* orays, float* ow, int32_t* opix, int32_t* osam);
+hipError_t launch_gather_shadow_self(hipStream_t s, const spray_rt_ray* slots,
+                                     const uint32_t* sel, const int64_t* idx, size_t n,
+                                     spray_rt_ray* out);
 // best[idx[j]] = min(best[idx[j]], keys[j]) over the returned keys
 hipError_t launch_key_min(hipStream_t s, const int64_t* idx, const uint64_t* keys, size_t n,
                           uint64_t* best);

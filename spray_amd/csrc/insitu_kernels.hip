@@ -85,6 +85,42 @@ __global__ __launch_bounds__(kBlock) void k_gather_shadow(const float4* __restri
   out[2 * j + 1] = sh[2 * slot + 1];
 }
 
+// A rank's own copies, gathered from the holder arrays instead of packed,
+// sent to itself and unpacked: the records k_unpack_rad / k_unpack_shadow
+// would produce (tnear / tfar reset as on the wire).
+__global__ __launch_bounds__(kBlock) void k_gather_rad(const float4* __restrict__ rays,
+                                                       const float4* __restrict__ w,
+                                                       const int32_t* __restrict__ pix,
+                                                       const int32_t* __restrict__ sam,
+                                                       const int64_t* __restrict__ idx, size_t n,
+                                                       float4* __restrict__ orays,
+                                                       float4* __restrict__ ow,
+                                                       int32_t* __restrict__ opix,
+                                                       int32_t* __restrict__ osam) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t i = size_t(idx[j]);
+  const float4 a = rays[2 * i], b = rays[2 * i + 1], c = w[i];
+  orays[2 * j] = make_float4(a.x, a.y, a.z, kRayEpsilon);
+  orays[2 * j + 1] = make_float4(b.x, b.y, b.z, kInf);
+  ow[j] = make_float4(c.x, c.y, c.z, 0.f);
+  opix[j] = pix[i];
+  osam[j] = sam[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_shadow_self(const float4* __restrict__ sh,
+                                                               const uint32_t* __restrict__ sel,
+                                                               const int64_t* __restrict__ idx,
+                                                               size_t n,
+                                                               float4* __restrict__ rays) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const size_t slot = sel[idx[j]];
+  const float4 a = sh[2 * slot], b = sh[2 * slot + 1];
+  rays[2 * j] = make_float4(a.x, a.y, a.z, kRayEpsilon);
+  rays[2 * j + 1] = make_float4(b.x, b.y, b.z, kInf);
+}
+
 __global__ __launch_bounds__(kBlock) void k_key_min(const int64_t* __restrict__ idx,
                                                     const unsigned long long* __restrict__ keys,
                                                     size_t n,
@@ -121,9 +157,12 @@ __global__ __launch_bounds__(kBlock) void k_occ_return(const int64_t* __restrict
 }
 
 // HdrImage::add of the unoccluded shadows of the copies this rank shaded
-// (one thread per copy, its ns slots in order; copies of one pixel may sit
-// on any rank, so the adds are atomic -- the reference's per-rank images are
-// summed by MPI_Reduce too, image.h:167-181)
+// (copies of one pixel may sit on any rank, so the adds are atomic -- the
+// reference's per-rank images are summed by MPI_Reduce too, image.h:167-181).
+// One thread per copy sums its ns slots in order; the copies of one pixel
+// are neighbours (the spp samples of a pixel travel together), so a
+// segmented scan over the wave's runs of equal pixels leaves one hardware
+// fp32 atomic per run and channel at the run's last lane.
 __global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ image,
                                                         const int32_t* __restrict__ pix,
                                                         size_t m, int ns,
@@ -132,15 +171,46 @@ __global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ imag
                                                         const uint8_t* __restrict__ occ,
                                                         double scale) {
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= m) return;
-  float* px = image + 4 * size_t(pix[i]);
-  for (int k = 0; k < ns; ++k) {
-    const size_t j = i * size_t(ns) + k;
-    if (!sv[j] || occ[j]) continue;
-    const float4 L = sw[j];
-    atomicAdd(px, float(scale * double(L.x)));
-    atomicAdd(px + 1, float(scale * double(L.y)));
-    atomicAdd(px + 2, float(scale * double(L.z)));
+  const int lane = threadIdx.x & 63;
+  const bool in = i < m;
+  const int32_t p = in ? pix[i] : -1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  bool any = false;
+  if (in)
+    for (int k = 0; k < ns; ++k) {
+      const size_t j = i * size_t(ns) + k;
+      if (!sv[j] || occ[j]) continue;
+      const float4 L = sw[j];
+      a0 += float(scale * double(L.x));
+      a1 += float(scale * double(L.y));
+      a2 += float(scale * double(L.z));
+      any = true;
+    }
+  if (__ballot(any) == 0ull) return;
+  // runs of equal pixels: heads, and each lane's run start
+  const int32_t pp = __shfl_up(p, 1);
+  const bool head = lane == 0 || pp != p;
+  const uint64_t heads = __ballot(head);
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  const int start = 63 - __clzll((long long)(heads & le));
+  int cnt = any ? 1 : 0;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float b0 = __shfl_up(a0, off), b1 = __shfl_up(a1, off), b2 = __shfl_up(a2, off);
+    const int bc = __shfl_up(cnt, off);
+    if (lane - off >= start) {
+      a0 += b0;
+      a1 += b1;
+      a2 += b2;
+      cnt += bc;
+    }
+  }
+  const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
+  if (in && tail && cnt) {
+    float* px = image + 4 * size_t(p);
+    unsafeAtomicAdd(px, a0);
+    unsafeAtomicAdd(px + 1, a1);
+    unsafeAtomicAdd(px + 2, a2);
   }
 }
 
@@ -225,6 +295,19 @@ hipError_t launch_unpack_shadow(hipStream_t s, const void* in, size_t m, spray_r
 hipError_t launch_gather_shadow(hipStream_t s, const spray_rt_ray* slots, const uint32_t* sel,
                                 size_t n, spray_rt_ray* out) {
   LAUNCH(n, k_gather_shadow, reinterpret_cast<const float4*>(slots), sel, n,
+         reinterpret_cast<float4*>(out));
+}
+hipError_t launch_gather_rad(hipStream_t s, const spray_rt_ray* rays, const float* w,
+                             const int32_t* pix, const int32_t* sam, const int64_t* idx, size_t n,
+                             spray_rt_ray* orays, float* ow, int32_t* opix, int32_t* osam) {
+  LAUNCH(n, k_gather_rad, reinterpret_cast<const float4*>(rays),
+         reinterpret_cast<const float4*>(w), pix, sam, idx, n, reinterpret_cast<float4*>(orays),
+         reinterpret_cast<float4*>(ow), opix, osam);
+}
+hipError_t launch_gather_shadow_self(hipStream_t s, const spray_rt_ray* slots,
+                                     const uint32_t* sel, const int64_t* idx, size_t n,
+                                     spray_rt_ray* out) {
+  LAUNCH(n, k_gather_shadow_self, reinterpret_cast<const float4*>(slots), sel, idx, n,
          reinterpret_cast<float4*>(out));
 }
 hipError_t launch_key_min(hipStream_t s, const int64_t* idx, const uint64_t* keys, size_t n,

@@ -1099,46 +1099,56 @@ constexpr int kSelTile = kBlock * kSelPer;
 
 // Exchange plan of a routed batch: for every destination rank d, the
 // ascending indices of the rays whose mask has bit d, concatenated in rank
-// order.  Tiles of kSelTile rays x ranks: count -> one exclusive scan over
-// the [rank][tile] counts (rank-major, so the concatenation falls out) ->
-// ordered write.
-__device__ __forceinline__ uint32_t mask_bits16(const uint64_t* m, size_t n, size_t base,
-                                                int d, uint32_t& bits) {
-  bits = 0;
-#pragma unroll
-  for (int k = 0; k < kSelPer; ++k)
-    if (base + k < n && ((m[base + k] >> d) & 1ull)) bits |= 1u << k;
-  return __popc(bits);
-}
+// order.  One wave owns kPlanWave consecutive rays (coalesced 8-B mask loads,
+// 64 rays per step) and counts / places every rank's entries from the same
+// load (one ballot per rank): count -> one exclusive scan over the
+// [rank][wave tile] counts (rank-major, so the concatenation falls out) ->
+// ordered write.  Lane d of a wave keeps rank d's running count / offset.
+constexpr int kPlanSteps = 16;
+constexpr size_t kPlanWave = 64 * kPlanSteps;
 
 __global__ __launch_bounds__(kBlock) void k_plan_count(const uint64_t* __restrict__ m,
-                                                       size_t n, uint32_t* __restrict__ tc) {
-  using Reduce = hipcub::BlockReduce<uint32_t, kBlock>;
-  __shared__ typename Reduce::TempStorage tmp;
-  const int d = blockIdx.y;
-  uint32_t bits;
-  const size_t base = size_t(blockIdx.x) * kSelTile + size_t(threadIdx.x) * kSelPer;
-  const uint32_t c = base < n ? mask_bits16(m, n, base, d, bits) : 0u;
-  const uint32_t total = Reduce(tmp).Sum(c);
-  if (threadIdx.x == 0) tc[size_t(d) * gridDim.x + blockIdx.x] = total;
+                                                       size_t n, int world, size_t wtiles,
+                                                       uint32_t* __restrict__ tc) {
+  const int lane = threadIdx.x & 63;
+  const size_t wt = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  if (wt >= wtiles) return;  // whole waves
+  const size_t base = wt * kPlanWave;
+  uint32_t acc = 0;
+  for (int p = 0; p < kPlanSteps; ++p) {
+    const size_t i = base + size_t(p) * 64 + lane;
+    const uint64_t v = i < n ? m[i] : 0ull;
+    if (__ballot(v != 0ull) == 0ull) continue;
+    for (int d = 0; d < world; ++d) {
+      const uint32_t c = uint32_t(__popcll(__ballot((v >> d) & 1ull)));
+      if (lane == d) acc += c;
+    }
+  }
+  if (lane < world) tc[size_t(lane) * wtiles + wt] = acc;
 }
 
 __global__ __launch_bounds__(kBlock) void k_plan_write(const uint64_t* __restrict__ m,
-                                                       size_t n, const uint32_t* __restrict__ tc,
+                                                       size_t n, int world, size_t wtiles,
+                                                       const uint32_t* __restrict__ tc,
                                                        int64_t* __restrict__ idx) {
-  using Scan = hipcub::BlockScan<uint32_t, kBlock>;
-  __shared__ typename Scan::TempStorage tmp;
-  const int d = blockIdx.y;
-  uint32_t bits = 0;
-  const size_t base = size_t(blockIdx.x) * kSelTile + size_t(threadIdx.x) * kSelPer;
-  const uint32_t c = base < n ? mask_bits16(m, n, base, d, bits) : 0u;
-  uint32_t k, total;
-  Scan(tmp).ExclusiveSum(c, k, total);
-  k += tc[size_t(d) * gridDim.x + blockIdx.x];
-  while (bits) {
-    const int b = __ffs(bits) - 1;
-    bits &= bits - 1;
-    idx[k++] = int64_t(base + b);
+  const int lane = threadIdx.x & 63;
+  const size_t wt = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  if (wt >= wtiles) return;
+  const size_t base = wt * kPlanWave;
+  uint32_t off = lane < world ? tc[size_t(lane) * wtiles + wt] : 0u;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int p = 0; p < kPlanSteps; ++p) {
+    const size_t i = base + size_t(p) * 64 + lane;
+    const uint64_t v = i < n ? m[i] : 0ull;
+    if (__ballot(v != 0ull) == 0ull) continue;
+    for (int d = 0; d < world; ++d) {
+      const bool mine = (v >> d) & 1ull;
+      const uint64_t b = __ballot(mine);
+      if (!b) continue;
+      const uint32_t o = uint32_t(__builtin_amdgcn_readlane(int(off), d));
+      if (mine) idx[o + uint32_t(__popcll(b & below))] = int64_t(i);
+      if (lane == d) off += uint32_t(__popcll(b));
+    }
   }
 }
 
@@ -1842,23 +1852,24 @@ hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w
 }
 
 size_t plan_temp_bytes(size_t n, int world) {
-  const size_t tiles = (n + kSelTile - 1) / kSelTile;
+  const size_t tiles = (n + kPlanWave - 1) / kPlanWave;
   return (tiles * size_t(world) + 2) * sizeof(uint32_t);
 }
 
 hipError_t launch_plan(hipStream_t s, const uint64_t* masks, size_t n, int world,
                        int64_t* idx, int64_t* starts, void* temp) {
-  const size_t tiles = (n + kSelTile - 1) / kSelTile;
+  const size_t tiles = (n + kPlanWave - 1) / kPlanWave;  // wave tiles
   uint32_t* tc = static_cast<uint32_t*>(temp);
   uint32_t* total = tc + tiles * size_t(world) + 1;
   if (n == 0 || world <= 0) {
     hipError_t e = hipMemsetAsync(starts, 0, (world + 1) * sizeof(int64_t), s);
     return e;
   }
-  const dim3 g{unsigned(tiles), unsigned(world), 1u};
-  k_plan_count<<<g, kBlock, 0, s>>>(masks, n, tc);
+  if (world > 64) return hipErrorInvalidValue;
+  const unsigned g = unsigned((tiles + kBlock / 64 - 1) / (kBlock / 64));
+  k_plan_count<<<g, kBlock, 0, s>>>(masks, n, world, tiles, tc);
   k_scan_blocks<<<1, 1024, 0, s>>>(tc, uint32_t(tiles * world), total);
-  if (idx) k_plan_write<<<g, kBlock, 0, s>>>(masks, n, tc, idx);
+  if (idx) k_plan_write<<<g, kBlock, 0, s>>>(masks, n, world, tiles, tc, idx);
   k_plan_bounds<<<1, 128, 0, s>>>(tc, uint32_t(tiles), world, total, starts);
   return hipGetLastError();
 }
