@@ -137,7 +137,7 @@ struct spray_rt_insitu {
   // holder side of the key composite
   DBuf best, keyback;
   // shadow slots of the shaded copies and their exchange
-  DBuf sray, ssw, ssv, socc, ssel, sgray, smask, sidx, sstarts, ashadow, aocc, sret;
+  DBuf sray, ssw, ssv, socc, ssel, smask, sidx, sstarts, ashadow, aocc, sret;
   DBuf nsel, sel_tmp, dnum, dstats, dtot;
   unsigned long long* h_small = nullptr;  // pinned: counts, totals
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
@@ -314,7 +314,7 @@ struct Routed {
 };
 
 int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf& mask, DBuf& idx,
-                    DBuf& starts, Routed* R) {
+                    DBuf& starts, Routed* R, const uint32_t* sel = nullptr) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
   const int W = I->world;
@@ -323,7 +323,7 @@ int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf
   GROW(starts, (W + 1) * 8);
   GROW(I->plan_tmp, plan_temp_bytes(n, W));
   GROW(I->dcnt, 128 * 8);
-  if (n) HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, mask.as<uint64_t>()));
+  if (n) HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, mask.as<uint64_t>(), sel));
   HIPCHK(c, launch_plan(s, mask.as<uint64_t>(), n, W, idx.as<int64_t>(), starts.as<int64_t>(),
                         I->plan_tmp.p));
   HIPCHK(c, launch_counts_from_starts(s, starts.as<int64_t>(), W, I->dcnt.as<int64_t>()));
@@ -372,9 +372,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
   const spray_rt_ray* hr = rays;
   const int32_t* hp = pixid;
   const int32_t* hs = samid;
-  GROW(I->hw[0], n * 16);
-  HIPCHK(c, launch_weights_one(s, I->hw[0].as<float>(), n));
-  const float* hw = I->hw[0].as<float>();
+  const float* hw = nullptr;  // bounce 0: the packers write weights (1, 1, 1)
   size_t hn = n;
   int cur = 0;
   unsigned long long nrad = 0, nsh = 0;
@@ -470,11 +468,9 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     nsh += cs;
     // ---- shadow rays to the owners of their domains, occlusion OR-ed back
     if (MS) HIPCHK(c, hipMemsetAsync(I->socc.p, 0, MS, s));
-    GROW(I->sgray, cs * 32);
-    HIPCHK(c, launch_gather_shadow(s, I->sray.as<spray_rt_ray>(), I->ssel.as<uint32_t>(), cs,
-                                   I->sgray.as<spray_rt_ray>()));
-    Routed S;
-    CALL(route_and_count(I, I->sgray.as<spray_rt_ray>(), cs, I->smask, I->sidx, I->sstarts, &S));
+    Routed S;  // the compacted shadow rays, read in place through ssel
+    CALL(route_and_count(I, I->sray.as<spray_rt_ray>(), cs, I->smask, I->sidx, I->sstarts, &S,
+                         I->ssel.as<uint32_t>()));
     GROW(I->sendb, S.total * kShadowRecBytes);
     GROW(I->recvb, S.recv * kShadowRecBytes);
     {
@@ -532,14 +528,17 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     }
   }
   // ---- the group's totals (WorkStats-like: one small all-reduce)
-  unsigned long long* ht = I->h_small + 8;
-  HIPCHK(c, hipMemcpyAsync(ht, I->dstats.p, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  const unsigned long long aborts = ht[0];
-  ht[0] = nrad;
-  ht[1] = nsh;
-  ht[2] = aborts;
-  HIPCHK(c, hipMemcpyAsync(I->dtot.p, ht, 3 * 8, hipMemcpyHostToDevice, s));
+  // (rays, shadows) from the host's counts, aborts from the device's shading
+  // counter: staged without a round trip, one all-reduce, one read
+  // (h_small[0, 128) holds the count exchanges; every earlier use of these
+  // two slots finished at this trace's last host read)
+  unsigned long long* hin = I->h_small + 192;  // read by the queued copy
+  unsigned long long* ht = I->h_small + 200;
+  hin[0] = nrad;
+  hin[1] = nsh;
+  HIPCHK(c, hipMemcpyAsync(I->dtot.p, hin, 2 * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(I->dtot.as<unsigned long long>() + 2, I->dstats.p, 8,
+                           hipMemcpyDeviceToDevice, s));
   CALL(I->tr->allreduce_u64(I, I->dtot.as<unsigned long long>(), 3));
   HIPCHK(c, hipMemcpyAsync(ht, I->dtot.p, 3 * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
@@ -556,7 +555,7 @@ void free_all(spray_rt_insitu* I) {
                  &I->hsam[0], &I->hsam[1], &I->mask, &I->idx, &I->starts, &I->plan_tmp,
                  &I->dcnt, &I->sendb, &I->recvb, &I->oray, &I->ow, &I->opix, &I->osam,
                  &I->ohit, &I->okey, &I->obest, &I->owin, &I->ovalid, &I->best, &I->keyback,
-                 &I->sray, &I->ssw, &I->ssv, &I->socc, &I->ssel, &I->sgray, &I->smask,
+                 &I->sray, &I->ssw, &I->ssv, &I->socc, &I->ssel, &I->smask,
                  &I->sidx, &I->sstarts, &I->ashadow, &I->aocc, &I->sret, &I->nsel,
                  &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot};
   for (DBuf* b : all)

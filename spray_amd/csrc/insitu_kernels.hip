@@ -26,7 +26,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_rad(const float4* __restrict__ 
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= n) return;
   const size_t i = size_t(idx[j]);
-  const float4 a = rays[2 * i], b = rays[2 * i + 1], c = w[i];
+  const float4 a = rays[2 * i], b = rays[2 * i + 1];
+  const float4 c = w ? w[i] : make_float4(1.f, 1.f, 1.f, 0.f);  // bounce 0: weights (1, 1, 1)
   out[3 * j] = make_float4(a.x, a.y, a.z, b.x);
   out[3 * j + 1] = make_float4(b.y, b.z, c.x, c.y);
   out[3 * j + 2] = make_float4(c.z, __int_as_float(pix[i]), __int_as_float(sam[i]), 0.f);
@@ -100,7 +101,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_rad(const float4* __restrict_
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= n) return;
   const size_t i = size_t(idx[j]);
-  const float4 a = rays[2 * i], b = rays[2 * i + 1], c = w[i];
+  const float4 a = rays[2 * i], b = rays[2 * i + 1];
+  const float4 c = w ? w[i] : make_float4(1.f, 1.f, 1.f, 0.f);
   orays[2 * j] = make_float4(a.x, a.y, a.z, kRayEpsilon);
   orays[2 * j + 1] = make_float4(b.x, b.y, b.z, kInf);
   ow[j] = make_float4(c.x, c.y, c.z, 0.f);

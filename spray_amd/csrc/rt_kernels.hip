@@ -901,6 +901,7 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tlas,
                                                   int ntlas, const int* __restrict__ owner,
                                                   int ndom, const spray_rt_ray* __restrict__ rays,
+                                                  const uint32_t* __restrict__ sel,
                                                   size_t M, uint64_t* __restrict__ out) {
   __shared__ int32_t wstack[(kBlock / 64) * kStack];
   __shared__ float4 stl[4 * 64 * W];
@@ -910,7 +911,7 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
   __syncthreads();
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= M) return;
-  const float4* rp = reinterpret_cast<const float4*>(rays + i);
+  const float4* rp = reinterpret_cast<const float4*>(rays + (sel ? sel[i] : i));
   const float4 o4 = rp[0], d4 = rp[1];
   uint64_t m[W];
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
@@ -1829,12 +1830,12 @@ hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
 }
 
 hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,
-                        const spray_rt_ray* rays, size_t M, uint64_t* out) {
+                        const spray_rt_ray* rays, size_t M, uint64_t* out, const uint32_t* sel) {
   if (M == 0) return hipSuccess;
   if (v.ndom <= 64)
-    k_route<1><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, M, out);
+    k_route<1><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, sel, M, out);
   else
-    k_route<4><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, M, out);
+    k_route<4><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, sel, M, out);
   return hipGetLastError();
 }
 
