@@ -70,6 +70,7 @@ def algorithmic_bytes(n_rays, nodes, tris, out_bytes):
 # the dominant kernels' names in the rocprofv3 summaries (profiles/)
 KERNEL_FUSED = "k_scene<1, false, false, 3, 16, 1>"  # closest hit + PT spawn + shadow any hit
 KERNEL_AO = "k_scene<1, true, false, 0, 16, 0>"      # per-lane any hit (AO rays)
+KERNEL_AO_GEN = "k_scene<1, true, false, 5, 16, 0>"  # per-lane any hit, AO rays made in the lane
 PMC = os.path.join(ROOT, "profiles", "pmc_counters.json")
 
 
@@ -261,25 +262,36 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     dev = prim.device
     stream = torch.cuda.current_stream(dev)
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
-    ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
-    src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
+    fused = bool(args.ao_fused)
     traced = bool(args.ao_traced)
-    order = None if traced else torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
+    src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
+    if fused:  # (source, sample) pairs; the any-hit lanes make the rays
+        samp = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
+    else:
+        ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
+        order = None if traced else torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
 
     def frame(ev=None):
         rt.set_coherence(rt.RAYS_COHERENT)  # camera rays: packets
         rt.intersect_scene(prim, hits)
         # the spp rays of a pixel share every sample direction (seed
         # pixid * (l + 1)): traced sample-major, they sit on neighbouring
-        # lanes -- written in that order (traced), or permuted through order
-        rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order,
-                            traced=traced)
+        # lanes -- as (source, sample) pairs (fused), written rays in that
+        # order (traced), or permuted through order
+        if fused:
+            rt.spawn_shadows_ao_pairs(prim, hits, pixid, n_prim, nsamples, src, samp, cnt)
+        else:
+            rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order,
+                                traced=traced)
         rt.set_coherence(rt.RAYS_INCOHERENT)  # hemisphere rays: one walk per lane
         if ev:
             ev[0].record(stream)
-        rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
+        if fused:
+            rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, samp, cnt, occ)
+        else:
+            rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
         if ev:
             ev[1].record(stream)
 
@@ -304,22 +316,34 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     ah_s = float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e-3
     # canonical counts of the AO rays (counting build, outside the timing)
     ctr = torch.zeros(3, dtype=torch.int64, device=dev)
-    rt.occluded_scene(ao[:n_ao * 32], occ[:n_ao], counters=ctr)
+    if fused:
+        rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, samp, cnt, occ,
+                             counters=ctr)
+    else:
+        rt.occluded_scene(ao[:n_ao * 32], occ[:n_ao], counters=ctr)
     torch.cuda.synchronize()
     idx = algorithmic_bytes(n_ao, int(ctr[0]), int(ctr[1]), 4)
-    # compulsory bytes: 32-B rays (+ 4-B trace order) in, 1 B out, the scene once
-    comp = n_ao * (32 + (0 if traced else 4) + 1) + sbytes
+    if fused:
+        # compulsory bytes: a 5-B (source, sample) pair in and 1 B out per AO
+        # ray, the source rays / hit records / pixel ids (32 + 48 + 4 B) and
+        # the scene once
+        comp = n_ao * (5 + 1) + n_prim * (32 + 48 + 4) + sbytes
+    else:
+        # 32-B rays (+ 4-B trace order) in, 1 B out, the scene once
+        comp = n_ao * (32 + (0 if traced else 4) + 1) + sbytes
     rt.set_coherence(rt.RAYS_ADAPTIVE)
     return {"value": round((n_prim + n_ao) * world * args.steps / el / 1e6, 3),
             "unit": "Mrays/s", "ms_per_step": round(el / args.steps * 1e3, 4),
             "scaling": "weak", "rays_per_step": n_prim + n_ao, "ao_rays": n_ao,
             "canonical_counts": {"nodes": int(ctr[0]), "tris": int(ctr[1]),
                                  "visits": int(ctr[2]), "rays": n_ao},
-            "roofline": roofline(KERNEL_AO, ah_s, comp, idx,
+            "roofline": roofline(KERNEL_AO_GEN if fused else KERNEL_AO, ah_s, comp, idx,
                                  "SURVEY 8(d) per-ray bytes over the AO rays' canonical counts "
                                  "(counting build of this run)"),
             "config": "configs[4] workload on one GPU: 64 domains resident, primary + "
-                      "AO-%d rays per hit traced sample-major per pixel" % nsamples}
+                      "AO-%d rays per hit traced sample-major per pixel%s"
+                      % (nsamples, ", spawned as (source, sample) pairs and generated in the "
+                                   "any-hit lanes" if fused else "")}
 
 
 def run_frame(args, dist, world, rt, cam, lights):
@@ -373,6 +397,10 @@ def run_ooc(args, rt_main, prim, n_prim, slots=4):
     dev = prim.device
     rt, oc = spray_amd.ooc_scene(SCENE, SCENES, slots, device=dev.index or 0)
     rt.set_stream(torch.cuda.current_stream(dev))
+    # drain walk form (A/B): adaptive per wave by default
+    coh = os.environ.get("SPRAY_BENCH_OOC_WALK")
+    if coh:
+        rt.set_coherence({"packet": rt.RAYS_COHERENT, "lane": rt.RAYS_INCOHERENT}[coh])
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
     shadow = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim, dtype=torch.int32, device=dev)
@@ -423,6 +451,10 @@ def main():
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
+    ap.add_argument("--ao-fused", type=int, default=0,
+                    help="1: AO rays generated in the any-hit lanes from (source, sample) pairs "
+                         "(measured slower: 5.55 vs 5.36 ms, the generation costs the any hit "
+                         "21 VGPRs and a wave per SIMD); 0: spawned rays written and read back")
     ap.add_argument("--ao-traced", type=int, default=1,
                     help="AO rays spawned in their trace order (0: compacted + order permutation)")
     ap.add_argument("--frame", type=int, default=1,

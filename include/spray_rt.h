@@ -384,6 +384,31 @@ int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t ctx, const spray_rt_ray* ray
                                      const spray_rt_hit* hits, const int32_t* pixid,
                                      size_t M, int nsamples, spray_rt_ray* out_rays,
                                      int32_t* out_src, uint32_t* d_count);
+/* The spawn of spray_rt_spawn_shadows_ao_traced without the rays: pair k of
+ * the same trace order is (out_src[k], out_sample[k]) = (source ray, sample
+ * l), k < *d_count (5 bytes per AO ray instead of 36).  nsamples <= 32;
+ * out_src / out_sample hold M * nsamples entries. */
+int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                                    const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                                    int nsamples, int32_t* out_src, uint8_t* out_sample,
+                                    uint32_t* d_count);
+/* Scene::occluded of those AO rays (ooc_shader_ao.h:114-160 spawn +
+ * scene.inl:201-209), each ray generated in its any-hit lane from
+ * (rays[src], hits[src], pixid[src], sample) with the spawn's operations --
+ * the same bits as spawn_shadows_ao_traced + occluded_scene_order(order =
+ * NULL), without writing and re-reading 32 B per ray.  occ[k], k <
+ * *d_count <= max_n.  d_counters (optional, device u64[3]): the canonical
+ * node / triangle / domain-visit counts (counting build). */
+int spray_rt_occluded_ao_pairs(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
+                               const spray_rt_hit* hits, const int32_t* pixid, size_t max_n,
+                               const int32_t* src, const uint8_t* sample,
+                               const uint32_t* d_count, uint8_t* occ,
+                               unsigned long long* d_counters);
+/* Both, one call. */
+int spray_rt_occluded_ao(spray_rt_ctx_t ctx, const spray_rt_ray* rays, const spray_rt_hit* hits,
+                         const int32_t* pixid, size_t M, int nsamples, int32_t* out_src,
+                         uint8_t* out_sample, uint32_t* d_count, uint8_t* occ,
+                         unsigned long long* d_counters);
 
 /* ---- frames: path shading, film, tiles (callers of the hot path) ---- */
 /* The shading pass of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-227) /

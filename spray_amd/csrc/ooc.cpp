@@ -269,7 +269,13 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
     return SPRAY_RT_OK;
   };
   std::vector<char> done(n, 0);
-  int r = SPRAY_RT_OK, prev_ring = -1;
+  int r = SPRAY_RT_OK;
+  int rings[4] = {0, 0, 0, 0};
+  static const int lag = [] {
+    const char* e = std::getenv("SPRAY_OOC_LAG");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 1 ? 1 : (v > 3 ? 3 : v);
+  }();
   static const bool trace = std::getenv("SPRAY_OOC_TRACE") != nullptr;  // schedule log
   if (trace)
     std::fprintf(stderr, "ooc pass %s: %zu queues, %u pairs\n", any_hit ? "any" : "closest",
@@ -314,9 +320,13 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
       o->slot[bslot[k]].released = ring;
     }
     o->drains += B.count;
-    if (S.launch > 0 && (r = absorb(S.launch - 1, prev_ring))) return r;
+    // the counts of launch (this one - lag) before the next batch is chosen:
+    // lag 1 keeps one launch queued behind the running one, lag 2 two
+    rings[S.launch % 4] = ring;
+    if (S.launch >= uint32_t(lag) &&
+        (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag) % 4])))
+      return r;
     ++S.launch;
-    prev_ring = ring;
   }
   return SPRAY_RT_OK;
 }
@@ -456,7 +466,7 @@ int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
   if ((r = build_queues(o, rays, valid, M, nullptr, occluded))) return r;
   const int W = c->ndom <= 64 ? 1 : 4;
   return drain(o, true, boxes, [&](hipStream_t s, const OocBatch& B, const OocSnapshot& S) {
-    return launch_ooc_ah_batch(s, B, W, rays, o->q, occluded, o->done, S);
+    return launch_ooc_ah_batch(s, B, W, rays, o->q, occluded, o->done, S, c->coherence);
   });
 }
 

@@ -12,6 +12,8 @@
 // position), so the result is the whole-scene one whatever the drain order.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rt_device.h"
 #include "rt_kernels.h"
 
@@ -535,22 +537,61 @@ __global__ __launch_bounds__(kBlock) void k_ooc_finish(const uint64_t* __restric
 }
 
 // Any hit of the rays queued to the batch's domains, OR-ed into occ (a ray
-// already occluded by an earlier batch is skipped).  Shadow rays diverge, so
-// each lane walks its own ray (occluded_tree_ww: while-while with postponed
-// leaves, the in-core any-hit walk) rather than the packet.  The OR is an
-// atomic on the byte's word so that exactly one writer sees the ray's first
-// occlusion and counts its pairs dead.
-template <int W>
+// already occluded by an earlier batch is skipped).  PACKET: the wave walks
+// the domain tree as a packet (trace_tree_packet<ANY>: one scalar fetch per
+// node, a lane leaves at its first occluder) -- a queue holds neighbouring
+// rays in ascending order, and point-light shadow rays of neighbouring
+// pixels are coherent; else each lane walks its own ray (occluded_tree_ww,
+// the in-core per-lane walk, for incoherent rays).  The OR is an atomic on
+// the byte's word so that exactly one writer sees the ray's first occlusion
+// and counts its pairs dead.
+template <int W, int MODE>
 __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok,
                                         const spray_rt_ray* rays, const uint32_t* idx,
-                                        const uint64_t* masks, uint8_t* occ, int32_t* stk,
-                                        uint32_t* dead) {
+                                        const uint64_t* masks, uint8_t* occ, int32_t* lstk,
+                                        int32_t* wstk, uint32_t* dead) {
   const uint32_t i = ok ? idx[pj] : 0u;
-  if (!ok || occ[i]) return;
-  const float4* rp = reinterpret_cast<const float4*>(rays + i);
-  const float4 o4 = rp[0], d4 = rp[1];
-  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  if (!occluded_tree_ww<false>(D.nodes, D.tris, r, o4.w, d4.w, stk)) return;
+  bool act = ok && !occ[i];
+  bool hit = false;
+  bool packet = MODE == 1;
+  if (MODE == 2) {  // the in-core rule: directions within ~8 degrees of the first lane's
+    float dx = 0.f, dy = 0.f, dz = 0.f;
+    if (act) {
+      const float4 d4 = reinterpret_cast<const float4*>(rays + i)[1];
+      dx = d4.x;
+      dy = d4.y;
+      dz = d4.z;
+    }
+    const uint64_t vb = __ballot(act);
+    if (!vb) return;
+    const int lead = __ffsll((long long)vb) - 1;
+    const float lx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), lead));
+    const float ly = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), lead));
+    const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), lead));
+    const float c = (dx * lx + dy * ly) + dz * lz;
+    packet = __ballot(act && !(c >= 0.99f)) == 0;
+  }
+  if (packet) {
+    if (!__ballot(act)) return;
+    float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+    if (act) {
+      const float4* rp = reinterpret_cast<const float4*>(rays + i);
+      o4 = rp[0];
+      d4 = rp[1];
+    }
+    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    Best best{0.f, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    trace_tree_packet<true>(reinterpret_cast<uint64_t>(D.nodes), reinterpret_cast<uint64_t>(D.tris),
+                            reinterpret_cast<uint64_t>(D.prims), r, o4.w, d4.w, best, act, hit,
+                            wstk);
+  } else {
+    if (!act) return;
+    const float4* rp = reinterpret_cast<const float4*>(rays + i);
+    const float4 o4 = rp[0], d4 = rp[1];
+    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    hit = occluded_tree_ww<false>(D.nodes, D.tris, r, o4.w, d4.w, lstk);
+  }
+  if (!hit) return;
   const uintptr_t a = reinterpret_cast<uintptr_t>(occ + i);
   const uint32_t sh = 8u * uint32_t(a & 3u);
   const uint32_t was = atomicOr(reinterpret_cast<uint32_t*>(a & ~uintptr_t(3)), 1u << sh);
@@ -568,12 +609,14 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
 
 // The last block to finish (done counter) publishes the live counts and
 // rearms the counter for the next launch.
-template <int W>
+template <int W, int MODE>
 __global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, uint8_t* __restrict__ occ,
     uint32_t* __restrict__ live, uint32_t* __restrict__ done, OocSnapshot S, int ndom) {
-  __shared__ int32_t stack[kStack * kBlock];  // per-lane stacks, lane-interleaved
+  // per lane: lane-interleaved stacks; packet: one stack per wave
+  __shared__ int32_t stack[MODE != 1 ? kStack * kBlock : 1];
+  __shared__ int32_t wstack[MODE != 0 ? kWaves * kStack : 1];
   __shared__ uint32_t dead[64 * W];
   __shared__ bool last;
   for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
@@ -582,7 +625,8 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(
   bool ok;
   const int s = batch_pair(B, pj, ok);
   if (s >= 0)
-    ah_pair<W>(B.d[s], pj, ok, rays, idx, masks, occ, stack + threadIdx.x, dead);
+    ah_pair<W, MODE>(B.d[s], pj, ok, rays, idx, masks, occ, stack + (MODE != 1 ? threadIdx.x : 0),
+                     wstack + (MODE != 0 ? (threadIdx.x >> 6) * kStack : 0), dead);
   flush_deaths<W>(dead, live);
   __threadfence();
   __syncthreads();
@@ -666,17 +710,36 @@ hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* h
 
 hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
                                const OocScratch& q, uint8_t* occ, uint32_t* done,
-                               OocSnapshot snap) {
+                               OocSnapshot snap, int coherence) {
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
   const int ndom = 64 * W;
   unsigned g = batch_grid(B);
   if (g == 0) g = 1;  // the last block publishes even when empty
-  if (W == 1)
-    k_ooc_ah_batch<1><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap,
-                                           ndom);
-  else
-    k_ooc_ah_batch<4><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap,
-                                           ndom);
+#define SPRAY_AH_LAUNCH(WW, MM)                                                       \
+  k_ooc_ah_batch<WW, MM><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap, \
+                                              ndom)
+  // the context's coherence setting: incoherent -> per lane, else packets
+  // (measured on configs[3]'s PT shadows, one box: packets 4.08, per lane
+  // 4.60, the per-wave choice 4.72 ms per frame -- the choice's direction
+  // loads and the two walks' registers and stacks cost more than it saves
+  // on queues of neighbouring rays; SPRAY_OOC_AH_ADAPTIVE=1 keeps it)
+  static const bool adaptive = [] {
+    const char* e = std::getenv("SPRAY_OOC_AH_ADAPTIVE");
+    return e && e[0] == '1';
+  }();
+  const int mode = coherence == SPRAY_RT_RAYS_INCOHERENT                  ? 0
+                   : (coherence == SPRAY_RT_RAYS_ADAPTIVE && adaptive) ? 2
+                                                                          : 1;
+  if (W == 1) {
+    if (mode == 0) SPRAY_AH_LAUNCH(1, 0);
+    else if (mode == 1) SPRAY_AH_LAUNCH(1, 1);
+    else SPRAY_AH_LAUNCH(1, 2);
+  } else {
+    if (mode == 0) SPRAY_AH_LAUNCH(4, 0);
+    else if (mode == 1) SPRAY_AH_LAUNCH(4, 1);
+    else SPRAY_AH_LAUNCH(4, 2);
+  }
+#undef SPRAY_AH_LAUNCH
   return hipGetLastError();
 }
 

@@ -152,6 +152,18 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
                            void* scratch, uint32_t* order = nullptr, bool traced = false);
+// AO spawn as (source, sample) pairs in the trace order of launch_spawn_ao
+// (traced); nsamples <= 32; scratch: ao_scratch_bytes(M, nsamples).
+hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
+                                 const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                                 int nsamples, int32_t* out_src, uint8_t* out_sample,
+                                 uint32_t* d_count, void* scratch);
+// any hit of those pairs' AO rays, each generated in its any-hit lane
+hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                    const spray_rt_hit* hits, const int32_t* pixid,
+                                    size_t max_n, const int32_t* src, const uint8_t* sample,
+                                    const uint32_t* d_count, uint8_t* occ,
+                                    unsigned long long* counters);
 size_t ao_scratch_bytes(size_t M, int nsamples);
 
 // ---- out-of-core path (ooc_kernels.hip) ----
@@ -233,9 +245,10 @@ hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
 hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* hits, size_t M);
 // Any hit of a batch; the pairs of newly occluded rays are counted off
 // q.live; the snapshot follows.  done: a device counter, 0 between launches.
+// coherence: SPRAY_RT_RAYS_* (the walk form, as the scene path's any hit)
 hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
                                const OocScratch& q, uint8_t* occ, uint32_t* done,
-                               OocSnapshot snap);
+                               OocSnapshot snap, int coherence);
 // frame layer (frame_kernels.hip)
 hipError_t launch_shade(hipStream_t s, const spray_rt_shader& P, const spray_rt_bsdf* bsdfs,
                         int nbsdf, int bounce, int ns, spray_rt_ray* rays,

@@ -220,6 +220,13 @@ struct SceneArgs {
   // positional mask: only rays with valid[i] != 0 are traced (occ / hits of
   // the others untouched)
   const uint8_t* valid;
+  // kEpiAoGen: ray k is AO sample ao_l[k] of source ray ao_src[k], generated
+  // in the lane (ooc::ShaderAo's spawn) instead of read from rays
+  const spray_rt_ray* ao_rays;
+  const spray_rt_hit* ao_hits;
+  const int32_t* ao_pix;
+  const int32_t* ao_src;
+  const uint8_t* ao_l;
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -243,12 +250,45 @@ constexpr int kEpiShadow = 3; // + PT spawn and the shadow ray's any hit, same l
 // ooc::ShaderPt's shading pass (k_shade, one point light, path weight 1),
 // the weight written to sw[i] for the film
 constexpr int kEpiShadowFrame = 4;
+// any hit of AO rays generated in the lane from (source ray, sample) pairs
+constexpr int kEpiAoGen = 5;
 
 // Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): one work
 // queue of the persistent launches; bands 8x .. 8x+7 (a contiguous eighth of
 // the rays) are the home queues of XCD x.
 __device__ __host__ __forceinline__ size_t band_size(size_t M) {
   return (((M + kQueues - 1) / kQueues) + 63) / 64 * 64;
+}
+
+// AO ray k of a fused spawn + any hit: sample l = ao_l[k] of source ray
+// i = ao_src[k] -- the operations of k_spawn_ao_write_hits (ao_sample's
+// prologue, the local hemisphere sample, the rotation) on the same values,
+// so the same bits as the written ray.
+__device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f& b) {
+  const uint32_t i = uint32_t(A.ao_src[k]);
+  const uint32_t l = A.ao_l[k];
+  const spray_rt_ray r = A.ao_rays[i];
+  const float ht = A.ao_hits[i].t;
+  float N[3] = {A.ao_hits[i].ns[0], A.ao_hits[i].ns[1], A.ao_hits[i].ns[2]};
+  const int32_t px = A.ao_pix[i];
+  const float o[3] = {r.dir[0] * ht + r.org[0], r.dir[1] * ht + r.org[1],
+                      r.dir[2] * ht + r.org[2]};
+  const float wo[3] = {-r.dir[0], -r.dir[1], -r.dir[2]};
+  if (!(gdot3(wo, N) > 0.0f)) {
+    N[0] = -N[0];
+    N[1] = -N[1];
+    N[2] = -N[2];
+  }
+  gnorm3(N);
+  float ax[3], ay[3];
+  hemisphere_frame(N, ax, ay);
+  uint32_t st = sampler_init1(px * int32_t(l + 1));
+  const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+  float lv[3], w[3], pdf;
+  hemisphere_local(u1, u2, lv);
+  hemisphere_apply(lv, N, ax, ay, w, pdf);
+  a = v4f{o[0], o[1], o[2], kRayEpsilon};
+  b = v4f{w[0], w[1], w[2], kInf};
 }
 
 template <int W, bool ANY, bool COUNT, int EPI>
@@ -264,14 +304,18 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   spray_rt_hit* __restrict__ hits = A.hits;
   uint8_t* __restrict__ occ = A.occ;
   {
-    const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
     v4f a, b;
-    if (SPRAY_NT_IO_LANE) {
-      a = __builtin_nontemporal_load(rp);
-      b = __builtin_nontemporal_load(rp + 1);
+    if (EPI == kEpiAoGen) {
+      ao_gen(A, i, a, b);
     } else {
-      a = rp[0];
-      b = rp[1];
+      const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
+      if (SPRAY_NT_IO_LANE) {
+        a = __builtin_nontemporal_load(rp);
+        b = __builtin_nontemporal_load(rp + 1);
+      } else {
+        a = rp[0];
+        b = rp[1];
+      }
     }
     const float4 o4 = make_float4(a.x, a.y, a.z, a.w), d4 = make_float4(b.x, b.y, b.z, b.w);
     const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
@@ -1559,6 +1603,42 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write_hits(
   }
 }
 
+// The trace order of k_spawn_ao_write_hits (traced), as (source ray, sample)
+// pairs only: src[pos] = i, samp[pos] = l -- for the fused spawn + any hit,
+// whose lanes generate the rays themselves (kEpiAoGen).
+__global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t ns,
+                                                           const uint2* __restrict__ meta,
+                                                           const uint32_t* __restrict__ tile_off,
+                                                           int32_t* __restrict__ src,
+                                                           uint8_t* __restrict__ samp) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const bool in = i < M;
+  const uint2 m = in ? meta[i] : make_uint2(0u, 0u);
+  const int lane = threadIdx.x & 63, g0 = lane & ~int(kAoGroup - 1), me = lane - g0;
+  if (__ballot(m.x != 0) == 0) return;
+  uint32_t gm[kAoGroup];
+#pragma unroll
+  for (int t = 0; t < int(kAoGroup); ++t) gm[t] = __shfl(m.x, g0 + t);
+  const uint32_t tile = in ? tile_off[blockIdx.x] : 0u;
+  const uint32_t gpos = tile + __shfl(m.y, g0);
+  uint32_t run = 0;
+  for (uint32_t l = 0; l < ns; ++l) {
+    uint32_t col = 0, before = 0;
+#pragma unroll
+    for (int t = 0; t < int(kAoGroup); ++t) {
+      const uint32_t b = (gm[t] >> l) & 1u;
+      col += b;
+      before += t < me ? b : 0u;
+    }
+    if ((m.x >> l) & 1u) {
+      const uint32_t pos = gpos + run + before;
+      src[pos] = int32_t(i);
+      samp[pos] = uint8_t(l);
+    }
+    run += col;
+  }
+}
+
 // frame counters of a fused bounce: live slots (= radiance rays) and shadows
 __global__ void k_frame_stats_add(unsigned long long* __restrict__ stats, int stripes, size_t M,
                                   const uint32_t* __restrict__ d_count) {
@@ -1639,8 +1719,11 @@ static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
 template <int W, bool ANY, int EPI, int STK>
 static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherence) {
   if (a.counters) return launch_scene_t<W, ANY, true, EPI, STK, 0>(s, a);
-  // the fused spawn / keyed closest-hit forms serve camera rays: packets
-  if constexpr (!ANY && EPI != kEpiNone) {
+  // the fused spawn / keyed closest-hit forms serve camera rays: packets;
+  // generated AO rays (hemispheres) walk per lane
+  if constexpr (ANY && EPI == kEpiAoGen) {
+    return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
+  } else if constexpr (!ANY && EPI != kEpiNone) {
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
   } else {
     switch (coherence) {
@@ -1980,6 +2063,41 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
   // more samples than a mask holds: the trace order is the output order
   if (order) k_iota<<<(npairs + kBlock - 1) / kBlock, kBlock, 0, s>>>(order, npairs);
   return hipGetLastError();
+}
+
+hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
+                                 const spray_rt_hit* hits, const int32_t* pixid, size_t M,
+                                 int nsamples, int32_t* out_src, uint8_t* out_sample,
+                                 uint32_t* d_count, void* scratch) {
+  if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+  if (nsamples > 32) return hipErrorInvalidValue;
+  const uint32_t g = uint32_t((M + kBlock - 1) / kBlock);
+  uint2* meta = static_cast<uint2*>(scratch);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(meta + M);
+  k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M), uint32_t(nsamples),
+                                          meta, tiles);
+  k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
+  k_spawn_ao_index<<<g, kBlock, 0, s>>>(uint32_t(M), uint32_t(nsamples), meta, tiles, out_src,
+                                        out_sample);
+  return hipGetLastError();
+}
+
+hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                    const spray_rt_hit* hits, const int32_t* pixid,
+                                    size_t max_n, const int32_t* src, const uint8_t* sample,
+                                    const uint32_t* d_count, uint8_t* occ,
+                                    unsigned long long* counters) {
+  if (max_n == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, nullptr, max_n);
+  a.d_count = d_count;
+  a.occ = occ;
+  a.counters = counters;
+  a.ao_rays = rays;
+  a.ao_hits = hits;
+  a.ao_pix = pixid;
+  a.ao_src = src;
+  a.ao_l = sample;
+  return launch_scene_w<true, kEpiAoGen>(s, a, v);
 }
 
 size_t ao_scratch_bytes(size_t M, int nsamples) {

@@ -404,6 +404,50 @@ class RtContext:
         self._check(lib().spray_rt_occluded_scene_order(self.h, a, int(max_rays), o, b, c),
                     "occluded_scene_order")
 
+    def occluded_ao(self, rays, hits, pixid, n, nsamples, out_src, out_sample, d_count, occ,
+                    counters=None):
+        """ooc::ShaderAo's spawn fused into the any hit (device): AO ray k of
+        the sample-major trace order is sample out_sample[k] of source ray
+        out_src[k]; occ[k] its occlusion; *d_count rays.  The rays are made in
+        the any-hit lanes, never stored."""
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        p, k3 = _addr(pixid)
+        c, k4 = _addr(out_src)
+        d, k5 = _addr(out_sample)
+        e, k6 = _addr(d_count)
+        f, k7 = _addr(occ)
+        g, k8 = _addr(counters) if counters is not None else (None, None)
+        self._check(lib().spray_rt_occluded_ao(self.h, a, b, p, int(n), int(nsamples), c, d, e,
+                                               f, g), "occluded_ao")
+
+    def spawn_shadows_ao_pairs(self, rays, hits, pixid, n, nsamples, out_src, out_sample,
+                               d_count):
+        """The traced AO spawn as (source, sample) pairs only (device)."""
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        p, k3 = _addr(pixid)
+        c, k4 = _addr(out_src)
+        d, k5 = _addr(out_sample)
+        e, k6 = _addr(d_count)
+        self._check(lib().spray_rt_spawn_shadows_ao_pairs(self.h, a, b, p, int(n), int(nsamples),
+                                                          c, d, e), "spawn_shadows_ao_pairs")
+
+    def occluded_ao_pairs(self, rays, hits, pixid, max_n, src, sample, d_count, occ,
+                          counters=None):
+        """Any hit of the AO rays of (src, sample) pairs, each generated in its
+        lane (device); occ[k], k < *d_count."""
+        a, k1 = _addr(rays)
+        b, k2 = _addr(hits)
+        p, k3 = _addr(pixid)
+        c, k4 = _addr(src)
+        d, k5 = _addr(sample)
+        e, k6 = _addr(d_count)
+        f, k7 = _addr(occ)
+        g, k8 = _addr(counters) if counters is not None else (None, None)
+        self._check(lib().spray_rt_occluded_ao_pairs(self.h, a, b, p, int(max_n), c, d, e, f, g),
+                    "occluded_ao_pairs")
+
     # ---- frame layer (shading, film, tiles) ----
     def set_bsdfs(self, bsdfs):
         """Per-domain BSDFs: a sequence of (type, p0, p1, p2) (Scene::getBsdf)."""

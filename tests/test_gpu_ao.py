@@ -105,6 +105,25 @@ def test_ao16_spawn_and_occlusion(oracle, ns):
     rt.occluded_scene_order(out3, m, None, cnt3, occ)
     rt.sync()
     assert (occ.cpu().numpy() == ref[ordh]).all()
+    if ns <= 32:
+        # fused: the rays generated in the any-hit lanes (never stored) -- the
+        # traced order's (source, sample) pairs and occlusion bits
+        fsrc = torch.full((n * ns,), -1, dtype=torch.int32, device="cuda")
+        fsam = torch.full((n * ns,), 255, dtype=torch.uint8, device="cuda")
+        fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        focc = torch.full((n * ns,), 9, dtype=torch.uint8, device="cuda")
+        rt.occluded_ao(rays, h, pixid, n, ns, fsrc, fsam, fcnt, focc)
+        rt.sync()
+        assert int(fcnt.item()) == m
+        fs = fsrc[:m].cpu().numpy()
+        assert (fs == src[ordh]).all()
+        assert (focc[:m].cpu().numpy() == ref[ordh]).all()
+        sam = fsam[:m].cpu().numpy().astype(np.int64)
+        # per source: its samples once each, in the order the spawn made them
+        key = fs.astype(np.int64) * 64 + sam
+        assert len(np.unique(key)) == m and (sam < ns).all()
+        kk = np.sort(key)
+        assert np.array_equal(kk // 64, src)
     if ns == 16:
         # a batch of >= 16 Mi rays capacity runs the persistent any-hit form
         # (kPersistAhRays); the device count bounds it to the m written rays
@@ -117,5 +136,52 @@ def test_ao16_spawn_and_occlusion(oracle, ns):
         ob = occb.cpu().numpy()
         assert (ob[:m] == ref[ordh]).all() and (ob[m:] == 9).all()
         del big, occb
+    rt.set_coherence(rt.RAYS_ADAPTIVE)
+    scene.close()
+
+
+def test_ao16_fused_full_frame():
+    """configs[4] at its benchmarked size: the whole 1024x1024x8spp frame's
+    36.6 M AO-16 rays through the fused spawn + any hit (persistent form)
+    give the traced spawn + any hit's pairs and occlusion bits (the traced
+    path is pinned to the oracle above)."""
+    import spray_amd
+    c = BENCH_CAMERA
+    scene = spray_amd.Scene(WAVELETS64, SCENES)
+    rt = scene.rt
+    cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 1024, 1024)
+    n, ns, per = 1024 * 1024 * 8, 16, 1024 * 128 * 8
+    rays = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    pix = torch.empty(n, dtype=torch.int32, device="cuda")
+    for k in range(8):
+        rt.eye_rays_ooc(cam, 1024, 8, (0, 128 * k, 1024, 128), rays[k * per * 32:(k + 1) * per * 32],
+                        pix[k * per:(k + 1) * per])
+    h = torch.empty(n * 48, dtype=torch.uint8, device="cuda")
+    rt.intersect_scene(rays, h)
+    cap = 40_000_000  # the frame spawns ~36.6 M AO rays; writes stay below *d_count
+    out = torch.empty((cap, 8), dtype=torch.float32, device="cuda")
+    osrc = torch.empty(cap, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rt.spawn_shadows_ao(rays, h, pix, n, ns, out, osrc, cnt, traced=True)
+    rt.sync()
+    m = int(cnt.item())
+    assert 30_000_000 < m <= out.shape[0]
+    rt.set_coherence(rt.RAYS_INCOHERENT)
+    occ = torch.empty(m, dtype=torch.uint8, device="cuda")
+    rt.occluded_scene_order(out, m, None, cnt, occ)
+    rt.sync()
+    ref_occ = occ.cpu().numpy()
+    ref_src = osrc[:m].cpu().numpy()
+    del out, occ
+    fsrc = torch.empty(n * ns, dtype=torch.int32, device="cuda")
+    fsam = torch.empty(n * ns, dtype=torch.uint8, device="cuda")
+    fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    focc = torch.empty(n * ns, dtype=torch.uint8, device="cuda")
+    rt.occluded_ao(rays, h, pix, n, ns, fsrc, fsam, fcnt, focc)
+    rt.sync()
+    assert int(fcnt.item()) == m
+    assert np.array_equal(fsrc[:m].cpu().numpy(), ref_src)
+    fo = focc[:m].cpu().numpy()
+    assert np.array_equal(fo, ref_occ) and 0 < fo.sum() < m
     rt.set_coherence(rt.RAYS_ADAPTIVE)
     scene.close()
