@@ -30,8 +30,9 @@ namespace {
 
 struct HostDomain {
   SlotImage img;           // layout only: the bytes live in `pinned`
-  void* pinned = nullptr;  // the image, page-locked (DMA source)
-  size_t nbytes = 0;
+  void* pinned = nullptr;  // the image, page-locked and device-mapped
+  void* dpinned = nullptr; // its device-side address (read by the copy blocks)
+  size_t nbytes = 0;       // padded to 16 B
   bool set = false;
 };
 
@@ -40,7 +41,6 @@ struct CacheSlot {
   size_t bytes = 0;
   int domain = -1;
   uint64_t used = 0;                // LRU stamp
-  int released = -1;                // launch ring entry of its last drain, -1 none
 };
 
 }  // namespace
@@ -49,8 +49,6 @@ struct spray_rt_ooc {
   spray_rt_ctx* ctx = nullptr;
   std::vector<HostDomain> dom;
   std::vector<CacheSlot> slot;
-  hipStream_t up = nullptr;
-  hipEvent_t up_done = nullptr;  // a batch's uploads done (upload stream)
   uint64_t clock = 0;
   unsigned long long loads = 0, hits = 0, bytes = 0, drains = 0;
   // queue scratch
@@ -152,9 +150,13 @@ int build_queues(spray_rt_ooc* o, const spray_rt_ray* rays, const uint8_t* valid
 }
 
 // Makes domain d resident (LruCache::load) and returns its slot.  A miss
-// queues the upload on the upload stream after the slot's last drain;
-// *uploaded tells the caller to make the compute stream wait for it.
-int acquire(spray_rt_ooc* o, int d, int* out, bool* uploaded) {
+// evicts the least recently used slot (an empty one first) and returns the
+// upload in *up (the caller issues it: copy blocks of the launch before, or
+// a DMA on the compute stream); slots in `busy` are never evicted.
+struct Upload {
+  int slot = -1, domain = -1;
+};
+int acquire(spray_rt_ooc* o, int d, const std::vector<char>& busy, int* out, Upload* up) {
   spray_rt_ctx* c = o->ctx;
   int best = -1;
   for (size_t k = 0; k < o->slot.size(); ++k)
@@ -162,31 +164,29 @@ int acquire(spray_rt_ooc* o, int d, int* out, bool* uploaded) {
   if (best >= 0) {
     ++o->hits;
   } else {
-    // victim: an empty slot, else the least recently used
     for (size_t k = 0; k < o->slot.size() && best < 0; ++k)
-      if (o->slot[k].domain < 0) best = int(k);
-    if (best < 0) {
-      best = 0;
-      for (size_t k = 1; k < o->slot.size(); ++k)
-        if (o->slot[k].used < o->slot[best].used) best = int(k);
+      if (o->slot[k].domain < 0 && !busy[k]) best = int(k);
+    if (best < 0)
+      for (size_t k = 0; k < o->slot.size(); ++k)
+        if (!busy[k] && (best < 0 || o->slot[k].used < o->slot[best].used)) best = int(k);
+    if (best < 0) {  // every slot is held by the batch before: after its launch
+      *out = -1;
+      return SPRAY_RT_OK;
     }
     CacheSlot& cs = o->slot[best];
-    const HostDomain& hd = o->dom[d];
-    const size_t n = hd.nbytes;
-    if (cs.bytes < n) {  // grow: wait for the slot's readers, reallocate
-      if (cs.released >= 0) HIPCHK(c, hipEventSynchronize(o->launch_ev[cs.released]));
+    const size_t n = o->dom[d].nbytes;
+    if (cs.bytes < n) {  // grow: every queued reader of the slot first
+      HIPCHK(c, hipStreamSynchronize(stream_of(c)));
       if (cs.dmem) HIPCHK(c, hipFree(cs.dmem));
       cs.dmem = nullptr;
       HIPCHK(c, hipMalloc(&cs.dmem, n));
       cs.bytes = n;
     }
-    // a ring entry re-recorded by a later launch only makes this wait longer
-    if (cs.released >= 0) HIPCHK(c, hipStreamWaitEvent(o->up, o->launch_ev[cs.released], 0));
-    HIPCHK(c, hipMemcpyAsync(cs.dmem, hd.pinned, n, hipMemcpyHostToDevice, o->up));
     cs.domain = d;
     ++o->loads;
     o->bytes += n;
-    *uploaded = true;
+    up->slot = best;
+    up->domain = d;
   }
   o->slot[best].used = ++o->clock;
   *out = best;
@@ -212,8 +212,12 @@ OocDomain domain_view(const spray_rt_ooc* o, int d, int k, const float* boxes) {
 // (ooc_pcontext.h:128-132: rstats_.schedule(), highest score first;
 // ooc_domain_stats.cc:60-111), the any-hit pass starting with the domains
 // the closest-hit pass left resident.  max(1, slots / 2) resident domains
-// per launch: while one batch drains, the LRU victims of the next are the
-// previous batch's slots, so its uploads overlap the drain.
+// per launch, and each launch also uploads the next batch's missing images
+// into the other slots (copy blocks reading the pinned images; the slots of
+// the launch itself are never evicted): the upload overlaps the drain on
+// the one compute stream, with no cross-stream wait.  With fewer than two
+// batches' worth of slots the upload is a DMA on the stream between the two
+// launches instead.
 //
 // A queue with no live pair left (q.live, see k_ooc_ch_batch: every queued
 // ray already has a hit nearer than the domain's entry t, or is occluded) is
@@ -221,13 +225,10 @@ OocDomain domain_view(const spray_rt_ooc* o, int d, int k, const float* boxes) {
 // of the queue when it drains it (filterRqs / filterSqs,
 // ooc_tcontext.inl:138-170) and the sweep visits domains near the camera
 // first, so most far domains die this way.  Each launch publishes its
-// counts to pinned host memory from the device (OocSnapshot); before
-// choosing batch k + 1 the host waits for launch k - 1's snapshot, which
-// has landed by the time launch k runs, so the compute stream always holds
-// the next launch.  Counts only fall, so a queue seen dead is dead for
-// certain and results equal draining everything.  (A second compute stream
-// alternating batches measured no faster with the 4-slot cache of
-// configs[3]: at most two batches' domains are resident at once.)
+// counts to pinned host memory from the device (OocSnapshot); the batch
+// after next is chosen once the previous launch's counts have landed, so
+// the compute stream always holds the next launch.  Counts only fall, so a
+// queue seen dead is dead for certain and results equal draining everything.
 template <typename Launch>
 int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch launch) {
   spray_rt_ctx* c = o->ctx;
@@ -280,11 +281,12 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   if (trace)
     std::fprintf(stderr, "ooc pass %s: %zu queues, %u pairs\n", any_hit ? "any" : "closest",
                  order.size(), o->first[n]);
-  for (;;) {
-    // the next batch: the first `per` undone queues not known dead
-    OocBatch B{};
-    int bslot[kOocBatch];
-    bool uploaded = false;
+  // the next batch: the first `per` undone queues not known dead; `busy`
+  // slots (the batch launched before it) are not evicted
+  std::vector<char> busy(o->slot.size(), 0);
+  auto pick = [&](OocBatch& B, int* bslot, std::vector<Upload>& ups) -> int {
+    B = OocBatch{};
+    ups.clear();
     for (int d : order) {
       if (done[d]) continue;
       if (live[d] == 0) {
@@ -293,40 +295,67 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
         continue;
       }
       int sl = -1;
-      if ((r = acquire(o, d, &sl, &uploaded))) return r;
+      Upload up;
+      if (int e = acquire(o, d, busy, &sl, &up)) return e;
+      if (sl < 0) break;  // no free slot until the batch before has run
+      if (up.slot >= 0) ups.push_back(up);
       B.d[B.count] = domain_view(o, d, sl, boxes.data());
       B.begin[B.count] = o->first[d];
       B.n[B.count] = o->first[d + 1] - o->first[d];
       bslot[B.count] = sl;
+      done[d] = 1;
       if (++B.count == per) break;
     }
-    if (B.count == 0) break;
-    const int ring = int(o->launches++ % spray_rt_ooc::kRing);
-    if (uploaded) {  // one wait for all of the batch's uploads
-      HIPCHK(c, hipEventRecord(o->up_done, o->up));
-      HIPCHK(c, hipStreamWaitEvent(s, o->up_done, 0));
+    return SPRAY_RT_OK;
+  };
+  auto dma = [&](const Upload& u) -> int {
+    HIPCHK(c, hipMemcpyAsync(o->slot[u.slot].dmem, o->dom[u.domain].pinned,
+                             o->dom[u.domain].nbytes, hipMemcpyHostToDevice, s));
+    return SPRAY_RT_OK;
+  };
+  OocBatch cur, nxt;
+  int cslot[kOocBatch], nslot[kOocBatch];
+  std::vector<Upload> cups, nups;
+  if ((r = pick(cur, cslot, cups))) return r;
+  for (const Upload& u : cups)  // the pass's first batch: DMA before its launch
+    if ((r = dma(u))) return r;
+  while (cur.count) {
+    std::fill(busy.begin(), busy.end(), 0);
+    for (int k = 0; k < cur.count; ++k) busy[cslot[k]] = 1;
+    if ((r = pick(nxt, nslot, nups))) return r;
+    // the next batch's uploads ride on this launch (their slots are free)
+    cur.pf_count = 0;
+    for (const Upload& u : nups) {
+      CacheSlot& cs = o->slot[u.slot];
+      cur.pf_src[cur.pf_count] = static_cast<const uint4*>(o->dom[u.domain].dpinned);
+      cur.pf_dst[cur.pf_count] = static_cast<uint4*>(cs.dmem);
+      cur.pf_n16[cur.pf_count] = uint32_t(o->dom[u.domain].nbytes / 16);
+      ++cur.pf_count;
     }
+    const int ring = int(o->launches++ % spray_rt_ooc::kRing);
     if (trace) {
       std::fprintf(stderr, "  launch %u:", S.launch);
-      for (int k = 0; k < B.count; ++k)
-        std::fprintf(stderr, " d%d q%u live%u score%llu", B.d[k].domain, B.n[k],
-                     live[B.d[k].domain], o->score[B.d[k].domain]);
-      std::fprintf(stderr, "%s\n", uploaded ? " (upload)" : "");
+      for (int k = 0; k < cur.count; ++k)
+        std::fprintf(stderr, " d%d q%u live%u score%llu", cur.d[k].domain, cur.n[k],
+                     live[cur.d[k].domain], o->score[cur.d[k].domain]);
+      std::fprintf(stderr, " (+%d prefetched)\n", cur.pf_count);
     }
-    HIPCHK(c, launch(s, B, S));
+    HIPCHK(c, launch(s, cur, S));
     HIPCHK(c, hipEventRecord(o->launch_ev[ring], s));
-    for (int k = 0; k < B.count; ++k) {
-      done[B.d[k].domain] = 1;
-      o->slot[bslot[k]].released = ring;
+    if (nxt.count == 0) {  // slots all held by this batch (small caches): pick
+      std::fill(busy.begin(), busy.end(), 0);  // again, upload after the launch
+      if ((r = pick(nxt, nslot, nups))) return r;
+      for (const Upload& u : nups)
+        if ((r = dma(u))) return r;
     }
-    o->drains += B.count;
-    // the counts of launch (this one - lag) before the next batch is chosen:
-    // lag 1 keeps one launch queued behind the running one, lag 2 two
+    o->drains += cur.count;
     rings[S.launch % 4] = ring;
     if (S.launch >= uint32_t(lag) &&
         (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag) % 4])))
       return r;
     ++S.launch;
+    cur = nxt;
+    std::copy(nslot, nslot + kOocBatch, cslot);
   }
   return SPRAY_RT_OK;
 }
@@ -361,16 +390,14 @@ int spray_rt_ooc_create(spray_rt_ctx_t c, int cache_slots, spray_rt_ooc_t* out) 
   o->ctx = c;
   o->dom.resize(c->ndom);
   o->slot.resize(cache_slots);
-  hipError_t e = hipStreamCreateWithFlags(&o->up, hipStreamNonBlocking);
-  if (e == hipSuccess)  // fine-grained: device stores reach the host while kernels run
-    e = hipHostMalloc(reinterpret_cast<void**>(&o->snap), 257 * sizeof(unsigned long long),
+  // fine-grained: device stores reach the host while kernels run
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&o->snap), 257 * sizeof(unsigned long long),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) std::memset(o->snap, 0, 257 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&o->done), sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(o->done, 0, sizeof(uint32_t));
   for (int k = 0; k < spray_rt_ooc::kRing && e == hipSuccess; ++k)
     e = hipEventCreateWithFlags(&o->launch_ev[k], hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&o->up_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     spray_rt_ooc_destroy(o);
     return fail(c, SPRAY_RT_ERR_HIP, "ooc setup: %s", hipGetErrorString(e));
@@ -391,11 +418,9 @@ int spray_rt_ooc_destroy(spray_rt_ooc_t o) {
   free_scratch(o);
   if (o->tie) (void)hipFree(o->tie);
   if (o->snap) (void)hipHostFree(o->snap);
-  if (o->up_done) (void)hipEventDestroy(o->up_done);
   if (o->done) (void)hipFree(o->done);
   for (hipEvent_t ev : o->launch_ev)
     if (ev) (void)hipEventDestroy(ev);
-  if (o->up) (void)hipStreamDestroy(o->up);
   delete o;
   return SPRAY_RT_OK;
 }
@@ -420,9 +445,12 @@ int spray_rt_ooc_set_domain(spray_rt_ooc_t o, int id, const float* verts, size_t
     if (s.domain == id) s.domain = -1;  // stale
   if (hd.pinned) HIPCHK(c, hipHostFree(hd.pinned));
   hd.pinned = nullptr;
-  HIPCHK(c, hipHostMalloc(&hd.pinned, img.bytes.size(), hipHostMallocDefault));
+  const size_t padded = (img.bytes.size() + 15) / 16 * 16;
+  HIPCHK(c, hipHostMalloc(&hd.pinned, padded, hipHostMallocMapped));
   std::memcpy(hd.pinned, img.bytes.data(), img.bytes.size());
-  hd.nbytes = img.bytes.size();
+  std::memset(static_cast<char*>(hd.pinned) + img.bytes.size(), 0, padded - img.bytes.size());
+  HIPCHK(c, hipHostGetDevicePointer(&hd.dpinned, hd.pinned, 0));
+  hd.nbytes = padded;
   hd.img = std::move(img);
   hd.img.bytes.clear();
   hd.img.bytes.shrink_to_fit();

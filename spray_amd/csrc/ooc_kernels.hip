@@ -358,6 +358,28 @@ __device__ __forceinline__ int batch_pair(const OocBatch& B, uint32_t& pj, bool&
   return s;
 }
 
+// Copy blocks of a launch (blockIdx >= B.copy0): the next batch's images,
+// pinned host memory -> HBM slot, 16-B lanes, four loads in flight per lane.
+__device__ __forceinline__ void prefetch_copy(const OocBatch& B) {
+  const uint32_t nthreads = B.ncopy * kBlock;
+  const uint32_t t = (blockIdx.x - B.copy0) * kBlock + threadIdx.x;
+  for (int e = 0; e < B.pf_count; ++e) {
+    const uint4* __restrict__ src = B.pf_src[e];
+    uint4* __restrict__ dst = B.pf_dst[e];
+    const uint32_t n = B.pf_n16[e];
+    uint32_t q = t;
+    for (; q + 3 * nthreads < n; q += 4 * nthreads) {
+      const uint4 a = src[q], b = src[q + nthreads], c = src[q + 2 * nthreads],
+                  d = src[q + 3 * nthreads];
+      dst[q] = a;
+      dst[q + nthreads] = b;
+      dst[q + 2 * nthreads] = c;
+      dst[q + 3 * nthreads] = d;
+    }
+    for (; q < n; q += nthreads) dst[q] = src[q];
+  }
+}
+
 // Liveness bookkeeping of the drains: live[d] counts the pairs of domain d's
 // queue that can still change a result -- closest hit: the domain's entry t
 // is not beyond the ray's best t (filterRqs, ooc_tcontext.inl:147: tdom <=
@@ -467,6 +489,10 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
     const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
     uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf,
     uint32_t* __restrict__ live) {
+  if (blockIdx.x >= B.copy0) {
+    prefetch_copy(B);
+    return;
+  }
   __shared__ int32_t wstack[kWaves * kStack];
   __shared__ uint32_t dead[64 * W];
   for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
@@ -623,7 +649,8 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(
   __syncthreads();
   uint32_t pj;
   bool ok;
-  const int s = batch_pair(B, pj, ok);
+  const int s = blockIdx.x >= B.copy0 ? -1 : batch_pair(B, pj, ok);
+  if (blockIdx.x >= B.copy0) prefetch_copy(B);  // then counted in `done` like the others
   if (s >= 0)
     ah_pair<W, MODE>(B.d[s], pj, ok, rays, idx, masks, occ, stack + (MODE != 1 ? threadIdx.x : 0),
                      wstack + (MODE != 0 ? (threadIdx.x >> 6) * kStack : 0), dead);
@@ -676,10 +703,22 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   return q.npair > q.pair_cap ? hipErrorOutOfMemory : hipSuccess;  // caller grows, redoes
 }
 
+static uint32_t copy_blocks() {
+  static const uint32_t n = [] {
+    const char* e = std::getenv("SPRAY_OOC_COPY_BLOCKS");
+    const int v = e ? std::atoi(e) : kOocCopyBlocks;
+    return uint32_t(v < 1 ? 1 : (v > 256 ? 256 : v));
+  }();
+  return n;
+}
+
 static unsigned batch_grid(OocBatch& B) {
+  B.ncopy = copy_blocks();
   B.wave0[0] = 0;
   for (int k = 0; k < B.count; ++k) B.wave0[k + 1] = B.wave0[k] + (B.n[k] + 63) / 64;
-  return (B.wave0[B.count] + kWaves - 1) / kWaves;
+  const unsigned g = (B.wave0[B.count] + kWaves - 1) / kWaves;
+  B.copy0 = g;
+  return g;
 }
 
 hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
@@ -688,13 +727,16 @@ hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
   const int ndom = 64 * W;
   unsigned g = batch_grid(B);
+  const unsigned gc = g + (B.pf_count ? B.ncopy : 0);
   if (g == 0) g = 1;  // the resolve publishes even when empty
-  if (W == 1)
-    k_ooc_ch_batch<1><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
-                                           q.pleaf, q.live);
-  else
-    k_ooc_ch_batch<4><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
-                                           q.pleaf, q.live);
+  if (gc) {
+    if (W == 1)
+      k_ooc_ch_batch<1><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
+                                              q.pleaf, q.live);
+    else
+      k_ooc_ch_batch<4><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
+                                              q.pleaf, q.live);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, q.val, key, q.pkey, q.pleaf, hits, q.live,
@@ -714,6 +756,7 @@ hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
   const int ndom = 64 * W;
   unsigned g = batch_grid(B);
+  g += B.pf_count ? B.ncopy : 0;
   if (g == 0) g = 1;  // the last block publishes even when empty
 #define SPRAY_AH_LAUNCH(WW, MM)                                                       \
   k_ooc_ah_batch<WW, MM><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap, \

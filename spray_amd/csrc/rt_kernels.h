@@ -234,7 +234,17 @@ struct OocBatch {
   uint32_t n[kOocBatch];
   uint32_t wave0[kOocBatch + 1];  // filled by the launcher
   int count;
+  // the next batch's domain images, copied by extra blocks of this launch
+  // from pinned host memory (device-mapped) into slots no launch of this
+  // batch reads: the upload overlaps the drain without a second stream
+  const uint4* pf_src[kOocBatch];
+  uint4* pf_dst[kOocBatch];
+  uint32_t pf_n16[kOocBatch];  // 16-B units
+  int pf_count;
+  uint32_t copy0;    // first copy block (filled by the launcher)
+  uint32_t ncopy;    // copy blocks (filled by the launcher)
 };
+constexpr int kOocCopyBlocks = 16;  // copy blocks of a launch with prefetches (default)
 // Closest hit of a batch (traversal + key atomicMin, then the winners'
 // records) over the queues of q; boxes the domain boxes.  Pairs whose ray
 // gets a nearer hit are counted off q.live; the snapshot follows.
