@@ -7,13 +7,15 @@
   blocking tiles of 1024x128, PT point-light shadow rays), the per-unit
   figures of the algorithmic-byte formula.
 * vectors_*.npz -- small ray batches with expected hit records (inputs and
-  outputs only), checked by tests/test_oracle.py on every CPU run and used by
-  the GPU parity tests.
+  outputs only), checked by tests/test_oracle.py on every CPU run and by
+  tests/test_gpu_configs.py::test_golden_vectors_on_device through the C ABI.
 
 The oracle is pinned by internal consistency (BVH == brute force bit for bit,
-float64 checker within 1e-4) and by the survey's known answers (primary hit
-fraction 0.274, 1.38 domains per ray on the 48x48 pixel-centre probe); no
-Embree output exists to pin it further ("Oracle").
+float64 checker within 1e-4), by the survey's known answers (primary hit
+fraction 0.274, 1.38 domains per ray on the 48x48 pixel-centre probe) and by
+the reference's published renders (tests/golden/reference_images.npz, made by
+make_image_fixtures.py; tests/test_image_pin.py); no Embree output exists to
+pin it further ("Oracle").
 """
 import json
 import os

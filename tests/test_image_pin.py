@@ -1,7 +1,8 @@
 """The oracle pinned to the reference's own output: its film
 renders of the two documented examples match the published images
-(tests/image_pin.py).  The GPU counterpart, tests/test_gpu_image_pin.py,
-renders the same frames on the device and requires them bit-equal to these."""
+(tests/image_pin.py).  The GPU counterpart,
+tests/test_gpu_configs.py::test_device_render_matches_published, renders the
+same frames on the device and checks them against the same images."""
 import numpy as np
 import pytest
 
