@@ -267,21 +267,22 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
-    if fused:  # (source, sample) pairs; the any-hit lanes make the rays
-        samp = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
+    if fused:  # the (pixel, sample) local hemisphere samples
+        lv = torch.empty(W * H * nsamples * 4, dtype=torch.float32, device=dev)
     else:
         ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
         order = None if traced else torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
 
     def frame(ev=None):
         rt.set_coherence(rt.RAYS_COHERENT)  # camera rays: packets
-        rt.intersect_scene(prim, hits)
         # the spp rays of a pixel share every sample direction (seed
         # pixid * (l + 1)): traced sample-major, they sit on neighbouring
         # lanes -- as (source, sample) pairs (fused), written rays in that
         # order (traced), or permuted through order
+        rt.intersect_scene(prim, hits)
         if fused:
-            rt.spawn_shadows_ao_pairs(prim, hits, pixid, n_prim, nsamples, src, samp, cnt)
+            # (source << 5 | sample) pairs; the any-hit lanes make the rays
+            rt.spawn_shadows_ao_pairs(prim, hits, pixid, n_prim, nsamples, src, lv, cnt)
         else:
             rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order,
                                 traced=traced)
@@ -289,7 +290,7 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
         if ev:
             ev[0].record(stream)
         if fused:
-            rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, samp, cnt, occ)
+            rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, lv, nsamples, cnt, occ)
         else:
             rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
         if ev:
@@ -317,17 +318,17 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     # canonical counts of the AO rays (counting build, outside the timing)
     ctr = torch.zeros(3, dtype=torch.int64, device=dev)
     if fused:
-        rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, samp, cnt, occ,
+        rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, lv, nsamples, cnt, occ,
                              counters=ctr)
     else:
         rt.occluded_scene(ao[:n_ao * 32], occ[:n_ao], counters=ctr)
     torch.cuda.synchronize()
     idx = algorithmic_bytes(n_ao, int(ctr[0]), int(ctr[1]), 4)
     if fused:
-        # compulsory bytes: a 5-B (source, sample) pair in and 1 B out per AO
+        # compulsory bytes: a 4-B (source, sample) pair in and 1 B out per AO
         # ray, the source rays / hit records / pixel ids (32 + 48 + 4 B) and
-        # the scene once
-        comp = n_ao * (5 + 1) + n_prim * (32 + 48 + 4) + sbytes
+        # the (pixel, sample) local samples (16 B) once, and the scene once
+        comp = n_ao * (4 + 1) + n_prim * (32 + 48 + 4) + W * H * nsamples * 16 + sbytes
     else:
         # 32-B rays (+ 4-B trace order) in, 1 B out, the scene once
         comp = n_ao * (32 + (0 if traced else 4) + 1) + sbytes
@@ -451,10 +452,9 @@ def main():
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
-    ap.add_argument("--ao-fused", type=int, default=0,
-                    help="1: AO rays generated in the any-hit lanes from (source, sample) pairs "
-                         "(measured slower: 5.55 vs 5.36 ms, the generation costs the any hit "
-                         "21 VGPRs and a wave per SIMD); 0: spawned rays written and read back")
+    ap.add_argument("--ao-fused", type=int, default=1,
+                    help="1: AO rays generated in the any-hit lanes from (source, sample) pairs; "
+                         "0: spawned rays written in trace order and read back")
     ap.add_argument("--ao-traced", type=int, default=1,
                     help="AO rays spawned in their trace order (0: compacted + order permutation)")
     ap.add_argument("--frame", type=int, default=1,

@@ -1056,53 +1056,56 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
 
 int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                    int nsamples, int32_t* out_src, uint8_t* out_sample,
+                                    int nsamples, uint32_t* out_pairs, float* lv,
                                     uint32_t* d_count) {
   if (!c) return SPRAY_RT_ERR_ARG;
   if (!d_count || nsamples <= 0 || nsamples > 32)
     return fail(c, SPRAY_RT_ERR_ARG, "AO pairs need 1..32 samples and a device count");
-  if (M * size_t(nsamples) > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "too many rays");
+  if (M >= (size_t(1) << 27) || M * size_t(nsamples) > 0xFFFFFFFFull)
+    return fail(c, SPRAY_RT_ERR_LIMIT, "AO pairs need M < 2^27 source rays");
   if (!is_device_ptr(d_count) ||
       (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(pixid) ||
-             !is_device_ptr(out_src) || !is_device_ptr(out_sample))))
+             !is_device_ptr(out_pairs) || !is_device_ptr(lv))))
     return fail(c, SPRAY_RT_ERR_ARG, "AO pairs need device buffers");
   HIPCHK(c, hipSetDevice(c->device));
   void* bc = c->d_block_counts;
   int r = ensure(c, &bc, &c->block_cap, ao_scratch_bytes(M, nsamples));
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
-  HIPCHK(c, launch_spawn_ao_pairs(stream_of(c), rays, hits, pixid, M, nsamples, out_src,
-                                  out_sample, d_count, c->d_block_counts));
+  HIPCHK(c, launch_spawn_ao_pairs(stream_of(c), rays, hits, pixid, M, nsamples, out_pairs, lv,
+                                  d_count, c->d_block_counts));
   return SPRAY_RT_OK;
 }
 
 int spray_rt_occluded_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                const spray_rt_hit* hits, const int32_t* pixid, size_t max_n,
-                               const int32_t* src, const uint8_t* sample,
+                               const uint32_t* pairs, const float* lv, int nsamples,
                                const uint32_t* d_count, uint8_t* occ,
                                unsigned long long* d_counters) {
-  int r = scene_common(c, src, max_n, occ);
+  int r = scene_common(c, pairs, max_n, occ);
+  if (r) return r;
+  if (nsamples <= 0 || nsamples > 32) return fail(c, SPRAY_RT_ERR_ARG, "1..32 AO samples");
   if (r) return r;
   if (max_n == 0) return SPRAY_RT_OK;
   if (max_n > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "max_n > 2^32");
   if (!d_count || !is_device_ptr(d_count) || (d_counters && !is_device_ptr(d_counters)) ||
       !is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(pixid) ||
-      !is_device_ptr(src) || !is_device_ptr(sample) || !is_device_ptr(occ))
+      !is_device_ptr(pairs) || !is_device_ptr(lv) || !is_device_ptr(occ))
     return fail(c, SPRAY_RT_ERR_ARG, "AO any hit needs device buffers and a device count");
-  HIPCHK(c, launch_occluded_ao_pairs(stream_of(c), view(c), rays, hits, pixid, max_n, src,
-                                     sample, d_count, occ, d_counters));
+  HIPCHK(c, launch_occluded_ao_pairs(stream_of(c), view(c), rays, hits, pixid, max_n, pairs, lv,
+                                     nsamples, d_count, occ, d_counters));
   return SPRAY_RT_OK;
 }
 
 int spray_rt_occluded_ao(spray_rt_ctx_t c, const spray_rt_ray* rays, const spray_rt_hit* hits,
-                         const int32_t* pixid, size_t M, int nsamples, int32_t* out_src,
-                         uint8_t* out_sample, uint32_t* d_count, uint8_t* occ,
+                         const int32_t* pixid, size_t M, int nsamples, uint32_t* out_pairs,
+                         float* lv, uint32_t* d_count, uint8_t* occ,
                          unsigned long long* d_counters) {
-  int r = spray_rt_spawn_shadows_ao_pairs(c, rays, hits, pixid, M, nsamples, out_src, out_sample,
+  int r = spray_rt_spawn_shadows_ao_pairs(c, rays, hits, pixid, M, nsamples, out_pairs, lv,
                                           d_count);
   if (r) return r;
-  return spray_rt_occluded_ao_pairs(c, rays, hits, pixid, M * size_t(nsamples), out_src,
-                                    out_sample, d_count, occ, d_counters);
+  return spray_rt_occluded_ao_pairs(c, rays, hits, pixid, M * size_t(nsamples), out_pairs, lv,
+                                    nsamples, d_count, occ, d_counters);
 }
 
 int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t c, const spray_rt_ray* rays,

@@ -152,17 +152,20 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
                            const int32_t* pixid, size_t M, int nsamples,
                            spray_rt_ray* out_rays, int32_t* out_src, uint32_t* d_count,
                            void* scratch, uint32_t* order = nullptr, bool traced = false);
-// AO spawn as (source, sample) pairs in the trace order of launch_spawn_ao
-// (traced); nsamples <= 32; scratch: ao_scratch_bytes(M, nsamples).
+// AO spawn as (source, sample) pairs i << 5 | l in the trace order of
+// launch_spawn_ao (traced); nsamples <= 32, M < 2^27; scratch:
+// ao_scratch_bytes(M, nsamples).
+// lv: the local hemisphere sample of every (pixel, l) the pairs use, as
+// float4 at pixel * nsamples + l.
 hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                 int nsamples, int32_t* out_src, uint8_t* out_sample,
+                                 int nsamples, uint32_t* out_pairs, float* lv,
                                  uint32_t* d_count, void* scratch);
 // any hit of those pairs' AO rays, each generated in its any-hit lane
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid,
-                                    size_t max_n, const int32_t* src, const uint8_t* sample,
-                                    const uint32_t* d_count, uint8_t* occ,
+                                    size_t max_n, const uint32_t* pairs, const float* lv,
+                                    int nsamples, const uint32_t* d_count, uint8_t* occ,
                                     unsigned long long* counters);
 size_t ao_scratch_bytes(size_t M, int nsamples);
 

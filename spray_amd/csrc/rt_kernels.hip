@@ -67,6 +67,10 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #ifndef SPRAY_WAVES_AH
 #define SPRAY_WAVES_AH 1
 #endif
+// the in-lane AO generation would take the any hit to 91 VGPRs (5 waves)
+#ifndef SPRAY_WAVES_AOGEN
+#define SPRAY_WAVES_AOGEN 6
+#endif
 #ifndef SPRAY_DIAG_MODE
 #define SPRAY_DIAG_MODE 0
 #endif
@@ -220,13 +224,15 @@ struct SceneArgs {
   // positional mask: only rays with valid[i] != 0 are traced (occ / hits of
   // the others untouched)
   const uint8_t* valid;
-  // kEpiAoGen: ray k is AO sample ao_l[k] of source ray ao_src[k], generated
-  // in the lane (ooc::ShaderAo's spawn) instead of read from rays
+  // kEpiAoGen: ray k is AO sample (ao_pairs[k] & 31) of source ray
+  // ao_pairs[k] >> 5, generated in the lane (ooc::ShaderAo's spawn) instead
+  // of read from rays
   const spray_rt_ray* ao_rays;
   const spray_rt_hit* ao_hits;
   const int32_t* ao_pix;
-  const int32_t* ao_src;
-  const uint8_t* ao_l;
+  const uint32_t* ao_pairs;
+  const float4* ao_lv;  // local hemisphere sample of (pixel, l) at pixel * ao_ns + l
+  int ao_ns;
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -260,17 +266,19 @@ __device__ __host__ __forceinline__ size_t band_size(size_t M) {
   return (((M + kQueues - 1) / kQueues) + 63) / 64 * 64;
 }
 
-// AO ray k of a fused spawn + any hit: sample l = ao_l[k] of source ray
-// i = ao_src[k] -- the operations of k_spawn_ao_write_hits (ao_sample's
-// prologue, the local hemisphere sample, the rotation) on the same values,
-// so the same bits as the written ray.
+// AO ray k of a fused spawn + any hit: sample l of source ray i, (i, l) =
+// (ao_pairs[k] >> 5, ao_pairs[k] & 31) -- the operations of
+// k_spawn_ao_write_hits (ao_sample's prologue, the rotation) on the same
+// values, with the local hemisphere sample (the double sincos) taken from
+// the (pixel, l) table k_spawn_ao_index wrote, so the same bits as the
+// written ray.
 __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f& b) {
-  const uint32_t i = uint32_t(A.ao_src[k]);
-  const uint32_t l = A.ao_l[k];
+  const uint32_t pr = A.ao_pairs[k];
+  const uint32_t i = pr >> 5, l = pr & 31u;
   const spray_rt_ray r = A.ao_rays[i];
   const float ht = A.ao_hits[i].t;
   float N[3] = {A.ao_hits[i].ns[0], A.ao_hits[i].ns[1], A.ao_hits[i].ns[2]};
-  const int32_t px = A.ao_pix[i];
+  const float4 l4 = A.ao_lv[size_t(A.ao_pix[i]) * uint32_t(A.ao_ns) + l];
   const float o[3] = {r.dir[0] * ht + r.org[0], r.dir[1] * ht + r.org[1],
                       r.dir[2] * ht + r.org[2]};
   const float wo[3] = {-r.dir[0], -r.dir[1], -r.dir[2]};
@@ -282,10 +290,8 @@ __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f
   gnorm3(N);
   float ax[3], ay[3];
   hemisphere_frame(N, ax, ay);
-  uint32_t st = sampler_init1(px * int32_t(l + 1));
-  const float u1 = sampler_1d(st), u2 = sampler_1d(st);
-  float lv[3], w[3], pdf;
-  hemisphere_local(u1, u2, lv);
+  const float lv[3] = {l4.x, l4.y, l4.z};
+  float w[3], pdf;
   hemisphere_apply(lv, N, ax, ay, w, pdf);
   a = v4f{o[0], o[1], o[2], kRayEpsilon};
   b = v4f{w[0], w[1], w[2], kInf};
@@ -835,7 +841,7 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
 // and per-lane for the others (any-hit only; the counting variants always
 // walk per lane, the canonical order the counts are defined on).
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
-__global__ __launch_bounds__(kBlock, ANY ? SPRAY_WAVES_AH
+__global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN : SPRAY_WAVES_AH)
                                      : (W == 1 && STK == 16
                                             ? (EPI == kEpiShadow || EPI == kEpiShadowFrame ? SPRAY_WAVES_SHADOW
                                                                  : SPRAY_WAVES_CH)
@@ -1604,13 +1610,14 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write_hits(
 }
 
 // The trace order of k_spawn_ao_write_hits (traced), as (source ray, sample)
-// pairs only: src[pos] = i, samp[pos] = l -- for the fused spawn + any hit,
+// pairs only: pairs[pos] = i << 5 | l -- for the fused spawn + any hit,
 // whose lanes generate the rays themselves (kEpiAoGen).
 __global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t ns,
                                                            const uint2* __restrict__ meta,
                                                            const uint32_t* __restrict__ tile_off,
-                                                           int32_t* __restrict__ src,
-                                                           uint8_t* __restrict__ samp) {
+                                                           uint32_t* __restrict__ pairs,
+                                                           const int32_t* __restrict__ pixid,
+                                                           float4* __restrict__ lv) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const bool in = i < M;
   const uint2 m = in ? meta[i] : make_uint2(0u, 0u);
@@ -1619,6 +1626,43 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t 
   uint32_t gm[kAoGroup];
 #pragma unroll
   for (int t = 0; t < int(kAoGroup); ++t) gm[t] = __shfl(m.x, g0 + t);
+  // the local hemisphere samples of the group's pixels, lv[pixel * ns + l]:
+  // the group's lanes share its leader pixel's (samples l = me, me + 8, ...,
+  // the union of that pixel's masks in the group); the first lane of any
+  // other pixel's run in the group draws that run's samples alone.  A pixel
+  // spread over groups is written by each, with the same values.
+  {
+    const int32_t px = in ? pixid[i] : -1;
+    int32_t gpx[kAoGroup];  // every lane takes part in the shuffles
+#pragma unroll
+    for (int t = 0; t < int(kAoGroup); ++t) gpx[t] = __shfl(px, g0 + t);
+    const int32_t lead = gpx[0];
+    uint32_t lor = 0, ror = 0;
+    int32_t prev = -2;
+#pragma unroll
+    for (int t = 0; t < int(kAoGroup); ++t) {
+      if (gpx[t] == lead) lor |= gm[t];
+      if (t >= me && gpx[t] == px) ror |= gm[t];
+      if (t == me - 1) prev = gpx[t];
+    }
+    for (uint32_t l = uint32_t(me); l < ns; l += kAoGroup)
+      if ((lor >> l) & 1u) {
+        uint32_t st = sampler_init1(lead * int32_t(l + 1));
+        const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+        float v[3];
+        hemisphere_local(u1, u2, v);
+        lv[size_t(lead) * ns + l] = make_float4(v[0], v[1], v[2], 0.f);
+      }
+    if (in && m.x && px != lead && prev != px)
+      for (uint32_t l = 0; l < ns; ++l)
+        if ((ror >> l) & 1u) {
+          uint32_t st = sampler_init1(px * int32_t(l + 1));
+          const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+          float v[3];
+          hemisphere_local(u1, u2, v);
+          lv[size_t(px) * ns + l] = make_float4(v[0], v[1], v[2], 0.f);
+        }
+  }
   const uint32_t tile = in ? tile_off[blockIdx.x] : 0u;
   const uint32_t gpos = tile + __shfl(m.y, g0);
   uint32_t run = 0;
@@ -1632,8 +1676,7 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t 
     }
     if ((m.x >> l) & 1u) {
       const uint32_t pos = gpos + run + before;
-      src[pos] = int32_t(i);
-      samp[pos] = uint8_t(l);
+      pairs[pos] = (i << 5) | l;
     }
     run += col;
   }
@@ -2067,7 +2110,7 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
 
 hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                 int nsamples, int32_t* out_src, uint8_t* out_sample,
+                                 int nsamples, uint32_t* out_pairs, float* lv,
                                  uint32_t* d_count, void* scratch) {
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
   if (nsamples > 32) return hipErrorInvalidValue;
@@ -2077,15 +2120,15 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
   k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M), uint32_t(nsamples),
                                           meta, tiles);
   k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
-  k_spawn_ao_index<<<g, kBlock, 0, s>>>(uint32_t(M), uint32_t(nsamples), meta, tiles, out_src,
-                                        out_sample);
+  k_spawn_ao_index<<<g, kBlock, 0, s>>>(uint32_t(M), uint32_t(nsamples), meta, tiles,
+                                        out_pairs, pixid, reinterpret_cast<float4*>(lv));
   return hipGetLastError();
 }
 
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid,
-                                    size_t max_n, const int32_t* src, const uint8_t* sample,
-                                    const uint32_t* d_count, uint8_t* occ,
+                                    size_t max_n, const uint32_t* pairs, const float* lv,
+                                    int nsamples, const uint32_t* d_count, uint8_t* occ,
                                     unsigned long long* counters) {
   if (max_n == 0) return hipSuccess;
   SceneArgs a = scene_args(v, nullptr, max_n);
@@ -2095,8 +2138,9 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spr
   a.ao_rays = rays;
   a.ao_hits = hits;
   a.ao_pix = pixid;
-  a.ao_src = src;
-  a.ao_l = sample;
+  a.ao_pairs = pairs;
+  a.ao_lv = reinterpret_cast<const float4*>(lv);
+  a.ao_ns = nsamples;
   return launch_scene_w<true, kEpiAoGen>(s, a, v);
 }
 

@@ -108,17 +108,18 @@ def test_ao16_spawn_and_occlusion(oracle, ns):
     if ns <= 32:
         # fused: the rays generated in the any-hit lanes (never stored) -- the
         # traced order's (source, sample) pairs and occlusion bits
-        fsrc = torch.full((n * ns,), -1, dtype=torch.int32, device="cuda")
-        fsam = torch.full((n * ns,), 255, dtype=torch.uint8, device="cuda")
+        fpair = torch.full((n * ns,), -1, dtype=torch.int32, device="cuda")
         fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
         focc = torch.full((n * ns,), 9, dtype=torch.uint8, device="cuda")
-        rt.occluded_ao(rays, h, pixid, n, ns, fsrc, fsam, fcnt, focc)
+        lv = torch.full((1024 * 1024 * ns, 4), float("nan"), dtype=torch.float32, device="cuda")
+        rt.occluded_ao(rays, h, pixid, n, ns, fpair, lv, fcnt, focc)
         rt.sync()
         assert int(fcnt.item()) == m
-        fs = fsrc[:m].cpu().numpy()
+        fp = fpair[:m].cpu().numpy().view(np.uint32)
+        fs = (fp >> 5).astype(np.int64)
         assert (fs == src[ordh]).all()
         assert (focc[:m].cpu().numpy() == ref[ordh]).all()
-        sam = fsam[:m].cpu().numpy().astype(np.int64)
+        sam = (fp & 31).astype(np.int64)
         # per source: its samples once each, in the order the spawn made them
         key = fs.astype(np.int64) * 64 + sam
         assert len(np.unique(key)) == m and (sam < ns).all()
@@ -173,14 +174,15 @@ def test_ao16_fused_full_frame():
     ref_occ = occ.cpu().numpy()
     ref_src = osrc[:m].cpu().numpy()
     del out, occ
-    fsrc = torch.empty(n * ns, dtype=torch.int32, device="cuda")
-    fsam = torch.empty(n * ns, dtype=torch.uint8, device="cuda")
+    fpair = torch.empty(n * ns, dtype=torch.int32, device="cuda")
     fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     focc = torch.empty(n * ns, dtype=torch.uint8, device="cuda")
-    rt.occluded_ao(rays, h, pix, n, ns, fsrc, fsam, fcnt, focc)
+    lv = torch.empty((1024 * 1024 * ns, 4), dtype=torch.float32, device="cuda")
+    rt.occluded_ao(rays, h, pix, n, ns, fpair, lv, fcnt, focc)
     rt.sync()
     assert int(fcnt.item()) == m
-    assert np.array_equal(fsrc[:m].cpu().numpy(), ref_src)
+    assert np.array_equal((fpair[:m].cpu().numpy().view(np.uint32) >> 5).astype(np.int32),
+                          ref_src)
     fo = focc[:m].cpu().numpy()
     assert np.array_equal(fo, ref_occ) and 0 < fo.sum() < m
     rt.set_coherence(rt.RAYS_ADAPTIVE)
