@@ -267,8 +267,9 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     occ = torch.empty(n_prim * nsamples, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
-    if fused:  # the (pixel, sample) local hemisphere samples
+    if fused:  # the (pixel, sample) local hemisphere samples, the hits' frames
         lv = torch.empty(W * H * nsamples * 4, dtype=torch.float32, device=dev)
+        rec = torch.empty(n_prim * 16, dtype=torch.float32, device=dev)
     else:
         ao = torch.empty(n_prim * nsamples * 32, dtype=torch.uint8, device=dev)
         order = None if traced else torch.empty(n_prim * nsamples, dtype=torch.int32, device=dev)
@@ -282,7 +283,7 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
         rt.intersect_scene(prim, hits)
         if fused:
             # (source << 5 | sample) pairs; the any-hit lanes make the rays
-            rt.spawn_shadows_ao_pairs(prim, hits, pixid, n_prim, nsamples, src, lv, cnt)
+            rt.spawn_shadows_ao_pairs(prim, hits, pixid, n_prim, nsamples, src, lv, rec, cnt)
         else:
             rt.spawn_shadows_ao(prim, hits, pixid, n_prim, nsamples, ao, src, cnt, order=order,
                                 traced=traced)
@@ -290,7 +291,7 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
         if ev:
             ev[0].record(stream)
         if fused:
-            rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, lv, nsamples, cnt, occ)
+            rt.occluded_ao_pairs(n_prim * nsamples, src, rec, lv, nsamples, cnt, occ)
         else:
             rt.occluded_scene_order(ao, n_prim * nsamples, order, cnt, occ)
         if ev:
@@ -318,17 +319,17 @@ def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     # canonical counts of the AO rays (counting build, outside the timing)
     ctr = torch.zeros(3, dtype=torch.int64, device=dev)
     if fused:
-        rt.occluded_ao_pairs(prim, hits, pixid, n_prim * nsamples, src, lv, nsamples, cnt, occ,
-                             counters=ctr)
+        rt.occluded_ao_pairs(n_prim * nsamples, src, rec, lv, nsamples, cnt, occ, counters=ctr)
     else:
         rt.occluded_scene(ao[:n_ao * 32], occ[:n_ao], counters=ctr)
     torch.cuda.synchronize()
     idx = algorithmic_bytes(n_ao, int(ctr[0]), int(ctr[1]), 4)
     if fused:
         # compulsory bytes: a 4-B (source, sample) pair in and 1 B out per AO
-        # ray, the source rays / hit records / pixel ids (32 + 48 + 4 B) and
-        # the (pixel, sample) local samples (16 B) once, and the scene once
-        comp = n_ao * (4 + 1) + n_prim * (32 + 48 + 4) + W * H * nsamples * 16 + sbytes
+        # ray, the 64-B frame record of each spawning source ray and the
+        # 16-B (pixel, sample) local samples once, and the scene once
+        n_src = int(torch.unique(src[:n_ao] >> 5).numel())
+        comp = n_ao * (4 + 1) + n_src * 64 + W * H * nsamples * 16 + sbytes
     else:
         # 32-B rays (+ 4-B trace order) in, 1 B out, the scene once
         comp = n_ao * (32 + (0 if traced else 4) + 1) + sbytes

@@ -386,31 +386,32 @@ int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t ctx, const spray_rt_ray* ray
                                      int32_t* out_src, uint32_t* d_count);
 /* The spawn of spray_rt_spawn_shadows_ao_traced without the rays: entry k
  * of the same trace order is out_pairs[k] = source ray << 5 | sample l,
- * k < *d_count (4 bytes per AO ray instead of 36), and lv receives the local
+ * k < *d_count (4 bytes per AO ray instead of 36); lv receives the local
  * hemisphere sample of every (pixel, l) those rays use (the sampler draw
  * and the double-precision sincos, once per pixel and sample), float4 at
- * pixid * nsamples + l.  nsamples <= 32, M < 2^27, 0 <= pixid < npix;
- * out_pairs holds M * nsamples entries, lv npix * nsamples * 4 floats. */
+ * pixid * nsamples + l, and rec the origin, normal and tangent frame of
+ * every source ray that spawns (16 floats at 16 * i).  nsamples <= 32,
+ * M < 2^27, 0 <= pixid < npix; out_pairs holds M * nsamples entries, lv
+ * npix * nsamples * 4 floats, rec M * 16 floats. */
 int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                    int nsamples, uint32_t* out_pairs, float* lv,
+                                    int nsamples, uint32_t* out_pairs, float* lv, float* rec,
                                     uint32_t* d_count);
 /* Scene::occluded of those AO rays (ooc_shader_ao.h:114-160 spawn +
  * scene.inl:201-209), each ray generated in its any-hit lane from
- * (rays[i], hits[i], lv[pixid[i] * nsamples + l]) with the spawn's operations --
+ * (rec[i], lv[pixel * nsamples + l]) with the spawn's operations --
  * the same bits as spawn_shadows_ao_traced + occluded_scene_order(order =
  * NULL), without writing and re-reading 32 B per ray.  occ[k], k <
  * *d_count <= max_n.  d_counters (optional, device u64[3]): the canonical
  * node / triangle / domain-visit counts (counting build). */
-int spray_rt_occluded_ao_pairs(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
-                               const spray_rt_hit* hits, const int32_t* pixid, size_t max_n,
-                               const uint32_t* pairs, const float* lv, int nsamples,
+int spray_rt_occluded_ao_pairs(spray_rt_ctx_t ctx, size_t max_n, const uint32_t* pairs,
+                               const float* rec, const float* lv, int nsamples,
                                const uint32_t* d_count, uint8_t* occ,
                                unsigned long long* d_counters);
 /* Both, one call. */
 int spray_rt_occluded_ao(spray_rt_ctx_t ctx, const spray_rt_ray* rays, const spray_rt_hit* hits,
                          const int32_t* pixid, size_t M, int nsamples, uint32_t* out_pairs,
-                         float* lv, uint32_t* d_count, uint8_t* occ,
+                         float* lv, float* rec, uint32_t* d_count, uint8_t* occ,
                          unsigned long long* d_counters);
 
 /* ---- frames: path shading, film, tiles (callers of the hot path) ---- */

@@ -98,9 +98,9 @@ SIGNATURES = {
     "spray_rt_spawn_shadows_ao_ordered": (I, [P, P, P, P, SZ, I, P, P, P, P]),
     "spray_rt_spawn_shadows_ao_traced": (I, [P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_occluded_scene_order": (I, [P, P, SZ, P, P, P]),
-    "spray_rt_occluded_ao": (I, [P, P, P, P, SZ, I, P, P, P, P, P]),
-    "spray_rt_spawn_shadows_ao_pairs": (I, [P, P, P, P, SZ, I, P, P, P]),
-    "spray_rt_occluded_ao_pairs": (I, [P, P, P, P, SZ, P, P, I, P, P, P]),
+    "spray_rt_occluded_ao": (I, [P, P, P, P, SZ, I, P, P, P, P, P, P]),
+    "spray_rt_spawn_shadows_ao_pairs": (I, [P, P, P, P, SZ, I, P, P, P, P]),
+    "spray_rt_occluded_ao_pairs": (I, [P, SZ, P, P, P, I, P, P, P]),
     "spray_rt_ooc_create": (I, [P, I, P]),
     "spray_rt_ooc_destroy": (I, [P]),
     "spray_rt_ooc_set_domain": (I, [P, I, P, SZ, P, SZ, P, P]),

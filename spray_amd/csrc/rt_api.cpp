@@ -1056,7 +1056,7 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
 
 int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                    int nsamples, uint32_t* out_pairs, float* lv,
+                                    int nsamples, uint32_t* out_pairs, float* lv, float* rec,
                                     uint32_t* d_count) {
   if (!c) return SPRAY_RT_ERR_ARG;
   if (!d_count || nsamples <= 0 || nsamples > 32)
@@ -1065,7 +1065,7 @@ int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
     return fail(c, SPRAY_RT_ERR_LIMIT, "AO pairs need M < 2^27 source rays");
   if (!is_device_ptr(d_count) ||
       (M && (!is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(pixid) ||
-             !is_device_ptr(out_pairs) || !is_device_ptr(lv))))
+             !is_device_ptr(out_pairs) || !is_device_ptr(lv) || !is_device_ptr(rec))))
     return fail(c, SPRAY_RT_ERR_ARG, "AO pairs need device buffers");
   HIPCHK(c, hipSetDevice(c->device));
   void* bc = c->d_block_counts;
@@ -1073,13 +1073,12 @@ int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
   HIPCHK(c, launch_spawn_ao_pairs(stream_of(c), rays, hits, pixid, M, nsamples, out_pairs, lv,
-                                  d_count, c->d_block_counts));
+                                  rec, d_count, c->d_block_counts));
   return SPRAY_RT_OK;
 }
 
-int spray_rt_occluded_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
-                               const spray_rt_hit* hits, const int32_t* pixid, size_t max_n,
-                               const uint32_t* pairs, const float* lv, int nsamples,
+int spray_rt_occluded_ao_pairs(spray_rt_ctx_t c, size_t max_n, const uint32_t* pairs,
+                               const float* rec, const float* lv, int nsamples,
                                const uint32_t* d_count, uint8_t* occ,
                                unsigned long long* d_counters) {
   int r = scene_common(c, pairs, max_n, occ);
@@ -1089,23 +1088,22 @@ int spray_rt_occluded_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
   if (max_n == 0) return SPRAY_RT_OK;
   if (max_n > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "max_n > 2^32");
   if (!d_count || !is_device_ptr(d_count) || (d_counters && !is_device_ptr(d_counters)) ||
-      !is_device_ptr(rays) || !is_device_ptr(hits) || !is_device_ptr(pixid) ||
-      !is_device_ptr(pairs) || !is_device_ptr(lv) || !is_device_ptr(occ))
+      !is_device_ptr(pairs) || !is_device_ptr(rec) || !is_device_ptr(lv) || !is_device_ptr(occ))
     return fail(c, SPRAY_RT_ERR_ARG, "AO any hit needs device buffers and a device count");
-  HIPCHK(c, launch_occluded_ao_pairs(stream_of(c), view(c), rays, hits, pixid, max_n, pairs, lv,
-                                     nsamples, d_count, occ, d_counters));
+  HIPCHK(c, launch_occluded_ao_pairs(stream_of(c), view(c), max_n, pairs, rec, lv, nsamples,
+                                     d_count, occ, d_counters));
   return SPRAY_RT_OK;
 }
 
 int spray_rt_occluded_ao(spray_rt_ctx_t c, const spray_rt_ray* rays, const spray_rt_hit* hits,
                          const int32_t* pixid, size_t M, int nsamples, uint32_t* out_pairs,
-                         float* lv, uint32_t* d_count, uint8_t* occ,
+                         float* lv, float* rec, uint32_t* d_count, uint8_t* occ,
                          unsigned long long* d_counters) {
-  int r = spray_rt_spawn_shadows_ao_pairs(c, rays, hits, pixid, M, nsamples, out_pairs, lv,
+  int r = spray_rt_spawn_shadows_ao_pairs(c, rays, hits, pixid, M, nsamples, out_pairs, lv, rec,
                                           d_count);
   if (r) return r;
-  return spray_rt_occluded_ao_pairs(c, rays, hits, pixid, M * size_t(nsamples), out_pairs, lv,
-                                    nsamples, d_count, occ, d_counters);
+  return spray_rt_occluded_ao_pairs(c, M * size_t(nsamples), out_pairs, rec, lv, nsamples,
+                                    d_count, occ, d_counters);
 }
 
 int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t c, const spray_rt_ray* rays,

@@ -156,15 +156,15 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
 // launch_spawn_ao (traced); nsamples <= 32, M < 2^27; scratch:
 // ao_scratch_bytes(M, nsamples).
 // lv: the local hemisphere sample of every (pixel, l) the pairs use, as
-// float4 at pixel * nsamples + l.
+// float4 at pixel * nsamples + l; rec: per source ray that spawns, 4 float4
+// (origin + pixel bits, normal, tangent frame).
 hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                 int nsamples, uint32_t* out_pairs, float* lv,
+                                 int nsamples, uint32_t* out_pairs, float* lv, float* rec,
                                  uint32_t* d_count, void* scratch);
 // any hit of those pairs' AO rays, each generated in its any-hit lane
-hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
-                                    const spray_rt_hit* hits, const int32_t* pixid,
-                                    size_t max_n, const uint32_t* pairs, const float* lv,
+hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
+                                    const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
                                     unsigned long long* counters);
 size_t ao_scratch_bytes(size_t M, int nsamples);

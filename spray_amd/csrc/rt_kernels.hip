@@ -227,11 +227,9 @@ struct SceneArgs {
   // kEpiAoGen: ray k is AO sample (ao_pairs[k] & 31) of source ray
   // ao_pairs[k] >> 5, generated in the lane (ooc::ShaderAo's spawn) instead
   // of read from rays
-  const spray_rt_ray* ao_rays;
-  const spray_rt_hit* ao_hits;
-  const int32_t* ao_pix;
   const uint32_t* ao_pairs;
-  const float4* ao_lv;  // local hemisphere sample of (pixel, l) at pixel * ao_ns + l
+  const float4* ao_rec;  // per source ray: (origin, pixel), normal, tangent frame
+  const float4* ao_lv;   // local hemisphere sample of (pixel, l) at pixel * ao_ns + l
   int ao_ns;
 };
 
@@ -267,33 +265,22 @@ __device__ __host__ __forceinline__ size_t band_size(size_t M) {
 }
 
 // AO ray k of a fused spawn + any hit: sample l of source ray i, (i, l) =
-// (ao_pairs[k] >> 5, ao_pairs[k] & 31) -- the operations of
-// k_spawn_ao_write_hits (ao_sample's prologue, the rotation) on the same
-// values, with the local hemisphere sample (the double sincos) taken from
-// the (pixel, l) table k_spawn_ao_index wrote, so the same bits as the
-// written ray.
+// (ao_pairs[k] >> 5, ao_pairs[k] & 31) -- the rotation of
+// k_spawn_ao_write_hits on the same values: the hit's origin, normal and
+// tangent frame from its record and the local hemisphere sample (the double
+// sincos) from the (pixel, l) table, both written by k_spawn_ao_index, so
+// the same bits as the written ray.
 __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f& b) {
   const uint32_t pr = A.ao_pairs[k];
   const uint32_t i = pr >> 5, l = pr & 31u;
-  const spray_rt_ray r = A.ao_rays[i];
-  const float ht = A.ao_hits[i].t;
-  float N[3] = {A.ao_hits[i].ns[0], A.ao_hits[i].ns[1], A.ao_hits[i].ns[2]};
-  const float4 l4 = A.ao_lv[size_t(A.ao_pix[i]) * uint32_t(A.ao_ns) + l];
-  const float o[3] = {r.dir[0] * ht + r.org[0], r.dir[1] * ht + r.org[1],
-                      r.dir[2] * ht + r.org[2]};
-  const float wo[3] = {-r.dir[0], -r.dir[1], -r.dir[2]};
-  if (!(gdot3(wo, N) > 0.0f)) {
-    N[0] = -N[0];
-    N[1] = -N[1];
-    N[2] = -N[2];
-  }
-  gnorm3(N);
-  float ax[3], ay[3];
-  hemisphere_frame(N, ax, ay);
+  const float4* rec = A.ao_rec + 4 * size_t(i);
+  const float4 op = rec[0], n4 = rec[1], x4 = rec[2], y4 = rec[3];
+  const float4 l4 = A.ao_lv[size_t(__float_as_uint(op.w)) * uint32_t(A.ao_ns) + l];
+  const float N[3] = {n4.x, n4.y, n4.z}, ax[3] = {x4.x, x4.y, x4.z}, ay[3] = {y4.x, y4.y, y4.z};
   const float lv[3] = {l4.x, l4.y, l4.z};
   float w[3], pdf;
   hemisphere_apply(lv, N, ax, ay, w, pdf);
-  a = v4f{o[0], o[1], o[2], kRayEpsilon};
+  a = v4f{op.x, op.y, op.z, kRayEpsilon};
   b = v4f{w[0], w[1], w[2], kInf};
 }
 
@@ -1356,7 +1343,7 @@ __device__ __forceinline__ AoOut ao_sample(const spray_rt_ray& ray, const spray_
 // and the weight kd * (ct / (pi * ns * pdf)) is positive exactly when a
 // colour channel is (kd >= 1/255, the factor is ~1/ns: no underflow) --
 // given a finite normalised N.  Otherwise the full sample decides.
-__device__ __forceinline__ bool ao_ok(const spray_rt_ray& ray, const spray_rt_hit& h,
+__device__ __forceinline__ bool ao_ok(const spray_rt_ray* ray, const spray_rt_hit& h,
                                       int32_t pixid, int l, int nsamples) {
   if (h.domain < 0) return false;
   float N[3] = {h.ns[0], h.ns[1], h.ns[2]};
@@ -1366,7 +1353,7 @@ __device__ __forceinline__ bool ao_ok(const spray_rt_ray& ray, const spray_rt_hi
   const float u1 = sampler_1d(st), u2 = sampler_1d(st);
   const float rr = fmaxf(fabsf(2 * u1 - 1), fabsf(2 * u2 - 1));
   if (nfin && rr < 0.999f) return (h.color & 0xFFFFFFu) != 0u;
-  return ao_sample(ray, h, pixid, l, nsamples).ok;
+  return ao_sample(*ray, h, pixid, l, nsamples).ok;  // the ray is read only here
 }
 
 // One lane per (hit, sample) pair q = i * ns + l (32-bit: the API bounds
@@ -1397,7 +1384,7 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_count(
     const uint32_t q = base + uint32_t(r * kBlock);
     const uint32_t i = q < npairs ? q / ns : 0u;
     const spray_rt_hit h = hits[i];
-    if (q < npairs && h.domain >= 0 && ao_ok(rays[i], h, pixid[i], int(q - i * ns), int(ns)))
+    if (q < npairs && h.domain >= 0 && ao_ok(rays + i, h, pixid[i], int(q - i * ns), int(ns)))
       ++c;
   }
   const uint32_t total = Reduce(tmp).Sum(c);
@@ -1424,7 +1411,7 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write(
     const uint32_t i = q < npairs ? q / ns : 0u;
     const spray_rt_hit h = hits[i];
     const bool ok =
-        q < npairs && h.domain >= 0 && ao_ok(rays[i], h, pixid[i], int(q - i * ns), int(ns));
+        q < npairs && h.domain >= 0 && ao_ok(rays + i, h, pixid[i], int(q - i * ns), int(ns));
     const unsigned long long bal = __ballot(ok);
     spre[r][threadIdx.x] = __popcll(bal & below);
     if (lane == 0) wcnt[r][wave] = __popcll(bal);
@@ -1471,10 +1458,13 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write(
 // as a sample mask plus the hit's exclusive prefix within its tile of kBlock
 // hits; the write pass (one lane per pair, coalesced stores) then needs no
 // prefix work: slot = tile offset + prefix + popcount of the mask below l.
+// rec (optional): the origin, normal and tangent frame of every hit that
+// spawns (ao_sample's prologue; 4 float4, the pixel in the first's w), read
+// by the any-hit lanes that generate the AO rays (kEpiAoGen).
 __global__ __launch_bounds__(kBlock) void k_spawn_ao_hitmask(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
     const int32_t* __restrict__ pixid, uint32_t M, uint32_t ns, uint2* __restrict__ meta,
-    uint32_t* __restrict__ tile_counts) {
+    uint32_t* __restrict__ tile_counts, float4* __restrict__ rec) {
   using Scan = hipcub::BlockScan<uint32_t, kBlock>;
   __shared__ typename Scan::TempStorage tmp;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -1482,10 +1472,30 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_hitmask(
   if (i < M) {
     const spray_rt_hit h = hits[i];
     if (h.domain >= 0) {
-      const spray_rt_ray r = rays[i];
       const int32_t px = pixid[i];
       for (uint32_t l = 0; l < ns; ++l)
-        if (ao_ok(r, h, px, int(l), int(ns))) mask |= 1u << l;
+        if (ao_ok(rays + i, h, px, int(l), int(ns))) mask |= 1u << l;
+      if (rec && mask) {
+        const spray_rt_ray r = rays[i];
+        const float ht = h.t;
+        float N[3] = {h.ns[0], h.ns[1], h.ns[2]};
+        const float o[3] = {r.dir[0] * ht + r.org[0], r.dir[1] * ht + r.org[1],
+                            r.dir[2] * ht + r.org[2]};
+        const float wo[3] = {-r.dir[0], -r.dir[1], -r.dir[2]};
+        if (!(gdot3(wo, N) > 0.0f)) {
+          N[0] = -N[0];
+          N[1] = -N[1];
+          N[2] = -N[2];
+        }
+        gnorm3(N);
+        float ax[3], ay[3];
+        hemisphere_frame(N, ax, ay);
+        float4* q = rec + 4 * size_t(i);
+        q[0] = make_float4(o[0], o[1], o[2], __uint_as_float(uint32_t(px)));
+        q[1] = make_float4(N[0], N[1], N[2], 0.f);
+        q[2] = make_float4(ax[0], ax[1], ax[2], 0.f);
+        q[3] = make_float4(ay[0], ay[1], ay[2], 0.f);
+      }
     }
   }
   uint32_t pre, total;
@@ -2090,7 +2100,7 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
     uint2* meta = static_cast<uint2*>(scratch);
     uint32_t* tiles = reinterpret_cast<uint32_t*>(meta + M);
     k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
-                                            uint32_t(nsamples), meta, tiles);
+                                            uint32_t(nsamples), meta, tiles, nullptr);
     k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
     k_spawn_ao_write_hits<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
                                                uint32_t(nsamples), meta, tiles, out_rays,
@@ -2110,7 +2120,7 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
 
 hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                 int nsamples, uint32_t* out_pairs, float* lv,
+                                 int nsamples, uint32_t* out_pairs, float* lv, float* rec,
                                  uint32_t* d_count, void* scratch) {
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
   if (nsamples > 32) return hipErrorInvalidValue;
@@ -2118,16 +2128,15 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
   uint2* meta = static_cast<uint2*>(scratch);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(meta + M);
   k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M), uint32_t(nsamples),
-                                          meta, tiles);
+                                          meta, tiles, reinterpret_cast<float4*>(rec));
   k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
   k_spawn_ao_index<<<g, kBlock, 0, s>>>(uint32_t(M), uint32_t(nsamples), meta, tiles,
                                         out_pairs, pixid, reinterpret_cast<float4*>(lv));
   return hipGetLastError();
 }
 
-hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
-                                    const spray_rt_hit* hits, const int32_t* pixid,
-                                    size_t max_n, const uint32_t* pairs, const float* lv,
+hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
+                                    const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
                                     unsigned long long* counters) {
   if (max_n == 0) return hipSuccess;
@@ -2135,10 +2144,8 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, const spr
   a.d_count = d_count;
   a.occ = occ;
   a.counters = counters;
-  a.ao_rays = rays;
-  a.ao_hits = hits;
-  a.ao_pix = pixid;
   a.ao_pairs = pairs;
+  a.ao_rec = reinterpret_cast<const float4*>(rec);
   a.ao_lv = reinterpret_cast<const float4*>(lv);
   a.ao_ns = nsamples;
   return launch_scene_w<true, kEpiAoGen>(s, a, v);

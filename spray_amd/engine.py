@@ -404,50 +404,52 @@ class RtContext:
         self._check(lib().spray_rt_occluded_scene_order(self.h, a, int(max_rays), o, b, c),
                     "occluded_scene_order")
 
-    def occluded_ao(self, rays, hits, pixid, n, nsamples, out_pairs, lv, d_count, occ,
+    def occluded_ao(self, rays, hits, pixid, n, nsamples, out_pairs, lv, rec, d_count, occ,
                     counters=None):
         """ooc::ShaderAo's spawn fused into the any hit (device): AO ray k of
         the sample-major trace order is sample out_pairs[k] & 31 of source ray
         out_pairs[k] >> 5; occ[k] its occlusion; *d_count rays.  The rays are
         made in the any-hit lanes, never stored; lv (float32, npix * nsamples
-        * 4) holds the (pixel, sample) local hemisphere samples."""
+        * 4) holds the (pixel, sample) local hemisphere samples, rec (float32,
+        n * 16) the source rays' origins and frames."""
         a, k1 = _addr(rays)
         b, k2 = _addr(hits)
         p, k3 = _addr(pixid)
         c, k4 = _addr(out_pairs)
         d, k5 = _addr(lv)
+        r, k9 = _addr(rec)
         e, k6 = _addr(d_count)
         f, k7 = _addr(occ)
         g, k8 = _addr(counters) if counters is not None else (None, None)
-        self._check(lib().spray_rt_occluded_ao(self.h, a, b, p, int(n), int(nsamples), c, d, e,
-                                               f, g), "occluded_ao")
+        self._check(lib().spray_rt_occluded_ao(self.h, a, b, p, int(n), int(nsamples), c, d, r,
+                                               e, f, g), "occluded_ao")
 
-    def spawn_shadows_ao_pairs(self, rays, hits, pixid, n, nsamples, out_pairs, lv, d_count):
+    def spawn_shadows_ao_pairs(self, rays, hits, pixid, n, nsamples, out_pairs, lv, rec,
+                               d_count):
         """The traced AO spawn as (source << 5 | sample) pairs plus the
-        (pixel, sample) local hemisphere samples lv (device)."""
+        (pixel, sample) local hemisphere samples lv and the source rays'
+        origins / frames rec (device)."""
         a, k1 = _addr(rays)
         b, k2 = _addr(hits)
         p, k3 = _addr(pixid)
         c, k4 = _addr(out_pairs)
         d, k5 = _addr(lv)
+        r, k7 = _addr(rec)
         e, k6 = _addr(d_count)
         self._check(lib().spray_rt_spawn_shadows_ao_pairs(self.h, a, b, p, int(n), int(nsamples),
-                                                          c, d, e), "spawn_shadows_ao_pairs")
+                                                          c, d, r, e), "spawn_shadows_ao_pairs")
 
-    def occluded_ao_pairs(self, rays, hits, pixid, max_n, pairs, lv, nsamples, d_count, occ,
-                          counters=None):
+    def occluded_ao_pairs(self, max_n, pairs, rec, lv, nsamples, d_count, occ, counters=None):
         """Any hit of the AO rays of (source << 5 | sample) pairs, each
-        generated in its lane (device); occ[k], k < *d_count."""
-        a, k1 = _addr(rays)
-        b, k2 = _addr(hits)
-        p, k3 = _addr(pixid)
+        generated in its lane from rec / lv (device); occ[k], k < *d_count."""
         c, k4 = _addr(pairs)
+        r, k9 = _addr(rec)
         d, k5 = _addr(lv)
         e, k6 = _addr(d_count)
         f, k7 = _addr(occ)
         g, k8 = _addr(counters) if counters is not None else (None, None)
-        self._check(lib().spray_rt_occluded_ao_pairs(self.h, a, b, p, int(max_n), c, d,
-                                                     int(nsamples), e, f, g), "occluded_ao_pairs")
+        self._check(lib().spray_rt_occluded_ao_pairs(self.h, int(max_n), c, r, d, int(nsamples),
+                                                     e, f, g), "occluded_ao_pairs")
 
     # ---- frame layer (shading, film, tiles) ----
     def set_bsdfs(self, bsdfs):

@@ -112,7 +112,8 @@ def test_ao16_spawn_and_occlusion(oracle, ns):
         fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
         focc = torch.full((n * ns,), 9, dtype=torch.uint8, device="cuda")
         lv = torch.full((1024 * 1024 * ns, 4), float("nan"), dtype=torch.float32, device="cuda")
-        rt.occluded_ao(rays, h, pixid, n, ns, fpair, lv, fcnt, focc)
+        rec = torch.empty((n, 16), dtype=torch.float32, device="cuda")
+        rt.occluded_ao(rays, h, pixid, n, ns, fpair, lv, rec, fcnt, focc)
         rt.sync()
         assert int(fcnt.item()) == m
         fp = fpair[:m].cpu().numpy().view(np.uint32)
@@ -178,7 +179,8 @@ def test_ao16_fused_full_frame():
     fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     focc = torch.empty(n * ns, dtype=torch.uint8, device="cuda")
     lv = torch.empty((1024 * 1024 * ns, 4), dtype=torch.float32, device="cuda")
-    rt.occluded_ao(rays, h, pix, n, ns, fpair, lv, fcnt, focc)
+    rec = torch.empty((n, 16), dtype=torch.float32, device="cuda")
+    rt.occluded_ao(rays, h, pix, n, ns, fpair, lv, rec, fcnt, focc)
     rt.sync()
     assert int(fcnt.item()) == m
     assert np.array_equal((fpair[:m].cpu().numpy().view(np.uint32) >> 5).astype(np.int32),
