@@ -21,6 +21,12 @@ namespace spray_rt {
 namespace {
 
 constexpr int kWaves = kBlock / 64;
+// adaptive any-hit drains: the largest id span of a wave's rays that still
+// walks as a packet (8 pixels x 8 spp = 64 consecutive camera rays)
+#ifndef SPRAY_OOC_PACKET_SPAN
+#define SPRAY_OOC_PACKET_SPAN 1024
+#endif
+constexpr uint32_t kOocPacketSpan = SPRAY_OOC_PACKET_SPAN;
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
   uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
@@ -386,12 +392,14 @@ __device__ __forceinline__ void prefetch_copy(const OocBatch& B) {
 // the ray's t); any hit: the ray is not occluded yet (filterSqs, :165).  It
 // starts at the queue length; a ray whose best t drops from `to` to `tn`
 // kills exactly its pairs with entry t in (tn, to], and a ray's first
-// occlusion kills all of its pairs, so each pair is counted down once.  Per
-// block the deaths are summed in LDS, one global atomic per domain.
+// occlusion kills all of its pairs, so each pair is counted down once.  A
+// lane collects its killed domains as a mask; the wave sums the masks per
+// domain (one ballot each) and adds once per domain in LDS -- the lanes of a
+// wave mostly kill the same domains, and same-address LDS atomics
+// serialise -- and the block adds once per domain globally.
 template <int W>
-__device__ __forceinline__ void count_deaths(const uint64_t* m, const float* boxes,
-                                             const DRay& dr, float tn, float to,
-                                             uint32_t* dead) {
+__device__ __forceinline__ void death_mask(const uint64_t* m, const float* boxes,
+                                           const DRay& dr, float tn, float to, uint64_t* dm) {
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     uint64_t bits = m[w];
@@ -400,7 +408,22 @@ __device__ __forceinline__ void count_deaths(const uint64_t* m, const float* box
       bits &= bits - 1;
       float te;
       if (aabb_ref(boxes + 6 * (64 * w + j), dr, te) && te > tn && !(te > to))
-        atomicAdd(dead + 64 * w + j, 1u);
+        dm[w] |= 1ull << j;
+    }
+  }
+}
+
+// every lane of the wave calls this (converged)
+template <int W>
+__device__ __forceinline__ void wave_add_deaths(const uint64_t* dm, uint32_t* dead) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t u = wave_or64(dm[w]);
+    while (u) {
+      const int j = __ffsll((long long)u) - 1;
+      u &= u - 1;
+      const uint32_t n = uint32_t(__popcll(__ballot((dm[w] >> j) & 1ull)));
+      if ((threadIdx.x & 63) == 0) atomicAdd(dead + 64 * w + j, n);
     }
   }
 }
@@ -464,23 +487,28 @@ __device__ __forceinline__ void ch_pair(const OocDomain& D, uint32_t pj, bool va
                              reinterpret_cast<uint64_t>(D.tris),
                              reinterpret_cast<uint64_t>(D.prims), r, o4.w, 0.f, best, act, hit,
                              stack);
-  if (!valid) return;
-  uint64_t mine = kOocMissKey;
-  if (best.leaf != 0xFFFFFFFFu) {
-    uint64_t m[W];
+  uint64_t dm[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
-    mine = (uint64_t(__float_as_uint(best.t)) << 32) |
-           (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
-    const uint64_t old =
-        atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
-    if (mine < old) {
-      const float to = old == kOocMissKey ? kInf : __uint_as_float(uint32_t(old >> 32));
-      if (best.t < to) count_deaths<W>(m, boxes, dr, best.t, to, dead);
+  for (int w = 0; w < W; ++w) dm[w] = 0;
+  if (valid) {
+    uint64_t mine = kOocMissKey;
+    if (best.leaf != 0xFFFFFFFFu) {
+      uint64_t m[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
+      mine = (uint64_t(__float_as_uint(best.t)) << 32) |
+             (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
+      const uint64_t old =
+          atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
+      if (mine < old) {
+        const float to = old == kOocMissKey ? kInf : __uint_as_float(uint32_t(old >> 32));
+        if (best.t < to) death_mask<W>(m, boxes, dr, best.t, to, dm);
+      }
     }
+    pkey[pj] = mine;
+    pleaf[pj] = best.leaf;
   }
-  pkey[pj] = mine;
-  pleaf[pj] = best.leaf;
+  wave_add_deaths<W>(dm, dead);
 }
 
 template <int W>
@@ -580,57 +608,52 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
   bool act = ok && !occ[i];
   bool hit = false;
   bool packet = MODE == 1;
-  if (MODE == 2) {  // the in-core rule: directions within ~8 degrees of the first lane's
-    float dx = 0.f, dy = 0.f, dz = 0.f;
-    if (act) {
-      const float4 d4 = reinterpret_cast<const float4*>(rays + i)[1];
-      dx = d4.x;
-      dy = d4.y;
-      dz = d4.z;
-    }
-    const uint64_t vb = __ballot(act);
-    if (!vb) return;
-    const int lead = __ffsll((long long)vb) - 1;
-    const float lx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), lead));
-    const float ly = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), lead));
-    const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), lead));
-    const float c = (dx * lx + dy * ly) + dz * lz;
-    packet = __ballot(act && !(c >= 0.99f)) == 0;
-  }
-  if (packet) {
-    if (!__ballot(act)) return;
-    float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-    if (act) {
-      const float4* rp = reinterpret_cast<const float4*>(rays + i);
-      o4 = rp[0];
-      d4 = rp[1];
-    }
-    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-    Best best{0.f, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    trace_tree_packet<true>(reinterpret_cast<uint64_t>(D.nodes), reinterpret_cast<uint64_t>(D.tris),
-                            reinterpret_cast<uint64_t>(D.prims), r, o4.w, d4.w, best, act, hit,
-                            wstk);
-  } else {
-    if (!act) return;
+  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+  if (act) {
     const float4* rp = reinterpret_cast<const float4*>(rays + i);
-    const float4 o4 = rp[0], d4 = rp[1];
-    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    o4 = rp[0];
+    d4 = rp[1];
+  }
+  if (MODE == 2) {
+    // packets for neighbouring rays: the wave's queue entries (ascending ray
+    // ids) span few rays, and the directions are within ~8 degrees of the
+    // first lane's (the in-core rule); a far domain's sparse queue walks
+    // per lane
+    const uint64_t vb = __ballot(act);
+    const int lead = vb ? __ffsll((long long)vb) - 1 : 0;
+    const int last = vb ? 63 - __clzll((long long)vb) : 0;
+    const uint32_t span = uint32_t(__builtin_amdgcn_readlane(int(i), last)) -
+                          uint32_t(__builtin_amdgcn_readlane(int(i), lead));
+    const float lx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d4.x), lead));
+    const float ly = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d4.y), lead));
+    const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d4.z), lead));
+    const float c = (d4.x * lx + d4.y * ly) + d4.z * lz;
+    packet = span <= kOocPacketSpan && __ballot(act && !(c >= 0.99f)) == 0;
+  }
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  if (packet) {
+    Best best{0.f, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (__ballot(act))
+      trace_tree_packet<true>(reinterpret_cast<uint64_t>(D.nodes),
+                              reinterpret_cast<uint64_t>(D.tris),
+                              reinterpret_cast<uint64_t>(D.prims), r, o4.w, d4.w, best, act, hit,
+                              wstk);
+  } else if (act) {
     hit = occluded_tree_ww<false>(D.nodes, D.tris, r, o4.w, d4.w, lstk);
   }
-  if (!hit) return;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(occ + i);
-  const uint32_t sh = 8u * uint32_t(a & 3u);
-  const uint32_t was = atomicOr(reinterpret_cast<uint32_t*>(a & ~uintptr_t(3)), 1u << sh);
-  if ((was >> sh) & 0xFFu) return;  // another writer was first
+  uint64_t dm[W];
 #pragma unroll
-  for (int w = 0; w < W; ++w) {
-    uint64_t bits = masks[size_t(i) * W + w];
-    while (bits) {
-      const int j = __ffsll((long long)bits) - 1;
-      bits &= bits - 1;
-      atomicAdd(dead + 64 * w + j, 1u);
+  for (int w = 0; w < W; ++w) dm[w] = 0;
+  if (hit) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(occ + i);
+    const uint32_t sh = 8u * uint32_t(a & 3u);
+    const uint32_t was = atomicOr(reinterpret_cast<uint32_t*>(a & ~uintptr_t(3)), 1u << sh);
+    if (!((was >> sh) & 0xFFu)) {  // the first writer counts the ray's pairs dead
+#pragma unroll
+      for (int w = 0; w < W; ++w) dm[w] = masks[size_t(i) * W + w];
     }
   }
+  wave_add_deaths<W>(dm, dead);
 }
 
 // The last block to finish (done counter) publishes the live counts and

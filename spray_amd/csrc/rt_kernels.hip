@@ -844,7 +844,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   __shared__ float4 stl[4 * 64 * W];   // top-level tree
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
-  __shared__ int32_t wstack[(kBlock / 64) * kStack];  // top-level stacks, one per wave
+  // top-level / packet stacks, one per wave: STK entries suffice (the launch
+  // picks STK >= every resident tree's depth and the top-level tree's), and
+  // at STK 16 the any-hit kernels' 23.3 KB of LDS let 7 blocks share a CU
+  __shared__ int32_t wstack[(kBlock / 64) * STK];
   constexpr bool kShadow = EPI == kEpiShadow || EPI == kEpiShadowFrame;
   __shared__ float sq_ray[kShadow ? (kBlock / 64) * kShadowQ * 6 : 1];
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
@@ -862,7 +865,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   __syncthreads();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
   int32_t* stk = stack + threadIdx.x;
-  int32_t* wstk = wstack + (threadIdx.x >> 6) * kStack;
+  int32_t* wstk = wstack + (threadIdx.x >> 6) * STK;
   bool flag = false;
   float pos[3], wi[3];
   const bool persist = ANY ? (SPRAY_PERSIST_AH != 0 || A.persist != 0) : SPRAY_PERSIST_CH != 0;
