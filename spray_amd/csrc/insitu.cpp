@@ -314,7 +314,8 @@ struct Routed {
 };
 
 int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf& mask, DBuf& idx,
-                    DBuf& starts, Routed* R, const uint32_t* sel = nullptr) {
+                    DBuf& starts, Routed* R, const uint32_t* sel = nullptr,
+                    const uint8_t* valid = nullptr) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
   const int W = I->world;
@@ -323,7 +324,7 @@ int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf
   GROW(starts, (W + 1) * 8);
   GROW(I->plan_tmp, plan_temp_bytes(n, W));
   GROW(I->dcnt, 128 * 8);
-  if (n) HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, mask.as<uint64_t>(), sel));
+  if (n) HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, mask.as<uint64_t>(), sel, valid));
   HIPCHK(c, launch_plan(s, mask.as<uint64_t>(), n, W, idx.as<int64_t>(), starts.as<int64_t>(),
                         I->plan_tmp.p));
   HIPCHK(c, launch_counts_from_starts(s, starts.as<int64_t>(), W, I->dcnt.as<int64_t>()));
@@ -375,7 +376,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
   const float* hw = nullptr;  // bounce 0: the packers write weights (1, 1, 1)
   size_t hn = n;
   int cur = 0;
-  unsigned long long nrad = 0, nsh = 0;
+  unsigned long long nrad = 0;
   for (int b = 0; b < P->bounces; ++b) {
     nrad += hn;
     // ---- radiance rays to the owners of their domains
@@ -443,34 +444,49 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
                            I->opix.as<int32_t>(), I->osam.as<int32_t>(), m,
                            I->sray.as<spray_rt_ray>(), I->ssw.as<float>(), I->ssv.as<uint8_t>(),
                            I->dstats.as<unsigned long long>(), 1));
-    // ---- shadow slots and next radiance rays, compacted (one host read)
-    size_t t1 = 0, t2 = 0;
-    HIPCHK(c, launch_select_flagged(s, nullptr, MS, nullptr, nullptr, nullptr, &t1));
-    HIPCHK(c, launch_select_flagged(s, nullptr, m, nullptr, nullptr, nullptr, &t2));
-    GROW(I->sel_tmp, std::max(t1, t2));
-    GROW(I->ssel, MS * 4);
-    GROW(I->nsel, m * 4);
-    uint32_t* dnum = I->dnum.as<uint32_t>();
-    HIPCHK(c, launch_select_flagged(s, I->ssv.as<uint8_t>(), MS, I->ssel.as<uint32_t>(), dnum,
-                                    I->sel_tmp.p, &t1));
+    // ---- shadow slots and next radiance rays.  One shadow slot per copy
+    // (PT): the slots are routed in place, invalid ones owning no rank -- no
+    // compaction and no host read.  Several (AO): compacted first (the
+    // count is read); so are the next bounce's radiance rays.
     const bool more = b + 1 < P->bounces;
-    if (more)
-      HIPCHK(c, launch_select_flagged(s, I->ovalid.as<uint8_t>(), m, I->nsel.as<uint32_t>(),
-                                      dnum + 1, I->sel_tmp.p, &t2));
-    else
-      HIPCHK(c, hipMemsetAsync(dnum + 1, 0, 4, s));
-    HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    ++I->st[3];
-    uint32_t cnt2[2];
-    std::memcpy(cnt2, I->h_small, 8);
-    const size_t cs = cnt2[0], cn = cnt2[1];
-    nsh += cs;
+    const bool slots_direct = ns == 1;
+    size_t cs = 0, cn = 0;
+    if (!slots_direct || more) {
+      size_t t1 = 0, t2 = 0;
+      HIPCHK(c, launch_select_flagged(s, nullptr, MS, nullptr, nullptr, nullptr, &t1));
+      HIPCHK(c, launch_select_flagged(s, nullptr, m, nullptr, nullptr, nullptr, &t2));
+      GROW(I->sel_tmp, std::max(t1, t2));
+      GROW(I->ssel, MS * 4);
+      GROW(I->nsel, m * 4);
+      uint32_t* dnum = I->dnum.as<uint32_t>();
+      if (!slots_direct)
+        HIPCHK(c, launch_select_flagged(s, I->ssv.as<uint8_t>(), MS, I->ssel.as<uint32_t>(), dnum,
+                                        I->sel_tmp.p, &t1));
+      else
+        HIPCHK(c, hipMemsetAsync(dnum, 0, 4, s));
+      if (more)
+        HIPCHK(c, launch_select_flagged(s, I->ovalid.as<uint8_t>(), m, I->nsel.as<uint32_t>(),
+                                        dnum + 1, I->sel_tmp.p, &t2));
+      else
+        HIPCHK(c, hipMemsetAsync(dnum + 1, 0, 4, s));
+      HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(c, hipStreamSynchronize(s));
+      ++I->st[3];
+      uint32_t cnt2[2];
+      std::memcpy(cnt2, I->h_small, 8);
+      cs = cnt2[0];
+      cn = cnt2[1];
+    }
     // ---- shadow rays to the owners of their domains, occlusion OR-ed back
     if (MS) HIPCHK(c, hipMemsetAsync(I->socc.p, 0, MS, s));
-    Routed S;  // the compacted shadow rays, read in place through ssel
-    CALL(route_and_count(I, I->sray.as<spray_rt_ray>(), cs, I->smask, I->sidx, I->sstarts, &S,
-                         I->ssel.as<uint32_t>()));
+    Routed S;  // the shadow rays, read in place (through ssel when compacted)
+    const uint32_t* ssel = slots_direct ? nullptr : I->ssel.as<uint32_t>();
+    if (slots_direct)
+      CALL(route_and_count(I, I->sray.as<spray_rt_ray>(), MS, I->smask, I->sidx, I->sstarts, &S,
+                           nullptr, I->ssv.as<uint8_t>()));
+    else
+      CALL(route_and_count(I, I->sray.as<spray_rt_ray>(), cs, I->smask, I->sidx, I->sstarts, &S,
+                           ssel));
     GROW(I->sendb, S.total * kShadowRecBytes);
     GROW(I->recvb, S.recv * kShadowRecBytes);
     {
@@ -478,7 +494,6 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
       const size_t a0 = sdir ? S.self_send : S.total, a1 = sdir ? S.self_send + S.self_n : S.total;
       const size_t b0 = sdir ? S.self_recv : S.recv, b1 = sdir ? S.self_recv + S.self_n : S.recv;
       const spray_rt_ray* sr = I->sray.as<spray_rt_ray>();
-      const uint32_t* ssel = I->ssel.as<uint32_t>();
       const int64_t* six = I->sidx.as<int64_t>();
       char* sbp = static_cast<char*>(I->sendb.p);
       char* rbp = static_cast<char*>(I->recvb.p);
@@ -498,8 +513,8 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
       HIPCHK(c, launch_scene_occluded(s, view(c), I->ashadow.as<spray_rt_ray>(), S.recv, nullptr,
                                       I->aocc.as<uint8_t>(), nullptr));
     CALL(exchange(I, S, 1, true, I->aocc.p, I->sret.p));
-    HIPCHK(c, launch_occ_return(s, I->sidx.as<int64_t>(), I->sret.as<uint8_t>(), S.total,
-                                I->ssel.as<uint32_t>(), I->socc.as<uint8_t>()));
+    HIPCHK(c, launch_occ_return(s, I->sidx.as<int64_t>(), I->sret.as<uint8_t>(), S.total, ssel,
+                                I->socc.as<uint8_t>()));
     // ---- film of the copies this rank shaded
     HIPCHK(c, launch_film_atomic(s, image, I->opix.as<int32_t>(), m, ns, I->ssw.as<float>(),
                                  I->ssv.as<uint8_t>(), I->socc.as<uint8_t>(), scale));
@@ -528,15 +543,16 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     }
   }
   // ---- the group's totals (WorkStats-like: one small all-reduce)
-  // (rays, shadows) from the host's counts, aborts from the device's shading
-  // counter: staged without a round trip, one all-reduce, one read
+  // rays from the host's counts, shadows and aborts from the device's
+  // shading counters: staged without a round trip, one all-reduce, one read
   // (h_small[0, 128) holds the count exchanges; every earlier use of these
   // two slots finished at this trace's last host read)
   unsigned long long* hin = I->h_small + 192;  // read by the queued copy
   unsigned long long* ht = I->h_small + 200;
   hin[0] = nrad;
-  hin[1] = nsh;
-  HIPCHK(c, hipMemcpyAsync(I->dtot.p, hin, 2 * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(I->dtot.p, hin, 8, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(I->dtot.as<unsigned long long>() + 1,
+                           I->dstats.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(c, hipMemcpyAsync(I->dtot.as<unsigned long long>() + 2, I->dstats.p, 8,
                            hipMemcpyDeviceToDevice, s));
   CALL(I->tr->allreduce_u64(I, I->dtot.as<unsigned long long>(), 3));

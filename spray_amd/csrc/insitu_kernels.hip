@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_shadow(const float4* __restrict
                                                         size_t n, float* __restrict__ out) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= n) return;
-  const size_t slot = sel[idx[j]];
+  const size_t slot = sel ? sel[idx[j]] : size_t(idx[j]);  // sel null: idx are slots
   const float4 a = sh[2 * slot], b = sh[2 * slot + 1];
   float2* o = reinterpret_cast<float2*>(out + 6 * j);
   o[0] = make_float2(a.x, a.y);
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_shadow_self(const float4* __r
                                                                float4* __restrict__ rays) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= n) return;
-  const size_t slot = sel[idx[j]];
+  const size_t slot = sel ? sel[idx[j]] : size_t(idx[j]);  // sel null: idx are slots
   const float4 a = sh[2 * slot], b = sh[2 * slot + 1];
   rays[2 * j] = make_float4(a.x, a.y, a.z, kRayEpsilon);
   rays[2 * j + 1] = make_float4(b.x, b.y, b.z, kInf);
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_occ_return(const int64_t* __restrict
                                                        uint8_t* __restrict__ occ) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= n) return;
-  if (ret[j]) occ[sel[idx[j]]] = 1;
+  if (ret[j]) occ[sel ? sel[idx[j]] : size_t(idx[j])] = 1;
 }
 
 // HdrImage::add of the unoccluded shadows of the copies this rank shaded

@@ -102,10 +102,12 @@ hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
                                         spray_rt_hit* hits, uint64_t* keys);
 // out[i] = OR over the ray's domain list of (1 << owner[domain]); owner < 0:
 // unowned.  owner: device int[ndom], ranks < 64.  sel (optional): ray i is
-// rays[sel[i]].
+// rays[sel[i]]; valid (optional): only slots with valid[i] hold a ray (mask
+// 0 elsewhere), their number added to *nvalid (optional).
 hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,
                         const spray_rt_ray* rays, size_t M, uint64_t* out,
-                        const uint32_t* sel = nullptr);
+                        const uint32_t* sel = nullptr, const uint8_t* valid = nullptr,
+                        unsigned long long* nvalid = nullptr);
 hipError_t launch_eye_rays_insitu(hipStream_t s, const float* cam14, int image_w,
                                   int spp, int bx, int by, int bw, int tx, int ty,
                                   int tw, int th, spray_rt_ray* rays, int32_t* pixid,

@@ -942,7 +942,9 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
                                                   int ntlas, const int* __restrict__ owner,
                                                   int ndom, const spray_rt_ray* __restrict__ rays,
                                                   const uint32_t* __restrict__ sel,
-                                                  size_t M, uint64_t* __restrict__ out) {
+                                                  size_t M, uint64_t* __restrict__ out,
+                                                  const uint8_t* __restrict__ valid,
+                                                  unsigned long long* __restrict__ nvalid) {
   __shared__ int32_t wstack[(kBlock / 64) * kStack];
   __shared__ float4 stl[4 * 64 * W];
   __shared__ int sown[64 * W];
@@ -951,15 +953,27 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
   __syncthreads();
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= M) return;
-  const float4* rp = reinterpret_cast<const float4*>(rays + (sel ? sel[i] : i));
-  const float4 o4 = rp[0], d4 = rp[1];
+  // valid (optional): slot i holds a ray only where valid[i] (its mask is 0
+  // otherwise; the wave still walks the top-level tree together)
+  const bool live = !valid || valid[i];
+  if (nvalid) {
+    const uint64_t b = __ballot(live);
+    if ((threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
+      atomicAdd(nvalid, (unsigned long long)__popcll(b));
+  }
+  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+  if (live) {
+    const float4* rp = reinterpret_cast<const float4*>(rays + (sel ? sel[i] : i));
+    o4 = rp[0];
+    d4 = rp[1];
+  }
   uint64_t m[W];
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
   uint64_t ranks = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) {
-    uint64_t bits = m[w];
+    uint64_t bits = live ? m[w] : 0ull;
     while (bits) {
       const int j = __ffsll((long long)bits) - 1;
       bits &= bits - 1;
@@ -1969,12 +1983,15 @@ hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
 }
 
 hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,
-                        const spray_rt_ray* rays, size_t M, uint64_t* out, const uint32_t* sel) {
+                        const spray_rt_ray* rays, size_t M, uint64_t* out, const uint32_t* sel,
+                        const uint8_t* valid, unsigned long long* nvalid) {
   if (M == 0) return hipSuccess;
   if (v.ndom <= 64)
-    k_route<1><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, sel, M, out);
+    k_route<1><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, sel, M, out,
+                                              valid, nvalid);
   else
-    k_route<4><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, sel, M, out);
+    k_route<4><<<grid_for(M), kBlock, 0, s>>>(v.tlas, v.ntlas, owner, v.ndom, rays, sel, M, out,
+                                              valid, nvalid);
   return hipGetLastError();
 }
 
