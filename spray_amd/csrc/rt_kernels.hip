@@ -1636,6 +1636,16 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write_hits(
   }
 }
 
+// 8x8 bit-matrix transpose: bit c of byte r <-> bit r of byte c
+__device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
+  uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+  x = x ^ t ^ (t << 7);
+  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+  x = x ^ t ^ (t << 14);
+  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+  return x ^ t ^ (t << 28);
+}
+
 // The trace order of k_spawn_ao_write_hits (traced), as (source ray, sample)
 // pairs only: pairs[pos] = i << 5 | l -- for the fused spawn + any hit,
 // whose lanes generate the rays themselves (kEpiAoGen).
@@ -1692,20 +1702,24 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t 
   }
   const uint32_t tile = in ? tile_off[blockIdx.x] : 0u;
   const uint32_t gpos = tile + __shfl(m.y, g0);
+  // the group's masks as columns: byte l of cols[q] = the group members
+  // with sample 8q + l (an 8x8 bit transpose per 8 samples), so each
+  // sample's count and this lane's rank are two popcounts
+  static_assert(kAoGroup == 8, "one byte per group member");
+  uint64_t cols[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int t = 0; t < int(kAoGroup); ++t) x |= uint64_t((gm[t] >> (8 * q)) & 0xFFu) << (8 * t);
+    cols[q] = transpose8x8(x);
+  }
+  const uint32_t below = (1u << me) - 1u;
   uint32_t run = 0;
   for (uint32_t l = 0; l < ns; ++l) {
-    uint32_t col = 0, before = 0;
-#pragma unroll
-    for (int t = 0; t < int(kAoGroup); ++t) {
-      const uint32_t b = (gm[t] >> l) & 1u;
-      col += b;
-      before += t < me ? b : 0u;
-    }
-    if ((m.x >> l) & 1u) {
-      const uint32_t pos = gpos + run + before;
-      pairs[pos] = (i << 5) | l;
-    }
-    run += col;
+    const uint32_t b = uint32_t(cols[l >> 3] >> (8 * (l & 7))) & 0xFFu;
+    if ((m.x >> l) & 1u) pairs[gpos + run + uint32_t(__popc(b & below))] = (i << 5) | l;
+    run += uint32_t(__popc(b));
   }
 }
 
