@@ -23,6 +23,10 @@ namespace {
 constexpr int kWaves = kBlock / 64;
 // adaptive any-hit drains: the largest id span of a wave's rays that still
 // walks as a packet (8 pixels x 8 spp = 64 consecutive camera rays)
+// waves per SIMD the any-hit drain is compiled for (register budget)
+#ifndef SPRAY_OOC_AH_WAVES
+#define SPRAY_OOC_AH_WAVES 1
+#endif
 #ifndef SPRAY_OOC_PACKET_SPAN
 #define SPRAY_OOC_PACKET_SPAN 1024
 #endif
@@ -34,6 +38,17 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
     lo |= __shfl_xor(lo, off);
     hi |= __shfl_xor(hi, off);
   }
+  return (uint64_t(hi) << 32) | lo;
+}
+
+// A wave-uniform pointer as the packet walk's SGPR address: the segment's
+// domain is the wave's, but the compiler cannot prove a pointer read through
+// a dynamically indexed kernel argument uniform, and would fetch every node
+// and triangle through the vector path into each lane.
+__device__ __forceinline__ uint64_t uniform_ptr(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v))));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))));
   return (uint64_t(hi) << 32) | lo;
 }
 
@@ -483,10 +498,8 @@ __device__ __forceinline__ void ch_pair(const OocDomain& D, uint32_t pj, bool va
   Best best{tcur, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool act = valid && !(te > tcur), hit = false;
   if (__ballot(act))
-    trace_tree_packet<false>(reinterpret_cast<uint64_t>(D.nodes),
-                             reinterpret_cast<uint64_t>(D.tris),
-                             reinterpret_cast<uint64_t>(D.prims), r, o4.w, 0.f, best, act, hit,
-                             stack);
+    trace_tree_packet<false>(uniform_ptr(D.nodes), uniform_ptr(D.tris), uniform_ptr(D.prims), r,
+                             o4.w, 0.f, best, act, hit, stack);
   uint64_t dm[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) dm[w] = 0;
@@ -634,10 +647,8 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
   if (packet) {
     Best best{0.f, 0xFFFFFFFFu, 0xFFFFFFFFu};
     if (__ballot(act))
-      trace_tree_packet<true>(reinterpret_cast<uint64_t>(D.nodes),
-                              reinterpret_cast<uint64_t>(D.tris),
-                              reinterpret_cast<uint64_t>(D.prims), r, o4.w, d4.w, best, act, hit,
-                              wstk);
+      trace_tree_packet<true>(uniform_ptr(D.nodes), uniform_ptr(D.tris), uniform_ptr(D.prims), r,
+                              o4.w, d4.w, best, act, hit, wstk);
   } else if (act) {
     hit = occluded_tree_ww<false>(D.nodes, D.tris, r, o4.w, d4.w, lstk);
   }
@@ -659,7 +670,7 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
 // The last block to finish (done counter) publishes the live counts and
 // rearms the counter for the next launch.
 template <int W, int MODE>
-__global__ __launch_bounds__(kBlock) void k_ooc_ah_batch(
+__global__ __launch_bounds__(kBlock, SPRAY_OOC_AH_WAVES) void k_ooc_ah_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, uint8_t* __restrict__ occ,
     uint32_t* __restrict__ live, uint32_t* __restrict__ done, OocSnapshot S, int ndom) {
