@@ -151,12 +151,20 @@ int spray_rt_bvh_build_host(const float* verts_xyz, size_t nverts,
                             size_t* nnodes, int* depth, void* nodes_out,
                             float* tris_out, uint32_t* prims_out);
 
-/* Host-only: the 16-bit quantized copy of that BVH2 the per-lane any-hit
- * walk reads (32-B nodes: u16 l_lo xyz, l_hi xyz, r_lo xyz, r_hi xyz, int32
+/* Host-only: the 16-bit quantized copy of that BVH2 (32-B nodes: u16 l_lo xyz, l_hi xyz, r_lo xyz, r_hi xyz, int32
  * left, right; decoded bound = base + q * scale, grid_out = base xyz, scale
  * xyz).  SPRAY_RT_ERR_LIMIT if the coordinates exceed the grid's range. */
 int spray_rt_qnodes_host(const float* verts_xyz, size_t nverts, const uint32_t* faces,
                          size_t nfaces, size_t* nnodes, float grid_out[6], void* qnodes_out);
+
+/* Host-only: the 4-wide quantized collapse of that BVH2 the per-lane any-hit
+ * walk reads (64-B nodes: u16 child boxes [4][lo xyz, hi xyz], int32 child
+ * refs [4], >= 0 node index, < 0 leaf ~((first << 2) | (count - 1)), INT32_MIN
+ * empty; same grid as above), and the walk's stack bound (entries).
+ * SPRAY_RT_ERR_LIMIT if the coordinates exceed the grid's range. */
+int spray_rt_qnodes4_host(const float* verts_xyz, size_t nverts, const uint32_t* faces,
+                          size_t nfaces, size_t* nnodes, int* stack_bound, float grid_out[6],
+                          void* qnodes_out);
 
 /* ---- Embree-1M-style streams (drop-in) ---- */
 int spray_rt_intersect1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,

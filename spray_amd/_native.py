@@ -75,6 +75,7 @@ SIGNATURES = {
     "spray_rt_slot_info": (I, [P, I, P, P, P]),
     "spray_rt_bvh_build_host": (I, [P, SZ, P, SZ, P, P, P, P, P]),
     "spray_rt_qnodes_host": (I, [P, SZ, P, SZ, P, P, P]),
+    "spray_rt_qnodes4_host": (I, [P, SZ, P, SZ, P, P, P, P]),
     "spray_rt_intersect1M": (I, [P, I, P, SZ, SZ]),
     "spray_rt_occluded1M": (I, [P, I, P, SZ, SZ]),
     "spray_rt_intersect_segments": (I, [P, P, P, I, P, SZ]),

@@ -321,18 +321,19 @@ bool build_domain_tree(const float* boxes, size_t n, std::vector<BvhNode>* out,
   return true;
 }
 
-bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
-                    std::vector<QNode>* out) {
-  out->assign(nodes.size(), QNode{});
+namespace {
+
+bool empty_box(const float* lo) { return lo[0] == kInf; }  // builder's never-hit box
+
+// grid over the union of the finite child boxes, ~700 steps of margin
+bool make_qgrid(const std::vector<BvhNode>& nodes, QGrid* grid) {
   *grid = QGrid{};
-  auto empty = [](const float* lo) { return lo[0] == kInf; };  // builder's never-hit box
-  // grid over the union of the finite child boxes, ~700 steps of margin
   float lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
   for (const BvhNode& n : nodes)
     for (int side = 0; side < 2; ++side) {
       const float* bl = side ? n.r_lo : n.l_lo;
       const float* bh = side ? n.r_hi : n.l_hi;
-      if (empty(bl)) continue;
+      if (empty_box(bl)) continue;
       for (int j = 0; j < 3; ++j) {
         if (!std::isfinite(bl[j]) || !std::isfinite(bh[j])) return false;
         lo[j] = std::min(lo[j], bl[j]);
@@ -355,39 +356,148 @@ bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
     grid->base[j] = float(double(lo[j]) - 700.0 * double(grid->scale[j]));
     if (!std::isfinite(grid->base[j]) || !(grid->scale[j] > 0.f)) return false;
   }
-  // decoded bound of grid coordinate q on axis j (the value the kernel's
-  // folded slab evaluates up to rounding, which the extra step covers)
-  auto dec = [&](int j, long q) {
-    return double(std::fma(float(q), grid->scale[j], grid->base[j]));
+  return true;
+}
+
+// One child box as grid coordinates q[0..2] = lo, q[3..5] = hi, rounded
+// outward with one extra step: the decoded bound (the value the kernel's
+// folded slab evaluates up to rounding, which the extra step covers) lies a
+// whole step outside the fp32 bound.  An empty box becomes the far corner.
+bool quant_box(const QGrid& grid, const float* bl, const float* bh, uint16_t* q) {
+  auto dec = [&](int j, long v) {
+    return double(std::fma(float(v), grid.scale[j], grid.base[j]));
   };
+  for (int j = 0; j < 3; ++j) {
+    if (empty_box(bl)) {
+      q[j] = q[3 + j] = 0xFFFF;
+      continue;
+    }
+    const double s = grid.scale[j];
+    long ql = long(std::floor((double(bl[j]) - grid.base[j]) / s)) - 2;
+    while (ql > 0 && !(dec(j, ql) + s <= double(bl[j]))) --ql;
+    long qh = long(std::ceil((double(bh[j]) - grid.base[j]) / s)) + 2;
+    while (qh < 0xFFFF && !(dec(j, qh) - s >= double(bh[j]))) ++qh;
+    if (ql < 0 || qh > 0xFFFF || !(dec(j, ql) + s <= double(bl[j])) ||
+        !(dec(j, qh) - s >= double(bh[j])))
+      return false;
+    q[j] = uint16_t(ql);
+    q[3 + j] = uint16_t(qh);
+  }
+  return true;
+}
+
+// Collapse of the BVH2 into QNode4s: a node's children start as the BVH2
+// node's two children; the inner child with the largest box area is replaced
+// by its own two children while fewer than four are held and the stack
+// budget allows it (the per-lane walk pushes every entered child but the
+// nearest: pend + k - 1 entries, and a child subtree of BVH2 height h can
+// always be walked with h more).
+struct Collapse {
+  const std::vector<BvhNode>& n2;
+  const QGrid& grid;
+  std::vector<QNode4>* out;
+  std::vector<int> height;  // BVH2 inner levels below (leaf 0)
+  int budget;
+  int bound = 0;
+  bool ok = true;
+
+  struct Cand {
+    const float* lo;
+    const float* hi;
+    int32_t ref;
+  };
+  int h_of(int32_t ref) const { return ref >= 0 ? height[size_t(ref)] : 0; }
+  static float area(const Cand& c) {
+    const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+    return (dx * dy + dy * dz) + dz * dx;
+  }
+  void children(int32_t node, std::vector<Cand>* cs) const {
+    const BvhNode& n = n2[size_t(node)];
+    if (n.left != kNoChild && !empty_box(n.l_lo)) cs->push_back({n.l_lo, n.l_hi, n.left});
+    if (n.right != kNoChild && !empty_box(n.r_lo)) cs->push_back({n.r_lo, n.r_hi, n.right});
+  }
+  int32_t emit(int32_t node, int pend) {
+    std::vector<Cand> cs;
+    children(node, &cs);
+    for (;;) {
+      if (cs.size() >= 4) break;
+      int pick = -1;
+      float best = -1.f;
+      for (size_t k = 0; k < cs.size(); ++k) {
+        if (cs[k].ref < 0) continue;
+        // the set after expanding k must keep pend + (size - 1) + max height <= budget
+        std::vector<Cand> gc;
+        children(cs[k].ref, &gc);
+        int hmax = 0;
+        for (size_t m = 0; m < cs.size(); ++m)
+          if (m != k) hmax = std::max(hmax, h_of(cs[m].ref));
+        for (const Cand& g : gc) hmax = std::max(hmax, h_of(g.ref));
+        const int size = int(cs.size()) - 1 + int(gc.size());
+        if (size > 4 || pend + size - 1 + hmax > budget) continue;
+        const float a = area(cs[k]);
+        if (a > best) {
+          best = a;
+          pick = int(k);
+        }
+      }
+      if (pick < 0) break;
+      std::vector<Cand> gc;
+      children(cs[size_t(pick)].ref, &gc);
+      cs.erase(cs.begin() + pick);
+      cs.insert(cs.begin() + pick, gc.begin(), gc.end());
+    }
+    const int32_t id = int32_t(out->size());
+    out->push_back(QNode4{});
+    const int k = int(cs.size());
+    const int p2 = pend + (k > 0 ? k - 1 : 0);
+    bound = std::max(bound, p2);
+    QNode4 q{};
+    for (int c = 0; c < 4; ++c) {
+      q.child[c] = kNoChild;
+      for (int j = 0; j < 6; ++j) q.q[6 * c + j] = 0xFFFF;
+    }
+    for (int c = 0; c < k; ++c) {
+      if (!quant_box(grid, cs[size_t(c)].lo, cs[size_t(c)].hi, q.q + 6 * c)) ok = false;
+      q.child[c] = cs[size_t(c)].ref;
+    }
+    for (int c = 0; c < k && ok; ++c)
+      if (cs[size_t(c)].ref >= 0) q.child[c] = emit(cs[size_t(c)].ref, p2);
+    (*out)[size_t(id)] = q;
+    return id;
+  }
+};
+
+}  // namespace
+
+bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
+                    std::vector<QNode>* out) {
+  out->assign(nodes.size(), QNode{});
+  if (!make_qgrid(nodes, grid)) return false;
   for (size_t i = 0; i < nodes.size(); ++i) {
     const BvhNode& n = nodes[i];
     QNode& o = (*out)[i];
     o.left = n.left;
     o.right = n.right;
-    for (int side = 0; side < 2; ++side) {
-      const float* bl = side ? n.r_lo : n.l_lo;
-      const float* bh = side ? n.r_hi : n.l_hi;
-      uint16_t* q = o.q + 6 * side;
-      for (int j = 0; j < 3; ++j) {
-        if (empty(bl)) {
-          q[j] = q[3 + j] = 0xFFFF;
-          continue;
-        }
-        const double s = grid->scale[j];
-        long ql = long(std::floor((double(bl[j]) - grid->base[j]) / s)) - 2;
-        while (ql > 0 && !(dec(j, ql) + s <= double(bl[j]))) --ql;
-        long qh = long(std::ceil((double(bh[j]) - grid->base[j]) / s)) + 2;
-        while (qh < 0xFFFF && !(dec(j, qh) - s >= double(bh[j]))) ++qh;
-        if (ql < 0 || qh > 0xFFFF || !(dec(j, ql) + s <= double(bl[j])) ||
-            !(dec(j, qh) - s >= double(bh[j])))
-          return false;
-        q[j] = uint16_t(ql);
-        q[3 + j] = uint16_t(qh);
-      }
-    }
+    if (!quant_box(*grid, n.l_lo, n.l_hi, o.q) || !quant_box(*grid, n.r_lo, n.r_hi, o.q + 6))
+      return false;
   }
   return true;
+}
+
+bool quantize_nodes4(const std::vector<BvhNode>& nodes, QGrid* grid,
+                     std::vector<QNode4>* out, int* stack_bound) {
+  out->clear();
+  if (stack_bound) *stack_bound = 0;
+  if (!make_qgrid(nodes, grid)) return false;
+  if (nodes.empty()) return true;
+  Collapse c{nodes, *grid, out, std::vector<int>(nodes.size(), 0), kQ4Stack};
+  // depth-first layout: children follow their parent
+  for (size_t i = nodes.size(); i-- > 0;)
+    c.height[i] = 1 + std::max(c.h_of(nodes[i].left), c.h_of(nodes[i].right));
+  if (c.height[0] > kQ4Stack) return false;
+  c.emit(0, 0);
+  if (stack_bound) *stack_bound = c.bound;
+  return c.ok && c.bound <= kQ4Stack;
 }
 
 }  // namespace spray_rt

@@ -34,6 +34,15 @@ bool build_bvh(const float* verts, size_t nverts, const uint32_t* faces,
 bool quantize_nodes(const std::vector<BvhNode>& nodes, QGrid* grid,
                     std::vector<QNode>* out);
 
+// 4-wide quantized copy (QNode4, rt_common.h) of a domain tree, the layout
+// the per-lane any hit walks: the BVH2 collapsed greedily (largest-area inner
+// child expanded first) under a stack budget of kQ4Stack entries, child
+// boxes quantized on the same grid as quantize_nodes.  stack_bound = the
+// most entries the walk can hold pending (every entered child but the
+// nearest pushed), <= kQ4Stack.  Node 0 is the root, children after parents.
+bool quantize_nodes4(const std::vector<BvhNode>& nodes, QGrid* grid,
+                     std::vector<QNode4>* out, int* stack_bound);
+
 // Top-level tree over domain boxes [n][6] (lo, hi): same builder, one domain
 // per leaf (ref ~(id << 2)), EXACT union boxes (no padding) so that the
 // reference's intersectAabb evaluated on a parent accepts whenever it accepts

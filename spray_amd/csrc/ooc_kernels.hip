@@ -650,7 +650,7 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
       trace_tree_packet<true>(uniform_ptr(D.nodes), uniform_ptr(D.tris), uniform_ptr(D.prims), r,
                               o4.w, d4.w, best, act, hit, wstk);
   } else if (act) {
-    hit = occluded_tree_ww<false>(D.nodes, D.tris, r, o4.w, d4.w, lstk);
+    hit = occluded_tree_ww(D.nodes, D.tris, r, o4.w, d4.w, lstk);
   }
   uint64_t dm[W];
 #pragma unroll

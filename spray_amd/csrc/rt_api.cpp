@@ -81,11 +81,12 @@ const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* 
     for (int k = 0; k < 9; ++k)
       if (!std::isfinite(img.tris[12 * i + k])) return "non-finite vertex coordinate";
   QGrid grid{};
-  std::vector<QNode> qn;
-  if (quantized && !img.nodes.empty() && !quantize_nodes(img.nodes, &grid, &qn))
+  std::vector<QNode4> qn;
+  int qstack = 0;  // <= kQ4Stack, which the any-hit launches provide
+  if (quantized && !img.nodes.empty() && !quantize_nodes4(img.nodes, &grid, &qn, &qstack))
     return "vertex coordinates beyond the range of the quantized node grid";
-  // QGrid at nodes - 32, QNode i at nodes - 64 - 32 i (rt_common.h)
-  const size_t b_q = qn.empty() ? 0 : align256(sizeof(QGrid) + qn.size() * sizeof(QNode));
+  // QGrid at nodes - 32, QNode4 i at nodes - 64 - 64 (i + 1) (rt_common.h)
+  const size_t b_q = qn.empty() ? 0 : align256(64 + qn.size() * sizeof(QNode4));
   const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
   const size_t b_tris = align256(img.tris.size() * sizeof(float));
   const size_t b_prims = align256(img.prims.size() * sizeof(uint32_t));
@@ -105,7 +106,7 @@ const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* 
   if (b_q) {
     std::memcpy(host + b_q - sizeof(QGrid), &grid, sizeof(QGrid));
     for (size_t i = 0; i < qn.size(); ++i)
-      std::memcpy(host + b_q - sizeof(QGrid) - (i + 1) * sizeof(QNode), &qn[i], sizeof(QNode));
+      std::memcpy(host + b_q - 64 - (i + 1) * sizeof(QNode4), &qn[i], sizeof(QNode4));
     off = b_q;
   }
   out->o_nodes = put(img.nodes.data(), img.nodes.size() * sizeof(BvhNode), b_nodes);
@@ -422,6 +423,27 @@ int spray_rt_qnodes_host(const float* verts, size_t nverts, const uint32_t* face
     std::memcpy(grid_out + 3, grid.scale, 12);
   }
   if (qnodes_out) std::memcpy(qnodes_out, qn.data(), qn.size() * sizeof(QNode));
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_qnodes4_host(const float* verts, size_t nverts, const uint32_t* faces,
+                          size_t nfaces, size_t* nnodes, int* stack_bound, float grid_out[6],
+                          void* qnodes_out) {
+  if ((nverts && !verts) || (nfaces && !faces)) return SPRAY_RT_ERR_ARG;
+  BvhImage img;
+  if (!build_bvh(verts, nverts, faces, nfaces, &img)) return SPRAY_RT_ERR_ARG;
+  QGrid grid{};
+  std::vector<QNode4> qn;
+  int bound = 0;
+  if (!img.nodes.empty() && !quantize_nodes4(img.nodes, &grid, &qn, &bound))
+    return SPRAY_RT_ERR_LIMIT;
+  if (nnodes) *nnodes = qn.size();
+  if (stack_bound) *stack_bound = bound;
+  if (grid_out) {
+    std::memcpy(grid_out, grid.base, 12);
+    std::memcpy(grid_out + 3, grid.scale, 12);
+  }
+  if (qnodes_out) std::memcpy(qnodes_out, qn.data(), qn.size() * sizeof(QNode4));
   return SPRAY_RT_OK;
 }
 

@@ -44,21 +44,35 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node must be 64 B");
 
-// 32-B quantized copy of a BvhNode for the per-lane any-hit walk (scene
-// slots only): both child boxes as 16-bit grid coordinates of the domain's
-// grid (base + q * scale per axis), rounded outward by at least one extra
-// grid step, so every decoded box contains the padded fp32 box and culling
-// stays conservative; an empty (+inf) box becomes the grid's far corner.
-// Placed in front of the fp32 nodes of the same slot:
-//   nodes - 32          : QGrid (base xyz, scale xyz)
-//   nodes - 64 - 32 * i : QNode i
-// so the scene descriptors (DomTrav) address them without another pointer.
+// 32-B quantized copy of a BvhNode: both child boxes as 16-bit grid
+// coordinates of the domain's grid (base + q * scale per axis), rounded
+// outward by at least one extra grid step, so every decoded box contains the
+// padded fp32 box and culling stays conservative; an empty (+inf) box
+// becomes the grid's far corner.  The BVH2 form of the quantization (host
+// export and tests); slots carry the 4-wide QNode4 below.  The quantized
+// copy sits in front of the fp32 nodes of the same slot, so the scene
+// descriptors (DomTrav) address it without another pointer.
 struct alignas(16) QNode {
   uint16_t q[12];  // l_lo xyz, l_hi xyz, r_lo xyz, r_hi xyz
   int32_t left;
   int32_t right;
 };
 static_assert(sizeof(QNode) == 32, "quantized node must be 32 B");
+// 64-B 4-wide quantized node (the BVH2 collapsed, bvh_build.h
+// quantize_nodes4), the node layout of the per-lane any-hit walk of scene
+// slots: four child boxes as 16-bit grid coordinates (child c: q[6c..6c+2]
+// lo, q[6c+3..6c+5] hi) and four child refs (>= 0 QNode4 index, < 0 leaf
+// as in BvhNode, kNoChild = empty).  In front of the fp32 nodes:
+//   nodes - 32                : QGrid
+//   nodes - 64 - 64 * (i + 1) : QNode4 i   (64-B aligned)
+struct alignas(16) QNode4 {
+  uint16_t q[24];
+  int32_t child[4];
+};
+static_assert(sizeof(QNode4) == 64, "4-wide quantized node must be 64 B");
+// stack entries of the 4-wide walk: the launch's LDS stack (STK) plus a
+// private overflow of kQ4Stack - STK
+constexpr int kQ4Stack = 40;
 struct alignas(16) QGrid {
   float base[3];
   float pad0;

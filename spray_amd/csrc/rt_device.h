@@ -22,6 +22,14 @@ namespace {
 
 constexpr float kInf = __builtin_inff();
 constexpr int32_t kNone = INT_MAX;
+constexpr int32_t kNoChildRef = INT32_MIN;
+// 4-wide any hit: 0 = the nearest entered child next, the others pushed in
+// child order; 1 = entered children pushed far to near (sorted; measured
+// 4.30 vs 4.11 ms for the AO-16 any hit); 2 = no ordering (first entered
+// child next)
+#ifndef SPRAY_Q4_SORT
+#define SPRAY_Q4_SORT 0
+#endif  // empty child (bvh_build.h kNoChild)
 
 inline unsigned grid_for(size_t M) { return unsigned((M + kBlock - 1) / kBlock); }
 
@@ -322,23 +330,14 @@ __device__ __forceinline__ bool trace_tree(const void* nodes, const void* tris,
 // Leaves go through the per-lane stack like inner nodes; a visit still
 // pushes at most one entry, so the stack bound (tree depth) is unchanged.
 //
-// Q: walk the slot's 32-B quantized node copy (QNode, rt_common.h) instead of
-// the 64-B fp32 nodes -- half the bytes through the vector data path, which
-// bounds this walk.  The grid decode is folded into the ray's slab constants
-// (t = q * (scale / d) + (base - o) / d); the extra grid step every quantized
-// box carries covers the rounding, so culling stays conservative and the
-// result is the fp32 walk's.
+// The fp32 walk of the 64-B nodes (OOC drains); scene slots use the 4-wide
+// quantized form below.
 //
-// Rounding of the folded form.  The fold (oix' = oix - base * ix, ix' =
-// scale * ix), the offsets and the slab's fmaf(q, ix', -oix') each round
-// once: the error of a plane's t is below 2^-24 (|oix| + 3 |oix'| +
-// 2 * 65536 |ix'|).  Far from the domain (|o - base| hundreds of domain
-// extents, or coordinates large against the extent) that outgrows the one
-// grid step of margin, so every plane moves outward in t by ex = 2^-20 *
-// (|oix| + |oix'| + 65536 |ix'|) per axis, folded into separate lo- and
-// hi-plane offsets like the fp32 walk's (Ray above).  The walk is then
-// conservative against its own decoded boxes, which contain the tight boxes,
-// so it finds every hit the fp32 walk finds (both equal brute force).
+// Quantized nodes (occluded_tree_q4): the grid decode is folded into the
+// ray's slab constants (t = q * (scale / d) + (base - o) / d); the extra grid
+// step every quantized box carries covers the rounding, so culling stays
+// conservative and the result is the fp32 walk's.
+//
 __device__ __forceinline__ float q_lo(float w) { return float(__float_as_uint(w) & 0xFFFFu); }
 __device__ __forceinline__ float q_hi(float w) { return float(__float_as_uint(w) >> 16); }
 
@@ -372,44 +371,21 @@ __device__ __forceinline__ bool slab_q(const QRay& r, float lx, float ly, float 
   return tmin <= tmax;
 }
 
-template <bool Q>
 __device__ __forceinline__ bool occluded_tree_ww(const void* nodes, const void* tris,
                                                  const Ray& r, float tnear, float tfar,
                                                  int32_t* stk) {
-  const char* nbytes = static_cast<const char*>(nodes);
-  QRay qr;
-  if (Q) {
-    const float4 base = ld4(nbytes - sizeof(QGrid), 0);
-    const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
-    q_axis(base.x, scale.x, r.ix, r.ox * r.ix, qr.ix, qr.olx, qr.ohx);
-    q_axis(base.y, scale.y, r.iy, r.oy * r.iy, qr.iy, qr.oly, qr.ohy);
-    q_axis(base.z, scale.z, r.iz, r.oz * r.iz, qr.iz, qr.olz, qr.ohz);
-  }
   int sp = 0;
   int32_t cur = 0;       // next entry: inner node >= 0, leaf < 0, kNone = done
   int32_t leaf = kNone;  // the parked leaf
   for (;;) {
     while (cur >= 0 && cur != kNone) {
       float tl, tr;
-      bool hl, hr;
-      int32_t c0, c1;
-      if (Q) {
-        const char* qp = nbytes - 2 * sizeof(QNode) - sizeof(QNode) * size_t(cur);
-        const float4 a = ld4(qp, 0), b = ld4(qp, 1);
-        hl = slab_q(qr, q_lo(a.x), q_hi(a.x), q_lo(a.y), q_hi(a.y), q_lo(a.z), q_hi(a.z),
-                    tnear, tfar, tl);
-        hr = slab_q(qr, q_lo(a.w), q_hi(a.w), q_lo(b.x), q_hi(b.x), q_lo(b.y), q_hi(b.y),
-                    tnear, tfar, tr);
-        c0 = __float_as_int(b.z);
-        c1 = __float_as_int(b.w);
-      } else {
-        float4 n0, n1, n2, n3;
-        ld_node(nodes, 4 * size_t(cur), n0, n1, n2, n3);
-        hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tfar, tl);
-        hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tfar, tr);
-        c0 = __float_as_int(n3.x);
-        c1 = __float_as_int(n3.y);
-      }
+      float4 n0, n1, n2, n3;
+      ld_node(nodes, 4 * size_t(cur), n0, n1, n2, n3);
+      const bool hl = slab(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, tnear, tfar, tl);
+      const bool hr = slab(r, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, tnear, tfar, tr);
+      int32_t c0 = __float_as_int(n3.x);
+      int32_t c1 = __float_as_int(n3.y);
       if (hl && hr && tr < tl) {
         const int32_t x = c0;
         c0 = c1;
@@ -443,6 +419,140 @@ __device__ __forceinline__ bool occluded_tree_ww(const void* nodes, const void* 
       if (cur < 0) {  // the walk stopped on a second leaf
         leaf = cur;
         cur = sp ? stk[--sp * kBlock] : kNone;
+      }
+    }
+    if (cur == kNone) return false;
+  }
+}
+
+// The same while-while any hit over the slot's 4-wide quantized nodes
+// (QNode4, rt_common.h): a visit tests four child boxes, goes on with the
+// nearest entered child and pushes the others (at most three), so a ray
+// walks about half the levels of the BVH2 with twice the boxes per fetch --
+// half the dependent node-fetch round trips and loop iterations, which bound
+// this divergent walk.  The stack holds STK entries in LDS (stride kBlock)
+// and kQ4Stack - STK in private memory; the host collapse bounds the pending
+// entries by kQ4Stack.  Empty children (kNoChild) are never entered.
+template <int STK>
+__device__ __forceinline__ bool occluded_tree_q4(const void* nodes, const void* tris,
+                                                 const Ray& r, float tnear, float tfar,
+                                                 int32_t* stk) {
+  const char* nbytes = static_cast<const char*>(nodes);
+  QRay qr;
+  {
+    const float4 base = ld4(nbytes - sizeof(QGrid), 0);
+    const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
+    q_axis(base.x, scale.x, r.ix, r.ox * r.ix, qr.ix, qr.olx, qr.ohx);
+    q_axis(base.y, scale.y, r.iy, r.oy * r.iy, qr.iy, qr.oly, qr.ohy);
+    q_axis(base.z, scale.z, r.iz, r.oz * r.iz, qr.iz, qr.olz, qr.ohz);
+  }
+  constexpr int kOvf = kQ4Stack > STK ? kQ4Stack - STK : 1;
+  int32_t ovf[kOvf];
+  int sp = 0;
+  auto push = [&](int32_t v) {
+    if (STK >= kQ4Stack || sp < STK)
+      stk[sp * kBlock] = v;
+    else
+      ovf[sp - STK] = v;
+    ++sp;
+  };
+  auto pop = [&]() -> int32_t {
+    if (sp == 0) return kNone;
+    --sp;
+    return (STK >= kQ4Stack || sp < STK) ? stk[sp * kBlock] : ovf[sp - STK];
+  };
+  int32_t cur = 0;       // next entry: inner node >= 0, leaf < 0, kNone = done
+  int32_t leaf = kNone;  // the parked leaf
+  for (;;) {
+    while (cur >= 0 && cur != kNone) {
+      const char* qp = nbytes - 128 - 64 * size_t(cur);
+      const float4 a = ld4(qp, 0), b = ld4(qp, 1), c = ld4(qp, 2), d = ld4(qp, 3);
+      const int32_t ref[4] = {__float_as_int(d.x), __float_as_int(d.y), __float_as_int(d.z),
+                              __float_as_int(d.w)};
+      float t[4];
+      bool h[4];
+      h[0] = slab_q(qr, q_lo(a.x), q_hi(a.x), q_lo(a.y), q_hi(a.y), q_lo(a.z), q_hi(a.z),
+                    tnear, tfar, t[0]);
+      h[1] = slab_q(qr, q_lo(a.w), q_hi(a.w), q_lo(b.x), q_hi(b.x), q_lo(b.y), q_hi(b.y),
+                    tnear, tfar, t[1]);
+      h[2] = slab_q(qr, q_lo(b.z), q_hi(b.z), q_lo(b.w), q_hi(b.w), q_lo(c.x), q_hi(c.x),
+                    tnear, tfar, t[2]);
+      h[3] = slab_q(qr, q_lo(c.y), q_hi(c.y), q_lo(c.z), q_hi(c.z), q_lo(c.w), q_hi(c.w),
+                    tnear, tfar, t[3]);
+#if SPRAY_Q4_SORT == 2
+      // no ordering: the first entered child next, the others pushed
+      int32_t next = kNone;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!h[k] || ref[k] == kNoChildRef) continue;
+        if (next == kNone)
+          next = ref[k];
+        else
+          push(ref[k]);
+      }
+#elif SPRAY_Q4_SORT == 1
+      // entered children sorted near to far (a 5-exchange network), pushed
+      // far first: the next pops are the nearer siblings
+      int32_t rs[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool e = h[k] && ref[k] != kNoChildRef;
+        rs[k] = e ? ref[k] : kNone;
+        t[k] = e ? t[k] : kInf;
+      }
+      auto cx = [&](int x, int y) {
+        const bool sw = t[y] < t[x];
+        const float tx = t[x];
+        const int32_t rx = rs[x];
+        t[x] = sw ? t[y] : tx;
+        t[y] = sw ? tx : t[y];
+        rs[x] = sw ? rs[y] : rx;
+        rs[y] = sw ? rx : rs[y];
+      };
+      cx(0, 1);
+      cx(2, 3);
+      cx(0, 2);
+      cx(1, 3);
+      cx(1, 2);
+      if (rs[3] != kNone) push(rs[3]);
+      if (rs[2] != kNone) push(rs[2]);
+      if (rs[1] != kNone) push(rs[1]);
+      const int32_t next = rs[0];
+#else
+      int32_t next = kNone;
+      float tn = kInf;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!h[k] || ref[k] == kNoChildRef) continue;
+        if (next == kNone || t[k] < tn) {
+          if (next != kNone) push(next);
+          next = ref[k];
+          tn = t[k];
+        } else {
+          push(ref[k]);
+        }
+      }
+#endif
+      cur = next != kNone ? next : pop();
+      if (cur < 0 && leaf == kNone) {  // park the leaf, keep descending
+        leaf = cur;
+        cur = pop();
+      }
+      if (__ballot(leaf == kNone) == 0) break;  // every active lane holds a leaf
+    }
+    while (leaf != kNone) {
+      const uint32_t enc = ~uint32_t(leaf);
+      const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
+      for (uint32_t q = 0; q < cnt; ++q) {
+        float4 a, b, c;
+        ld_tri(tris, first + q, a, b, c);
+        float t, u, v;
+        if (tri_test(r, tnear, a, b, c, t, u, v) && t <= tfar) return true;
+      }
+      leaf = kNone;
+      if (cur < 0) {  // the walk stopped on a second leaf
+        leaf = cur;
+        cur = pop();
       }
     }
     if (cur == kNone) return false;

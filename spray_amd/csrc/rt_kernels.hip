@@ -53,8 +53,8 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #ifndef SPRAY_AH_WW
 #define SPRAY_AH_WW 1
 #endif
-// Per-lane while-while any hit over the 32-B quantized node copy (QNode) of
-// scene slots: 1 = quantized nodes, 0 = the fp32 nodes.
+// Per-lane while-while any hit over the 64-B 4-wide quantized node copy
+// (QNode4) of scene slots: 1 = quantized 4-wide nodes, 0 = the fp32 BVH2.
 #ifndef SPRAY_AH_QNODES
 #define SPRAY_AH_QNODES 1
 #endif
@@ -284,7 +284,7 @@ __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f
   b = v4f{w[0], w[1], w[2], kInf};
 }
 
-template <int W, bool ANY, bool COUNT, int EPI>
+template <int W, bool ANY, bool COUNT, int EPI, int STK>
 __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                           const float4* stl, const float* sbox,
                                           const float4* sdom, int32_t* stk, int32_t* wstk,
@@ -391,7 +391,8 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         const bool o = (COUNT || SPRAY_AH_WW == 0)
                            ? trace_tree<true, COUNT>(nodes, tris, prims, r, o4.w, d4.w, best,
                                                      stk, nnode, ntri)
-                           : occluded_tree_ww<SPRAY_AH_QNODES != 0>(nodes, tris, r, o4.w, d4.w, stk);
+                           : SPRAY_AH_QNODES ? occluded_tree_q4<STK>(nodes, tris, r, o4.w, d4.w, stk)
+                                             : occluded_tree_ww(nodes, tris, r, o4.w, d4.w, stk);
         if (o) {
           occluded = true;
           break;
@@ -879,7 +880,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (ok)
-      scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
+      scene_ray<W, ANY, COUNT, EPI, STK>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
     if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
     if (kShadow) shadow_push<W>(A, sq, j < M, flag, i, pos, wi, stl, sbox, sdom, wstk);
@@ -913,7 +914,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           else if (ok)
-            scene_ray<W, ANY, COUNT, EPI>(A, i, stl, sbox, sdom, stk, wstk, nnode,
+            scene_ray<W, ANY, COUNT, EPI, STK>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
           if (kShadow)

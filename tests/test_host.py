@@ -4,6 +4,7 @@ PLY, transform, normals, camera, BVH builder) equals the oracle bit for bit."""
 import ctypes as C
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -288,6 +289,93 @@ def test_quantized_nodes_contain_fp32_boxes(native, oracle, case):
         dhi = base + qh[live] * scale
         assert (dlo + scale <= lo32[live]).all()
         assert (dhi - scale >= hi32[live]).all()
+
+
+QNODE4_DTYPE = np.dtype([("q", "<u2", 24), ("child", "<i4", 4)])
+Q4_STACK = 40  # rt_common.h kQ4Stack
+NO_CHILD = np.int32(-2 ** 31)
+
+
+@pytest.mark.parametrize("case", ["wavelet", "ground_y-1", "patch_1e4", "skewed", "tiny"])
+def test_quantized_4wide_collapse(native, oracle, case):
+    """The 4-wide quantized collapse the per-lane any hit walks (QNode4):
+    every node is reached once from the root, the leaves are exactly the
+    BVH2's leaves (same refs, each once), every decoded child box contains
+    all triangles below it with a grid step to spare (culling conservative),
+    and the walk's pending stack -- recomputed here as the sum of (entered
+    children - 1) along each path -- equals the reported bound <= kQ4Stack."""
+    rng = np.random.default_rng(5)
+    if case == "wavelet":
+        v, f, _ = oracle.load_ply(os.path.join(SCENES, "wavelet.ply"))
+    elif case == "ground_y-1":
+        v, f = _quad(1, -1.0, -100, 100)
+    elif case == "patch_1e4":
+        v, f = _quad(1, 1e4, 1e4, 1e4 + 0.01)
+    elif case == "skewed":  # the deep chain of test_bvh_depth_bound_on_skewed_input
+        n = 20000
+        x = (np.arange(n, dtype=np.float64) ** 3 / n ** 2).astype(np.float32)
+        v = np.zeros((3 * n, 3), np.float32)
+        v[0::3, 0] = x
+        v[1::3, 0] = x + 1e-3
+        v[1::3, 1] = 1e-3
+        v[2::3, 2] = 1e-3
+        v[2::3, 0] = x
+        f = np.arange(3 * n, dtype=np.uint32).reshape(-1, 3)
+    else:
+        v = rng.uniform(-1, 1, size=(6, 3)).astype(np.float32)
+        f = np.arange(6, dtype=np.uint32).reshape(-1, 3)
+    v = np.ascontiguousarray(v, np.float32)
+    f = np.ascontiguousarray(f, np.uint32)
+    nodes, _, prims, _ = _bvh(native, v, f)
+    L = native.lib()
+    nn, bound = C.c_size_t(), C.c_int()
+    grid = np.zeros(6, np.float32)
+    assert L.spray_rt_qnodes4_host(v.ctypes.data, len(v), f.ctypes.data, len(f), C.byref(nn),
+                                   C.byref(bound), grid.ctypes.data, None) == 0
+    q = np.zeros(nn.value, QNODE4_DTYPE)
+    assert L.spray_rt_qnodes4_host(v.ctypes.data, len(v), f.ctypes.data, len(f), None, None,
+                                   None, q.ctypes.data) == 0
+    base, scale = grid[:3].astype(np.float64), grid[3:].astype(np.float64)
+    refs = nodes[:, 12:14].view(np.int32)
+    live = np.stack([np.isfinite(nodes[:, 0]), np.isfinite(nodes[:, 6])], 1)  # never-hit boxes drop
+    bvh2_leaves = sorted(int(r) for r in refs[live & (refs < 0) & (refs != NO_CHILD)])
+    tri_v = v[f[prims]].astype(np.float64)  # leaf order, [ntris][3][3]
+    seen = np.zeros(len(q), np.int32)
+    leaves, worst = [], 0
+
+    def walk(i, pend):
+        nonlocal worst
+        seen[i] += 1
+        kids = [int(c) for c in q["child"][i] if c != NO_CHILD]
+        assert 1 <= len(kids) <= 4
+        p2 = pend + len(kids) - 1
+        worst = max(worst, p2)
+        lo_all, hi_all = [], []
+        for k, c in enumerate(q["child"][i]):
+            if c == NO_CHILD:
+                continue
+            if c >= 0:
+                lo, hi = walk(int(c), p2)
+            else:
+                enc = ~int(c)
+                first, cnt = int(enc) >> 2, (int(enc) & 3) + 1
+                leaves.append(int(c))
+                pts = tri_v[first:first + cnt].reshape(-1, 3)
+                lo, hi = pts.min(0), pts.max(0)
+            qq = q["q"][i, 6 * k:6 * k + 6].astype(np.float64)
+            assert (base + qq[:3] * scale + scale <= lo).all()
+            assert (base + qq[3:] * scale - scale >= hi).all()
+            lo_all.append(lo)
+            hi_all.append(hi)
+        return np.min(lo_all, 0), np.max(hi_all, 0)
+
+    sys.setrecursionlimit(10000)
+    walk(0, 0)
+    assert (seen == 1).all()
+    assert sorted(leaves) == bvh2_leaves
+    assert worst == bound.value <= Q4_STACK
+    if case == "wavelet":  # the collapse halves the node count of a real mesh
+        assert len(q) < 0.6 * len(nodes)
 
 
 def test_scene_adapter_header_compiles():
