@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-q4ab}
 mkdir -p "$OUT"
 if [ "${TESTS:-0}" = 1 ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_ao.py tests/test_gpu_qnodes.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+  timeout -k 10 600 python -u -m pytest ${TESTFILES:-tests} -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
   tail -2 "$OUT/pytest.log"
 fi
 for rep in 1 2; do
