@@ -239,6 +239,12 @@ struct SceneArgs {
 #ifndef SPRAY_NT_IO
 #define SPRAY_NT_IO 1
 #endif
+// Packet path hit records of a full wave of consecutive rays: 1 = three
+// wave-wide 1-KB stores (records transposed across the lanes), 0 = three
+// strided 16-B stores per lane.
+#ifndef SPRAY_HIT_TRANSPOSE
+#define SPRAY_HIT_TRANSPOSE 1
+#endif
 // The same for the per-lane path's ray loads and the AO rays' stores
 // (measured: AO step 6.27 vs 6.41 ms).
 #ifndef SPRAY_NT_IO_LANE
@@ -616,12 +622,11 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
       }
     }
   }
-  if (!valid) return;
   if (ANY) {
-    A.occ[i] = occluded ? 1 : 0;
+    if (valid) A.occ[i] = occluded ? 1 : 0;
     return;
   }
-  float4 h0, h1, h2;
+  float4 h0, h1, h2;  // invalid lanes: best_dom < 0, never stored
   if (best_dom < 0) {
     h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
     h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
@@ -640,17 +645,49 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
     h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
   }
-  if (SPRAY_NT_IO) {
-    v4f* hp = reinterpret_cast<v4f*>(A.hits + i);
-    __builtin_nontemporal_store(v4f{h0.x, h0.y, h0.z, h0.w}, hp);
-    __builtin_nontemporal_store(v4f{h1.x, h1.y, h1.z, h1.w}, hp + 1);
-    __builtin_nontemporal_store(v4f{h2.x, h2.y, h2.z, h2.w}, hp + 2);
-  } else {
-    float4* hp = reinterpret_cast<float4*>(A.hits + i);
-    hp[0] = h0;
-    hp[1] = h1;
-    hp[2] = h2;
+  // A whole wave of consecutive records (64 x 48 B = 24 full 128-B lines)
+  // goes out as three wave-wide 1-KB stores: lane l of store s writes 16-B
+  // chunk g = 64 s + l of the wave's region, chunk g % 3 of record g / 3,
+  // pulled from that record's lane (3 x 12 cross-lane reads).  The three
+  // strided 16-B stores per lane left lines partially written between
+  // instructions (WRITE_SIZE 1.25x the records).
+  const size_t i0 = size_t(__builtin_amdgcn_readfirstlane(uint32_t(i))) |
+                    (size_t(__builtin_amdgcn_readfirstlane(uint32_t(i >> 32))) << 32);
+  if (SPRAY_HIT_TRANSPOSE && (i0 & 63) == 0 &&
+      __ballot(valid && i == i0 + size_t(lane)) == ~0ull) {
+    const float hv[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
+                          h2.x, h2.y, h2.z, h2.w};
+    v4f* wp = reinterpret_cast<v4f*>(A.hits + i0);
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
+      const int g = 64 * st + lane;
+      const int src = g / 3, ch = g - 3 * src;
+      float o[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const float a0 = __shfl(hv[d], src), a1 = __shfl(hv[4 + d], src),
+                    a2 = __shfl(hv[8 + d], src);
+        o[d] = ch == 0 ? a0 : (ch == 1 ? a1 : a2);
+      }
+      if (SPRAY_NT_IO)
+        __builtin_nontemporal_store(v4f{o[0], o[1], o[2], o[3]}, wp + g);
+      else
+        wp[g] = v4f{o[0], o[1], o[2], o[3]};
+    }
+  } else if (valid) {
+    if (SPRAY_NT_IO) {
+      v4f* hp = reinterpret_cast<v4f*>(A.hits + i);
+      __builtin_nontemporal_store(v4f{h0.x, h0.y, h0.z, h0.w}, hp);
+      __builtin_nontemporal_store(v4f{h1.x, h1.y, h1.z, h1.w}, hp + 1);
+      __builtin_nontemporal_store(v4f{h2.x, h2.y, h2.z, h2.w}, hp + 2);
+    } else {
+      float4* hp = reinterpret_cast<float4*>(A.hits + i);
+      hp[0] = h0;
+      hp[1] = h1;
+      hp[2] = h2;
+    }
   }
+  if (!valid) return;
   if (EPI == kEpiKeys) {
     uint64_t key = 0x7FFFFFFFFFFFFFFFull;
     if (best_dom >= 0) {  // position of best_dom in the ray's sorted list
