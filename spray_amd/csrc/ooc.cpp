@@ -211,7 +211,7 @@ OocDomain domain_view(const spray_rt_ooc* o, int d, int k, const float* boxes) {
 // Drains the queues in the reference's DomainStats order
 // (ooc_pcontext.h:128-132: rstats_.schedule(), highest score first;
 // ooc_domain_stats.cc:60-111), the any-hit pass starting with the domains
-// the closest-hit pass left resident.  max(1, slots / 2) resident domains
+// the closest-hit pass left resident.  Up to slots - 1 resident domains
 // per launch, and each launch also uploads the next batch's missing images
 // into the other slots (copy blocks reading the pinned images; the slots of
 // the launch itself are never evicted): the upload overlaps the drain on
@@ -234,7 +234,18 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   spray_rt_ctx* c = o->ctx;
   hipStream_t s = stream_of(c);
   const int n = c->ndom;
-  const int per = std::max(1, std::min<int>(kOocBatch, int(o->slot.size()) / 2));
+  // Up to slots - 1 domains per launch: with 4 slots the batches alternate
+  // 3 / 1 (the one free slot takes the next batch's upload in the launch) --
+  // more waves per drain than two batches of slots / 2 (measured, configs[3]:
+  // 3.90 -> 3.68 ms per frame; every slot per launch, uploads as DMAs
+  // between the launches: 4.37 ms).  SPRAY_OOC_PER overrides (A/B).
+  static const int per_env = [] {
+    const char* e = std::getenv("SPRAY_OOC_PER");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int nslots = int(o->slot.size());
+  const int per = std::max(1, std::min<int>(kOocBatch, per_env > 0 ? std::min(per_env, nslots)
+                                                                   : nslots - 1));
   std::vector<int> order;
   std::vector<uint32_t> live(n, 0);
   for (int d = 0; d < n; ++d) {
