@@ -1,5 +1,5 @@
-"""The per-lane any hit over 32-B quantized nodes (rt_device.h,
-occluded_tree_ww<Q>) against the oracle on geometry that stresses its grid
+"""The per-lane any hit over the 4-wide quantized nodes (rt_device.h,
+occluded_tree_q4) against the oracle on geometry that stresses its grid
 (ADVICE r1): flat domains away from the origin (a ground quad at y = -1, a
 wall at x = 5), a small domain at large coordinates, and rays from origins
 hundreds to thousands of domain extents away aimed at triangle vertices and
@@ -73,6 +73,58 @@ def test_quantized_any_hit_far_origins(oracle):
     for mode in (rt.RAYS_INCOHERENT, rt.RAYS_ADAPTIVE, rt.RAYS_COHERENT):
         rt.set_coherence(mode)
         occ = torch.full((len(org),), 9, dtype=torch.uint8, device="cuda")
+        rt.occluded_scene(rays, occ)
+        rt.sync()
+        got = occ.cpu().numpy()
+        bad = np.nonzero(got != ref)[0]
+        assert len(bad) == 0, (mode, len(bad), bad[:8])
+    rt.close()
+
+
+def test_quantized_any_hit_deep_stack(oracle):
+    """A deep tree (the nested-sliver chain of test_host.py: depth 22, a
+    4-wide stack bound of kQ4Stack = 40) traced by rays along the chain that
+    sit inside every box but miss every triangle (s + t > 1 in each sliver's
+    plane) -- the walk holds the most pending entries, through the LDS stack
+    into the private overflow -- and by rays that hit; bit-exact occlusion
+    against the oracle in every traversal form."""
+    import torch
+    import spray_amd
+    n = 40000
+    x = (np.arange(n, dtype=np.float64) ** 3 / n ** 2).astype(np.float32)
+    v = np.zeros((3 * n, 3), np.float32)
+    v[0::3, 0] = x
+    v[1::3, 0] = x + 1e-3
+    v[1::3, 1] = 1e-3
+    v[2::3, 2] = 1e-3
+    v[2::3, 0] = x
+    f = np.arange(3 * n, dtype=np.uint32).reshape(-1, 3)
+    rt = spray_amd.RtContext(0)
+    osc = oracle.Scene(1)
+    rt.upload_domain(0, v, f)
+    box = np.concatenate([v.min(0), v.max(0)]).astype(np.float32)
+    osc.set_domain(0, v, f, np.zeros(len(v), np.uint32), np.zeros_like(v), box)
+    rt.domain_bounds(box[None])
+    rt.map_domain(0, 0)
+    rng = np.random.default_rng(8)
+    m = 8192
+    st = rng.uniform(0.02, 0.98, size=(m, 2))
+    miss = np.arange(m) % 2 == 0  # half inside every box, past the triangles
+    st[miss] = 1.0 - st[miss] * 0.45  # s + t > 1.1
+    st[~miss] *= 0.45                 # s + t < 0.9
+    org = np.zeros((m, 3), np.float32)
+    org[:, 0] = np.where(np.arange(m) % 4 < 2, -1.0, float(x[-1]) + 1.0)
+    org[:, 1:] = (st * 1e-3).astype(np.float32)
+    d = np.zeros((m, 3), np.float32)
+    d[:, 0] = np.where(org[:, 0] < 0, 1.0, -1.0)
+    d[:, 1:] = rng.normal(scale=1e-9, size=(m, 2)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    ref, _ = osc.occluded(org, d)
+    assert 0.3 < ref.mean() < 0.7
+    rays = torch.from_numpy(spray_amd.make_rays(org, d).view(np.uint8)).cuda()
+    for mode in (rt.RAYS_INCOHERENT, rt.RAYS_ADAPTIVE, rt.RAYS_COHERENT):
+        rt.set_coherence(mode)
+        occ = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
         rt.occluded_scene(rays, occ)
         rt.sync()
         got = occ.cpu().numpy()
