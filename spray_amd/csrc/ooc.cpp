@@ -211,8 +211,8 @@ OocDomain domain_view(const spray_rt_ooc* o, int d, int k, const float* boxes) {
 // Drains the queues in the reference's DomainStats order
 // (ooc_pcontext.h:128-132: rstats_.schedule(), highest score first;
 // ooc_domain_stats.cc:60-111), the any-hit pass starting with the domains
-// the closest-hit pass left resident.  Up to slots - 1 resident domains
-// per launch, and each launch also uploads the next batch's missing images
+// the closest-hit pass left resident.  slots / 2 resident domains per
+// launch, and each launch also uploads the next batch's missing images
 // into the other slots (copy blocks reading the pinned images; the slots of
 // the launch itself are never evicted): the upload overlaps the drain on
 // the one compute stream, with no cross-stream wait.  With fewer than two
@@ -234,18 +234,15 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   spray_rt_ctx* c = o->ctx;
   hipStream_t s = stream_of(c);
   const int n = c->ndom;
-  // Up to slots - 1 domains per launch: with 4 slots the batches alternate
-  // 3 / 1 (the one free slot takes the next batch's upload in the launch) --
-  // more waves per drain than two batches of slots / 2 (measured, configs[3]:
-  // 3.90 -> 3.68 ms per frame; every slot per launch, uploads as DMAs
-  // between the launches: 4.37 ms).  SPRAY_OOC_PER overrides (A/B).
-  static const int per_env = [] {
-    const char* e = std::getenv("SPRAY_OOC_PER");
-    return e ? std::atoi(e) : 0;
-  }();
+  // slots / 2 domains per launch, so that the next batch's uploads fit the
+  // other slots.  SPRAY_OOC_PER overrides (A/B): up to slots - 1 measured
+  // the same (4.14-4.22 vs 4.15-4.25 ms per frame, batches of 3 / 1), every
+  // slot with the uploads as DMAs between the launches slower (4.37 ms).
+  const char* per_s = std::getenv("SPRAY_OOC_PER");  // read per pass (tests set it)
+  const int per_env = per_s ? std::atoi(per_s) : 0;
   const int nslots = int(o->slot.size());
   const int per = std::max(1, std::min<int>(kOocBatch, per_env > 0 ? std::min(per_env, nslots)
-                                                                   : nslots - 1));
+                                                                   : nslots / 2));
   std::vector<int> order;
   std::vector<uint32_t> live(n, 0);
   for (int d = 0; d < n; ++d) {
@@ -293,7 +290,8 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
     std::fprintf(stderr, "ooc pass %s: %zu queues, %u pairs\n", any_hit ? "any" : "closest",
                  order.size(), o->first[n]);
   // the next batch: the first `per` undone queues not known dead; `busy`
-  // slots (the batch launched before it) are not evicted
+  // slots (the batch launched before it, and the slots this batch already
+  // took) are not evicted
   std::vector<char> busy(o->slot.size(), 0);
   auto pick = [&](OocBatch& B, int* bslot, std::vector<Upload>& ups) -> int {
     B = OocBatch{};
@@ -309,6 +307,7 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
       Upload up;
       if (int e = acquire(o, d, busy, &sl, &up)) return e;
       if (sl < 0) break;  // no free slot until the batch before has run
+      busy[size_t(sl)] = 1;  // not evicted by a later domain of this batch
       if (up.slot >= 0) ups.push_back(up);
       B.d[B.count] = domain_view(o, d, sl, boxes.data());
       B.begin[B.count] = o->first[d];

@@ -31,8 +31,13 @@ def batch(oracle):
             np.concatenate([d, d2, d3]).astype(np.float32))
 
 
-@pytest.mark.parametrize("slots", [1, 4, 64])
-def test_ooc_matches_whole_scene(spray, oracle, slots):
+@pytest.mark.parametrize("slots,per", [(1, None), (4, None), (64, None), (4, 3), (5, 4)])
+def test_ooc_matches_whole_scene(spray, oracle, slots, per, monkeypatch):
+    """per (SPRAY_OOC_PER): domains per drain launch beyond slots / 2 -- a
+    batch then takes every free slot, and no domain of it may evict another
+    one's slot (the bug of slots - 1 batches, results wrong at 4 slots)."""
+    if per is not None:
+        monkeypatch.setenv("SPRAY_OOC_PER", str(per))
     org, d = batch(oracle)
     sc, _, _ = oracle.load_scene(WAVELETS64, SCENES)
     ref, _ = sc.intersect(org, d)
