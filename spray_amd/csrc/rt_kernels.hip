@@ -67,9 +67,16 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #ifndef SPRAY_WAVES_AH
 #define SPRAY_WAVES_AH 1
 #endif
-// the in-lane AO generation would take the any hit to 91 VGPRs (5 waves)
+// LDS entries of the AO any hit's per-lane stack (the rest of kQ4Stack is
+// private): 12 instead of the launch's 16 leaves LDS for 7 blocks per CU, and
+// the register budget of 7 waves per SIMD (72 VGPRs) holds the 4-wide walk
+// (measured: AO any hit 4.12 / 4.14 -> 3.93 / 3.94 ms at 7 waves with 12 or 8
+// LDS entries, against 6 waves with 16; same bits)
+#ifndef SPRAY_AOGEN_LSTK
+#define SPRAY_AOGEN_LSTK 12
+#endif
 #ifndef SPRAY_WAVES_AOGEN
-#define SPRAY_WAVES_AOGEN 6
+#define SPRAY_WAVES_AOGEN 7
 #endif
 #ifndef SPRAY_DIAG_MODE
 #define SPRAY_DIAG_MODE 0
@@ -878,7 +885,13 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
       TRAV != 0 && !COUNT && (SPRAY_DIAG_MODE == 0 || SPRAY_DIAG_MODE >= 5);
   constexpr bool kAdaptive = kPacket && TRAV == 2;
   constexpr bool kLaneStack = !kPacket || kAdaptive;
-  __shared__ int32_t stack[(kLaneStack ? STK : 1) * kBlock];
+  // the AO any hit's 4-wide walk keeps kLStk entries in LDS and the rest of
+  // its kQ4Stack in private memory (LDS for more resident blocks)
+  constexpr int kLStk = (ANY && EPI == kEpiAoGen && !COUNT && SPRAY_AH_QNODES &&
+                         SPRAY_AH_WW && SPRAY_AOGEN_LSTK < STK)
+                            ? SPRAY_AOGEN_LSTK
+                            : STK;
+  __shared__ int32_t stack[(kLaneStack ? kLStk : 1) * kBlock];
   __shared__ float4 stl[4 * 64 * W];   // top-level tree
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
@@ -917,7 +930,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (ok)
-      scene_ray<W, ANY, COUNT, EPI, STK>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
+      scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
     if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
     if (kShadow) shadow_push<W>(A, sq, j < M, flag, i, pos, wi, stl, sbox, sdom, wstk);
@@ -951,7 +964,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           else if (ok)
-            scene_ray<W, ANY, COUNT, EPI, STK>(A, i, stl, sbox, sdom, stk, wstk, nnode,
+            scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
           if (kShadow)
