@@ -68,15 +68,15 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #define SPRAY_WAVES_AH 1
 #endif
 // LDS entries of the AO any hit's per-lane stack (the rest of kQ4Stack is
-// private): 12 instead of the launch's 16 leaves LDS for 7 blocks per CU, and
-// the register budget of 7 waves per SIMD (72 VGPRs) holds the 4-wide walk
-// (measured: AO any hit 4.12 / 4.14 -> 3.93 / 3.94 ms at 7 waves with 12 or 8
-// LDS entries, against 6 waves with 16; same bits)
+// private): 8 instead of the launch's 16 leaves LDS for 8 blocks per CU, and
+// the register budget of 8 waves per SIMD (64 VGPRs) holds the 4-wide walk
+// (measured: AO any hit 4.12 / 4.14 ms at 6 waves with 16 entries -> 3.93 /
+// 3.94 at 7 waves with 12 or 8 -> 3.85 / 3.85 at 8 waves with 8; same bits)
 #ifndef SPRAY_AOGEN_LSTK
-#define SPRAY_AOGEN_LSTK 12
+#define SPRAY_AOGEN_LSTK 8
 #endif
 #ifndef SPRAY_WAVES_AOGEN
-#define SPRAY_WAVES_AOGEN 7
+#define SPRAY_WAVES_AOGEN 8
 #endif
 #ifndef SPRAY_DIAG_MODE
 #define SPRAY_DIAG_MODE 0
