@@ -87,14 +87,20 @@ def scene_bytes(sc, rt):
 
 
 def roofline(kernel, launch_s, compulsory, index_bytes, index_note):
-    """The roofline object of one kernel.  achieved = its compulsory
-    (algorithmic) HBM bytes per launch -- rays in, results out, the scene
-    image once -- over the launch time measured here; traffic = the HBM bytes
-    its PMC pass measured (profiles/pmc_counters.json, labelled with the
-    round it comes from), and the other ceilings from the same profile."""
-    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+    """The roofline object of one kernel.  The traversal kernels are bound by
+    memory latency (dependent node fetches from L2 / MALL), not by HBM
+    bandwidth: "bound" says so and "ceilings" carries the counters that show
+    it.  achieved / frac stay the HBM-roofline figures: the kernel's
+    compulsory HBM bytes per launch -- rays in, results out, the scene image
+    once -- over the launch time measured here, against the 8 TB/s peak.
+    traffic = the HBM bytes its PMC passes measured
+    (profiles/pmc_counters.json), attached only when that profile measured
+    this very library build (build id of spray_amd/lib, spray_amd/build.py)."""
+    out = {"bound": "latency", "unit": "GB/s", "peak": HBM_PEAK_GBS,
            "achieved": round(compulsory / launch_s / 1e9, 1),
            "frac": round(compulsory / launch_s / 1e9 / HBM_PEAK_GBS, 4),
+           "frac_basis": "HBM roofline (secondary): compulsory bytes per launch / launch time / "
+                         "8 TB/s; the walk is latency-bound (see ceilings)",
            "algorithmic_bytes_per_launch": compulsory, "avg_launch_ms": round(launch_s * 1e3, 4),
            "kernel": kernel, "traffic": None,
            "index_8d": {"bytes_per_launch": index_bytes,
@@ -105,10 +111,18 @@ def roofline(kernel, launch_s, compulsory, index_bytes, index_note):
             dv = pm["kernels"][kernel]["derived"]
         except (KeyError, ValueError):
             return out
+        from spray_amd import build as spray_build
+        bid = spray_build.build_id()
+        if not bid or pm.get("build_id") != bid:
+            out["traffic_source"] = ("not attached: profiles/pmc_counters.json (%s) measured "
+                                     "library build %s, this run loads build %s"
+                                     % (pm.get("round"), pm.get("build_id"), bid))
+            return out
         t = dv.get("traffic_bytes")
         out["traffic"] = round(t) if t else None
-        out["traffic_source"] = ("profiles/pmc_counters.json (%s): 2 x FETCH_SIZE + WRITE_SIZE "
-                                 "of this kernel, separate --pmc passes" % pm.get("round"))
+        out["traffic_source"] = ("profiles/pmc_counters.json (%s, library build %s = this run's): "
+                                 "2 x FETCH_SIZE + WRITE_SIZE of this kernel, separate --pmc "
+                                 "passes" % (pm.get("round"), bid))
         if t:
             out["traffic_frac"] = round(t / launch_s / 1e9 / HBM_PEAK_GBS, 4)
         ceil = {}

@@ -171,6 +171,13 @@ int spray_rt_intersect1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,
                          size_t stride);
 int spray_rt_occluded1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,
                         size_t stride);
+/* TriMeshBuffer::updateIntersection (src/render/trimesh_buffer.cc:328-360;
+ * Scene::updateIntersection, src/render/scene.h:203) over a stream: color
+ * (offset 60) and Ns (offset 84) of every record whose geomID marks a hit,
+ * from its primID, u and v and slot's mesh -- the epilogue intersect1M
+ * fuses.  stride >= 96. */
+int spray_rt_update_intersection1M(spray_rt_ctx_t ctx, int slot, void* rays, size_t M,
+                                   size_t stride);
 /* nseg segments: rays [offsets[i], offsets[i+1]) against slots[i];
  * offsets has nseg+1 entries (host memory). */
 int spray_rt_intersect_segments(spray_rt_ctx_t ctx, const int* slots,
@@ -196,12 +203,18 @@ int spray_rt_domains1M(spray_rt_ctx_t ctx, const float* org, const float* dir,
  * in place (host) or completed on the lane's stream (device). */
 typedef struct spray_rt_lane* spray_rt_lane_t;
 int spray_rt_lane_create(spray_rt_ctx_t ctx, spray_rt_lane_t* out);
+/* The calling thread's last spray_rt_lane_create failure ("" after a
+ * success): lane creation never writes the context's shared message, so
+ * threads creating lanes concurrently do not race on it. */
+const char* spray_rt_lane_create_error(void);
 int spray_rt_lane_destroy(spray_rt_lane_t lane);
 const char* spray_rt_lane_last_error(spray_rt_lane_t lane);
 int spray_rt_lane_intersect1M(spray_rt_lane_t lane, int slot, void* rays, size_t M,
                               size_t stride);
 int spray_rt_lane_occluded1M(spray_rt_lane_t lane, int slot, void* rays, size_t M,
                              size_t stride);
+int spray_rt_lane_update_intersection1M(spray_rt_lane_t lane, int slot, void* rays, size_t M,
+                                        size_t stride);
 int spray_rt_lane_domains1M(spray_rt_lane_t lane, const float* org, const float* dir, size_t M,
                             int* ids, float* ts, int* counts, int maxhits);
 
@@ -399,12 +412,13 @@ int spray_rt_spawn_shadows_ao_traced(spray_rt_ctx_t ctx, const spray_rt_ray* ray
  * and the double-precision sincos, once per pixel and sample), float4 at
  * pixid * nsamples + l, and rec the origin, normal and tangent frame of
  * every source ray that spawns (16 floats at 16 * i).  nsamples <= 32,
- * M < 2^27, 0 <= pixid < npix; out_pairs holds M * nsamples entries, lv
- * npix * nsamples * 4 floats, rec M * 16 floats. */
+ * M < 2^27; out_pairs holds M * nsamples entries, lv npix * nsamples * 4
+ * floats, rec M * 16 floats.  A ray whose pixid lies outside [0, npix)
+ * spawns no AO ray (its table entries would lie outside lv). */
 int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t ctx, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                    int nsamples, uint32_t* out_pairs, float* lv, float* rec,
-                                    uint32_t* d_count);
+                                    int nsamples, size_t npix, uint32_t* out_pairs, float* lv,
+                                    float* rec, uint32_t* d_count);
 /* Scene::occluded of those AO rays (ooc_shader_ao.h:114-160 spawn +
  * scene.inl:201-209), each ray generated in its any-hit lane from
  * (rec[i], lv[pixel * nsamples + l]) with the spawn's operations --
@@ -418,9 +432,9 @@ int spray_rt_occluded_ao_pairs(spray_rt_ctx_t ctx, size_t max_n, const uint32_t*
                                unsigned long long* d_counters);
 /* Both, one call. */
 int spray_rt_occluded_ao(spray_rt_ctx_t ctx, const spray_rt_ray* rays, const spray_rt_hit* hits,
-                         const int32_t* pixid, size_t M, int nsamples, uint32_t* out_pairs,
-                         float* lv, float* rec, uint32_t* d_count, uint8_t* occ,
-                         unsigned long long* d_counters);
+                         const int32_t* pixid, size_t M, int nsamples, size_t npix,
+                         uint32_t* out_pairs, float* lv, float* rec, uint32_t* d_count,
+                         uint8_t* occ, unsigned long long* d_counters);
 
 /* ---- frames: path shading, film, tiles (callers of the hot path) ---- */
 /* The shading pass of ooc::ShaderPt (src/ooc/ooc_shader_pt.h:93-227) /

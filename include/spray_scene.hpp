@@ -36,6 +36,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "spray_rt.h"
@@ -152,6 +153,16 @@ class Scene {
                                spray_scene_last_error(scene_));
     sinfo->cache_block = block;
     sinfo->rtc_scene = slot_handle(block);
+    cache_block_ = block;
+  }
+  // Scene::load(int id) (scene.h:154, scene.inl:161-187): the loaded domain
+  // becomes the scene's current one (the reference's scene_ / cache_block_),
+  // which the scene-less queries below use -- the baseline tracers' form
+  // (baseline_shader_ao.h:90, baseline_shader_pt.h:110, 139,
+  // baseline_insitu_tracer.inl:653, 695, 700).
+  void load(int id) {
+    SceneInfo s;
+    load(id, &s);
   }
 
   // Scene::intersect (scene.h:157-173): makeRadianceRay (rays.h:345-363),
@@ -173,6 +184,12 @@ class Scene {
     return intersect(rtc_scene, cache_block, o, dir, isect);
   }
 
+  // Scene::intersect(org, dir, isect) (scene.h:169-173): the current domain.
+  template <typename IsectT>
+  bool intersect(const float org[3], const float dir[3], IsectT* isect) const {
+    return intersect(slot_handle(current()), current(), org, dir, isect);
+  }
+
   // Scene::occluded (scene.h:175-195): makeShadowRay (rays.h:389-423), any
   // hit in the domain rtc_scene names; geomID = 0 when occluded.
   template <typename RayT>
@@ -187,6 +204,28 @@ class Scene {
     const float o[3] = {org[0], org[1], org[2]}, d[3] = {dir[0], dir[1], dir[2]};
     return occluded(rtc_scene, o, d, ray);
   }
+  // Scene::occluded(org, dir, ray) (scene.h:175-178, 185-188): the current
+  // domain (float[3] and glm::vec3 forms).
+  template <typename RayT>
+  bool occluded(const float org[3], const float dir[3], RayT* ray) const {
+    return occluded(slot_handle(current()), org, dir, ray);
+  }
+  template <typename V, typename RayT,
+            typename = decltype(std::declval<const V&>()[0] + 0.0f)>
+  bool occluded(const V& org, const V& dir, RayT* ray) const {
+    const float o[3] = {org[0], org[1], org[2]}, d[3] = {dir[0], dir[1], dir[2]};
+    return occluded(slot_handle(current()), o, d, ray);
+  }
+
+  // Scene::updateIntersection (scene.h:203-205, TriMeshBuffer::
+  // updateIntersection trimesh_buffer.cc:328-360): color and Ns of a hit
+  // record from its primID, u, v and the current domain's mesh.
+  template <typename IsectT>
+  void updateIntersection(IsectT* isect) const {
+    static_assert(sizeof(IsectT) >= sizeof(spray_rt_ray_intersection),
+                  "RTCRayIntersection layout (96 B) expected");
+    lane_call(spray_rt_lane_update_intersection1M(lane(), current(), isect, 1, sizeof(IsectT)));
+  }
 
   // Scene::intersectDomains (scene.h:197, WbvhEmbree::intersect +
   // DomainList::sort): the ray's domain list, (t, id) ascending.
@@ -200,6 +239,40 @@ class Scene {
                                       n > 0 ? n : 1));
     ray.domains->reset();
     for (int k = 0; k < cnt; ++k) ray.domains->push(ids[size_t(k)], ts[size_t(k)]);
+  }
+
+  // ---- batched drains ----------------------------------------------------
+  // The per-domain drains of the schedulers (ooc_tcontext.inl:28-100,
+  // insitu_tcontext.inl:125-186) as gather -> one stream call -> scatter:
+  // a thread copies its queue's rays into a record array (makeRay: the
+  // fields makeRadianceRay / makeShadowRay set), submits it in one call on
+  // its lane, and then runs its update / shade loop over the results in the
+  // original queue order -- the results are pure functions of the rays, so
+  // the VBuf / shading order of the reference is unchanged ("hard
+  // parts").  M records of sizeof(RecordT) bytes, host or device memory.
+  template <typename IsectT>
+  void intersect1M(const SceneInfo& sinfo, IsectT* isects, size_t M) const {
+    static_assert(sizeof(IsectT) >= sizeof(spray_rt_ray_intersection),
+                  "RTCRayIntersection layout (96 B) expected");
+    lane_call(spray_rt_lane_intersect1M(lane(), sinfo.cache_block, isects, M, sizeof(IsectT)));
+  }
+  template <typename RayT>
+  void occluded1M(const SceneInfo& sinfo, RayT* rays, size_t M) const {
+    static_assert(sizeof(RayT) >= 84, "Embree 2 RTCRay layout expected");
+    lane_call(spray_rt_lane_occluded1M(lane(), handle_slot(sinfo.rtc_scene), rays, M,
+                                       sizeof(RayT)));
+  }
+  // Isector::isectDomains over a queue (ooc_isector.h:116-124): ids / ts
+  // [M][maxhits], counts[M], each list sorted by (t, id).
+  void intersectDomains1M(const float* org, const float* dir, size_t M, int* ids, float* ts,
+                          int* counts, int maxhits) const {
+    lane_call(spray_rt_lane_domains1M(lane(), org, dir, M, ids, ts, counts, maxhits));
+  }
+  // RTCRayUtil::makeRadianceRay / makeShadowRay (rays.h:345-363, 389-423):
+  // the same fields (tnear 0.001, tfar +inf, ids invalid, mask ~0, time 0).
+  template <typename R>
+  static void makeRay(const float org[3], const float dir[3], R* r) {
+    make_ray(org, dir, r);
   }
 
   // Scene::getBsdf (scene.h:211): the domain's material record.
@@ -247,9 +320,14 @@ class Scene {
     spray_rt_lane_t l = nullptr;
     if (spray_rt_lane_create(rt_, &l))
       throw std::runtime_error(std::string("spray_amd::Scene: lane: ") +
-                               spray_rt_last_error(rt_));
+                               spray_rt_lane_create_error());
     lanes_[me] = l;
     return l;
+  }
+  int current() const {
+    if (cache_block_ < 0)
+      throw std::runtime_error("spray_amd::Scene: no domain loaded (call load(id) first)");
+    return cache_block_;
   }
   void lane_call(int rc) const {
     if (rc) throw std::runtime_error(std::string("spray_amd::Scene: ") +
@@ -264,6 +342,7 @@ class Scene {
   float bound_[6] = {0, 0, 0, 0, 0, 0};
   InsituPartition partition_;
   bool insitu_ = false;
+  int cache_block_ = -1;  // the last loaded domain's cache block (scene_ / cache_block_)
   mutable std::shared_mutex mu_;
   mutable std::map<std::thread::id, spray_rt_lane_t> lanes_;
 };

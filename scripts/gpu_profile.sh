@@ -8,6 +8,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-prof}
 mkdir -p "$OUT"
+# provenance: the build id of the profiled library (bench.py matches it)
+cp spray_amd/lib/libspray_rt.build.json "$OUT/build.json" || exit 1
 step() {  # name, timeout, cmd...
   local name=$1 to=$2; shift 2
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1

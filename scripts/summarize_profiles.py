@@ -103,8 +103,13 @@ def main(src, tag):
         for k in names:
             for c, v in sorted(ctr[k].items()):
                 w.writerow([k, c, "%.6g" % v])
-    out = {"round": tag, "source": src, "kernels": {}}
-    lines = ["# rocprofv3 summary, %s" % tag, "",
+    # the build the profile measured (scripts/gpu_profile.sh copies the
+    # library's build info next to the traces); bench.py attaches these
+    # counters only to a library with the same build id
+    binfo = os.path.join(src, "build.json")
+    build_id = json.load(open(binfo)).get("build_id") if os.path.exists(binfo) else None
+    out = {"round": tag, "source": src, "build_id": build_id, "kernels": {}}
+    lines = ["# rocprofv3 summary, %s (library build %s)" % (tag, build_id), "",
              "Kernel trace: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 20 "
              "--warmup 5 --cpu-baseline 0`.  PMC: one `rocprofv3 --pmc <set>` pass per counter "
              "set of `bench.py --steps 2 --warmup 1 --cpu-baseline 0 --ooc 0 --frame 0 "

@@ -99,8 +99,8 @@ SIGNATURES = {
     "spray_rt_spawn_shadows_ao_ordered": (I, [P, P, P, P, SZ, I, P, P, P, P]),
     "spray_rt_spawn_shadows_ao_traced": (I, [P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_occluded_scene_order": (I, [P, P, SZ, P, P, P]),
-    "spray_rt_occluded_ao": (I, [P, P, P, P, SZ, I, P, P, P, P, P, P]),
-    "spray_rt_spawn_shadows_ao_pairs": (I, [P, P, P, P, SZ, I, P, P, P, P]),
+    "spray_rt_occluded_ao": (I, [P, P, P, P, SZ, I, SZ, P, P, P, P, P, P]),
+    "spray_rt_spawn_shadows_ao_pairs": (I, [P, P, P, P, SZ, I, SZ, P, P, P, P]),
     "spray_rt_occluded_ao_pairs": (I, [P, SZ, P, P, P, I, P, P, P]),
     "spray_rt_ooc_create": (I, [P, I, P]),
     "spray_rt_ooc_destroy": (I, [P]),
@@ -122,6 +122,9 @@ SIGNATURES = {
     "spray_rt_tile_list": (I, [I, I, I, I, I, I, C.c_longlong, P, I, P]),
     "spray_rt_write_ppm": (I, [C.c_char_p, P, I, I]),
     "spray_rt_lane_create": (I, [P, P]),
+    "spray_rt_lane_create_error": (C.c_char_p, []),
+    "spray_rt_lane_update_intersection1M": (I, [P, I, P, SZ, SZ]),
+    "spray_rt_update_intersection1M": (I, [P, I, P, SZ, SZ]),
     "spray_rt_lane_destroy": (I, [P]),
     "spray_rt_lane_last_error": (C.c_char_p, [P]),
     "spray_rt_lane_intersect1M": (I, [P, I, P, SZ, SZ]),

@@ -494,7 +494,10 @@ bool quantize_nodes4(const std::vector<BvhNode>& nodes, QGrid* grid,
   // depth-first layout: children follow their parent
   for (size_t i = nodes.size(); i-- > 0;)
     c.height[i] = 1 + std::max(c.h_of(nodes[i].left), c.h_of(nodes[i].right));
-  if (c.height[0] > kQ4Stack) return false;
+  if (c.height[0] > kQ4Stack) {  // reported as a stack overflow, not a grid failure
+    if (stack_bound) *stack_bound = c.height[0];
+    return false;
+  }
   c.emit(0, 0);
   if (stack_bound) *stack_bound = c.bound;
   return c.ok && c.bound <= kQ4Stack;

@@ -84,7 +84,8 @@ const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* 
   std::vector<QNode4> qn;
   int qstack = 0;  // <= kQ4Stack, which the any-hit launches provide
   if (quantized && !img.nodes.empty() && !quantize_nodes4(img.nodes, &grid, &qn, &qstack))
-    return "vertex coordinates beyond the range of the quantized node grid";
+    return qstack > kQ4Stack ? "4-wide node collapse exceeds the any-hit walk's stack (kQ4Stack)"
+                             : "vertex coordinates beyond the range of the quantized node grid";
   // QGrid at nodes - 32, QNode4 i at nodes - 64 - 64 (i + 1) (rt_common.h)
   const size_t b_q = qn.empty() ? 0 : align256(64 + qn.size() * sizeof(QNode4));
   const size_t b_nodes = align256(img.nodes.size() * sizeof(BvhNode));
@@ -541,6 +542,14 @@ int spray_rt_occluded1M(spray_rt_ctx_t c, int slot, void* rays, size_t M,
   return run_rtc(c, &slot, off, 1, rays, stride, launch_rtc_occluded);
 }
 
+int spray_rt_update_intersection1M(spray_rt_ctx_t c, int slot, void* rays, size_t M,
+                                   size_t stride) {
+  if (c && stride < sizeof(spray_rt_ray_intersection))
+    return fail(c, SPRAY_RT_ERR_ARG, "stride %zu below the 96-B RTCRayIntersection", stride);
+  size_t off[2] = {0, M};
+  return run_rtc(c, &slot, off, 1, rays, stride, launch_rtc_update);
+}
+
 int spray_rt_intersect_segments(spray_rt_ctx_t c, const int* slots,
                                 const size_t* offsets, int nseg, void* rays,
                                 size_t stride) {
@@ -632,22 +641,42 @@ int lane_rtc(spray_rt_lane* L, int slot, void* rays, size_t M, size_t stride, La
 
 extern "C" {
 
+// Lane creation runs on many host threads at once (one lane per thread,
+// created on first use): its failures go to a thread-local message, never to
+// the context's shared error string.
+static thread_local std::string t_lane_create_err;
+
 int spray_rt_lane_create(spray_rt_ctx_t c, spray_rt_lane_t* out) {
-  if (!c || !out) return SPRAY_RT_ERR_ARG;
+  if (!c || !out) {
+    t_lane_create_err = "null context or output";
+    return SPRAY_RT_ERR_ARG;
+  }
   *out = nullptr;
-  HIPCHK(c, hipSetDevice(c->device));
+  const hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) {
+    t_lane_create_err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return SPRAY_RT_ERR_HIP;
+  }
   spray_rt_lane* L = new (std::nothrow) spray_rt_lane;
-  if (!L) return SPRAY_RT_ERR_NOMEM;
+  if (!L) {
+    t_lane_create_err = "out of host memory";
+    return SPRAY_RT_ERR_NOMEM;
+  }
   L->ctx = c;
   if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&L->d_seg_slot), 256) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&L->d_seg_off), 256) != hipSuccess) {
+    (void)hipGetLastError();
     spray_rt_lane_destroy(L);
-    return fail(c, SPRAY_RT_ERR_HIP, "lane creation failed");
+    t_lane_create_err = "lane creation failed (stream or device buffers)";
+    return SPRAY_RT_ERR_HIP;
   }
+  t_lane_create_err.clear();
   *out = L;
   return SPRAY_RT_OK;
 }
+
+const char* spray_rt_lane_create_error(void) { return t_lane_create_err.c_str(); }
 
 int spray_rt_lane_destroy(spray_rt_lane_t L) {
   if (!L) return SPRAY_RT_ERR_ARG;
@@ -671,6 +700,13 @@ int spray_rt_lane_intersect1M(spray_rt_lane_t L, int slot, void* rays, size_t M,
 
 int spray_rt_lane_occluded1M(spray_rt_lane_t L, int slot, void* rays, size_t M, size_t stride) {
   return lane_rtc(L, slot, rays, M, stride, launch_rtc_occluded);
+}
+
+int spray_rt_lane_update_intersection1M(spray_rt_lane_t L, int slot, void* rays, size_t M,
+                                        size_t stride) {
+  if (L && stride < sizeof(spray_rt_ray_intersection))
+    return lane_fail(L, SPRAY_RT_ERR_ARG, "stride %zu below the 96-B RTCRayIntersection", stride);
+  return lane_rtc(L, slot, rays, M, stride, launch_rtc_update);
 }
 
 int spray_rt_lane_domains1M(spray_rt_lane_t L, const float* org, const float* dir, size_t M,
@@ -1078,9 +1114,11 @@ int spray_rt_spawn_shadows_ao(spray_rt_ctx_t c, const spray_rt_ray* rays,
 
 int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
                                     const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                    int nsamples, uint32_t* out_pairs, float* lv, float* rec,
-                                    uint32_t* d_count) {
+                                    int nsamples, size_t npix, uint32_t* out_pairs, float* lv,
+                                    float* rec, uint32_t* d_count) {
   if (!c) return SPRAY_RT_ERR_ARG;
+  if (npix == 0 || npix > (size_t(1) << 31))
+    return fail(c, SPRAY_RT_ERR_ARG, "AO pairs need 0 < npix <= 2^31 (lv holds npix pixels)");
   if (!d_count || nsamples <= 0 || nsamples > 32)
     return fail(c, SPRAY_RT_ERR_ARG, "AO pairs need 1..32 samples and a device count");
   if (M >= (size_t(1) << 27) || M * size_t(nsamples) > 0xFFFFFFFFull)
@@ -1094,8 +1132,8 @@ int spray_rt_spawn_shadows_ao_pairs(spray_rt_ctx_t c, const spray_rt_ray* rays,
   int r = ensure(c, &bc, &c->block_cap, ao_scratch_bytes(M, nsamples));
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
-  HIPCHK(c, launch_spawn_ao_pairs(stream_of(c), rays, hits, pixid, M, nsamples, out_pairs, lv,
-                                  rec, d_count, c->d_block_counts));
+  HIPCHK(c, launch_spawn_ao_pairs(stream_of(c), rays, hits, pixid, M, nsamples, npix, out_pairs,
+                                  lv, rec, d_count, c->d_block_counts));
   return SPRAY_RT_OK;
 }
 
@@ -1118,11 +1156,11 @@ int spray_rt_occluded_ao_pairs(spray_rt_ctx_t c, size_t max_n, const uint32_t* p
 }
 
 int spray_rt_occluded_ao(spray_rt_ctx_t c, const spray_rt_ray* rays, const spray_rt_hit* hits,
-                         const int32_t* pixid, size_t M, int nsamples, uint32_t* out_pairs,
-                         float* lv, float* rec, uint32_t* d_count, uint8_t* occ,
-                         unsigned long long* d_counters) {
-  int r = spray_rt_spawn_shadows_ao_pairs(c, rays, hits, pixid, M, nsamples, out_pairs, lv, rec,
-                                          d_count);
+                         const int32_t* pixid, size_t M, int nsamples, size_t npix,
+                         uint32_t* out_pairs, float* lv, float* rec, uint32_t* d_count,
+                         uint8_t* occ, unsigned long long* d_counters) {
+  int r = spray_rt_spawn_shadows_ao_pairs(c, rays, hits, pixid, M, nsamples, npix, out_pairs, lv,
+                                          rec, d_count);
   if (r) return r;
   return spray_rt_occluded_ao_pairs(c, M * size_t(nsamples), out_pairs, rec, lv, nsamples,
                                     d_count, occ, d_counters);

@@ -73,6 +73,10 @@ static_assert(sizeof(QNode4) == 64, "4-wide quantized node must be 64 B");
 // stack entries of the 4-wide walk: the launch's LDS stack (STK) plus a
 // private overflow of kQ4Stack - STK
 constexpr int kQ4Stack = 40;
+// the collapse's stack bound never exceeds the BVH2 height, which the builder
+// caps at kMaxDepth (+1 for the root level): a tree the builder accepts always
+// fits the 4-wide walk's stack, so quantize_nodes4 fails only on the grid
+static_assert(kMaxDepth + 1 <= kQ4Stack, "4-wide walk stack below the BVH2 height bound");
 struct alignas(16) QGrid {
   float base[3];
   float pad0;

@@ -18,6 +18,10 @@ hipError_t launch_rtc_intersect(hipStream_t s, const SlotDesc* slots,
 hipError_t launch_rtc_occluded(hipStream_t s, const SlotDesc* slots,
                                const int* seg_slot, const size_t* seg_off,
                                int nseg, char* rays, size_t stride, size_t M);
+// TriMeshBuffer::updateIntersection alone: color and Ns of the hit records
+hipError_t launch_rtc_update(hipStream_t s, const SlotDesc* slots, const int* seg_slot,
+                             const size_t* seg_off, int nseg, char* rays, size_t stride,
+                             size_t M);
 
 hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
                           const float* org, const float* dir, size_t M,
@@ -162,8 +166,8 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
 // (origin + pixel bits, normal, tangent frame).
 hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                 int nsamples, uint32_t* out_pairs, float* lv, float* rec,
-                                 uint32_t* d_count, void* scratch);
+                                 int nsamples, size_t npix, uint32_t* out_pairs, float* lv,
+                                 float* rec, uint32_t* d_count, void* scratch);
 // any hit of those pairs' AO rays, each generated in its any-hit lane
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,

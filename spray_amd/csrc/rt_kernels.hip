@@ -138,6 +138,30 @@ __global__ __launch_bounds__(kBlock) void k_rtc_intersect(
   o[23] = nsz;
 }
 
+// TriMeshBuffer::updateIntersection (src/render/trimesh_buffer.cc:328-360)
+// on its own: color and Ns of every record whose geomID says hit, from its
+// primID, u and v -- the epilogue k_rtc_intersect fuses, same operations.
+__global__ __launch_bounds__(kBlock) void k_rtc_update(
+    const SlotDesc* __restrict__ slots, const int* __restrict__ seg_slot,
+    const size_t* __restrict__ seg_off, int nseg, char* __restrict__ rays,
+    size_t stride, size_t M) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= M) return;
+  const int seg = nseg == 1 ? 0 : find_segment(seg_off, nseg, i);
+  const SlotDesc s = slots[seg_slot[seg]];
+  char* rec = rays + i * stride;
+  uint32_t* ou = reinterpret_cast<uint32_t*>(rec);
+  float* o = reinterpret_cast<float*>(rec);
+  if (ou[18] == 0xFFFFFFFFu || ou[19] >= s.ntris) return;  // no hit / not this mesh
+  uint32_t color;
+  float nsx, nsy, nsz;
+  epilogue(s, ou[19], o[16], o[17], color, nsx, nsy, nsz);
+  ou[15] = color;
+  o[21] = nsx;
+  o[22] = nsy;
+  o[23] = nsz;
+}
+
 __global__ __launch_bounds__(kBlock) void k_rtc_occluded(
     const SlotDesc* __restrict__ slots, const int* __restrict__ seg_slot,
     const size_t* __restrict__ seg_off, int nseg, char* __restrict__ rays,
@@ -1532,7 +1556,7 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write(
 __global__ __launch_bounds__(kBlock) void k_spawn_ao_hitmask(
     const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
     const int32_t* __restrict__ pixid, uint32_t M, uint32_t ns, uint2* __restrict__ meta,
-    uint32_t* __restrict__ tile_counts, float4* __restrict__ rec) {
+    uint32_t* __restrict__ tile_counts, float4* __restrict__ rec, uint32_t npix) {
   using Scan = hipcub::BlockScan<uint32_t, kBlock>;
   __shared__ typename Scan::TempStorage tmp;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -1541,8 +1565,11 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_hitmask(
     const spray_rt_hit h = hits[i];
     if (h.domain >= 0) {
       const int32_t px = pixid[i];
-      for (uint32_t l = 0; l < ns; ++l)
-        if (ao_ok(rays + i, h, px, int(l), int(ns))) mask |= 1u << l;
+      // pairs form: the (pixel, sample) table holds npix pixels; a ray of a
+      // pixel outside it spawns nothing (its table entries do not exist)
+      if (!rec || uint32_t(px) < npix)
+        for (uint32_t l = 0; l < ns; ++l)
+          if (ao_ok(rays + i, h, px, int(l), int(ns))) mask |= 1u << l;
       if (rec && mask) {
         const spray_rt_ray r = rays[i];
         const float ht = h.t;
@@ -1808,6 +1835,14 @@ hipError_t launch_rtc_occluded(hipStream_t s, const SlotDesc* slots,
   if (M == 0) return hipSuccess;
   k_rtc_occluded<<<grid_for(M), kBlock, 0, s>>>(slots, seg_slot, seg_off, nseg,
                                                 rays, stride, M);
+  return hipGetLastError();
+}
+
+hipError_t launch_rtc_update(hipStream_t s, const SlotDesc* slots, const int* seg_slot,
+                             const size_t* seg_off, int nseg, char* rays, size_t stride,
+                             size_t M) {
+  if (M == 0) return hipSuccess;
+  k_rtc_update<<<grid_for(M), kBlock, 0, s>>>(slots, seg_slot, seg_off, nseg, rays, stride, M);
   return hipGetLastError();
 }
 
@@ -2185,7 +2220,8 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
     uint2* meta = static_cast<uint2*>(scratch);
     uint32_t* tiles = reinterpret_cast<uint32_t*>(meta + M);
     k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
-                                            uint32_t(nsamples), meta, tiles, nullptr);
+                                            uint32_t(nsamples), meta, tiles, nullptr,
+                                            0xFFFFFFFFu);
     k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
     k_spawn_ao_write_hits<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M),
                                                uint32_t(nsamples), meta, tiles, out_rays,
@@ -2205,15 +2241,16 @@ hipError_t launch_spawn_ao(hipStream_t s, const spray_rt_ray* rays, const spray_
 
 hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
-                                 int nsamples, uint32_t* out_pairs, float* lv, float* rec,
-                                 uint32_t* d_count, void* scratch) {
+                                 int nsamples, size_t npix, uint32_t* out_pairs, float* lv,
+                                 float* rec, uint32_t* d_count, void* scratch) {
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
   if (nsamples > 32) return hipErrorInvalidValue;
   const uint32_t g = uint32_t((M + kBlock - 1) / kBlock);
   uint2* meta = static_cast<uint2*>(scratch);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(meta + M);
   k_spawn_ao_hitmask<<<g, kBlock, 0, s>>>(rays, hits, pixid, uint32_t(M), uint32_t(nsamples),
-                                          meta, tiles, reinterpret_cast<float4*>(rec));
+                                          meta, tiles, reinterpret_cast<float4*>(rec),
+                                          uint32_t(npix < 0xFFFFFFFFull ? npix : 0xFFFFFFFFull));
   k_scan_blocks<<<1, 1024, 0, s>>>(tiles, g, d_count);
   k_spawn_ao_index<<<g, kBlock, 0, s>>>(uint32_t(M), uint32_t(nsamples), meta, tiles,
                                         out_pairs, pixid, reinterpret_cast<float4*>(lv));

@@ -44,6 +44,12 @@ def _nbytes(x):
     return x.numel() * x.element_size()
 
 
+def _lv_pixels(lv, nsamples):
+    """Pixels the (pixel, sample) table lv holds (float4 per entry): the
+    engine's bound on the pixel ids of an AO pairs spawn."""
+    return _nbytes(lv) // (16 * int(nsamples))
+
+
 def camera_init(pos, lookat, up, vfov, w, h):
     """Camera::init (src/render/camera.h:128-166) -> float32[14]."""
     cam = np.zeros(14, np.float32)
@@ -421,8 +427,9 @@ class RtContext:
         e, k6 = _addr(d_count)
         f, k7 = _addr(occ)
         g, k8 = _addr(counters) if counters is not None else (None, None)
-        self._check(lib().spray_rt_occluded_ao(self.h, a, b, p, int(n), int(nsamples), c, d, r,
-                                               e, f, g), "occluded_ao")
+        self._check(lib().spray_rt_occluded_ao(self.h, a, b, p, int(n), int(nsamples),
+                                               _lv_pixels(lv, nsamples), c, d, r, e, f, g),
+                    "occluded_ao")
 
     def spawn_shadows_ao_pairs(self, rays, hits, pixid, n, nsamples, out_pairs, lv, rec,
                                d_count):
@@ -437,7 +444,8 @@ class RtContext:
         r, k7 = _addr(rec)
         e, k6 = _addr(d_count)
         self._check(lib().spray_rt_spawn_shadows_ao_pairs(self.h, a, b, p, int(n), int(nsamples),
-                                                          c, d, r, e), "spawn_shadows_ao_pairs")
+                                                          _lv_pixels(lv, nsamples), c, d, r, e),
+                    "spawn_shadows_ao_pairs")
 
     def occluded_ao_pairs(self, max_n, pairs, rec, lv, nsamples, d_count, occ, counters=None):
         """Any hit of the AO rays of (source << 5 | sample) pairs, each

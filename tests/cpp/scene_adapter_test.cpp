@@ -1,28 +1,43 @@
-// Mock ooc drain over the SceneT drop-in (include/spray_scene.hpp) from N
-// OpenMP threads, with the reference's call shapes (ooc_tcontext.inl:28-100,
-// ooc_pcontext.h:144-157, ooc_isector.h:116-124):
+// Mock drains over the SceneT drop-in (include/spray_scene.hpp) from N
+// OpenMP threads, with the reference's call shapes.  Test infrastructure:
+// built by __graft_entry__.build(), run by tests/test_gpu_adapter.py.
 //
+//   scene_adapter_test <scene.spray> <ply_path> <threads> <cache_size> [mode] [image]
+//
+// mode "single" (default; ooc_tcontext.inl:28-100, ooc_pcontext.h:144-157,
+// ooc_isector.h:116-124): one ray per call, as the reference calls Scene:
 //   #pragma omp single   scene.load(id, &sinfo);
 //   every thread:        scene.intersect(sinfo.rtc_scene, sinfo.cache_block,
 //                                        r->org, r->dir, &rtc_isect_);
 //                        scene.occluded(sinfo.rtc_scene, pos, wi, &rtc_ray_);
 //                        scene.intersectDomains(ray_ext);
+// every result checked against brute force over the domain's triangles.
 //
-// Every result is checked against the CPU oracle (oracle/oracle.h): domain
-// lists bit-exact against or_domain_query, each per-domain closest hit
-// (t, u, v, primID, Ng, color, Ns) and occlusion bit-exact against brute
-// force over that domain's triangles.  Test infrastructure: built by
-// __graft_entry__.build(), run by tests/test_gpu_adapter.py.
+// mode "current": the baseline tracers' scene-less forms (load(id), then
+// intersect(org, dir, isect) / occluded(org, dir, ray) on the current
+// domain, updateIntersection(isect); baseline_shader_pt.h:110, 139,
+// baseline_shader_ao.h:90, baseline_insitu_tracer.inl:653-700).
 //
-//   scene_adapter_test <scene.spray> <ply_path> <threads> <cache_size>
+// mode "batched": the same drain as gather -> one stream call -> scatter per
+// thread and domain (Scene::intersect1M / occluded1M /
+// intersectDomains1M): each thread copies its share of the domain's queue
+// into RTCRayIntersection records, makes one call, and checks the results
+// in queue order; its shadow rays likewise.  image x image camera rays at
+// 1 spp; every result checked against the oracle's canonical BVH of the
+// domain (bit-equal to brute force, tests/test_oracle.py).  Prints the
+// drain's rate (ray-domain pairs + shadow rays per second, timed apart from
+// the checks) and, for comparison, the per-ray form's rate over the first
+// queues.
 #include <omp.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "spray_scene.hpp"
@@ -69,17 +84,85 @@ struct RTCRayExt {  // rays.h:117-170
 };
 
 bool same(float a, float b) { return std::memcmp(&a, &b, 4) == 0; }
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
-}  // namespace
+const float kLight[3] = {0.f, 500.f, 1000.f};
 
-int main(int argc, char** argv) {
-  if (argc < 5) {
-    std::fprintf(stderr, "usage: %s scene.spray ply_path threads cache_size\n", argv[0]);
-    return 2;
+// the point-light shadow ray of a hit (the test's own, same on both sides)
+void shadow_ray(const float* o, const float* d, float t, float ps[3], float wi[3]) {
+  for (int k = 0; k < 3; ++k) ps[k] = o[k] + t * d[k];
+  float len = 0.f;
+  for (int k = 0; k < 3; ++k) {
+    wi[k] = kLight[k] - ps[k];
+    len += wi[k] * wi[k];
   }
-  const int T = std::atoi(argv[3]), cache = std::atoi(argv[4]);
+  len = std::sqrt(len);
+  for (int k = 0; k < 3; ++k) wi[k] /= len;
+}
+
+struct Meshes {  // per-domain oracle data (TriMeshBuffer::load through the host layer)
+  std::vector<std::vector<float>> tri, normals, verts;
+  std::vector<std::vector<uint32_t>> faces, colors;
+  std::vector<or_bvh*> bvh;
+  std::vector<float> boxes;
+  ~Meshes() {
+    for (or_bvh* b : bvh)
+      if (b) or_bvh_free(b);
+  }
+};
+
+void load_meshes(const char* desc, const char* ply, const spray_amd::Scene<>& scene, Meshes* m,
+                 bool bvh) {
+  const int nd = int(scene.getNumDomains());
+  m->tri.resize(nd);
+  m->verts.resize(nd);
+  m->faces.resize(nd);
+  m->colors.resize(nd);
+  m->normals.resize(nd);
+  m->bvh.assign(nd, nullptr);
+  m->boxes.resize(6 * size_t(nd));
+  for (int d = 0; d < nd; ++d) {
+    size_t nv = 0, nf = 0;
+    spray_host_domain_mesh(desc, ply, d, &nv, &nf, nullptr, nullptr, nullptr, nullptr);
+    m->verts[d].resize(3 * nv);
+    m->faces[d].resize(3 * nf);
+    m->colors[d].resize(nv);
+    m->normals[d].resize(3 * nv);
+    spray_host_domain_mesh(desc, ply, d, &nv, &nf, m->verts[d].data(), m->faces[d].data(),
+                           m->colors[d].data(), m->normals[d].data());
+    m->tri[d].resize(12 * nf);
+    or_prep_tris(m->verts[d].data(), m->faces[d].data(), nf, m->tri[d].data());
+    if (bvh) m->bvh[d] = or_bvh_build(m->verts[d].data(), m->faces[d].data(), nf);
+    std::memcpy(&m->boxes[6 * size_t(d)], scene.getDomains()[size_t(d)].world_aabb, 24);
+  }
+}
+
+// the closest-hit record of one ray in domain id against the oracle's
+// (t, u, v, prim); p == 0xFFFFFFFF: a miss (the record must say so)
+bool check_hit(const Meshes& m, int id, const RTCRayIntersection& r, bool hit, float t, float u,
+               float v, uint32_t p) {
+  bool ok = hit == (p != 0xFFFFFFFFu);
+  if (ok && hit) {
+    uint32_t col;
+    float ns[3];
+    or_epilogue(m.faces[id].data(), m.colors[id].data(), m.normals[id].data(), &p, &u, &v, 1,
+                &col, ns);
+    const float* ng = &m.tri[id][12 * size_t(p) + 9];
+    ok = r.primID == p && same(r.tfar, t) && same(r.u, u) && same(r.v, v) && r.geomID == 0 &&
+         r.color == col;
+    for (int k = 0; k < 3; ++k) ok = ok && same(r.Ns[k], ns[k]) && same(r.Ng[k], ng[k]);
+  }
+  if (!hit) ok = ok && std::isinf(r.tfar) && r.geomID == SPRAY_RT_INVALID_ID;
+  return ok;
+}
+
+// mode "single" / "current": one ray per call, brute-force checks
+int run_single(const char* desc, const char* ply, int T, int cache, bool current) {
   spray_amd::Scene<> scene;
-  scene.init(argv[1], argv[2], "", cache, 0, false, 1);
+  scene.init(desc, ply, "", cache, 0, false, 1);
   const int nd = int(scene.getNumDomains());
   const int W = 96, H = 96;
   const float pos[3] = {90.172180f, 84.141418f, 82.480225f}, at[3] = {30.f, 28.649426f, 30.f},
@@ -90,33 +173,15 @@ int main(int argc, char** argv) {
   std::vector<float> org(3 * n), dir(3 * n);
   std::vector<int32_t> pix(n), sam(n);
   or_eye_rays_ooc(cam, W, 1, 0, 0, W, H, org.data(), dir.data(), pix.data(), sam.data());
-  const float light[3] = {0.f, 500.f, 1000.f};
-
-  // per-domain oracle meshes (TriMeshBuffer::load through the host layer)
-  std::vector<std::vector<float>> tri(nd);
-  std::vector<std::vector<uint32_t>> faces(nd), colors(nd);
-  std::vector<std::vector<float>> normals(nd);
-  std::vector<float> boxes(6 * size_t(nd));
-  for (int d = 0; d < nd; ++d) {
-    size_t nv = 0, nf = 0;
-    spray_host_domain_mesh(argv[1], argv[2], d, &nv, &nf, nullptr, nullptr, nullptr, nullptr);
-    std::vector<float> v(3 * nv);
-    faces[d].resize(3 * nf);
-    colors[d].resize(nv);
-    normals[d].resize(3 * nv);
-    spray_host_domain_mesh(argv[1], argv[2], d, &nv, &nf, v.data(), faces[d].data(),
-                           colors[d].data(), normals[d].data());
-    tri[d].resize(12 * nf);
-    or_prep_tris(v.data(), faces[d].data(), nf, tri[d].data());
-    std::memcpy(&boxes[6 * size_t(d)], scene.getDomains()[size_t(d)].world_aabb, 24);
-  }
+  Meshes m;
+  load_meshes(desc, ply, scene, &m, false);
 
   std::atomic<long> bad{0}, nhit{0}, nocc{0}, ncalls{0};
   // domain lists from every thread at once (Isector::isectDomains)
   std::vector<std::vector<int>> lists(n);
   std::vector<int32_t> oids(n * size_t(nd)), ocnt(n);
   std::vector<float> ots(n * size_t(nd));
-  or_domain_query(org.data(), dir.data(), n, boxes.data(), nd, nd, oids.data(), ots.data(),
+  or_domain_query(org.data(), dir.data(), n, m.boxes.data(), nd, nd, oids.data(), ots.data(),
                   ocnt.data());
 #pragma omp parallel for num_threads(T) schedule(dynamic, 32)
   for (long i = 0; i < long(n); ++i) {
@@ -144,43 +209,43 @@ int main(int argc, char** argv) {
     RTCRay rtc_ray_;
     for (int id = 0; id < nd; ++id) {
 #pragma omp single
-      scene.load(id, &sinfo);
+      {
+        if (current)
+          scene.load(id);
+        else
+          scene.load(id, &sinfo);
+      }
 #pragma omp for schedule(dynamic, 8)
       for (long q = 0; q < long(queue[id].size()); ++q) {
         const long i = queue[id][q];
         const float* o = &org[3 * i];
         const float* d = &dir[3 * i];
-        const bool hit = scene.intersect(sinfo.rtc_scene, sinfo.cache_block, o, d, &rtc_isect_);
+        bool hit;
+        if (current) {
+          hit = scene.intersect(o, d, &rtc_isect_);
+          if (hit) {  // Scene::updateIntersection recomputes color / Ns in place
+            rtc_isect_.color = 0xDEADBEEFu;
+            rtc_isect_.Ns[0] = rtc_isect_.Ns[1] = rtc_isect_.Ns[2] = -7.f;
+            scene.updateIntersection(&rtc_isect_);
+          }
+        } else {
+          hit = scene.intersect(sinfo.rtc_scene, sinfo.cache_block, o, d, &rtc_isect_);
+        }
         ++ncalls;
         float t, u, v;
         uint32_t p;
-        or_brute_intersect(tri[id].data(), faces[id].size() / 3, o, d, nullptr, nullptr, 1, &t,
-                           &u, &v, &p);
-        bool ok = hit == (p != 0xFFFFFFFFu);
+        or_brute_intersect(m.tri[id].data(), m.faces[id].size() / 3, o, d, nullptr, nullptr, 1,
+                           &t, &u, &v, &p);
+        bool ok = check_hit(m, id, rtc_isect_, hit, t, u, v, p);
         if (ok && hit) {
-          uint32_t col;
-          float ns[3];
-          or_epilogue(faces[id].data(), colors[id].data(), normals[id].data(), &p, &u, &v, 1,
-                      &col, ns);
-          const float* ng = &tri[id][12 * p + 9];
-          ok = rtc_isect_.primID == p && same(rtc_isect_.tfar, t) && same(rtc_isect_.u, u) &&
-               same(rtc_isect_.v, v) && rtc_isect_.geomID == 0 && rtc_isect_.color == col;
-          for (int k = 0; k < 3; ++k)
-            ok = ok && same(rtc_isect_.Ns[k], ns[k]) && same(rtc_isect_.Ng[k], ng[k]);
           // a shadow ray toward the light from the hit, in the same domain
           float ps[3], wi[3];
-          for (int k = 0; k < 3; ++k) ps[k] = o[k] + t * d[k];
-          float len = 0.f;
-          for (int k = 0; k < 3; ++k) {
-            wi[k] = light[k] - ps[k];
-            len += wi[k] * wi[k];
-          }
-          len = std::sqrt(len);
-          for (int k = 0; k < 3; ++k) wi[k] /= len;
-          const bool occ = scene.occluded(sinfo.rtc_scene, ps, wi, &rtc_ray_);
+          shadow_ray(o, d, t, ps, wi);
+          const bool occ = current ? scene.occluded(ps, wi, &rtc_ray_)
+                                   : scene.occluded(sinfo.rtc_scene, ps, wi, &rtc_ray_);
           uint8_t oo;
-          or_brute_occluded(tri[id].data(), faces[id].size() / 3, ps, wi, nullptr, nullptr, 1,
-                            &oo);
+          or_brute_occluded(m.tri[id].data(), m.faces[id].size() / 3, ps, wi, nullptr, nullptr,
+                            1, &oo);
           ok = ok && occ == (oo != 0) && (!occ || rtc_ray_.geomID == 0);
           ++nhit;
           if (occ) ++nocc;
@@ -189,13 +254,197 @@ int main(int argc, char** argv) {
       }
     }
   }
-  std::printf("threads %d cache %d rays %zu domain-list mismatches %ld calls %ld hits %ld "
-              "occluded %ld mismatches %ld\n",
-              T, cache, n, bad_lists, ncalls.load(), nhit.load(), nocc.load(), bad.load());
+  std::printf("mode %s threads %d cache %d rays %zu domain-list mismatches %ld calls %ld "
+              "hits %ld occluded %ld mismatches %ld\n",
+              current ? "current" : "single", T, cache, n, bad_lists, ncalls.load(), nhit.load(),
+              nocc.load(), bad.load());
   if (bad.load() || nhit.load() < 1000 || nocc.load() == 0 || nocc.load() == nhit.load()) {
     std::printf("FAIL\n");
     return 1;
   }
   std::printf("ok\n");
   return 0;
+}
+
+// mode "batched": per thread and domain one gather -> stream call -> scatter
+int run_batched(const char* desc, const char* ply, int T, int cache, int img) {
+  spray_amd::Scene<> scene;
+  scene.init(desc, ply, "", cache, 0, false, 1);
+  const int nd = int(scene.getNumDomains());
+  const float pos[3] = {90.172180f, 84.141418f, 82.480225f}, at[3] = {30.f, 28.649426f, 30.f},
+              up[3] = {0.f, 1.f, 0.f};
+  float cam[14];
+  or_camera_init(pos, at, up, 90.f, img, img, cam);
+  const size_t n = size_t(img) * size_t(img);
+  std::vector<float> org(3 * n), dir(3 * n);
+  std::vector<int32_t> pix(n), sam(n);
+  or_eye_rays_ooc(cam, img, 1, 0, 0, img, img, org.data(), dir.data(), pix.data(), sam.data());
+  Meshes m;
+  load_meshes(desc, ply, scene, &m, true);
+
+  // domain lists of the whole queue in one call (Isector::isectDomains)
+  std::vector<int32_t> ids(n * size_t(nd)), cnt(n), oids(n * size_t(nd)), ocnt(n);
+  std::vector<float> ts(n * size_t(nd)), ots(n * size_t(nd));
+  scene.intersectDomains1M(org.data(), dir.data(), n, ids.data(), ts.data(), cnt.data(), nd);
+  or_domain_query(org.data(), dir.data(), n, m.boxes.data(), nd, nd, oids.data(), ots.data(),
+                  ocnt.data());
+  long bad_lists = 0;
+  for (size_t i = 0; i < n; ++i) {
+    bool ok = cnt[i] == ocnt[i];
+    for (int k = 0; ok && k < cnt[i]; ++k)
+      ok = ids[i * nd + k] == oids[i * nd + k] && same(ts[i * nd + k], ots[i * nd + k]);
+    if (!ok) ++bad_lists;
+  }
+  std::vector<std::vector<long>> queue(nd);
+  for (size_t i = 0; i < n; ++i)
+    for (int k = 0; k < cnt[i]; ++k) queue[ids[i * nd + k]].push_back(long(i));
+
+  // per (domain, thread) results of the timed drain, checked afterwards
+  struct Part {
+    std::vector<long> rays;
+    std::vector<RTCRayIntersection> isect;
+    std::vector<long> src;  // shadow ray -> position in rays
+    std::vector<RTCRay> shadow;
+  };
+  std::vector<std::vector<Part>> parts(nd, std::vector<Part>(T));
+  std::atomic<long> npair{0}, nshadow{0}, ncalls{0};
+  spray_amd::SceneInfo sinfo;
+  // warm the lanes (first call per thread creates its stream)
+  scene.load(0, &sinfo);
+#pragma omp parallel num_threads(T)
+  {
+    RTCRayIntersection w;
+    spray_amd::Scene<>::makeRay(&org[0], &dir[0], &w);
+    scene.intersect1M(sinfo, &w, 1);
+  }
+  const double t0 = now();
+#pragma omp parallel num_threads(T)
+  {
+    const int me = omp_get_thread_num();
+    for (int id = 0; id < nd; ++id) {
+#pragma omp single
+      scene.load(id, &sinfo);
+      // this thread's share of the queue (omp for static: contiguous)
+      const long qn = long(queue[id].size());
+      const long b = qn * me / T, e = qn * (me + 1) / T;
+      Part& P = parts[id][me];
+      if (e > b) {
+        P.rays.assign(queue[id].begin() + b, queue[id].begin() + e);
+        P.isect.resize(P.rays.size());
+        for (size_t k = 0; k < P.rays.size(); ++k)  // gather
+          spray_amd::Scene<>::makeRay(&org[3 * P.rays[k]], &dir[3 * P.rays[k]], &P.isect[k]);
+        scene.intersect1M(sinfo, P.isect.data(), P.isect.size());
+        ++ncalls;
+        for (size_t k = 0; k < P.rays.size(); ++k) {  // scatter, queue order: spawn
+          const RTCRayIntersection& r = P.isect[k];
+          if (r.geomID == SPRAY_RT_INVALID_ID) continue;
+          float ps[3], wi[3];
+          shadow_ray(&org[3 * P.rays[k]], &dir[3 * P.rays[k]], r.tfar, ps, wi);
+          RTCRay s;
+          spray_amd::Scene<>::makeRay(ps, wi, &s);
+          P.shadow.push_back(s);
+          P.src.push_back(long(k));
+        }
+        if (!P.shadow.empty()) {
+          scene.occluded1M(sinfo, P.shadow.data(), P.shadow.size());
+          ++ncalls;
+        }
+        npair += long(P.rays.size());
+        nshadow += long(P.shadow.size());
+      }
+#pragma omp barrier
+    }
+  }
+  const double dt = now() - t0;
+
+  // checks against the oracle's BVH of each domain
+  long bad = 0, nhit = 0, nocc = 0;
+  for (int id = 0; id < nd; ++id)
+    for (int th = 0; th < T; ++th) {
+      const Part& P = parts[id][size_t(th)];
+      const size_t k = P.rays.size();
+      if (!k) continue;
+      std::vector<float> o(3 * k), d(3 * k), t(k), u(k), v(k);
+      std::vector<uint32_t> p(k);
+      for (size_t j = 0; j < k; ++j) {
+        std::memcpy(&o[3 * j], &org[3 * P.rays[j]], 12);
+        std::memcpy(&d[3 * j], &dir[3 * P.rays[j]], 12);
+      }
+      or_bvh_intersect(m.bvh[id], o.data(), d.data(), nullptr, nullptr, k, t.data(), u.data(),
+                       v.data(), p.data(), nullptr);
+      size_t sh = 0;
+      for (size_t j = 0; j < k; ++j) {
+        const bool hit = P.isect[j].geomID != SPRAY_RT_INVALID_ID;
+        if (!check_hit(m, id, P.isect[j], hit, t[j], u[j], v[j], p[j])) ++bad;
+        if (hit) {
+          ++nhit;
+          // the shadow ray this hit spawned, in queue order
+          if (sh >= P.src.size() || P.src[sh] != long(j)) {
+            ++bad;
+            continue;
+          }
+          float ps[3], wi[3];
+          shadow_ray(&o[3 * j], &d[3 * j], t[j], ps, wi);
+          uint8_t oo;
+          or_bvh_occluded(m.bvh[id], ps, wi, nullptr, nullptr, 1, &oo, nullptr);
+          const bool occ = P.shadow[sh].geomID != SPRAY_RT_INVALID_ID;
+          if (occ != (oo != 0) || (occ && P.shadow[sh].geomID != 0)) ++bad;
+          if (occ) ++nocc;
+          ++sh;
+        }
+      }
+      if (sh != P.src.size()) ++bad;
+    }
+  const double rate = double(npair.load() + nshadow.load()) / dt / 1e6;
+
+  // the per-ray form on the first queues (same calls as mode "single"), timed
+  long single_rays = 0;
+  double single_s = 0.0;
+  {
+    const double s0 = now();
+    for (int id = 0; id < nd && single_rays < 40000; ++id) {
+      scene.load(id, &sinfo);
+#pragma omp parallel for num_threads(T) schedule(dynamic, 64)
+      for (long q = 0; q < long(queue[id].size()); ++q) {
+        RTCRayIntersection r;
+        const long i = queue[id][q];
+        scene.intersect(sinfo.rtc_scene, sinfo.cache_block, &org[3 * i], &dir[3 * i], &r);
+      }
+      single_rays += long(queue[id].size());
+    }
+    single_s = now() - s0;
+  }
+  std::printf("mode batched threads %d cache %d rays %zu pairs %ld shadow %ld calls %ld "
+              "drain_s %.4f batched_Mrays_s %.2f per_ray_Mrays_s %.3f (%ld rays) "
+              "domain-list mismatches %ld hits %ld occluded %ld mismatches %ld\n",
+              T, cache, n, npair.load(), nshadow.load(), ncalls.load(), dt, rate,
+              single_rays / single_s / 1e6, single_rays, bad_lists, nhit, nocc, bad);
+  if (bad || bad_lists || nhit < 1000 || nocc == 0 || nocc == nhit) {
+    std::printf("FAIL\n");
+    return 1;
+  }
+  std::printf("ok\n");
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    std::fprintf(stderr,
+                 "usage: %s scene.spray ply_path threads cache_size [single|current|batched] "
+                 "[image]\n",
+                 argv[0]);
+    return 2;
+  }
+  const int T = std::atoi(argv[3]), cache = std::atoi(argv[4]);
+  const std::string mode = argc > 5 ? argv[5] : "single";
+  try {
+    if (mode == "batched") return run_batched(argv[1], argv[2], T, cache,
+                                              argc > 6 ? std::atoi(argv[6]) : 512);
+    return run_single(argv[1], argv[2], T, cache, mode == "current");
+  } catch (const std::exception& e) {
+    std::printf("FAIL exception: %s\n", e.what());
+    return 1;
+  }
 }

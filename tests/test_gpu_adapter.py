@@ -4,8 +4,12 @@ scene_adapter_test.cpp, built by __graft_entry__.build()) with domain loads in
 `omp single` and intersect / occluded / intersectDomains from every OpenMP
 thread at once, each result bit-exact against the CPU oracle -- with every
 domain resident and with a 4-block LRU cache that evicts while the threads
-drain."""
+drain; the baseline tracers' scene-less forms (load(id), intersect(org, dir,
+isect), occluded(org, dir, ray), updateIntersection); and the batched drain
+(gather -> intersect1M / occluded1M -> scatter per thread and domain), whose
+rate the test prints beside the per-ray form's."""
 import os
+import re
 import subprocess
 
 import pytest
@@ -16,11 +20,34 @@ pytestmark = pytest.mark.gpu
 BIN = os.path.join(ROOT, "tests", "cpp", "_build", "scene_adapter_test")
 
 
-@pytest.mark.parametrize("threads,cache", [(8, -1), (16, 4), (1, 2)])
-def test_scene_adapter_concurrent_drain(threads, cache):
+def _run(*args, timeout=240):
     assert os.path.exists(BIN), "build it with __graft_entry__.build()"
-    r = subprocess.run([BIN, WAVELETS64, SCENES, str(threads), str(cache)], capture_output=True,
-                       text=True, timeout=240)
+    r = subprocess.run([BIN, WAVELETS64, SCENES, *[str(a) for a in args]], capture_output=True,
+                       text=True, timeout=timeout)
     print(r.stdout, r.stderr)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
-    assert "mismatches 0" in r.stdout and "domain-list mismatches 0" in r.stdout
+    assert " mismatches 0" in r.stdout and "domain-list mismatches 0" in r.stdout
+    return r.stdout
+
+
+@pytest.mark.parametrize("threads,cache", [(8, -1), (16, 4), (1, 2)])
+def test_scene_adapter_concurrent_drain(threads, cache):
+    _run(threads, cache)
+
+
+@pytest.mark.parametrize("threads,cache", [(8, -1), (4, 4)])
+def test_scene_adapter_current_domain_forms(threads, cache):
+    """load(id) + the scene-less intersect / occluded and updateIntersection
+    of the baseline tracers (scene.h:169-189, 203)."""
+    _run(threads, cache, "current")
+
+
+@pytest.mark.parametrize("threads,cache,img", [(1, -1, 512), (8, -1, 1024), (16, 4, 1024)])
+def test_scene_adapter_batched_drain(threads, cache, img):
+    """The batched drain from 1, 8 and 16 threads (1024x1024 camera rays at
+    8 and 16), bit-exact against the oracle; prints its Mrays/s."""
+    out = _run(threads, cache, "batched", img, timeout=400)
+    m = re.search(r"batched_Mrays_s ([\d.]+) per_ray_Mrays_s ([\d.]+)", out)
+    assert m
+    batched, per_ray = float(m.group(1)), float(m.group(2))
+    assert batched > per_ray
