@@ -56,11 +56,15 @@ struct Carve {
 // fused launch (closest hit + shading + the shadow rays' any hit) and the
 // film.
 bool fused_frame(const spray_rt_ctx* c, const spray_rt_shader* P) {
-  return SPRAY_FRAME_FUSED && P->shader == SPRAY_RT_SHADER_PT && P->bounces == 1 &&
-         P->nlights == 1 && P->lights[0].type == SPRAY_RT_LIGHT_POINT && !c->bsdf_delta;
+  return SPRAY_FRAME_FUSED && spray_rt::detail::fused_pt_shading(c, P);
 }
 
 }  // namespace
+
+bool spray_rt::detail::fused_pt_shading(const spray_rt_ctx* c, const spray_rt_shader* P) {
+  return P->shader == SPRAY_RT_SHADER_PT && P->bounces == 1 && P->nlights == 1 &&
+         P->lights[0].type == SPRAY_RT_LIGHT_POINT && !c->bsdf_delta;
+}
 
 extern "C" {
 

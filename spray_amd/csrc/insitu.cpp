@@ -566,6 +566,112 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
   return SPRAY_RT_OK;
 }
 
+// Every domain is this rank's (one rank, or a partition that gives it all
+// of them): no copy of any ray can leave the rank and every ray's only
+// owner is its holder, so the exchange plans, the count reads and the key
+// round trip have nothing to decide.  The frame then runs as the device
+// frame layer does on the holder's own slots: per bounce closest hit over
+// the whole domain list, shading, any hit of the shadow slots, film --
+// with a single-point-light PT bounce as ONE fused launch (closest hit +
+// shading + the shadow rays' any hit, launch_scene_frame_pt).  Results per
+// sample are the protocol's (the same winner, shading and occlusion); the
+// film adds with the same atomics; the totals come from the shading
+// counters on the device and go through the transport's all-reduce.
+bool all_local(const spray_rt_insitu* I) {
+  const spray_rt_ctx* c = I->ctx;
+  if (I->world == 1) return true;
+  if (int(c->h_owner.size()) != c->ndom) return false;
+  for (int d = 0; d < c->ndom; ++d)
+    if (c->h_owner[d] != I->rank) return false;
+  return true;
+}
+
+int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
+                const int32_t* pixid, const int32_t* samid, size_t n, int spp, float* image,
+                const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  const int ns = spray_rt_shadow_slots(P);
+  const size_t MS = n * size_t(ns);
+  if (MS > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "in-situ batch too large");
+  const double scale = 1.0 / double(spp);
+  GROW(I->dstats, 4 * 8);
+  GROW(I->dtot, 4 * 8);
+  GROW(I->dnum, 2 * 4);
+  GROW(I->ohit, n * 48);
+  GROW(I->owin, n);
+  GROW(I->sray, MS * 32);
+  GROW(I->ssw, MS * 16);
+  GROW(I->ssv, MS);
+  GROW(I->socc, MS);
+  HIPCHK(c, hipMemsetAsync(I->dstats.p, 0, 4 * 8, s));
+  unsigned long long* st = I->dstats.as<unsigned long long>();
+  spray_rt_hit* hits = I->ohit.as<spray_rt_hit>();
+  uint8_t* sv = I->ssv.as<uint8_t>();
+  uint8_t* occ = I->socc.as<uint8_t>();
+  float* sw = I->ssw.as<float>();
+  if (n && fused_pt_shading(c, P)) {
+    const spray_rt_light& lt = P->lights[0];
+    const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
+                               lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
+                               P->ks[2],       P->shininess};
+    uint32_t* nshadow = I->dnum.as<uint32_t>();
+    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, n, hits, shade10, occ, sv, sw, nshadow));
+    HIPCHK(c, launch_frame_stats_add(s, st, 1, n, nshadow));
+    HIPCHK(c, launch_film_atomic(s, image, pixid, n, ns, sw, sv, occ, scale));
+    if (rec) {
+      HIPCHK(c, launch_hit_flags(s, nullptr, hits, n, I->owin.as<uint8_t>()));
+      HIPCHK(c, launch_record(s, I->owin.as<uint8_t>(), n, 0, ns, samid, hits, sv, occ, *rec));
+    }
+  } else if (n) {
+    GROW(I->oray, n * 32);
+    GROW(I->ow, n * 16);
+    GROW(I->ovalid, n);
+    spray_rt_ray* r = I->oray.as<spray_rt_ray>();
+    uint8_t* valid = I->ovalid.as<uint8_t>();
+    float* w = I->ow.as<float>();
+    HIPCHK(c, hipMemcpyAsync(r, rays, n * 32, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, launch_path_init(s, w, valid, n));
+    const int user = c->coherence;
+    for (int b = 0; b < P->bounces; ++b) {
+      if (b == 0) {  // camera rays: coherent packets
+        c->coherence = SPRAY_RT_RAYS_COHERENT;
+        const hipError_t e = launch_scene_intersect(s, view(c), r, n, hits, nullptr);
+        c->coherence = user;
+        HIPCHK(c, e);
+      } else {
+        CALL(spray_rt_intersect_scene_masked(c, r, n, valid, hits));
+      }
+      // the samples this bounce shades (live slots that hit), before the
+      // shading pass turns the slots into the next bounce's rays
+      HIPCHK(c, launch_hit_flags(s, valid, hits, n, I->owin.as<uint8_t>()));
+      HIPCHK(c, launch_shade(s, *P, c->d_bsdf, c->nbsdf, b, ns, r, hits, w, valid, pixid, samid,
+                             n, I->sray.as<spray_rt_ray>(), sw, sv, st, 1));
+      if (ns) {
+        CALL(spray_rt_occluded_scene_masked(c, I->sray.as<spray_rt_ray>(), MS, sv, occ));
+        HIPCHK(c, launch_film_atomic(s, image, pixid, n, ns, sw, sv, occ, scale));
+      }
+      if (rec)
+        HIPCHK(c, launch_record(s, I->owin.as<uint8_t>(), n, b, ns, samid, hits, sv, occ, *rec));
+    }
+  }
+  // the group's totals: radiance rays = live slots shaded, shadows, aborts
+  unsigned long long* dt = I->dtot.as<unsigned long long>();
+  HIPCHK(c, hipMemcpyAsync(dt, st + 3, 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(dt + 1, st + 1, 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(dt + 2, st, 8, hipMemcpyDeviceToDevice, s));
+  CALL(I->tr->allreduce_u64(I, dt, 3));
+  unsigned long long* ht = I->h_small + 200;
+  HIPCHK(c, hipMemcpyAsync(ht, dt, 3 * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (totals)
+    for (int k = 0; k < 3; ++k) totals[k] = ht[k];
+  ++I->st[5];
+  if (ht[2])
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED, "%llu shading cases the reference aborts on", ht[2]);
+  return SPRAY_RT_OK;
+}
+
 void free_all(spray_rt_insitu* I) {
   DBuf* all[] = {&I->hray[0], &I->hray[1], &I->hw[0], &I->hw[1], &I->hpix[0], &I->hpix[1],
                  &I->hsam[0], &I->hsam[1], &I->mask, &I->idx, &I->starts, &I->plan_tmp,
@@ -710,6 +816,13 @@ int spray_rt_insitu_trace(spray_rt_insitu_t I, const spray_rt_shader* P, const s
   int r = scene_common(c, image, 1, image);
   if (r) return r;
   if (!c->d_owner) return fail(c, SPRAY_RT_ERR_STATE, "no owner map set");
+  // every domain local: the frame needs no exchange (trace_local).  The full
+  // protocol stays selectable (SPRAY_INSITU_LOCAL=0) and is what a test of
+  // the self exchange through RCCL (SPRAY_INSITU_NCCL_SELF=1) runs.
+  const char* lo = std::getenv("SPRAY_INSITU_LOCAL");
+  const bool local_ok = !(lo && lo[0] == '0') && I->tr->self_direct();
+  if (local_ok && all_local(I)) return trace_local(I, P, rays, pixid, samid, n, spp, image, rec,
+                                                   totals);
   return trace(I, P, rays, pixid, samid, n, spp, image, rec, totals);
 }
 

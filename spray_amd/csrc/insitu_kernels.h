@@ -57,6 +57,9 @@ hipError_t launch_gather_next(hipStream_t s, const spray_rt_ray* rays, const flo
                               size_t n, spray_rt_ray* orays, float* ow, int32_t* opix,
                               int32_t* osam);
 hipError_t launch_weights_one(hipStream_t s, float* w, size_t n);
+// win[i] = (valid == null || valid[i]) && hits[i] is a hit
+hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_hit* hits,
+                            size_t n, uint8_t* win);
 // counts[r] = starts[r + 1] - starts[r], r < world (<= 64)
 hipError_t launch_counts_from_starts(hipStream_t s, const int64_t* starts, int world,
                                      int64_t* counts);

@@ -240,6 +240,15 @@ __global__ __launch_bounds__(kBlock) void k_record(const uint8_t* __restrict__ w
   rec.occluded[k] = o;
 }
 
+// the samples a bounce of the all-local path shades: live slots that hit
+__global__ __launch_bounds__(kBlock) void k_hit_flags(const uint8_t* __restrict__ valid,
+                                                      const spray_rt_hit* __restrict__ hits,
+                                                      size_t n, uint8_t* __restrict__ win) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  win[i] = ((!valid || valid[i]) && hits[i].domain >= 0) ? 1 : 0;
+}
+
 // the next bounce's holder arrays: rays / weights / pixel / sample of the
 // copies sel[0..n) that spawned a radiance ray
 __global__ __launch_bounds__(kBlock) void k_gather_next(const float4* __restrict__ rays,
@@ -348,6 +357,10 @@ hipError_t launch_gather_next(hipStream_t s, const spray_rt_ray* rays, const flo
   LAUNCH(n, k_gather_next, reinterpret_cast<const float4*>(rays),
          reinterpret_cast<const float4*>(w), pix, sam, sel, n, reinterpret_cast<float4*>(orays),
          reinterpret_cast<float4*>(ow), opix, osam);
+}
+hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_hit* hits,
+                            size_t n, uint8_t* win) {
+  LAUNCH(n, k_hit_flags, valid, hits, n, win);
 }
 hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);

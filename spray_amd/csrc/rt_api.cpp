@@ -490,6 +490,7 @@ int spray_rt_domain_bounds(spray_rt_ctx_t c, int ndomains, const float* boxes) {
   c->d_dom2slot = nullptr;
   c->d_domtrav = nullptr;
   c->d_owner = nullptr;
+  c->h_owner.clear();
   c->d_tlas = nullptr;
   c->ntlas = 0;
   c->tlas_depth = 0;
@@ -994,6 +995,7 @@ int spray_rt_set_owners(spray_rt_ctx_t c, const int* owner) {
   hipStream_t s = stream_of(c);
   HIPCHK(c, hipMemcpyAsync(c->d_owner, owner, c->ndom * sizeof(int), hipMemcpyHostToDevice, s));
   HIPCHK(c, hipStreamSynchronize(s));
+  c->h_owner.assign(owner, owner + c->ndom);
   return SPRAY_RT_OK;
 }
 

@@ -53,6 +53,7 @@ struct spray_rt_ctx {
   int* d_dom2slot = nullptr;
   DomTrav* d_domtrav = nullptr;  // per-domain traversal descriptors
   int* d_owner = nullptr;        // in-situ domain -> rank map
+  std::vector<int> h_owner;      // the same map on the host
   BvhNode* d_tlas = nullptr;  // top-level tree over the domain boxes
   int ntlas = 0;
   int tlas_depth = 0;
@@ -135,6 +136,10 @@ int ensure(spray_rt_ctx* c, void** buf, size_t* cap, size_t bytes);
 int scene_common(spray_rt_ctx* c, const void* rays, size_t M, const void* out);
 // the kernels' view of the resident scene (coherence = the context's)
 SceneView view(const spray_rt_ctx* c);
+// the whole shading of a bounce is the point-light term of camera rays (PT,
+// one point light, diffuse surfaces, bounces = 1): it fuses into the
+// closest-hit launch (launch_scene_frame_pt)
+bool fused_pt_shading(const spray_rt_ctx* c, const spray_rt_shader* P);
 
 }  // namespace detail
 }  // namespace spray_rt

@@ -301,6 +301,14 @@ __device__ __host__ __forceinline__ size_t band_size(size_t M) {
   return (((M + kQueues - 1) / kQueues) + 63) / 64 * 64;
 }
 
+// LDS written by some lanes of a wave and read by others: ordered within
+// the wave (no block barrier)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // AO ray k of a fused spawn + any hit: sample l of source ray i, (i, l) =
 // (ao_pairs[k] >> 5, ao_pairs[k] & 31) -- the rotation of
 // k_spawn_ao_write_hits on the same values: the hit's origin, normal and
@@ -502,6 +510,234 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
       }
     }
   }
+}
+
+// Per-lane any hit as one wave-collective loop, with the leaf triangles of
+// all lanes spread over the wave.  Each lane walks its own ray through the
+// 4-wide quantized trees of its domains (occluded_tree_q4's step: nearest
+// entered child next, the others pushed, a first leaf parked while the lane
+// keeps descending), but the lanes never leave the loop on their own: a
+// lane whose walk of a domain ends picks its next domain at the top of the
+// loop (no per-domain wave barrier), and when every stepping lane holds a
+// leaf, the parked leaves -- plus a second leaf a walk stopped on -- become
+// (lane, triangle) tasks dealt out to all 64 lanes (ballot prefix of the
+// counts, owner lane per task in LDS, the owner's ray and triangle array by
+// cross-lane reads).  A lane with per-lane leaf tests idles while the lane
+// with the most triangles tests them: scripts/walk_sim.py measures the
+// triangle iterations per 64 AO-16 rays 24.4 -> 9.7 (lane use 0.28 ->
+// 0.80).  Every triangle of the parked leaves is tested (no early exit
+// inside one phase); occlusion is an OR, so the bits are the per-lane
+// walk's.  wtask: 8 * 64 owner bytes of the wave, whit: 64 hit bytes.
+#ifndef SPRAY_AH_SPREAD
+#define SPRAY_AH_SPREAD 0
+#endif
+template <int W, int STK, int EPI>
+__device__ __forceinline__ void scene_ray_ah_wave(const SceneArgs& A, size_t i, bool valid,
+                                                  const float4* stl, const float* sbox,
+                                                  const float4* sdom, int32_t* stk,
+                                                  int32_t* wstk, uint8_t* wtask, uint8_t* whit) {
+  const uint32_t lane = threadIdx.x & 63;
+  v4f a = v4f{0.f, 0.f, 0.f, kRayEpsilon}, b = v4f{0.f, 0.f, 1.f, kInf};
+  if (valid) {
+    if (EPI == kEpiAoGen) {
+      ao_gen(A, i, a, b);
+    } else {
+      const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
+      a = __builtin_nontemporal_load(rp);
+      b = __builtin_nontemporal_load(rp + 1);
+    }
+  }
+  const float4 o4 = make_float4(a.x, a.y, a.z, a.w), d4 = make_float4(b.x, b.y, b.z, b.w);
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  const float tnear = o4.w, tfar = d4.w;
+  uint64_t m[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
+  bool alive = valid, occluded = false;
+  // the lane's current domain walk
+  QRay qr{};
+  const char* nbytes = nullptr;
+  uint64_t tris_u = 0;
+  int32_t cur = kNone, leaf = kNone;
+  constexpr int kOvf = kQ4Stack > STK ? kQ4Stack - STK : 1;
+  int32_t ovf[kOvf];
+  int sp = 0;
+  auto push = [&](int32_t v) {
+    if (STK >= kQ4Stack || sp < STK)
+      stk[sp * kBlock] = v;
+    else
+      ovf[sp - STK] = v;
+    ++sp;
+  };
+  auto pop = [&]() -> int32_t {
+    if (sp == 0) return kNone;
+    --sp;
+    return (STK >= kQ4Stack || sp < STK) ? stk[sp * kBlock] : ovf[sp - STK];
+  };
+  for (;;) {
+    // lanes between walks: the nearest remaining domain of the list (the
+    // reference's intersectAabb entry t; the order only steers early exit)
+    if (alive && cur == kNone && leaf == kNone) {
+      float dx = r.dx, dy = r.dy, dz = r.dz;
+      asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+      const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
+      for (;;) {
+        bool any_left = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) any_left |= m[w] != 0;
+        if (!any_left) {
+          alive = false;
+          break;
+        }
+        float st = kInf;
+        int sb = -1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          uint64_t bits = m[w];
+          while (bits) {
+            const int j = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            const int bx = 64 * w + j;
+            float tm;
+            aabb_ref(sbox + 6 * bx, dr, tm);
+            if (sb < 0 || tm < st) {
+              st = tm;
+              sb = bx;
+            }
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
+        const float4 dt = sdom[sb];
+        nbytes = reinterpret_cast<const char*>(
+            (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
+        if (!nbytes) continue;  // not resident here (or empty)
+        tris_u = uint64_t(nbytes) + __float_as_uint(dt.z);
+        const float4 base = ld4(nbytes - sizeof(QGrid), 0);
+        const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
+        // make_ray's inverse, recomputed (same bits) rather than held live
+        // through the walk: the registers go to the 8-waves-per-SIMD budget
+        const float ix = 1.0f / clamp_dir(dx), iy = 1.0f / clamp_dir(dy),
+                    iz = 1.0f / clamp_dir(dz);
+        q_axis(base.x, scale.x, ix, r.ox * ix, qr.ix, qr.olx, qr.ohx);
+        q_axis(base.y, scale.y, iy, r.oy * iy, qr.iy, qr.oly, qr.ohy);
+        q_axis(base.z, scale.z, iz, r.oz * iz, qr.iz, qr.olz, qr.ohz);
+        cur = 0;
+        sp = 0;
+        break;
+      }
+    }
+    if (!__ballot(alive)) break;
+    // node steps until every stepping lane holds a leaf
+    for (;;) {
+      const bool step = alive && cur >= 0 && cur != kNone;
+      if (!__ballot(step)) break;
+      if (step) {
+        const char* qp = nbytes - 128 - 64 * size_t(cur);
+        const float4 qa = ld4(qp, 0), qb = ld4(qp, 1), qc = ld4(qp, 2), qd = ld4(qp, 3);
+        const int32_t ref[4] = {__float_as_int(qd.x), __float_as_int(qd.y), __float_as_int(qd.z),
+                                __float_as_int(qd.w)};
+        float t[4];
+        bool h[4];
+        h[0] = slab_q(qr, q_lo(qa.x), q_hi(qa.x), q_lo(qa.y), q_hi(qa.y), q_lo(qa.z), q_hi(qa.z),
+                      tnear, tfar, t[0]);
+        h[1] = slab_q(qr, q_lo(qa.w), q_hi(qa.w), q_lo(qb.x), q_hi(qb.x), q_lo(qb.y), q_hi(qb.y),
+                      tnear, tfar, t[1]);
+        h[2] = slab_q(qr, q_lo(qb.z), q_hi(qb.z), q_lo(qb.w), q_hi(qb.w), q_lo(qc.x), q_hi(qc.x),
+                      tnear, tfar, t[2]);
+        h[3] = slab_q(qr, q_lo(qc.y), q_hi(qc.y), q_lo(qc.z), q_hi(qc.z), q_lo(qc.w), q_hi(qc.w),
+                      tnear, tfar, t[3]);
+        int32_t next = kNone;
+        float tn = kInf;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!h[k] || ref[k] == kNoChildRef) continue;
+          if (next == kNone || t[k] < tn) {
+            if (next != kNone) push(next);
+            next = ref[k];
+            tn = t[k];
+          } else {
+            push(ref[k]);
+          }
+        }
+        cur = next != kNone ? next : pop();
+        if (cur < 0 && cur != kNone && leaf == kNone) {  // park the leaf, keep descending
+          leaf = cur;
+          cur = pop();
+        }
+      }
+      if (__ballot(step && leaf == kNone) == 0) break;
+    }
+    // the parked leaf and a second leaf the walk stopped on, as tasks
+    uint32_t f0 = 0, c0 = 0, f1 = 0, c1 = 0;
+    if (alive && leaf != kNone) {
+      const uint32_t e0 = ~uint32_t(leaf);
+      f0 = e0 >> 2;
+      c0 = (e0 & 3u) + 1u;
+      leaf = kNone;
+      if (cur < 0 && cur != kNone) {
+        const uint32_t e1 = ~uint32_t(cur);
+        f1 = e1 >> 2;
+        c1 = (e1 & 3u) + 1u;
+        cur = pop();
+      }
+    }
+    const uint32_t nt = c0 + c1;  // 0..8: four bits
+    uint32_t off = 0, T = 0;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const uint64_t bm = __ballot((nt >> bit) & 1u);
+      off += uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32),
+                                                __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)))
+             << bit;
+      T += uint32_t(__popcll(bm)) << bit;
+    }
+    if (T) {
+      for (uint32_t j = 0; j < nt; ++j) wtask[off + j] = uint8_t(lane);
+      whit[lane] = 0;
+      wave_lds_sync();
+      for (uint32_t base = 0; base < T; base += 64) {
+        const uint32_t t = base + lane;
+        const bool ok = t < T;
+        const int ow = ok ? int(wtask[t]) : int(lane);
+        const uint32_t j = t - uint32_t(__shfl(int(off), ow));
+        const uint32_t of0 = uint32_t(__shfl(int(f0), ow)), oc0 = uint32_t(__shfl(int(c0), ow)),
+                       of1 = uint32_t(__shfl(int(f1), ow));
+        const uint64_t otris = (uint64_t(uint32_t(__shfl(int(uint32_t(tris_u >> 32)), ow))) << 32) |
+                               uint32_t(__shfl(int(uint32_t(tris_u)), ow));
+        Ray ro;
+        ro.ox = __shfl(r.ox, ow);
+        ro.oy = __shfl(r.oy, ow);
+        ro.oz = __shfl(r.oz, ow);
+        ro.dx = __shfl(r.dx, ow);
+        ro.dy = __shfl(r.dy, ow);
+        ro.dz = __shfl(r.dz, ow);
+        const float otn = EPI == kEpiAoGen ? kRayEpsilon : __shfl(tnear, ow);
+        const float otf = EPI == kEpiAoGen ? kInf : __shfl(tfar, ow);
+        if (ok) {
+          const uint32_t p = j < oc0 ? of0 + j : of1 + (j - oc0);
+          float4 ta, tb, tc;
+          ld_tri(reinterpret_cast<const void*>(otris), p, ta, tb, tc);
+          float th, tu, tv;
+          if (tri_test(ro, otn, ta, tb, tc, th, tu, tv) && th <= otf) whit[ow] = 1;
+        }
+      }
+      wave_lds_sync();
+      if (alive && whit[lane]) {
+        occluded = true;
+        alive = false;
+      }
+      wave_lds_sync();  // the next phase rewrites wtask / whit
+    }
+    // a popped entry that is a leaf is parked for the next phase
+    if (alive && cur < 0 && cur != kNone) {
+      leaf = cur;
+      cur = pop();
+    }
+  }
+  if (valid) A.occ[i] = occluded ? 1 : 0;
 }
 
 // A wave's rays are coherent when every direction is within ~8 degrees of
@@ -825,12 +1061,6 @@ struct ShadowQueue {
   uint32_t n;     // waiting (wave-uniform)
 };
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <int W>
 __device__ __forceinline__ void shadow_trace(const SceneArgs& A, const ShadowQueue& q,
                                              uint32_t cnt, const float4* stl, const float* sbox,
@@ -915,7 +1145,15 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
                          SPRAY_AH_WW && SPRAY_AOGEN_LSTK < STK)
                             ? SPRAY_AOGEN_LSTK
                             : STK;
+  // the per-lane any hit as one wave-collective loop with the leaf
+  // triangles spread over the wave (scene_ray_ah_wave)
+  constexpr bool kSpread = ANY && !COUNT && kLaneStack && SPRAY_AH_SPREAD && SPRAY_AH_QNODES &&
+                           SPRAY_AH_WW && (EPI == kEpiNone || EPI == kEpiAoGen);
   __shared__ int32_t stack[(kLaneStack ? kLStk : 1) * kBlock];
+  __shared__ uint8_t wtask[kSpread ? (kBlock / 64) * 512 : 1];
+  __shared__ uint8_t whit[kSpread ? kBlock : 1];
+  uint8_t* my_task = wtask + (kSpread ? (threadIdx.x >> 6) * 512 : 0);
+  uint8_t* my_hit = whit + (kSpread ? (threadIdx.x & ~63u) : 0);
   __shared__ float4 stl[4 * 64 * W];   // top-level tree
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
@@ -953,6 +1191,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     const bool ok = j < M && i < A.M && (!A.valid || A.valid[i]);
     if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+    else if (kSpread)
+      scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task, my_hit);
     else if (ok)
       scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
@@ -987,6 +1227,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           flag = false;
           if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+          else if (kSpread)
+            scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task,
+                                             my_hit);
           else if (ok)
             scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);

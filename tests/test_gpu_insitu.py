@@ -179,6 +179,27 @@ def test_engine_one_rank_host(oracle):
     _check(oracle, "pt1", [_engine_rank(0, 1, "pt1", "host")])
 
 
+@pytest.mark.parametrize("case", ["pt1", "ao16", "pt3"])
+def test_engine_one_rank_all_local(oracle, case):
+    """One rank owns every domain: the frame takes the exchange-free path
+    (insitu.cpp trace_local: the fused closest hit + shading + shadow any
+    hit for a point-light PT bounce, the device frame layer's passes
+    otherwise) -- the same records, totals and image as the protocol, and no
+    exchange at all."""
+    res = _engine_rank(0, 1, case, "rccl")
+    _check(oracle, case, [res])
+    st = res[3]
+    assert st["exchanges"] == 0 and st["host_count_reads"] == 0 and st["traces"] == 2
+
+
+def test_engine_one_rank_protocol_forced(oracle, monkeypatch):
+    """SPRAY_INSITU_LOCAL=0 keeps the whole protocol at one rank."""
+    monkeypatch.setenv("SPRAY_INSITU_LOCAL", "0")
+    res = _engine_rank(0, 1, "pt1", "rccl")
+    _check(oracle, "pt1", [res])
+    assert res[3]["exchanges"] > 0
+
+
 def _gpu_rank_main(rank, world, port, out, case):
     import pickle
     import sys
