@@ -159,6 +159,60 @@ def run_packet(L, s, boxes, org, d, any_, label, packets=(64, 128)):
                  tot[1] / n, tot[2] / nw, tot[3] / (2.0 * pk * tot[0])))
 
 
+def morton3(x, y, z, bits=10):
+    """interleaved bits of three coordinates in [0, 1)"""
+    out = np.zeros(len(x), np.uint64)
+    q = [np.clip((c * (1 << bits)).astype(np.int64), 0, (1 << bits) - 1).astype(np.uint64)
+         for c in (x, y, z)]
+    for b in range(bits):
+        for k in range(3):
+            out |= ((q[k] >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b + k)
+    return out
+
+
+def run_ooc_queues(L, s, boxes, org, d, any_, label):
+    """The out-of-core drains' waves: 64 consecutive entries of ONE domain's
+    queue walk that domain as a packet -- queues in ascending ray order (the
+    shipped scatter) against queues sorted by the Morton code of the ray's
+    entry point into the domain box."""
+    ids, cnt = lists(org, d, boxes)
+    n = len(org)
+    rows = np.repeat(np.arange(n), cnt)
+    k = np.arange(len(rows)) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    dom = ids[rows, k]
+    for sort in ("ascending", "entry-morton"):
+        if sort == "ascending":
+            o = np.lexsort((rows, dom))
+        else:
+            lo, hi = boxes[dom, :3], boxes[dom, 3:]
+            inv = 1.0 / np.where(np.abs(d[rows]) < 1e-20, 1e-20, d[rows])
+            t0 = np.maximum(np.max(np.minimum((lo - org[rows]) * inv, (hi - org[rows]) * inv), 1),
+                            0.0)
+            pt = org[rows] + t0[:, None] * d[rows]
+            u = np.clip((pt - lo) / (hi - lo), 0, 0.999)
+            key = morton3(u[:, 0], u[:, 1], u[:, 2])
+            o = np.lexsort((rows, key, dom))
+        r, dd = rows[o], dom[o]
+        po = np.ascontiguousarray(org[r])
+        pd = np.ascontiguousarray(d[r])
+        pid = np.full((len(r), MAXH), -1, np.int32)
+        pid[:, 0] = dd
+        pc = np.ones(len(r), np.int32)
+        # waves never straddle two queues: pad each queue to a multiple of 64
+        starts = np.flatnonzero(np.r_[True, dd[1:] != dd[:-1]])
+        lens = np.diff(np.r_[starts, len(dd)])
+        tot_nodes = tot_waves = 0
+        for a, ln in zip(starts, lens):
+            nw = (ln + 63) // 64
+            out = np.zeros((nw, 5), np.int64)
+            L.ws_packet(s, int(any_), p(po[a:a + ln]), p(pd[a:a + ln]), int(ln),
+                        p(np.ascontiguousarray(pid[a:a + ln])), p(pc[a:a + ln]), MAXH, 64, p(out))
+            tot_nodes += out[:, 0].sum()
+            tot_waves += nw
+        print("%s OOC queue waves (%s): %d pairs, %d waves, node fetches %.1f/wave (%.2f/pair)"
+              % (label, sort, len(r), tot_waves, tot_nodes / tot_waves, tot_nodes / len(r)))
+
+
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     tiles = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [3]
@@ -177,6 +231,12 @@ def main():
                                               SHADE[9])
             run_packet(L, s, boxes, np.ascontiguousarray(so), np.ascontiguousarray(sd), True,
                        "shadow AH")
+        if what in ("ooc", "all"):
+            so, sd, src = po.spawn_shadows_pt(org, d, hits, SHADE[0:3], SHADE[3:6], SHADE[6:9],
+                                              SHADE[9])
+            run_ooc_queues(L, s, boxes, np.ascontiguousarray(so), np.ascontiguousarray(sd), True,
+                           "shadow AH")
+            run_ooc_queues(L, s, boxes, org, d, False, "primary CH")
         if what in ("ao", "all"):
             run_ao(L, s, boxes, org, d, hits, pix)
         if what in ("ao2", "all"):

@@ -98,7 +98,9 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   const size_t b_dom = align256(257 * sizeof(uint32_t));
   const size_t b_score = align256(256 * sizeof(unsigned long long));
   const size_t b_ch = align256(nchk * sizeof(uint32_t));
-  const size_t total = b_masks + 2 * b_v + b_pk + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score;
+  const size_t b_dsh = align256(256 * kOocDeadShards * sizeof(uint32_t));
+  const size_t total =
+      b_masks + 2 * b_v + b_pk + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score + b_dsh;
   HIPCHK(c, hipMalloc(&o->q_mem, total));
   char* p = static_cast<char*>(o->q_mem);
   auto take = [&](size_t n) {
@@ -118,6 +120,7 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   o->q.csum = reinterpret_cast<uint32_t*>(take(b_ch));
   o->q.cw = reinterpret_cast<uint32_t*>(take(b_ch));
   o->q.score = reinterpret_cast<unsigned long long*>(take(b_score));
+  o->q.dshard = reinterpret_cast<uint32_t*>(take(b_dsh));
   o->q.block_cap = nblk;
   o->q.chunk_cap = nchk;
   o->q.pair_cap = pairs;

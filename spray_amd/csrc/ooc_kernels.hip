@@ -443,25 +443,47 @@ __device__ __forceinline__ void wave_add_deaths(const uint64_t* dm, uint32_t* de
   }
 }
 
+// A block's deaths go to one of kOocDeadShards counters per domain (by block
+// index): a launch's blocks end at nearly the same time, and same-address
+// atomics serialise in L2 -- one counter per domain, and one "last block"
+// counter per launch, queued thousands of atomics behind each other.
 template <int W>
-__device__ __forceinline__ void flush_deaths(const uint32_t* dead, uint32_t* live) {
+__device__ __forceinline__ void flush_deaths(const uint32_t* dead, uint32_t* dshard) {
   __syncthreads();
+  const uint32_t sh = blockIdx.x % kOocDeadShards;
   for (int k = threadIdx.x; k < 64 * W; k += kBlock)
-    if (dead[k]) atomicSub(live + k, dead[k]);
+    if (dead[k]) atomicAdd(dshard + size_t(k) * kOocDeadShards + sh, dead[k]);
 }
 
-// The live counts to the host (OocSnapshot): values, then the sequence
-// number with system-scope release.  One block; every live atomic of the
-// launch is complete.
-__device__ __forceinline__ void write_snapshot(const uint32_t* live, const OocSnapshot& S,
-                                               int ndom) {
+// The live counts to the host (OocSnapshot): the launch's deaths summed out
+// of their shards (which are cleared) and taken off live, the values, then
+// the sequence number with system-scope release.  One block, after every
+// drain block of the launch (a kernel boundary).
+__device__ __forceinline__ void write_snapshot(uint32_t* live, uint32_t* dshard,
+                                               const OocSnapshot& S, int ndom) {
   const unsigned long long g = (unsigned long long)S.gen << 32;
-  for (int k = threadIdx.x; k < ndom; k += blockDim.x)
-    S.snap[k] = g | __hip_atomic_load(live + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = threadIdx.x; k < ndom; k += blockDim.x) {
+    uint32_t* d = dshard + size_t(k) * kOocDeadShards;
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t j = 0; j < kOocDeadShards; ++j) {
+      sum += d[j];
+      d[j] = 0;
+    }
+    const uint32_t v = live[k] - sum;
+    live[k] = v;
+    S.snap[k] = g | v;
+  }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0)
     __hip_atomic_store(S.seq, g | (S.launch + 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void k_ooc_snapshot(uint32_t* __restrict__ live,
+                                                      uint32_t* __restrict__ dshard,
+                                                      OocSnapshot S, int ndom) {
+  write_snapshot(live, dshard, S, ndom);
 }
 
 // Closest hit of the rays queued to up to kOocBatch resident domains in one
@@ -529,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
     uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf,
-    uint32_t* __restrict__ live) {
+    uint32_t* __restrict__ dshard) {
   if (blockIdx.x >= B.copy0) {
     prefetch_copy(B);
     return;
@@ -544,7 +566,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
   if (s >= 0)
     ch_pair<W>(B.d[s], pj, valid, rays, idx, masks, boxes, key, pkey, pleaf,
                wstack + (threadIdx.x >> 6) * kStack, dead);
-  flush_deaths<W>(dead, live);
+  flush_deaths<W>(dead, dshard);
 }
 
 // Hit records of the batch's winners: the one pair whose key equals its
@@ -555,8 +577,8 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ key, const uint64_t* __restrict__ pkey,
     const uint32_t* __restrict__ pleaf, spray_rt_hit* __restrict__ hits,
-    const uint32_t* __restrict__ live, OocSnapshot S, int ndom) {
-  if (blockIdx.x == 0) write_snapshot(live, S, ndom);
+    uint32_t* __restrict__ live, uint32_t* __restrict__ dshard, OocSnapshot S, int ndom) {
+  if (blockIdx.x == 0) write_snapshot(live, dshard, S, ndom);
   uint32_t pj;
   bool valid;
   const int s = batch_pair(B, pj, valid);
@@ -667,18 +689,16 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
   wave_add_deaths<W>(dm, dead);
 }
 
-// The last block to finish (done counter) publishes the live counts and
-// rearms the counter for the next launch.
+// k_ooc_snapshot (one block) follows and publishes the live counts.
 template <int W, int MODE>
 __global__ __launch_bounds__(kBlock, SPRAY_OOC_AH_WAVES) void k_ooc_ah_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, uint8_t* __restrict__ occ,
-    uint32_t* __restrict__ live, uint32_t* __restrict__ done, OocSnapshot S, int ndom) {
+    uint32_t* __restrict__ dshard) {
   // per lane: lane-interleaved stacks; packet: one stack per wave
   __shared__ int32_t stack[MODE != 1 ? kStack * kBlock : 1];
   __shared__ int32_t wstack[MODE != 0 ? kWaves * kStack : 1];
   __shared__ uint32_t dead[64 * W];
-  __shared__ bool last;
   for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
   __syncthreads();
   uint32_t pj;
@@ -688,15 +708,7 @@ __global__ __launch_bounds__(kBlock, SPRAY_OOC_AH_WAVES) void k_ooc_ah_batch(
   if (s >= 0)
     ah_pair<W, MODE>(B.d[s], pj, ok, rays, idx, masks, occ, stack + (MODE != 1 ? threadIdx.x : 0),
                      wstack + (MODE != 0 ? (threadIdx.x >> 6) * kStack : 0), dead);
-  flush_deaths<W>(dead, live);
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  write_snapshot(live, S, ndom);
-  if (threadIdx.x == 0) *done = 0;
+  flush_deaths<W>(dead, dshard);
 }
 
 }  // namespace
@@ -721,6 +733,9 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   k_ooc_chunk_sums<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.sb, g, ndom, q.csum, q.cw);
   k_ooc_chunk_scan<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.csum, g, ndom, q.off);
   k_ooc_first<<<1, 256, 0, s>>>(q.csum, q.cw, int(nch), ndom, q.first, q.live, q.score);
+  if (hipMemsetAsync(q.dshard, 0, size_t(ndom) * kOocDeadShards * sizeof(uint32_t), s) !=
+      hipSuccess)
+    return hipGetLastError();
   if (W == 1)
     k_ooc_scatter<1><<<g, kBlock, 0, s>>>(q.masks, M, q.first, q.off, q.val, q.pair_cap);
   else
@@ -766,15 +781,15 @@ hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
   if (gc) {
     if (W == 1)
       k_ooc_ch_batch<1><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
-                                              q.pleaf, q.live);
+                                              q.pleaf, q.dshard);
     else
       k_ooc_ch_batch<4><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
-                                              q.pleaf, q.live);
+                                              q.pleaf, q.dshard);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, q.val, key, q.pkey, q.pleaf, hits, q.live,
-                                        snap, ndom);
+                                        q.dshard, snap, ndom);
   return hipGetLastError();
 }
 
@@ -789,12 +804,11 @@ hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
                                OocSnapshot snap, int coherence) {
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
   const int ndom = 64 * W;
+  (void)done;
   unsigned g = batch_grid(B);
   g += B.pf_count ? B.ncopy : 0;
-  if (g == 0) g = 1;  // the last block publishes even when empty
-#define SPRAY_AH_LAUNCH(WW, MM)                                                       \
-  k_ooc_ah_batch<WW, MM><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.live, done, snap, \
-                                              ndom)
+#define SPRAY_AH_LAUNCH(WW, MM) \
+  k_ooc_ah_batch<WW, MM><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.dshard)
   // the context's coherence setting: incoherent -> per lane, else packets
   // (measured on configs[3]'s PT shadows, one box: packets 4.08, per lane
   // 4.60, the per-wave choice 4.72 ms per frame -- the choice's direction
@@ -807,16 +821,21 @@ hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
   const int mode = coherence == SPRAY_RT_RAYS_INCOHERENT                  ? 0
                    : (coherence == SPRAY_RT_RAYS_ADAPTIVE && adaptive) ? 2
                                                                           : 1;
-  if (W == 1) {
-    if (mode == 0) SPRAY_AH_LAUNCH(1, 0);
-    else if (mode == 1) SPRAY_AH_LAUNCH(1, 1);
-    else SPRAY_AH_LAUNCH(1, 2);
-  } else {
-    if (mode == 0) SPRAY_AH_LAUNCH(4, 0);
-    else if (mode == 1) SPRAY_AH_LAUNCH(4, 1);
-    else SPRAY_AH_LAUNCH(4, 2);
+  if (g) {
+    if (W == 1) {
+      if (mode == 0) SPRAY_AH_LAUNCH(1, 0);
+      else if (mode == 1) SPRAY_AH_LAUNCH(1, 1);
+      else SPRAY_AH_LAUNCH(1, 2);
+    } else {
+      if (mode == 0) SPRAY_AH_LAUNCH(4, 0);
+      else if (mode == 1) SPRAY_AH_LAUNCH(4, 1);
+      else SPRAY_AH_LAUNCH(4, 2);
+    }
   }
 #undef SPRAY_AH_LAUNCH
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  k_ooc_snapshot<<<1, 256, 0, s>>>(q.live, q.dshard, snap, ndom);
   return hipGetLastError();
 }
 

@@ -200,6 +200,7 @@ struct OocScratch {
   uint32_t* cw;               // [chunk_cap] DomainStats weight per (domain, chunk)
   unsigned long long* score;  // [256] DomainStats score per domain
   uint32_t* live;             // [256] live pairs per queue (see k_ooc_ch_batch)
+  uint32_t* dshard;           // [256 * kOocDeadShards] deaths since the last snapshot
   uint64_t* pkey;             // [pair_cap] closest-hit key of each (ray, domain) pair
   uint32_t* pleaf;            // [pair_cap] its triangle (leaf order)
   size_t block_cap;           // >= ndom * ray blocks
@@ -233,6 +234,7 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
                              size_t M, OocScratch& q, uint64_t* key_init, uint8_t* occ_clear,
                              uint32_t* h_first, unsigned long long* h_score);
 constexpr uint32_t kOocChunk = 4096;  // ray blocks per chunk of the queue-offset scan
+constexpr uint32_t kOocDeadShards = 64;  // death counters per domain (by drain block)
 // Per-ray closest-hit key of the ooc drains: t bits << 32 | position in the
 // ray's sorted domain list << 16 | domain; a miss is kOocMissKey.
 constexpr uint64_t kOocMissKey = ~0ull;

@@ -1054,7 +1054,15 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
 // the caches -- and the rest is traced when the wave runs out of work.
 // occ[i] / sh_valid[i] are positional by source ray, as the two-launch form
 // (spawn, select, any hit) writes them.
-constexpr uint32_t kShadowQ = 128;  // >= 63 waiting + 64 new
+// capacity; a packet of min(waiting, 64) rays is traced once kShadowT wait
+// (kShadowT - 1 waiting + 64 new fit): 128 / 64 = full packets only;
+// smaller queues trade packet fill for LDS (more resident blocks)
+#ifndef SPRAY_SHADOW_Q
+#define SPRAY_SHADOW_Q 104
+#endif
+constexpr uint32_t kShadowQ = SPRAY_SHADOW_Q;
+constexpr uint32_t kShadowT = kShadowQ - 64;
+static_assert(kShadowQ > 64 && kShadowQ <= 128, "shadow queue capacity in (64, 128]");
 struct ShadowQueue {
   float* ray;     // [kShadowQ][6]: org, dir
   uint32_t* src;  // [kShadowQ]: source ray index
@@ -1096,18 +1104,19 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
     q.src[k] = uint32_t(i);
   }
   q.n += uint32_t(__popcll(bal));
-  if (q.n < 64) return;
+  if (q.n < kShadowT) return;
   wave_lds_sync();
-  shadow_trace<W>(A, q, 64, stl, sbox, sdom, wstk);
+  const uint32_t cnt = q.n < 64 ? q.n : 64u;
+  shadow_trace<W>(A, q, cnt, stl, sbox, sdom, wstk);
   // the remainder (< 64) moves to the front
-  const uint32_t rest = q.n - 64;
+  const uint32_t rest = q.n - cnt;
   const bool mv = lane < rest;
   float e[6];
   uint32_t si = 0;
   if (mv) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) e[k] = q.ray[6 * (64 + lane) + k];
-    si = q.src[64 + lane];
+    for (int k = 0; k < 6; ++k) e[k] = q.ray[6 * (cnt + lane) + k];
+    si = q.src[cnt + lane];
   }
   wave_lds_sync();
   if (mv) {

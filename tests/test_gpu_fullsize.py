@@ -79,6 +79,7 @@ def test_ooc_full_frame_4_slots(spray, oracle, oframe):
     the domains streamed through a 4-slot LRU, compacted PT spawn, any hit of
     the shadow rays -- the whole frame, bit for bit against the oracle."""
     rt, oc = spray.ooc_scene(WAVELETS64, SCENES, 4)
+    rt.set_stream(torch.cuda.current_stream())  # as bench.py: counts read through torch
     rays, _ = device_rays(spray, rt)
     hits = torch.empty(N * 48, dtype=torch.uint8, device="cuda")
     shadow = torch.empty(N * 32, dtype=torch.uint8, device="cuda")
