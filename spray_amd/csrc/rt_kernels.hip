@@ -1029,7 +1029,8 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // sh_valid[i] says whether it exists; one atomic per wave for the total.
 __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
                                              bool flag, size_t i,
-                                             const float* pos, const float* wi) {
+                                             const float* pos, const float* wi,
+                                             uint32_t& wcount) {
   if (active) {
     A.sh_valid[i] = flag ? 1 : 0;
     if (flag) {
@@ -1038,10 +1039,7 @@ __device__ __forceinline__ void store_shadow(const SceneArgs& A, bool active,
       op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
     }
   }
-  if (A.sh_count) {
-    const unsigned long long bal = __ballot(flag);
-    if (bal && (threadIdx.x & 63) == 0) atomicAdd(A.sh_count, uint32_t(__popcll(bal)));
-  }
+  wcount += uint32_t(__popcll(__ballot(flag)));
 }
 
 // The closest-hit register target (SPRAY_WAVES_CH) applies to the 16-entry
@@ -1086,12 +1084,12 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
                                             bool flag, size_t i, const float* pos,
                                             const float* wi, const float4* stl,
                                             const float* sbox, const float4* sdom,
-                                            int32_t* wstk) {
+                                            int32_t* wstk, uint32_t& wcount) {
   const uint32_t lane = threadIdx.x & 63;
   if (active) A.sh_valid[i] = flag ? 1 : 0;
   const unsigned long long bal = __ballot(flag);
   if (!bal) return;
-  if (A.sh_count && lane == 0) atomicAdd(A.sh_count, uint32_t(__popcll(bal)));
+  wcount += uint32_t(__popcll(bal));
   if (flag) {
     const uint32_t k = q.n + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
     float* e = q.ray + 6 * k;
@@ -1190,6 +1188,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   int32_t* wstk = wstack + (threadIdx.x >> 6) * STK;
   bool flag = false;
   float pos[3], wi[3];
+  // spawned shadow rays of the wave, added to *sh_count once at its end (a
+  // same-address atomic per chunk queued ~10^5 atomics behind each other)
+  uint32_t wcount = 0;
   const bool persist = ANY ? (SPRAY_PERSIST_AH != 0 || A.persist != 0) : SPRAY_PERSIST_CH != 0;
   const int lane = threadIdx.x & 63;
   const uint32_t* __restrict__ idx = A.idx;
@@ -1205,8 +1206,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     else if (ok)
       scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
-    if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi);
-    if (kShadow) shadow_push<W>(A, sq, j < M, flag, i, pos, wi, stl, sbox, sdom, wstk);
+    if (EPI == kEpiSpawn) store_shadow(A, j < M, flag, i, pos, wi, wcount);
+    if (kShadow) shadow_push<W>(A, sq, j < M, flag, i, pos, wi, stl, sbox, sdom, wstk, wcount);
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     constexpr uint32_t kPerXcd = kQueues / 8;
@@ -1242,9 +1243,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           else if (ok)
             scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
-          if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi);
+          if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi, wcount);
           if (kShadow)
-            shadow_push<W>(A, sq, j < end, flag, i, pos, wi, stl, sbox, sdom, wstk);
+            shadow_push<W>(A, sq, j < end, flag, i, pos, wi, stl, sbox, sdom, wstk, wcount);
         }
         base = __builtin_amdgcn_readfirstlane(next);
       }
@@ -1254,6 +1255,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     wave_lds_sync();
     shadow_trace<W>(A, sq, sq.n, stl, sbox, sdom, wstk);
   }
+  if ((EPI == kEpiSpawn || kShadow) && A.sh_count && wcount && lane == 0)
+    atomicAdd(A.sh_count, wcount);
   if (COUNT) {
     atomicAdd(&A.counters[0], (unsigned long long)nnode);
     atomicAdd(&A.counters[1], (unsigned long long)ntri);
