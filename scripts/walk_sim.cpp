@@ -317,8 +317,11 @@ void ws_lane_ah(void* sp, const float* org, const float* dir, size_t n, const in
 // refill != 0 -- a lane whose ray is done takes the next ray of the wave's
 // chunk of `chunk` rays (a refill needs the new ray's domain list: counted
 // as refill rounds, the wave iterations in which some lane refilled).
-// out (per wave, 6 counters): node iterations, lane node steps, triangle
-// iterations, lane triangle tests, refill rounds, refills.
+// refill 1: at once, inside the node loop; refill R >= 2: only between
+// phases (after a triangle phase), once at least R lanes are idle.
+// out (per wave, 8 counters): node iterations, lane node steps, triangle
+// iterations (spread), lane triangle tests, refill rounds, refills, triangle
+// iterations with per-lane leaf tests (max per lane per phase), 0.
 void ws_lane_ah2(void* sp, const float* org, const float* dir, size_t n, const int32_t* ids,
                  const int32_t* cnt, int maxhits, int chunk, int refill, long long* out,
                  uint8_t* occ) {
@@ -326,9 +329,10 @@ void ws_lane_ah2(void* sp, const float* org, const float* dir, size_t n, const i
   const size_t nw = (n + size_t(chunk) - 1) / size_t(chunk);
 #pragma omp parallel for schedule(dynamic, 4)
   for (long w = 0; w < long(nw); ++w) {
-    long long c[6] = {0, 0, 0, 0, 0, 0};
+    long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     Lane L[64];
     int ray[64], kk[64];
+    const bool at_once = refill == 1;
     const size_t i0 = size_t(w) * size_t(chunk);
     const size_t i1 = std::min(n, i0 + size_t(chunk));
     size_t next = i0;
@@ -388,7 +392,7 @@ void ws_lane_ah2(void* sp, const float* org, const float* dir, size_t n, const i
           if (!ran[l]) continue;
           node_step(L[l]);
           ++c[1];
-          if (L[l].cur == kNone && L[l].leaf == kNone && domain_done(l) && refill) {
+          if (L[l].cur == kNone && L[l].leaf == kNone && domain_done(l) && at_once) {
             refilled += take_ray(l);
           }
         }
@@ -403,10 +407,11 @@ void ws_lane_ah2(void* sp, const float* org, const float* dir, size_t n, const i
       }
       // triangle phase, spread over the wave
       long long T = 0;
-      int refilled = 0;
+      int refilled = 0, tmax = 0;
       for (int l = 0; l < 64; ++l) {
         Lane& A = L[l];
         if (!A.active || A.leaf == kNone) continue;
+        const long long T0 = T;
         int32_t lv[2] = {A.leaf, kNone};
         A.leaf = kNone;
         if (A.cur < 0 && A.cur != kNone) {
@@ -424,16 +429,24 @@ void ws_lane_ah2(void* sp, const float* org, const float* dir, size_t n, const i
               A.hit = true;
           }
         }
+        tmax = std::max(tmax, int(T - T0));
         if (A.hit) {
           occ[size_t(ray[l])] = 1;
           A.active = false;
-          if (refill) refilled += take_ray(l);
+          if (at_once) refilled += take_ray(l);
         } else if (A.cur < 0 && A.cur != kNone) {
           A.leaf = A.cur;
           A.cur = pop(A);
-        } else if (A.cur == kNone && domain_done(l) && refill) {
+        } else if (A.cur == kNone && domain_done(l) && at_once) {
           refilled += take_ray(l);
         }
+      }
+      if (refill >= 2) {  // between phases, once enough lanes are idle
+        int idle = 0;
+        for (int l = 0; l < 64; ++l) idle += !L[l].active;
+        if (idle >= refill || idle == 64)
+          for (int l = 0; l < 64 && next < i1; ++l)
+            if (!L[l].active) refilled += take_ray(l);
       }
       if (refilled) {
         ++c[4];
@@ -441,11 +454,12 @@ void ws_lane_ah2(void* sp, const float* org, const float* dir, size_t n, const i
       }
       c[2] += (T + 63) / 64;
       c[3] += T;
+      c[6] += tmax;
       bool any = false;
       for (int l = 0; l < 64; ++l) any |= L[l].active;
       if (!any) break;
     }
-    for (int k = 0; k < 6; ++k) out[6 * size_t(w) + k] = c[k];
+    for (int k = 0; k < 8; ++k) out[8 * size_t(w) + k] = c[k];
   }
 }
 

@@ -106,19 +106,21 @@ def ao_rays(org, d, hits, pix, boxes):
 def run_ao2(L, s, boxes, org, d, hits, pix):
     so, sd, ids, cnt = ao_rays(org, d, hits, pix, boxes)
     n = len(so)
-    for chunk, refill in ((64, 0), (256, 1), (1024, 1)):
+    for chunk, refill in ((64, 0), (1024, 0), (1024, 1), (1024, 8), (1024, 16), (1024, 32),
+                          (1024, 48)):
         nw = (n + chunk - 1) // chunk
-        out = np.zeros((nw, 6), np.int64)
+        out = np.zeros((nw, 8), np.int64)
         occ = np.zeros(n, np.uint8)
         t0 = time.time()
         L.ws_lane_ah2(s, p(so), p(sd), n, p(ids), p(cnt), MAXH, chunk, refill, p(out), p(occ))
         tot = out.sum(0)
         w64 = n / 64.0
         print("AO state machine, chunk %d refill %d (%.1f s): occluded %.3f; per 64 rays: node "
-              "iters %.1f (util %.3f), tri iters %.1f (util %.3f), refill rounds %.1f (%.1f rays)"
+              "iters %.1f (util %.3f), tri iters %.1f spread (util %.3f) / %.1f per lane, refill "
+              "rounds %.1f (%.1f rays)"
               % (chunk, refill, time.time() - t0, occ.mean(), tot[0] / w64,
                  tot[1] / (64.0 * tot[0]), tot[2] / w64, tot[3] / (64.0 * max(tot[2], 1)),
-                 tot[4] / w64, tot[5] / w64))
+                 tot[6] / w64, tot[4] / w64, tot[5] / w64))
 
 
 def _run_ao(L, s, boxes, org, d, hits, pix):

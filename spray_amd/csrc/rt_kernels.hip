@@ -81,6 +81,24 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #ifndef SPRAY_DIAG_MODE
 #define SPRAY_DIAG_MODE 0
 #endif
+// AO any hit with lane refill (scene_ray_ah_refill, diagnostic builds): a
+// lane whose ray ended takes the next (source, sample) pair of the wave's
+// band queues once at least SPRAY_AO_REFILL lanes are idle; 0 (shipped) =
+// one chunk of 64 rays per wave at a time (scene_ray).  Measured slower at
+// every threshold ("Lane refill"); SPRAY_CHUNK_AO: pairs per
+// queue dequeue.
+#ifndef SPRAY_AO_REFILL
+#define SPRAY_AO_REFILL 0
+#endif
+#ifndef SPRAY_CHUNK_AO
+#define SPRAY_CHUNK_AO 256
+#endif
+// refill granularity: aligned groups of this many lanes take aligned groups
+// of consecutive pairs (the sample-major trace order puts one pixel's 8
+// near-identical rays of a sample side by side; 1 = single lanes)
+#ifndef SPRAY_AO_REFILL_GROUP
+#define SPRAY_AO_REFILL_GROUP 8
+#endif
 
 // ---------------------------------------------------------------------------
 // Embree-layout streams (RTCRayIntersection / RTCRay, byte stride)
@@ -740,6 +758,278 @@ __device__ __forceinline__ void scene_ray_ah_wave(const SceneArgs& A, size_t i, 
   if (valid) A.occ[i] = occluded ? 1 : 0;
 }
 
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
+
+// Wave-uniform cursor over the persistent launch's band queues: a wave's
+// own XCD's queues first (from the one its block index picks), then the
+// others -- the visit order of k_scene's persistent loop.
+struct BandCursor {
+  uint32_t k;         // next queue of the visit order to dequeue from
+  size_t cur, end;    // the current chunk's undealt pairs [cur, end)
+};
+
+// Dequeues the next chunk of kChunk pairs into bc (uniform control flow:
+// every lane of the wave active).  false once every queue is drained.
+template <uint32_t kChunk>
+__device__ __forceinline__ bool band_next(const SceneArgs& A, size_t M, size_t S, uint32_t xcd,
+                                          uint32_t sub, BandCursor& bc) {
+  constexpr uint32_t kPerXcd = kQueues / 8;
+  const uint32_t lane = threadIdx.x & 63;
+  while (bc.k < uint32_t(kQueues)) {
+    const uint32_t k = bc.k;
+    const uint32_t q = ((xcd + k / kPerXcd) & 7u) * kPerXcd + (sub + k) % kPerXcd;
+    const size_t begin = size_t(q) * S;
+    const size_t end = begin + S < M ? begin + S : M;
+    if (begin < end) {
+      uint32_t* head = &A.heads[32 * q];
+      uint32_t base = 0;
+      if (lane == 0) {
+        base = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (begin + base < end) base = atomicAdd(head, kChunk);
+      }
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (begin + base < end) {
+        bc.cur = begin + base;
+        bc.end = bc.cur + kChunk < end ? bc.cur + kChunk : end;
+        return true;
+      }
+    }
+    ++bc.k;
+  }
+  return false;
+}
+
+// The AO any hit of a persistent wave with lane refill (north-star: re-pack
+// the active lanes under divergent traversal).  Each lane walks its own ray
+// through the 4-wide quantized trees of its domains (occluded_tree_q4's
+// while-while step, as one wave-collective loop: a lane that finishes a
+// domain picks its next one at the top of the loop), and a lane whose ray
+// ended -- occluded, or its domain list exhausted -- writes its byte and
+// goes idle.  Once kMin lanes are idle (or all), the idle lanes take the
+// next pairs of the wave's band queues (ballot + mbcnt rank, one chunk
+// dequeue per kChunk pairs), build their rays (ao_gen) and walk the
+// top-level tree for their domain masks together (tlas_mask_wave over the
+// refilled lanes).  So a wave keeps its lanes busy until the queues drain
+// instead of idling until the slowest ray of each 64.  Every pair is traced
+// by exactly one lane with the per-lane walk's arithmetic: the bits are
+// scene_ray's.  scripts/walk_sim.py (ao2, refill 16, chunk 1024): node-loop
+// iterations per 64 AO-16 rays 21.4 -> 15.6, leaf iterations 22.1 -> 14.4,
+// 1.6 top-level walks instead of 1.
+template <int W, int STK, uint32_t kMin, uint32_t kChunk>
+__device__ __forceinline__ void scene_ray_ah_refill(const SceneArgs& A, size_t M, size_t S,
+                                                    const float4* stl, const float* sbox,
+                                                    const float4* sdom, int32_t* stk,
+                                                    int32_t* wstk) {
+  constexpr uint32_t kPerXcd = kQueues / 8;
+  constexpr uint32_t kGroup = SPRAY_AO_REFILL_GROUP;
+  static_assert(kGroup == 1 || kGroup == 2 || kGroup == 4 || kGroup == 8 || kGroup == 16,
+                "refill groups: a power of two dividing the chunk");
+  static_assert(kChunk % kGroup == 0 && (64 * size_t(kQueues)) % kGroup == 0, "aligned groups");
+  constexpr uint64_t kGroupLead = kGroup == 1 ? ~0ull
+                                  : kGroup == 2 ? 0x5555555555555555ull
+                                  : kGroup == 4 ? 0x1111111111111111ull
+                                  : kGroup == 8 ? 0x0101010101010101ull
+                                                : 0x0001000100010001ull;
+  const uint32_t xcd = xcc_id() & 7u;
+  const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
+  BandCursor bc{0u, 0, 0};
+  bool more = true;  // wave-uniform: pairs may remain in the queues
+  size_t i = 0;      // the lane's pair
+  bool alive = false;
+  Ray r{};
+  uint64_t m[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) m[w] = 0;
+  // the lane's current domain walk
+  QRay qr{};
+  const char* nbytes = nullptr;
+  uint64_t tris_u = 0;
+  int32_t cur = kNone, leaf = kNone;
+  constexpr int kOvf = kQ4Stack > STK ? kQ4Stack - STK : 1;
+  int32_t ovf[kOvf];
+  int sp = 0;
+  auto push = [&](int32_t v) {
+    if (STK >= kQ4Stack || sp < STK)
+      stk[sp * kBlock] = v;
+    else
+      ovf[sp - STK] = v;
+    ++sp;
+  };
+  auto pop = [&]() -> int32_t {
+    if (sp == 0) return kNone;
+    --sp;
+    return (STK >= kQ4Stack || sp < STK) ? stk[sp * kBlock] : ovf[sp - STK];
+  };
+  for (;;) {
+    // ---- refill (uniform): the idle lane groups take the next pairs
+    uint64_t idle = __ballot(!alive);
+    if (kGroup > 1) {  // a group is idle when all its lanes are
+#pragma unroll
+      for (uint32_t sh = 1; sh < kGroup; sh <<= 1) idle &= idle >> sh;
+      idle &= kGroupLead;
+#pragma unroll
+      for (uint32_t sh = 1; sh < kGroup; sh <<= 1) idle |= idle << sh;
+    }
+    const uint32_t nidle = uint32_t(__popcll(idle));
+    if (more && (nidle >= kMin || nidle == 64u)) {
+      const bool mine = (idle >> (threadIdx.x & 63)) & 1ull;
+      // this lane's rank among the idle lanes, in groups
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u));
+      bool fresh = false;
+      uint32_t dealt = 0;
+      while (dealt < nidle) {
+        if (bc.cur == bc.end && !band_next<kChunk>(A, M, S, xcd, sub, bc)) {
+          more = false;
+          break;
+        }
+        const size_t left = bc.end - bc.cur;
+        // whole groups of pairs (chunks start at multiples of kGroup; a
+        // band's ragged end leaves the lanes past it idle)
+        const size_t lg = (left + kGroup - 1) / kGroup * kGroup;
+        const uint32_t take = lg < size_t(nidle - dealt) ? uint32_t(lg) : nidle - dealt;
+        if (mine && rank >= dealt && rank < dealt + take && bc.cur + (rank - dealt) < bc.end) {
+          i = bc.cur + (rank - dealt);
+          fresh = true;
+        }
+        bc.cur = bc.cur + take < bc.end ? bc.cur + take : bc.end;
+        dealt += take;
+      }
+      if (fresh) {
+        v4f a, b;
+        ao_gen(A, i, a, b);
+        r = make_ray(a.x, a.y, a.z, b.x, b.y, b.z);
+        alive = true;
+        cur = leaf = kNone;
+        // AO rays: tnear = kRayEpsilon, tfar = kInf (ao_gen)
+        tlas_mask_wave<W>(stl, A.ntlas, wstk, r, make_float4(a.x, a.y, a.z, a.w),
+                          make_float4(b.x, b.y, b.z, b.w), m);
+      }
+    }
+    // ---- lanes between walks: the nearest remaining domain of the list
+    if (alive && cur == kNone && leaf == kNone) {
+      float dx = r.dx, dy = r.dy, dz = r.dz;
+      asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+      const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
+      for (;;) {
+        bool any_left = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) any_left |= m[w] != 0;
+        if (!any_left) {
+          alive = false;  // domain list exhausted: not occluded
+          A.occ[i] = 0;
+          break;
+        }
+        float st = kInf;
+        int sb = -1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          uint64_t bits = m[w];
+          while (bits) {
+            const int j = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            const int bx = 64 * w + j;
+            float tm;
+            aabb_ref(sbox + 6 * bx, dr, tm);
+            if (sb < 0 || tm < st) {
+              st = tm;
+              sb = bx;
+            }
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
+        const float4 dt = sdom[sb];
+        nbytes = reinterpret_cast<const char*>(
+            (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
+        if (!nbytes) continue;  // not resident here (or empty)
+        tris_u = uint64_t(nbytes) + __float_as_uint(dt.z);
+        const float4 base = ld4(nbytes - sizeof(QGrid), 0);
+        const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
+        const float ix = 1.0f / clamp_dir(dx), iy = 1.0f / clamp_dir(dy),
+                    iz = 1.0f / clamp_dir(dz);
+        q_axis(base.x, scale.x, ix, r.ox * ix, qr.ix, qr.olx, qr.ohx);
+        q_axis(base.y, scale.y, iy, r.oy * iy, qr.iy, qr.oly, qr.ohy);
+        q_axis(base.z, scale.z, iz, r.oz * iz, qr.iz, qr.olz, qr.ohz);
+        cur = 0;
+        sp = 0;
+        break;
+      }
+    }
+    if (!more && !__ballot(alive)) break;
+    // ---- node steps until every stepping lane holds a leaf
+    for (;;) {
+      const bool step = alive && cur >= 0 && cur != kNone;
+      if (!__ballot(step)) break;
+      if (step) {
+        const char* qp = nbytes - 128 - 64 * size_t(cur);
+        const float4 qa = ld4(qp, 0), qb = ld4(qp, 1), qc = ld4(qp, 2), qd = ld4(qp, 3);
+        const int32_t ref[4] = {__float_as_int(qd.x), __float_as_int(qd.y), __float_as_int(qd.z),
+                                __float_as_int(qd.w)};
+        float t[4];
+        bool h[4];
+        h[0] = slab_q(qr, q_lo(qa.x), q_hi(qa.x), q_lo(qa.y), q_hi(qa.y), q_lo(qa.z), q_hi(qa.z),
+                      kRayEpsilon, kInf, t[0]);
+        h[1] = slab_q(qr, q_lo(qa.w), q_hi(qa.w), q_lo(qb.x), q_hi(qb.x), q_lo(qb.y), q_hi(qb.y),
+                      kRayEpsilon, kInf, t[1]);
+        h[2] = slab_q(qr, q_lo(qb.z), q_hi(qb.z), q_lo(qb.w), q_hi(qb.w), q_lo(qc.x), q_hi(qc.x),
+                      kRayEpsilon, kInf, t[2]);
+        h[3] = slab_q(qr, q_lo(qc.y), q_hi(qc.y), q_lo(qc.z), q_hi(qc.z), q_lo(qc.w), q_hi(qc.w),
+                      kRayEpsilon, kInf, t[3]);
+        int32_t next = kNone;
+        float tn = kInf;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!h[k] || ref[k] == kNoChildRef) continue;
+          if (next == kNone || t[k] < tn) {
+            if (next != kNone) push(next);
+            next = ref[k];
+            tn = t[k];
+          } else {
+            push(ref[k]);
+          }
+        }
+        cur = next != kNone ? next : pop();
+        if (cur < 0 && cur != kNone && leaf == kNone) {  // park the leaf, keep descending
+          leaf = cur;
+          cur = pop();
+        }
+      }
+      if (__ballot(step && leaf == kNone) == 0) break;
+    }
+    // ---- leaf tests per lane: the parked leaf, then a leaf the walk stopped on
+    while (alive && leaf != kNone) {
+      const uint32_t enc = ~uint32_t(leaf);
+      const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
+      bool hit = false;
+      for (uint32_t q = 0; q < cnt; ++q) {
+        float4 ta, tb, tc;
+        ld_tri(reinterpret_cast<const void*>(tris_u), first + q, ta, tb, tc);
+        float th, tu, tv;
+        if (tri_test(r, kRayEpsilon, ta, tb, tc, th, tu, tv) && th <= kInf) {
+          hit = true;
+          break;
+        }
+      }
+      if (hit) {
+        alive = false;
+        A.occ[i] = 1;
+        break;
+      }
+      leaf = kNone;
+      if (cur < 0 && cur != kNone) {
+        leaf = cur;
+        cur = pop();
+      }
+    }
+  }
+}
+
 // A wave's rays are coherent when every direction is within ~8 degrees of
 // the first valid lane's (camera rays of neighbouring pixels, shadow rays
 // toward one point light); hemisphere-sampled AO rays are not, and walk
@@ -1010,12 +1300,6 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   }
 }
 
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x;
-}
-
 // Persistent launch: each wave dequeues kChunk-ray chunks from kQueues
 // queues, each owning a contiguous band of the rays.  XCD x's waves start on
 // its eight bands (an eighth of the image: its L2 holds the BVH nodes of that
@@ -1156,6 +1440,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   // triangles spread over the wave (scene_ray_ah_wave)
   constexpr bool kSpread = ANY && !COUNT && kLaneStack && SPRAY_AH_SPREAD && SPRAY_AH_QNODES &&
                            SPRAY_AH_WW && (EPI == kEpiNone || EPI == kEpiAoGen);
+  // the AO any hit of the persistent launch with lane refill
+  constexpr bool kRefill = ANY && !COUNT && EPI == kEpiAoGen && TRAV == 0 && !kSpread &&
+                           SPRAY_AO_REFILL > 0 && SPRAY_AH_QNODES && SPRAY_AH_WW &&
+                           SPRAY_DIAG_MODE == 0;
   __shared__ int32_t stack[(kLaneStack ? kLStk : 1) * kBlock];
   __shared__ uint8_t wtask[kSpread ? (kBlock / 64) * 512 : 1];
   __shared__ uint8_t whit[kSpread ? kBlock : 1];
@@ -1191,6 +1479,11 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   // spawned shadow rays of the wave, added to *sh_count once at its end (a
   // same-address atomic per chunk queued ~10^5 atomics behind each other)
   uint32_t wcount = 0;
+  if constexpr (kRefill) {  // always persistent (launch_scene_t); pairs, no index list
+    scene_ray_ah_refill<W, kLStk, uint32_t(SPRAY_AO_REFILL), uint32_t(SPRAY_CHUNK_AO)>(
+        A, M, S, stl, sbox, sdom, stk, wstk);
+    return;
+  }
   const bool persist = ANY ? (SPRAY_PERSIST_AH != 0 || A.persist != 0) : SPRAY_PERSIST_CH != 0;
   const int lane = threadIdx.x & 63;
   const uint32_t* __restrict__ idx = A.idx;
@@ -2112,8 +2405,12 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
-  const bool kPersist =
-      ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays) : SPRAY_PERSIST_CH != 0;
+  // the AO rays generated in the lanes walk with lane refill at every size
+  constexpr bool kRefillLaunch = ANY && !COUNT && EPI == kEpiAoGen && TRAV == 0 &&
+                                 SPRAY_AO_REFILL > 0 && SPRAY_AH_QNODES && SPRAY_AH_WW &&
+                                 !SPRAY_AH_SPREAD && SPRAY_DIAG_MODE == 0;
+  const bool kPersist = kRefillLaunch || (ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays)
+                                              : SPRAY_PERSIST_CH != 0);
   a.persist = kPersist ? 1 : 0;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
   if (kPersist && !grid) {
