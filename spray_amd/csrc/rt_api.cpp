@@ -271,7 +271,7 @@ int spray_rt::detail::scene_common(spray_rt_ctx* c, const void* rays, size_t M,
   if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->d_heads)
-    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), kQueues * 32 * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), kHeadsBytes));
   return prepare(c);
 }
 

@@ -111,5 +111,6 @@ static_assert(sizeof(DomTrav) == 16, "DomTrav must be 16 B");
 // Persistent scene launches: kQueues work queues (kQueues / 8 per XCD), head
 // counters 32 words apart.
 constexpr int kQueues = 64;
+constexpr size_t kHeadsBytes = size_t(kQueues) * 32 * 4;  // queue heads, 32 words apart
 
 }  // namespace spray_rt

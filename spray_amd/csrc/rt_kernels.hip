@@ -8,6 +8,8 @@
 // other kernel here -- VBuf compares t with == (ooc_vbuf.cc:41-52).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <hipcub/block/block_reduce.hpp>
 #include <hipcub/block/block_scan.hpp>
 
@@ -21,15 +23,18 @@ namespace spray_rt {
 namespace {
 
 // Work distribution of the scene kernels (measured, profiles/): closest hit
-// = persistent waves dequeuing 128-ray chunks from per-XCD band queues
-// (1.02 -> 0.71 ms: no block-coupled wave lifetimes, band-local L2); any hit
+// = persistent waves dequeuing 256-ray chunks (four neighbouring packets,
+// which share the scalar cache) from per-XCD band queues (1.02 -> 0.71 ms:
+// no block-coupled wave lifetimes, band-local L2; 128 -> 256 with the
+// dequeue during the last packet, SPRAY_DEQ_AHEAD: fused launch 0.759 ->
+// 0.744 ms, DESIGN §4 "Launch tail"); any hit
 // = one ray per lane over a plain grid for batches below kPersistAhRays
 // (shadow batches: the persistent tail costs more than it saves, 0.27 vs
 // 0.33 ms), persistent above it (AO-16 batches, 36.6 M rays: 6.23 -> 5.71 ms
 // per AO step).  SPRAY_PERSIST_*/SPRAY_CHUNK_* select the other forms in
 // diagnostic builds.
 #ifndef SPRAY_CHUNK_CH
-#define SPRAY_CHUNK_CH 128
+#define SPRAY_CHUNK_CH 256
 #endif
 #ifndef SPRAY_CHUNK_AH
 #define SPRAY_CHUNK_AH 128
@@ -1063,12 +1068,22 @@ __device__ __forceinline__ bool wave_coherent(const SceneArgs& A, size_t i, bool
 // rin (optional): the lane's ray as org[3], dir[3] (a shadow ray queued in
 // LDS, tnear = SPRAY_RAY_EPSILON, tfar = +inf) instead of A.rays[i]; i is
 // then only the index its result is written at.
-template <int W, bool ANY, int EPI>
+struct NoPost {
+  __device__ void operator()() const {}
+};
+// post (optional): called once the lane's ray has arrived -- a vector-memory
+// operation it issues (the steal scheduler's next-packet claim) then
+// overlaps the walk, whose node and triangle fetches are scalar loads and
+// whose stack is LDS: no vmcnt wait until the epilogue's gathers.  (Issued
+// before the ray loads' wait it would be waited for with them: vector
+// memory returns in order.)
+template <int W, bool ANY, int EPI, typename Post = NoPost>
 __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, bool valid,
                                                  const float4* stl, const float* sbox,
                                                  const float4* sdom, int32_t* wstk,
                                                  bool& spawn, float* pos, float* wi,
-                                                 const float* rin = nullptr) {
+                                                 const float* rin = nullptr,
+                                                 const Post& post = Post()) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int lane = threadIdx.x & 63;
@@ -1090,6 +1105,13 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     d4 = make_float4(b.x, b.y, b.z, b.w);
   }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  if constexpr (!std::is_same<Post, NoPost>::value) {
+    // the ray registers are consumed here, so their wait is emitted before
+    // the hook's operation (the compiler would otherwise schedule the hook
+    // first and wait for both together)
+    asm volatile("" ::"v"(o4.x), "v"(d4.x));
+    post();
+  }
   uint64_t m[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) m[w] = 0;
@@ -1300,6 +1322,41 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   }
 }
 
+// Diagnostic (SPRAY_WAVE_TIMES builds only): per wave of the persistent
+// scene launches, 100-MHz wall-clock stamps at entry, after the LDS
+// staging, when the band queues ran dry and at exit, plus its chunk count
+// and XCD -- the launch's ramp and tail (scripts/wave_times.py).
+#ifndef SPRAY_WAVE_TIMES
+#define SPRAY_WAVE_TIMES 0
+#endif
+// When a wave takes its next chunk: 1 = before tracing the current one (the
+// atomic in flight during the chunk, but the chunk dequeued ahead waits in
+// the wave's hands while the queues run dry); 0 = after it; 2 = during the
+// walk of the chunk's last packet, once that packet's rays have landed
+// (packet kernels, scene_ray_packet's post hook; the atomic overlaps the
+// walk and nothing waits in a wave's hands for longer than one packet).
+#ifndef SPRAY_DEQ_AHEAD
+#define SPRAY_DEQ_AHEAD 2
+#endif
+#if SPRAY_WAVE_TIMES
+__device__ unsigned long long g_wave_times[5 * 16384];
+// per wave up to 255 events: (start << 24 | duration) stamps and (kind << 40 | index)
+__device__ unsigned long long g_pkt_log[2 * 6144 * 256];
+__device__ unsigned int g_pkt_n[6144];
+__device__ __forceinline__ void pkt_log(uint32_t kind, uint64_t index, unsigned long long t0) {
+  const unsigned long long t1 = wall_clock64();
+  const uint32_t wid = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && wid < 6144) {
+    const uint32_t n = g_pkt_n[wid];
+    if (n < 256) {
+      g_pkt_log[2 * (size_t(wid) * 256 + n)] = ((t0 & 0xFFFFFFFFFFull) << 24) | ((t1 - t0) & 0xFFFFFFull);
+      g_pkt_log[2 * (size_t(wid) * 256 + n) + 1] = (uint64_t(kind) << 40) | index;
+      g_pkt_n[wid] = n + 1;
+    }
+  }
+}
+#endif
+
 // Persistent launch: each wave dequeues kChunk-ray chunks from kQueues
 // queues, each owning a contiguous band of the rays.  XCD x's waves start on
 // its eight bands (an eighth of the image: its L2 holds the BVH nodes of that
@@ -1389,7 +1446,13 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
   if (q.n < kShadowT) return;
   wave_lds_sync();
   const uint32_t cnt = q.n < 64 ? q.n : 64u;
+#if SPRAY_WAVE_TIMES
+  const unsigned long long t0 = wall_clock64();
+#endif
   shadow_trace<W>(A, q, cnt, stl, sbox, sdom, wstk);
+#if SPRAY_WAVE_TIMES
+  pkt_log(1u, cnt, t0);
+#endif
   // the remainder (< 64) moves to the front
   const uint32_t rest = q.n - cnt;
   const bool mv = lane < rest;
@@ -1461,6 +1524,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
   ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
                  sq_src + (kShadow ? (threadIdx.x >> 6) * kShadowQ : 0), 0u};
+  const unsigned long long wt0 = SPRAY_WAVE_TIMES ? wall_clock64() : 0ull;
+  unsigned long long wt1 = 0, wt2 = 0;
+  uint32_t wchunks = 0;
   size_t M = A.M;
   if (A.d_count) {  // ray count produced on the device
     const size_t dc = *A.d_count;
@@ -1471,6 +1537,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < A.ndom; k += kBlock) sdom[k] = ld4(A.domtrav, k);
   __syncthreads();
+  if (SPRAY_WAVE_TIMES) wt1 = wall_clock64();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
   int32_t* stk = stack + threadIdx.x;
   int32_t* wstk = wstack + (threadIdx.x >> 6) * STK;
@@ -1522,13 +1589,26 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
         // the next chunk is dequeued before this one is traced: the atomic's
         // latency overlaps the traversal
         uint32_t next = 0;
-        if (lane == 0) next = atomicAdd(head, kChunk);
+        if (SPRAY_DEQ_AHEAD == 1 && lane == 0) next = atomicAdd(head, kChunk);
+        const size_t cbeg = begin + base;
         for (uint32_t c = 0; c < kChunk; c += 64) {
-          const size_t j = begin + base + c + lane;
+          const size_t j = cbeg + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
           const bool ok = j < end && i < A.M && (!A.valid || A.valid[i]);
           flag = false;
-          if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
+#if SPRAY_WAVE_TIMES
+          const unsigned long long pt0 = wall_clock64();
+#endif
+          if (kPacket && !kAdaptive && SPRAY_DEQ_AHEAD == 2) {
+            // the next chunk is dequeued by the chunk's last packet once its
+            // rays have landed: the atomic overlaps that packet's walk, and
+            // no chunk waits in a wave's hands while another is traced
+            const bool last = c + 64 >= kChunk;
+            scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi, nullptr,
+                                          [&]() {
+                                            if (last && lane == 0) next = atomicAdd(head, kChunk);
+                                          });
+          } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           else if (kSpread)
             scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task,
@@ -1536,18 +1616,45 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           else if (ok)
             scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
+#if SPRAY_WAVE_TIMES
+          pkt_log(0u, (cbeg + c) / 64, pt0);
+#endif
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi, wcount);
           if (kShadow)
             shadow_push<W>(A, sq, j < end, flag, i, pos, wi, stl, sbox, sdom, wstk, wcount);
         }
+        if ((SPRAY_DEQ_AHEAD == 0 || (SPRAY_DEQ_AHEAD == 2 && !(kPacket && !kAdaptive))) &&
+            lane == 0)
+          next = atomicAdd(head, kChunk);
         base = __builtin_amdgcn_readfirstlane(next);
+        ++wchunks;
       }
     }
   }
+  if (SPRAY_WAVE_TIMES) wt2 = wall_clock64();
   if (kShadow && sq.n) {  // the wave's last shadow rays (fewer than 64)
     wave_lds_sync();
+#if SPRAY_WAVE_TIMES
+    const unsigned long long t0 = wall_clock64();
+#endif
     shadow_trace<W>(A, sq, sq.n, stl, sbox, sdom, wstk);
+#if SPRAY_WAVE_TIMES
+    pkt_log(2u, sq.n, t0);
+#endif
   }
+#if SPRAY_WAVE_TIMES
+  if (persist && lane == 0) {
+    const uint32_t wid = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (wid < 16384) {
+      unsigned long long* o = g_wave_times + 5 * size_t(wid);
+      o[0] = wt0;
+      o[1] = wt1;
+      o[2] = wt2;
+      o[3] = wall_clock64();
+      o[4] = (unsigned long long)wchunks | ((unsigned long long)(xcc_id() & 7u) << 32);
+    }
+  }
+#endif
   if ((EPI == kEpiSpawn || kShadow) && A.sh_count && wcount && lane == 0)
     atomicAdd(A.sh_count, wcount);
   if (COUNT) {
@@ -2364,6 +2471,30 @@ __global__ __launch_bounds__(kBlock) void k_iota(uint32_t* __restrict__ out, uin
 }
 
 }  // namespace
+
+#if SPRAY_WAVE_TIMES
+// copies the last persistent scene launch's wave stamps (n words, 5 per wave)
+extern "C" int spray_rt_diag_packet_log(void* host_log, void* host_n, int reset) {
+  if (reset) {
+    static unsigned int zero[6144];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pkt_n), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+  }
+  if (hipMemcpyFromSymbol(host_n, HIP_SYMBOL(g_pkt_n), 6144 * 4, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return -1;
+  return hipMemcpyFromSymbol(host_log, HIP_SYMBOL(g_pkt_log), size_t(2) * 6144 * 256 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+extern "C" int spray_rt_diag_wave_times(void* host, size_t n) {
+  if (n > 5 * 16384) n = 5 * 16384;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_times), n * 8, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // launchers
