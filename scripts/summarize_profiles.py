@@ -24,7 +24,9 @@ Derived metrics (MI355X_MICROARCH.md):
   (the L2 line; an upper bound of the bytes the L2 served);
 * scalar-cache hit = SQC_DCACHE_HITS / SQC_DCACHE_REQ; TA busy =
   TA_BUSY_avr / cycles; VALU lane utilisation = SQ_THREAD_CYCLES_VALU /
-  (64 x SQ_ACTIVE_INST_VALU); memory wait = SQ_WAIT_ANY / SQ_WAVE_CYCLES.
+  (64 x SQ_ACTIVE_INST_VALU); memory wait = SQ_WAIT_ANY / SQ_WAVE_CYCLES;
+  wave life = 4 x SQ_WAVE_CYCLES / SQ_WAVES / cycles (quad-cycle units; for
+  a persistent launch the share of the launch its waves are alive).
 """
 import csv
 import glob
@@ -79,6 +81,10 @@ def derive(c, dur_s):
         d["scalar_cache_hit"] = c.get("SQC_DCACHE_HITS", 0) / c["SQC_DCACHE_REQ"]
     if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
         d["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"])
+    if c.get("SQ_WAVE_CYCLES") and c.get("SQ_WAVES") and cyc:
+        # mean wave lifetime over the launch (SQ_WAVE_CYCLES counts quad-cycles);
+        # for the persistent launches, the share of the launch a wave is alive
+        d["wave_life_frac"] = c["SQ_WAVE_CYCLES"] * 4 / c["SQ_WAVES"] / cyc
     if c.get("SQ_WAVE_CYCLES"):
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in c:
@@ -116,8 +122,8 @@ def main(src, tag):
              "--insitu 0` (scripts/gpu_profile.sh); raw counters in `%s_pmc.csv`; derivations "
              "in scripts/summarize_profiles.py." % tag, "",
              "| kernel | calls | avg us | traffic B | HBM frac | L2 hit | L2 req frac | "
-             "VALU issue | SALU issue | lane util | scalar hit | TA busy | mem wait |",
-             "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+             "VALU issue | SALU issue | lane util | scalar hit | TA busy | mem wait | wave life |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
 
     def f(x, fmt="%.3f"):
         return fmt % x if x is not None else "-"
@@ -127,11 +133,12 @@ def main(src, tag):
         out["kernels"][k] = {"avg_us": dur.get(k, 0) * 1e6, "counters": ctr[k], "derived": dv}
         if not k.startswith("k_") or k not in dur:
             continue
-        lines.append("| `%s` | %s | %.2f | %s | %s | %s | %s | %s | %s | %s | %s | %s | %s |" % (
+        lines.append("| `%s` | %s | %.2f | %s | %s | %s | %s | %s | %s | %s | %s | %s | %s | %s |" % (
             k, calls.get(k, "-"), dur[k] * 1e6, f(dv.get("traffic_bytes"), "%.3e"),
             f(dv.get("hbm_frac")), f(dv.get("l2_hit")), f(dv.get("l2_frac")),
             f(dv.get("valu_issue")), f(dv.get("salu_issue")), f(dv.get("valu_lane_util")),
-            f(dv.get("scalar_cache_hit")), f(dv.get("ta_busy")), f(dv.get("wait_any_frac"))))
+            f(dv.get("scalar_cache_hit")), f(dv.get("ta_busy")), f(dv.get("wait_any_frac")),
+            f(dv.get("wave_life_frac"))))
     json.dump(out, open(os.path.join(prof, "pmc_counters.json"), "w"), indent=1)
     bench = os.path.join(src, "bench.log")
     if os.path.exists(bench):

@@ -98,7 +98,8 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   const size_t b_dom = align256(257 * sizeof(uint32_t));
   const size_t b_score = align256(256 * sizeof(unsigned long long));
   const size_t b_ch = align256(nchk * sizeof(uint32_t));
-  const size_t b_dsh = align256(256 * kOocDeadShards * sizeof(uint32_t));
+  // two sets: an any-hit launch adds to one while it publishes the other
+  const size_t b_dsh = align256(2 * 256 * kOocDeadShards * sizeof(uint32_t));
   const size_t total =
       b_masks + 2 * b_v + b_pk + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score + b_dsh;
   HIPCHK(c, hipMalloc(&o->q_mem, total));
@@ -266,6 +267,9 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   const unsigned long long g = (unsigned long long)S.gen << 32;
   // waits for launch `k` of this pass (0-based) to publish (or complete),
   // then folds the newest counts in
+  // launch k's counts are published by launch k (closest hit: its resolve)
+  // or by launch k + 1 (any hit: a block of the next drain), so the wait
+  // watches the publisher's event
   auto absorb = [&](uint32_t k, int ring) -> int {
     for (unsigned spins = 0; snap[256] < g + k + 1; ++spins) {
       if ((spins & 1023) == 1023) {  // also watch the launch itself (errors)
@@ -363,8 +367,9 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
     }
     o->drains += cur.count;
     rings[S.launch % 4] = ring;
+    const uint32_t pub = any_hit ? 1u : 0u;  // the publisher's offset (lag >= 1)
     if (S.launch >= uint32_t(lag) &&
-        (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag) % 4])))
+        (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag + pub) % 4])))
       return r;
     ++S.launch;
     cur = nxt;
@@ -507,7 +512,7 @@ int spray_rt_ooc_occluded(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
   if ((r = build_queues(o, rays, valid, M, nullptr, occluded))) return r;
   const int W = c->ndom <= 64 ? 1 : 4;
   return drain(o, true, boxes, [&](hipStream_t s, const OocBatch& B, const OocSnapshot& S) {
-    return launch_ooc_ah_batch(s, B, W, rays, o->q, occluded, o->done, S, c->coherence);
+    return launch_ooc_ah_batch(s, B, W, rays, o->q, occluded, S, c->coherence);
   });
 }
 

@@ -367,8 +367,9 @@ __global__ __launch_bounds__(kBlock) void k_ooc_scatter(
 // The pair handled by this lane of a batch launch: the waves of segment s
 // (one resident domain's queue) are wave0[s] .. wave0[s+1]-1, so a wave
 // always walks one domain tree.  Returns the segment, or -1 past the end.
-__device__ __forceinline__ int batch_pair(const OocBatch& B, uint32_t& pj, bool& valid) {
-  const uint32_t gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+__device__ __forceinline__ int batch_pair(const OocBatch& B, uint32_t& pj, bool& valid,
+                                          uint32_t blk) {
+  const uint32_t gw = (blk * kBlock + threadIdx.x) >> 6;
   if (gw >= B.wave0[B.count]) return -1;
   int s = 0;
   while (s + 1 < B.count && B.wave0[s + 1] <= gw) ++s;
@@ -381,9 +382,9 @@ __device__ __forceinline__ int batch_pair(const OocBatch& B, uint32_t& pj, bool&
 
 // Copy blocks of a launch (blockIdx >= B.copy0): the next batch's images,
 // pinned host memory -> HBM slot, 16-B lanes, four loads in flight per lane.
-__device__ __forceinline__ void prefetch_copy(const OocBatch& B) {
+__device__ __forceinline__ void prefetch_copy(const OocBatch& B, uint32_t blk) {
   const uint32_t nthreads = B.ncopy * kBlock;
-  const uint32_t t = (blockIdx.x - B.copy0) * kBlock + threadIdx.x;
+  const uint32_t t = (blk - B.copy0) * kBlock + threadIdx.x;
   for (int e = 0; e < B.pf_count; ++e) {
     const uint4* __restrict__ src = B.pf_src[e];
     uint4* __restrict__ dst = B.pf_dst[e];
@@ -553,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
     uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf,
     uint32_t* __restrict__ dshard) {
   if (blockIdx.x >= B.copy0) {
-    prefetch_copy(B);
+    prefetch_copy(B, blockIdx.x);
     return;
   }
   __shared__ int32_t wstack[kWaves * kStack];
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
   __syncthreads();
   uint32_t pj;
   bool valid;
-  const int s = batch_pair(B, pj, valid);
+  const int s = batch_pair(B, pj, valid, blockIdx.x);
   if (s >= 0)
     ch_pair<W>(B.d[s], pj, valid, rays, idx, masks, boxes, key, pkey, pleaf,
                wstack + (threadIdx.x >> 6) * kStack, dead);
@@ -581,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
   if (blockIdx.x == 0) write_snapshot(live, dshard, S, ndom);
   uint32_t pj;
   bool valid;
-  const int s = batch_pair(B, pj, valid);
+  const int s = batch_pair(B, pj, valid, blockIdx.x);
   if (s < 0 || !valid) return;
   const uint64_t mine = pkey[pj];
   if (mine == kOocMissKey) return;
@@ -689,22 +690,40 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
   wave_add_deaths<W>(dm, dead);
 }
 
-// k_ooc_snapshot (one block) follows and publishes the live counts.
+// The launch's deaths go to shard set S.launch & 1; its block 0 publishes
+// the launch before it (set (S.launch - 1) & 1, complete at this kernel's
+// start; block 0 is dispatched first, so the host, which chooses the batch
+// after next from these counts, is not kept waiting for the drain) -- one
+// launch per any-hit batch instead of a drain and a one-block snapshot
+// kernel.  The drain and copy blocks follow at blockIdx.x - 1.  Launch 0 of
+// a pass publishes nothing (the queue build cleared both sets); the pass's
+// last launch is never published (no batch follows it).
 template <int W, int MODE>
 __global__ __launch_bounds__(kBlock, SPRAY_OOC_AH_WAVES) void k_ooc_ah_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, uint8_t* __restrict__ occ,
-    uint32_t* __restrict__ dshard) {
+    uint32_t* __restrict__ dshard, uint32_t* __restrict__ live, OocSnapshot S, int ndom) {
   // per lane: lane-interleaved stacks; packet: one stack per wave
   __shared__ int32_t stack[MODE != 1 ? kStack * kBlock : 1];
   __shared__ int32_t wstack[MODE != 0 ? kWaves * kStack : 1];
   __shared__ uint32_t dead[64 * W];
+  const size_t set = size_t(ndom) * kOocDeadShards;
+  if (blockIdx.x == 0) {  // the previous launch's counts
+    if (S.launch > 0) {
+      OocSnapshot P = S;
+      P.launch = S.launch - 1;
+      write_snapshot(live, dshard + ((S.launch - 1) & 1u) * set, P, ndom);
+    }
+    return;
+  }
+  dshard += (S.launch & 1u) * set;
   for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
   __syncthreads();
   uint32_t pj;
   bool ok;
-  const int s = blockIdx.x >= B.copy0 ? -1 : batch_pair(B, pj, ok);
-  if (blockIdx.x >= B.copy0) prefetch_copy(B);  // then counted in `done` like the others
+  const uint32_t blk = blockIdx.x - 1;
+  const int s = blk >= B.copy0 ? -1 : batch_pair(B, pj, ok, blk);
+  if (blk >= B.copy0) prefetch_copy(B, blk);
   if (s >= 0)
     ah_pair<W, MODE>(B.d[s], pj, ok, rays, idx, masks, occ, stack + (MODE != 1 ? threadIdx.x : 0),
                      wstack + (MODE != 0 ? (threadIdx.x >> 6) * kStack : 0), dead);
@@ -733,7 +752,7 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   k_ooc_chunk_sums<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.sb, g, ndom, q.csum, q.cw);
   k_ooc_chunk_scan<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.csum, g, ndom, q.off);
   k_ooc_first<<<1, 256, 0, s>>>(q.csum, q.cw, int(nch), ndom, q.first, q.live, q.score);
-  if (hipMemsetAsync(q.dshard, 0, size_t(ndom) * kOocDeadShards * sizeof(uint32_t), s) !=
+  if (hipMemsetAsync(q.dshard, 0, 2 * size_t(ndom) * kOocDeadShards * sizeof(uint32_t), s) !=
       hipSuccess)
     return hipGetLastError();
   if (W == 1)
@@ -800,15 +819,16 @@ hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* h
 }
 
 hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
-                               const OocScratch& q, uint8_t* occ, uint32_t* done,
-                               OocSnapshot snap, int coherence) {
+                               const OocScratch& q, uint8_t* occ, OocSnapshot snap,
+                               int coherence) {
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
   const int ndom = 64 * W;
-  (void)done;
   unsigned g = batch_grid(B);
   g += B.pf_count ? B.ncopy : 0;
-#define SPRAY_AH_LAUNCH(WW, MM) \
-  k_ooc_ah_batch<WW, MM><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.dshard)
+  g += 1;  // block 0 publishes the previous launch's counts
+#define SPRAY_AH_LAUNCH(WW, MM)                                                              \
+  k_ooc_ah_batch<WW, MM><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, occ, q.dshard, q.live, \
+                                              snap, ndom)
   // the context's coherence setting: incoherent -> per lane, else packets
   // (measured on configs[3]'s PT shadows, one box: packets 4.08, per lane
   // 4.60, the per-wave choice 4.72 ms per frame -- the choice's direction
@@ -821,7 +841,7 @@ hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
   const int mode = coherence == SPRAY_RT_RAYS_INCOHERENT                  ? 0
                    : (coherence == SPRAY_RT_RAYS_ADAPTIVE && adaptive) ? 2
                                                                           : 1;
-  if (g) {
+  {
     if (W == 1) {
       if (mode == 0) SPRAY_AH_LAUNCH(1, 0);
       else if (mode == 1) SPRAY_AH_LAUNCH(1, 1);
@@ -833,9 +853,6 @@ hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
     }
   }
 #undef SPRAY_AH_LAUNCH
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  k_ooc_snapshot<<<1, 256, 0, s>>>(q.live, q.dshard, snap, ndom);
   return hipGetLastError();
 }
 

@@ -200,7 +200,7 @@ struct OocScratch {
   uint32_t* cw;               // [chunk_cap] DomainStats weight per (domain, chunk)
   unsigned long long* score;  // [256] DomainStats score per domain
   uint32_t* live;             // [256] live pairs per queue (see k_ooc_ch_batch)
-  uint32_t* dshard;           // [256 * kOocDeadShards] deaths since the last snapshot
+  uint32_t* dshard;           // [2][256 * kOocDeadShards] deaths since the last snapshot
   uint64_t* pkey;             // [pair_cap] closest-hit key of each (ray, domain) pair
   uint32_t* pleaf;            // [pair_cap] its triangle (leaf order)
   size_t block_cap;           // >= ndom * ray blocks
@@ -268,8 +268,8 @@ hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* h
 // q.live; the snapshot follows.  done: a device counter, 0 between launches.
 // coherence: SPRAY_RT_RAYS_* (the walk form, as the scene path's any hit)
 hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
-                               const OocScratch& q, uint8_t* occ, uint32_t* done,
-                               OocSnapshot snap, int coherence);
+                               const OocScratch& q, uint8_t* occ, OocSnapshot snap,
+                               int coherence);
 // frame layer (frame_kernels.hip)
 hipError_t launch_shade(hipStream_t s, const spray_rt_shader& P, const spray_rt_bsdf* bsdfs,
                         int nbsdf, int bounce, int ns, spray_rt_ray* rays,
