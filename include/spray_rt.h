@@ -603,6 +603,14 @@ int spray_rt_insitu_destroy(spray_rt_insitu_t ins);
  * ndomains / nranks.  Host only. */
 int spray_rt_insitu_partition(const float* boxes, int ndomains, const float scene_bound[6],
                               int nranks, int* owner_out);
+/* The same with the partition mode of data_partition.h: GROUP_CLOSE (the
+ * contiguous shares above, :118-137, the reference's compiled mode) or
+ * ROUND_ROBIN (the sorted Morton order dealt out one domain per rank in
+ * turn, "trying to scatter close domains", :139-155). */
+#define SPRAY_RT_PARTITION_GROUP_CLOSE 0
+#define SPRAY_RT_PARTITION_ROUND_ROBIN 1
+int spray_rt_insitu_partition_mode(const float* boxes, int ndomains, const float scene_bound[6],
+                                   int nranks, int mode, int* owner_out);
 /* This rank's part of a frame: rays[n] / pixid / samid are its eye rays
  * (spray_rt_eye_rays_insitu of its stripe; samid = blocking-tile sample id),
  * traced for shader->bounces bounces across the group; the contributions

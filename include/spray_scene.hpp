@@ -4,13 +4,17 @@
 //
 // A tracer template (ooc::Tracer, insitu::MultiThreadTracer, the shaders)
 // takes its scene type as ShaderT::SceneType (src/ooc/ooc_tracer.h:55); with
-// spray_amd::Scene<> there the per-domain drains keep their call shapes:
+// spray_amd::Scene<AppTypes> there the tracers and shaders compile unchanged:
 //
 //   scene->load(id, &sinfo);                                  // omp single
 //   scene->intersect(sinfo.rtc_scene, sinfo.cache_block, r->org, r->dir,
 //                    &rtc_isect_);                            // every thread
 //   scene->occluded(sinfo.rtc_scene, r->org, r->dir, &rtc_ray_);
 //   scene->intersectDomains(ray_ext);                         // Isector
+//   lights_ = scene->getLights();          // std::vector<Light*> (ooc_shader_pt.h:51)
+//   const Bsdf* bsdf = scene_->getBsdf(domain_id);            // (:118)
+//   const auto& ids = partition_->getDomains(rank);   // (insitu_tcontext.inl:98)
+//   Aabb aabb = scene_.getBound(); scene_.buildWbvh();  // (spray_renderer.inl:47,96)
 //
 // (ooc_tcontext.inl:28-100, insitu_tcontext.inl:125-186,
 // ooc_isector.h:116-174).  The const queries are safe from any number of
@@ -19,6 +23,25 @@
 // not run concurrently with queries -- the reference calls it inside omp
 // single between barriers (ooc_pcontext.h:144-157).
 //
+// Application types.  The shaders hold the scene's lights and materials as
+// the application's own polymorphic classes (spray::Light with sample /
+// sampleArea / isAreaLight, spray::Bsdf with isDelta / sampleDelta /
+// sampleRandom, spray::Aabb with bounds[2]).  Scene<Types> builds them from
+// the scene file through a policy:
+//
+//   struct SprayTypes {                       // what the reference would add
+//     typedef spray::Light Light;  typedef spray::Bsdf Bsdf;  typedef spray::Aabb Aabb;
+//     static Light* makeLight(const spray_amd::LightDesc& d);   // new PointLight(...)
+//     static Bsdf* makeBsdf(const spray_rt_bsdf& b);            // new DiffuseBsdf(...)
+//     static Aabb makeAabb(const float lo_hi[6]);
+//   };
+//   typedef spray_amd::Scene<SprayTypes> SceneType;
+//
+// DefaultTypes (below) are plain records with the same query methods for
+// callers that bring no types of their own.  Lights are owned and deleted
+// by the scene (as Scene::~Scene does, scene.h:66-71), BSDFs likewise (the
+// reference's Domain owns its Bsdf, domain.h:33).
+//
 // Record types are the caller's: RTCRayIntersection (96 B), Embree 2's
 // RTCRay (96 B) and RTCRayExt (org / dir at the same offsets, a DomainList*
 // with reset / push).  Only the byte offsets of spray_rt_ray_intersection
@@ -26,11 +49,14 @@
 // CHECK-aborts).
 #pragma once
 
+#include <cmath>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <list>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
@@ -57,46 +83,189 @@ inline RTCScene slot_handle(int block) {
 }
 inline int handle_slot(RTCScene s) { return int(reinterpret_cast<uintptr_t>(s)) - 1; }
 
-// Domain (src/render/domain.h:32-44), the fields the tracers read.
-struct Domain {
-  int id = 0;
-  size_t num_vertices = 0, num_faces = 0;
-  float world_aabb[6] = {0, 0, 0, 0, 0, 0};
-};
-
-// InsituPartition (src/render/data_partition.h:31-156): rank(domain).
-class InsituPartition {
- public:
-  void partition(const std::vector<Domain>& domains, const float bound[6], int nranks) {
-    std::vector<float> boxes(6 * domains.size());
-    for (size_t i = 0; i < domains.size(); ++i)
-      std::memcpy(&boxes[6 * i], domains[i].world_aabb, 6 * sizeof(float));
-    rank_.assign(domains.size(), 0);
-    if (!domains.empty() &&
-        spray_rt_insitu_partition(boxes.data(), int(domains.size()), bound, nranks, rank_.data()))
-      throw std::runtime_error("spray_amd::InsituPartition: partition failed");
-  }
-  int rank(int id) const { return rank_[size_t(id)]; }
-  size_t getNumDomains() const { return rank_.size(); }
-
- private:
-  std::vector<int> rank_;
-};
-
-struct Light {  // PointLight / DiffuseHemisphereLight (src/render/light.h:31-89)
-  int type = 0;  // 0 point, 1 diffuse hemisphere
+// A light of the scene file (SceneLoader, scene_loader.cc:262-313):
+// type = SPRAY_RT_LIGHT_POINT (position, radiance) or
+// SPRAY_RT_LIGHT_HEMISPHERE (radiance).
+struct LightDesc {
+  int type = SPRAY_RT_LIGHT_POINT;
   float position[3] = {0, 0, 0};
   float radiance[3] = {0, 0, 0};
 };
 
-template <typename Unused = void>
+// ---- default application types ---------------------------------------------
+struct vec3 {
+  float x = 0, y = 0, z = 0;
+  vec3() = default;
+  vec3(float a, float b, float c) : x(a), y(b), z(c) {}
+  float& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+  const float& operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+};
+
+// Aabb (src/render/aabb.h:32-80): the members the tracers read.
+struct Aabb {
+  vec3 bounds[2];
+  const vec3& getMin() const { return bounds[0]; }
+  const vec3& getMax() const { return bounds[1]; }
+  const vec3& getBound(std::uint8_t i) const { return bounds[i]; }
+  vec3 getCenter() const {  // (min + max) * 0.5
+    return vec3((bounds[0].x + bounds[1].x) * 0.5f, (bounds[0].y + bounds[1].y) * 0.5f,
+                (bounds[0].z + bounds[1].z) * 0.5f);
+  }
+  bool isValid() const {
+    return bounds[0].x <= bounds[1].x && bounds[0].y <= bounds[1].y && bounds[0].z <= bounds[1].z;
+  }
+};
+
+// Light / PointLight / DiffuseHemisphereLight (src/render/light.h:31-89):
+// the parameters and the point light's sample(); area-light sampling is the
+// shading layer's (spray_rt_shade on the device).
+class Light {
+ public:
+  virtual ~Light() = default;
+  virtual bool isAreaLight() const = 0;
+  virtual int type() const = 0;
+  const vec3& radiance() const { return radiance_; }
+
+ protected:
+  explicit Light(const vec3& r) : radiance_(r) {}
+  vec3 radiance_;
+};
+class PointLight : public Light {
+ public:
+  PointLight(const vec3& position, const vec3& radiance) : Light(radiance), position_(position) {}
+  bool isAreaLight() const override { return false; }
+  int type() const override { return SPRAY_RT_LIGHT_POINT; }
+  const vec3& position() const { return position_; }
+  // PointLight::sample (light.h:47-53): wi = normalize(position - p), pdf 1
+  vec3 sample(const vec3& p, vec3* wi, float* pdf) const {
+    vec3 d(position_.x - p.x, position_.y - p.y, position_.z - p.z);
+    const float inv = 1.0f / std::sqrt((d.x * d.x + d.y * d.y) + d.z * d.z);
+    *wi = vec3(d.x * inv, d.y * inv, d.z * inv);
+    *pdf = 1.0f;
+    return radiance_;
+  }
+
+ private:
+  vec3 position_;
+};
+class DiffuseHemisphereLight : public Light {
+ public:
+  explicit DiffuseHemisphereLight(const vec3& radiance) : Light(radiance) {}
+  bool isAreaLight() const override { return true; }
+  int type() const override { return SPRAY_RT_LIGHT_HEMISPHERE; }
+};
+
+// Bsdf (src/render/reflection.h:219-239): the material record of a domain.
+class Bsdf {
+ public:
+  explicit Bsdf(const spray_rt_bsdf& r) : rec_(r) {}
+  virtual ~Bsdf() = default;
+  bool isDelta() const { return rec_.type != SPRAY_RT_BSDF_DIFFUSE; }
+  int type() const { return rec_.type; }
+  const spray_rt_bsdf& record() const { return rec_; }
+
+ private:
+  spray_rt_bsdf rec_;
+};
+
+struct DefaultTypes {
+  typedef spray_amd::Light Light;
+  typedef spray_amd::Bsdf Bsdf;
+  typedef spray_amd::Aabb Aabb;
+  static Light* makeLight(const LightDesc& d) {
+    const vec3 r(d.radiance[0], d.radiance[1], d.radiance[2]);
+    if (d.type == SPRAY_RT_LIGHT_HEMISPHERE) return new DiffuseHemisphereLight(r);
+    return new PointLight(vec3(d.position[0], d.position[1], d.position[2]), r);
+  }
+  static Bsdf* makeBsdf(const spray_rt_bsdf& b) { return new Bsdf(b); }
+  static Aabb makeAabb(const float b[6]) {
+    Aabb a;
+    a.bounds[0] = vec3(b[0], b[1], b[2]);
+    a.bounds[1] = vec3(b[3], b[4], b[5]);
+    return a;
+  }
+};
+
+// Domain (src/render/domain.h:32-44), the fields the tracers read; bsdf is
+// owned by the scene.
+template <typename Types>
+struct BasicDomain {
+  unsigned id = 0;
+  std::size_t num_vertices = 0, num_faces = 0;
+  typename Types::Aabb world_aabb{};
+  typename Types::Bsdf* bsdf = nullptr;
+};
+
+// InsituPartition (src/render/data_partition.h:31-243): rank(domain),
+// getDomains(rank), computePartition(n).  The Morton codes and their
+// dealing are the engine's (spray_rt_insitu_partition_mode).
+class InsituPartition {
+ public:
+  enum Mode {
+    GROUP_CLOSE_DOMAINS = SPRAY_RT_PARTITION_GROUP_CLOSE,  // the reference's compiled mode
+    ROUND_ROBIN = SPRAY_RT_PARTITION_ROUND_ROBIN,          // :139-155, "scatter close domains"
+  };
+
+  // partition(ndomains, domains, scene_aabb, num_ranks) (:59-156)
+  template <typename DomainT, typename AabbT>
+  void partition(int ndomains, const std::vector<DomainT>& domains, const AabbT& scene_aabb,
+                 int num_ranks, Mode mode = GROUP_CLOSE_DOMAINS) {
+    if (ndomains != int(domains.size()) || num_ranks <= 0)
+      throw std::runtime_error("spray_amd::InsituPartition: bad arguments");
+    boxes_.assign(6 * domains.size(), 0.f);
+    for (size_t i = 0; i < domains.size(); ++i)
+      for (int k = 0; k < 3; ++k) {
+        boxes_[6 * size_t(domains[i].id) + size_t(k)] = domains[i].world_aabb.bounds[0][k];
+        boxes_[6 * size_t(domains[i].id) + 3 + size_t(k)] = domains[i].world_aabb.bounds[1][k];
+      }
+    for (int k = 0; k < 3; ++k) {
+      bound_[k] = scene_aabb.bounds[0][k];
+      bound_[3 + k] = scene_aabb.bounds[1][k];
+    }
+    mode_ = mode;
+    domain_to_rank_ = deal(num_ranks);
+    rank_to_domains_.assign(size_t(num_ranks), std::list<int>());
+    for (size_t id = 0; id < domain_to_rank_.size(); ++id)  // mapDomains (:226-240)
+      rank_to_domains_[size_t(domain_to_rank_[id])].push_back(int(id));
+  }
+  int rank(int id) const { return domain_to_rank_[size_t(id)]; }
+  const std::list<int>& getDomains(int rank) const { return rank_to_domains_[size_t(rank)]; }
+  std::size_t getNumDomains(int rank) const { return rank_to_domains_[size_t(rank)].size(); }
+  int getNumDomains() const { return int(domain_to_rank_.size()); }
+  // computePartition (:157-213): the same dealing over num_partitions
+  std::vector<int> computePartition(int num_partitions) const { return deal(num_partitions); }
+  Mode mode() const { return mode_; }
+
+ private:
+  std::vector<int> deal(int nranks) const {
+    const int n = int(boxes_.size() / 6);
+    std::vector<int> owner(size_t(n), 0);
+    if (n && spray_rt_insitu_partition_mode(boxes_.data(), n, bound_, nranks, int(mode_),
+                                            owner.data()))
+      throw std::runtime_error("spray_amd::InsituPartition: partition failed");
+    return owner;
+  }
+  std::vector<float> boxes_;
+  float bound_[6] = {0, 0, 0, 0, 0, 0};
+  Mode mode_ = GROUP_CLOSE_DOMAINS;
+  std::vector<int> domain_to_rank_;
+  std::vector<std::list<int>> rank_to_domains_;
+};
+
+template <typename Types = DefaultTypes>
 class Scene {
  public:
+  typedef typename Types::Light Light;
+  typedef typename Types::Bsdf Bsdf;
+  typedef typename Types::Aabb Aabb;
+  typedef BasicDomain<Types> Domain;
+
   Scene() = default;
   Scene(const Scene&) = delete;
   Scene& operator=(const Scene&) = delete;
   ~Scene() {
     for (auto& kv : lanes_) spray_rt_lane_destroy(kv.second);
+    for (Light* l : lights_) delete l;
     if (scene_) spray_scene_destroy(scene_);
   }
 
@@ -115,33 +284,45 @@ class Scene {
       throw std::runtime_error(std::string("spray_amd::Scene::init: ") + err);
     rt_ = spray_scene_rt(scene_);
     const int n = spray_scene_num_domains(scene_);
-    std::vector<float> boxes(6 * size_t(n));
-    spray_scene_bounds(scene_, boxes.data(), bound_);
+    boxes_.assign(6 * size_t(n), 0.f);
+    spray_scene_bounds(scene_, boxes_.data(), bound_);
+    int nb = 0;
+    spray_host_scene_bsdfs(desc_filename.c_str(), &nb, nullptr, err, sizeof(err));
+    std::vector<spray_rt_bsdf> recs(static_cast<size_t>(nb));
+    if (nb && spray_host_scene_bsdfs(desc_filename.c_str(), &nb, recs.data(), err, sizeof(err)))
+      throw std::runtime_error(std::string("spray_amd::Scene::init: ") + err);
     domains_.resize(size_t(n));
     for (int i = 0; i < n; ++i) {
       Domain& d = domains_[size_t(i)];
-      d.id = i;
-      std::memcpy(d.world_aabb, &boxes[6 * size_t(i)], sizeof(d.world_aabb));
+      d.id = unsigned(i);
+      d.world_aabb = Types::makeAabb(&boxes_[6 * size_t(i)]);
       spray_scene_domain_mesh(scene_, i, &d.num_vertices, &d.num_faces, nullptr, nullptr,
                               nullptr, nullptr);
+      if (i < nb) {
+        bsdfs_.emplace_back(Types::makeBsdf(recs[size_t(i)]));
+        d.bsdf = bsdfs_.back().get();
+      }
     }
     for (int l = 0; l < spray_scene_num_lights(scene_); ++l) {
       float v[7];
       spray_scene_light(scene_, l, v);
-      Light L;
+      LightDesc L;
       L.type = int(v[0]);
       std::memcpy(L.position, v + 1, 12);
       std::memcpy(L.radiance, v + 4, 12);
-      lights_.push_back(L);
+      lights_.push_back(Types::makeLight(L));
     }
-    int nb = 0;
-    spray_host_scene_bsdfs(desc_filename.c_str(), &nb, nullptr, err, sizeof(err));
-    bsdfs_.resize(size_t(nb));
-    if (nb && spray_host_scene_bsdfs(desc_filename.c_str(), &nb, bsdfs_.data(), err,
-                                     sizeof(err)))
-      throw std::runtime_error(std::string("spray_amd::Scene::init: ") + err);
     insitu_ = insitu_mode;
-    partition_.partition(domains_, bound_, num_virtual_ranks > 0 ? num_virtual_ranks : 1);
+    partition_.partition(n, domains_, getBound(), num_virtual_ranks > 0 ? num_virtual_ranks : 1);
+  }
+
+  // Scene::buildWbvh (scene.inl:103-105): the domain-level BVH.  The engine
+  // builds its top-level tree over the domain boxes when they are set; this
+  // sets them (again), so a caller that edited nothing gets the same tree.
+  void buildWbvh() {
+    if (spray_rt_domain_bounds(rt_, int(domains_.size()), boxes_.data()))
+      throw std::runtime_error(std::string("spray_amd::Scene::buildWbvh: ") +
+                               spray_rt_last_error(rt_));
   }
 
   // Scene::load(id, SceneInfo*) (scene.inl:161-187): not concurrent with
@@ -275,15 +456,20 @@ class Scene {
     make_ray(org, dir, r);
   }
 
-  // Scene::getBsdf (scene.h:211): the domain's material record.
-  const spray_rt_bsdf* getBsdf(int id) const { return &bsdfs_[size_t(id)]; }
+  // Scene::getBsdf (scene.h:213): the domain's material (null when the
+  // scene file gives it none, as the reference's Domain::bsdf).
+  const Bsdf* getBsdf(int id) const { return domains_[size_t(id)].bsdf; }
   const InsituPartition& getInsituPartition() const { return partition_; }
   bool insitu() const { return insitu_; }
-  size_t getNumDomains() const { return domains_.size(); }
+  std::size_t getNumDomains() const { return domains_.size(); }
   const std::vector<Domain>& getDomains() const { return domains_; }
-  const std::vector<Light>& getLights() const { return lights_; }
-  size_t getNumLights() const { return lights_.size(); }
-  const float* getBound() const { return bound_; }
+  // Scene::getLights (scene.h:219): the shaders copy it into their own
+  // std::vector<Light*> (ooc_shader_pt.h:51)
+  const std::vector<Light*>& getLights() const { return lights_; }
+  std::size_t getNumLights() const { return lights_.size(); }
+  // Scene::getBound (scene.h:82-85): the scene's world bound
+  Aabb getBound() const { return Types::makeAabb(bound_); }
+  const float* getBoundArray() const { return bound_; }
   spray_rt_ctx_t rt() const { return rt_; }
 
  private:
@@ -337,8 +523,9 @@ class Scene {
   spray_scene_t scene_ = nullptr;
   spray_rt_ctx_t rt_ = nullptr;
   std::vector<Domain> domains_;
-  std::vector<Light> lights_;
-  std::vector<spray_rt_bsdf> bsdfs_;
+  std::vector<float> boxes_;
+  std::vector<Light*> lights_;
+  std::vector<std::unique_ptr<Bsdf>> bsdfs_;
   float bound_[6] = {0, 0, 0, 0, 0, 0};
   InsituPartition partition_;
   bool insitu_ = false;

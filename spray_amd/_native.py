@@ -134,6 +134,7 @@ SIGNATURES = {
     "spray_rt_insitu_create": (I, [P, I, I, P, P, P]),
     "spray_rt_insitu_destroy": (I, [P]),
     "spray_rt_insitu_partition": (I, [P, I, P, I, P]),
+    "spray_rt_insitu_partition_mode": (I, [P, I, P, I, I, P]),
     "spray_rt_insitu_trace": (I, [P, P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_insitu_composite": (I, [P, P, SZ]),
     "spray_rt_insitu_stats": (I, [P, P]),

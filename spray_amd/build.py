@@ -50,6 +50,11 @@ def build(force=False, verbose=False, defines=(), out=None):
     """Builds the engine; `defines`/`out` produce diagnostic variants (never
     the shipped library)."""
     target = out or LIB
+    if defines and out is None:
+        # the shipped library's build id names its sources only; a variant
+        # written over it would inherit that id (and the committed PMC
+        # traffic of the clean build)
+        raise ValueError("diagnostic defines need an explicit `out` path")
     if not force and not defines and out is None and not _stale():
         return LIB
     os.makedirs(os.path.dirname(target), exist_ok=True)
@@ -101,6 +106,7 @@ def source_id():
     """Hash of everything the shipped library is built from: the sources,
     the headers, the public headers and this file's compile line."""
     h = hashlib.sha256()
+    h.update(ARCH.encode())
     for f in [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + PUBLIC + [__file__]:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
@@ -125,7 +131,8 @@ def build_tests():
     """The C++ caller test of the SceneT drop-in (include/spray_scene.hpp):
     links the engine and the CPU oracle (test infrastructure)."""
     os.makedirs(os.path.dirname(TEST_BIN), exist_ok=True)
-    cmd = ["g++", "-O2", "-std=c++17", "-fopenmp", "-Wall", "-I" + os.path.join(ROOT, "include"),
+    cmd = ["g++", "-O2", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-Wall",
+           "-I" + os.path.join(ROOT, "include"),
            "-I" + os.path.join(ROOT, "oracle"), TEST_SRC, "-L" + LIBDIR, "-lspray_rt",
            "-L" + os.path.join(ROOT, "oracle", "_build"), "-loracle",
            "-Wl,-rpath,$ORIGIN/../../../spray_amd/lib:$ORIGIN/../../../oracle/_build",

@@ -577,14 +577,13 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
 // sample are the protocol's (the same winner, shading and occlusion); the
 // film adds with the same atomics; the totals come from the shading
 // counters on the device and go through the transport's all-reduce.
-bool all_local(const spray_rt_insitu* I) {
-  const spray_rt_ctx* c = I->ctx;
-  if (I->world == 1) return true;
-  if (int(c->h_owner.size()) != c->ndom) return false;
-  for (int d = 0; d < c->ndom; ++d)
-    if (c->h_owner[d] != I->rank) return false;
-  return true;
-}
+//
+// Only a one-rank group decides this alone.  With world > 1, a rank that owns
+// every domain cannot tell from its owner map that the others hold no rays:
+// they still route theirs to it through the count exchange, so every rank
+// must run the same collectives (trace) -- a rank-local shortcut there would
+// pair an all-reduce with the others' all-to-all and hang the group.
+bool all_local(const spray_rt_insitu* I) { return I->world == 1; }
 
 int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
                 const int32_t* pixid, const int32_t* samid, size_t n, int spp, float* image,
@@ -767,7 +766,15 @@ int spray_rt_insitu_destroy(spray_rt_insitu_t I) {
 
 int spray_rt_insitu_partition(const float* boxes, int n, const float sb[6], int nranks,
                               int* owner) {
+  return spray_rt_insitu_partition_mode(boxes, n, sb, nranks, SPRAY_RT_PARTITION_GROUP_CLOSE,
+                                        owner);
+}
+
+int spray_rt_insitu_partition_mode(const float* boxes, int n, const float sb[6], int nranks,
+                                   int mode, int* owner) {
   if (!boxes || !sb || !owner || n < 0 || nranks <= 0) return SPRAY_RT_ERR_ARG;
+  if (mode != SPRAY_RT_PARTITION_GROUP_CLOSE && mode != SPRAY_RT_PARTITION_ROUND_ROBIN)
+    return SPRAY_RT_ERR_ARG;
   // scale + offset of the unit-cube transform, evaluated as glm's
   // trans * scale matrix applied to (c, 1): fl(fl(s * c) + off)
   float scale[3], off[3];
@@ -787,6 +794,14 @@ int spray_rt_insitu_partition(const float* boxes, int n, const float sb[6], int 
   }
   // std::sort by code leaves equal codes unordered; the id makes it total
   std::sort(codes.begin(), codes.end());
+  if (mode == SPRAY_RT_PARTITION_ROUND_ROBIN) {  // data_partition.h:139-155
+    int rank = 0;
+    for (const auto& cd : codes) {
+      owner[cd.second] = rank;
+      if (++rank == nranks) rank = 0;
+    }
+    return SPRAY_RT_OK;
+  }
   const int shares = n / nranks;
   int rank = 0, s = 0;
   for (const auto& cd : codes) {

@@ -481,12 +481,6 @@ __device__ __forceinline__ void write_snapshot(uint32_t* live, uint32_t* dshard,
     __hip_atomic_store(S.seq, g | (S.launch + 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void k_ooc_snapshot(uint32_t* __restrict__ live,
-                                                      uint32_t* __restrict__ dshard,
-                                                      OocSnapshot S, int ndom) {
-  write_snapshot(live, dshard, S, ndom);
-}
-
 // Closest hit of the rays queued to up to kOocBatch resident domains in one
 // launch.  Each live (ray, domain) pair walks its domain tree as a packet (a
 // queue holds neighbouring rays) with the ray's current best t as the cut,
@@ -752,7 +746,11 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   k_ooc_chunk_sums<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.sb, g, ndom, q.csum, q.cw);
   k_ooc_chunk_scan<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.csum, g, ndom, q.off);
   k_ooc_first<<<1, 256, 0, s>>>(q.csum, q.cw, int(nch), ndom, q.first, q.live, q.score);
-  if (hipMemsetAsync(q.dshard, 0, 2 * size_t(ndom) * kOocDeadShards * sizeof(uint32_t), s) !=
+  // both shard sets at the drains' stride: the drain kernels index them by
+  // 64 * W queues (the any-hit launches alternate sets 64 * W * shards apart),
+  // not by the scene's ndom -- a set left dirty by a pass's unpublished last
+  // launch would be added into the next pass's snapshots
+  if (hipMemsetAsync(q.dshard, 0, 2 * size_t(64 * W) * kOocDeadShards * sizeof(uint32_t), s) !=
       hipSuccess)
     return hipGetLastError();
   if (W == 1)

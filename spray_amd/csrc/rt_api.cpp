@@ -123,6 +123,48 @@ const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* 
   return nullptr;
 }
 
+int upload_slot_image(spray_rt_ctx* c, int slot, const SlotImage& img, const void* pinned_src,
+                      bool async) {
+  if (slot < 0 || slot > 1 << 20) return fail(c, SPRAY_RT_ERR_ARG, "bad slot %d", slot);
+  if (size_t(slot) >= c->slots.size()) c->slots.resize(slot + 1);
+  SlotHost& sh = c->slots[slot];
+  HIPCHK(c, hipSetDevice(c->device));
+  // the previous image may still be read by queued work
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
+  if (sh.ready) HIPCHK(c, hipEventSynchronize(sh.ready));
+  const size_t total = img.bytes.size();
+  if (sh.bytes < total) {
+    if (sh.dmem) HIPCHK(c, hipFree(sh.dmem));
+    sh.dmem = nullptr;
+    sh.bytes = 0;
+    HIPCHK(c, hipMalloc(&sh.dmem, total));
+    sh.bytes = total;
+  }
+  char* d = static_cast<char*>(sh.dmem);
+  if (async || pinned_src) {  // from pinned memory, completion tracked by an event
+    const void* src = pinned_src;
+    if (!src) {  // staged through the slot's own pinned buffer
+      if (sh.pinned_bytes < total) {
+        if (sh.pinned) HIPCHK(c, hipHostFree(sh.pinned));
+        sh.pinned = nullptr;
+        HIPCHK(c, hipHostMalloc(&sh.pinned, total, hipHostMallocDefault));
+        sh.pinned_bytes = total;
+      }
+      std::memcpy(sh.pinned, img.bytes.data(), total);
+      src = sh.pinned;
+    }
+    if (!sh.ready) HIPCHK(c, hipEventCreateWithFlags(&sh.ready, hipEventDisableTiming));
+    HIPCHK(c, hipMemcpyAsync(d, src, total, hipMemcpyHostToDevice, c->upload_stream));
+    HIPCHK(c, hipEventRecord(sh.ready, c->upload_stream));
+  } else {
+    HIPCHK(c, hipMemcpy(d, img.bytes.data(), total, hipMemcpyHostToDevice));
+  }
+  sh.desc = img.desc_at(d);
+  sh.depth = img.depth;
+  c->slots_dirty = true;
+  return SPRAY_RT_OK;
+}
+
 SlotDesc SlotImage::desc_at(const void* base) const {
   const char* d = static_cast<const char*>(base);
   SlotDesc s{};
@@ -358,39 +400,7 @@ int spray_rt_domain_upload(spray_rt_ctx_t c, int slot, const float* verts,
   SlotImage img;
   if (const char* why = build_slot_image(verts, nverts, faces, nfaces, colors, normals, &img))
     return fail(c, SPRAY_RT_ERR_ARG, "domain upload (slot %d): %s", slot, why);
-  if (size_t(slot) >= c->slots.size()) c->slots.resize(slot + 1);
-  SlotHost& sh = c->slots[slot];
-  HIPCHK(c, hipSetDevice(c->device));
-  // the previous image may still be read by queued work
-  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
-  if (sh.ready) HIPCHK(c, hipEventSynchronize(sh.ready));
-  const size_t total = img.bytes.size();
-  if (sh.bytes < total) {
-    if (sh.dmem) HIPCHK(c, hipFree(sh.dmem));
-    sh.dmem = nullptr;
-    sh.bytes = 0;
-    HIPCHK(c, hipMalloc(&sh.dmem, total));
-    sh.bytes = total;
-  }
-  char* d = static_cast<char*>(sh.dmem);
-  if (async) {  // staged through pinned memory, completion tracked by an event
-    if (sh.pinned_bytes < total) {
-      if (sh.pinned) HIPCHK(c, hipHostFree(sh.pinned));
-      sh.pinned = nullptr;
-      HIPCHK(c, hipHostMalloc(&sh.pinned, total, hipHostMallocDefault));
-      sh.pinned_bytes = total;
-    }
-    std::memcpy(sh.pinned, img.bytes.data(), total);
-    if (!sh.ready) HIPCHK(c, hipEventCreateWithFlags(&sh.ready, hipEventDisableTiming));
-    HIPCHK(c, hipMemcpyAsync(d, sh.pinned, total, hipMemcpyHostToDevice, c->upload_stream));
-    HIPCHK(c, hipEventRecord(sh.ready, c->upload_stream));
-  } else {
-    HIPCHK(c, hipMemcpy(d, img.bytes.data(), total, hipMemcpyHostToDevice));
-  }
-  sh.desc = img.desc_at(d);
-  sh.depth = img.depth;
-  c->slots_dirty = true;
-  return SPRAY_RT_OK;
+  return upload_slot_image(c, slot, img, nullptr, async != 0);
 }
 
 int spray_rt_bvh_build_host(const float* verts, size_t nverts,

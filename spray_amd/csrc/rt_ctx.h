@@ -126,6 +126,14 @@ const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* 
                       size_t nfaces, const uint32_t* colors, const float* normals,
                       SlotImage* out, bool quantized = true);
 
+// Copies a packed image into cache slot `slot` (allocating it), after the
+// queued work that may read the slot's previous image.  From pinned_src
+// (pinned host memory holding img.bytes, kept alive by the caller) or with
+// async = true: an async copy on the upload stream, ordered before the next
+// query by the slot's ready event; else a synchronous copy.
+int upload_slot_image(spray_rt_ctx* c, int slot, const SlotImage& img, const void* pinned_src,
+                      bool async);
+
 // Records a message in the context; returns code.
 int fail(spray_rt_ctx* c, int code, const char* fmt, ...);
 hipStream_t stream_of(spray_rt_ctx* c);

@@ -265,7 +265,10 @@ hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
 // Miss records of the rays no batch hit (after the last closest-hit batch).
 hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* hits, size_t M);
 // Any hit of a batch; the pairs of newly occluded rays are counted off
-// q.live; the snapshot follows.  done: a device counter, 0 between launches.
+// q.live.  Launch k adds its deaths to shard set k & 1 of q.dshard (sets
+// 64 * W * kOocDeadShards words apart); its block 0 publishes launch k - 1's
+// set (complete at the kernel boundary) as snapshot k - 1.  The pass's last
+// launch is not published; launch_ooc_queues clears both sets.
 // coherence: SPRAY_RT_RAYS_* (the walk form, as the scene path's any hit)
 hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
                                const OocScratch& q, uint8_t* occ, OocSnapshot snap,

@@ -1,6 +1,7 @@
 // scene_host.cpp -- scene files, PLY meshes, domain cache and the GpuScene
 // adapter (see scene_host.h), plus a C ABI (spray_scene_*) for bindings.
 #include "scene_host.h"
+#include "rt_ctx.h"
 #include "spray_scene.h"
 
 #include <hip/hip_runtime.h>
@@ -12,7 +13,7 @@
 #include <fstream>
 #include <sstream>
 
-namespace spray_amd {
+namespace spray_host {
 
 // ---------------------------------------------------------------------------
 // column-major 4x4 helpers (glm 0.9.8 operand order)
@@ -484,6 +485,8 @@ bool DomainCache::load(int domid, int* block) {
 // ---------------------------------------------------------------------------
 GpuScene::~GpuScene() {
   if (rt_) spray_rt_destroy(rt_);
+  for (void* p : pinned_)
+    if (p) (void)hipHostFree(p);
 }
 
 int GpuScene::fail(int code, const std::string& msg) {
@@ -525,25 +528,43 @@ int GpuScene::init(const std::string& desc, const std::string& ply_path,
   return SPRAY_RT_OK;
 }
 
+// A cache miss uploads the domain's device image.  TriMeshBuffer::load
+// (trimesh_buffer.cc:117-169) re-reads, transforms and rebuilds on every
+// miss; the image is a pure function of the domain, so it is built on the
+// first load only and kept in pinned host memory -- a later miss is one
+// async DMA (the bytes, hence every result, are the same).
 int GpuScene::upload(int id, int block) {
-  const Domain& d = domains_[id];
-  auto it = ply_cache_.find(d.filename);
-  if (it == ply_cache_.end()) {
-    Mesh m;
-    std::string e;
-    if (!load_ply(d.filename, &m, &e)) return fail(SPRAY_RT_ERR_ARG, e);
-    it = ply_cache_.emplace(d.filename, std::move(m)).first;
+  if (images_.size() != domains_.size()) {
+    images_.resize(domains_.size());
+    pinned_.assign(domains_.size(), nullptr);
   }
-  Mesh mesh = it->second;  // world-space copy
-  float ident[16];
-  mat_identity(ident);
-  if (std::memcmp(ident, d.transform, sizeof(ident)) != 0)
-    transform_vertices(d.transform, mesh.vertices.data(), mesh.vertices.size() / 3);
-  compute_normals(&mesh);
-  int r = spray_rt_domain_upload(rt_, block, mesh.vertices.data(),
-                                 mesh.vertices.size() / 3, mesh.faces.data(),
-                                 mesh.faces.size() / 3, mesh.colors.data(),
-                                 mesh.normals.data(), 0);
+  spray_rt::detail::SlotImage& img = images_[size_t(id)];
+  if (!pinned_[size_t(id)]) {
+    const Domain& d = domains_[id];
+    auto it = ply_cache_.find(d.filename);
+    if (it == ply_cache_.end()) {
+      Mesh m;
+      std::string e;
+      if (!load_ply(d.filename, &m, &e)) return fail(SPRAY_RT_ERR_ARG, e);
+      it = ply_cache_.emplace(d.filename, std::move(m)).first;
+    }
+    Mesh mesh = it->second;  // world-space copy
+    float ident[16];
+    mat_identity(ident);
+    if (std::memcmp(ident, d.transform, sizeof(ident)) != 0)
+      transform_vertices(d.transform, mesh.vertices.data(), mesh.vertices.size() / 3);
+    compute_normals(&mesh);
+    if (const char* why = spray_rt::detail::build_slot_image(
+            mesh.vertices.data(), mesh.vertices.size() / 3, mesh.faces.data(),
+            mesh.faces.size() / 3, mesh.colors.data(), mesh.normals.data(), &img))
+      return fail(SPRAY_RT_ERR_ARG, std::string("domain ") + std::to_string(id) + ": " + why);
+    void* p = nullptr;
+    if (hipHostMalloc(&p, img.bytes.size(), hipHostMallocDefault) != hipSuccess)
+      return fail(SPRAY_RT_ERR_NOMEM, "pinned host memory for a domain image");
+    std::memcpy(p, img.bytes.data(), img.bytes.size());
+    pinned_[size_t(id)] = p;
+  }
+  int r = spray_rt::detail::upload_slot_image(rt_, block, img, pinned_[size_t(id)], true);
   if (r) return fail(r, spray_rt_last_error(rt_));
   // keep the scene path's domain -> slot map in step with the cache
   if (block_domain_[block] >= 0)
@@ -609,12 +630,12 @@ int GpuScene::occluded1M(int block, spray_rt_ray_intersection* rays, size_t n) {
   return spray_rt_occluded1M(rt_, block, rays, n, sizeof(*rays));
 }
 
-}  // namespace spray_amd
+}  // namespace spray_host
 
 // ---------------------------------------------------------------------------
 // C ABI for bindings (include/spray_scene.h)
 // ---------------------------------------------------------------------------
-using spray_amd::GpuScene;
+using spray_host::GpuScene;
 
 extern "C" {
 
@@ -682,7 +703,7 @@ int spray_scene_light(spray_scene_t h, int i, float* out7) {
 
 int spray_scene_load(spray_scene_t h, int id, int* cache_block) {
   GpuScene* s = reinterpret_cast<GpuScene*>(h);
-  spray_amd::SceneInfo si;
+  spray_host::SceneInfo si;
   int r = s->load(id, &si);
   if (!r && cache_block) *cache_block = si.cache_block;
   return r;
@@ -690,21 +711,21 @@ int spray_scene_load(spray_scene_t h, int id, int* cache_block) {
 
 int spray_scene_intersect1(spray_scene_t h, int cache_block, const float* org,
                            const float* dir, spray_rt_ray_intersection* isect) {
-  spray_amd::SceneInfo si;
+  spray_host::SceneInfo si;
   si.cache_block = cache_block;
   return reinterpret_cast<GpuScene*>(h)->intersect(si, org, dir, isect) ? 1 : 0;
 }
 
 int spray_scene_occluded1(spray_scene_t h, int cache_block, const float* org,
                           const float* dir, spray_rt_ray_intersection* ray) {
-  spray_amd::SceneInfo si;
+  spray_host::SceneInfo si;
   si.cache_block = cache_block;
   return reinterpret_cast<GpuScene*>(h)->occluded(si, org, dir, ray) ? 1 : 0;
 }
 
 int spray_camera_init(const float* pos, const float* lookat, const float* up,
                       float vfov, int w, int h, float* cam14) {
-  spray_amd::camera_init(pos, lookat, up, vfov, w, h, cam14);
+  spray_host::camera_init(pos, lookat, up, vfov, w, h, cam14);
   return SPRAY_RT_OK;
 }
 
@@ -714,18 +735,18 @@ int spray_scene_domain_mesh(spray_scene_t h, int id, size_t* nverts,
                             size_t* nfaces, float* verts, uint32_t* faces,
                             uint32_t* colors, float* normals);
 
-static int prep_mesh(const spray_amd::Domain& d, spray_amd::Mesh* m) {
+static int prep_mesh(const spray_host::Domain& d, spray_host::Mesh* m) {
   std::string e;
-  if (!spray_amd::load_ply(d.filename, m, &e)) return SPRAY_RT_ERR_ARG;
+  if (!spray_host::load_ply(d.filename, m, &e)) return SPRAY_RT_ERR_ARG;
   float ident[16];
   for (int i = 0; i < 16; ++i) ident[i] = (i % 5 == 0) ? 1.0f : 0.0f;
   if (std::memcmp(ident, d.transform, sizeof(ident)) != 0)
-    spray_amd::transform_vertices(d.transform, m->vertices.data(), m->vertices.size() / 3);
-  spray_amd::compute_normals(m);
+    spray_host::transform_vertices(d.transform, m->vertices.data(), m->vertices.size() / 3);
+  spray_host::compute_normals(m);
   return SPRAY_RT_OK;
 }
 
-static void copy_mesh(const spray_amd::Mesh& m, size_t* nverts, size_t* nfaces,
+static void copy_mesh(const spray_host::Mesh& m, size_t* nverts, size_t* nfaces,
                       float* verts, uint32_t* faces, uint32_t* colors,
                       float* normals) {
   *nverts = m.vertices.size() / 3;
@@ -741,10 +762,10 @@ int spray_host_parse_scene(const char* desc, const char* ply_path,
                            float* transforms, float* lights, char* err,
                            size_t errlen) {
   if (!desc) return SPRAY_RT_ERR_ARG;
-  std::vector<spray_amd::Domain> doms;
-  std::vector<spray_amd::Light> ls;
+  std::vector<spray_host::Domain> doms;
+  std::vector<spray_host::Light> ls;
   std::string e;
-  if (!spray_amd::load_scene_file(desc, ply_path ? ply_path : "", &doms, &ls, &e)) {
+  if (!spray_host::load_scene_file(desc, ply_path ? ply_path : "", &doms, &ls, &e)) {
     if (err && errlen) std::snprintf(err, errlen, "%s", e.c_str());
     return SPRAY_RT_ERR_ARG;
   }
@@ -766,10 +787,10 @@ int spray_host_parse_scene(const char* desc, const char* ply_path,
 int spray_host_scene_bsdfs(const char* desc, int* ndomains, spray_rt_bsdf* bsdfs, char* err,
                            size_t errlen) {
   if (!desc || !ndomains) return SPRAY_RT_ERR_ARG;
-  std::vector<spray_amd::Domain> doms;
-  std::vector<spray_amd::Light> ls;
+  std::vector<spray_host::Domain> doms;
+  std::vector<spray_host::Light> ls;
   std::string e;
-  if (!spray_amd::load_scene_file(desc, "", &doms, &ls, &e)) {
+  if (!spray_host::load_scene_file(desc, "", &doms, &ls, &e)) {
     if (err && errlen) std::snprintf(err, errlen, "%s", e.c_str());
     return SPRAY_RT_ERR_ARG;
   }
@@ -802,14 +823,14 @@ int spray_host_scene_bsdfs(const char* desc, int* ndomains, spray_rt_bsdf* bsdfs
 int spray_host_domain_mesh(const char* desc, const char* ply_path, int id,
                            size_t* nverts, size_t* nfaces, float* verts,
                            uint32_t* faces, uint32_t* colors, float* normals) {
-  std::vector<spray_amd::Domain> doms;
-  std::vector<spray_amd::Light> ls;
+  std::vector<spray_host::Domain> doms;
+  std::vector<spray_host::Light> ls;
   std::string e;
   if (!desc || !nverts || !nfaces ||
-      !spray_amd::load_scene_file(desc, ply_path ? ply_path : "", &doms, &ls, &e))
+      !spray_host::load_scene_file(desc, ply_path ? ply_path : "", &doms, &ls, &e))
     return SPRAY_RT_ERR_ARG;
   if (id < 0 || size_t(id) >= doms.size()) return SPRAY_RT_ERR_ARG;
-  spray_amd::Mesh m;
+  spray_host::Mesh m;
   int r = prep_mesh(doms[id], &m);
   if (r) return r;
   copy_mesh(m, nverts, nfaces, verts, faces, colors, normals);
@@ -822,7 +843,7 @@ int spray_scene_domain_mesh(spray_scene_t h, int id, size_t* nverts,
   GpuScene* s = reinterpret_cast<GpuScene*>(h);
   if (!s || id < 0 || size_t(id) >= s->getNumDomains() || !nverts || !nfaces)
     return SPRAY_RT_ERR_ARG;
-  spray_amd::Mesh m;
+  spray_host::Mesh m;
   int r = prep_mesh(s->getDomains()[id], &m);
   if (r) return r;
   copy_mesh(m, nverts, nfaces, verts, faces, colors, normals);

@@ -20,7 +20,13 @@
 
 #include "spray_rt.h"
 
-namespace spray_amd {
+namespace spray_rt {
+namespace detail {
+struct SlotImage;
+}
+}  // namespace spray_rt
+
+namespace spray_host {
 
 struct Domain {  // src/render/domain.h:32-44
   int id = 0;
@@ -130,8 +136,11 @@ class GpuScene {
   DomainCache cache_;
   std::vector<int> block_domain_;  // cache block -> resident domain
   std::map<std::string, Mesh> ply_cache_;  // parsed PLY by filename
+  // per-domain device images, built on the first load (upload())
+  std::vector<spray_rt::detail::SlotImage> images_;
+  std::vector<void*> pinned_;  // their bytes in pinned host memory
   spray_rt_ctx_t rt_ = nullptr;
   std::string err_;
 };
 
-}  // namespace spray_amd
+}  // namespace spray_host

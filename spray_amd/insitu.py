@@ -29,23 +29,30 @@ import numpy as np
 
 from ._native import SprayRtError, lib
 
-__all__ = ["morton_partition", "horizontal_stripe", "setup_rank_context", "InsituEngine",
+__all__ = ["morton_partition", "PARTITION_GROUP_CLOSE", "PARTITION_ROUND_ROBIN", "horizontal_stripe", "setup_rank_context", "InsituEngine",
            "InsituRecords", "MISS_KEY"]
 
 MISS_KEY = 0x7FFFFFFFFFFFFFFF
 
 
-def morton_partition(boxes, scene_bound, nranks):
-    """Owner rank per domain (InsituPartition::partition, GROUP_CLOSE_DOMAINS):
-    spray_rt_insitu_partition.  boxes [n, 6] (lo, hi) world bounds in
+PARTITION_GROUP_CLOSE = 0
+PARTITION_ROUND_ROBIN = 1
+
+
+def morton_partition(boxes, scene_bound, nranks, mode=PARTITION_GROUP_CLOSE):
+    """Owner rank per domain (InsituPartition::partition,
+    src/render/data_partition.h:59-155): spray_rt_insitu_partition_mode.
+    mode GROUP_CLOSE (contiguous shares of the sorted Morton order, the
+    reference's compiled mode) or ROUND_ROBIN (the sorted order dealt out one
+    domain per rank in turn).  boxes [n, 6] (lo, hi) world bounds in
     domain-id order, scene_bound [6]."""
     b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
     sb = np.ascontiguousarray(scene_bound, np.float32).reshape(6)
     if nranks <= 0:
         raise ValueError("nranks must be > 0")
     owner = np.zeros(len(b), np.int32)
-    rc = lib().spray_rt_insitu_partition(b.ctypes.data, len(b), sb.ctypes.data, int(nranks),
-                                         owner.ctypes.data)
+    rc = lib().spray_rt_insitu_partition_mode(b.ctypes.data, len(b), sb.ctypes.data,
+                                              int(nranks), int(mode), owner.ctypes.data)
     if rc != 0:
         raise SprayRtError("insitu_partition failed (%d)" % rc)
     return owner

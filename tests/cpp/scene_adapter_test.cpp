@@ -37,9 +37,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <vector>
 
+#include "ref_mock.h"
 #include "spray_scene.hpp"
 
 extern "C" {
@@ -114,8 +117,8 @@ struct Meshes {  // per-domain oracle data (TriMeshBuffer::load through the host
   }
 };
 
-void load_meshes(const char* desc, const char* ply, const spray_amd::Scene<>& scene, Meshes* m,
-                 bool bvh) {
+template <typename SceneT>
+void load_meshes(const char* desc, const char* ply, const SceneT& scene, Meshes* m, bool bvh) {
   const int nd = int(scene.getNumDomains());
   m->tri.resize(nd);
   m->verts.resize(nd);
@@ -136,7 +139,11 @@ void load_meshes(const char* desc, const char* ply, const spray_amd::Scene<>& sc
     m->tri[d].resize(12 * nf);
     or_prep_tris(m->verts[d].data(), m->faces[d].data(), nf, m->tri[d].data());
     if (bvh) m->bvh[d] = or_bvh_build(m->verts[d].data(), m->faces[d].data(), nf);
-    std::memcpy(&m->boxes[6 * size_t(d)], scene.getDomains()[size_t(d)].world_aabb, 24);
+    const auto& a = scene.getDomains()[size_t(d)].world_aabb;
+    for (int k = 0; k < 3; ++k) {
+      m->boxes[6 * size_t(d) + size_t(k)] = a.bounds[0][k];
+      m->boxes[6 * size_t(d) + 3 + size_t(k)] = a.bounds[1][k];
+    }
   }
 }
 
@@ -397,6 +404,42 @@ int run_batched(const char* desc, const char* ply, int T, int cache, int img) {
     }
   const double rate = double(npair.load() + nshadow.load()) / dt / 1e6;
 
+  // the CPU baseline of the same drain: the oracle's canonical BVH (C,
+  // OpenMP over T threads) on every queue's rays and the shadow rays of its
+  // hits, gathers included -- the reference's Embree drain, restated
+  long cpu_rays = 0;
+  double cpu_s = 0.0;
+  {
+    omp_set_num_threads(T);
+    const double c0 = now();
+    for (int id = 0; id < nd; ++id) {
+      const size_t k = queue[id].size();
+      if (!k) continue;
+      std::vector<float> o(3 * k), d(3 * k), t(k), u(k), v(k);
+      std::vector<uint32_t> p(k);
+      for (size_t j = 0; j < k; ++j) {
+        std::memcpy(&o[3 * j], &org[3 * queue[id][j]], 12);
+        std::memcpy(&d[3 * j], &dir[3 * queue[id][j]], 12);
+      }
+      or_bvh_intersect(m.bvh[id], o.data(), d.data(), nullptr, nullptr, k, t.data(), u.data(),
+                       v.data(), p.data(), nullptr);
+      std::vector<float> so, sd;
+      for (size_t j = 0; j < k; ++j) {
+        if (p[j] == 0xFFFFFFFFu) continue;
+        float ps[3], wi[3];
+        shadow_ray(&o[3 * j], &d[3 * j], t[j], ps, wi);
+        so.insert(so.end(), ps, ps + 3);
+        sd.insert(sd.end(), wi, wi + 3);
+      }
+      std::vector<uint8_t> oo(so.size() / 3 + 1);
+      if (!so.empty())
+        or_bvh_occluded(m.bvh[id], so.data(), sd.data(), nullptr, nullptr, so.size() / 3,
+                        oo.data(), nullptr);
+      cpu_rays += long(k + so.size() / 3);
+    }
+    cpu_s = now() - c0;
+  }
+
   // the per-ray form on the first queues (same calls as mode "single"), timed
   long single_rays = 0;
   double single_s = 0.0;
@@ -416,10 +459,265 @@ int run_batched(const char* desc, const char* ply, int T, int cache, int img) {
   }
   std::printf("mode batched threads %d cache %d rays %zu pairs %ld shadow %ld calls %ld "
               "drain_s %.4f batched_Mrays_s %.2f per_ray_Mrays_s %.3f (%ld rays) "
+              "oracle_Mrays_s %.2f (%d threads) "
               "domain-list mismatches %ld hits %ld occluded %ld mismatches %ld\n",
               T, cache, n, npair.load(), nshadow.load(), ncalls.load(), dt, rate,
-              single_rays / single_s / 1e6, single_rays, bad_lists, nhit, nocc, bad);
+              single_rays / single_s / 1e6, single_rays, cpu_rays / cpu_s / 1e6, T, bad_lists,
+              nhit, nocc, bad);
   if (bad || bad_lists || nhit < 1000 || nocc == 0 || nocc == nhit) {
+    std::printf("FAIL\n");
+    return 1;
+  }
+  std::printf("ok\n");
+  return 0;
+}
+
+// the scene file's lights, read independently of the engine (the checker's
+// view; SceneLoader::parseLight, scene_loader.cc:205-231)
+std::vector<or_light> read_lights(const char* desc) {
+  std::vector<or_light> out;
+  std::ifstream in(desc);
+  std::string line;
+  while (std::getline(in, line)) {
+    std::istringstream ss(line);
+    std::string tag, kind;
+    if (!(ss >> tag) || tag != "light" || !(ss >> kind)) continue;
+    or_light L{};
+    if (kind == "point") {
+      L.type = OR_LIGHT_POINT;
+      ss >> L.pos[0] >> L.pos[1] >> L.pos[2];
+    } else {
+      L.type = OR_LIGHT_HEMISPHERE;
+    }
+    ss >> L.radiance[0] >> L.radiance[1] >> L.radiance[2];
+    out.push_back(L);
+  }
+  return out;
+}
+
+bool same_vec(const float* a, const float* b) { return std::memcmp(a, b, 12) == 0; }
+
+// mode "shade": the reference's application types through the adapter
+// (spray_amd::Scene<spray::RefTypes>, tests/cpp/ref_mock.h): getBound() as
+// the app's Aabb, buildWbvh(), the in-situ partition's getDomains(rank),
+// getLights() as std::vector<Light*> and getBsdf(id) as const Bsdf*, used by
+// a ShaderPt written with the reference's expressions inside the batched
+// drain -- every shadow and continuation ray it spawns checked bit for bit
+// against the oracle's ShaderPt (or_shade), every shadow's occlusion against
+// the oracle's BVH.
+int run_shade(const char* desc, const char* ply, int T, int cache, int img) {
+  typedef spray_amd::Scene<spray::RefTypes> SceneT;
+  SceneT scene;
+  const int kRanks = 4;
+  scene.init(desc, ply, "", cache, 0, true, kRanks);
+  scene.buildWbvh();  // SprayRenderer::init (spray_renderer.inl:47)
+  const int nd = int(scene.getNumDomains());
+  long bad = 0;
+
+  // getBound (spray_renderer.inl:96): the app's Aabb, the union of the boxes
+  spray::Aabb aabb = scene.getBound();
+  for (int k = 0; k < 3; ++k) {
+    float lo = INFINITY, hi = -INFINITY;
+    for (const auto& d : scene.getDomains()) {
+      lo = std::min(lo, d.world_aabb.bounds[0][k]);
+      hi = std::max(hi, d.world_aabb.bounds[1][k]);
+    }
+    if (!same(aabb.bounds[0][k], lo) || !same(aabb.bounds[1][k], hi)) ++bad;
+  }
+  // the in-situ contexts' view of the partition (insitu_tcontext.inl:98)
+  const spray_amd::InsituPartition* partition_ = &scene.getInsituPartition();
+  std::vector<float> boxes(6 * size_t(nd));
+  for (int d = 0; d < nd; ++d)
+    for (int k = 0; k < 3; ++k) {
+      boxes[6 * size_t(d) + size_t(k)] = scene.getDomains()[size_t(d)].world_aabb.bounds[0][k];
+      boxes[6 * size_t(d) + 3 + size_t(k)] = scene.getDomains()[size_t(d)].world_aabb.bounds[1][k];
+    }
+  std::vector<int> owner(static_cast<size_t>(nd));
+  const float bnd[6] = {aabb.bounds[0].x, aabb.bounds[0].y, aabb.bounds[0].z,
+                        aabb.bounds[1].x, aabb.bounds[1].y, aabb.bounds[1].z};
+  spray_rt_insitu_partition(boxes.data(), nd, bnd, kRanks, owner.data());
+  int listed = 0;
+  for (int rank = 0; rank < kRanks; ++rank) {
+    const auto& ids = partition_->getDomains(rank);
+    for (int id : ids) {
+      ++listed;
+      if (partition_->rank(id) != rank || owner[size_t(id)] != rank) ++bad;
+    }
+  }
+  if (listed != nd || partition_->getNumDomains() != nd) ++bad;
+
+  // lights and materials as the app's own classes
+  const std::vector<or_light> ref_lights = read_lights(desc);
+  std::vector<spray::Light*> lights_ = scene.getLights();
+  if (lights_.size() != ref_lights.size()) ++bad;
+  for (size_t l = 0; l < lights_.size() && l < ref_lights.size(); ++l)
+    if (lights_[l]->isAreaLight() != (ref_lights[l].type == OR_LIGHT_HEMISPHERE)) ++bad;
+  for (int d = 0; d < nd; ++d) {
+    const spray::Bsdf* b = scene.getBsdf(d);
+    if (!b || b->isDelta() || !dynamic_cast<const spray::DiffuseBsdf*>(b)) ++bad;
+  }
+  const long bad_scene = bad;
+
+  spray::ooc::ShaderPt<SceneT>::Config cfg{2, 2, glm::vec3(0.4f, 0.4f, 0.4f), 10.0f};
+  spray::ooc::ShaderPt<SceneT> shader;
+  shader.init(cfg, &scene);
+  or_shader P{};
+  P.shader = OR_SHADER_PT;
+  P.bounces = cfg.bounces;
+  P.samples = cfg.ao_samples;
+  P.nlights = int(ref_lights.size());
+  for (int k = 0; k < 3; ++k) P.ks[k] = cfg.ks[k];
+  P.shininess = cfg.shininess;
+  for (size_t l = 0; l < ref_lights.size() && l < OR_MAX_LIGHTS; ++l) P.lights[l] = ref_lights[l];
+  const int ns = or_shadow_slots(&P);
+
+  // camera at the scene, image x image rays at 1 spp
+  float c[3], e[3];
+  for (int k = 0; k < 3; ++k) {
+    c[k] = (aabb.bounds[0][k] + aabb.bounds[1][k]) * 0.5f;
+    e[k] = aabb.bounds[1][k] - aabb.bounds[0][k];
+  }
+  const float pos[3] = {c[0] + 1.1f * e[0], c[1] + 0.9f * e[1], c[2] + 1.2f * e[2]};
+  const float up[3] = {0.f, 1.f, 0.f};
+  float cam[14];
+  or_camera_init(pos, c, up, 60.f, img, img, cam);
+  const size_t n = size_t(img) * size_t(img);
+  std::vector<float> org(3 * n), dir(3 * n);
+  std::vector<int32_t> pix(n), sam(n);
+  or_eye_rays_ooc(cam, img, 1, 0, 0, img, img, org.data(), dir.data(), pix.data(), sam.data());
+  Meshes m;
+  load_meshes(desc, ply, scene, &m, true);
+  std::vector<int32_t> ids(n * size_t(nd)), cnt(n);
+  std::vector<float> ts(n * size_t(nd));
+  scene.intersectDomains1M(org.data(), dir.data(), n, ids.data(), ts.data(), cnt.data(), nd);
+  std::vector<std::vector<long>> queue(nd);
+  for (size_t i = 0; i < n; ++i)
+    for (int k = 0; k < cnt[i]; ++k) queue[ids[i * nd + k]].push_back(long(i));
+
+  struct Part {
+    std::vector<long> rays;
+    std::vector<RTCRayIntersection> isect;
+    std::vector<spray::ooc::Ray> shadows, next;
+    std::vector<int> nshadow, nnext;  // per hit, in queue order
+    std::vector<RTCRay> srays;
+  };
+  std::vector<std::vector<Part>> parts(nd, std::vector<Part>(T));
+  spray_amd::SceneInfo sinfo;
+#pragma omp parallel num_threads(T)
+  {
+    const int me = omp_get_thread_num();
+    for (int id = 0; id < nd; ++id) {
+#pragma omp single
+      scene.load(id, &sinfo);
+      const long qn = long(queue[id].size());
+      const long b = qn * me / T, e2 = qn * (me + 1) / T;
+      Part& Q = parts[id][me];
+      if (e2 > b) {
+        Q.rays.assign(queue[id].begin() + b, queue[id].begin() + e2);
+        Q.isect.resize(Q.rays.size());
+        for (size_t k = 0; k < Q.rays.size(); ++k)
+          SceneT::makeRay(&org[3 * Q.rays[k]], &dir[3 * Q.rays[k]], &Q.isect[k]);
+        scene.intersect1M(sinfo, Q.isect.data(), Q.isect.size());
+        for (size_t k = 0; k < Q.rays.size(); ++k) {  // procRads: shade every hit
+          const RTCRayIntersection& r = Q.isect[k];
+          if (r.geomID == SPRAY_RT_INVALID_ID) continue;
+          spray::ooc::Ray rin{};
+          std::memcpy(rin.org, &org[3 * Q.rays[k]], 12);
+          std::memcpy(rin.dir, &dir[3 * Q.rays[k]], 12);
+          rin.w[0] = rin.w[1] = rin.w[2] = 1.0f;
+          rin.pixid = pix[size_t(Q.rays[k])];
+          rin.samid = sam[size_t(Q.rays[k])];
+          const size_t s0 = Q.shadows.size(), n0 = Q.next.size();
+          shader(id, rin, r, &Q.shadows, &Q.next, 0);
+          Q.nshadow.push_back(int(Q.shadows.size() - s0));
+          Q.nnext.push_back(int(Q.next.size() - n0));
+        }
+        Q.srays.resize(Q.shadows.size());
+        for (size_t k = 0; k < Q.shadows.size(); ++k)
+          SceneT::makeRay(Q.shadows[k].org, Q.shadows[k].dir, &Q.srays[k]);
+        if (!Q.srays.empty()) scene.occluded1M(sinfo, Q.srays.data(), Q.srays.size());
+      }
+#pragma omp barrier
+    }
+  }
+
+  // checks: the oracle's ShaderPt over the same hit records, per part
+  long nhit = 0, nshadow = 0, nnext = 0, nocc = 0;
+  for (int id = 0; id < nd; ++id)
+    for (int th = 0; th < T; ++th) {
+      const Part& Q = parts[id][size_t(th)];
+      std::vector<float> o, d, w;
+      std::vector<or_hit> h;
+      std::vector<int32_t> hp, hs;
+      for (size_t k = 0; k < Q.rays.size(); ++k) {
+        const RTCRayIntersection& r = Q.isect[k];
+        if (r.geomID == SPRAY_RT_INVALID_ID) continue;
+        or_hit x{};
+        x.t = r.tfar;
+        x.u = r.u;
+        x.v = r.v;
+        x.prim = r.primID;
+        std::memcpy(x.ng, r.Ng, 12);
+        x.color = r.color;
+        std::memcpy(x.ns, r.Ns, 12);
+        x.domain = id;
+        h.push_back(x);
+        o.insert(o.end(), &org[3 * Q.rays[k]], &org[3 * Q.rays[k]] + 3);
+        d.insert(d.end(), &dir[3 * Q.rays[k]], &dir[3 * Q.rays[k]] + 3);
+        hp.push_back(pix[size_t(Q.rays[k])]);
+        hs.push_back(sam[size_t(Q.rays[k])]);
+      }
+      const size_t nh = h.size();
+      if (nh != Q.nshadow.size()) {
+        ++bad;
+        continue;
+      }
+      if (!nh) continue;
+      w.assign(3 * nh, 1.0f);
+      std::vector<uint8_t> valid(nh, 1), svalid(nh * size_t(ns));
+      std::vector<float> so(3 * nh * size_t(ns)), sd(so.size()), sw(so.size());
+      if (or_shade(&P, nullptr, 0, 0, o.data(), d.data(), h.data(), w.data(), valid.data(),
+                   hp.data(), hs.data(), nh, so.data(), sd.data(), sw.data(), svalid.data()))
+        ++bad;
+      size_t sj = 0, nj = 0;
+      for (size_t j = 0; j < nh; ++j) {
+        ++nhit;
+        int got = 0;
+        for (int k = 0; k < ns; ++k) {
+          const size_t slot = j * size_t(ns) + size_t(k);
+          if (!svalid[slot]) continue;
+          ++got;
+          if (sj >= Q.shadows.size()) {
+            ++bad;
+            continue;
+          }
+          const spray::ooc::Ray& sh = Q.shadows[sj];
+          if (!same_vec(sh.org, &so[3 * slot]) || !same_vec(sh.dir, &sd[3 * slot]) ||
+              !same_vec(sh.w, &sw[3 * slot]))
+            ++bad;
+          uint8_t oo;
+          or_bvh_occluded(m.bvh[id], sh.org, sh.dir, nullptr, nullptr, 1, &oo, nullptr);
+          const bool occ = Q.srays[sj].geomID != SPRAY_RT_INVALID_ID;
+          if (occ != (oo != 0) || (occ && Q.srays[sj].geomID != 0)) ++bad;
+          if (occ) ++nocc;
+          ++sj;
+          ++nshadow;
+        }
+        if (got != Q.nshadow[j]) ++bad;
+        if (int(valid[j]) != Q.nnext[j]) ++bad;
+        if (valid[j]) {
+          const spray::ooc::Ray& nx = Q.next[nj++];
+          if (!same_vec(nx.org, &o[3 * j]) || !same_vec(nx.dir, &d[3 * j]) ||
+              !same_vec(nx.w, &w[3 * j]) || nx.depth != 1)
+            ++bad;
+          ++nnext;
+        }
+      }
+    }
+  std::printf("mode shade threads %d cache %d rays %zu lights %zu scene-interface mismatches %ld "
+              "hits %ld shadows %ld next %ld occluded %ld mismatches %ld\n",
+              T, cache, n, lights_.size(), bad_scene, nhit, nshadow, nnext, nocc, bad);
+  if (bad || nhit < 500 || nshadow < 500 || nnext < 500 || nocc == 0) {
     std::printf("FAIL\n");
     return 1;
   }
@@ -432,7 +730,7 @@ int run_batched(const char* desc, const char* ply, int T, int cache, int img) {
 int main(int argc, char** argv) {
   if (argc < 5) {
     std::fprintf(stderr,
-                 "usage: %s scene.spray ply_path threads cache_size [single|current|batched] "
+                 "usage: %s scene.spray ply_path threads cache_size [single|current|batched|shade] "
                  "[image]\n",
                  argv[0]);
     return 2;
@@ -442,6 +740,8 @@ int main(int argc, char** argv) {
   try {
     if (mode == "batched") return run_batched(argv[1], argv[2], T, cache,
                                               argc > 6 ? std::atoi(argv[6]) : 512);
+    if (mode == "shade") return run_shade(argv[1], argv[2], T, cache,
+                                          argc > 6 ? std::atoi(argv[6]) : 256);
     return run_single(argv[1], argv[2], T, cache, mode == "current");
   } catch (const std::exception& e) {
     std::printf("FAIL exception: %s\n", e.what());

@@ -99,8 +99,9 @@ CASES = {  # name: (shader kind, bounces, samples, image size, spp)
 LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)]}
 
 
-def _engine_rank(rank, world, case, transport, dist=None):
-    """One rank's engine frame of CASES[case]: returns (records, totals, image)."""
+def _engine_rank(rank, world, case, transport, dist=None, one_owner=False):
+    """One rank's engine frame of CASES[case]: returns (records, totals, image).
+    one_owner: the last rank owns every domain (the others hold rays only)."""
     import spray_amd
     from spray_amd import insitu
     from oracle import pyoracle as po
@@ -108,6 +109,8 @@ def _engine_rank(rank, world, case, transport, dist=None):
     kind, bounces, samples, img, spp = CASES[case]
     boxes, bound = scene_boxes()
     owner = insitu.morton_partition(boxes, bound, world)
+    if one_owner:
+        owner = np.full_like(owner, world - 1)
     rt = spray_amd.RtContext(0)
     insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
     rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
@@ -200,7 +203,7 @@ def test_engine_one_rank_protocol_forced(oracle, monkeypatch):
     assert res[3]["exchanges"] > 0
 
 
-def _gpu_rank_main(rank, world, port, out, case):
+def _gpu_rank_main(rank, world, port, out, case, one_owner=False):
     import pickle
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -210,7 +213,7 @@ def _gpu_rank_main(rank, world, port, out, case):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _engine_rank(rank, world, case, "host", dist)
+        res = _engine_rank(rank, world, case, "host", dist, one_owner)
         with open(os.path.join(out, "r%d.pkl" % rank), "wb") as fh:
             pickle.dump(res, fh)
     finally:
@@ -235,6 +238,24 @@ def test_engine_ranks_on_gpu(oracle, world, case):
     _check(oracle, case, res)
     assert sum(len(r[0]["samid"]) > 50 for r in res) >= max(2, world // 2)
     assert all(r[3]["bytes_sent"] > 0 for r in res if len(r[0]["samid"]))
+
+
+def test_engine_two_ranks_one_owner(oracle):
+    """world 2, every domain on rank 1: rank 0 holds rays and no domain, rank
+    1 owns everything -- both must run the same collectives (the exchange;
+    no rank-local all-local shortcut at world > 1) and rank 0's
+    rays must reach rank 1."""
+    import pickle
+    with tempfile.TemporaryDirectory() as out:
+        torch.multiprocessing.spawn(_gpu_rank_main,
+                                    args=(2, _free_port(), out, "pt1", True), nprocs=2)
+        res = []
+        for r in range(2):
+            with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
+                res.append(pickle.load(fh))
+    _check(oracle, "pt1", res)
+    assert len(res[0][0]["samid"]) == 0 and len(res[1][0]["samid"]) > 50
+    assert res[0][3]["bytes_sent"] > 0
 
 
 def test_domain_mask_exact_on_box_boundaries(spray, oracle):

@@ -138,3 +138,52 @@ def test_cross_domain_tie_goes_to_earlier_list_entry(spray, oracle):
     assert ((k[hit] & 0xFFFF) == 0).all() and ((k[hit] >> 16 & 0xFFFF) == 0).all()
     oc.close()
     rt.close()
+
+
+def _subscene(tmp_path, ndom):
+    """The first ndom domains of wavelets64 as a scene file of their own."""
+    text = open(WAVELETS64).read()
+    head, *blocks = text.split("\ndomain\n")
+    path = tmp_path / ("wavelets%d.spray" % ndom)
+    path.write_text("\ndomain\n".join([head] + blocks[:ndom]))
+    return str(path)
+
+
+@pytest.mark.parametrize("ndom,slots", [(27, 2), (20, 3)])
+def test_ooc_any_hit_repeated_passes_fewer_domains(spray, oracle, tmp_path, ndom, slots):
+    """A scene of fewer than 64 domains, several any-hit passes in a row:
+    the drains keep two shard sets of death counts 64 * W queues apart, and
+    a pass's last (unpublished) launch leaves its set dirty -- the queue build
+    must clear both sets at that stride, or the next pass's snapshots count
+    old deaths, undercount the live pairs and skip queues that still hold
+    shadow rays."""
+    desc = _subscene(tmp_path, ndom)
+    org, d = batch(oracle)
+    sc, _, _ = oracle.load_scene(desc, SCENES)
+    assert sc.ndomains == ndom
+    ref, _ = sc.intersect(org, d)
+    so, sd, src = oracle.spawn_shadows_pt(org, d, ref, H.SHADE[0:3], H.SHADE[3:6],
+                                          H.SHADE[6:9], H.SHADE[9])
+    ref_occ, _ = sc.occluded(so, sd)
+    rng = np.random.default_rng(5)
+    o2, d2 = random_rays(rng, 20000, np.array([20, 19, 20], np.float32), 40.0)
+    ref2, _ = sc.occluded(o2, d2)
+
+    rt, oc = spray.engine.ooc_scene(desc, SCENES, slots)
+    hits = torch.empty((len(org), 12), dtype=torch.float32, device="cuda")
+    oc.intersect(H.rays_tensor(org, d).cuda(), hits)
+    rt.sync()
+    assert hits.cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1).tobytes() == ref.tobytes()
+    srays = H.rays_tensor(so, sd).cuda()
+    rays2 = H.rays_tensor(o2, d2).cuda()
+    for rep in range(3):
+        occ = torch.empty(len(so), dtype=torch.uint8, device="cuda")
+        oc.occluded(srays, None, occ)
+        occ2 = torch.empty(len(o2), dtype=torch.uint8, device="cuda")
+        oc.occluded(rays2, None, occ2)
+        rt.sync()
+        assert (occ.cpu().numpy() == ref_occ).all(), rep
+        assert (occ2.cpu().numpy() == ref2).all(), rep
+    assert oc.stats()["drains"] > 6
+    oc.close()
+    rt.close()

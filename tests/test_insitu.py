@@ -43,14 +43,20 @@ def morton_code(x, y, z):
         return int((c[0] * np.uint32(4) + c[1] * np.uint32(2) + c[2]) & np.uint32(0xFFFFFFFF))
 
 
-def partition_restated(boxes, sb, nranks):
-    """InsituPartition::partition (data_partition.h:59-137) in numpy."""
+def partition_restated(boxes, sb, nranks, mode=0):
+    """InsituPartition::partition (data_partition.h:59-155) in numpy; mode 0
+    GROUP_CLOSE_DOMAINS (contiguous shares, :118-137), 1 round robin over the
+    sorted codes (:139-155)."""
     f = np.float32
     scale = (f(1.0) / (sb[3:] - sb[:3])).astype(f)
     off = (f(0.0) - (sb[:3] * scale).astype(f)).astype(f)
     codes = sorted((morton_code(*(((b[:3] + b[3:]) * f(0.5)).astype(f) * scale + off).astype(f)), i)
                    for i, b in enumerate(boxes))
     owner = np.zeros(len(boxes), np.int32)
+    if mode == 1:
+        for k, (_, dom) in enumerate(codes):
+            owner[dom] = k % nranks
+        return owner
     shares, rank, s = len(boxes) // nranks, 0, 0
     for _, dom in codes:
         owner[dom] = rank
@@ -75,8 +81,20 @@ def test_engine_partition_matches_restatement(nranks):
     jitter = boxes + rng.uniform(-3, 3, size=(len(boxes), 1)).astype(np.float32)
     for b in (boxes, jitter.astype(np.float32)):
         sb = np.concatenate([b[:, :3].min(0), b[:, 3:].max(0)])
-        assert np.array_equal(insitu.morton_partition(b, sb, nranks),
-                              partition_restated(b, sb, nranks))
+        for mode in (0, 1):
+            assert np.array_equal(insitu.morton_partition(b, sb, nranks, mode),
+                                  partition_restated(b, sb, nranks, mode))
+
+
+def test_round_robin_scatters_close_domains():
+    """ROUND_ROBIN over 8 ranks: every rank holds one domain of every 2x2x2
+    octant (the GROUP_CLOSE octants dealt out one per rank)."""
+    boxes, bound = scene_boxes()
+    owner = insitu.morton_partition(boxes, bound, 8, insitu.PARTITION_ROUND_ROBIN)
+    close = insitu.morton_partition(boxes, bound, 8)
+    assert np.bincount(owner, minlength=8).tolist() == [8] * 8
+    for r in range(8):
+        assert sorted(close[owner == r].tolist()) == list(range(8))
 
 
 def test_partition_octants_of_the_grid():
@@ -124,7 +142,7 @@ CASES = {  # name: (shader kind, bounces, samples, image size, spp)
 LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)]}
 
 
-def _rank_main(rank, world, port, out, case):
+def _rank_main(rank, world, port, out, case, mode=0):
     import pickle
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -137,7 +155,7 @@ def _rank_main(rank, world, port, out, case):
     try:
         kind, bounces, samples, img, spp = CASES[case]
         boxes, bound = scene_boxes()
-        owner = insitu.morton_partition(boxes, bound, world)
+        owner = insitu.morton_partition(boxes, bound, world, mode)
         local = H.OracleLocal(po, owner, rank)
         c = H.BENCH_CAMERA
         cam = po.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
@@ -156,17 +174,19 @@ def _rank_main(rank, world, port, out, case):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,case", [(1, "pt1"), (2, "pt1"), (3, "pt1"), (2, "pt3"),
-                                        (8, "pt1"), (8, "ao16"), (8, "pt3")])
-def test_insitu_protocol_gloo(oracle, world, case):
+@pytest.mark.parametrize("world,case,mode", [(1, "pt1", 0), (2, "pt1", 0), (3, "pt1", 0),
+                                             (2, "pt3", 0), (8, "pt1", 0), (8, "ao16", 0),
+                                             (8, "pt3", 0), (8, "pt1", 1), (3, "pt3", 1)])
+def test_insitu_protocol_gloo(oracle, world, case, mode):
     import pickle
     import insitu_helpers as H
     with tempfile.TemporaryDirectory() as out:
         port = _free_port()
         if world == 1:
-            _rank_main(0, 1, port, out, case)
+            _rank_main(0, 1, port, out, case, mode)
         else:
-            torch.multiprocessing.spawn(_rank_main, args=(world, port, out, case), nprocs=world)
+            torch.multiprocessing.spawn(_rank_main, args=(world, port, out, case, mode),
+                                        nprocs=world)
         res = []
         for r in range(world):
             with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
