@@ -571,6 +571,10 @@ typedef struct spray_rt_transport {
                    const size_t* recv_bytes);
   int (*allreduce_u64)(void* user, unsigned long long* data, size_t n); /* SUM, in place */
   int (*reduce_f32)(void* user, float* data, size_t n, int root);       /* SUM to root */
+  /* replicated-ray frames (spray_rt_insitu_trace_frame); may be NULL, the
+   * frame then fails with SPRAY_RT_ERR_UNSUPPORTED */
+  int (*allreduce_min_u64)(void* user, unsigned long long* data, size_t n); /* MIN, in place */
+  int (*allreduce_sum_u8)(void* user, uint8_t* data, size_t n);            /* SUM, in place */
 } spray_rt_transport;
 
 /* Optional per-sample record of a trace (tests, VBuf dumps): for every copy
@@ -622,6 +626,44 @@ int spray_rt_insitu_trace(spray_rt_insitu_t ins, const spray_rt_shader* shader,
                           const spray_rt_ray* rays, const int32_t* pixid, const int32_t* samid,
                           size_t n, int spp, float* image_rgba, const spray_rt_insitu_rec* rec,
                           unsigned long long totals[3]);
+/* The whole frame with replicated eye rays: rays[n] / pixid / samid are
+ * EVERY eye ray of the frame (spray_rt_eye_rays_insitu over the whole
+ * blocking tile), the same on every rank.  Instead of moving rays to their
+ * domains' owners, each rank
+ *   1. computes every ray's owner-rank mask (its domain list through the
+ *      partition) -- C = the rays with a non-empty list, the same ascending
+ *      list on every rank;
+ *   2. traces the rays of C with a domain of its own over its own domains
+ *      (keyed closest hit: t, list position, domain);
+ *   3. joins one MIN all-reduce of the keys over C -- the sequential walk's
+ *      winner of every ray, on every rank (VBuf::compositeTbuf,
+ *      insitu_vbuf.h:109-129, per ray instead of per tile);
+ *   4. builds the point-light shadow ray of every hit from (org, dir, t),
+ *      the winner's bits, and any-hits it over its own domains; the winner
+ *      shades (ooc::ShaderPt point light);
+ *   5. joins one SUM all-reduce of the occlusion bytes over C, the frame
+ *      totals riding behind them (compositeObuf + WorkStats::reduce);
+ *   6. films the unoccluded shadows of the rays it won.
+ * No ray, hit or shadow record crosses the wire and no count is exchanged:
+ * two all-reduces and one host read per frame.  Results per sample are the
+ * protocol's (the same winner, shading and occlusion).  Needs the fused PT
+ * case (one bounce, one point light, diffuse surfaces) and, with host
+ * collectives, allreduce_min_u64 / allreduce_sum_u8; SPRAY_RT_ERR_UNSUPPORTED
+ * otherwise (trace with spray_rt_insitu_trace).  World 1: the all-local
+ * fused frame. */
+int spray_rt_insitu_trace_frame(spray_rt_insitu_t ins, const spray_rt_shader* shader,
+                                const spray_rt_ray* rays, const int32_t* pixid,
+                                const int32_t* samid, size_t n, int spp, float* image_rgba,
+                                const spray_rt_insitu_rec* rec, unsigned long long totals[3]);
+/* Per-phase device time of the traces since the last call (then reset),
+ * HIP events on the context's stream, when phase timing is on
+ * (spray_rt_insitu_set_timing).  out_ms[8]; *nphases = phases of the last
+ * trace's form: replicated frame {lists, keyed closest hit, key all-reduce,
+ * shadows, occlusion all-reduce, film, totals}; protocol {route + counts,
+ * ray exchange, keyed closest hit, key composite, shading, shadow route +
+ * exchange, shadow any hit + return, film + totals}. */
+int spray_rt_insitu_set_timing(spray_rt_insitu_t ins, int on);
+int spray_rt_insitu_phase_times(spray_rt_insitu_t ins, double out_ms[8], int* nphases);
 /* HdrImage::composite (src/display/image.h:167-181): SUM of the ranks'
  * images at rank 0 (device float[nfloats], in place). */
 int spray_rt_insitu_composite(spray_rt_insitu_t ins, float* image_rgba, size_t nfloats);

@@ -41,6 +41,11 @@ class Comm:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
         return t
 
+    def all_reduce_min(self, t):
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        return t
+
 
 class Exchange:
     """One routed exchange: row i of a batch goes to every rank whose bit is
@@ -155,3 +160,76 @@ def trace_frame(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, image):
     tot = t.tensor([nrad, nsh], dtype=t.int64)
     comm.all_reduce_sum(tot)
     return recs, (int(tot[0]), int(tot[1]))
+
+
+def _shadow_from_t(org, d, t, lp):
+    """RTCRayUtil::hitPosition + PointLight::sample (rays.h:436-441,
+    light.h:47-53) in float32, glm's operation order: the shadow ray of a hit
+    from (org, dir, t) alone."""
+    f = np.float32
+    pos = (d * t[:, None]).astype(f) + org
+    lv = (np.asarray(lp, f)[None, :] - pos).astype(f)
+    dot = ((lv[:, 0] * lv[:, 0] + lv[:, 1] * lv[:, 1]).astype(f) + lv[:, 2] * lv[:, 2]).astype(f)
+    inv = (f(1.0) / np.sqrt(dot)).astype(f)
+    return pos.astype(f), (lv * inv[:, None]).astype(f)
+
+
+def trace_frame_replicated(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, image):
+    """The replicated-ray frame of insitu.cpp (trace_replicated): org / d /
+    pix / sam are EVERY eye ray of the frame, the same on every rank.  Each
+    rank: owner-rank masks of all rays; C = the rays with a non-empty domain
+    list; keyed closest hit of the rays of C with a domain of its own over
+    its own domains; MIN all-reduce of the keys over C; the point-light
+    shadow ray of every hit from (org, dir, t) traced over its own domains;
+    the winner shades (ooc::ShaderPt); SUM all-reduce of the occlusion bytes;
+    film of the rays it won.  PT, one bounce, one point light.  Returns
+    (records, (group's radiance rays, shadow rays))."""
+    import torch as t
+    assert sh.bounces == 1 and sh.nlights == 1
+    org, d = np.ascontiguousarray(org, np.float32), np.ascontiguousarray(d, np.float32)
+    pix, sam = np.asarray(pix, np.int32), np.asarray(sam, np.int32)
+    n = len(org)
+    rays = _rays(org, d)
+    mask = local.route(rays).numpy()
+    C = np.flatnonzero(mask != 0)
+    mine = ((mask[C] >> comm.rank) & 1).astype(bool)
+    keys_c = np.full(len(C), MISS_KEY, np.int64)
+    hits_c = np.zeros(len(C), po.HIT_DTYPE)
+    if mine.any():
+        h, k = local.intersect_keyed(rays[C[mine]])
+        keys_c[mine] = k.numpy()
+        hits_c[mine] = np.ascontiguousarray(h.numpy()).view(po.HIT_DTYPE).reshape(-1)
+    own = keys_c.copy()
+    best = comm.all_reduce_min(t.from_numpy(keys_c.copy())).numpy()
+    hit = best != MISS_KEY
+    win = hit & (own == best)
+    # every hit's shadow ray, traced over this rank's domains
+    tt = (best[hit] >> 32).astype(np.uint32).view(np.float32)
+    lp = [sh.lights[0].pos[k] for k in range(3)]
+    so, sd = _shadow_from_t(org[C[hit]], d[C[hit]], tt, lp)
+    occ = np.zeros(len(C), np.int32)
+    if len(so):
+        occ[hit] = local.occluded(_rays(so, sd)).numpy()
+    # the winners shade: spawn rule and light weight (ooc::ShaderPt)
+    oc, dc = np.ascontiguousarray(org[C]), np.ascontiguousarray(d[C])
+    w = np.ones((len(C), 3), np.float32)
+    valid = win.astype(np.uint8)
+    so2, sd2, sw, sv, _ = po.shade(sh, bsdfs, 0, oc, dc, hits_c, w, valid, pix[C], sam[C])
+    sv = sv.astype(bool) & win
+    # the winner's own shadow ray is the one every rank built from t
+    so_c = np.zeros((len(C), 3), np.float32)
+    sd_c = np.zeros((len(C), 3), np.float32)
+    so_c[hit], sd_c[hit] = so, sd
+    assert so2[sv].tobytes() == so_c[sv].tobytes() and sd2[sv].tobytes() == sd_c[sv].tobytes()
+    tail = t.tensor([n if comm.rank == 0 else 0, int(sv.sum())], dtype=t.int64)
+    occ_t = comm.all_reduce_sum(t.from_numpy(occ))
+    comm.all_reduce_sum(tail)
+    occ = occ_t.numpy() > 0
+    lit = np.flatnonzero(sv & ~occ)
+    if len(lit):
+        img = image.reshape(-1, 4)
+        add = ((1.0 / spp) * sw[lit].astype(np.float64)).astype(np.float32)
+        np.add.at(img[:, :3], pix[C[lit]], add)
+    recs = [(0, int(sam[C[j]]), hits_c[j].tobytes(), int(sv[j]), int(sv[j] and occ[j]))
+            for j in np.flatnonzero(win)]
+    return recs, (int(tail[0]), int(tail[1]))

@@ -12,6 +12,9 @@
 // at VBuf::compositeTbuf), and a fixed number of bounces replaces the
 // WorkStats termination test (no rays exist past shader->bounces).
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -117,6 +120,15 @@ struct InsituTransport {
                         const size_t* rb, bool skip_self = false) = 0;
   virtual int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) = 0;
   virtual int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) = 0;
+  // replicated-ray frames: MIN of u64 keys, SUM of bytes (device, in place)
+  virtual bool has_rep() const { return true; }
+  virtual int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) = 0;
+  virtual int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) = 0;
+  // rehearsal only: the rank's device work runs while it holds a lock
+  // shared by the group's processes (SPRAY_INSITU_SERIAL), so the phase
+  // timings of ranks sharing one GPU are not inflated by each other
+  virtual void serial_begin() {}
+  virtual void serial_end() {}
   // copies a rank sends itself may skip the wire (the owner gathers them
   // straight from the holder's arrays)
   virtual bool self_direct() const { return true; }
@@ -141,6 +153,16 @@ struct spray_rt_insitu {
   DBuf nsel, sel_tmp, dnum, dstats, dtot;
   unsigned long long* h_small = nullptr;  // pinned: counts, totals
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
+  // replicated-ray frames (trace_replicated)
+  DBuf rmask, rfc, rfl, ridx_c, ridx_l, rnum, rsel_tmp, rkeys_n, rhits_n, rkeys_c;
+  DBuf rsray, rsflag, rwin, rsvalid, rsw, rocc, rpix, rsam, rhit_c, rnsh;
+  // phase timing (spray_rt_insitu_set_timing): events on the stream
+  bool timing = false;
+  static constexpr int kMaxEv = 48;
+  hipEvent_t ev[kMaxEv] = {};
+  int ev_phase[kMaxEv] = {};
+  int nev = 0, nph = 0;
+  double phase_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -228,6 +250,16 @@ struct RcclTransport : InsituTransport {
     return chk(I, nccl().Reduce(dev, dev, n, ncclFloat32, ncclSum, root, comm, stream_of(I->ctx)),
                "ncclReduce");
   }
+  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) override {
+    ++I->st[4];
+    return chk(I, nccl().AllReduce(dev, dev, n, ncclUint64, ncclMin, comm, stream_of(I->ctx)),
+               "ncclAllReduce(min)");
+  }
+  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) override {
+    ++I->st[4];
+    return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclSum, comm, stream_of(I->ctx)),
+               "ncclAllReduce(sum u8)");
+  }
   bool self_direct() const override { return !self_via_nccl; }
   ~RcclTransport() override {
     if (comm) nccl().CommDestroy(comm);
@@ -238,9 +270,48 @@ struct RcclTransport : InsituTransport {
 struct HostTransport : InsituTransport {
   spray_rt_transport cb{};
   std::vector<char> hs, hr;
+  int lock_fd = -1;  // SPRAY_INSITU_SERIAL: the group's device-work lock
 
+  ~HostTransport() override {
+    if (lock_fd >= 0) close(lock_fd);
+  }
+  void serial_begin() override {
+    if (lock_fd >= 0) (void)flock(lock_fd, LOCK_EX);
+  }
+  void serial_end() override {
+    if (lock_fd >= 0) (void)flock(lock_fd, LOCK_UN);
+  }
+  // every collective first drains the stream (the staging below does), then
+  // lets the other ranks' device work run while this one waits
   int sync(spray_rt_insitu* I) {
     HIPCHK(I->ctx, hipStreamSynchronize(stream_of(I->ctx)));
+    return SPRAY_RT_OK;
+  }
+  bool has_rep() const override { return cb.allreduce_min_u64 && cb.allreduce_sum_u8; }
+  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) override {
+    std::vector<unsigned long long> h(std::max<size_t>(n, 1));
+    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 8, hipMemcpyDeviceToHost, stream_of(I->ctx)));
+    CALL(sync(I));
+    serial_end();
+    const int bad = cb.allreduce_min_u64(cb.user, h.data(), n);
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: min all-reduce failed");
+    HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * 8, hipMemcpyHostToDevice, stream_of(I->ctx)));
+    CALL(sync(I));
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) override {
+    std::vector<uint8_t> h(std::max<size_t>(n, 1));
+    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n, hipMemcpyDeviceToHost, stream_of(I->ctx)));
+    CALL(sync(I));
+    serial_end();
+    const int bad = cb.allreduce_sum_u8(cb.user, h.data(), n);
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: byte all-reduce failed");
+    HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n, hipMemcpyHostToDevice, stream_of(I->ctx)));
+    CALL(sync(I));
+    ++I->st[4];
     return SPRAY_RT_OK;
   }
   int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
@@ -250,8 +321,10 @@ struct HostTransport : InsituTransport {
                                   stream_of(I->ctx)));
     CALL(sync(I));
     std::vector<size_t> b(W, sizeof(int64_t));
-    if (cb.alltoallv(cb.user, h_send, b.data(), h_recv, b.data()))
-      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: count exchange failed");
+    serial_end();
+    const int bad = cb.alltoallv(cb.user, h_send, b.data(), h_recv, b.data());
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: count exchange failed");
     ++I->st[3];
     ++I->st[4];
     return SPRAY_RT_OK;
@@ -266,8 +339,10 @@ struct HostTransport : InsituTransport {
     hipStream_t s = stream_of(I->ctx);
     if (ts) HIPCHK(I->ctx, hipMemcpyAsync(hs.data(), send, ts, hipMemcpyDeviceToHost, s));
     CALL(sync(I));
-    if (cb.alltoallv(cb.user, hs.data(), sb, hr.data(), rb))
-      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: all-to-all failed");
+    serial_end();
+    const int bad = cb.alltoallv(cb.user, hs.data(), sb, hr.data(), rb);
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: all-to-all failed");
     if (trv) HIPCHK(I->ctx, hipMemcpyAsync(recv, hr.data(), trv, hipMemcpyHostToDevice, s));
     CALL(sync(I));  // hr is reused by the next call
     ++I->st[4];
@@ -277,8 +352,10 @@ struct HostTransport : InsituTransport {
     std::vector<unsigned long long> h(n);
     HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 8, hipMemcpyDeviceToHost, stream_of(I->ctx)));
     CALL(sync(I));
-    if (cb.allreduce_u64(cb.user, h.data(), n))
-      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: all-reduce failed");
+    serial_end();
+    const int bad = cb.allreduce_u64(cb.user, h.data(), n);
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: all-reduce failed");
     HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * 8, hipMemcpyHostToDevice, stream_of(I->ctx)));
     CALL(sync(I));
     ++I->st[4];
@@ -288,8 +365,10 @@ struct HostTransport : InsituTransport {
     std::vector<float> h(n);
     HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 4, hipMemcpyDeviceToHost, stream_of(I->ctx)));
     CALL(sync(I));
-    if (cb.reduce_f32(cb.user, h.data(), n, root))
-      return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: reduce failed");
+    serial_end();
+    const int bad = cb.reduce_f32(cb.user, h.data(), n, root);
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: reduce failed");
     if (I->rank == root)
       HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * 4, hipMemcpyHostToDevice, stream_of(I->ctx)));
     CALL(sync(I));
@@ -312,6 +391,28 @@ struct Routed {
     return b;
   }
 };
+
+// ---- phase timing: an event at each phase start; the time to the next
+// event is charged to that phase (read after the trace's last sync)
+int mark(spray_rt_insitu* I, int phase) {
+  if (!I->timing || I->nev >= spray_rt_insitu::kMaxEv) return SPRAY_RT_OK;
+  hipEvent_t& e = I->ev[I->nev];
+  if (!e) HIPCHK(I->ctx, hipEventCreate(&e));
+  HIPCHK(I->ctx, hipEventRecord(e, stream_of(I->ctx)));
+  I->ev_phase[I->nev++] = phase;
+  return SPRAY_RT_OK;
+}
+void flush_phases(spray_rt_insitu* I, int nphases) {
+  if (!I->timing) return;
+  for (int k = 0; k + 1 < I->nev; ++k) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, I->ev[k], I->ev[k + 1]) == hipSuccess)
+      I->phase_ms[I->ev_phase[k]] += double(ms);
+  }
+  I->nev = 0;
+  I->nph = nphases;
+}
+#define MARK(ph) CALL(mark(I, (ph)))
 
 int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf& mask, DBuf& idx,
                     DBuf& starts, Routed* R, const uint32_t* sel = nullptr,
@@ -380,8 +481,10 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
   for (int b = 0; b < P->bounces; ++b) {
     nrad += hn;
     // ---- radiance rays to the owners of their domains
+    MARK(0);
     Routed R;
     CALL(route_and_count(I, hr, hn, I->mask, I->idx, I->starts, &R));
+    MARK(1);
     const size_t m = R.recv;
     GROW(I->sendb, std::max(R.total * kRadRecBytes, R.total * 8));
     GROW(I->recvb, m * kRadRecBytes);
@@ -415,10 +518,12 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     if (direct)
       HIPCHK(c, launch_gather_rad(s, hr, hw, hp, hs, ix + R.self_send, R.self_n, oray + us,
                                   ow + 4 * us, opix + us, osam + us));
+    MARK(2);
     if (m)
       HIPCHK(c, launch_scene_intersect_keyed(s, view(c), I->oray.as<spray_rt_ray>(), m,
                                              I->ohit.as<spray_rt_hit>(), I->okey.as<uint64_t>()));
     // ---- keys back to the holder, minimum per ray, the minimum forward
+    MARK(3);
     GROW(I->keyback, R.total * 8);
     GROW(I->best, hn * 8);
     CALL(exchange(I, R, 8, true, I->okey.p, I->keyback.p));
@@ -431,6 +536,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     HIPCHK(c, launch_winners(s, I->okey.as<uint64_t>(), I->obest.as<uint64_t>(), m,
                              I->owin.as<uint8_t>()));
     // ---- the winning owner shades (ShaderPt / ShaderAo at ray depth b)
+    MARK(4);
     const size_t MS = m * size_t(ns);
     if (m > 0xFFFFFFFFull || MS > 0xFFFFFFFFull)
       return fail(c, SPRAY_RT_ERR_LIMIT, "in-situ batch too large (copies x shadow slots > 2^32)");
@@ -478,6 +584,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
       cn = cnt2[1];
     }
     // ---- shadow rays to the owners of their domains, occlusion OR-ed back
+    MARK(5);
     if (MS) HIPCHK(c, hipMemsetAsync(I->socc.p, 0, MS, s));
     Routed S;  // the shadow rays, read in place (through ssel when compacted)
     const uint32_t* ssel = slots_direct ? nullptr : I->ssel.as<uint32_t>();
@@ -509,6 +616,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
       if (sdir)
         HIPCHK(c, launch_gather_shadow_self(s, sr, ssel, six + S.self_send, S.self_n, ash + b0));
     }
+    MARK(6);
     if (S.recv)
       HIPCHK(c, launch_scene_occluded(s, view(c), I->ashadow.as<spray_rt_ray>(), S.recv, nullptr,
                                       I->aocc.as<uint8_t>(), nullptr));
@@ -516,6 +624,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
     HIPCHK(c, launch_occ_return(s, I->sidx.as<int64_t>(), I->sret.as<uint8_t>(), S.total, ssel,
                                 I->socc.as<uint8_t>()));
     // ---- film of the copies this rank shaded
+    MARK(7);
     HIPCHK(c, launch_film_atomic(s, image, I->opix.as<int32_t>(), m, ns, I->ssw.as<float>(),
                                  I->ssv.as<uint8_t>(), I->socc.as<uint8_t>(), scale));
     if (rec)
@@ -557,7 +666,9 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
                            hipMemcpyDeviceToDevice, s));
   CALL(I->tr->allreduce_u64(I, I->dtot.as<unsigned long long>(), 3));
   HIPCHK(c, hipMemcpyAsync(ht, I->dtot.p, 3 * 8, hipMemcpyDeviceToHost, s));
+  MARK(7);
   HIPCHK(c, hipStreamSynchronize(s));
+  flush_phases(I, 8);
   if (totals)
     for (int k = 0; k < 3; ++k) totals[k] = ht[k];
   ++I->st[5];
@@ -603,6 +714,7 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   GROW(I->ssw, MS * 16);
   GROW(I->ssv, MS);
   GROW(I->socc, MS);
+  MARK(0);
   HIPCHK(c, hipMemsetAsync(I->dstats.p, 0, 4 * 8, s));
   unsigned long long* st = I->dstats.as<unsigned long long>();
   spray_rt_hit* hits = I->ohit.as<spray_rt_hit>();
@@ -662,12 +774,134 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   CALL(I->tr->allreduce_u64(I, dt, 3));
   unsigned long long* ht = I->h_small + 200;
   HIPCHK(c, hipMemcpyAsync(ht, dt, 3 * 8, hipMemcpyDeviceToHost, s));
+  MARK(0);
   HIPCHK(c, hipStreamSynchronize(s));
   if (totals)
     for (int k = 0; k < 3; ++k) totals[k] = ht[k];
   ++I->st[5];
   if (ht[2])
     return fail(c, SPRAY_RT_ERR_UNSUPPORTED, "%llu shading cases the reference aborts on", ht[2]);
+  return SPRAY_RT_OK;
+}
+
+// The frame with replicated eye rays (spray_rt_insitu_trace_frame): see
+// include/spray_rt.h.  Phases: 0 lists, 1 keyed closest hit, 2 key
+// all-reduce, 3 shadows, 4 occlusion all-reduce, 5 film, 6 totals.
+int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
+                     const int32_t* pixid, const int32_t* samid, size_t n, int spp,
+                     float* image, const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  const double scale = 1.0 / double(spp);
+  const spray_rt_light& lt = P->lights[0];
+  RepSpawnArgs A{};
+  const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
+                             lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
+                             P->ks[2],       P->shininess};
+  std::memcpy(A.shade10, shade10, sizeof(shade10));
+  MARK(0);
+  // ---- 1. owner-rank masks, C and L (one host read: |C|, which sizes the
+  // all-reduces -- the same on every rank)
+  GROW(I->rmask, n * 8);
+  GROW(I->rfc, n);
+  GROW(I->rfl, n);
+  GROW(I->ridx_c, n * 4);
+  GROW(I->ridx_l, n * 4);
+  GROW(I->rnum, 2 * 4);
+  size_t t1 = 0;
+  HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
+  GROW(I->rsel_tmp, t1);
+  uint32_t* dnum = I->rnum.as<uint32_t>();
+  HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, I->rmask.as<uint64_t>()));
+  HIPCHK(c, launch_rep_flags(s, I->rmask.as<uint64_t>(), n, I->rank, I->rfc.as<uint8_t>(),
+                             I->rfl.as<uint8_t>()));
+  HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
+                                  I->rsel_tmp.p, &t1));
+  HIPCHK(c, launch_select_flagged(s, I->rfl.as<uint8_t>(), n, I->ridx_l.as<uint32_t>(), dnum + 1,
+                                  I->rsel_tmp.p, &t1));
+  HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  ++I->st[3];
+  uint32_t cnt[2];
+  std::memcpy(cnt, I->h_small, 8);
+  const size_t nc = cnt[0];
+  // ---- 2. own closest hits (keyed) of L, their keys over C
+  MARK(1);
+  GROW(I->rkeys_n, n * 8);
+  GROW(I->rhits_n, n * 48);
+  GROW(I->rkeys_c, nc * 8 + 8);
+  if (cnt[1])
+    HIPCHK(c, launch_scene_intersect_keyed_indexed(s, view(c), rays, n, I->ridx_l.as<uint32_t>(),
+                                                   dnum + 1, I->rhits_n.as<spray_rt_hit>(),
+                                                   I->rkeys_n.as<uint64_t>()));
+  HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
+                            I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
+  // ---- 3. the winning key of every ray of C, on every rank
+  MARK(2);
+  if (nc) CALL(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
+  // ---- 4. shadow rays of every hit, own any hit; the winners shade
+  MARK(3);
+  GROW(I->rsray, nc * 32 + 32);
+  GROW(I->rsflag, nc + 1);
+  GROW(I->rwin, nc + 1);
+  GROW(I->rsvalid, nc + 1);
+  GROW(I->rsw, nc * 16 + 16);
+  GROW(I->rocc, nc + 192);
+  GROW(I->rpix, nc * 4 + 4);
+  GROW(I->rsam, nc * 4 + 4);
+  GROW(I->rnsh, 8);
+  if (rec) GROW(I->rhit_c, nc * 48 + 48);
+  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, 8, s));
+  A.nc = nc;
+  A.rank = I->rank;
+  A.idx_c = I->ridx_c.as<uint32_t>();
+  A.keys_c = I->rkeys_c.as<uint64_t>();
+  A.keys_n = I->rkeys_n.as<uint64_t>();
+  A.mask = I->rmask.as<uint64_t>();
+  A.rays = reinterpret_cast<const float4*>(rays);
+  A.hits_n = I->rhits_n.as<spray_rt_hit>();
+  A.pix = pixid;
+  A.sam = samid;
+  A.sray = I->rsray.as<float4>();
+  A.sflag = I->rsflag.as<uint8_t>();
+  A.win = I->rwin.as<uint8_t>();
+  A.svalid = I->rsvalid.as<uint8_t>();
+  A.sw = I->rsw.as<float4>();
+  A.occ = I->rocc.as<uint8_t>();
+  A.pix_c = I->rpix.as<int32_t>();
+  A.sam_c = I->rsam.as<int32_t>();
+  A.hit_c = rec ? I->rhit_c.as<spray_rt_hit>() : nullptr;
+  A.nshadow = I->rnsh.as<unsigned long long>();
+  HIPCHK(c, launch_rep_spawn(s, A));
+  if (nc)
+    HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
+                                           I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
+  // the frame totals behind the occlusion bytes: rank 0 counts the frame's
+  // radiance rays, every rank the shadow rays it spawned
+  HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nc, I->rank == 0 ? n : 0,
+                              I->rnsh.as<unsigned long long>()));
+  // ---- 5. occlusion OR (a byte SUM) + totals
+  MARK(4);
+  CALL(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nc + 192));
+  // ---- 6. film of the rays this rank won
+  MARK(5);
+  HIPCHK(c, launch_film_atomic(s, image, I->rpix.as<int32_t>(), nc, 1, I->rsw.as<float>(),
+                               I->rsvalid.as<uint8_t>(), I->rocc.as<uint8_t>(), scale));
+  if (rec)
+    HIPCHK(c, launch_record(s, I->rwin.as<uint8_t>(), nc, 0, 1, I->rsam.as<int32_t>(),
+                            I->rhit_c.as<spray_rt_hit>(), I->rsvalid.as<uint8_t>(),
+                            I->rocc.as<uint8_t>(), *rec));
+  MARK(6);
+  uint8_t* ht = reinterpret_cast<uint8_t*>(I->h_small + 128);  // 192 bytes
+  HIPCHK(c, hipMemcpyAsync(ht, I->rocc.as<uint8_t>() + nc, 192, hipMemcpyDeviceToHost, s));
+  MARK(6);
+  HIPCHK(c, hipStreamSynchronize(s));
+  flush_phases(I, 7);
+  unsigned long long tot[3] = {0, 0, 0};
+  for (int k = 0; k < 192; ++k) tot[k >> 6] += (unsigned long long)ht[k] << (k & 63);
+  if (totals)
+    for (int k = 0; k < 3; ++k) totals[k] = tot[k];
+  ++I->st[5];
   return SPRAY_RT_OK;
 }
 
@@ -678,9 +912,14 @@ void free_all(spray_rt_insitu* I) {
                  &I->ohit, &I->okey, &I->obest, &I->owin, &I->ovalid, &I->best, &I->keyback,
                  &I->sray, &I->ssw, &I->ssv, &I->socc, &I->ssel, &I->smask,
                  &I->sidx, &I->sstarts, &I->ashadow, &I->aocc, &I->sret, &I->nsel,
-                 &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot};
+                 &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot, &I->rmask, &I->rfc, &I->rfl,
+                 &I->ridx_c, &I->ridx_l, &I->rnum, &I->rsel_tmp, &I->rkeys_n, &I->rhits_n,
+                 &I->rkeys_c, &I->rsray, &I->rsflag, &I->rwin, &I->rsvalid, &I->rsw, &I->rocc,
+                 &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
+  for (hipEvent_t e : I->ev)
+    if (e) (void)hipEventDestroy(e);
   if (I->h_small) (void)hipHostFree(I->h_small);
 }
 
@@ -749,6 +988,8 @@ int spray_rt_insitu_create(spray_rt_ctx_t c, int world, int rank, const void* nc
   } else {
     auto t = std::make_unique<HostTransport>();
     t->cb = *host;
+    if (const char* lk = std::getenv("SPRAY_INSITU_SERIAL"))
+      if (lk[0]) t->lock_fd = open(lk, O_RDWR | O_CREAT, 0666);
     I->tr = std::move(t);
   }
   *out = I.release();
@@ -836,9 +1077,67 @@ int spray_rt_insitu_trace(spray_rt_insitu_t I, const spray_rt_shader* P, const s
   // the self exchange through RCCL (SPRAY_INSITU_NCCL_SELF=1) runs.
   const char* lo = std::getenv("SPRAY_INSITU_LOCAL");
   const bool local_ok = !(lo && lo[0] == '0') && I->tr->self_direct();
-  if (local_ok && all_local(I)) return trace_local(I, P, rays, pixid, samid, n, spp, image, rec,
-                                                   totals);
-  return trace(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+  I->nev = 0;
+  I->tr->serial_begin();
+  if (local_ok && all_local(I)) {
+    r = trace_local(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+    flush_phases(I, 1);
+  } else {
+    r = trace(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+  }
+  I->tr->serial_end();
+  return r;
+}
+
+int spray_rt_insitu_trace_frame(spray_rt_insitu_t I, const spray_rt_shader* P,
+                                const spray_rt_ray* rays, const int32_t* pixid,
+                                const int32_t* samid, size_t n, int spp, float* image,
+                                const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = I->ctx;
+  if (spray_rt_shadow_slots(P) < 0 || spp <= 0)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad shader configuration");
+  if (rec && (!rec->d_count || !is_device_ptr(rec->d_count)))
+    return fail(c, SPRAY_RT_ERR_ARG, "records need a device counter");
+  if (n > 0xFFFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "n > 2^32");
+  if (!image || !is_device_ptr(image) ||
+      (n && (!is_device_ptr(rays) || !is_device_ptr(pixid) || !is_device_ptr(samid))))
+    return fail(c, SPRAY_RT_ERR_ARG, "in-situ trace needs device buffers");
+  int r = scene_common(c, image, 1, image);
+  if (r) return r;
+  if (!c->d_owner) return fail(c, SPRAY_RT_ERR_STATE, "no owner map set");
+  if (!fused_pt_shading(c, P))
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
+                "replicated frames need one bounce, one point light and diffuse surfaces");
+  if (!I->tr->has_rep())
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
+                "the host transport gives no allreduce_min_u64 / allreduce_sum_u8");
+  I->nev = 0;
+  I->tr->serial_begin();
+  if (I->world == 1) {
+    r = trace_local(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+    flush_phases(I, 1);
+  } else {
+    r = trace_replicated(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+  }
+  I->tr->serial_end();
+  return r;
+}
+
+int spray_rt_insitu_set_timing(spray_rt_insitu_t I, int on) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  I->timing = on != 0;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_phase_times(spray_rt_insitu_t I, double out_ms[8], int* nphases) {
+  if (!I || !out_ms) return SPRAY_RT_ERR_ARG;
+  for (int k = 0; k < 8; ++k) {
+    out_ms[k] = I->phase_ms[k];
+    I->phase_ms[k] = 0.0;
+  }
+  if (nphases) *nphases = I->nph;
+  return SPRAY_RT_OK;
 }
 
 int spray_rt_insitu_composite(spray_rt_insitu_t I, float* image, size_t nfloats) {

@@ -60,6 +60,40 @@ hipError_t launch_weights_one(hipStream_t s, float* w, size_t n);
 // win[i] = (valid == null || valid[i]) && hits[i] is a hit
 hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_hit* hits,
                             size_t n, uint8_t* win);
+// ---- replicated-ray frames (insitu.cpp, trace_replicated) ----
+// fc[i] = mask[i] != 0 (some domain on the list), fl[i] = bit `rank` of it
+hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
+                            uint8_t* fl);
+// keys_c[j] = keys_n[idx_c[j]] where bit `rank` of its mask is set, else a miss
+hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
+                           int rank, const uint64_t* keys_n, uint64_t* keys_c);
+struct RepSpawnArgs {
+  size_t nc;
+  int rank;
+  const uint32_t* idx_c;      // [nc] ray ids of C
+  const uint64_t* keys_c;     // [nc] winning keys (after the MIN all-reduce)
+  const uint64_t* keys_n;     // [n] this rank's keys (valid where its mask bit is set)
+  const uint64_t* mask;       // [n] owner-rank masks
+  const float4* rays;         // [n] eye rays (32 B)
+  const spray_rt_hit* hits_n; // [n] this rank's hit records
+  const int32_t* pix;         // [n]
+  const int32_t* sam;         // [n]
+  float shade10[10];          // light position, radiance, ks, shininess
+  float4* sray;               // [nc] shadow ray of each hit (32 B)
+  uint8_t* sflag;             // [nc] 1: ray j hit (its shadow ray is traced here)
+  uint8_t* win;               // [nc] 1: this rank shades ray j
+  uint8_t* svalid;            // [nc] 1: the winner spawned the shadow ray
+  float4* sw;                 // [nc] its light weight
+  uint8_t* occ;               // [nc] zeroed (any hit writes own-domain occlusion)
+  int32_t* pix_c;             // [nc]
+  int32_t* sam_c;             // [nc]
+  spray_rt_hit* hit_c;        // [nc] winners' hit records (optional: records)
+  unsigned long long* nshadow;  // += spawned shadow rays
+};
+hipError_t launch_rep_spawn(hipStream_t s, const RepSpawnArgs& a);
+// tail[64 c + k] = bit k of {nrad, *nshadow, 0}[c] (192 bytes)
+hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
+                             const unsigned long long* nshadow);
 // counts[r] = starts[r + 1] - starts[r], r < world (<= 64)
 hipError_t launch_counts_from_starts(hipStream_t s, const int64_t* starts, int world,
                                      int64_t* counts);

@@ -10,6 +10,7 @@
 
 #include "insitu_kernels.h"
 #include "rt_device.h"
+#include "shade_device.h"
 
 namespace spray_rt {
 namespace {
@@ -275,6 +276,98 @@ __global__ __launch_bounds__(kBlock) void k_weights_one(float4* __restrict__ w, 
   if (j < n) w[j] = make_float4(1.f, 1.f, 1.f, 0.f);
 }
 
+// ---- replicated-ray frames (insitu.cpp, trace_replicated) ----------------
+// Every rank holds the frame's eye rays; C = the rays whose domain list is
+// not empty (the same ascending list on every rank), L = the rays with a
+// domain of this rank on their list.
+__global__ __launch_bounds__(kBlock) void k_rep_flags(const uint64_t* __restrict__ mask, size_t n,
+                                                      int rank, uint8_t* __restrict__ fc,
+                                                      uint8_t* __restrict__ fl) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t m = mask[i];
+  fc[i] = m != 0;
+  fl[i] = uint8_t((m >> rank) & 1ull);
+}
+
+// keys_c[j] = this rank's key of ray idx_c[j] (a miss where no domain of the
+// rank is on its list: the keyed launch did not visit it)
+__global__ __launch_bounds__(kBlock) void k_rep_keys(const uint32_t* __restrict__ idx_c, size_t nc,
+                                                     const uint64_t* __restrict__ mask, int rank,
+                                                     const uint64_t* __restrict__ keys_n,
+                                                     uint64_t* __restrict__ keys_c) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= nc) return;
+  const uint32_t i = idx_c[j];
+  keys_c[j] = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
+}
+
+// After the MIN all-reduce keys_c[j] is the winning key of ray idx_c[j] on
+// every rank.  Every rank builds the point-light shadow ray of every hit
+// from (org, dir, t) -- RTCRayUtil::hitPosition and PointLight::sample, the
+// operations of shade_pt_point, so the winner's bits -- and marks it for
+// its own any hit; the winner (its own key equals the minimum) shades:
+// spawn rule and light weight of ooc::ShaderPt (shade_pt_point).
+__global__ __launch_bounds__(kBlock) void k_rep_spawn(RepSpawnArgs A) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  ShadePt sh;
+  for (int k = 0; k < 3; ++k) {
+    sh.lp[k] = A.shade10[k];
+    sh.lr[k] = A.shade10[3 + k];
+    sh.ks[k] = A.shade10[6 + k];
+  }
+  sh.shininess = A.shade10[9];
+  bool spawned = false;
+  if (j < A.nc) {
+    const uint32_t i = A.idx_c[j];
+    const uint64_t key = A.keys_c[j];
+    const bool hit = key != kInsituMissKey;
+    const bool win = hit && ((A.mask[i] >> A.rank) & 1ull) && A.keys_n[i] == key;
+    float4 sw = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 o4 = A.rays[2 * size_t(i)], d4 = A.rays[2 * size_t(i) + 1];
+    const float o[3] = {o4.x, o4.y, o4.z}, d[3] = {d4.x, d4.y, d4.z};
+    float pos[3] = {0.f, 0.f, 0.f}, wi[3] = {0.f, 0.f, 1.f};
+    if (win) {
+      const spray_rt_hit h = A.hits_n[i];
+      float L[3];
+      spawned = shade_pt_point(o, d, h, sh, pos, wi, L);
+      sw = make_float4(L[0], L[1], L[2], 0.f);
+      if (A.hit_c) A.hit_c[j] = h;
+    } else if (hit) {
+      const float t = __uint_as_float(uint32_t(key >> 32));
+      pos[0] = d[0] * t + o[0];
+      pos[1] = d[1] * t + o[1];
+      pos[2] = d[2] * t + o[2];
+      wi[0] = sh.lp[0] - pos[0];
+      wi[1] = sh.lp[1] - pos[1];
+      wi[2] = sh.lp[2] - pos[2];
+      gnorm3(wi);
+    }
+    A.sray[2 * j] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
+    A.sray[2 * j + 1] = make_float4(wi[0], wi[1], wi[2], kInf);
+    A.sflag[j] = hit;
+    A.win[j] = win;
+    A.svalid[j] = spawned;
+    A.sw[j] = sw;
+    A.occ[j] = 0;
+    A.pix_c[j] = A.pix[i];
+    A.sam_c[j] = A.sam[i];
+  }
+  const uint64_t b = __ballot(spawned);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(A.nshadow, (unsigned long long)__popcll(b));
+}
+
+// The frame totals as bits (byte 64 c + k = bit k of total c) behind the
+// occlusion bytes: one SUM all-reduce of bytes adds them up exactly (a
+// byte sums at most `world` ones).
+__global__ void k_rep_totals(uint8_t* __restrict__ tail, unsigned long long nrad,
+                             const unsigned long long* __restrict__ nshadow) {
+  const int k = threadIdx.x;  // 192 threads
+  const int c = k >> 6, b = k & 63;
+  const unsigned long long v = c == 0 ? nrad : (c == 1 ? *nshadow : 0ull);
+  tail[k] = uint8_t((v >> b) & 1ull);
+}
+
 }  // namespace
 
 #define LAUNCH(n, kern, ...)                                  \
@@ -364,6 +457,22 @@ hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_
 }
 hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
+}
+hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
+                            uint8_t* fl) {
+  LAUNCH(n, k_rep_flags, mask, n, rank, fc, fl);
+}
+hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
+                           int rank, const uint64_t* keys_n, uint64_t* keys_c) {
+  LAUNCH(nc, k_rep_keys, idx_c, nc, mask, rank, keys_n, keys_c);
+}
+hipError_t launch_rep_spawn(hipStream_t s, const RepSpawnArgs& a) {
+  LAUNCH(a.nc, k_rep_spawn, a);
+}
+hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
+                             const unsigned long long* nshadow) {
+  k_rep_totals<<<1, 192, 0, s>>>(tail, nrad, nshadow);
+  return hipGetLastError();
 }
 
 }  // namespace spray_rt

@@ -104,6 +104,12 @@ hipError_t launch_frame_stats_add(hipStream_t s, unsigned long long* stats, int 
 hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
                                         const spray_rt_ray* rays, size_t M,
                                         spray_rt_hit* hits, uint64_t* keys);
+// The same over rays idx[0..*d_num) (d_num <= max_n; ray ids < max_n):
+// hits[idx[j]] and keys[idx[j]] written.
+hipError_t launch_scene_intersect_keyed_indexed(hipStream_t s, const SceneView& v,
+                                                const spray_rt_ray* rays, size_t max_n,
+                                                const uint32_t* idx, const uint32_t* d_num,
+                                                spray_rt_hit* hits, uint64_t* keys);
 // out[i] = OR over the ray's domain list of (1 << owner[domain]); owner < 0:
 // unowned.  owner: device int[ndom], ranks < 64.  sel (optional): ray i is
 // rays[sel[i]]; valid (optional): only slots with valid[i] hold a ray (mask

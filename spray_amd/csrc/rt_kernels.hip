@@ -2765,6 +2765,19 @@ hipError_t launch_scene_intersect_keyed(hipStream_t s, const SceneView& v,
   return launch_scene_w<false, kEpiKeys>(s, a, v);
 }
 
+hipError_t launch_scene_intersect_keyed_indexed(hipStream_t s, const SceneView& v,
+                                                const spray_rt_ray* rays, size_t max_n,
+                                                const uint32_t* idx, const uint32_t* d_num,
+                                                spray_rt_hit* hits, uint64_t* keys) {
+  if (max_n == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, max_n);
+  a.idx = idx;
+  a.d_count = d_num;
+  a.hits = hits;
+  a.keys = keys;
+  return launch_scene_w<false, kEpiKeys>(s, a, v);
+}
+
 hipError_t launch_route(hipStream_t s, const SceneView& v, const int* owner,
                         const spray_rt_ray* rays, size_t M, uint64_t* out, const uint32_t* sel,
                         const uint8_t* valid, unsigned long long* nvalid) {

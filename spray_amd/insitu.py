@@ -98,7 +98,7 @@ _RED = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int)
 
 class Transport(C.Structure):
     _fields_ = [("user", C.c_void_p), ("alltoallv", _A2A), ("allreduce_u64", _AR),
-                ("reduce_f32", _RED)]
+                ("reduce_f32", _RED), ("allreduce_min_u64", _AR), ("allreduce_sum_u8", _AR)]
 
 
 class RecStruct(C.Structure):
@@ -157,7 +157,29 @@ class _HostCollectives:
                 print("insitu host reduce failed:", e)
                 return 1
 
-        self._cbs = (_A2A(a2a), _AR(ar), _RED(red))  # kept alive with the engine
+        def armin(user, data, n):
+            try:  # keys are < 2^63: int64 MIN is their u64 MIN
+                a = _host_view(data, 8 * n).view(np.int64)
+                t = torch.from_numpy(a.copy())
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+                a[:] = t.numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001
+                print("insitu host min all-reduce failed:", e)
+                return 1
+
+        def arsum8(user, data, n):
+            try:  # each byte sums at most `world` ones
+                a = _host_view(data, n)
+                t = torch.from_numpy(a.astype(np.int32))
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+                a[:] = t.numpy().astype(np.uint8)
+                return 0
+            except Exception as e:  # noqa: BLE001
+                print("insitu host byte all-reduce failed:", e)
+                return 1
+
+        self._cbs = (_A2A(a2a), _AR(ar), _RED(red), _AR(armin), _AR(arsum8))  # kept alive
         self.struct = Transport(None, *self._cbs)
 
 
@@ -260,6 +282,42 @@ class InsituEngine:
         self.rt._check(rc, "insitu_trace")
         return int(tot[0]), int(tot[1])
 
+    def trace_frame(self, shader, rays, pixid, samid, spp, image, records=None):
+        """The whole frame with replicated eye rays (spray_rt_insitu_trace_frame):
+        rays / pixid / samid are EVERY eye ray of the frame, the same on every
+        rank.  Returns the group's (radiance rays, shadow rays)."""
+        from .engine import _addr, _nbytes
+        n = _nbytes(rays) // 32
+        a, k1 = _addr(rays)
+        p, k2 = _addr(pixid)
+        s, k3 = _addr(samid)
+        im, k4 = _addr(image)
+        tot = (C.c_ulonglong * 3)()
+        rec = C.byref(records.struct) if records is not None else None
+        rc = lib().spray_rt_insitu_trace_frame(self.h, C.byref(shader), a, p, s, n, int(spp), im,
+                                               rec, C.byref(tot))
+        self.rt._check(rc, "insitu_trace_frame")
+        return int(tot[0]), int(tot[1])
+
+    def set_timing(self, on=True):
+        """Per-phase HIP-event timing of the traces (phase_times)."""
+        self.rt._check(lib().spray_rt_insitu_set_timing(self.h, 1 if on else 0), "set_timing")
+
+    REP_PHASES = ("lists", "keyed_closest_hit", "key_allreduce", "shadows",
+                  "occlusion_allreduce", "film", "totals")
+    PROTOCOL_PHASES = ("route_counts", "ray_exchange", "keyed_closest_hit", "key_composite",
+                       "shading", "shadow_route_exchange", "shadow_any_hit_return",
+                       "film_totals")
+
+    def phase_times(self):
+        """{phase: ms} accumulated since the last call (then reset)."""
+        out = (C.c_double * 8)()
+        n = C.c_int(0)
+        lib().spray_rt_insitu_phase_times(self.h, C.byref(out), C.byref(n))
+        names = {7: self.REP_PHASES, 8: self.PROTOCOL_PHASES, 1: ("frame",)}.get(
+            n.value, tuple("phase%d" % k for k in range(n.value)))
+        return {names[k]: float(out[k]) for k in range(n.value)}
+
     def composite(self, image):
         """HdrImage::composite: SUM of the ranks' images at rank 0."""
         from .engine import _addr
@@ -286,5 +344,6 @@ class _LocalCollectives:
                 C.memmove(recv, send, n)
             return 0
 
-        self._cbs = (_A2A(a2a), _AR(lambda u, d, n: 0), _RED(lambda u, d, n, r: 0))
+        self._cbs = (_A2A(a2a), _AR(lambda u, d, n: 0), _RED(lambda u, d, n, r: 0),
+                     _AR(lambda u, d, n: 0), _AR(lambda u, d, n: 0))
         self.struct = Transport(None, *self._cbs)

@@ -99,16 +99,19 @@ CASES = {  # name: (shader kind, bounces, samples, image size, spp)
 LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)]}
 
 
-def _engine_rank(rank, world, case, transport, dist=None, one_owner=False):
+def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, replicated=False,
+                 mode=0):
     """One rank's engine frame of CASES[case]: returns (records, totals, image).
-    one_owner: the last rank owns every domain (the others hold rays only)."""
+    one_owner: the last rank owns every domain (the others hold rays only).
+    replicated: spray_rt_insitu_trace_frame with every eye ray on every rank;
+    mode: the partition (GROUP_CLOSE / ROUND_ROBIN)."""
     import spray_amd
     from spray_amd import insitu
     from oracle import pyoracle as po
     from test_insitu import scene_boxes
     kind, bounces, samples, img, spp = CASES[case]
     boxes, bound = scene_boxes()
-    owner = insitu.morton_partition(boxes, bound, world)
+    owner = insitu.morton_partition(boxes, bound, world, mode)
     if one_owner:
         owner = np.full_like(owner, world - 1)
     rt = spray_amd.RtContext(0)
@@ -118,7 +121,7 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False):
     c = H.BENCH_CAMERA
     cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
     block = (0, 0, img, img)
-    stripe = insitu.horizontal_stripe(world, rank, block)
+    stripe = block if replicated else insitu.horizontal_stripe(world, rank, block)
     n = stripe[2] * stripe[3] * spp
     rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device="cuda")[:n]
     pix = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
@@ -129,9 +132,13 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False):
     eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport=transport)
     recs = insitu.InsituRecords(img * img * spp * bounces + 16)
     image = torch.zeros(img * img * 4, dtype=torch.float32, device="cuda")
-    tot = eng.trace(sh, rays, pix, sam, spp, image, recs)
+    trace = eng.trace_frame if replicated else eng.trace
+    eng.set_timing(True)
+    tot = trace(sh, rays, pix, sam, spp, image, recs)
     # a second trace reuses the engine's buffers: same totals, image doubles
-    tot2 = eng.trace(sh, rays, pix, sam, spp, image)
+    tot2 = trace(sh, rays, pix, sam, spp, image)
+    ph = eng.phase_times()
+    assert ph and all(v >= 0 for v in ph.values()), ph
     assert tot2 == tot
     image.mul_(0.5)
     st = eng.stats()
@@ -203,7 +210,7 @@ def test_engine_one_rank_protocol_forced(oracle, monkeypatch):
     assert res[3]["exchanges"] > 0
 
 
-def _gpu_rank_main(rank, world, port, out, case, one_owner=False):
+def _gpu_rank_main(rank, world, port, out, case, one_owner=False, replicated=False, mode=0):
     import pickle
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -213,7 +220,7 @@ def _gpu_rank_main(rank, world, port, out, case, one_owner=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _engine_rank(rank, world, case, "host", dist, one_owner)
+        res = _engine_rank(rank, world, case, "host", dist, one_owner, replicated, mode)
         with open(os.path.join(out, "r%d.pkl" % rank), "wb") as fh:
             pickle.dump(res, fh)
     finally:
@@ -256,6 +263,43 @@ def test_engine_two_ranks_one_owner(oracle):
     _check(oracle, "pt1", res)
     assert len(res[0][0]["samid"]) == 0 and len(res[1][0]["samid"]) > 50
     assert res[0][3]["bytes_sent"] > 0
+
+
+@pytest.mark.parametrize("world,mode", [(2, 0), (8, 0), (8, 1), (3, 1)])
+def test_engine_replicated_frame_ranks(oracle, world, mode):
+    """spray_rt_insitu_trace_frame with world processes sharing the GPU over
+    the host transport: every eye ray on every rank, the keys' MIN and the
+    occlusion bytes' SUM all-reduced (the host transport's
+    allreduce_min_u64 / allreduce_sum_u8) -- every shaded sample bit-exact
+    against the whole-scene oracle, totals exact, the image within
+    summation-order tolerance; both partitions."""
+    import pickle
+    with tempfile.TemporaryDirectory() as out:
+        torch.multiprocessing.spawn(_gpu_rank_main,
+                                    args=(world, _free_port(), out, "pt1", False, True, mode),
+                                    nprocs=world)
+        res = []
+        for r in range(world):
+            with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
+                res.append(pickle.load(fh))
+    _check(oracle, "pt1", res)
+    assert sum(len(r[0]["samid"]) > 50 for r in res) >= max(2, world // 2)
+    for r in res:  # two all-reduces and one host read per frame, no exchange
+        assert r[3]["exchanges"] == 0 and r[3]["host_count_reads"] == 2
+
+
+def test_engine_replicated_frame_one_rank_rccl(oracle):
+    """World 1 through RCCL: trace_frame takes the all-local fused frame."""
+    res = _engine_rank(0, 1, "pt1", "rccl", replicated=True)
+    _check(oracle, "pt1", [res])
+
+
+def test_engine_replicated_frame_unsupported_shading(oracle):
+    """AO (or several bounces) is not a replicated frame: UNSUPPORTED, and
+    nothing traced."""
+    import spray_amd
+    with pytest.raises(spray_amd.SprayRtError, match="-6|replicated"):
+        _engine_rank(0, 1, "ao16", "rccl", replicated=True)
 
 
 def test_domain_mask_exact_on_box_boundaries(spray, oracle):

@@ -142,7 +142,7 @@ CASES = {  # name: (shader kind, bounces, samples, image size, spp)
 LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)]}
 
 
-def _rank_main(rank, world, port, out, case, mode=0):
+def _rank_main(rank, world, port, out, case, mode=0, replicated=False):
     import pickle
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -160,15 +160,18 @@ def _rank_main(rank, world, port, out, case, mode=0):
         c = H.BENCH_CAMERA
         cam = po.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
         block = (0, 0, img, img)
-        stripe = insitu.horizontal_stripe(world, rank, block)
+        # replicated frames: every rank holds every eye ray of the frame
+        stripe = block if replicated else insitu.horizontal_stripe(world, rank, block)
         org, d, pix, sam = po.eye_rays_insitu(cam, img, spp, block, stripe)
         sh = H.insitu_shader(po, kind, bounces, samples, LIGHTS.get(case))
         bs = po.scene_bsdfs(local.domains)
         image = np.zeros(img * img * 4, np.float32)
         comm = insitu_ref.Comm(dist if world > 1 else None)
-        recs, tot = insitu_ref.trace_frame(po, local, comm, sh, bs, org, d, pix, sam, spp, image)
+        fn = insitu_ref.trace_frame_replicated if replicated else insitu_ref.trace_frame
+        recs, tot = fn(po, local, comm, sh, bs, org, d, pix, sam, spp, image)
         with open(os.path.join(out, "r%d.pkl" % rank), "wb") as fh:
-            pickle.dump({"recs": recs, "tot": tot, "image": image, "n": len(org)}, fh)
+            pickle.dump({"recs": recs, "tot": tot, "image": image,
+                         "n": len(org) if (rank == 0 or not replicated) else 0}, fh)
     finally:
         if world > 1:
             dist.destroy_process_group()
@@ -177,15 +180,16 @@ def _rank_main(rank, world, port, out, case, mode=0):
 @pytest.mark.parametrize("world,case,mode", [(1, "pt1", 0), (2, "pt1", 0), (3, "pt1", 0),
                                              (2, "pt3", 0), (8, "pt1", 0), (8, "ao16", 0),
                                              (8, "pt3", 0), (8, "pt1", 1), (3, "pt3", 1)])
-def test_insitu_protocol_gloo(oracle, world, case, mode):
+def test_insitu_protocol_gloo(oracle, world, case, mode, replicated=False):
     import pickle
     import insitu_helpers as H
     with tempfile.TemporaryDirectory() as out:
         port = _free_port()
         if world == 1:
-            _rank_main(0, 1, port, out, case, mode)
+            _rank_main(0, 1, port, out, case, mode, replicated)
         else:
-            torch.multiprocessing.spawn(_rank_main, args=(world, port, out, case, mode),
+            torch.multiprocessing.spawn(_rank_main,
+                                        args=(world, port, out, case, mode, replicated),
                                         nprocs=world)
         res = []
         for r in range(world):
@@ -211,3 +215,13 @@ def test_insitu_protocol_gloo(oracle, world, case, mode):
     total = np.sum([r["image"] for r in res], axis=0)
     assert (ref_img > 0).sum() > 500
     np.testing.assert_allclose(total, ref_img, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("world,mode", [(1, 0), (2, 0), (3, 1), (8, 0), (8, 1)])
+def test_replicated_frame_gloo(oracle, world, mode):
+    """The replicated-ray frame (insitu.cpp trace_replicated, restated in
+    oracle/insitu_ref.py): every rank holds all eye rays, one MIN all-reduce
+    of the keys and one SUM all-reduce of the occlusion bytes -- the same
+    shaded samples, bits and totals as the whole-scene oracle, for the
+    GROUP_CLOSE and ROUND_ROBIN partitions."""
+    test_insitu_protocol_gloo(oracle, world, "pt1", mode, replicated=True)
