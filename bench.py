@@ -181,18 +181,26 @@ def cpu_baseline(target_s=10.0):
                       "%.1f s traversal+spawn" % (reps, n, threads, dt)}
 
 
-def run_insitu(args, dist, world, rank, local, cam, kind="pt"):
+def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     """configs[2] (kind "pt": one bounce, the scene's point light) and
-    configs[4] (kind "ao": 16 AO rays per hit): one in-situ frame per step.
-    The domains are sharded by the reference's Morton partition (64/N per
-    GPU), each rank's eye rays are its horizontal stripe of the frame (one
-    blocking tile = the frame; HBM holds it), and the engine's in-situ tracer
-    (spray_rt_insitu_trace) moves the rays to their domains' owners with
-    count-first RCCL all-to-all-v exchanges, composites the hit keys, shades
-    at the winner, exchanges the shadow rays and films; the ranks' images are
-    composited by one RCCL reduce (HdrImage::composite).  Eye rays are made
-    once before timing (resident, like the main line).  RCCL is used at every
-    N, N = 1 included.  Timed like the main line (barrier + max over ranks)."""
+    configs[4] (kind "ao": 16 AO rays per hit): one in-situ frame per step,
+    the domains sharded by the reference's Morton partition (64/N per GPU;
+    --partition: GROUP_CLOSE or ROUND_ROBIN).
+
+    PT at N > 1 is the replicated-ray frame (spray_rt_insitu_trace_frame):
+    every rank holds the frame's eye rays, traces the rays that touch its
+    domains over its domains, and the ranks agree on every ray's winner with
+    one MIN all-reduce of the hit keys and on every shadow ray's occlusion with
+    one SUM all-reduce of bytes -- no ray crosses the wire.  AO (and
+    protocol=True) is the stripe protocol (spray_rt_insitu_trace): each rank
+    its horizontal stripe of eye rays, count-first RCCL all-to-all-v exchanges
+    of rays to their owners, key composite, shading at the winner, shadow
+    exchange.  The ranks' images are composited by one RCCL reduce
+    (HdrImage::composite).  Eye rays are made once before timing (resident,
+    like the main line).  RCCL is used at every N, N = 1 included (at N = 1
+    PT runs the all-local fused frame unless protocol=True).  Timed like the
+    main line (barrier + max over ranks); the per-phase device times come
+    from a separate pass with HIP-event timing on."""
     import torch
     import spray_amd
     from spray_amd import insitu
@@ -200,14 +208,16 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt"):
     dev = torch.device("cuda", local)
     boxes, lights = host_parse_scene(SCENE, SCENES)
     bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
-    owner = insitu.morton_partition(boxes, bound, world)
+    mode = insitu.PARTITION_ROUND_ROBIN if args.partition == "rr" else insitu.PARTITION_GROUP_CLOSE
+    owner = insitu.morton_partition(boxes, bound, world, mode)
     rt = spray_amd.RtContext(local)
     insitu.setup_rank_context(rt, SCENE, SCENES, owner, rank)
     rt.set_bsdfs(host_scene_bsdfs(SCENE))
     rt.set_stream(torch.cuda.current_stream(dev))
     eng = insitu.InsituEngine(rt, world, rank, dist=dist if world > 1 else None,
                               transport="host" if REHEARSE else "rccl")
-    stripe = insitu.horizontal_stripe(world, rank, (0, 0, W, H))
+    replicated = kind == "pt" and not protocol
+    stripe = (0, 0, W, H) if replicated else insitu.horizontal_stripe(world, rank, (0, 0, W, H))
     n = stripe[2] * stripe[3] * SPP
     rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)[:n]
     pix = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
@@ -220,47 +230,74 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt"):
         sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
                                          lights=lights)
     image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    old_local = os.environ.get("SPRAY_INSITU_LOCAL")
+    if protocol:
+        os.environ["SPRAY_INSITU_LOCAL"] = "0"  # the whole protocol, even at one rank
+    trace = eng.trace_frame if replicated else eng.trace
 
     def frame():
         image.zero_()
-        t = eng.trace(sh, rays, pix, sam, SPP, image)
+        t = trace(sh, rays, pix, sam, SPP, image)
         eng.composite(image)
         return t
 
-    tot = None
-    for _ in range(max(args.warmup, 1)):
-        tot = frame()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    s0 = eng.stats()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tot = frame()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    s1 = eng.stats()
+    try:
+        tot = None
+        for _ in range(max(args.warmup, 1)):
+            tot = frame()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        s0 = eng.stats()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tot = frame()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        s1 = eng.stats()
+        # per-phase device times (HIP events on the stream), a separate pass
+        eng.set_timing(True)
+        eng.phase_times()
+        nph = 3
+        for _ in range(nph):
+            frame()
+        torch.cuda.synchronize()
+        phases = {k: round(v / nph, 4) for k, v in eng.phase_times().items()}
+        eng.set_timing(False)
+    finally:
+        if protocol:
+            if old_local is None:
+                os.environ.pop("SPRAY_INSITU_LOCAL", None)
+            else:
+                os.environ["SPRAY_INSITU_LOCAL"] = old_local
     if world > 1:
         e = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e.item())
     rays_step = tot[0] + tot[1]
     k = args.steps
+    form = ("replicated-ray frame: every rank traces the rays that touch its domains, "
+            "keys MIN-all-reduced, occlusion bytes SUM-all-reduced" if replicated and world > 1
+            else "all-local fused frame" if replicated or (world == 1 and not protocol)
+            else "stripe protocol: speculative ray exchange over RCCL all-to-all-v")
     out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
            "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
            "rays_per_step": rays_step, "radiance_rays": tot[0], "shadow_rays": tot[1],
            "rank0_MB_sent_per_step": round((s1["bytes_sent"] - s0["bytes_sent"]) / k / 1e6, 2),
            "rank0_host_count_reads_per_step": (s1["host_count_reads"] -
                                                s0["host_count_reads"]) / k,
+           "rank0_collectives_per_step": (s1["collectives"] - s0["collectives"]) / k,
+           "rank0_phases_ms": phases,
            "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
-           "config": "%s: 64 domains, %d per GPU (Morton partition), 1024x1024x8spp frame in "
-                     "%d horizontal stripes, %s, speculative ray exchange over RCCL "
-                     "all-to-all-v, image composite by RCCL reduce"
+           "partition": args.partition,
+           "config": "%s: 64 domains, %d per GPU (Morton partition, %s), 1024x1024x8spp, %s, %s, "
+                     "image composite by RCCL reduce"
                      % ("configs[4]" if kind == "ao" else "configs[2]",
-                        int(np.bincount(owner, minlength=world)[rank]), world,
-                        "AO-16 rays per hit" if kind == "ao" else "PT point-light shadows")}
+                        int(np.bincount(owner, minlength=world)[rank]),
+                        "round robin" if mode == insitu.PARTITION_ROUND_ROBIN else "close groups",
+                        "AO-16 rays per hit" if kind == "ao" else "PT point-light shadows", form)}
     eng.close()
     rt.close()
     return out
@@ -464,6 +501,9 @@ def main():
     ap.add_argument("--insitu", type=int, default=1,
                     help="also measure configs[2] through the engine's RCCL in-situ tracer "
                          "(always on with more than one rank: it is the headline there)")
+    ap.add_argument("--partition", choices=("close", "rr"), default="close",
+                    help="in-situ domain partition: close (GROUP_CLOSE_DOMAINS, the reference's "
+                         "compiled mode) or rr (round robin over the Morton order)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
@@ -618,6 +658,10 @@ def main():
     }
     if args.insitu != 0 or world > 1:
         out["insitu"] = run_insitu(args, dist, world, rank, local, cam)
+    if world == 1 and args.insitu != 0:
+        # the exchange protocol N > 1 AO frames use, timed at one rank through
+        # the one-rank RCCL communicator (SPRAY_INSITU_LOCAL=0), phase split
+        out["insitu_protocol"] = run_insitu(args, dist, world, rank, local, cam, protocol=True)
     if world > 1:
         # configs[2] is the N > 1 headline: the frame split across the GPUs by
         # domain (strong scaling); the frame replicas stay as a secondary key

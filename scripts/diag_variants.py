@@ -2,10 +2,14 @@
 
     python scripts/diag_variants.py build     # here: compiles the variants
     python scripts/diag_variants.py run       # GPU box: times each variant
+    python scripts/diag_variants.py check     # GPU box: AO parity tests per variant
 
 Variants: SPRAY_DIAG_MODE=1 (domain mask only), 2 (mask + ordered domain
-selection, no BVH), and the shipped kernel.  Prints the bench's per-kernel
-milliseconds for each.
+selection, no BVH), the any-hit variants of spray_amd/csrc/rt_kernels_diag.inc
+(SPRAY_AH_SPREAD=1, SPRAY_AO_REFILL=32 -- re-packing schemes measured slower
+than the shipped walk), and the shipped kernel.  "run" prints the bench's
+per-kernel milliseconds for each; "check" runs tests/test_gpu_ao.py against
+each any-hit variant (they must stay bit-exact).
 """
 import json
 import os
@@ -15,7 +19,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DIAG = os.path.join(ROOT, "spray_amd", "lib", "diag")
-VARIANTS = {"mask_only": ["SPRAY_DIAG_MODE=1"], "mask_select": ["SPRAY_DIAG_MODE=2"]}
+VARIANTS = {"mask_only": ["SPRAY_DIAG_MODE=1"], "mask_select": ["SPRAY_DIAG_MODE=2"],
+            "ah_spread": ["SPRAY_AH_SPREAD=1"], "ao_refill": ["SPRAY_AO_REFILL=32"]}
+CHECKED = ("ah_spread", "ao_refill")  # bit-exact variants: parity tests apply
 EXTRA = dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a)  # name=DEF1,DEF2
 
 
@@ -48,5 +54,19 @@ def run():
               flush=True)
 
 
+def check():
+    bad = 0
+    for name in CHECKED:
+        lib = os.path.join(DIAG, "libspray_rt_%s.so" % name)
+        env = dict(os.environ, SPRAY_RT_LIB=lib)
+        r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "--timeout",
+                            "300", os.path.join(ROOT, "tests", "test_gpu_ao.py")], env=env,
+                           capture_output=True, text=True, timeout=900)
+        print(name, "rc", r.returncode, r.stdout.strip().splitlines()[-1] if r.stdout else "",
+              flush=True)
+        bad += r.returncode != 0
+    sys.exit(1 if bad else 0)
+
+
 if __name__ == "__main__":
-    build() if sys.argv[1] == "build" else run()
+    {"build": build, "run": run, "check": check}[sys.argv[1]]()

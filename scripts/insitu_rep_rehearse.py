@@ -1,0 +1,158 @@
+"""Per-rank device time of the replicated-ray in-situ frame at N ranks,
+rehearsed on ONE GPU (the input of scripts/insitu_rep_projection.py).
+
+    python scripts/insitu_rep_rehearse.py --worlds 2 4 8 --modes close rr \
+        --out gpurun_out/rep/rehearse.json
+
+For each (N, partition) N processes share the GPU, each an engine rank with
+its 64/N domains (gloo + the engine's host transport), and trace the bench
+frame (1024x1024x8spp, PT) with spray_rt_insitu_trace_frame.  With
+SPRAY_INSITU_SERIAL the ranks' device work runs one rank at a time (a file
+lock released while a rank waits in a collective), so the per-phase HIP-event
+times of a rank are its own kernels' times, not shared-GPU contention.  The
+collectives' times (host-staged here) are NOT measurements of RCCL: the
+projection models them.  Also measured: the one-rank RCCL all-reduce of the
+frame's message sizes (the per-call floor of the real collectives).
+"""
+import argparse
+import json
+import os
+import socket
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+SCENE = os.path.join(SCENES, "wavelets64.spray")
+CAM = dict(pos=[90.172180, 84.141418, 82.480225], lookat=[30.0, 28.649426, 30.0],
+           up=[0.0, 1.0, 0.0], fov=90.0)
+W = H = 1024
+SPP = 8
+SHADE = [0.0, 500.0, 1000.0, 1.0, 1.0, 1.0, 0.4, 0.4, 0.4, 10.0]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, mode, frames, out):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import spray_amd
+    from spray_amd import insitu
+    from spray_amd.engine import host_parse_scene, host_scene_bsdfs
+    boxes, lights = host_parse_scene(SCENE, SCENES)
+    bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
+    pm = insitu.PARTITION_ROUND_ROBIN if mode == "rr" else insitu.PARTITION_GROUP_CLOSE
+    owner = insitu.morton_partition(boxes, bound, world, pm)
+    rt = spray_amd.RtContext(0)
+    insitu.setup_rank_context(rt, SCENE, SCENES, owner, rank)
+    rt.set_bsdfs(host_scene_bsdfs(SCENE))
+    stream = torch.cuda.Stream()
+    rt.set_stream(stream)
+    eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport="host")
+    cam = spray_amd.camera_init(CAM["pos"], CAM["lookat"], CAM["up"], CAM["fov"], W, H)
+    n = W * H * SPP
+    rays = torch.empty((n, 8), dtype=torch.float32, device="cuda")
+    pix = torch.empty(n, dtype=torch.int32, device="cuda")
+    sam = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), (0, 0, W, H), rays, pix, sam)
+    sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
+                                     lights=lights)
+    image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    rt.sync()
+    tot = eng.trace_frame(sh, rays, pix, sam, SPP, image)  # warm-up (buffers)
+    eng.set_timing(True)
+    eng.phase_times()
+    for _ in range(frames):
+        tot = eng.trace_frame(sh, rays, pix, sam, SPP, image)
+    ph = {k: v / frames for k, v in eng.phase_times().items()}
+    res = {"rank": rank, "domains": int((owner == rank).sum()), "phases_ms": ph,
+           "totals": list(tot), "stats": eng.stats()}
+    with open(os.path.join(out, "r%d.json" % rank), "w") as fh:
+        json.dump(res, fh)
+    eng.close()
+    rt.close()
+    dist.destroy_process_group()
+
+
+def rccl_floor(sizes):
+    """One-rank RCCL all-reduce time per message size (ms): the per-call
+    floor of the frame's collectives (no link traffic at one rank)."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    out = {}
+    for name, (nbytes, dtype, op) in sizes.items():
+        t = torch.zeros(max(nbytes // torch.tensor([], dtype=dtype).element_size(), 1),
+                        dtype=dtype, device="cuda")
+        for _ in range(5):
+            dist.all_reduce(t, op=op)
+        torch.cuda.synchronize()
+        k = 50
+        t0 = time.perf_counter()
+        for _ in range(k):
+            dist.all_reduce(t, op=op)
+        torch.cuda.synchronize()
+        out[name] = {"bytes": nbytes, "ms": (time.perf_counter() - t0) / k * 1e3}
+    dist.destroy_process_group()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--modes", nargs="+", default=["close", "rr"])
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--out", default="gpurun_out/rep/rehearse.json")
+    ap.add_argument("--rccl-floor", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+    import torch.multiprocessing as mp
+    os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+    lock = os.path.join(tempfile.gettempdir(), "spray_insitu_serial_%d.lock" % os.getpid())
+    os.environ["SPRAY_INSITU_SERIAL"] = lock
+    report = {"frame": "wavelets64 1024x1024x8spp PT (configs[2]), replicated-ray frame",
+              "runs": []}
+    for mode in args.modes:
+        for world in args.worlds:
+            t0 = time.time()
+            with tempfile.TemporaryDirectory() as out:
+                mp.spawn(_rank, args=(world, _port(), mode, args.frames, out), nprocs=world)
+                ranks = [json.load(open(os.path.join(out, "r%d.json" % r))) for r in range(world)]
+            report["runs"].append({"world": world, "partition": mode, "ranks": ranks})
+            print("world %d %s: %.1f s; per-rank phase sums (ms): %s" % (
+                world, mode, time.time() - t0,
+                [round(sum(r["phases_ms"].values()), 3) for r in ranks]), flush=True)
+            with open(args.out, "w") as fh:
+                json.dump(report, fh, indent=1)
+    os.environ.pop("SPRAY_INSITU_SERIAL", None)
+    if args.rccl_floor:
+        nc = 2600000  # ~ rays of the bench frame with a non-empty domain list
+        report["rccl_one_rank_floor"] = rccl_floor({
+            "keys_min_u64": (8 * nc, torch.int64, torch.distributed.ReduceOp.MIN),
+            "occ_sum_u8": (nc + 192, torch.uint8, torch.distributed.ReduceOp.SUM),
+            "image_16MB": (W * H * 16, torch.float32, torch.distributed.ReduceOp.SUM),
+            "small_8B": (8, torch.int64, torch.distributed.ReduceOp.SUM)})
+        print("rccl floor:", report["rccl_one_rank_floor"], flush=True)
+    with open(args.out, "w") as fh:
+        json.dump(report, fh, indent=1)
+    try:
+        os.unlink(lock)
+    except OSError:
+        pass
+
+
+if __name__ == "__main__":
+    main()

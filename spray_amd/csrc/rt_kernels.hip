@@ -535,233 +535,23 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   }
 }
 
-// Per-lane any hit as one wave-collective loop, with the leaf triangles of
-// all lanes spread over the wave.  Each lane walks its own ray through the
-// 4-wide quantized trees of its domains (occluded_tree_q4's step: nearest
-// entered child next, the others pushed, a first leaf parked while the lane
-// keeps descending), but the lanes never leave the loop on their own: a
-// lane whose walk of a domain ends picks its next domain at the top of the
-// loop (no per-domain wave barrier), and when every stepping lane holds a
-// leaf, the parked leaves -- plus a second leaf a walk stopped on -- become
-// (lane, triangle) tasks dealt out to all 64 lanes (ballot prefix of the
-// counts, owner lane per task in LDS, the owner's ray and triangle array by
-// cross-lane reads).  A lane with per-lane leaf tests idles while the lane
-// with the most triangles tests them: scripts/walk_sim.py measures the
-// triangle iterations per 64 AO-16 rays 24.4 -> 9.7 (lane use 0.28 ->
-// 0.80).  Every triangle of the parked leaves is tested (no early exit
-// inside one phase); occlusion is an OR, so the bits are the per-lane
-// walk's.  wtask: 8 * 64 owner bytes of the wave, whit: 64 hit bytes.
+// Diagnostic variants of the any hit (rt_kernels_diag.inc, compiled only
+// into the builds that enable them: SPRAY_AH_SPREAD=1 -- the leaf triangles
+// of all lanes spread over the wave; SPRAY_AO_REFILL=R -- lane refill of the
+// persistent AO any hit).  Both bit-exact and slower than the shipped walk
+// ("Lane re-packing"); scripts/diag_variants.py builds
+// and checks them.
 #ifndef SPRAY_AH_SPREAD
 #define SPRAY_AH_SPREAD 0
 #endif
 template <int W, int STK, int EPI>
-__device__ __forceinline__ void scene_ray_ah_wave(const SceneArgs& A, size_t i, bool valid,
-                                                  const float4* stl, const float* sbox,
-                                                  const float4* sdom, int32_t* stk,
-                                                  int32_t* wstk, uint8_t* wtask, uint8_t* whit) {
-  const uint32_t lane = threadIdx.x & 63;
-  v4f a = v4f{0.f, 0.f, 0.f, kRayEpsilon}, b = v4f{0.f, 0.f, 1.f, kInf};
-  if (valid) {
-    if (EPI == kEpiAoGen) {
-      ao_gen(A, i, a, b);
-    } else {
-      const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
-      a = __builtin_nontemporal_load(rp);
-      b = __builtin_nontemporal_load(rp + 1);
-    }
-  }
-  const float4 o4 = make_float4(a.x, a.y, a.z, a.w), d4 = make_float4(b.x, b.y, b.z, b.w);
-  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  const float tnear = o4.w, tfar = d4.w;
-  uint64_t m[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) m[w] = 0;
-  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
-  bool alive = valid, occluded = false;
-  // the lane's current domain walk
-  QRay qr{};
-  const char* nbytes = nullptr;
-  uint64_t tris_u = 0;
-  int32_t cur = kNone, leaf = kNone;
-  constexpr int kOvf = kQ4Stack > STK ? kQ4Stack - STK : 1;
-  int32_t ovf[kOvf];
-  int sp = 0;
-  auto push = [&](int32_t v) {
-    if (STK >= kQ4Stack || sp < STK)
-      stk[sp * kBlock] = v;
-    else
-      ovf[sp - STK] = v;
-    ++sp;
-  };
-  auto pop = [&]() -> int32_t {
-    if (sp == 0) return kNone;
-    --sp;
-    return (STK >= kQ4Stack || sp < STK) ? stk[sp * kBlock] : ovf[sp - STK];
-  };
-  for (;;) {
-    // lanes between walks: the nearest remaining domain of the list (the
-    // reference's intersectAabb entry t; the order only steers early exit)
-    if (alive && cur == kNone && leaf == kNone) {
-      float dx = r.dx, dy = r.dy, dz = r.dz;
-      asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
-      const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
-      for (;;) {
-        bool any_left = false;
-#pragma unroll
-        for (int w = 0; w < W; ++w) any_left |= m[w] != 0;
-        if (!any_left) {
-          alive = false;
-          break;
-        }
-        float st = kInf;
-        int sb = -1;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          uint64_t bits = m[w];
-          while (bits) {
-            const int j = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            const int bx = 64 * w + j;
-            float tm;
-            aabb_ref(sbox + 6 * bx, dr, tm);
-            if (sb < 0 || tm < st) {
-              st = tm;
-              sb = bx;
-            }
-          }
-        }
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
-        const float4 dt = sdom[sb];
-        nbytes = reinterpret_cast<const char*>(
-            (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
-        if (!nbytes) continue;  // not resident here (or empty)
-        tris_u = uint64_t(nbytes) + __float_as_uint(dt.z);
-        const float4 base = ld4(nbytes - sizeof(QGrid), 0);
-        const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
-        // make_ray's inverse, recomputed (same bits) rather than held live
-        // through the walk: the registers go to the 8-waves-per-SIMD budget
-        const float ix = 1.0f / clamp_dir(dx), iy = 1.0f / clamp_dir(dy),
-                    iz = 1.0f / clamp_dir(dz);
-        q_axis(base.x, scale.x, ix, r.ox * ix, qr.ix, qr.olx, qr.ohx);
-        q_axis(base.y, scale.y, iy, r.oy * iy, qr.iy, qr.oly, qr.ohy);
-        q_axis(base.z, scale.z, iz, r.oz * iz, qr.iz, qr.olz, qr.ohz);
-        cur = 0;
-        sp = 0;
-        break;
-      }
-    }
-    if (!__ballot(alive)) break;
-    // node steps until every stepping lane holds a leaf
-    for (;;) {
-      const bool step = alive && cur >= 0 && cur != kNone;
-      if (!__ballot(step)) break;
-      if (step) {
-        const char* qp = nbytes - 128 - 64 * size_t(cur);
-        const float4 qa = ld4(qp, 0), qb = ld4(qp, 1), qc = ld4(qp, 2), qd = ld4(qp, 3);
-        const int32_t ref[4] = {__float_as_int(qd.x), __float_as_int(qd.y), __float_as_int(qd.z),
-                                __float_as_int(qd.w)};
-        float t[4];
-        bool h[4];
-        h[0] = slab_q(qr, q_lo(qa.x), q_hi(qa.x), q_lo(qa.y), q_hi(qa.y), q_lo(qa.z), q_hi(qa.z),
-                      tnear, tfar, t[0]);
-        h[1] = slab_q(qr, q_lo(qa.w), q_hi(qa.w), q_lo(qb.x), q_hi(qb.x), q_lo(qb.y), q_hi(qb.y),
-                      tnear, tfar, t[1]);
-        h[2] = slab_q(qr, q_lo(qb.z), q_hi(qb.z), q_lo(qb.w), q_hi(qb.w), q_lo(qc.x), q_hi(qc.x),
-                      tnear, tfar, t[2]);
-        h[3] = slab_q(qr, q_lo(qc.y), q_hi(qc.y), q_lo(qc.z), q_hi(qc.z), q_lo(qc.w), q_hi(qc.w),
-                      tnear, tfar, t[3]);
-        int32_t next = kNone;
-        float tn = kInf;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!h[k] || ref[k] == kNoChildRef) continue;
-          if (next == kNone || t[k] < tn) {
-            if (next != kNone) push(next);
-            next = ref[k];
-            tn = t[k];
-          } else {
-            push(ref[k]);
-          }
-        }
-        cur = next != kNone ? next : pop();
-        if (cur < 0 && cur != kNone && leaf == kNone) {  // park the leaf, keep descending
-          leaf = cur;
-          cur = pop();
-        }
-      }
-      if (__ballot(step && leaf == kNone) == 0) break;
-    }
-    // the parked leaf and a second leaf the walk stopped on, as tasks
-    uint32_t f0 = 0, c0 = 0, f1 = 0, c1 = 0;
-    if (alive && leaf != kNone) {
-      const uint32_t e0 = ~uint32_t(leaf);
-      f0 = e0 >> 2;
-      c0 = (e0 & 3u) + 1u;
-      leaf = kNone;
-      if (cur < 0 && cur != kNone) {
-        const uint32_t e1 = ~uint32_t(cur);
-        f1 = e1 >> 2;
-        c1 = (e1 & 3u) + 1u;
-        cur = pop();
-      }
-    }
-    const uint32_t nt = c0 + c1;  // 0..8: four bits
-    uint32_t off = 0, T = 0;
-#pragma unroll
-    for (int bit = 0; bit < 4; ++bit) {
-      const uint64_t bm = __ballot((nt >> bit) & 1u);
-      off += uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(bm >> 32),
-                                                __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u)))
-             << bit;
-      T += uint32_t(__popcll(bm)) << bit;
-    }
-    if (T) {
-      for (uint32_t j = 0; j < nt; ++j) wtask[off + j] = uint8_t(lane);
-      whit[lane] = 0;
-      wave_lds_sync();
-      for (uint32_t base = 0; base < T; base += 64) {
-        const uint32_t t = base + lane;
-        const bool ok = t < T;
-        const int ow = ok ? int(wtask[t]) : int(lane);
-        const uint32_t j = t - uint32_t(__shfl(int(off), ow));
-        const uint32_t of0 = uint32_t(__shfl(int(f0), ow)), oc0 = uint32_t(__shfl(int(c0), ow)),
-                       of1 = uint32_t(__shfl(int(f1), ow));
-        const uint64_t otris = (uint64_t(uint32_t(__shfl(int(uint32_t(tris_u >> 32)), ow))) << 32) |
-                               uint32_t(__shfl(int(uint32_t(tris_u)), ow));
-        Ray ro;
-        ro.ox = __shfl(r.ox, ow);
-        ro.oy = __shfl(r.oy, ow);
-        ro.oz = __shfl(r.oz, ow);
-        ro.dx = __shfl(r.dx, ow);
-        ro.dy = __shfl(r.dy, ow);
-        ro.dz = __shfl(r.dz, ow);
-        const float otn = EPI == kEpiAoGen ? kRayEpsilon : __shfl(tnear, ow);
-        const float otf = EPI == kEpiAoGen ? kInf : __shfl(tfar, ow);
-        if (ok) {
-          const uint32_t p = j < oc0 ? of0 + j : of1 + (j - oc0);
-          float4 ta, tb, tc;
-          ld_tri(reinterpret_cast<const void*>(otris), p, ta, tb, tc);
-          float th, tu, tv;
-          if (tri_test(ro, otn, ta, tb, tc, th, tu, tv) && th <= otf) whit[ow] = 1;
-        }
-      }
-      wave_lds_sync();
-      if (alive && whit[lane]) {
-        occluded = true;
-        alive = false;
-      }
-      wave_lds_sync();  // the next phase rewrites wtask / whit
-    }
-    // a popped entry that is a leaf is parked for the next phase
-    if (alive && cur < 0 && cur != kNone) {
-      leaf = cur;
-      cur = pop();
-    }
-  }
-  if (valid) A.occ[i] = occluded ? 1 : 0;
-}
+__device__ void scene_ray_ah_wave(const SceneArgs& A, size_t i, bool valid, const float4* stl,
+                                  const float* sbox, const float4* sdom, int32_t* stk,
+                                  int32_t* wstk, uint8_t* wtask, uint8_t* whit);
+template <int W, int STK, uint32_t kMin, uint32_t kChunk>
+__device__ void scene_ray_ah_refill(const SceneArgs& A, size_t M, size_t S, const float4* stl,
+                                    const float* sbox, const float4* sdom, int32_t* stk,
+                                    int32_t* wstk);
 
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t x;
@@ -769,271 +559,9 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 
-// Wave-uniform cursor over the persistent launch's band queues: a wave's
-// own XCD's queues first (from the one its block index picks), then the
-// others -- the visit order of k_scene's persistent loop.
-struct BandCursor {
-  uint32_t k;         // next queue of the visit order to dequeue from
-  size_t cur, end;    // the current chunk's undealt pairs [cur, end)
-};
-
-// Dequeues the next chunk of kChunk pairs into bc (uniform control flow:
-// every lane of the wave active).  false once every queue is drained.
-template <uint32_t kChunk>
-__device__ __forceinline__ bool band_next(const SceneArgs& A, size_t M, size_t S, uint32_t xcd,
-                                          uint32_t sub, BandCursor& bc) {
-  constexpr uint32_t kPerXcd = kQueues / 8;
-  const uint32_t lane = threadIdx.x & 63;
-  while (bc.k < uint32_t(kQueues)) {
-    const uint32_t k = bc.k;
-    const uint32_t q = ((xcd + k / kPerXcd) & 7u) * kPerXcd + (sub + k) % kPerXcd;
-    const size_t begin = size_t(q) * S;
-    const size_t end = begin + S < M ? begin + S : M;
-    if (begin < end) {
-      uint32_t* head = &A.heads[32 * q];
-      uint32_t base = 0;
-      if (lane == 0) {
-        base = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (begin + base < end) base = atomicAdd(head, kChunk);
-      }
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (begin + base < end) {
-        bc.cur = begin + base;
-        bc.end = bc.cur + kChunk < end ? bc.cur + kChunk : end;
-        return true;
-      }
-    }
-    ++bc.k;
-  }
-  return false;
-}
-
-// The AO any hit of a persistent wave with lane refill (north-star: re-pack
-// the active lanes under divergent traversal).  Each lane walks its own ray
-// through the 4-wide quantized trees of its domains (occluded_tree_q4's
-// while-while step, as one wave-collective loop: a lane that finishes a
-// domain picks its next one at the top of the loop), and a lane whose ray
-// ended -- occluded, or its domain list exhausted -- writes its byte and
-// goes idle.  Once kMin lanes are idle (or all), the idle lanes take the
-// next pairs of the wave's band queues (ballot + mbcnt rank, one chunk
-// dequeue per kChunk pairs), build their rays (ao_gen) and walk the
-// top-level tree for their domain masks together (tlas_mask_wave over the
-// refilled lanes).  So a wave keeps its lanes busy until the queues drain
-// instead of idling until the slowest ray of each 64.  Every pair is traced
-// by exactly one lane with the per-lane walk's arithmetic: the bits are
-// scene_ray's.  scripts/walk_sim.py (ao2, refill 16, chunk 1024): node-loop
-// iterations per 64 AO-16 rays 21.4 -> 15.6, leaf iterations 22.1 -> 14.4,
-// 1.6 top-level walks instead of 1.
-template <int W, int STK, uint32_t kMin, uint32_t kChunk>
-__device__ __forceinline__ void scene_ray_ah_refill(const SceneArgs& A, size_t M, size_t S,
-                                                    const float4* stl, const float* sbox,
-                                                    const float4* sdom, int32_t* stk,
-                                                    int32_t* wstk) {
-  constexpr uint32_t kPerXcd = kQueues / 8;
-  constexpr uint32_t kGroup = SPRAY_AO_REFILL_GROUP;
-  static_assert(kGroup == 1 || kGroup == 2 || kGroup == 4 || kGroup == 8 || kGroup == 16,
-                "refill groups: a power of two dividing the chunk");
-  static_assert(kChunk % kGroup == 0 && (64 * size_t(kQueues)) % kGroup == 0, "aligned groups");
-  constexpr uint64_t kGroupLead = kGroup == 1 ? ~0ull
-                                  : kGroup == 2 ? 0x5555555555555555ull
-                                  : kGroup == 4 ? 0x1111111111111111ull
-                                  : kGroup == 8 ? 0x0101010101010101ull
-                                                : 0x0001000100010001ull;
-  const uint32_t xcd = xcc_id() & 7u;
-  const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
-  BandCursor bc{0u, 0, 0};
-  bool more = true;  // wave-uniform: pairs may remain in the queues
-  size_t i = 0;      // the lane's pair
-  bool alive = false;
-  Ray r{};
-  uint64_t m[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) m[w] = 0;
-  // the lane's current domain walk
-  QRay qr{};
-  const char* nbytes = nullptr;
-  uint64_t tris_u = 0;
-  int32_t cur = kNone, leaf = kNone;
-  constexpr int kOvf = kQ4Stack > STK ? kQ4Stack - STK : 1;
-  int32_t ovf[kOvf];
-  int sp = 0;
-  auto push = [&](int32_t v) {
-    if (STK >= kQ4Stack || sp < STK)
-      stk[sp * kBlock] = v;
-    else
-      ovf[sp - STK] = v;
-    ++sp;
-  };
-  auto pop = [&]() -> int32_t {
-    if (sp == 0) return kNone;
-    --sp;
-    return (STK >= kQ4Stack || sp < STK) ? stk[sp * kBlock] : ovf[sp - STK];
-  };
-  for (;;) {
-    // ---- refill (uniform): the idle lane groups take the next pairs
-    uint64_t idle = __ballot(!alive);
-    if (kGroup > 1) {  // a group is idle when all its lanes are
-#pragma unroll
-      for (uint32_t sh = 1; sh < kGroup; sh <<= 1) idle &= idle >> sh;
-      idle &= kGroupLead;
-#pragma unroll
-      for (uint32_t sh = 1; sh < kGroup; sh <<= 1) idle |= idle << sh;
-    }
-    const uint32_t nidle = uint32_t(__popcll(idle));
-    if (more && (nidle >= kMin || nidle == 64u)) {
-      const bool mine = (idle >> (threadIdx.x & 63)) & 1ull;
-      // this lane's rank among the idle lanes, in groups
-      const uint32_t rank =
-          __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0u));
-      bool fresh = false;
-      uint32_t dealt = 0;
-      while (dealt < nidle) {
-        if (bc.cur == bc.end && !band_next<kChunk>(A, M, S, xcd, sub, bc)) {
-          more = false;
-          break;
-        }
-        const size_t left = bc.end - bc.cur;
-        // whole groups of pairs (chunks start at multiples of kGroup; a
-        // band's ragged end leaves the lanes past it idle)
-        const size_t lg = (left + kGroup - 1) / kGroup * kGroup;
-        const uint32_t take = lg < size_t(nidle - dealt) ? uint32_t(lg) : nidle - dealt;
-        if (mine && rank >= dealt && rank < dealt + take && bc.cur + (rank - dealt) < bc.end) {
-          i = bc.cur + (rank - dealt);
-          fresh = true;
-        }
-        bc.cur = bc.cur + take < bc.end ? bc.cur + take : bc.end;
-        dealt += take;
-      }
-      if (fresh) {
-        v4f a, b;
-        ao_gen(A, i, a, b);
-        r = make_ray(a.x, a.y, a.z, b.x, b.y, b.z);
-        alive = true;
-        cur = leaf = kNone;
-        // AO rays: tnear = kRayEpsilon, tfar = kInf (ao_gen)
-        tlas_mask_wave<W>(stl, A.ntlas, wstk, r, make_float4(a.x, a.y, a.z, a.w),
-                          make_float4(b.x, b.y, b.z, b.w), m);
-      }
-    }
-    // ---- lanes between walks: the nearest remaining domain of the list
-    if (alive && cur == kNone && leaf == kNone) {
-      float dx = r.dx, dy = r.dy, dz = r.dz;
-      asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
-      const DRay dr = make_dray(r.ox, r.oy, r.oz, dx, dy, dz);
-      for (;;) {
-        bool any_left = false;
-#pragma unroll
-        for (int w = 0; w < W; ++w) any_left |= m[w] != 0;
-        if (!any_left) {
-          alive = false;  // domain list exhausted: not occluded
-          A.occ[i] = 0;
-          break;
-        }
-        float st = kInf;
-        int sb = -1;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          uint64_t bits = m[w];
-          while (bits) {
-            const int j = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            const int bx = 64 * w + j;
-            float tm;
-            aabb_ref(sbox + 6 * bx, dr, tm);
-            if (sb < 0 || tm < st) {
-              st = tm;
-              sb = bx;
-            }
-          }
-        }
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
-        const float4 dt = sdom[sb];
-        nbytes = reinterpret_cast<const char*>(
-            (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
-        if (!nbytes) continue;  // not resident here (or empty)
-        tris_u = uint64_t(nbytes) + __float_as_uint(dt.z);
-        const float4 base = ld4(nbytes - sizeof(QGrid), 0);
-        const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
-        const float ix = 1.0f / clamp_dir(dx), iy = 1.0f / clamp_dir(dy),
-                    iz = 1.0f / clamp_dir(dz);
-        q_axis(base.x, scale.x, ix, r.ox * ix, qr.ix, qr.olx, qr.ohx);
-        q_axis(base.y, scale.y, iy, r.oy * iy, qr.iy, qr.oly, qr.ohy);
-        q_axis(base.z, scale.z, iz, r.oz * iz, qr.iz, qr.olz, qr.ohz);
-        cur = 0;
-        sp = 0;
-        break;
-      }
-    }
-    if (!more && !__ballot(alive)) break;
-    // ---- node steps until every stepping lane holds a leaf
-    for (;;) {
-      const bool step = alive && cur >= 0 && cur != kNone;
-      if (!__ballot(step)) break;
-      if (step) {
-        const char* qp = nbytes - 128 - 64 * size_t(cur);
-        const float4 qa = ld4(qp, 0), qb = ld4(qp, 1), qc = ld4(qp, 2), qd = ld4(qp, 3);
-        const int32_t ref[4] = {__float_as_int(qd.x), __float_as_int(qd.y), __float_as_int(qd.z),
-                                __float_as_int(qd.w)};
-        float t[4];
-        bool h[4];
-        h[0] = slab_q(qr, q_lo(qa.x), q_hi(qa.x), q_lo(qa.y), q_hi(qa.y), q_lo(qa.z), q_hi(qa.z),
-                      kRayEpsilon, kInf, t[0]);
-        h[1] = slab_q(qr, q_lo(qa.w), q_hi(qa.w), q_lo(qb.x), q_hi(qb.x), q_lo(qb.y), q_hi(qb.y),
-                      kRayEpsilon, kInf, t[1]);
-        h[2] = slab_q(qr, q_lo(qb.z), q_hi(qb.z), q_lo(qb.w), q_hi(qb.w), q_lo(qc.x), q_hi(qc.x),
-                      kRayEpsilon, kInf, t[2]);
-        h[3] = slab_q(qr, q_lo(qc.y), q_hi(qc.y), q_lo(qc.z), q_hi(qc.z), q_lo(qc.w), q_hi(qc.w),
-                      kRayEpsilon, kInf, t[3]);
-        int32_t next = kNone;
-        float tn = kInf;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!h[k] || ref[k] == kNoChildRef) continue;
-          if (next == kNone || t[k] < tn) {
-            if (next != kNone) push(next);
-            next = ref[k];
-            tn = t[k];
-          } else {
-            push(ref[k]);
-          }
-        }
-        cur = next != kNone ? next : pop();
-        if (cur < 0 && cur != kNone && leaf == kNone) {  // park the leaf, keep descending
-          leaf = cur;
-          cur = pop();
-        }
-      }
-      if (__ballot(step && leaf == kNone) == 0) break;
-    }
-    // ---- leaf tests per lane: the parked leaf, then a leaf the walk stopped on
-    while (alive && leaf != kNone) {
-      const uint32_t enc = ~uint32_t(leaf);
-      const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
-      bool hit = false;
-      for (uint32_t q = 0; q < cnt; ++q) {
-        float4 ta, tb, tc;
-        ld_tri(reinterpret_cast<const void*>(tris_u), first + q, ta, tb, tc);
-        float th, tu, tv;
-        if (tri_test(r, kRayEpsilon, ta, tb, tc, th, tu, tv) && th <= kInf) {
-          hit = true;
-          break;
-        }
-      }
-      if (hit) {
-        alive = false;
-        A.occ[i] = 1;
-        break;
-      }
-      leaf = kNone;
-      if (cur < 0 && cur != kNone) {
-        leaf = cur;
-        cur = pop();
-      }
-    }
-  }
-}
+#if SPRAY_AH_SPREAD || SPRAY_AO_REFILL || SPRAY_WAVE_TIMES
+#include "rt_kernels_diag.inc"
+#endif
 
 // A wave's rays are coherent when every direction is within ~8 degrees of
 // the first valid lane's (camera rays of neighbouring pixels, shadow rays
@@ -1337,24 +865,6 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 // walk and nothing waits in a wave's hands for longer than one packet).
 #ifndef SPRAY_DEQ_AHEAD
 #define SPRAY_DEQ_AHEAD 2
-#endif
-#if SPRAY_WAVE_TIMES
-__device__ unsigned long long g_wave_times[5 * 16384];
-// per wave up to 255 events: (start << 24 | duration) stamps and (kind << 40 | index)
-__device__ unsigned long long g_pkt_log[2 * 6144 * 256];
-__device__ unsigned int g_pkt_n[6144];
-__device__ __forceinline__ void pkt_log(uint32_t kind, uint64_t index, unsigned long long t0) {
-  const unsigned long long t1 = wall_clock64();
-  const uint32_t wid = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) == 0 && wid < 6144) {
-    const uint32_t n = g_pkt_n[wid];
-    if (n < 256) {
-      g_pkt_log[2 * (size_t(wid) * 256 + n)] = ((t0 & 0xFFFFFFFFFFull) << 24) | ((t1 - t0) & 0xFFFFFFull);
-      g_pkt_log[2 * (size_t(wid) * 256 + n) + 1] = (uint64_t(kind) << 40) | index;
-      g_pkt_n[wid] = n + 1;
-    }
-  }
-}
 #endif
 
 // Persistent launch: each wave dequeues kChunk-ray chunks from kQueues
