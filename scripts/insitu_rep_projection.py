@@ -1,0 +1,96 @@
+"""Projection of the configs[2] frame (wavelets64, 1024x1024x8spp, PT) at
+N = 2 / 4 / 8 GPUs for the replicated-ray in-situ frame, from MEASURED
+per-rank device times and a stated model of the collectives.
+
+    python scripts/insitu_rep_projection.py profiles/r4_rep_rehearse.json \
+        [--n1-ms 0.77] [--out profiles/r4_insitu_projection.json]
+
+Inputs
+* rehearse.json (scripts/insitu_rep_rehearse.py on one MI355X): for each N
+  and partition, every rank's per-phase device time of the frame (HIP events;
+  the ranks' device work serialised, so a rank's times are its own kernels'
+  times), and the one-rank RCCL all-reduce times of the frame's message
+  sizes (the per-call floor).
+* the measured N = 1 frame (the bench's fused single-GPU frame, --n1-ms).
+
+Model of one frame at N ranks (every rank runs the same sequence):
+  T = max_r(lists + keyed closest hit) + AR(8 |C|) + max_r(shadows)
+      + AR(|C| + 192) + max_r(film) + max_r(totals read) + RED(16 MB)
+  AR(B)  = alpha + 2 (N - 1) / N * B / bw     (ring all-reduce)
+  RED(B) = alpha + (N - 1) / N * B / bw * 2   (reduce to rank 0 as reduce-
+           scatter + gather)
+The phases are taken per rank and maxed per phase (each phase ends in a
+collective every rank waits for).  alpha and bw are NOT measured (no
+multi-GPU box): the table gives a conservative and an optimistic pair.
+"""
+import argparse
+import json
+
+LINK = {  # per-collective latency (ms) and ring bus bandwidth (GB/s) at 8 GPUs
+    "conservative": {"alpha_ms": 0.030, "bw_GBs": 300.0},
+    "optimistic": {"alpha_ms": 0.015, "bw_GBs": 500.0},
+}
+IMAGE_BYTES = 1024 * 1024 * 16
+
+
+def ar(b, n, link):
+    return link["alpha_ms"] + 2.0 * (n - 1) / n * b / (link["bw_GBs"] * 1e9) * 1e3
+
+
+def red(b, n, link):
+    return link["alpha_ms"] + 2.0 * (n - 1) / n * b / (link["bw_GBs"] * 1e9) * 1e3
+
+
+def project(run, link):
+    n = run["world"]
+    ranks = run["ranks"]
+    ph = lambda r, k: r["phases_ms"].get(k, 0.0)  # noqa: E731
+    st = ranks[0]["stats"]  # bytes_sent = the all-reduce payload 9 |C| + 192 per trace
+    nc = (st["bytes_sent"] / max(st["traces"], 1) - 192) / 9
+    a = max(ph(r, "lists") + ph(r, "keyed_closest_hit") for r in ranks)
+    b = max(ph(r, "shadows") for r in ranks)
+    c = max(ph(r, "film") for r in ranks)
+    d = max(ph(r, "totals") for r in ranks)
+    comm = ar(8 * nc, n, link) + ar(nc + 192, n, link) + red(IMAGE_BYTES, n, link)
+    return {"device_ms": round(a + b + c + d, 4), "comm_ms": round(comm, 4),
+            "frame_ms": round(a + b + c + d + comm, 4),
+            "busiest": {"lists+keyed": round(a, 4), "shadows": round(b, 4), "film": round(c, 4),
+                        "totals": round(d, 4)}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("rehearse")
+    ap.add_argument("--n1-ms", type=float, default=0.77)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    rep = json.load(open(args.rehearse))
+    rows = []
+    for run in rep["runs"]:
+        row = {"world": run["world"], "partition": run["partition"],
+               "domains_per_rank": [r["domains"] for r in run["ranks"]],
+               "rank_phase_sums_ms": [round(sum(r["phases_ms"].values()), 4)
+                                      for r in run["ranks"]]}
+        for name, link in LINK.items():
+            p = project(run, link)
+            p["speedup_vs_n1"] = round(args.n1_ms / p["frame_ms"], 3)
+            row[name] = p
+        rows.append(row)
+    out = {"model": __doc__.strip().split("\n\n")[2], "links": LINK, "n1_ms": args.n1_ms,
+           "rccl_one_rank_floor": rep.get("rccl_one_rank_floor"), "rows": rows}
+    print("| N | partition | busiest lists+keyed | shadows | film | device ms | comm ms (cons.) "
+          "| frame ms (cons. / opt.) | x N=1 (cons. / opt.) |")
+    print("|---|---|---|---|---|---|---|---|---|")
+    for r in rows:
+        c, o = r["conservative"], r["optimistic"]
+        print("| %d | %s | %.3f | %.3f | %.3f | %.3f | %.3f | %.3f / %.3f | %.2f / %.2f |" % (
+            r["world"], r["partition"], c["busiest"]["lists+keyed"], c["busiest"]["shadows"],
+            c["busiest"]["film"], c["device_ms"], c["comm_ms"], c["frame_ms"], o["frame_ms"],
+            c["speedup_vs_n1"], o["speedup_vs_n1"]))
+    if args.out:
+        with open(args.out, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

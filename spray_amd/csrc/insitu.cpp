@@ -838,6 +838,8 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                             I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
   // ---- 3. the winning key of every ray of C, on every rank
   MARK(2);
+  I->st[0] += 9 * nc + 192;  // the two all-reduces' payload (stats: bytes sent / received)
+  I->st[1] += 9 * nc + 192;
   if (nc) CALL(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   // ---- 4. shadow rays of every hit, own any hit; the winners shade
   MARK(3);
