@@ -21,6 +21,11 @@ namespace spray_rt {
 namespace {
 
 constexpr int kWaves = kBlock / 64;
+// blocks of the queue pass (k_ooc_masks): ~6 per CU resident at its LDS
+#ifndef SPRAY_OOC_MASK_BLOCKS
+#define SPRAY_OOC_MASK_BLOCKS 3072
+#endif
+constexpr unsigned kOocMaskBlocks = SPRAY_OOC_MASK_BLOCKS;
 // adaptive any-hit drains: the largest id span of a wave's rays that still
 // walks as a packet (8 pixels x 8 spp = 64 consecutive camera rays)
 // waves per SIMD the any-hit drain is compiled for (register budget)
@@ -95,7 +100,7 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_ooc_masks(
     const BvhNode* __restrict__ tlas, int ntlas, const float* __restrict__ boxes, int ndom,
     const spray_rt_ray* __restrict__ rays, const uint8_t* __restrict__ valid, size_t M,
-    uint64_t* __restrict__ masks, uint64_t* __restrict__ key_init,
+    uint32_t nrb, uint64_t* __restrict__ masks, uint64_t* __restrict__ key_init,
     uint8_t* __restrict__ occ_clear, uint32_t* __restrict__ bc, uint32_t* __restrict__ sb) {
   __shared__ int32_t wstack[kWaves * kStack];
   __shared__ float4 stl[4 * 64 * W];
@@ -103,102 +108,109 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
   __shared__ uint32_t cnt[64 * W], sc[64 * W];
   __shared__ float lte[kLaneList][kBlock];
   __shared__ int lid[kLaneList][kBlock];
+  // the top-level tree and the boxes are staged once per block, which then
+  // walks ray blocks rb = blockIdx.x, + gridDim.x, ... (one launch-wide
+  // staging of 5.5 KB per ray block of 256 rays was 180 MB of L2 reads per
+  // 8 M rays)
   for (int q = threadIdx.x; q < 4 * ntlas; q += kBlock) stl[q] = ld4(tlas, q);
   for (int q = threadIdx.x; q < 6 * ndom; q += kBlock) sbox[q] = boxes[q];
-  for (int q = threadIdx.x; q < 64 * W; q += kBlock) cnt[q] = sc[q] = 0;
-  __syncthreads();
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  const bool in = i < M;
-  const bool live = in && (!valid || valid[i]);
-  uint64_t m[W];
+  for (uint32_t rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+    for (int q = threadIdx.x; q < 64 * W; q += kBlock) cnt[q] = sc[q] = 0;
+    __syncthreads();
+    const size_t i = size_t(rb) * kBlock + threadIdx.x;
+    const bool in = i < M;
+    const bool live = in && (!valid || valid[i]);
+    uint64_t m[W];
 #pragma unroll
-  for (int w = 0; w < W; ++w) m[w] = 0;
-  float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  if (live) {
-    const float4* rp = reinterpret_cast<const float4*>(rays + i);
-    o4 = rp[0];
-    d4 = rp[1];
-    const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-    tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
-  }
-  // confirm; the confirmed entry t's go to the lane's LDS list
-  uint32_t k = 0;
-  const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  if (live) {
+    for (int w = 0; w < W; ++w) m[w] = 0;
+    float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
+    if (live) {
+      const float4* rp = reinterpret_cast<const float4*>(rays + i);
+      o4 = rp[0];
+      d4 = rp[1];
+      const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+      tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
+    }
+    // confirm; the confirmed entry t's go to the lane's LDS list
+    uint32_t k = 0;
+    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    if (live) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t bits = m[w];
+        while (bits) {
+          const int j = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          float te;
+          if (aabb_ref(sbox + 6 * (64 * w + j), dr, te)) {
+            if (k < kLaneList) {
+              lte[k][threadIdx.x] = te;
+              lid[k][threadIdx.x] = 64 * w + j;
+            }
+            ++k;
+          } else {
+            m[w] &= ~(1ull << j);
+          }
+        }
+      }
+    }
+    // list position of each confirmed domain = its rank by (entry t, id);
+    // the weight goes into the entry's upper half
+    if (k <= kLaneList)
+      for (uint32_t a = 0; a < k; ++a) {
+        const float ta = lte[a][threadIdx.x];
+        const int da = lid[a][threadIdx.x] & 0xFFFF;
+        uint32_t pos = 0;
+        for (uint32_t b = 0; b < k; ++b) {
+          const float tb = lte[b][threadIdx.x];
+          pos += (tb < ta || (tb == ta && (lid[b][threadIdx.x] & 0xFFFF) < da)) ? 1u : 0u;
+        }
+        lid[a][threadIdx.x] = da | int((pos < kDomainListSize ? kDomainListSize - pos : 1u) << 16);
+      }
+    // per domain of the wave: pairs and weights summed over the wave first
+    // (a wave's rays mostly share domains: same-address LDS atomics serialise)
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      uint64_t bits = m[w];
-      while (bits) {
-        const int j = __ffsll((long long)bits) - 1;
-        bits &= bits - 1;
-        float te;
-        if (aabb_ref(sbox + 6 * (64 * w + j), dr, te)) {
-          if (k < kLaneList) {
-            lte[k][threadIdx.x] = te;
-            lid[k][threadIdx.x] = 64 * w + j;
+      uint64_t u = wave_or64(m[w]);
+      while (u) {
+        const int j = __ffsll((long long)u) - 1;
+        u &= u - 1;
+        const int dom = 64 * w + j;
+        const bool has = (m[w] >> j) & 1;
+        uint32_t add = 0;
+        if (has) {
+          if (k <= kLaneList) {
+            for (uint32_t a = 0; a < k; ++a) {
+              const int e = lid[a][threadIdx.x];
+              if ((e & 0xFFFF) == dom) add = uint32_t(e) >> 16;
+            }
+          } else {  // long list: the position from the mask
+            float te;
+            aabb_ref(sbox + 6 * dom, dr, te);
+            const uint32_t pos = list_pos<W>(m, sbox, dom, te, dr);
+            add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
           }
-          ++k;
-        } else {
-          m[w] &= ~(1ull << j);
+        }
+        const uint32_t n = uint32_t(__popcll(__ballot(has)));
+        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o);
+        if ((threadIdx.x & 63) == 0) {
+          atomicAdd(&cnt[dom], n);
+          atomicAdd(&sc[dom], add);
         }
       }
     }
-  }
-  // list position of each confirmed domain = its rank by (entry t, id); the
-  // weight goes into the entry's upper half
-  if (k <= kLaneList)
-    for (uint32_t a = 0; a < k; ++a) {
-      const float ta = lte[a][threadIdx.x];
-      const int da = lid[a][threadIdx.x] & 0xFFFF;
-      uint32_t pos = 0;
-      for (uint32_t b = 0; b < k; ++b) {
-        const float tb = lte[b][threadIdx.x];
-        pos += (tb < ta || (tb == ta && (lid[b][threadIdx.x] & 0xFFFF) < da)) ? 1u : 0u;
-      }
-      lid[a][threadIdx.x] = da | int((pos < kDomainListSize ? kDomainListSize - pos : 1u) << 16);
-    }
-  // per domain of the wave: pairs and weights summed over the wave first
-  // (a wave's rays mostly share domains: same-address LDS atomics serialise)
+    if (in) {
 #pragma unroll
-  for (int w = 0; w < W; ++w) {
-    uint64_t u = wave_or64(m[w]);
-    while (u) {
-      const int j = __ffsll((long long)u) - 1;
-      u &= u - 1;
-      const int dom = 64 * w + j;
-      const bool has = (m[w] >> j) & 1;
-      uint32_t add = 0;
-      if (has) {
-        if (k <= kLaneList) {
-          for (uint32_t a = 0; a < k; ++a) {
-            const int e = lid[a][threadIdx.x];
-            if ((e & 0xFFFF) == dom) add = uint32_t(e) >> 16;
-          }
-        } else {  // long list: the position from the mask
-          float te;
-          aabb_ref(sbox + 6 * dom, dr, te);
-          const uint32_t pos = list_pos<W>(m, sbox, dom, te, dr);
-          add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
-        }
-      }
-      const uint32_t n = uint32_t(__popcll(__ballot(has)));
-      for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o);
-      if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&cnt[dom], n);
-        atomicAdd(&sc[dom], add);
-      }
+      for (int w = 0; w < W; ++w) masks[i * W + w] = m[w];
+      if (key_init) key_init[i] = kOocMissKey;
+      if (occ_clear && live) occ_clear[i] = 0;
     }
-  }
-  if (in) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) masks[i * W + w] = m[w];
-    if (key_init) key_init[i] = kOocMissKey;
-    if (occ_clear && live) occ_clear[i] = 0;
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < ndom; q += kBlock) {
-    bc[size_t(blockIdx.x) * ndom + q] = cnt[q];
-    sb[size_t(blockIdx.x) * ndom + q] = sc[q];
+    __syncthreads();
+    for (int q = threadIdx.x; q < ndom; q += kBlock) {
+      bc[size_t(rb) * ndom + q] = cnt[q];
+      sb[size_t(rb) * ndom + q] = sc[q];
+    }
+    __syncthreads();  // cnt / sc are cleared for the next ray block
   }
 }
 
@@ -735,12 +747,14 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   const unsigned g = grid_for(M);
   const size_t n = size_t(ndom) * g;
   if (n > q.block_cap) return hipErrorInvalidValue;  // the caller sizes for M
+  // a few ray blocks per block (the tree is staged once per block)
+  const unsigned gm = g < kOocMaskBlocks ? g : kOocMaskBlocks;
   if (W == 1)
-    k_ooc_masks<1><<<g, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, q.masks,
-                                        key_init, occ_clear, q.bc, q.sb);
+    k_ooc_masks<1><<<gm, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, g, q.masks,
+                                         key_init, occ_clear, q.bc, q.sb);
   else
-    k_ooc_masks<4><<<g, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, q.masks,
-                                        key_init, occ_clear, q.bc, q.sb);
+    k_ooc_masks<4><<<gm, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, g, q.masks,
+                                         key_init, occ_clear, q.bc, q.sb);
   const unsigned nch = (g + kOocChunk - 1) / kOocChunk;
   if (size_t(ndom) * nch > q.chunk_cap) return hipErrorInvalidValue;  // the caller sizes for M
   k_ooc_chunk_sums<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.sb, g, ndom, q.csum, q.cw);

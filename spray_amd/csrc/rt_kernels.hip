@@ -866,6 +866,10 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 #ifndef SPRAY_DEQ_AHEAD
 #define SPRAY_DEQ_AHEAD 2
 #endif
+// guided chunk size near a band's end (closest-hit launches; 0 = off)
+#ifndef SPRAY_CHUNK_TAIL
+#define SPRAY_CHUNK_TAIL 0
+#endif
 
 // Persistent launch: each wave dequeues kChunk-ray chunks from kQueues
 // queues, each owning a contiguous band of the rays.  XCD x's waves start on
@@ -1081,6 +1085,11 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     constexpr uint32_t kPerXcd = kQueues / 8;
+    // guided chunks (SPRAY_CHUNK_TAIL > 0, closest hit): a dequeue that
+    // finds fewer than SPRAY_CHUNK_TAIL rays left in its band takes one
+    // packet instead of kChunk, so the band's last rays spread over many
+    // waves instead of waiting in a few waves' hands
+    constexpr uint32_t kTail = ANY ? 0u : uint32_t(SPRAY_CHUNK_TAIL);
     const uint32_t xcd = xcc_id() & 7u;
     const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
     for (uint32_t k = 0; k < uint32_t(kQueues); ++k) {
@@ -1089,19 +1098,26 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
       const size_t end = begin + S < M ? begin + S : M;
       if (begin >= end) continue;
       uint32_t* head = &A.heads[32 * q];
-      uint32_t base = 0;
+      const auto chunk_at = [&](uint32_t b) -> uint32_t {
+        return (kTail && begin + b + kTail >= end) ? 64u : kChunk;
+      };
+      uint32_t base = 0, csz = kChunk;
       if (lane == 0) {
         base = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (begin + base < end) base = atomicAdd(head, kChunk);
+        if (begin + base < end) {
+          csz = chunk_at(base);
+          base = atomicAdd(head, csz);
+        }
       }
       base = __builtin_amdgcn_readfirstlane(base);
+      csz = kTail ? __builtin_amdgcn_readfirstlane(csz) : kChunk;
       while (begin + base < end) {
         // the next chunk is dequeued before this one is traced: the atomic's
         // latency overlaps the traversal
-        uint32_t next = 0;
+        uint32_t next = 0, ncsz = kChunk;
         if (SPRAY_DEQ_AHEAD == 1 && lane == 0) next = atomicAdd(head, kChunk);
         const size_t cbeg = begin + base;
-        for (uint32_t c = 0; c < kChunk; c += 64) {
+        for (uint32_t c = 0; c < (kTail ? csz : kChunk); c += 64) {
           const size_t j = cbeg + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
           const bool ok = j < end && i < A.M && (!A.valid || A.valid[i]);
@@ -1113,10 +1129,13 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             // the next chunk is dequeued by the chunk's last packet once its
             // rays have landed: the atomic overlaps that packet's walk, and
             // no chunk waits in a wave's hands while another is traced
-            const bool last = c + 64 >= kChunk;
+            const bool last = c + 64 >= (kTail ? csz : kChunk);
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi, nullptr,
                                           [&]() {
-                                            if (last && lane == 0) next = atomicAdd(head, kChunk);
+                                            if (last && lane == 0) {
+                                              ncsz = chunk_at(base + csz);
+                                              next = atomicAdd(head, ncsz);
+                                            }
                                           });
           } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
@@ -1134,9 +1153,12 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             shadow_push<W>(A, sq, j < end, flag, i, pos, wi, stl, sbox, sdom, wstk, wcount);
         }
         if ((SPRAY_DEQ_AHEAD == 0 || (SPRAY_DEQ_AHEAD == 2 && !(kPacket && !kAdaptive))) &&
-            lane == 0)
-          next = atomicAdd(head, kChunk);
+            lane == 0) {
+          ncsz = chunk_at(base + csz);
+          next = atomicAdd(head, ncsz);
+        }
         base = __builtin_amdgcn_readfirstlane(next);
+        if (kTail) csz = __builtin_amdgcn_readfirstlane(ncsz);
         ++wchunks;
       }
     }
