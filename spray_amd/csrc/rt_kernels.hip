@@ -611,12 +611,16 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
                                                  const float4* sdom, int32_t* wstk,
                                                  bool& spawn, float* pos, float* wi,
                                                  const float* rin = nullptr,
-                                                 const Post& post = Post()) {
+                                                 const Post& post = Post(),
+                                                 const float4* lray = nullptr) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int lane = threadIdx.x & 63;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  if (valid && rin) {
+  if (valid && lray) {  // the packet's rays, prefetched into the wave's LDS
+    o4 = lray[2 * lane];
+    d4 = lray[2 * lane + 1];
+  } else if (valid && rin) {
     o4 = make_float4(rin[0], rin[1], rin[2], kRayEpsilon);
     d4 = make_float4(rin[3], rin[4], rin[5], kInf);
   } else if (valid) {
@@ -866,6 +870,12 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 #ifndef SPRAY_DEQ_AHEAD
 #define SPRAY_DEQ_AHEAD 2
 #endif
+// next packet's rays copied global -> LDS (global_load_lds) during the
+// current packet's walk (plain closest-hit launches without index list or
+// mask; 0 = off)
+#ifndef SPRAY_RAY_PREFETCH
+#define SPRAY_RAY_PREFETCH 0
+#endif
 // guided chunk size near a band's end (closest-hit launches; 0 = off)
 #ifndef SPRAY_CHUNK_TAIL
 #define SPRAY_CHUNK_TAIL 0
@@ -1036,6 +1046,11 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   constexpr bool kShadow = EPI == kEpiShadow || EPI == kEpiShadowFrame;
   __shared__ float sq_ray[kShadow ? (kBlock / 64) * kShadowQ * 6 : 1];
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
+  // ray prefetch: one packet (64 rays x 32 B) per wave
+  constexpr bool kPre = SPRAY_RAY_PREFETCH && kPacket && !kAdaptive && SPRAY_DEQ_AHEAD == 2 &&
+                        !ANY && EPI != kEpiAoGen;
+  __shared__ float4 pre_ray[kPre ? (kBlock / 64) * 128 : 1];
+  float4* my_pre = pre_ray + (kPre ? (threadIdx.x >> 6) * 128 : 0);
   ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
                  sq_src + (kShadow ? (threadIdx.x >> 6) * kShadowQ : 0), 0u};
   const unsigned long long wt0 = SPRAY_WAVE_TIMES ? wall_clock64() : 0ull;
@@ -1130,13 +1145,36 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             // rays have landed: the atomic overlaps that packet's walk, and
             // no chunk waits in a wave's hands while another is traced
             const bool last = c + 64 >= (kTail ? csz : kChunk);
-            scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi, nullptr,
-                                          [&]() {
-                                            if (last && lane == 0) {
-                                              ncsz = chunk_at(base + csz);
-                                              next = atomicAdd(head, ncsz);
-                                            }
-                                          });
+            // ray prefetch: this packet's rays came into LDS during the
+            // previous packet (not the chunk's first); the next packet's are
+            // copied while this one is walked
+            const bool pre = kPre && !idx && !A.valid;
+            const bool have = pre && c > 0;
+            if (have) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            scene_ray_packet<W, ANY, EPI>(
+                A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi, nullptr,
+                [&]() {
+                  if (last && lane == 0) {
+                    ncsz = chunk_at(base + csz);
+                    next = atomicAdd(head, ncsz);
+                  }
+                  if (kPre && pre && !last) {
+                    // rays cbeg + c + 64 .. + 127: lane l copies 16 B (half
+                    // of ray l / 2) of each half-packet, LDS = lane order
+                    const size_t n0 = cbeg + c + 64;
+                    for (int h = 0; h < 2; ++h) {
+                      size_t rr = n0 + 32 * h + (lane >> 1);
+                      rr = rr < end ? rr : end - 1;
+                      const GAS char* src =
+                          (const GAS char*)(A.rays + rr) + 16 * (lane & 1);
+                      __builtin_amdgcn_global_load_lds(
+                          (GAS void*)src,
+                          (__attribute__((address_space(3))) void*)(my_pre + 64 * h), 16, 0,
+                          0);
+                    }
+                  }
+                },
+                have ? my_pre : nullptr);
           } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           else if (kSpread)
