@@ -18,6 +18,8 @@ PT shadows) is computed once per module.  References: src/ooc/
 ooc_pcontext.h:128-157, src/ooc/ooc_shader_ao.h:131-144, src/insitu/
 insitu_multithread_tracer.inl:313-442.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -260,3 +262,83 @@ def test_insitu_full_frame_rccl_one_rank(spray, oracle):
     np.testing.assert_allclose(img, ref["image"], rtol=1e-5, atol=1e-6)
     eng.close()
     rt.close()
+
+
+def _rep_rank_main(rank, world, port, out, mode):
+    """One rank of the full-size replicated-ray frame (8 processes sharing the
+    GPU, gloo + the engine's host transport): records to out/r<rank>.npz."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    import torch.distributed as dist
+    import spray_amd
+    from spray_amd import insitu
+    from spray_amd.engine import host_parse_scene, host_scene_bsdfs
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        boxes, lights = host_parse_scene(WAVELETS64, SCENES)
+        bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
+        owner = insitu.morton_partition(boxes, bound, world, mode)
+        rt = spray_amd.RtContext(0)
+        insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
+        rt.set_bsdfs(host_scene_bsdfs(WAVELETS64))
+        rt.set_stream(torch.cuda.current_stream())
+        eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport="host")
+        c = BENCH_CAMERA
+        cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], W, H)
+        rays = torch.empty((N, 8), dtype=torch.float32, device="cuda")
+        pix = torch.empty(N, dtype=torch.int32, device="cuda")
+        sam = torch.empty(N, dtype=torch.int32, device="cuda")
+        rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), (0, 0, W, H), rays, pix, sam)
+        sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
+                                         lights=lights)
+        image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+        recs = insitu.InsituRecords(N // 2)
+        tot = eng.trace_frame(sh, rays, pix, sam, SPP, image, recs)
+        eng.composite(image)
+        torch.cuda.synchronize()
+        g = recs.numpy()
+        np.savez(os.path.join(out, "r%d.npz" % rank), samid=g["samid"], bounce=g["bounce"],
+                 hits=g["hits"], svalid=g["svalid"], occluded=g["occluded"],
+                 tot=np.array(tot, np.int64), image=image.cpu().numpy() if rank == 0 else
+                 np.zeros(0, np.float32))
+        eng.close()
+        rt.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_replicated_full_frame_eight_ranks(spray, oracle, mode):
+    """configs[2] at N = 8, the bench's replicated-ray frame at full size
+    (1024x1024x8spp, every eye ray on every rank, 8 domains per rank, both
+    partitions), 8 engine processes sharing the GPU over the host transport:
+    every shaded sample's record bit-exact against the whole-scene oracle,
+    shaded exactly once across the ranks, totals exact, the composited image
+    within summation order."""
+    import socket
+    import tempfile
+    from spray_amd.engine import host_parse_scene
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 8
+    with tempfile.TemporaryDirectory() as out:
+        torch.multiprocessing.spawn(_rep_rank_main, args=(world, port, out, mode), nprocs=world)
+        parts = [dict(np.load(os.path.join(out, "r%d.npz" % r))) for r in range(world)]
+    _, lights = host_parse_scene(WAVELETS64, SCENES)
+    ref = _oracle_insitu_frame(oracle, [tuple(float(x) for x in l) for l in lights])
+    for p in parts:
+        assert tuple(p["tot"]) == ref["totals"]
+    assert sum(len(p["samid"]) > 10_000 for p in parts) >= 4  # the shading is spread
+    sam = np.concatenate([p["samid"] for p in parts])
+    order = np.argsort(sam, kind="stable")
+    hits = np.concatenate([p["hits"] for p in parts])[order]
+    assert np.array_equal(sam[order], ref["samid"])  # each sample shaded exactly once
+    assert hits.tobytes() == ref["hits"].tobytes()
+    assert np.array_equal(np.concatenate([p["svalid"] for p in parts])[order], ref["svalid"])
+    assert np.array_equal(np.concatenate([p["occluded"] for p in parts])[order], ref["occluded"])
+    np.testing.assert_allclose(parts[0]["image"], ref["image"], rtol=1e-5, atol=1e-6)
