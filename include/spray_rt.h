@@ -657,13 +657,14 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t ins, const spray_rt_shader* sh
                                 const spray_rt_insitu_rec* rec, unsigned long long totals[3]);
 /* Per-phase device time of the traces since the last call (then reset),
  * HIP events on the context's stream, when phase timing is on
- * (spray_rt_insitu_set_timing).  out_ms[8]; *nphases = phases of the last
- * trace's form: replicated frame {lists, keyed closest hit, key all-reduce,
- * shadows, occlusion all-reduce, film, totals}; protocol {route + counts,
- * ray exchange, keyed closest hit, key composite, shading, shadow route +
- * exchange, shadow any hit + return, film + totals}. */
+ * (spray_rt_insitu_set_timing).  out_ms[9]; *nphases = phases of the last
+ * trace's form: replicated frame {lists, keyed closest hit, shadows, film,
+ * totals}; protocol {route + plan, ray exchange, keyed closest hit, key
+ * composite, shading, shadow route + exchange, shadow any hit + return,
+ * film + totals}; all-local {frame}.  out_ms[8]: the time inside the
+ * collectives (and the host reads of their counts), whatever the form. */
 int spray_rt_insitu_set_timing(spray_rt_insitu_t ins, int on);
-int spray_rt_insitu_phase_times(spray_rt_insitu_t ins, double out_ms[8], int* nphases);
+int spray_rt_insitu_phase_times(spray_rt_insitu_t ins, double out_ms[9], int* nphases);
 /* HdrImage::composite (src/display/image.h:167-181): SUM of the ranks'
  * images at rank 0 (device float[nfloats], in place). */
 int spray_rt_insitu_composite(spray_rt_insitu_t ins, float* image_rgba, size_t nfloats);

@@ -47,7 +47,7 @@ def project(run, link):
     ph = lambda r, k: r["phases_ms"].get(k, 0.0)  # noqa: E731
     st = ranks[0]["stats"]  # bytes_sent = the all-reduce payload 9 |C| + 192 per trace
     nc = (st["bytes_sent"] / max(st["traces"], 1) - 192) / 9
-    a = max(ph(r, "lists") + ph(r, "keyed_closest_hit") for r in ranks)
+    a = max(ph(r, "lists") + ph(r, "keyed_closest_hit") for r in ranks)  # excl. collectives
     b = max(ph(r, "shadows") for r in ranks)
     c = max(ph(r, "film") for r in ranks)
     d = max(ph(r, "totals") for r in ranks)
@@ -67,10 +67,12 @@ def main():
     rep = json.load(open(args.rehearse))
     rows = []
     for run in rep["runs"]:
+        if run.get("kind", "pt") != "pt":
+            continue
         row = {"world": run["world"], "partition": run["partition"],
                "domains_per_rank": [r["domains"] for r in run["ranks"]],
-               "rank_phase_sums_ms": [round(sum(r["phases_ms"].values()), 4)
-                                      for r in run["ranks"]]}
+               "rank_device_ms": [round(sum(v for k, v in r["phases_ms"].items()
+                                            if k != "collectives"), 4) for r in run["ranks"]]}
         for name, link in LINK.items():
             p = project(run, link)
             p["speedup_vs_n1"] = round(args.n1_ms / p["frame_ms"], 3)

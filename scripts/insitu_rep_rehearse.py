@@ -15,6 +15,7 @@ projection models them.  Also measured: the one-rank RCCL all-reduce of the
 frame's message sizes (the per-call floor of the real collectives).
 """
 import argparse
+import itertools
 import json
 import os
 import socket
@@ -43,7 +44,7 @@ def _port():
     return p
 
 
-def _rank(rank, world, port, mode, frames, out):
+def _rank(rank, world, port, mode, frames, out, kind="pt"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -62,23 +63,30 @@ def _rank(rank, world, port, mode, frames, out):
     rt.set_stream(stream)
     eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport="host")
     cam = spray_amd.camera_init(CAM["pos"], CAM["lookat"], CAM["up"], CAM["fov"], W, H)
-    n = W * H * SPP
-    rays = torch.empty((n, 8), dtype=torch.float32, device="cuda")
-    pix = torch.empty(n, dtype=torch.int32, device="cuda")
-    sam = torch.empty(n, dtype=torch.int32, device="cuda")
-    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), (0, 0, W, H), rays, pix, sam)
-    sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
-                                     lights=lights)
+    # pt: the replicated-ray frame (every eye ray on every rank); ao: AO-16
+    # through the stripe protocol (the rank's horizontal stripe)
+    stripe = (0, 0, W, H) if kind == "pt" else insitu.horizontal_stripe(world, rank, (0, 0, W, H))
+    n = stripe[2] * stripe[3] * SPP
+    rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device="cuda")[:n]
+    pix = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
+    sam = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
+    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, pix, sam)
+    sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1, ks=SHADE[6:9],
+                                     shininess=SHADE[9], lights=lights)
+    trace = eng.trace_frame if kind == "pt" else eng.trace
     image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
     rt.sync()
-    tot = eng.trace_frame(sh, rays, pix, sam, SPP, image)  # warm-up (buffers)
+    tot = trace(sh, rays, pix, sam, SPP, image)  # warm-up (buffers)
     eng.set_timing(True)
     eng.phase_times()
+    s0 = eng.stats()
     for _ in range(frames):
-        tot = eng.trace_frame(sh, rays, pix, sam, SPP, image)
+        tot = trace(sh, rays, pix, sam, SPP, image)
+    s1 = eng.stats()
     ph = {k: v / frames for k, v in eng.phase_times().items()}
     res = {"rank": rank, "domains": int((owner == rank).sum()), "phases_ms": ph,
-           "totals": list(tot), "stats": eng.stats()}
+           "totals": list(tot), "stats": eng.stats(),
+           "per_frame": {k: (s1[k] - s0[k]) / frames for k in s1}}
     with open(os.path.join(out, "r%d.json" % rank), "w") as fh:
         json.dump(res, fh)
     eng.close()
@@ -115,6 +123,8 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--modes", nargs="+", default=["close", "rr"])
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--kinds", nargs="+", default=["pt"],
+                    help="pt: replicated PT frame (configs[2]); ao: AO-16 protocol (configs[4])")
     ap.add_argument("--out", default="gpurun_out/rep/rehearse.json")
     ap.add_argument("--rccl-floor", type=int, default=1)
     args = ap.parse_args()
@@ -123,20 +133,20 @@ def main():
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     lock = os.path.join(tempfile.gettempdir(), "spray_insitu_serial_%d.lock" % os.getpid())
     os.environ["SPRAY_INSITU_SERIAL"] = lock
-    report = {"frame": "wavelets64 1024x1024x8spp PT (configs[2]), replicated-ray frame",
-              "runs": []}
-    for mode in args.modes:
-        for world in args.worlds:
-            t0 = time.time()
-            with tempfile.TemporaryDirectory() as out:
-                mp.spawn(_rank, args=(world, _port(), mode, args.frames, out), nprocs=world)
-                ranks = [json.load(open(os.path.join(out, "r%d.json" % r))) for r in range(world)]
-            report["runs"].append({"world": world, "partition": mode, "ranks": ranks})
-            print("world %d %s: %.1f s; per-rank phase sums (ms): %s" % (
-                world, mode, time.time() - t0,
-                [round(sum(r["phases_ms"].values()), 3) for r in ranks]), flush=True)
-            with open(args.out, "w") as fh:
-                json.dump(report, fh, indent=1)
+    report = {"frame": "wavelets64 1024x1024x8spp: PT replicated-ray frame (configs[2]), "
+                       "AO-16 stripe protocol (configs[4])", "runs": []}
+    for kind, mode, world in itertools.product(args.kinds, args.modes, args.worlds):
+        t0 = time.time()
+        with tempfile.TemporaryDirectory() as out:
+            mp.spawn(_rank, args=(world, _port(), mode, args.frames, out, kind), nprocs=world)
+            ranks = [json.load(open(os.path.join(out, "r%d.json" % r))) for r in range(world)]
+        report["runs"].append({"world": world, "partition": mode, "kind": kind, "ranks": ranks})
+        print("%s world %d %s: %.1f s; per-rank device ms: %s" % (
+            kind, world, mode, time.time() - t0,
+            [round(sum(v for k, v in r["phases_ms"].items() if k != "collectives"), 3)
+             for r in ranks]), flush=True)
+        with open(args.out, "w") as fh:
+            json.dump(report, fh, indent=1)
     os.environ.pop("SPRAY_INSITU_SERIAL", None)
     if args.rccl_floor:
         nc = 2600000  # ~ rays of the bench frame with a non-empty domain list

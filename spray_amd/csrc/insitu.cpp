@@ -161,8 +161,8 @@ struct spray_rt_insitu {
   static constexpr int kMaxEv = 48;
   hipEvent_t ev[kMaxEv] = {};
   int ev_phase[kMaxEv] = {};
-  int nev = 0, nph = 0;
-  double phase_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int nev = 0, nph = 0, cur_phase = 0;
+  double phase_ms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8]: inside collectives
 };
 
 namespace {
@@ -393,8 +393,12 @@ struct Routed {
 };
 
 // ---- phase timing: an event at each phase start; the time to the next
-// event is charged to that phase (read after the trace's last sync)
+// event is charged to that phase (read after the trace's last sync).  The
+// time inside collectives (and the host reads they imply) goes to its own
+// slot, kCommPhase, so the phases are the device work around them.
+constexpr int kCommPhase = 8;
 int mark(spray_rt_insitu* I, int phase) {
+  if (phase != kCommPhase) I->cur_phase = phase;
   if (!I->timing || I->nev >= spray_rt_insitu::kMaxEv) return SPRAY_RT_OK;
   hipEvent_t& e = I->ev[I->nev];
   if (!e) HIPCHK(I->ctx, hipEventCreate(&e));
@@ -413,6 +417,14 @@ void flush_phases(spray_rt_insitu* I, int nphases) {
   I->nph = nphases;
 }
 #define MARK(ph) CALL(mark(I, (ph)))
+// a collective: its stream time to kCommPhase, then back to the phase
+#define COMM(expr)                    \
+  do {                                \
+    const int _ph = I->cur_phase;     \
+    MARK(kCommPhase);                 \
+    CALL(expr);                       \
+    MARK(_ph);                        \
+  } while (0)
 
 int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf& mask, DBuf& idx,
                     DBuf& starts, Routed* R, const uint32_t* sel = nullptr,
@@ -431,7 +443,7 @@ int route_and_count(spray_rt_insitu* I, const spray_rt_ray* rays, size_t n, DBuf
   HIPCHK(c, launch_counts_from_starts(s, starts.as<int64_t>(), W, I->dcnt.as<int64_t>()));
   R->send_n.assign(W, 0);
   R->recv_n.assign(W, 0);
-  CALL(I->tr->counts(I, I->dcnt.as<int64_t>(), R->send_n.data(), R->recv_n.data()));
+  COMM(I->tr->counts(I, I->dcnt.as<int64_t>(), R->send_n.data(), R->recv_n.data()));
   R->total = R->recv = 0;
   for (int r = 0; r < W; ++r) {
     if (R->send_n[r] < 0 || R->recv_n[r] < 0)
@@ -456,7 +468,8 @@ int exchange(spray_rt_insitu* I, const Routed& R, size_t per, bool back, const v
       I->st[0] += sb[r];
       I->st[1] += rb[r];
     }
-  return I->tr->alltoallv(I, send, sb.data(), recv, rb.data(), skip_self);
+  COMM(I->tr->alltoallv(I, send, sb.data(), recv, rb.data(), skip_self));
+  return SPRAY_RT_OK;
 }
 
 int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
@@ -664,7 +677,7 @@ int trace(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays
                            I->dstats.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(c, hipMemcpyAsync(I->dtot.as<unsigned long long>() + 2, I->dstats.p, 8,
                            hipMemcpyDeviceToDevice, s));
-  CALL(I->tr->allreduce_u64(I, I->dtot.as<unsigned long long>(), 3));
+  COMM(I->tr->allreduce_u64(I, I->dtot.as<unsigned long long>(), 3));
   HIPCHK(c, hipMemcpyAsync(ht, I->dtot.p, 3 * 8, hipMemcpyDeviceToHost, s));
   MARK(7);
   HIPCHK(c, hipStreamSynchronize(s));
@@ -771,7 +784,7 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   HIPCHK(c, hipMemcpyAsync(dt, st + 3, 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(c, hipMemcpyAsync(dt + 1, st + 1, 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(c, hipMemcpyAsync(dt + 2, st, 8, hipMemcpyDeviceToDevice, s));
-  CALL(I->tr->allreduce_u64(I, dt, 3));
+  COMM(I->tr->allreduce_u64(I, dt, 3));
   unsigned long long* ht = I->h_small + 200;
   HIPCHK(c, hipMemcpyAsync(ht, dt, 3 * 8, hipMemcpyDeviceToHost, s));
   MARK(0);
@@ -837,12 +850,11 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
                             I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
   // ---- 3. the winning key of every ray of C, on every rank
-  MARK(2);
   I->st[0] += 9 * nc + 192;  // the two all-reduces' payload (stats: bytes sent / received)
   I->st[1] += 9 * nc + 192;
-  if (nc) CALL(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
+  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   // ---- 4. shadow rays of every hit, own any hit; the winners shade
-  MARK(3);
+  MARK(2);
   GROW(I->rsray, nc * 32 + 32);
   GROW(I->rsflag, nc + 1);
   GROW(I->rwin, nc + 1);
@@ -883,22 +895,21 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nc, I->rank == 0 ? n : 0,
                               I->rnsh.as<unsigned long long>()));
   // ---- 5. occlusion OR (a byte SUM) + totals
-  MARK(4);
-  CALL(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nc + 192));
+  COMM(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nc + 192));
   // ---- 6. film of the rays this rank won
-  MARK(5);
+  MARK(3);
   HIPCHK(c, launch_film_atomic(s, image, I->rpix.as<int32_t>(), nc, 1, I->rsw.as<float>(),
                                I->rsvalid.as<uint8_t>(), I->rocc.as<uint8_t>(), scale));
   if (rec)
     HIPCHK(c, launch_record(s, I->rwin.as<uint8_t>(), nc, 0, 1, I->rsam.as<int32_t>(),
                             I->rhit_c.as<spray_rt_hit>(), I->rsvalid.as<uint8_t>(),
                             I->rocc.as<uint8_t>(), *rec));
-  MARK(6);
+  MARK(4);
   uint8_t* ht = reinterpret_cast<uint8_t*>(I->h_small + 128);  // 192 bytes
   HIPCHK(c, hipMemcpyAsync(ht, I->rocc.as<uint8_t>() + nc, 192, hipMemcpyDeviceToHost, s));
-  MARK(6);
+  MARK(4);
   HIPCHK(c, hipStreamSynchronize(s));
-  flush_phases(I, 7);
+  flush_phases(I, 5);
   unsigned long long tot[3] = {0, 0, 0};
   for (int k = 0; k < 192; ++k) tot[k >> 6] += (unsigned long long)ht[k] << (k & 63);
   if (totals)
@@ -1132,9 +1143,9 @@ int spray_rt_insitu_set_timing(spray_rt_insitu_t I, int on) {
   return SPRAY_RT_OK;
 }
 
-int spray_rt_insitu_phase_times(spray_rt_insitu_t I, double out_ms[8], int* nphases) {
+int spray_rt_insitu_phase_times(spray_rt_insitu_t I, double out_ms[9], int* nphases) {
   if (!I || !out_ms) return SPRAY_RT_ERR_ARG;
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < 9; ++k) {
     out_ms[k] = I->phase_ms[k];
     I->phase_ms[k] = 0.0;
   }

@@ -303,20 +303,22 @@ class InsituEngine:
         """Per-phase HIP-event timing of the traces (phase_times)."""
         self.rt._check(lib().spray_rt_insitu_set_timing(self.h, 1 if on else 0), "set_timing")
 
-    REP_PHASES = ("lists", "keyed_closest_hit", "key_allreduce", "shadows",
-                  "occlusion_allreduce", "film", "totals")
-    PROTOCOL_PHASES = ("route_counts", "ray_exchange", "keyed_closest_hit", "key_composite",
-                       "shading", "shadow_route_exchange", "shadow_any_hit_return",
+    REP_PHASES = ("lists", "keyed_closest_hit", "shadows", "film", "totals")
+    PROTOCOL_PHASES = ("route_plan", "ray_pack_unpack", "keyed_closest_hit", "key_composite",
+                       "shading", "shadow_route_pack", "shadow_any_hit_return",
                        "film_totals")
 
     def phase_times(self):
-        """{phase: ms} accumulated since the last call (then reset)."""
-        out = (C.c_double * 8)()
+        """{phase: ms} accumulated since the last call (then reset); "collectives":
+        the stream time inside the collectives and their count reads."""
+        out = (C.c_double * 9)()
         n = C.c_int(0)
         lib().spray_rt_insitu_phase_times(self.h, C.byref(out), C.byref(n))
-        names = {7: self.REP_PHASES, 8: self.PROTOCOL_PHASES, 1: ("frame",)}.get(
+        names = {5: self.REP_PHASES, 8: self.PROTOCOL_PHASES, 1: ("frame",)}.get(
             n.value, tuple("phase%d" % k for k in range(n.value)))
-        return {names[k]: float(out[k]) for k in range(n.value)}
+        d = {names[k]: float(out[k]) for k in range(n.value)}
+        d["collectives"] = float(out[8])
+        return d
 
     def composite(self, image):
         """HdrImage::composite: SUM of the ranks' images at rank 0."""
