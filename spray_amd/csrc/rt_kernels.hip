@@ -285,6 +285,8 @@ struct SceneArgs {
   const float4* ao_rec;  // per source ray: (origin, pixel), normal, tangent frame
   const float4* ao_lv;   // local hemisphere sample of (pixel, l) at pixel * ao_ns + l
   int ao_ns;
+  // shadow pool of the fused launch (SPRAY_SHADOW_POOL): launch generation
+  uint32_t pool_gen;
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -1178,6 +1180,98 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
   q.n = rest;
 }
 
+// Shadow pool of the fused launch (SPRAY_SHADOW_POOL=1).  A wave that finds
+// its band queues dry publishes the shadow rays still waiting in its LDS
+// queue (fewer than kShadowT) to a launch-wide pool and then drains the
+// pool as 64-ray any-hit packets together with every other idle wave,
+// instead of tracing its own partial packet alone: the launch's last shadow
+// rays leave as full packets, spread over the waves that are free.  Slots
+// are reserved by an atomic on the tail, written, then flagged with the
+// launch's generation (release); a drainer claims up to 64 reserved slots
+// by a CAS on the head and waits for their flags (acquire).  No wave waits
+// for another wave's progress beyond a reserved slot's write: a drainer
+// that finds the pool empty sleeps briefly and leaves after kPoolIdle empty
+// polls, and a publisher drains what it published itself, so every ray is
+// traced even if no other wave is left.
+#ifndef SPRAY_SHADOW_POOL
+#define SPRAY_SHADOW_POOL 0
+#endif
+#if SPRAY_SHADOW_POOL
+constexpr uint32_t kPoolCap = 1u << 19;  // >= resident waves x 64
+constexpr int kPoolIdle = 64;
+__device__ float4 g_pool_ray[2 * kPoolCap];
+__device__ uint32_t g_pool_ready[kPoolCap];
+__device__ uint32_t g_pool_ctr[64];  // [0] reserved tail, [32] claimed head (zeroed per launch)
+
+template <int W>
+__device__ __forceinline__ void shadow_pool(const SceneArgs& A, const ShadowQueue& q,
+                                            const float4* stl, const float* sbox,
+                                            const float4* sdom, int32_t* wstk) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t gen = A.pool_gen;
+  if (q.n) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&g_pool_ctr[0], q.n);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (lane < q.n) {
+      const uint32_t k = base + lane;  // < kPoolCap: the host sizes the grid
+      g_pool_ray[2 * k] =
+          make_float4(q.ray[6 * lane], q.ray[6 * lane + 1], q.ray[6 * lane + 2],
+                      __uint_as_float(q.src[lane]));
+      g_pool_ray[2 * k + 1] =
+          make_float4(q.ray[6 * lane + 3], q.ray[6 * lane + 4], q.ray[6 * lane + 5], 0.f);
+      __hip_atomic_store(&g_pool_ready[k], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  int idle = 0;
+  for (;;) {
+    uint32_t h = 0, n = 0;
+    if (lane == 0) {
+      const uint32_t t = __hip_atomic_load(&g_pool_ctr[0], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      h = __hip_atomic_load(&g_pool_ctr[32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (h < t) {
+        const uint32_t want = t - h < 64u ? t - h : 64u;
+        if (__hip_atomic_compare_exchange_strong(&g_pool_ctr[32], &h, h + want,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          n = want;
+          break;
+        }
+      }
+    }
+    n = __builtin_amdgcn_readfirstlane(n);
+    h = __builtin_amdgcn_readfirstlane(h);
+    if (!n) {
+      if (++idle > kPoolIdle) break;
+      __builtin_amdgcn_s_sleep(16);
+      continue;
+    }
+    idle = 0;
+    const bool v = lane < n;
+    float r6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 1.f};
+    uint32_t src = 0;
+    if (v) {
+      const uint32_t k = h + lane;
+      while (__hip_atomic_load(&g_pool_ready[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
+             gen)
+        __builtin_amdgcn_s_sleep(1);
+      const float4 a = g_pool_ray[2 * k], b = g_pool_ray[2 * k + 1];
+      r6[0] = a.x;
+      r6[1] = a.y;
+      r6[2] = a.z;
+      r6[3] = b.x;
+      r6[4] = b.y;
+      r6[5] = b.z;
+      src = __float_as_uint(a.w);
+    }
+    bool f = false;
+    float p[3], w[3];
+    scene_ray_packet<W, true, kEpiNone>(A, src, v, stl, sbox, sdom, wstk, f, p, w, r6);
+  }
+}
+#endif
+
 // STK: traversal-stack entries per lane, >= the depth of every resident
 // slot tree and of the top-level tree (a node at depth k has at most k
 // pending siblings).  LDS = STK KiB + 4 KiB per 64 domains, so STK 16 lets 8
@@ -1393,6 +1487,12 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     }
   }
   if (SPRAY_WAVE_TIMES) wt2 = wall_clock64();
+#if SPRAY_SHADOW_POOL
+  if (kShadow && persist) {  // the wave's last shadow rays through the pool
+    wave_lds_sync();
+    shadow_pool<W>(A, sq, stl, sbox, sdom, wstk);
+  } else
+#endif
   if (kShadow && sq.n) {  // the wave's last shadow rays (fewer than 64)
     wave_lds_sync();
 #if SPRAY_WAVE_TIMES
@@ -2318,6 +2418,16 @@ static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
+#if SPRAY_SHADOW_POOL
+  if (e == hipSuccess && kPersist && (EPI == kEpiShadow || EPI == kEpiShadowFrame)) {
+    static void* ctr = nullptr;
+    static uint32_t gen = 0;
+    if (!ctr) e = hipGetSymbolAddress(&ctr, HIP_SYMBOL(g_pool_ctr));
+    if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, 64 * sizeof(uint32_t), s);
+    a.pool_gen = ++gen ? gen : ++gen;  // never 0 (the flags' initial value)
+    if (size_t(grid) * (kBlock / 64) * 64 > kPoolCap) return hipErrorInvalidValue;
+  }
+#endif
   if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) &&
       a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
