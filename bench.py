@@ -191,12 +191,15 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     every rank holds the frame's eye rays, traces the rays that touch its
     domains over its domains, and the ranks agree on every ray's winner with
     one MIN all-reduce of the hit keys and on every shadow ray's occlusion with
-    one SUM all-reduce of bytes -- no ray crosses the wire.  AO (and
-    protocol=True) is the stripe protocol (spray_rt_insitu_trace): each rank
-    its horizontal stripe of eye rays, count-first RCCL all-to-all-v exchanges
-    of rays to their owners, key composite, shading at the winner, shadow
-    exchange.  The ranks' images are composited by one RCCL reduce
-    (HdrImage::composite).  Eye rays are made once before timing (resident,
+    one SUM all-reduce of bytes -- no ray crosses the wire.  AO at N > 1 is
+    the replicated-ray AO frame: the same keys, the winners' normals and
+    colours SUM-all-reduced, every rank any-hits every AO ray over its own
+    domains, occlusion count fields SUM-all-reduced, rank 0 films the whole
+    frame (no composite).  protocol=True is the stripe protocol
+    (spray_rt_insitu_trace): each rank its horizontal stripe of eye rays,
+    count-first RCCL all-to-all-v exchanges of rays to their owners, key
+    composite, shading at the winner, shadow exchange.  The ranks' PT images
+    are composited by one RCCL reduce (HdrImage::composite).  Eye rays are made once before timing (resident,
     like the main line).  RCCL is used at every N, N = 1 included (at N = 1
     PT runs the all-local fused frame unless protocol=True).  Timed like the
     main line (barrier + max over ranks); the per-phase device times come
@@ -216,7 +219,7 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     rt.set_stream(torch.cuda.current_stream(dev))
     eng = insitu.InsituEngine(rt, world, rank, dist=dist if world > 1 else None,
                               transport="host" if REHEARSE else "rccl")
-    replicated = kind == "pt" and not protocol
+    replicated = not protocol
     stripe = (0, 0, W, H) if replicated else insitu.horizontal_stripe(world, rank, (0, 0, W, H))
     n = stripe[2] * stripe[3] * SPP
     rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)[:n]
@@ -235,10 +238,14 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
         os.environ["SPRAY_INSITU_LOCAL"] = "0"  # the whole protocol, even at one rank
     trace = eng.trace_frame if replicated else eng.trace
 
+    # the replicated AO frame films the whole image on rank 0: no composite
+    composite = not (replicated and kind == "ao" and world > 1)
+
     def frame():
         image.zero_()
         t = trace(sh, rays, pix, sam, SPP, image)
-        eng.composite(image)
+        if composite:
+            eng.composite(image)
         return t
 
     try:
@@ -280,7 +287,11 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     k = args.steps
     form = ("replicated-ray frame: every rank traces the rays that touch its domains, "
             "keys MIN-all-reduced, occlusion bytes SUM-all-reduced" if replicated and world > 1
-            else "all-local fused frame" if replicated or (world == 1 and not protocol)
+            and kind == "pt"
+            else "replicated-ray AO frame: keys MIN-all-reduced, winners' normals and colours "
+            "SUM-all-reduced, every rank any-hits every AO ray over its domains, occlusion "
+            "count fields SUM-all-reduced, film on rank 0" if replicated and world > 1
+            else "all-local frame" if replicated or (world == 1 and not protocol)
             else "stripe protocol: speculative ray exchange over RCCL all-to-all-v")
     out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
            "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",

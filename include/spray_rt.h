@@ -646,11 +646,18 @@ int spray_rt_insitu_trace(spray_rt_insitu_t ins, const spray_rt_shader* shader,
  *   6. films the unoccluded shadows of the rays it won.
  * No ray, hit or shadow record crosses the wire and no count is exchanged:
  * two all-reduces and one host read per frame.  Results per sample are the
- * protocol's (the same winner, shading and occlusion).  Needs the fused PT
- * case (one bounce, one point light, diffuse surfaces) and, with host
- * collectives, allreduce_min_u64 / allreduce_sum_u8; SPRAY_RT_ERR_UNSUPPORTED
- * otherwise (trace with spray_rt_insitu_trace).  World 1: the all-local
- * fused frame. */
+ * protocol's (the same winner, shading and occlusion).
+ * AO (ooc::ShaderAo, one bounce, <= 32 samples, diffuse surfaces): after 3.
+ * the winners publish their hits' shading normal and colour (one SUM
+ * all-reduce, 16 B per ray of C), every rank spawns the same AO rays of
+ * every hit and any-hits them over its own domains, one SUM all-reduce of
+ * per-sample occlusion count fields (2 / 4 / 8 bits for world <= 3 / 15 /
+ * 64) ORs the group's results, and rank 0 films the WHOLE frame (the other
+ * ranks' images are not touched: no composite needed).  Three all-reduces
+ * and one host read per frame; totals without a collective.
+ * Needs one of those two cases and, with host collectives,
+ * allreduce_min_u64 / allreduce_sum_u8; SPRAY_RT_ERR_UNSUPPORTED otherwise
+ * (trace with spray_rt_insitu_trace).  World 1: the all-local frame. */
 int spray_rt_insitu_trace_frame(spray_rt_insitu_t ins, const spray_rt_shader* shader,
                                 const spray_rt_ray* rays, const int32_t* pixid,
                                 const int32_t* samid, size_t n, int spp, float* image_rgba,

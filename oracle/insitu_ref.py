@@ -185,7 +185,10 @@ def trace_frame_replicated(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, im
     film of the rays it won.  PT, one bounce, one point light.  Returns
     (records, (group's radiance rays, shadow rays))."""
     import torch as t
-    assert sh.bounces == 1 and sh.nlights == 1
+    assert sh.bounces == 1
+    if sh.shader == po.SHADER_AO:
+        return _frame_replicated_ao(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, image)
+    assert sh.nlights == 1
     org, d = np.ascontiguousarray(org, np.float32), np.ascontiguousarray(d, np.float32)
     pix, sam = np.asarray(pix, np.int32), np.asarray(sam, np.int32)
     n = len(org)
@@ -233,3 +236,81 @@ def trace_frame_replicated(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, im
     recs = [(0, int(sam[C[j]]), hits_c[j].tobytes(), int(sv[j]), int(sv[j] and occ[j]))
             for j in np.flatnonzero(win)]
     return recs, (int(tail[0]), int(tail[1]))
+
+
+def _frame_replicated_ao(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, image):
+    """The replicated-ray AO frame (insitu.cpp trace_replicated_ao): the
+    lists, keyed closest hits and key MIN of trace_frame_replicated; the
+    winners publish their hit's shading normal and colour (SUM all-reduce);
+    every rank shades every hit (ooc::ShaderAo: the same AO rays on every
+    rank) and any-hits the rays over its own domains; a SUM all-reduce of
+    the per-sample occlusion counts ORs the results; rank 0 films the whole
+    frame.  Totals need no collective (every rank spawned every AO ray)."""
+    import torch as t
+    ns = po.shadow_slots(sh)
+    org, d = np.ascontiguousarray(org, np.float32), np.ascontiguousarray(d, np.float32)
+    pix, sam = np.asarray(pix, np.int32), np.asarray(sam, np.int32)
+    n = len(org)
+    rays = _rays(org, d)
+    mask = local.route(rays).numpy()
+    C = np.flatnonzero(mask != 0)
+    mine = ((mask[C] >> comm.rank) & 1).astype(bool)
+    keys_c = np.full(len(C), MISS_KEY, np.int64)
+    hits_c = np.zeros(len(C), po.HIT_DTYPE)
+    if mine.any():
+        h, k = local.intersect_keyed(rays[C[mine]])
+        keys_c[mine] = k.numpy()
+        hits_c[mine] = np.ascontiguousarray(h.numpy()).view(po.HIT_DTYPE).reshape(-1)
+    own = keys_c.copy()
+    best = comm.all_reduce_min(t.from_numpy(keys_c.copy())).numpy()
+    hit = best != MISS_KEY
+    win = hit & (own == best)
+    # the winners' normals and colours, on every rank
+    pub = np.zeros((len(C), 4), np.int64)
+    pub[win, 0:3] = np.ascontiguousarray(hits_c["ns"][win]).view(np.uint32)
+    pub[win, 3] = hits_c["color"][win]
+    pub = comm.all_reduce_sum(t.from_numpy(pub)).numpy().astype(np.uint32)
+    hall = np.zeros(len(C), po.HIT_DTYPE)
+    hall["t"] = np.inf
+    hall["prim"] = 0xFFFFFFFF
+    hall["domain"] = -1
+    hall["t"][hit] = (best[hit] >> 32).astype(np.uint32).view(np.float32)
+    hall["domain"][hit] = (best[hit] & 0xFFFF).astype(np.int32)
+    hall["ns"] = np.ascontiguousarray(pub[:, 0:3]).view(np.float32)
+    hall["color"] = pub[:, 3]
+    # every hit's AO rays (the same on every rank)
+    def shade(hits, valid):
+        oc, dc = np.ascontiguousarray(org[C]), np.ascontiguousarray(d[C])
+        w = np.ones((len(C), 3), np.float32)
+        return po.shade(sh, bsdfs, 0, oc, dc, hits, w, valid.astype(np.uint8), pix[C], sam[C])
+    so, sd, sw, sv, aborts = shade(hall, hit)
+    assert aborts == 0
+    sv = sv.astype(bool)
+    # the winner's own shading spawns exactly those rays
+    so2, sd2, sw2, sv2, _ = shade(hits_c, win)
+    ws = np.repeat(win, ns)
+    assert (sv2.astype(bool) == (sv & ws)).all()
+    assert so2[sv2.astype(bool)].tobytes() == so[sv & ws].tobytes()
+    assert sd2[sv2.astype(bool)].tobytes() == sd[sv & ws].tobytes()
+    assert sw2[sv2.astype(bool)].tobytes() == sw[sv & ws].tobytes()
+    sel = np.flatnonzero(sv)
+    occ = np.zeros(len(C) * ns, np.int32)
+    if len(sel):
+        occ[sel] = local.occluded(_rays(so[sel], sd[sel])).numpy()
+    occ = comm.all_reduce_sum(t.from_numpy(occ)).numpy() > 0
+    if comm.rank == 0:
+        lit = np.flatnonzero(sv & ~occ)
+        if len(lit):
+            img = image.reshape(-1, 4)
+            add = ((1.0 / spp) * sw[lit].astype(np.float64)).astype(np.float32)
+            np.add.at(img[:, :3], pix[C[lit // ns]], add)
+    recs = []
+    for j in np.flatnonzero(win):
+        bv = bo = 0
+        for k in range(ns):
+            if sv[j * ns + k]:
+                bv |= 1 << k
+                if occ[j * ns + k]:
+                    bo |= 1 << k
+        recs.append((0, int(sam[C[j]]), hits_c[j].tobytes(), bv, bo))
+    return recs, (n, int(sv.sum()))

@@ -14,8 +14,12 @@ Inputs
 * the measured N = 1 frame (the bench's fused single-GPU frame, --n1-ms).
 
 Model of one frame at N ranks (every rank runs the same sequence):
-  T = max_r(lists + keyed closest hit) + AR(8 |C|) + max_r(shadows)
-      + AR(|C| + 192) + max_r(film) + max_r(totals read) + RED(16 MB)
+  PT: T = max_r(lists + keyed closest hit) + AR(8 |C|) + max_r(shadows)
+          + AR(|C| + 192) + max_r(film) + max_r(totals read) + RED(16 MB)
+  AO: T = max_r(lists + keyed closest hit) + AR(8 |C|) + AR(16 |C|)
+          + max_r(AO rays: spawn + any hit) + AR(16 |C| fb / 8) + film(rank 0)
+          + max_r(totals read)           (fb = 2 / 4 / 8 bits for N <= 3 / 15 / 64;
+                                          no image reduce: rank 0 films all)
   AR(B)  = alpha + 2 (N - 1) / N * B / bw     (ring all-reduce)
   RED(B) = alpha + (N - 1) / N * B / bw * 2   (reduce to rank 0 as reduce-
            scatter + gather)
@@ -41,17 +45,29 @@ def red(b, n, link):
     return link["alpha_ms"] + 2.0 * (n - 1) / n * b / (link["bw_GBs"] * 1e9) * 1e3
 
 
+def fbits(n):
+    return 2 if n <= 3 else (4 if n <= 15 else 8)
+
+
 def project(run, link):
     n = run["world"]
     ranks = run["ranks"]
     ph = lambda r, k: r["phases_ms"].get(k, 0.0)  # noqa: E731
-    st = ranks[0]["stats"]  # bytes_sent = the all-reduce payload 9 |C| + 192 per trace
-    nc = (st["bytes_sent"] / max(st["traces"], 1) - 192) / 9
+    st = ranks[0]["stats"]
+    per = st["bytes_sent"] / max(st["traces"], 1)
     a = max(ph(r, "lists") + ph(r, "keyed_closest_hit") for r in ranks)  # excl. collectives
     b = max(ph(r, "shadows") for r in ranks)
     c = max(ph(r, "film") for r in ranks)
     d = max(ph(r, "totals") for r in ranks)
-    comm = ar(8 * nc, n, link) + ar(nc + 192, n, link) + red(IMAGE_BYTES, n, link)
+    if run.get("kind", "pt") == "ao":
+        # bytes_sent = 24 |C| + |C| * 16 * fb / 8 per trace (keys, normals, fields)
+        fb = fbits(n)
+        nc = per / (24 + 2 * fb)
+        comm = ar(8 * nc, n, link) + ar(16 * nc, n, link) + ar(2 * fb * nc, n, link)
+    else:
+        # bytes_sent = the all-reduce payload 9 |C| + 192 per trace
+        nc = (per - 192) / 9
+        comm = ar(8 * nc, n, link) + ar(nc + 192, n, link) + red(IMAGE_BYTES, n, link)
     return {"device_ms": round(a + b + c + d, 4), "comm_ms": round(comm, 4),
             "frame_ms": round(a + b + c + d + comm, 4),
             "busiest": {"lists+keyed": round(a, 4), "shadows": round(b, 4), "film": round(c, 4),
@@ -61,34 +77,38 @@ def project(run, link):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("rehearse")
-    ap.add_argument("--n1-ms", type=float, default=0.77)
+    ap.add_argument("--n1-ms", type=float, default=0.77, help="measured N = 1 PT frame")
+    ap.add_argument("--n1-ao-ms", type=float, default=None, help="measured N = 1 AO frame")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     rep = json.load(open(args.rehearse))
     rows = []
     for run in rep["runs"]:
-        if run.get("kind", "pt") != "pt":
+        if run.get("kind", "pt") not in ("pt", "ao"):
             continue
         row = {"world": run["world"], "partition": run["partition"],
+               "kind": run.get("kind", "pt"),
                "domains_per_rank": [r["domains"] for r in run["ranks"]],
                "rank_device_ms": [round(sum(v for k, v in r["phases_ms"].items()
                                             if k != "collectives"), 4) for r in run["ranks"]]}
         for name, link in LINK.items():
             p = project(run, link)
-            p["speedup_vs_n1"] = round(args.n1_ms / p["frame_ms"], 3)
+            base = args.n1_ms if row["kind"] == "pt" else args.n1_ao_ms
+            p["speedup_vs_n1"] = round(base / p["frame_ms"], 3) if base else None
             row[name] = p
         rows.append(row)
     out = {"model": __doc__.strip().split("\n\n")[2], "links": LINK, "n1_ms": args.n1_ms,
            "rccl_one_rank_floor": rep.get("rccl_one_rank_floor"), "rows": rows}
-    print("| N | partition | busiest lists+keyed | shadows | film | device ms | comm ms (cons.) "
-          "| frame ms (cons. / opt.) | x N=1 (cons. / opt.) |")
-    print("|---|---|---|---|---|---|---|---|---|")
+    print("| frame | N | partition | busiest lists+keyed | shadows / AO rays | film | device ms "
+          "| comm ms (cons.) | frame ms (cons. / opt.) | x N=1 (cons. / opt.) |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
+    sx = lambda v: "-" if v is None else "%.2f" % v  # noqa: E731
     for r in rows:
         c, o = r["conservative"], r["optimistic"]
-        print("| %d | %s | %.3f | %.3f | %.3f | %.3f | %.3f | %.3f / %.3f | %.2f / %.2f |" % (
-            r["world"], r["partition"], c["busiest"]["lists+keyed"], c["busiest"]["shadows"],
-            c["busiest"]["film"], c["device_ms"], c["comm_ms"], c["frame_ms"], o["frame_ms"],
-            c["speedup_vs_n1"], o["speedup_vs_n1"]))
+        print("| %s | %d | %s | %.3f | %.3f | %.3f | %.3f | %.3f | %.3f / %.3f | %s / %s |" % (
+            r["kind"], r["world"], r["partition"], c["busiest"]["lists+keyed"],
+            c["busiest"]["shadows"], c["busiest"]["film"], c["device_ms"], c["comm_ms"],
+            c["frame_ms"], o["frame_ms"], sx(c["speedup_vs_n1"]), sx(o["speedup_vs_n1"])))
     if args.out:
         with open(args.out, "w") as fh:
             json.dump(out, fh, indent=1)

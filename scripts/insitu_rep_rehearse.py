@@ -63,17 +63,19 @@ def _rank(rank, world, port, mode, frames, out, kind="pt"):
     rt.set_stream(stream)
     eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport="host")
     cam = spray_amd.camera_init(CAM["pos"], CAM["lookat"], CAM["up"], CAM["fov"], W, H)
-    # pt: the replicated-ray frame (every eye ray on every rank); ao: AO-16
-    # through the stripe protocol (the rank's horizontal stripe)
-    stripe = (0, 0, W, H) if kind == "pt" else insitu.horizontal_stripe(world, rank, (0, 0, W, H))
+    # pt / ao: the replicated-ray frames (every eye ray on every rank);
+    # ao_protocol: AO-16 through the stripe protocol (the rank's stripe)
+    proto = kind == "ao_protocol"
+    stripe = insitu.horizontal_stripe(world, rank, (0, 0, W, H)) if proto else (0, 0, W, H)
     n = stripe[2] * stripe[3] * SPP
     rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device="cuda")[:n]
     pix = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
     sam = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
     rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, pix, sam)
-    sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1, ks=SHADE[6:9],
+    ao = kind != "pt"
+    sh = spray_amd.frame.make_shader("ao" if ao else "pt", 1, 16 if ao else 1, ks=SHADE[6:9],
                                      shininess=SHADE[9], lights=lights)
-    trace = eng.trace_frame if kind == "pt" else eng.trace
+    trace = eng.trace if proto else eng.trace_frame
     image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
     rt.sync()
     tot = trace(sh, rays, pix, sam, SPP, image)  # warm-up (buffers)
@@ -124,7 +126,8 @@ def main():
     ap.add_argument("--modes", nargs="+", default=["close", "rr"])
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--kinds", nargs="+", default=["pt"],
-                    help="pt: replicated PT frame (configs[2]); ao: AO-16 protocol (configs[4])")
+                    help="pt: replicated PT frame (configs[2]); ao: replicated AO-16 frame "
+                         "(configs[4]); ao_protocol: AO-16 through the stripe protocol")
     ap.add_argument("--out", default="gpurun_out/rep/rehearse.json")
     ap.add_argument("--rccl-floor", type=int, default=1)
     args = ap.parse_args()
@@ -133,8 +136,8 @@ def main():
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     lock = os.path.join(tempfile.gettempdir(), "spray_insitu_serial_%d.lock" % os.getpid())
     os.environ["SPRAY_INSITU_SERIAL"] = lock
-    report = {"frame": "wavelets64 1024x1024x8spp: PT replicated-ray frame (configs[2]), "
-                       "AO-16 stripe protocol (configs[4])", "runs": []}
+    report = {"frame": "wavelets64 1024x1024x8spp: PT / AO-16 replicated-ray frames "
+                       "(configs[2] / configs[4]), AO-16 stripe protocol", "runs": []}
     for kind, mode, world in itertools.product(args.kinds, args.modes, args.worlds):
         t0 = time.time()
         with tempfile.TemporaryDirectory() as out:
@@ -152,6 +155,8 @@ def main():
         nc = 2600000  # ~ rays of the bench frame with a non-empty domain list
         report["rccl_one_rank_floor"] = rccl_floor({
             "keys_min_u64": (8 * nc, torch.int64, torch.distributed.ReduceOp.MIN),
+            "ao_normals_u64": (16 * nc, torch.int64, torch.distributed.ReduceOp.SUM),
+            "ao_fields_u8": (8 * nc, torch.uint8, torch.distributed.ReduceOp.SUM),
             "occ_sum_u8": (nc + 192, torch.uint8, torch.distributed.ReduceOp.SUM),
             "image_16MB": (W * H * 16, torch.float32, torch.distributed.ReduceOp.SUM),
             "small_8B": (8, torch.int64, torch.distributed.ReduceOp.SUM)})

@@ -156,6 +156,8 @@ struct spray_rt_insitu {
   // replicated-ray frames (trace_replicated)
   DBuf rmask, rfc, rfl, ridx_c, ridx_l, rnum, rsel_tmp, rkeys_n, rhits_n, rkeys_c;
   DBuf rsray, rsflag, rwin, rsvalid, rsw, rocc, rpix, rsam, rhit_c, rnsh;
+  // replicated-ray AO frames (trace_replicated_ao)
+  DBuf apub, arays, ahits, apairs, aocc_p, alv, arec, ascratch, afields, acount;
   // phase timing (spray_rt_insitu_set_timing): events on the stream
   bool timing = false;
   static constexpr int kMaxEv = 48;
@@ -797,9 +799,60 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   return SPRAY_RT_OK;
 }
 
+// Steps 1-3 of a replicated-ray frame: owner-rank masks of every eye ray, C
+// and L (one host read: |C|, which sizes the all-reduces -- the same on
+// every rank -- and, for AO, the largest pixel id of C), the own closest
+// hits (keyed) of L, their keys over C and the MIN all-reduce: keys_c[j] is
+// then the winning key of ray idx_c[j] on every rank.
+int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* pixid, size_t n,
+                   bool want_pixmax, size_t* nc_out, uint32_t* pixmax_out) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  MARK(0);
+  GROW(I->rmask, n * 8);
+  GROW(I->rfc, n);
+  GROW(I->rfl, n);
+  GROW(I->ridx_c, n * 4);
+  GROW(I->ridx_l, n * 4);
+  GROW(I->rnum, 4 * 4);
+  size_t t1 = 0;
+  HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
+  GROW(I->rsel_tmp, t1);
+  uint32_t* dnum = I->rnum.as<uint32_t>();
+  if (want_pixmax) HIPCHK(c, hipMemsetAsync(dnum + 2, 0, 4, s));
+  HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, I->rmask.as<uint64_t>()));
+  HIPCHK(c, launch_rep_flags(s, I->rmask.as<uint64_t>(), n, I->rank, I->rfc.as<uint8_t>(),
+                             I->rfl.as<uint8_t>(), want_pixmax ? pixid : nullptr,
+                             want_pixmax ? dnum + 2 : nullptr));
+  HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
+                                  I->rsel_tmp.p, &t1));
+  HIPCHK(c, launch_select_flagged(s, I->rfl.as<uint8_t>(), n, I->ridx_l.as<uint32_t>(), dnum + 1,
+                                  I->rsel_tmp.p, &t1));
+  HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 12, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  ++I->st[3];
+  uint32_t cnt[3];
+  std::memcpy(cnt, I->h_small, 12);
+  const size_t nc = cnt[0];
+  *nc_out = nc;
+  if (pixmax_out) *pixmax_out = want_pixmax ? cnt[2] : 0;
+  MARK(1);
+  GROW(I->rkeys_n, n * 8);
+  GROW(I->rhits_n, n * 48);
+  GROW(I->rkeys_c, nc * 8 + 8);
+  if (cnt[1])
+    HIPCHK(c, launch_scene_intersect_keyed_indexed(s, view(c), rays, n, I->ridx_l.as<uint32_t>(),
+                                                   dnum + 1, I->rhits_n.as<spray_rt_hit>(),
+                                                   I->rkeys_n.as<uint64_t>()));
+  HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
+                            I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
+  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
+  return SPRAY_RT_OK;
+}
+
 // The frame with replicated eye rays (spray_rt_insitu_trace_frame): see
-// include/spray_rt.h.  Phases: 0 lists, 1 keyed closest hit, 2 key
-// all-reduce, 3 shadows, 4 occlusion all-reduce, 5 film, 6 totals.
+// include/spray_rt.h.  Phases: 0 lists, 1 keyed closest hit, 2 shadows,
+// 3 film, 4 totals (collectives: kCommPhase).
 int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
                      const int32_t* pixid, const int32_t* samid, size_t n, int spp,
                      float* image, const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
@@ -812,47 +865,11 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                              lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                              P->ks[2],       P->shininess};
   std::memcpy(A.shade10, shade10, sizeof(shade10));
-  MARK(0);
-  // ---- 1. owner-rank masks, C and L (one host read: |C|, which sizes the
-  // all-reduces -- the same on every rank)
-  GROW(I->rmask, n * 8);
-  GROW(I->rfc, n);
-  GROW(I->rfl, n);
-  GROW(I->ridx_c, n * 4);
-  GROW(I->ridx_l, n * 4);
-  GROW(I->rnum, 2 * 4);
-  size_t t1 = 0;
-  HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
-  GROW(I->rsel_tmp, t1);
-  uint32_t* dnum = I->rnum.as<uint32_t>();
-  HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, I->rmask.as<uint64_t>()));
-  HIPCHK(c, launch_rep_flags(s, I->rmask.as<uint64_t>(), n, I->rank, I->rfc.as<uint8_t>(),
-                             I->rfl.as<uint8_t>()));
-  HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
-                                  I->rsel_tmp.p, &t1));
-  HIPCHK(c, launch_select_flagged(s, I->rfl.as<uint8_t>(), n, I->ridx_l.as<uint32_t>(), dnum + 1,
-                                  I->rsel_tmp.p, &t1));
-  HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  ++I->st[3];
-  uint32_t cnt[2];
-  std::memcpy(cnt, I->h_small, 8);
-  const size_t nc = cnt[0];
-  // ---- 2. own closest hits (keyed) of L, their keys over C
-  MARK(1);
-  GROW(I->rkeys_n, n * 8);
-  GROW(I->rhits_n, n * 48);
-  GROW(I->rkeys_c, nc * 8 + 8);
-  if (cnt[1])
-    HIPCHK(c, launch_scene_intersect_keyed_indexed(s, view(c), rays, n, I->ridx_l.as<uint32_t>(),
-                                                   dnum + 1, I->rhits_n.as<spray_rt_hit>(),
-                                                   I->rkeys_n.as<uint64_t>()));
-  HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
-                            I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
-  // ---- 3. the winning key of every ray of C, on every rank
+  // ---- 1-3. lists, own keyed closest hits, the winning keys
+  size_t nc = 0;
+  CALL(rep_lists_keys(I, rays, pixid, n, false, &nc, nullptr));
   I->st[0] += 9 * nc + 192;  // the two all-reduces' payload (stats: bytes sent / received)
   I->st[1] += 9 * nc + 192;
-  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   // ---- 4. shadow rays of every hit, own any hit; the winners shade
   MARK(2);
   GROW(I->rsray, nc * 32 + 32);
@@ -918,6 +935,113 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   return SPRAY_RT_OK;
 }
 
+// The replicated-ray AO frame (ooc::ShaderAo, one bounce, diffuse
+// surfaces): steps 1-3 as trace_replicated; then the winners publish their
+// hits' shading normal and colour (a SUM all-reduce, 16 B per ray of C), so
+// every rank holds every hit's AO spawn input and spawns the same (source,
+// sample) pairs (launch_spawn_ao_pairs, ao_ok exact); each traces them over
+// its own domains; a SUM all-reduce of per-sample occlusion count fields
+// (fb bits each, position j * ns + l) ORs the group's results; rank 0 then
+// holds every weight and occlusion and films the whole frame (the other
+// ranks' images stay untouched: no composite is needed).  Records: each rank
+// its winners.  Totals: radiance rays n, AO rays = the pairs (the same count
+// on every rank), no all-reduce.  Phases: 0 lists, 1 keyed closest hit,
+// 2 AO rays (publish, spawn, any hit), 3 film, 4 totals.
+int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
+                        const int32_t* pixid, const int32_t* samid, size_t n, int spp,
+                        float* image, const spray_rt_insitu_rec* rec,
+                        unsigned long long totals[3]) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  const int ns = P->samples;
+  size_t nc = 0;
+  uint32_t pixmax = 0;
+  CALL(rep_lists_keys(I, rays, pixid, n, true, &nc, &pixmax));
+  if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C| >= 2^27");
+  MARK(2);
+  const int fb = I->world <= 3 ? 2 : (I->world <= 15 ? 4 : 8);
+  const size_t npair = nc * size_t(ns);
+  const size_t words = (npair * size_t(fb) + 31) / 32;
+  const size_t npix = size_t(pixmax) + 1;
+  GROW(I->apub, nc * 16 + 16);
+  GROW(I->rwin, nc + 1);
+  GROW(I->arays, nc * 32 + 32);
+  GROW(I->rpix, nc * 4 + 4);
+  GROW(I->rsam, nc * 4 + 4);
+  GROW(I->ahits, nc * 48 + 48);
+  GROW(I->apairs, npair * 4 + 4);
+  GROW(I->aocc_p, npair + 1);
+  GROW(I->alv, npix * size_t(ns) * 16);
+  GROW(I->arec, nc * 64 + 64);
+  GROW(I->ascratch, ao_scratch_bytes(nc, ns));
+  GROW(I->afields, words * 4 + 4);
+  GROW(I->acount, 8);
+  if (rec) GROW(I->rhit_c, nc * 48 + 48);
+  RepAoArgs A{};
+  A.nc = nc;
+  A.rank = I->rank;
+  A.ns = ns;
+  A.fb = fb;
+  A.idx_c = I->ridx_c.as<uint32_t>();
+  A.keys_c = I->rkeys_c.as<uint64_t>();
+  A.keys_n = I->rkeys_n.as<uint64_t>();
+  A.mask = I->rmask.as<uint64_t>();
+  A.rays = reinterpret_cast<const float4*>(rays);
+  A.hits_n = I->rhits_n.as<spray_rt_hit>();
+  A.pix = pixid;
+  A.sam = samid;
+  A.pub = I->apub.as<uint4>();
+  A.win = I->rwin.as<uint8_t>();
+  A.rays_c = I->arays.as<float4>();
+  A.pix_c = I->rpix.as<int32_t>();
+  A.sam_c = I->rsam.as<int32_t>();
+  A.hit_c = rec ? I->rhit_c.as<spray_rt_hit>() : nullptr;
+  A.hits_all = I->ahits.as<spray_rt_hit>();
+  A.rec_ao = I->arec.as<float4>();
+  A.lv = I->alv.as<float4>();
+  A.fields = I->afields.as<uint32_t>();
+  uint32_t* dcount = I->acount.as<uint32_t>();
+  HIPCHK(c, launch_rep_ao_publish(s, A));
+  // ---- 4. the winners' normals and colours on every rank
+  I->st[0] += 24 * nc + 4 * words;  // the three all-reduces' payload
+  I->st[1] += 24 * nc + 4 * words;
+  if (nc) COMM(I->tr->allreduce_u64(I, reinterpret_cast<unsigned long long*>(A.pub), 2 * nc));
+  // ---- 5. every hit's AO rays (the same pairs on every rank), own any hit
+  HIPCHK(c, launch_rep_ao_hits(s, A));
+  HIPCHK(c, hipMemsetAsync(dcount, 0, 4, s));
+  HIPCHK(c, hipMemsetAsync(I->afields.p, 0, words * 4, s));
+  if (nc) {
+    HIPCHK(c, launch_spawn_ao_pairs(s, reinterpret_cast<const spray_rt_ray*>(A.rays_c), A.hits_all,
+                                    A.pix_c, nc, ns, npix, I->apairs.as<uint32_t>(),
+                                    I->alv.as<float>(), I->arec.as<float>(), dcount,
+                                    I->ascratch.p));
+    HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
+                                       I->arec.as<float>(), I->alv.as<float>(), ns, dcount,
+                                       I->aocc_p.as<uint8_t>(), nullptr));
+    HIPCHK(c, launch_rep_ao_scatter(s, I->apairs.as<uint32_t>(), dcount, npair,
+                                    I->aocc_p.as<uint8_t>(), ns, fb, I->afields.as<uint32_t>()));
+  }
+  // ---- 6. occlusion OR over the group: a SUM of the count fields' bytes
+  if (words) COMM(I->tr->allreduce_sum_u8(I, I->afields.as<uint8_t>(), words * 4));
+  // ---- 7. the whole film on rank 0; records of each rank's winners
+  MARK(3);
+  if (I->rank == 0) HIPCHK(c, launch_rep_ao_film(s, A, image, 1.0 / double(spp)));
+  if (rec) HIPCHK(c, launch_rep_ao_record(s, A, *rec));
+  MARK(4);
+  uint32_t* hp = reinterpret_cast<uint32_t*>(I->h_small + 128);
+  HIPCHK(c, hipMemcpyAsync(hp, dcount, 4, hipMemcpyDeviceToHost, s));
+  MARK(4);
+  HIPCHK(c, hipStreamSynchronize(s));
+  flush_phases(I, 5);
+  if (totals) {
+    totals[0] = n;
+    totals[1] = *hp;
+    totals[2] = 0;
+  }
+  ++I->st[5];
+  return SPRAY_RT_OK;
+}
+
 void free_all(spray_rt_insitu* I) {
   DBuf* all[] = {&I->hray[0], &I->hray[1], &I->hw[0], &I->hw[1], &I->hpix[0], &I->hpix[1],
                  &I->hsam[0], &I->hsam[1], &I->mask, &I->idx, &I->starts, &I->plan_tmp,
@@ -928,7 +1052,9 @@ void free_all(spray_rt_insitu* I) {
                  &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot, &I->rmask, &I->rfc, &I->rfl,
                  &I->ridx_c, &I->ridx_l, &I->rnum, &I->rsel_tmp, &I->rkeys_n, &I->rhits_n,
                  &I->rkeys_c, &I->rsray, &I->rsflag, &I->rwin, &I->rsvalid, &I->rsw, &I->rocc,
-                 &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh};
+                 &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
+                 &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
+                 &I->afields, &I->acount};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
@@ -1119,9 +1245,12 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t I, const spray_rt_shader* P,
   int r = scene_common(c, image, 1, image);
   if (r) return r;
   if (!c->d_owner) return fail(c, SPRAY_RT_ERR_STATE, "no owner map set");
-  if (!fused_pt_shading(c, P))
+  const bool ao = P->shader == SPRAY_RT_SHADER_AO && P->bounces == 1 && !c->bsdf_delta &&
+                  P->samples >= 1 && P->samples <= 32;
+  if (!fused_pt_shading(c, P) && !ao)
     return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
-                "replicated frames need one bounce, one point light and diffuse surfaces");
+                "replicated frames need one bounce, diffuse surfaces and one point light "
+                "(PT) or <= 32 samples (AO)");
   if (!I->tr->has_rep())
     return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
                 "the host transport gives no allreduce_min_u64 / allreduce_sum_u8");
@@ -1131,7 +1260,8 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t I, const spray_rt_shader* P,
     r = trace_local(I, P, rays, pixid, samid, n, spp, image, rec, totals);
     flush_phases(I, 1);
   } else {
-    r = trace_replicated(I, P, rays, pixid, samid, n, spp, image, rec, totals);
+    r = ao ? trace_replicated_ao(I, P, rays, pixid, samid, n, spp, image, rec, totals)
+           : trace_replicated(I, P, rays, pixid, samid, n, spp, image, rec, totals);
   }
   I->tr->serial_end();
   return r;

@@ -61,9 +61,11 @@ hipError_t launch_weights_one(hipStream_t s, float* w, size_t n);
 hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_hit* hits,
                             size_t n, uint8_t* win);
 // ---- replicated-ray frames (insitu.cpp, trace_replicated) ----
-// fc[i] = mask[i] != 0 (some domain on the list), fl[i] = bit `rank` of it
+// fc[i] = mask[i] != 0 (some domain on the list), fl[i] = bit `rank` of it;
+// pixmax (optional, zeroed): atomic max of pix[i] over C
 hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
-                            uint8_t* fl);
+                            uint8_t* fl, const int32_t* pix = nullptr,
+                            uint32_t* pixmax = nullptr);
 // keys_c[j] = keys_n[idx_c[j]] where bit `rank` of its mask is set, else a miss
 hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
                            int rank, const uint64_t* keys_n, uint64_t* keys_c);
@@ -94,6 +96,39 @@ hipError_t launch_rep_spawn(hipStream_t s, const RepSpawnArgs& a);
 // tail[64 c + k] = bit k of {nrad, *nshadow, 0}[c] (192 bytes)
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow);
+// ---- replicated-ray AO frames (insitu.cpp, trace_replicated_ao) ----
+struct RepAoArgs {
+  size_t nc;
+  int rank;
+  int ns;                       // AO samples per hit (<= 32)
+  int fb;                       // bits per occlusion count field (2, 4 or 8)
+  const uint32_t* idx_c;        // [nc] ray ids of C
+  const uint64_t* keys_c;       // [nc] winning keys (after the MIN all-reduce)
+  const uint64_t* keys_n;       // [n] this rank's keys (valid where its mask bit is set)
+  const uint64_t* mask;         // [n] owner-rank masks
+  const float4* rays;           // [n] eye rays (32 B)
+  const spray_rt_hit* hits_n;   // [n] this rank's hit records
+  const int32_t* pix;           // [n]
+  const int32_t* sam;           // [n]
+  uint4* pub;                   // [nc] winner's normal bits + colour, zeros elsewhere
+  uint8_t* win;                 // [nc] 1: this rank won ray j
+  float4* rays_c;               // [nc] C's rays (32 B)
+  int32_t* pix_c;               // [nc]
+  int32_t* sam_c;               // [nc]
+  spray_rt_hit* hit_c;          // [nc] winners' hit records (optional: records)
+  spray_rt_hit* hits_all;       // [nc] every ray's hit as the group sees it
+  const float4* rec_ao;         // [nc] AO spawn records (launch_spawn_ao_pairs)
+  const float4* lv;             // (pixel, sample) table (launch_spawn_ao_pairs)
+  const uint32_t* fields;       // occlusion count fields, position j * ns + l
+};
+hipError_t launch_rep_ao_publish(hipStream_t s, const RepAoArgs& a);
+hipError_t launch_rep_ao_hits(hipStream_t s, const RepAoArgs& a);
+// fields[(j * ns + l) field] |= 1 for every occluded pair k < *d_count
+hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uint32_t* d_count,
+                                 size_t max_n, const uint8_t* occ, int ns, int fb,
+                                 uint32_t* fields);
+hipError_t launch_rep_ao_film(hipStream_t s, const RepAoArgs& a, float* image, double scale);
+hipError_t launch_rep_ao_record(hipStream_t s, const RepAoArgs& a, const spray_rt_insitu_rec& rec);
 // counts[r] = starts[r + 1] - starts[r], r < world (<= 64)
 hipError_t launch_counts_from_starts(hipStream_t s, const int64_t* starts, int world,
                                      int64_t* counts);

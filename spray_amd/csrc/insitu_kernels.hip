@@ -166,29 +166,9 @@ __global__ __launch_bounds__(kBlock) void k_occ_return(const int64_t* __restrict
 // are neighbours (the spp samples of a pixel travel together), so a
 // segmented scan over the wave's runs of equal pixels leaves one hardware
 // fp32 atomic per run and channel at the run's last lane.
-__global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ image,
-                                                        const int32_t* __restrict__ pix,
-                                                        size_t m, int ns,
-                                                        const float4* __restrict__ sw,
-                                                        const uint8_t* __restrict__ sv,
-                                                        const uint8_t* __restrict__ occ,
-                                                        double scale) {
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+__device__ __forceinline__ void film_runs(float* __restrict__ image, bool in, int32_t p,
+                                          bool any, float a0, float a1, float a2) {
   const int lane = threadIdx.x & 63;
-  const bool in = i < m;
-  const int32_t p = in ? pix[i] : -1;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-  bool any = false;
-  if (in)
-    for (int k = 0; k < ns; ++k) {
-      const size_t j = i * size_t(ns) + k;
-      if (!sv[j] || occ[j]) continue;
-      const float4 L = sw[j];
-      a0 += float(scale * double(L.x));
-      a1 += float(scale * double(L.y));
-      a2 += float(scale * double(L.z));
-      any = true;
-    }
   if (__ballot(any) == 0ull) return;
   // runs of equal pixels: heads, and each lane's run start
   const int32_t pp = __shfl_up(p, 1);
@@ -215,6 +195,31 @@ __global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ imag
     unsafeAtomicAdd(px + 1, a1);
     unsafeAtomicAdd(px + 2, a2);
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ image,
+                                                        const int32_t* __restrict__ pix,
+                                                        size_t m, int ns,
+                                                        const float4* __restrict__ sw,
+                                                        const uint8_t* __restrict__ sv,
+                                                        const uint8_t* __restrict__ occ,
+                                                        double scale) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool in = i < m;
+  const int32_t p = in ? pix[i] : -1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  bool any = false;
+  if (in)
+    for (int k = 0; k < ns; ++k) {
+      const size_t j = i * size_t(ns) + k;
+      if (!sv[j] || occ[j]) continue;
+      const float4 L = sw[j];
+      a0 += float(scale * double(L.x));
+      a1 += float(scale * double(L.y));
+      a2 += float(scale * double(L.z));
+      any = true;
+    }
+  film_runs(image, in, p, any, a0, a1, a2);
 }
 
 __global__ __launch_bounds__(kBlock) void k_record(const uint8_t* __restrict__ win, size_t m,
@@ -280,14 +285,25 @@ __global__ __launch_bounds__(kBlock) void k_weights_one(float4* __restrict__ w, 
 // Every rank holds the frame's eye rays; C = the rays whose domain list is
 // not empty (the same ascending list on every rank), L = the rays with a
 // domain of this rank on their list.
+// pixmax (optional): the largest pixel id of C (the AO frame's sample table)
 __global__ __launch_bounds__(kBlock) void k_rep_flags(const uint64_t* __restrict__ mask, size_t n,
                                                       int rank, uint8_t* __restrict__ fc,
-                                                      uint8_t* __restrict__ fl) {
+                                                      uint8_t* __restrict__ fl,
+                                                      const int32_t* __restrict__ pix,
+                                                      uint32_t* __restrict__ pixmax) {
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t m = mask[i];
-  fc[i] = m != 0;
-  fl[i] = uint8_t((m >> rank) & 1ull);
+  uint32_t px = 0;
+  if (i < n) {
+    const uint64_t m = mask[i];
+    fc[i] = m != 0;
+    fl[i] = uint8_t((m >> rank) & 1ull);
+    if (pixmax && m) px = uint32_t(max(pix[i], 0));
+  }
+  if (pixmax) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) px = max(px, uint32_t(__shfl_xor(int(px), off)));
+    if ((threadIdx.x & 63) == 0 && px) atomicMax(pixmax, px);
+  }
 }
 
 // keys_c[j] = this rank's key of ray idx_c[j] (a miss where no domain of the
@@ -368,6 +384,146 @@ __global__ void k_rep_totals(uint8_t* __restrict__ tail, unsigned long long nrad
   tail[k] = uint8_t((v >> b) & 1ull);
 }
 
+
+// ---- replicated-ray AO frames (insitu.cpp, trace_replicated_ao) ----------
+// After the key MIN all-reduce: the winner of ray j of C publishes its hit's
+// shading normal and colour (the rest of the group contributes zeros to the
+// SUM all-reduce that follows), and every rank gathers C's rays, pixels and
+// samples.
+__global__ __launch_bounds__(kBlock) void k_rep_ao_publish(RepAoArgs A) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= A.nc) return;
+  const uint32_t i = A.idx_c[j];
+  const uint64_t key = A.keys_c[j];
+  const bool win =
+      key != kInsituMissKey && ((A.mask[i] >> A.rank) & 1ull) && A.keys_n[i] == key;
+  uint4 pub = make_uint4(0u, 0u, 0u, 0u);
+  if (win) {
+    const spray_rt_hit h = A.hits_n[i];
+    pub = make_uint4(__float_as_uint(h.ns[0]), __float_as_uint(h.ns[1]),
+                     __float_as_uint(h.ns[2]), h.color);
+    if (A.hit_c) A.hit_c[j] = h;
+  }
+  A.pub[j] = pub;
+  A.win[j] = win;
+  A.rays_c[2 * j] = A.rays[2 * size_t(i)];
+  A.rays_c[2 * j + 1] = A.rays[2 * size_t(i) + 1];
+  A.pix_c[j] = A.pix[i];
+  A.sam_c[j] = A.sam[i];
+}
+
+// The hit of every ray of C as the whole group sees it after the publish
+// all-reduce: t and domain from the winning key, normal and colour from the
+// winner -- every field ooc::ShaderAo's spawn reads (ao_ok, ao_sample).
+__global__ __launch_bounds__(kBlock) void k_rep_ao_hits(RepAoArgs A) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= A.nc) return;
+  const uint64_t key = A.keys_c[j];
+  const uint4 pub = A.pub[j];
+  const bool hit = key != kInsituMissKey;
+  float4* h = reinterpret_cast<float4*>(A.hits_all + j);
+  h[0] = make_float4(hit ? __uint_as_float(uint32_t(key >> 32)) : kInf, 0.f, 0.f,
+                     __uint_as_float(0xFFFFFFFFu));
+  h[1] = make_float4(0.f, 0.f, 0.f, __uint_as_float(pub.w));
+  h[2] = make_float4(__uint_as_float(pub.x), __uint_as_float(pub.y), __uint_as_float(pub.z),
+                     __int_as_float(hit ? int32_t(key & 0xFFFFull) : -1));
+}
+
+// occlusion of pair k (this rank's domains) into the positional count field
+// of (source, sample): fields of fb bits (a SUM of `world` ones fits), so the
+// SUM all-reduce of their bytes counts the ranks that found an occluder
+__global__ __launch_bounds__(kBlock) void k_rep_ao_scatter(const uint32_t* __restrict__ pairs,
+                                                           const uint32_t* __restrict__ d_count,
+                                                           size_t max_n,
+                                                           const uint8_t* __restrict__ occ,
+                                                           int ns, int fb,
+                                                           uint32_t* __restrict__ fields) {
+  const size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= max_n || k >= *d_count || !occ[k]) return;
+  const uint32_t pr = pairs[k];
+  const size_t pos = size_t(pr >> 5) * uint32_t(ns) + (pr & 31u);
+  const uint32_t per = 32u / uint32_t(fb);
+  atomicOr(fields + pos / per, 1u << (uint32_t(pos % per) * uint32_t(fb)));
+}
+
+__device__ __forceinline__ bool rep_ao_occluded(const uint32_t* __restrict__ fields, size_t pos,
+                                                int fb) {
+  const uint32_t per = 32u / uint32_t(fb);
+  return ((fields[pos / per] >> (uint32_t(pos % per) * uint32_t(fb))) & ((1u << fb) - 1u)) != 0u;
+}
+
+// Sample l of ray j of C: ooc::ShaderAo's light weight (frame_kernels.hip,
+// k_shade, path weight (1, 1, 1)) from the direction the any-hit lanes
+// generated (record + (pixel, l) table: hemisphere_apply, the same bits).
+__device__ __forceinline__ void rep_ao_weight(const RepAoArgs& A, size_t j, int32_t px, int l,
+                                              const float kd[3], float L[3]) {
+  const float4* rc = A.rec_ao + 4 * j;
+  const float4 n4 = rc[1], x4 = rc[2], y4 = rc[3];
+  const float4 l4 = A.lv[size_t(px) * uint32_t(A.ns) + uint32_t(l)];
+  const float N[3] = {n4.x, n4.y, n4.z}, ax[3] = {x4.x, x4.y, x4.z}, ay[3] = {y4.x, y4.y, y4.z};
+  const float lv[3] = {l4.x, l4.y, l4.z};
+  float wi[3], pdf;
+  hemisphere_apply(lv, N, ax, ay, wi, pdf);
+  const float ao_w = 1.0f / float(A.ns);
+  const float ct = gclamp01(gdot3(N, wi));
+  const float s = 0.3183098861837907f * ct * ao_w / pdf;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) L[k] = (1.0f * kd[k]) * s;
+}
+
+// The film of the whole frame on one rank (every AO weight and occlusion is
+// known there after the all-reduces): one thread per ray of C, its samples
+// in order, the unoccluded ones added (k_film_atomic's sums and atomics).
+__global__ __launch_bounds__(kBlock) void k_rep_ao_film(RepAoArgs A, float* __restrict__ image,
+                                                        double scale) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool in = j < A.nc;
+  const int32_t p = in ? A.pix_c[j] : -1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  bool any = false;
+  if (in) {
+    const spray_rt_hit h = A.hits_all[j];
+    if (h.domain >= 0) {
+      const spray_rt_ray* ray = reinterpret_cast<const spray_rt_ray*>(A.rays_c) + j;
+      float kd[3];
+      unpack_rgb(h.color, kd);
+      for (int l = 0; l < A.ns; ++l) {
+        if (!ao_ok(ray, h, p, l, A.ns)) continue;
+        if (rep_ao_occluded(A.fields, j * size_t(A.ns) + l, A.fb)) continue;
+        float L[3];
+        rep_ao_weight(A, j, p, l, kd, L);
+        a0 += float(scale * double(L[0]));
+        a1 += float(scale * double(L[1]));
+        a2 += float(scale * double(L[2]));
+        any = true;
+      }
+    }
+  }
+  film_runs(image, in, p, any, a0, a1, a2);
+}
+
+// records of the rays this rank won: the winner's hit record, the spawned
+// samples (ao_ok) and the occluded ones
+__global__ __launch_bounds__(kBlock) void k_rep_ao_record(RepAoArgs A, spray_rt_insitu_rec rec) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= A.nc || !A.win[j]) return;
+  const spray_rt_hit h = A.hits_all[j];
+  const spray_rt_ray* ray = reinterpret_cast<const spray_rt_ray*>(A.rays_c) + j;
+  const int32_t p = A.pix_c[j];
+  unsigned long long v = 0, o = 0;
+  for (int l = 0; l < A.ns && l < 64; ++l) {
+    if (!ao_ok(ray, h, p, l, A.ns)) continue;
+    v |= 1ull << l;
+    if (rep_ao_occluded(A.fields, j * size_t(A.ns) + l, A.fb)) o |= 1ull << l;
+  }
+  const uint32_t k = atomicAdd(rec.d_count, 1u);
+  if (k >= rec.cap) return;
+  rec.samid[k] = A.sam_c[j];
+  rec.bounce[k] = 0;
+  rec.hits[k] = A.hit_c[j];
+  rec.svalid[k] = v;
+  rec.occluded[k] = o;
+}
 }  // namespace
 
 #define LAUNCH(n, kern, ...)                                  \
@@ -459,8 +615,8 @@ hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
 }
 hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
-                            uint8_t* fl) {
-  LAUNCH(n, k_rep_flags, mask, n, rank, fc, fl);
+                            uint8_t* fl, const int32_t* pix, uint32_t* pixmax) {
+  LAUNCH(n, k_rep_flags, mask, n, rank, fc, fl, pix, pixmax);
 }
 hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
                            int rank, const uint64_t* keys_n, uint64_t* keys_c) {
@@ -473,6 +629,25 @@ hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nr
                              const unsigned long long* nshadow) {
   k_rep_totals<<<1, 192, 0, s>>>(tail, nrad, nshadow);
   return hipGetLastError();
+}
+
+hipError_t launch_rep_ao_publish(hipStream_t s, const RepAoArgs& a) {
+  LAUNCH(a.nc, k_rep_ao_publish, a);
+}
+hipError_t launch_rep_ao_hits(hipStream_t s, const RepAoArgs& a) {
+  LAUNCH(a.nc, k_rep_ao_hits, a);
+}
+hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uint32_t* d_count,
+                                 size_t max_n, const uint8_t* occ, int ns, int fb,
+                                 uint32_t* fields) {
+  LAUNCH(max_n, k_rep_ao_scatter, pairs, d_count, max_n, occ, ns, fb, fields);
+}
+hipError_t launch_rep_ao_film(hipStream_t s, const RepAoArgs& a, float* image, double scale) {
+  LAUNCH(a.nc, k_rep_ao_film, a, image, scale);
+}
+hipError_t launch_rep_ao_record(hipStream_t s, const RepAoArgs& a,
+                                const spray_rt_insitu_rec& rec) {
+  LAUNCH(a.nc, k_rep_ao_record, a, rec);
 }
 
 }  // namespace spray_rt

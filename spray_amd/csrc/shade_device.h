@@ -205,5 +205,70 @@ __device__ __forceinline__ bool shade_pt_point(const float o[3], const float d[3
   return has_positive(L);
 }
 
+// ooc::ShaderAo (src/ooc/ooc_shader_ao.h:120-146): nsamples cosine-weighted
+// hemisphere directions per hit (DiffuseBsdf::sampleRandom, reflection.h:
+// 245-249; getCosineHemisphereSample, sampler.cc:54-60; ConcentricDisk-
+// Sampling, sampler.h:49-92; localToWorld, sampler.h:101-110), seeded by
+// pixid * (l + 1).  Sample l of hit i is emitted when its radiance weight
+// is positive.  Operation order as the oracle (glm), trig rounded once from
+// double (shade_device.h), so directions equal the host's bit for bit.
+struct AoOut {
+  float o[3], w[3];
+  bool ok;
+};
+__device__ __forceinline__ AoOut ao_sample(const spray_rt_ray& ray, const spray_rt_hit& h,
+                                           int32_t pixid, int l, int nsamples) {
+  AoOut r;
+  r.ok = false;
+  if (h.domain < 0) return r;
+  const float* o = ray.org;
+  const float* d = ray.dir;
+  r.o[0] = d[0] * h.t + o[0];
+  r.o[1] = d[1] * h.t + o[1];
+  r.o[2] = d[2] * h.t + o[2];
+  const float kd[3] = {float(double((h.color >> 16) & 0xffu) * 0.00392156862745098),
+                       float(double((h.color >> 8) & 0xffu) * 0.00392156862745098),
+                       float(double(h.color & 0xffu) * 0.00392156862745098)};
+  const float wo[3] = {-d[0], -d[1], -d[2]};
+  float N[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  if (!(gdot3(wo, N) > 0.0f)) {
+    N[0] = -N[0];
+    N[1] = -N[1];
+    N[2] = -N[2];
+  }
+  gnorm3(N);
+  const float ao_w = 1.0f / float(nsamples);
+  uint32_t st = sampler_init1(pixid * (l + 1));
+  const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+  float pdf;
+  cosine_hemisphere(u1, u2, N, r.w, pdf);
+  float ct = gdot3(N, r.w);
+  ct = ct < 0.0f ? 0.0f : (ct > 1.0f ? 1.0f : ct);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (kd[k] * (0.3183098861837907f * ct * ao_w / pdf) > 0.0f) r.ok = true;
+  return r;
+}
+
+// Whether sample l of a hit yields an AO ray -- ao_sample(...).ok, without
+// the trigonometry in the common case.  The concentric-disk radius is
+// rr = max(|sx|, |sy|); for rr < 0.999 the local direction has
+// lv.z >= 0.0447, so ct = N . w and pdf = lv.z / pi are positive and finite
+// and the weight kd * (ct / (pi * ns * pdf)) is positive exactly when a
+// colour channel is (kd >= 1/255, the factor is ~1/ns: no underflow) --
+// given a finite normalised N.  Otherwise the full sample decides.
+__device__ __forceinline__ bool ao_ok(const spray_rt_ray* ray, const spray_rt_hit& h,
+                                      int32_t pixid, int l, int nsamples) {
+  if (h.domain < 0) return false;
+  float N[3] = {h.ns[0], h.ns[1], h.ns[2]};
+  gnorm3(N);
+  const bool nfin = isfinite(N[0]) && isfinite(N[1]) && isfinite(N[2]);
+  uint32_t st = sampler_init1(pixid * (l + 1));
+  const float u1 = sampler_1d(st), u2 = sampler_1d(st);
+  const float rr = fmaxf(fabsf(2 * u1 - 1), fabsf(2 * u2 - 1));
+  if (nfin && rr < 0.999f) return (h.color & 0xFFFFFFu) != 0u;
+  return ao_sample(*ray, h, pixid, l, nsamples).ok;  // the ray is read only here
+}
+
 }  // namespace
 }  // namespace spray_rt

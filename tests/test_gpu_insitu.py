@@ -265,41 +265,48 @@ def test_engine_two_ranks_one_owner(oracle):
     assert res[0][3]["bytes_sent"] > 0
 
 
-@pytest.mark.parametrize("world,mode", [(2, 0), (8, 0), (8, 1), (3, 1)])
-def test_engine_replicated_frame_ranks(oracle, world, mode):
+@pytest.mark.parametrize("world,mode,case", [(2, 0, "pt1"), (8, 0, "pt1"), (8, 1, "pt1"),
+                                             (3, 1, "pt1"), (2, 0, "ao16"), (3, 1, "ao16"),
+                                             (8, 0, "ao16"), (8, 1, "ao16")])
+def test_engine_replicated_frame_ranks(oracle, world, mode, case):
     """spray_rt_insitu_trace_frame with world processes sharing the GPU over
     the host transport: every eye ray on every rank, the keys' MIN and the
     occlusion bytes' SUM all-reduced (the host transport's
-    allreduce_min_u64 / allreduce_sum_u8) -- every shaded sample bit-exact
-    against the whole-scene oracle, totals exact, the image within
-    summation-order tolerance; both partitions."""
+    allreduce_min_u64 / allreduce_sum_u8; AO: the winners' normals and
+    colours SUM-all-reduced, occlusion as 2- / 4-bit count fields, the film
+    on rank 0) -- every shaded sample bit-exact against the whole-scene
+    oracle, totals exact, the image within summation-order tolerance; both
+    partitions."""
     import pickle
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
-                                    args=(world, _free_port(), out, "pt1", False, True, mode),
+                                    args=(world, _free_port(), out, case, False, True, mode),
                                     nprocs=world)
         res = []
         for r in range(world):
             with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
                 res.append(pickle.load(fh))
-    _check(oracle, "pt1", res)
+    _check(oracle, case, res)
     assert sum(len(r[0]["samid"]) > 50 for r in res) >= max(2, world // 2)
-    for r in res:  # two all-reduces and one host read per frame, no exchange
+    for r in res:  # all-reduces and one host read per frame, no exchange
         assert r[3]["exchanges"] == 0 and r[3]["host_count_reads"] == 2
+    if case == "ao16":  # the whole film on rank 0
+        assert all(not r[2].any() for r in res[1:]) and res[0][2].any()
 
 
-def test_engine_replicated_frame_one_rank_rccl(oracle):
-    """World 1 through RCCL: trace_frame takes the all-local fused frame."""
-    res = _engine_rank(0, 1, "pt1", "rccl", replicated=True)
-    _check(oracle, "pt1", [res])
+@pytest.mark.parametrize("case", ["pt1", "ao16"])
+def test_engine_replicated_frame_one_rank_rccl(oracle, case):
+    """World 1 through RCCL: trace_frame takes the all-local frame."""
+    res = _engine_rank(0, 1, case, "rccl", replicated=True)
+    _check(oracle, case, [res])
 
 
 def test_engine_replicated_frame_unsupported_shading(oracle):
-    """AO (or several bounces) is not a replicated frame: UNSUPPORTED, and
-    nothing traced."""
+    """Several bounces are not a replicated frame: UNSUPPORTED, and nothing
+    traced."""
     import spray_amd
     with pytest.raises(spray_amd.SprayRtError, match="-6|replicated"):
-        _engine_rank(0, 1, "ao16", "rccl", replicated=True)
+        _engine_rank(0, 1, "pt3", "rccl", replicated=True)
 
 
 def test_domain_mask_exact_on_box_boundaries(spray, oracle):

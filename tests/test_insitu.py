@@ -217,11 +217,14 @@ def test_insitu_protocol_gloo(oracle, world, case, mode, replicated=False):
     np.testing.assert_allclose(total, ref_img, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("world,mode", [(1, 0), (2, 0), (3, 1), (8, 0), (8, 1)])
-def test_replicated_frame_gloo(oracle, world, mode):
-    """The replicated-ray frame (insitu.cpp trace_replicated, restated in
-    oracle/insitu_ref.py): every rank holds all eye rays, one MIN all-reduce
-    of the keys and one SUM all-reduce of the occlusion bytes -- the same
+@pytest.mark.parametrize("world,mode,case", [(1, 0, "pt1"), (2, 0, "pt1"), (3, 1, "pt1"),
+                                             (8, 0, "pt1"), (8, 1, "pt1"), (1, 0, "ao16"),
+                                             (3, 1, "ao16"), (8, 0, "ao16")])
+def test_replicated_frame_gloo(oracle, world, mode, case):
+    """The replicated-ray frame (insitu.cpp trace_replicated /
+    trace_replicated_ao, restated in oracle/insitu_ref.py): every rank holds
+    all eye rays, one MIN all-reduce of the keys and SUM all-reduces of the
+    occlusion bytes (AO: of the winners' normals and colours too) -- the same
     shaded samples, bits and totals as the whole-scene oracle, for the
     GROUP_CLOSE and ROUND_ROBIN partitions."""
-    test_insitu_protocol_gloo(oracle, world, "pt1", mode, replicated=True)
+    test_insitu_protocol_gloo(oracle, world, case, mode, replicated=True)
