@@ -195,11 +195,12 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     the replicated-ray AO frame: the same keys, the winners' normals and
     colours SUM-all-reduced, every rank any-hits every AO ray over its own
     domains, occlusion count fields SUM-all-reduced, rank 0 films the whole
-    frame (no composite).  protocol=True is the stripe protocol
+    frame.  Replicated frames leave the whole image on rank 0 (PT: per-pixel-
+    run sums reduced there).  protocol=True is the stripe protocol
     (spray_rt_insitu_trace): each rank its horizontal stripe of eye rays,
     count-first RCCL all-to-all-v exchanges of rays to their owners, key
-    composite, shading at the winner, shadow exchange.  The ranks' PT images
-    are composited by one RCCL reduce (HdrImage::composite).  Eye rays are made once before timing (resident,
+    composite, shading at the winner, shadow exchange; the ranks' images are
+    composited by one RCCL reduce (HdrImage::composite).  Eye rays are made once before timing (resident,
     like the main line).  RCCL is used at every N, N = 1 included (at N = 1
     PT runs the all-local fused frame unless protocol=True).  Timed like the
     main line (barrier + max over ranks); the per-phase device times come
@@ -238,8 +239,8 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
         os.environ["SPRAY_INSITU_LOCAL"] = "0"  # the whole protocol, even at one rank
     trace = eng.trace_frame if replicated else eng.trace
 
-    # the replicated AO frame films the whole image on rank 0: no composite
-    composite = not (replicated and kind == "ao" and world > 1)
+    # replicated frames leave the whole image on rank 0: no composite
+    composite = not replicated
 
     def frame():
         image.zero_()

@@ -643,9 +643,14 @@ int spray_rt_insitu_trace(spray_rt_insitu_t ins, const spray_rt_shader* shader,
  *      shades (ooc::ShaderPt point light);
  *   5. joins one SUM all-reduce of the occlusion bytes over C, the frame
  *      totals riding behind them (compositeObuf + WorkStats::reduce);
- *   6. films the unoccluded shadows of the rays it won.
- * No ray, hit or shadow record crosses the wire and no count is exchanged:
- * two all-reduces and one host read per frame.  Results per sample are the
+ *   6. films the unoccluded shadows of the rays it won into per-run sums
+ *      (a run = consecutive rays of C with one pixel: the spp samples of a
+ *      pixel), which one RCCL reduce (12 B per run instead of the 16-B-per-
+ *      pixel image) brings to rank 0, where they are added to image_rgba.
+ * The WHOLE frame lands in rank 0's image; the other ranks' images are not
+ * touched (no spray_rt_insitu_composite needed).  No ray, hit or shadow
+ * record crosses the wire and no count is exchanged: two all-reduces, one
+ * reduce and one host read per frame.  Results per sample are the
  * protocol's (the same winner, shading and occlusion).
  * AO (ooc::ShaderAo, one bounce, <= 32 samples, diffuse surfaces): after 3.
  * the winners publish their hits' shading normal and colour (one SUM

@@ -182,7 +182,8 @@ def trace_frame_replicated(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, im
     its own domains; MIN all-reduce of the keys over C; the point-light
     shadow ray of every hit from (org, dir, t) traced over its own domains;
     the winner shades (ooc::ShaderPt); SUM all-reduce of the occlusion bytes;
-    film of the rays it won.  PT, one bounce, one point light.  Returns
+    film of the rays it won, summed on rank 0 (the whole image there).  PT,
+    one bounce, one point light.  Returns
     (records, (group's radiance rays, shadow rays))."""
     import torch as t
     assert sh.bounces == 1
@@ -228,11 +229,15 @@ def trace_frame_replicated(po, local, comm, sh, bsdfs, org, d, pix, sam, spp, im
     occ_t = comm.all_reduce_sum(t.from_numpy(occ))
     comm.all_reduce_sum(tail)
     occ = occ_t.numpy() > 0
+    # film of the won rays into per-pixel sums, reduced to rank 0
     lit = np.flatnonzero(sv & ~occ)
+    acc = np.zeros((len(image) // 4, 3), np.float32)
     if len(lit):
-        img = image.reshape(-1, 4)
         add = ((1.0 / spp) * sw[lit].astype(np.float64)).astype(np.float32)
-        np.add.at(img[:, :3], pix[C[lit]], add)
+        np.add.at(acc, pix[C[lit]], add)
+    acc = comm.all_reduce_sum(t.from_numpy(acc)).numpy()
+    if comm.rank == 0:
+        image.reshape(-1, 4)[:, :3] += acc
     recs = [(0, int(sam[C[j]]), hits_c[j].tobytes(), int(sv[j]), int(sv[j] and occ[j]))
             for j in np.flatnonzero(win)]
     return recs, (int(tail[0]), int(tail[1]))

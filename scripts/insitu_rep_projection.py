@@ -15,7 +15,8 @@ Inputs
 
 Model of one frame at N ranks (every rank runs the same sequence):
   PT: T = max_r(lists + keyed closest hit) + AR(8 |C|) + max_r(shadows)
-          + AR(|C| + 192) + max_r(film) + max_r(totals read) + RED(16 MB)
+          + AR(|C| + 192) + max_r(film) + RED(12 runs) + max_r(totals read)
+          (runs = the pixel runs along C: the film's per-run sums go to rank 0)
   AO: T = max_r(lists + keyed closest hit) + AR(8 |C|) + AR(16 |C|)
           + max_r(AO rays: spawn + any hit) + AR(16 |C| fb / 8) + film(rank 0)
           + max_r(totals read)           (fb = 2 / 4 / 8 bits for N <= 3 / 15 / 64;
@@ -59,15 +60,17 @@ def project(run, link):
     b = max(ph(r, "shadows") for r in ranks)
     c = max(ph(r, "film") for r in ranks)
     d = max(ph(r, "totals") for r in ranks)
+    nc = ranks[0].get("nc")
     if run.get("kind", "pt") == "ao":
         # bytes_sent = 24 |C| + |C| * 16 * fb / 8 per trace (keys, normals, fields)
         fb = fbits(n)
-        nc = per / (24 + 2 * fb)
+        nc = nc if nc is not None else per / (24 + 2 * fb)
         comm = ar(8 * nc, n, link) + ar(16 * nc, n, link) + ar(2 * fb * nc, n, link)
     else:
-        # bytes_sent = the all-reduce payload 9 |C| + 192 per trace
-        nc = (per - 192) / 9
-        comm = ar(8 * nc, n, link) + ar(nc + 192, n, link) + red(IMAGE_BYTES, n, link)
+        runs = ranks[0].get("pixel_runs")
+        img = 12 * runs if runs is not None else IMAGE_BYTES
+        nc = nc if nc is not None else (per - 192) / 9
+        comm = ar(8 * nc, n, link) + ar(nc + 192, n, link) + red(img, n, link)
     return {"device_ms": round(a + b + c + d, 4), "comm_ms": round(comm, 4),
             "frame_ms": round(a + b + c + d + comm, 4),
             "busiest": {"lists+keyed": round(a, 4), "shadows": round(b, 4), "film": round(c, 4),

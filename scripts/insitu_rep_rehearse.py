@@ -86,7 +86,15 @@ def _rank(rank, world, port, mode, frames, out, kind="pt"):
         tot = trace(sh, rays, pix, sam, SPP, image)
     s1 = eng.stats()
     ph = {k: v / frames for k, v in eng.phase_times().items()}
+    # |C| (rays with a non-empty domain list) and the pixel runs along C:
+    # the sizes of the frame's collectives
+    m = torch.empty(n, dtype=torch.int64, device="cuda")
+    rt.route(rays, m)
+    on = m != 0
+    pc = pix[on]
+    nc, nruns = int(on.sum()), int(1 + (pc[1:] != pc[:-1]).sum()) if pc.numel() else 0
     res = {"rank": rank, "domains": int((owner == rank).sum()), "phases_ms": ph,
+           "nc": nc, "pixel_runs": nruns,
            "totals": list(tot), "stats": eng.stats(),
            "per_frame": {k: (s1[k] - s0[k]) / frames for k in s1}}
     with open(os.path.join(out, "r%d.json" % rank), "w") as fh:

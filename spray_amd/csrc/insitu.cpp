@@ -158,6 +158,9 @@ struct spray_rt_insitu {
   DBuf rsray, rsflag, rwin, rsvalid, rsw, rocc, rpix, rsam, rhit_c, rnsh;
   // replicated-ray AO frames (trace_replicated_ao)
   DBuf apub, arays, ahits, apairs, aocc_p, alv, arec, ascratch, afields, acount;
+  // compact film of replicated PT frames (runs of equal pixels along C)
+  DBuf rheads, rincl, rscan_tmp, rslot_c, rslot_pix, rcompact, rnp;
+  hipEvent_t ev_np = nullptr;  // the run count's copy to the host
   // phase timing (spray_rt_insitu_set_timing): events on the stream
   bool timing = false;
   static constexpr int kMaxEv = 48;
@@ -799,11 +802,12 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   return SPRAY_RT_OK;
 }
 
-// Steps 1-3 of a replicated-ray frame: owner-rank masks of every eye ray, C
+// Steps 1-2 of a replicated-ray frame: owner-rank masks of every eye ray, C
 // and L (one host read: |C|, which sizes the all-reduces -- the same on
 // every rank -- and, for AO, the largest pixel id of C), the own closest
-// hits (keyed) of L, their keys over C and the MIN all-reduce: keys_c[j] is
-// then the winning key of ray idx_c[j] on every rank.
+// hits (keyed) of L and their keys over C.  The caller's MIN all-reduce of
+// keys_c (step 3) makes keys_c[j] the winning key of ray idx_c[j] on every
+// rank.
 int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* pixid, size_t n,
                    bool want_pixmax, size_t* nc_out, uint32_t* pixmax_out) {
   spray_rt_ctx* c = I->ctx;
@@ -846,7 +850,6 @@ int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* 
                                                    I->rkeys_n.as<uint64_t>()));
   HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
                             I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
-  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   return SPRAY_RT_OK;
 }
 
@@ -865,11 +868,31 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                              lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                              P->ks[2],       P->shininess};
   std::memcpy(A.shade10, shade10, sizeof(shade10));
-  // ---- 1-3. lists, own keyed closest hits, the winning keys
+  // ---- 1-2. lists, own keyed closest hits
   size_t nc = 0;
   CALL(rep_lists_keys(I, rays, pixid, n, false, &nc, nullptr));
-  I->st[0] += 9 * nc + 192;  // the two all-reduces' payload (stats: bytes sent / received)
-  I->st[1] += 9 * nc + 192;
+  // the compact film's slots (runs of equal pixels along C), their count on
+  // its way to the host while the frame runs on
+  GROW(I->rheads, nc * 4 + 4);
+  GROW(I->rincl, nc * 4 + 4);
+  GROW(I->rslot_c, nc * 4 + 4);
+  GROW(I->rslot_pix, nc * 4 + 4);
+  GROW(I->rcompact, nc * 12 + 12);
+  GROW(I->rnp, 8);
+  size_t tsc = 0;
+  HIPCHK(c, launch_rep_slots(s, nullptr, nullptr, nc, nullptr, nullptr, nullptr, &tsc, nullptr,
+                             nullptr, nullptr));
+  GROW(I->rscan_tmp, tsc);
+  if (!I->ev_np) HIPCHK(c, hipEventCreateWithFlags(&I->ev_np, hipEventDisableTiming));
+  HIPCHK(c, launch_rep_slots(s, I->ridx_c.as<uint32_t>(), pixid, nc, I->rheads.as<uint32_t>(),
+                             I->rincl.as<uint32_t>(), I->rscan_tmp.p, &tsc,
+                             I->rslot_c.as<int32_t>(), I->rslot_pix.as<int32_t>(),
+                             I->rnp.as<uint32_t>()));
+  uint32_t* h_np = reinterpret_cast<uint32_t*>(I->h_small + 250);
+  HIPCHK(c, hipMemcpyAsync(h_np, I->rnp.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipEventRecord(I->ev_np, s));
+  // ---- 3. the winning key of every ray of C, on every rank
+  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   // ---- 4. shadow rays of every hit, own any hit; the winners shade
   MARK(2);
   GROW(I->rsray, nc * 32 + 32);
@@ -913,10 +936,24 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                               I->rnsh.as<unsigned long long>()));
   // ---- 5. occlusion OR (a byte SUM) + totals
   COMM(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nc + 192));
-  // ---- 6. film of the rays this rank won
+  // ---- 6. film of the rays this rank won into the runs' sums, reduced to
+  // rank 0 (12 B per run of C instead of the 16-B-per-pixel image)
   MARK(3);
-  HIPCHK(c, launch_film_atomic(s, image, I->rpix.as<int32_t>(), nc, 1, I->rsw.as<float>(),
-                               I->rsvalid.as<uint8_t>(), I->rocc.as<uint8_t>(), scale));
+  HIPCHK(c, hipEventSynchronize(I->ev_np));  // long done: the scan ran before the keyed launch
+  const size_t np = nc ? *h_np : 0;
+  I->st[0] += 9 * nc + 192 + 12 * np;  // the all-reduces' and the reduce's payload
+  I->st[1] += 9 * nc + 192 + 12 * np;
+  if (np) {
+    HIPCHK(c, hipMemsetAsync(I->rcompact.p, 0, np * 12, s));
+    HIPCHK(c, launch_film_atomic(s, I->rcompact.as<float>(), I->rslot_c.as<int32_t>(), nc, 1,
+                                 I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
+                                 I->rocc.as<uint8_t>(), scale, 3));
+    COMM(I->tr->reduce_f32(I, I->rcompact.as<float>(), np * 3, 0));
+    MARK(3);
+    if (I->rank == 0)
+      HIPCHK(c, launch_rep_expand(s, image, I->rslot_pix.as<int32_t>(), I->rcompact.as<float>(),
+                                  np));
+  }
   if (rec)
     HIPCHK(c, launch_record(s, I->rwin.as<uint8_t>(), nc, 0, 1, I->rsam.as<int32_t>(),
                             I->rhit_c.as<spray_rt_hit>(), I->rsvalid.as<uint8_t>(),
@@ -958,6 +995,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   uint32_t pixmax = 0;
   CALL(rep_lists_keys(I, rays, pixid, n, true, &nc, &pixmax));
   if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C| >= 2^27");
+  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   MARK(2);
   const int fb = I->world <= 3 ? 2 : (I->world <= 15 ? 4 : 8);
   const size_t npair = nc * size_t(ns);
@@ -1054,11 +1092,13 @@ void free_all(spray_rt_insitu* I) {
                  &I->rkeys_c, &I->rsray, &I->rsflag, &I->rwin, &I->rsvalid, &I->rsw, &I->rocc,
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
-                 &I->afields, &I->acount};
+                 &I->afields, &I->acount, &I->rheads, &I->rincl, &I->rscan_tmp,
+                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
     if (e) (void)hipEventDestroy(e);
+  if (I->ev_np) (void)hipEventDestroy(I->ev_np);
   if (I->h_small) (void)hipHostFree(I->h_small);
 }
 

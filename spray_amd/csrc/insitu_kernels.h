@@ -46,9 +46,10 @@ hipError_t launch_winners(hipStream_t s, const uint64_t* key, const uint64_t* be
 // occ[sel[idx[j]]] = 1 where ret[j]
 hipError_t launch_occ_return(hipStream_t s, const int64_t* idx, const uint8_t* ret, size_t n,
                              const uint32_t* sel, uint8_t* occ);
+// image + stride * pix[i] (+0, +1, +2) += the unoccluded weights of copy i
 hipError_t launch_film_atomic(hipStream_t s, float* image, const int32_t* pix, size_t m, int ns,
                               const float* sw, const uint8_t* sv, const uint8_t* occ,
-                              double scale);
+                              double scale, int stride = 4);
 hipError_t launch_record(hipStream_t s, const uint8_t* win, size_t m, int bounce, int ns,
                          const int32_t* sam, const spray_rt_hit* hits, const uint8_t* sv,
                          const uint8_t* occ, const spray_rt_insitu_rec& rec);
@@ -93,6 +94,15 @@ struct RepSpawnArgs {
   unsigned long long* nshadow;  // += spawned shadow rays
 };
 hipError_t launch_rep_spawn(hipStream_t s, const RepSpawnArgs& a);
+// The compact film's slots: the runs of equal pixels along C.  slot_c[j] =
+// run of ray j, slot_pix[run] = its pixel, *d_np = runs; heads / incl: [nc]
+// u32 scratch; temp == nullptr: *temp_bytes <- the scan's scratch size.
+hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
+                            uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,
+                            int32_t* slot_c, int32_t* slot_pix, uint32_t* d_np);
+// image[4 slot_pix[q] + k] += compact[3 q + k], q < np
+hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
+                             const float* compact, size_t np);
 // tail[64 c + k] = bit k of {nrad, *nshadow, 0}[c] (192 bytes)
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow);

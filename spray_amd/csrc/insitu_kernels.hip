@@ -7,6 +7,9 @@
 // the next bounce's compaction.  All are HBM-bound streaming passes: one
 // thread per record, 16-B (or 8-B) accesses.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
 
 #include "insitu_kernels.h"
 #include "rt_device.h"
@@ -167,7 +170,8 @@ __global__ __launch_bounds__(kBlock) void k_occ_return(const int64_t* __restrict
 // segmented scan over the wave's runs of equal pixels leaves one hardware
 // fp32 atomic per run and channel at the run's last lane.
 __device__ __forceinline__ void film_runs(float* __restrict__ image, bool in, int32_t p,
-                                          bool any, float a0, float a1, float a2) {
+                                          bool any, float a0, float a1, float a2,
+                                          int stride = 4) {
   const int lane = threadIdx.x & 63;
   if (__ballot(any) == 0ull) return;
   // runs of equal pixels: heads, and each lane's run start
@@ -190,7 +194,7 @@ __device__ __forceinline__ void film_runs(float* __restrict__ image, bool in, in
   }
   const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
   if (in && tail && cnt) {
-    float* px = image + 4 * size_t(p);
+    float* px = image + size_t(stride) * size_t(p);
     unsafeAtomicAdd(px, a0);
     unsafeAtomicAdd(px + 1, a1);
     unsafeAtomicAdd(px + 2, a2);
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ imag
                                                         const float4* __restrict__ sw,
                                                         const uint8_t* __restrict__ sv,
                                                         const uint8_t* __restrict__ occ,
-                                                        double scale) {
+                                                        double scale, int stride) {
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   const bool in = i < m;
   const int32_t p = in ? pix[i] : -1;
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ imag
       a2 += float(scale * double(L.z));
       any = true;
     }
-  film_runs(image, in, p, any, a0, a1, a2);
+  film_runs(image, in, p, any, a0, a1, a2, stride);
 }
 
 __global__ __launch_bounds__(kBlock) void k_record(const uint8_t* __restrict__ win, size_t m,
@@ -524,6 +528,50 @@ __global__ __launch_bounds__(kBlock) void k_rep_ao_record(RepAoArgs A, spray_rt_
   rec.svalid[k] = v;
   rec.occluded[k] = o;
 }
+
+// ---- the compact film of a replicated PT frame -------------------------
+// Slots = the runs of equal pixels along C (the spp samples of a pixel are
+// neighbours): heads[j] = ray j of C starts a run.
+__global__ __launch_bounds__(kBlock) void k_rep_heads(const uint32_t* __restrict__ idx_c,
+                                                      const int32_t* __restrict__ pix, size_t nc,
+                                                      uint32_t* __restrict__ heads) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= nc) return;
+  heads[j] = (j == 0 || pix[idx_c[j]] != pix[idx_c[j - 1]]) ? 1u : 0u;
+}
+
+// slot_c[j] = run of ray j (inclusive count - 1), slot_pix[run] = its pixel,
+// *d_np = the number of runs
+__global__ __launch_bounds__(kBlock) void k_rep_slot_pix(const uint32_t* __restrict__ idx_c,
+                                                         const int32_t* __restrict__ pix,
+                                                         const uint32_t* __restrict__ incl,
+                                                         size_t nc, int32_t* __restrict__ slot_c,
+                                                         int32_t* __restrict__ slot_pix,
+                                                         uint32_t* __restrict__ d_np) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= nc) return;
+  const uint32_t q = incl[j] - 1u;
+  slot_c[j] = int32_t(q);
+  const int32_t p = pix[idx_c[j]];
+  if (j == 0 || p != pix[idx_c[j - 1]]) slot_pix[q] = p;
+  if (j == nc - 1) *d_np = q + 1u;
+}
+
+// rank 0: the group's sums of the runs into the image (a pixel on several
+// runs gets each run's sum)
+__global__ __launch_bounds__(kBlock) void k_rep_expand(float* __restrict__ image,
+                                                       const int32_t* __restrict__ slot_pix,
+                                                       const float* __restrict__ compact,
+                                                       size_t np) {
+  const size_t q = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (q >= np) return;
+  float* px = image + 4 * size_t(slot_pix[q]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float v = compact[3 * q + k];
+    if (v != 0.0f) unsafeAtomicAdd(px + k, v);
+  }
+}
 }  // namespace
 
 #define LAUNCH(n, kern, ...)                                  \
@@ -589,10 +637,10 @@ hipError_t launch_occ_return(hipStream_t s, const int64_t* idx, const uint8_t* r
 }
 hipError_t launch_film_atomic(hipStream_t s, float* image, const int32_t* pix, size_t m, int ns,
                               const float* sw, const uint8_t* sv, const uint8_t* occ,
-                              double scale) {
+                              double scale, int stride) {
   if (ns == 0) return hipSuccess;
   LAUNCH(m, k_film_atomic, image, pix, m, ns, reinterpret_cast<const float4*>(sw), sv, occ,
-         scale);
+         scale, stride);
 }
 hipError_t launch_record(hipStream_t s, const uint8_t* win, size_t m, int bounce, int ns,
                          const int32_t* sam, const spray_rt_hit* hits, const uint8_t* sv,
@@ -631,6 +679,27 @@ hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nr
   return hipGetLastError();
 }
 
+hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
+                            uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,
+                            int32_t* slot_c, int32_t* slot_pix, uint32_t* d_np) {
+  if (!temp) {
+    size_t b = 0;
+    const hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, b, heads, incl,
+                                                          int(std::max<size_t>(nc, 1)), s);
+    *temp_bytes = b;
+    return e;
+  }
+  if (nc == 0) return hipMemsetAsync(d_np, 0, 4, s);
+  k_rep_heads<<<grid_for(nc), kBlock, 0, s>>>(idx_c, pix, nc, heads);
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, heads, incl, int(nc), s);
+  if (e != hipSuccess) return e;
+  k_rep_slot_pix<<<grid_for(nc), kBlock, 0, s>>>(idx_c, pix, incl, nc, slot_c, slot_pix, d_np);
+  return hipGetLastError();
+}
+hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
+                             const float* compact, size_t np) {
+  LAUNCH(np, k_rep_expand, image, slot_pix, compact, np);
+}
 hipError_t launch_rep_ao_publish(hipStream_t s, const RepAoArgs& a) {
   LAUNCH(a.nc, k_rep_ao_publish, a);
 }

@@ -272,9 +272,10 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case):
     """spray_rt_insitu_trace_frame with world processes sharing the GPU over
     the host transport: every eye ray on every rank, the keys' MIN and the
     occlusion bytes' SUM all-reduced (the host transport's
-    allreduce_min_u64 / allreduce_sum_u8; AO: the winners' normals and
-    colours SUM-all-reduced, occlusion as 2- / 4-bit count fields, the film
-    on rank 0) -- every shaded sample bit-exact against the whole-scene
+    allreduce_min_u64 / allreduce_sum_u8; PT: the film's per-run sums
+    reduced to rank 0; AO: the winners' normals and colours SUM-all-reduced,
+    occlusion as 2- / 4-bit count fields, the film on rank 0) -- every
+    shaded sample bit-exact against the whole-scene
     oracle, totals exact, the image within summation-order tolerance; both
     partitions."""
     import pickle
@@ -290,8 +291,8 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case):
     assert sum(len(r[0]["samid"]) > 50 for r in res) >= max(2, world // 2)
     for r in res:  # all-reduces and one host read per frame, no exchange
         assert r[3]["exchanges"] == 0 and r[3]["host_count_reads"] == 2
-    if case == "ao16":  # the whole film on rank 0
-        assert all(not r[2].any() for r in res[1:]) and res[0][2].any()
+    # the whole film on rank 0, the other ranks' images untouched
+    assert all(not r[2].any() for r in res[1:]) and res[0][2].any()
 
 
 @pytest.mark.parametrize("case", ["pt1", "ao16"])
