@@ -2197,8 +2197,11 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t 
   // the local hemisphere samples of the group's pixels, lv[pixel * ns + l]:
   // the group's lanes share its leader pixel's (samples l = me, me + 8, ...,
   // the union of that pixel's masks in the group); the first lane of any
-  // other pixel's run in the group draws that run's samples alone.  A pixel
-  // spread over groups is written by each, with the same values.
+  // other pixel's run in the group draws the samples of its own and every
+  // later lane of that pixel -- whether or not its own ray spawns (a run's
+  // first sample may miss while the next hits: runs need not align with
+  // the groups, e.g. a compacted subset of a frame's rays).  A pixel spread
+  // over groups is written by each, with the same values.
   {
     const int32_t px = in ? pixid[i] : -1;
     int32_t gpx[kAoGroup];  // every lane takes part in the shuffles
@@ -2221,7 +2224,7 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_index(uint32_t M, uint32_t 
         hemisphere_local(u1, u2, v);
         lv[size_t(lead) * ns + l] = make_float4(v[0], v[1], v[2], 0.f);
       }
-    if (in && m.x && px != lead && prev != px)
+    if (in && px != lead && prev != px)
       for (uint32_t l = 0; l < ns; ++l)
         if ((ror >> l) & 1u) {
           uint32_t st = sampler_init1(px * int32_t(l + 1));

@@ -189,3 +189,61 @@ def test_ao16_fused_full_frame():
     assert np.array_equal(fo, ref_occ) and 0 < fo.sum() < m
     rt.set_coherence(rt.RAYS_ADAPTIVE)
     scene.close()
+
+
+def test_ao_pairs_misaligned_pixel_runs(oracle):
+    """The fused pairs form over a subset of a frame's rays whose pixel runs
+    do not align with the 8-lane groups (the replicated AO frame's C: rays
+    dropped, a pixel's first ray a miss while its next one hits): the
+    (pixel, sample) table must hold every sample any pair reads (filled with
+    NaN beforehand), so pairs and occlusion equal the written-ray path's."""
+    import spray_amd
+    c = BENCH_CAMERA
+    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 1024, 1024)
+    org, d, pix, _ = oracle.eye_rays_ooc(cam, 1024, 2, (384, 448, 128, 32))
+    rng = np.random.default_rng(3)
+    keep = np.flatnonzero(rng.random(len(org)) > 0.3)[1:]
+    org, d, pix = org[keep], d[keep], pix[keep]
+    scene = spray_amd.Scene(WAVELETS64, SCENES)
+    rt = scene.rt
+    n, ns = len(org), 16
+    rays = torch.zeros((n, 8), dtype=torch.float32)
+    rays[:, 0:3] = torch.from_numpy(np.ascontiguousarray(org))
+    rays[:, 3] = 0.001
+    rays[:, 4:7] = torch.from_numpy(np.ascontiguousarray(d))
+    rays[:, 7] = float("inf")
+    rays = rays.cuda()
+    h = torch.empty((n, 12), dtype=torch.float32, device="cuda")
+    rt.intersect_scene(rays, h)
+    pixid = torch.from_numpy(np.ascontiguousarray(pix)).cuda()
+    hit = h.cpu().numpy().view(oracle.HIT_DTYPE).reshape(-1)["domain"] >= 0
+    # pixels whose first kept ray misses and whose next one hits
+    first = np.r_[True, pix[1:] != pix[:-1]]
+    assert ((~hit[:-1]) & first[:-1] & hit[1:] & (pix[1:] == pix[:-1])).sum() > 5
+    out = torch.empty((n * ns, 8), dtype=torch.float32, device="cuda")
+    osrc = torch.empty(n * ns, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rt.spawn_shadows_ao(rays, h, pixid, n, ns, out, osrc, cnt, traced=True)
+    rt.sync()
+    m = int(cnt.item())
+    rt.set_coherence(rt.RAYS_INCOHERENT)
+    occ = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+    rt.occluded_scene_order(out, m, None, cnt, occ)
+    rt.sync()
+    fpair = torch.full((n * ns,), -1, dtype=torch.int32, device="cuda")
+    fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    focc = torch.full((n * ns,), 9, dtype=torch.uint8, device="cuda")
+    lv = torch.full((1024 * 1024 * ns, 4), float("nan"), dtype=torch.float32, device="cuda")
+    rec = torch.empty((n, 16), dtype=torch.float32, device="cuda")
+    rt.occluded_ao(rays, h, pixid, n, ns, fpair, lv, rec, fcnt, focc)
+    rt.sync()
+    assert int(fcnt.item()) == m
+    fp = fpair[:m].cpu().numpy().view(np.uint32)
+    assert ((fp >> 5).astype(np.int32) == osrc[:m].cpu().numpy()).all()
+    # every table entry a pair reads was written
+    lvh = lv.cpu().numpy().reshape(-1, 4)
+    used = pix[(fp >> 5).astype(np.int64)].astype(np.int64) * ns + (fp & 31)
+    assert np.isfinite(lvh[used, :3]).all()
+    assert (focc[:m].cpu().numpy() == occ.cpu().numpy()).all()
+    rt.set_coherence(rt.RAYS_ADAPTIVE)
+    scene.close()

@@ -219,7 +219,7 @@ def test_insitu_protocol_gloo(oracle, world, case, mode, replicated=False):
 
 @pytest.mark.parametrize("world,mode,case", [(1, 0, "pt1"), (2, 0, "pt1"), (3, 1, "pt1"),
                                              (8, 0, "pt1"), (8, 1, "pt1"), (1, 0, "ao16"),
-                                             (3, 1, "ao16"), (8, 0, "ao16")])
+                                             (2, 0, "ao16"), (3, 1, "ao16"), (8, 0, "ao16")])
 def test_replicated_frame_gloo(oracle, world, mode, case):
     """The replicated-ray frame (insitu.cpp trace_replicated /
     trace_replicated_ao, restated in oracle/insitu_ref.py): every rank holds
