@@ -124,6 +124,10 @@ struct InsituTransport {
   virtual bool has_rep() const { return true; }
   virtual int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) = 0;
   virtual int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) = 0;
+  // split keys: MIN of u32 t bits; MIN of u8 list positions on stream st
+  // (overlapping the main stream's work; the host form runs it in order)
+  virtual int allreduce_min_u32(spray_rt_insitu* I, uint32_t* dev, size_t n) = 0;
+  virtual int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t st) = 0;
   // rehearsal only: the rank's device work runs while it holds a lock
   // shared by the group's processes (SPRAY_INSITU_SERIAL), so the phase
   // timings of ranks sharing one GPU are not inflated by each other
@@ -161,6 +165,11 @@ struct spray_rt_insitu {
   // compact film of replicated PT frames (runs of equal pixels along C)
   DBuf rheads, rincl, rscan_tmp, rslot_c, rslot_pix, rcompact, rnp;
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
+  // split keys: t bits and list positions over C; the list positions'
+  // all-reduce runs on a second stream (cs) beside the shadow any hit
+  DBuf rtk, rlp;
+  hipStream_t cs = nullptr;
+  hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
   // phase timing (spray_rt_insitu_set_timing): events on the stream
   bool timing = false;
   static constexpr int kMaxEv = 48;
@@ -265,6 +274,16 @@ struct RcclTransport : InsituTransport {
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclSum, comm, stream_of(I->ctx)),
                "ncclAllReduce(sum u8)");
   }
+  int allreduce_min_u32(spray_rt_insitu* I, uint32_t* dev, size_t n) override {
+    ++I->st[4];
+    return chk(I, nccl().AllReduce(dev, dev, n, ncclUint32, ncclMin, comm, stream_of(I->ctx)),
+               "ncclAllReduce(min u32)");
+  }
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t st) override {
+    ++I->st[4];
+    return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclMin, comm, st),
+               "ncclAllReduce(min u8)");
+  }
   bool self_direct() const override { return !self_via_nccl; }
   ~RcclTransport() override {
     if (comm) nccl().CommDestroy(comm);
@@ -318,6 +337,32 @@ struct HostTransport : InsituTransport {
     CALL(sync(I));
     ++I->st[4];
     return SPRAY_RT_OK;
+  }
+  // the narrow MINs through the 64-bit host callback (widened on the host)
+  template <typename T>
+  int min_widened(spray_rt_insitu* I, T* dev, size_t n) {
+    std::vector<T> h(std::max<size_t>(n, 1));
+    std::vector<unsigned long long> w(std::max<size_t>(n, 1));
+    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost,
+                                  stream_of(I->ctx)));
+    CALL(sync(I));
+    for (size_t k = 0; k < n; ++k) w[k] = h[k];
+    serial_end();
+    const int bad = cb.allreduce_min_u64(cb.user, w.data(), n);
+    serial_begin();
+    if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: min all-reduce failed");
+    for (size_t k = 0; k < n; ++k) h[k] = T(w[k]);
+    HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * sizeof(T), hipMemcpyHostToDevice,
+                                  stream_of(I->ctx)));
+    CALL(sync(I));
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int allreduce_min_u32(spray_rt_insitu* I, uint32_t* dev, size_t n) override {
+    return min_widened(I, dev, n);
+  }
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t) override {
+    return min_widened(I, dev, n);
   }
   int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
              int64_t* h_recv) override {
@@ -802,6 +847,15 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   return SPRAY_RT_OK;
 }
 
+// SPRAY_INSITU_SPLIT_KEYS=0: the replicated PT frame's 64-bit key MIN
+bool split_keys() {
+  static const bool on = [] {
+    const char* e = std::getenv("SPRAY_INSITU_SPLIT_KEYS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Steps 1-2 of a replicated-ray frame: owner-rank masks of every eye ray, C
 // and L (one host read: |C|, which sizes the all-reduces -- the same on
 // every rank -- and, for AO, the largest pixel id of C), the own closest
@@ -809,7 +863,8 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
 // keys_c (step 3) makes keys_c[j] the winning key of ray idx_c[j] on every
 // rank.
 int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* pixid, size_t n,
-                   bool want_pixmax, size_t* nc_out, uint32_t* pixmax_out) {
+                   bool want_pixmax, size_t* nc_out, uint32_t* pixmax_out,
+                   bool want_keys_c = true) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
   MARK(0);
@@ -848,8 +903,9 @@ int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* 
     HIPCHK(c, launch_scene_intersect_keyed_indexed(s, view(c), rays, n, I->ridx_l.as<uint32_t>(),
                                                    dnum + 1, I->rhits_n.as<spray_rt_hit>(),
                                                    I->rkeys_n.as<uint64_t>()));
-  HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
-                            I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
+  if (want_keys_c)
+    HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
+                              I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
   return SPRAY_RT_OK;
 }
 
@@ -870,7 +926,8 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   std::memcpy(A.shade10, shade10, sizeof(shade10));
   // ---- 1-2. lists, own keyed closest hits
   size_t nc = 0;
-  CALL(rep_lists_keys(I, rays, pixid, n, false, &nc, nullptr));
+  const bool split = split_keys() && c->ndom <= 255;
+  CALL(rep_lists_keys(I, rays, pixid, n, false, &nc, nullptr, !split));
   // the compact film's slots (runs of equal pixels along C), their count on
   // its way to the host while the frame runs on
   GROW(I->rheads, nc * 4 + 4);
@@ -891,8 +948,33 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   uint32_t* h_np = reinterpret_cast<uint32_t*>(I->h_small + 250);
   HIPCHK(c, hipMemcpyAsync(h_np, I->rnp.p, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipEventRecord(I->ev_np, s));
-  // ---- 3. the winning key of every ray of C, on every rank
-  if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
+  // ---- 3. the winning key of every ray of C, on every rank: split (t bits,
+  // then the list positions at that t, the latter beside the shadow rays'
+  // any hit) while list positions fit a byte, else the 64-bit keys
+  uint32_t* tk = nullptr;
+  uint8_t* lp = nullptr;
+  if (split) {
+    GROW(I->rtk, nc * 4 + 4);
+    GROW(I->rlp, nc + 1);
+    tk = I->rtk.as<uint32_t>();
+    lp = I->rlp.as<uint8_t>();
+    HIPCHK(c, launch_rep_tkeys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
+                               I->rkeys_n.as<uint64_t>(), tk));
+    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
+    HIPCHK(c, launch_rep_lpos(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
+                              I->rkeys_n.as<uint64_t>(), tk, lp));
+    if (nc) {
+      if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
+      if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
+      if (!I->ev_lp1) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp1, hipEventDisableTiming));
+      HIPCHK(c, hipEventRecord(I->ev_lp0, s));
+      HIPCHK(c, hipStreamWaitEvent(I->cs, I->ev_lp0, 0));
+      CALL(I->tr->allreduce_min_u8(I, lp, nc, I->cs));
+      HIPCHK(c, hipEventRecord(I->ev_lp1, I->cs));
+    }
+  } else if (nc) {
+    COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
+  }
   // ---- 4. shadow rays of every hit, own any hit; the winners shade
   MARK(2);
   GROW(I->rsray, nc * 32 + 32);
@@ -926,10 +1008,19 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   A.sam_c = I->rsam.as<int32_t>();
   A.hit_c = rec ? I->rhit_c.as<spray_rt_hit>() : nullptr;
   A.nshadow = I->rnsh.as<unsigned long long>();
-  HIPCHK(c, launch_rep_spawn(s, A));
-  if (nc)
-    HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
-                                           I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
+  if (split) {
+    HIPCHK(c, launch_rep_shadows(s, A, tk));
+    if (nc)
+      HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
+                                             I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
+    if (nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
+    HIPCHK(c, launch_rep_shade(s, A, tk, lp));
+  } else {
+    HIPCHK(c, launch_rep_spawn(s, A));
+    if (nc)
+      HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
+                                             I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
+  }
   // the frame totals behind the occlusion bytes: rank 0 counts the frame's
   // radiance rays, every rank the shadow rays it spawned
   HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nc, I->rank == 0 ? n : 0,
@@ -941,8 +1032,10 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   MARK(3);
   HIPCHK(c, hipEventSynchronize(I->ev_np));  // long done: the scan ran before the keyed launch
   const size_t np = nc ? *h_np : 0;
-  I->st[0] += 9 * nc + 192 + 12 * np;  // the all-reduces' and the reduce's payload
-  I->st[1] += 9 * nc + 192 + 12 * np;
+  // the all-reduces' and the reduce's payload
+  const size_t pay = (split ? 6 * nc : 9 * nc) + 192 + 12 * np;
+  I->st[0] += pay;
+  I->st[1] += pay;
   if (np) {
     HIPCHK(c, hipMemsetAsync(I->rcompact.p, 0, np * 12, s));
     HIPCHK(c, launch_film_atomic(s, I->rcompact.as<float>(), I->rslot_c.as<int32_t>(), nc, 1,
@@ -1093,12 +1186,15 @@ void free_all(spray_rt_insitu* I) {
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rheads, &I->rincl, &I->rscan_tmp,
-                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp};
+                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
     if (e) (void)hipEventDestroy(e);
   if (I->ev_np) (void)hipEventDestroy(I->ev_np);
+  if (I->ev_lp0) (void)hipEventDestroy(I->ev_lp0);
+  if (I->ev_lp1) (void)hipEventDestroy(I->ev_lp1);
+  if (I->cs) (void)hipStreamDestroy(I->cs);
   if (I->h_small) (void)hipHostFree(I->h_small);
 }
 

@@ -103,6 +103,16 @@ hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t*
 // image[4 slot_pix[q] + k] += compact[3 q + k], q < np
 hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
                              const float* compact, size_t np);
+// split keys: tk[j] = this rank's t bits of ray idx_c[j] (0xFFFFFFFF: none);
+// after their MIN, lp[j] = its list position where its t is the minimum
+// (0xFF elsewhere); the shadow rays from the minimum t; the winner's shading
+hipError_t launch_rep_tkeys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
+                            int rank, const uint64_t* keys_n, uint32_t* tk);
+hipError_t launch_rep_lpos(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
+                           int rank, const uint64_t* keys_n, const uint32_t* tmin, uint8_t* lp);
+hipError_t launch_rep_shadows(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin);
+hipError_t launch_rep_shade(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin,
+                            const uint8_t* lpmin);
 // tail[64 c + k] = bit k of {nrad, *nshadow, 0}[c] (192 bytes)
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow);

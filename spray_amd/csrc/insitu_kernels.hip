@@ -572,6 +572,101 @@ __global__ __launch_bounds__(kBlock) void k_rep_expand(float* __restrict__ image
     if (v != 0.0f) unsafeAtomicAdd(px + k, v);
   }
 }
+
+// ---- split keys of a replicated PT frame (insitu.cpp, trace_replicated) ---
+// The winner of ray j is the smallest (t, list position): a MIN all-reduce
+// of the t bits (u32: positive floats order as their bits), then one of the
+// list positions of the ranks at that t (u8) -- the shadow rays need only
+// t, so the second all-reduce overlaps their any hit.
+__global__ __launch_bounds__(kBlock) void k_rep_tkeys(const uint32_t* __restrict__ idx_c, size_t nc,
+                                                      const uint64_t* __restrict__ mask, int rank,
+                                                      const uint64_t* __restrict__ keys_n,
+                                                      uint32_t* __restrict__ tk) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= nc) return;
+  const uint32_t i = idx_c[j];
+  const uint64_t key = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
+  tk[j] = key != kInsituMissKey ? uint32_t(key >> 32) : 0xFFFFFFFFu;
+}
+
+// lp[j] = this rank's list position of ray j where its t is the minimum,
+// 0xFF elsewhere (list positions < 255: the caller checks the domain count)
+__global__ __launch_bounds__(kBlock) void k_rep_lpos(const uint32_t* __restrict__ idx_c, size_t nc,
+                                                     const uint64_t* __restrict__ mask, int rank,
+                                                     const uint64_t* __restrict__ keys_n,
+                                                     const uint32_t* __restrict__ tmin,
+                                                     uint8_t* __restrict__ lp) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= nc) return;
+  const uint32_t i = idx_c[j];
+  const uint64_t key = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
+  const bool cand = key != kInsituMissKey && uint32_t(key >> 32) == tmin[j];
+  lp[j] = cand ? uint8_t((key >> 16) & 0xFFu) : uint8_t(0xFF);
+}
+
+// Every hit's point-light shadow ray from (org, dir, t) -- the operations
+// of shade_pt_point, so the winner's bits -- marked for this rank's any hit.
+__global__ __launch_bounds__(kBlock) void k_rep_shadows(RepSpawnArgs A, const uint32_t* tmin) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= A.nc) return;
+  const uint32_t i = A.idx_c[j];
+  const uint32_t tb = tmin[j];
+  const bool hit = tb != 0xFFFFFFFFu;
+  const float4 o4 = A.rays[2 * size_t(i)], d4 = A.rays[2 * size_t(i) + 1];
+  float pos[3] = {0.f, 0.f, 0.f}, wi[3] = {0.f, 0.f, 1.f};
+  if (hit) {
+    const float t = __uint_as_float(tb);
+    pos[0] = d4.x * t + o4.x;
+    pos[1] = d4.y * t + o4.y;
+    pos[2] = d4.z * t + o4.z;
+    wi[0] = A.shade10[0] - pos[0];
+    wi[1] = A.shade10[1] - pos[1];
+    wi[2] = A.shade10[2] - pos[2];
+    gnorm3(wi);
+  }
+  A.sray[2 * j] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
+  A.sray[2 * j + 1] = make_float4(wi[0], wi[1], wi[2], kInf);
+  A.sflag[j] = hit;
+  A.occ[j] = 0;
+}
+
+// After the list-position all-reduce: the winner (its t and list position
+// are the minima) shades -- ooc::ShaderPt's spawn rule and light weight.
+__global__ __launch_bounds__(kBlock) void k_rep_shade(RepSpawnArgs A, const uint32_t* tmin,
+                                                      const uint8_t* lpmin) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  ShadePt sh;
+  for (int k = 0; k < 3; ++k) {
+    sh.lp[k] = A.shade10[k];
+    sh.lr[k] = A.shade10[3 + k];
+    sh.ks[k] = A.shade10[6 + k];
+  }
+  sh.shininess = A.shade10[9];
+  bool spawned = false;
+  if (j < A.nc) {
+    const uint32_t i = A.idx_c[j];
+    const uint64_t key = ((A.mask[i] >> A.rank) & 1ull) ? A.keys_n[i] : kInsituMissKey;
+    const bool win = key != kInsituMissKey && uint32_t(key >> 32) == tmin[j] &&
+                     uint8_t((key >> 16) & 0xFFu) == lpmin[j];
+    float4 sw = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (win) {
+      const float4 o4 = A.rays[2 * size_t(i)], d4 = A.rays[2 * size_t(i) + 1];
+      const float o[3] = {o4.x, o4.y, o4.z}, d[3] = {d4.x, d4.y, d4.z};
+      const spray_rt_hit h = A.hits_n[i];
+      float pos[3], wi[3], L[3];
+      spawned = shade_pt_point(o, d, h, sh, pos, wi, L);
+      sw = make_float4(L[0], L[1], L[2], 0.f);
+      if (A.hit_c) A.hit_c[j] = h;
+    }
+    A.win[j] = win;
+    A.svalid[j] = spawned;
+    A.sw[j] = sw;
+    A.pix_c[j] = A.pix[i];
+    A.sam_c[j] = A.sam[i];
+  }
+  const uint64_t b = __ballot(spawned);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(A.nshadow, (unsigned long long)__popcll(b));
+}
 }  // namespace
 
 #define LAUNCH(n, kern, ...)                                  \
@@ -679,6 +774,21 @@ hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nr
   return hipGetLastError();
 }
 
+hipError_t launch_rep_tkeys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
+                            int rank, const uint64_t* keys_n, uint32_t* tk) {
+  LAUNCH(nc, k_rep_tkeys, idx_c, nc, mask, rank, keys_n, tk);
+}
+hipError_t launch_rep_lpos(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
+                           int rank, const uint64_t* keys_n, const uint32_t* tmin, uint8_t* lp) {
+  LAUNCH(nc, k_rep_lpos, idx_c, nc, mask, rank, keys_n, tmin, lp);
+}
+hipError_t launch_rep_shadows(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin) {
+  LAUNCH(a.nc, k_rep_shadows, a, tmin);
+}
+hipError_t launch_rep_shade(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin,
+                            const uint8_t* lpmin) {
+  LAUNCH(a.nc, k_rep_shade, a, tmin, lpmin);
+}
 hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
                             uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,
                             int32_t* slot_c, int32_t* slot_pix, uint32_t* d_np) {

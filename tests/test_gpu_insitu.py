@@ -267,8 +267,8 @@ def test_engine_two_ranks_one_owner(oracle):
 
 @pytest.mark.parametrize("world,mode,case", [(2, 0, "pt1"), (8, 0, "pt1"), (8, 1, "pt1"),
                                              (3, 1, "pt1"), (2, 0, "ao16"), (3, 1, "ao16"),
-                                             (8, 0, "ao16"), (8, 1, "ao16")])
-def test_engine_replicated_frame_ranks(oracle, world, mode, case):
+                                             (8, 0, "ao16"), (8, 1, "ao16"), (8, 1, "pt1-u64")])
+def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
     """spray_rt_insitu_trace_frame with world processes sharing the GPU over
     the host transport: every eye ray on every rank, the keys' MIN and the
     occlusion bytes' SUM all-reduced (the host transport's
@@ -277,8 +277,12 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case):
     occlusion as 2- / 4-bit count fields, the film on rank 0) -- every
     shaded sample bit-exact against the whole-scene
     oracle, totals exact, the image within summation-order tolerance; both
-    partitions."""
+    partitions.  PT's winner keys are split (a MIN of the t bits, then of
+    the list positions at that t); "pt1-u64" keeps the 64-bit key MIN."""
     import pickle
+    if case == "pt1-u64":
+        monkeypatch.setenv("SPRAY_INSITU_SPLIT_KEYS", "0")
+        case = "pt1"
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
                                     args=(world, _free_port(), out, case, False, True, mode),
