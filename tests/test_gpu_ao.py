@@ -199,8 +199,9 @@ def test_ao_pairs_misaligned_pixel_runs(oracle):
     NaN beforehand), so pairs and occlusion equal the written-ray path's."""
     import spray_amd
     c = BENCH_CAMERA
-    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 1024, 1024)
-    org, d, pix, _ = oracle.eye_rays_ooc(cam, 1024, 2, (384, 448, 128, 32))
+    # the whole image at 128 x 128: silhouettes (pixels with hits and misses)
+    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 128, 128)
+    org, d, pix, _ = oracle.eye_rays_ooc(cam, 128, 2, (0, 0, 128, 128))
     rng = np.random.default_rng(3)
     keep = np.flatnonzero(rng.random(len(org)) > 0.3)[1:]
     org, d, pix = org[keep], d[keep], pix[keep]
@@ -233,7 +234,7 @@ def test_ao_pairs_misaligned_pixel_runs(oracle):
     fpair = torch.full((n * ns,), -1, dtype=torch.int32, device="cuda")
     fcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     focc = torch.full((n * ns,), 9, dtype=torch.uint8, device="cuda")
-    lv = torch.full((1024 * 1024 * ns, 4), float("nan"), dtype=torch.float32, device="cuda")
+    lv = torch.full((128 * 128 * ns, 4), float("nan"), dtype=torch.float32, device="cuda")
     rec = torch.empty((n, 16), dtype=torch.float32, device="cuda")
     rt.occluded_ao(rays, h, pixid, n, ns, fpair, lv, rec, fcnt, focc)
     rt.sync()
