@@ -201,7 +201,8 @@ def test_ao_pairs_misaligned_pixel_runs(oracle):
     c = BENCH_CAMERA
     # the whole image at 128 x 128: silhouettes (pixels with hits and misses)
     cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 128, 128)
-    org, d, pix, _ = oracle.eye_rays_ooc(cam, 128, 2, (0, 0, 128, 128))
+    # pixel-major, the spp samples of a pixel adjacent (the in-situ order)
+    org, d, pix, _ = oracle.eye_rays_insitu(cam, 128, 4, (0, 0, 128, 128), (0, 0, 128, 128))
     rng = np.random.default_rng(3)
     keep = np.flatnonzero(rng.random(len(org)) > 0.3)[1:]
     org, d, pix = org[keep], d[keep], pix[keep]
