@@ -11,7 +11,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <algorithm>
+#include <atomic>
 #include <sstream>
+#include <thread>
 
 namespace spray_host {
 
@@ -518,6 +521,10 @@ int GpuScene::init(const std::string& desc, const std::string& ply_path,
   if (r) return fail(r, spray_rt_last_error(rt_));
   cache_.init(int(domains_.size()), cache_size);
   block_domain_.assign(cache_.capacity(), -1);
+  images_.resize(domains_.size());
+  pinned_.assign(domains_.size(), nullptr);
+  r = prebuild_images();
+  if (r) return r;
   if (!cache_.lru()) {  // warm-up (scene.inl:86-93)
     for (size_t id = 0; id < domains_.size(); ++id) {
       SceneInfo s;
@@ -533,36 +540,86 @@ int GpuScene::init(const std::string& desc, const std::string& ply_path,
 // miss; the image is a pure function of the domain, so it is built on the
 // first load only and kept in pinned host memory -- a later miss is one
 // async DMA (the bytes, hence every result, are the same).
-int GpuScene::upload(int id, int block) {
-  if (images_.size() != domains_.size()) {
-    images_.resize(domains_.size());
-    pinned_.assign(domains_.size(), nullptr);
-  }
+int GpuScene::build_image(int id, std::string* err) {
   spray_rt::detail::SlotImage& img = images_[size_t(id)];
-  if (!pinned_[size_t(id)]) {
-    const Domain& d = domains_[id];
+  const Domain& d = domains_[id];
+  const auto it = ply_cache_.find(d.filename);
+  if (it == ply_cache_.end()) {
+    *err = "domain " + std::to_string(id) + ": mesh not loaded";
+    return SPRAY_RT_ERR_STATE;
+  }
+  Mesh mesh = it->second;  // world-space copy
+  float ident[16];
+  mat_identity(ident);
+  if (std::memcmp(ident, d.transform, sizeof(ident)) != 0)
+    transform_vertices(d.transform, mesh.vertices.data(), mesh.vertices.size() / 3);
+  compute_normals(&mesh);
+  if (const char* why = spray_rt::detail::build_slot_image(
+          mesh.vertices.data(), mesh.vertices.size() / 3, mesh.faces.data(),
+          mesh.faces.size() / 3, mesh.colors.data(), mesh.normals.data(), &img)) {
+    *err = std::string("domain ") + std::to_string(id) + ": " + why;
+    return SPRAY_RT_ERR_ARG;
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, img.bytes.size(), hipHostMallocDefault) != hipSuccess) {
+    *err = "pinned host memory for a domain image";
+    return SPRAY_RT_ERR_NOMEM;
+  }
+  std::memcpy(p, img.bytes.data(), img.bytes.size());
+  pinned_[size_t(id)] = p;
+  return SPRAY_RT_OK;
+}
+
+// The misses of an LRU cache would each build a domain image inside the
+// tracer's `omp single` while every other thread waits; building them all up
+// front (in parallel: the meshes first, then one image per task) leaves a
+// miss one async DMA.  Bounded by a host-memory budget (the images' bytes
+// ~ 100 B per triangle); past it images are built on their first miss.
+int GpuScene::prebuild_images() {
+  const char* e = std::getenv("SPRAY_SCENE_PREBUILD_MB");
+  const double budget_mb = e ? std::atof(e) : 16384.0;
+  if (budget_mb <= 0.0) return SPRAY_RT_OK;
+  double tris = 0.0;
+  for (const Domain& d : domains_) {
     auto it = ply_cache_.find(d.filename);
     if (it == ply_cache_.end()) {
       Mesh m;
-      std::string e;
-      if (!load_ply(d.filename, &m, &e)) return fail(SPRAY_RT_ERR_ARG, e);
+      std::string err;
+      if (!load_ply(d.filename, &m, &err)) return fail(SPRAY_RT_ERR_ARG, err);
       it = ply_cache_.emplace(d.filename, std::move(m)).first;
     }
-    Mesh mesh = it->second;  // world-space copy
-    float ident[16];
-    mat_identity(ident);
-    if (std::memcmp(ident, d.transform, sizeof(ident)) != 0)
-      transform_vertices(d.transform, mesh.vertices.data(), mesh.vertices.size() / 3);
-    compute_normals(&mesh);
-    if (const char* why = spray_rt::detail::build_slot_image(
-            mesh.vertices.data(), mesh.vertices.size() / 3, mesh.faces.data(),
-            mesh.faces.size() / 3, mesh.colors.data(), mesh.normals.data(), &img))
-      return fail(SPRAY_RT_ERR_ARG, std::string("domain ") + std::to_string(id) + ": " + why);
-    void* p = nullptr;
-    if (hipHostMalloc(&p, img.bytes.size(), hipHostMallocDefault) != hipSuccess)
-      return fail(SPRAY_RT_ERR_NOMEM, "pinned host memory for a domain image");
-    std::memcpy(p, img.bytes.data(), img.bytes.size());
-    pinned_[size_t(id)] = p;
+    tris += double(it->second.faces.size() / 3);
+  }
+  if (tris * 100.0 > budget_mb * 1048576.0) return SPRAY_RT_OK;
+  const int nd = int(domains_.size());
+  const int nt = std::max(1, std::min(nd, int(std::min(16u, std::thread::hardware_concurrency()))));
+  std::vector<int> rc(nd, SPRAY_RT_OK);
+  std::vector<std::string> err(nd);
+  std::atomic<int> next{0};
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; ++t)
+    pool.emplace_back([&] {
+      for (int id = next++; id < nd; id = next++) rc[id] = build_image(id, &err[id]);
+    });
+  for (std::thread& th : pool) th.join();
+  for (int id = 0; id < nd; ++id)
+    if (rc[id]) return fail(rc[id], err[id]);
+  return SPRAY_RT_OK;
+}
+
+int GpuScene::upload(int id, int block) {
+  spray_rt::detail::SlotImage& img = images_[size_t(id)];
+  if (!pinned_[size_t(id)]) {
+    const Domain& d = domains_[id];
+    if (ply_cache_.find(d.filename) == ply_cache_.end()) {
+      Mesh m;
+      std::string e;
+      if (!load_ply(d.filename, &m, &e)) return fail(SPRAY_RT_ERR_ARG, e);
+      ply_cache_.emplace(d.filename, std::move(m));
+    }
+    std::string e;
+    const int r = build_image(id, &e);
+    if (r) return fail(r, e);
   }
   int r = spray_rt::detail::upload_slot_image(rt_, block, img, pinned_[size_t(id)], true);
   if (r) return fail(r, spray_rt_last_error(rt_));

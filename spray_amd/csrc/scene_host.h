@@ -128,6 +128,12 @@ class GpuScene {
 
  private:
   int upload(int id, int block);
+  // the device image of domain id in pinned host memory (images_, pinned_);
+  // thread-safe for distinct ids once the domain's PLY is in ply_cache_
+  int build_image(int id, std::string* err);
+  // every image built up front, in parallel, when they fit the host budget
+  // (SPRAY_SCENE_PREBUILD_MB, default 16384; 0 = each on its first miss)
+  int prebuild_images();
   int fail(int code, const std::string& msg);
 
   std::vector<Domain> domains_;
