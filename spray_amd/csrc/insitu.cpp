@@ -136,6 +136,9 @@ struct InsituTransport {
   // copies a rank sends itself may skip the wire (the owner gathers them
   // straight from the holder's arrays)
   virtual bool self_direct() const { return true; }
+  // collectives enqueued on a side stream run beside the main stream's work
+  // (RCCL); the host form runs them in order, blocking
+  virtual bool side_stream() const { return false; }
 };
 
 struct spray_rt_insitu {
@@ -167,7 +170,7 @@ struct spray_rt_insitu {
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
   // split keys: t bits and list positions over C; the list positions'
   // all-reduce runs on a second stream (cs) beside the shadow any hit
-  DBuf rtk, rlp;
+  DBuf rtk, rlp, rbmax;
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
   // phase timing (spray_rt_insitu_set_timing): events on the stream
@@ -285,6 +288,7 @@ struct RcclTransport : InsituTransport {
                "ncclAllReduce(min u8)");
   }
   bool self_direct() const override { return !self_via_nccl; }
+  bool side_stream() const override { return true; }
   ~RcclTransport() override {
     if (comm) nccl().CommDestroy(comm);
   }
@@ -878,11 +882,12 @@ int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* 
   HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
   GROW(I->rsel_tmp, t1);
   uint32_t* dnum = I->rnum.as<uint32_t>();
-  if (want_pixmax) HIPCHK(c, hipMemsetAsync(dnum + 2, 0, 4, s));
+  if (want_pixmax) GROW(I->rbmax, (n / kBlock + 2) * 4);
   HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, I->rmask.as<uint64_t>()));
   HIPCHK(c, launch_rep_flags(s, I->rmask.as<uint64_t>(), n, I->rank, I->rfc.as<uint8_t>(),
                              I->rfl.as<uint8_t>(), want_pixmax ? pixid : nullptr,
-                             want_pixmax ? dnum + 2 : nullptr));
+                             want_pixmax ? dnum + 2 : nullptr,
+                             want_pixmax ? I->rbmax.as<uint32_t>() : nullptr));
   HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
                                   I->rsel_tmp.p, &t1));
   HIPCHK(c, launch_select_flagged(s, I->rfl.as<uint8_t>(), n, I->ridx_l.as<uint32_t>(), dnum + 1,
@@ -967,9 +972,13 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
       if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
       if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
       if (!I->ev_lp1) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp1, hipEventDisableTiming));
-      HIPCHK(c, hipEventRecord(I->ev_lp0, s));
-      HIPCHK(c, hipStreamWaitEvent(I->cs, I->ev_lp0, 0));
-      CALL(I->tr->allreduce_min_u8(I, lp, nc, I->cs));
+      if (I->tr->side_stream()) {
+        HIPCHK(c, hipEventRecord(I->ev_lp0, s));
+        HIPCHK(c, hipStreamWaitEvent(I->cs, I->ev_lp0, 0));
+        CALL(I->tr->allreduce_min_u8(I, lp, nc, I->cs));
+      } else {
+        COMM(I->tr->allreduce_min_u8(I, lp, nc, s));
+      }
       HIPCHK(c, hipEventRecord(I->ev_lp1, I->cs));
     }
   } else if (nc) {
@@ -1186,7 +1195,7 @@ void free_all(spray_rt_insitu* I) {
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rheads, &I->rincl, &I->rscan_tmp,
-                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp};
+                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)

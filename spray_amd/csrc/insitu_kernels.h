@@ -63,10 +63,10 @@ hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_
                             size_t n, uint8_t* win);
 // ---- replicated-ray frames (insitu.cpp, trace_replicated) ----
 // fc[i] = mask[i] != 0 (some domain on the list), fl[i] = bit `rank` of it;
-// pixmax (optional, zeroed): atomic max of pix[i] over C
+// pixmax (optional): max of pix[i] over C, through bmax (grid_for(n) u32)
 hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
                             uint8_t* fl, const int32_t* pix = nullptr,
-                            uint32_t* pixmax = nullptr);
+                            uint32_t* pixmax = nullptr, uint32_t* bmax = nullptr);
 // keys_c[j] = keys_n[idx_c[j]] where bit `rank` of its mask is set, else a miss
 hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
                            int rank, const uint64_t* keys_n, uint64_t* keys_c);

@@ -289,24 +289,50 @@ __global__ __launch_bounds__(kBlock) void k_weights_one(float4* __restrict__ w, 
 // Every rank holds the frame's eye rays; C = the rays whose domain list is
 // not empty (the same ascending list on every rank), L = the rays with a
 // domain of this rank on their list.
-// pixmax (optional): the largest pixel id of C (the AO frame's sample table)
+// bmax (optional): per block the largest pixel id of C (the AO frame's
+// sample table) -- one plain store per block, no same-address atomics
+// (131 K wave atomics on one word cost ~1.5 ms); k_max_u32 reduces them
 __global__ __launch_bounds__(kBlock) void k_rep_flags(const uint64_t* __restrict__ mask, size_t n,
                                                       int rank, uint8_t* __restrict__ fc,
                                                       uint8_t* __restrict__ fl,
                                                       const int32_t* __restrict__ pix,
-                                                      uint32_t* __restrict__ pixmax) {
+                                                      uint32_t* __restrict__ bmax) {
+  __shared__ uint32_t wmax[kBlock / 64];
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   uint32_t px = 0;
   if (i < n) {
     const uint64_t m = mask[i];
     fc[i] = m != 0;
     fl[i] = uint8_t((m >> rank) & 1ull);
-    if (pixmax && m) px = uint32_t(max(pix[i], 0));
+    if (bmax && m) px = uint32_t(max(pix[i], 0));
   }
-  if (pixmax) {
+  if (bmax) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) px = max(px, uint32_t(__shfl_xor(int(px), off)));
-    if ((threadIdx.x & 63) == 0 && px) atomicMax(pixmax, px);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = px;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t b = 0;
+      for (int w = 0; w < kBlock / 64; ++w) b = max(b, wmax[w]);
+      bmax[blockIdx.x] = b;
+    }
+  }
+}
+
+// *out = max(v[0..n)), one block
+__global__ __launch_bounds__(1024) void k_max_u32(const uint32_t* __restrict__ v, size_t n,
+                                                  uint32_t* __restrict__ out) {
+  __shared__ uint32_t part[1024 / 64];
+  uint32_t m = 0;
+  for (size_t k = threadIdx.x; k < n; k += 1024) m = max(m, v[k]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, uint32_t(__shfl_xor(int(m), off)));
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (int w = 0; w < 1024 / 64; ++w) b = max(b, part[w]);
+    *out = b;
   }
 }
 
@@ -758,8 +784,12 @@ hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
 }
 hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
-                            uint8_t* fl, const int32_t* pix, uint32_t* pixmax) {
-  LAUNCH(n, k_rep_flags, mask, n, rank, fc, fl, pix, pixmax);
+                            uint8_t* fl, const int32_t* pix, uint32_t* pixmax, uint32_t* bmax) {
+  if (n == 0) return pixmax ? hipMemsetAsync(pixmax, 0, 4, s) : hipSuccess;
+  k_rep_flags<<<grid_for(n), kBlock, 0, s>>>(mask, n, rank, fc, fl, pixmax ? pix : nullptr,
+                                             pixmax ? bmax : nullptr);
+  if (pixmax) k_max_u32<<<1, 1024, 0, s>>>(bmax, grid_for(n), pixmax);
+  return hipGetLastError();
 }
 hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
                            int rank, const uint64_t* keys_n, uint64_t* keys_c) {
