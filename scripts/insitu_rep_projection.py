@@ -14,13 +14,14 @@ Inputs
 * the measured N = 1 frame (the bench's fused single-GPU frame, --n1-ms).
 
 Model of one frame at N ranks (every rank runs the same sequence):
-  PT: T = max_r(lists + keyed closest hit) + AR(8 |C|) + max_r(shadows)
-          + AR(|C| + 192) + max_r(film) + RED(12 runs) + max_r(totals read)
-          (runs = the pixel runs along C: the film's per-run sums go to rank 0)
-  AO: T = max_r(lists + keyed closest hit) + AR(8 |C|) + AR(16 |C|)
-          + max_r(AO rays: spawn + any hit) + AR(16 |C| fb / 8) + film(rank 0)
-          + max_r(totals read)           (fb = 2 / 4 / 8 bits for N <= 3 / 15 / 64;
-                                          no image reduce: rank 0 films all)
+  PT: T = max_r(route + select + keyed closest hit + key prep) + AR(4 |C|)
+          + max_r(shadow trace + shade) + AR(|C| + 192) + max_r(film + totals)
+          + RED(12 runs)   (t bits MIN; the list positions' u8 MIN overlaps the
+          shadow any hit; runs = the pixel runs along C, their sums to rank 0)
+  AO: T = max_r(route + select + keyed closest hit) + AR(8 |C|) + max_r(publish)
+          + AR(16 |C|) + max_r(AO spawn + any hit) + AR(2 fb |C|)
+          + max_r(film + totals)  (fb = 2 / 4 / 8 bits for N <= 3 / 15 / 64;
+                                   no image reduce: rank 0 films all)
   AR(B)  = alpha + 2 (N - 1) / N * B / bw     (ring all-reduce)
   RED(B) = alpha + (N - 1) / N * B / bw * 2   (reduce to rank 0 as reduce-
            scatter + gather)
@@ -50,31 +51,34 @@ def fbits(n):
     return 2 if n <= 3 else (4 if n <= 15 else 8)
 
 
+SEGMENTS = {  # phases between the frame's collectives, in order
+    "pt": [("route", "select", "keyed_closest_hit", "key_prep"), ("shadow_trace", "shade"),
+           ("film_totals",)],
+    "ao": [("route", "select", "keyed_closest_hit"), ("publish",), ("ao_spawn", "ao_trace"),
+           ("film_totals",)],
+}
+
+
 def project(run, link):
     n = run["world"]
     ranks = run["ranks"]
+    kind = run.get("kind", "pt")
     ph = lambda r, k: r["phases_ms"].get(k, 0.0)  # noqa: E731
-    st = ranks[0]["stats"]
-    per = st["bytes_sent"] / max(st["traces"], 1)
-    a = max(ph(r, "lists") + ph(r, "keyed_closest_hit") for r in ranks)  # excl. collectives
-    b = max(ph(r, "shadows") for r in ranks)
-    c = max(ph(r, "film") for r in ranks)
-    d = max(ph(r, "totals") for r in ranks)
-    nc = ranks[0].get("nc")
-    if run.get("kind", "pt") == "ao":
-        # bytes_sent = 24 |C| + |C| * 16 * fb / 8 per trace (keys, normals, fields)
+    # every segment ends in a collective all ranks wait for: its busiest rank
+    seg = [max(sum(ph(r, k) for k in names) for r in ranks) for names in SEGMENTS[kind]]
+    nc = ranks[0]["nc"]
+    if kind == "ao":
         fb = fbits(n)
-        nc = nc if nc is not None else per / (24 + 2 * fb)
         comm = ar(8 * nc, n, link) + ar(16 * nc, n, link) + ar(2 * fb * nc, n, link)
     else:
-        runs = ranks[0].get("pixel_runs")
-        img = 12 * runs if runs is not None else IMAGE_BYTES
-        nc = nc if nc is not None else (per - 192) / 9
-        comm = ar(8 * nc, n, link) + ar(nc + 192, n, link) + red(img, n, link)
-    return {"device_ms": round(a + b + c + d, 4), "comm_ms": round(comm, 4),
-            "frame_ms": round(a + b + c + d + comm, 4),
-            "busiest": {"lists+keyed": round(a, 4), "shadows": round(b, 4), "film": round(c, 4),
-                        "totals": round(d, 4)}}
+        # t bits MIN, then occlusion bytes + totals SUM (the list positions'
+        # MIN runs beside the shadow any hit), the film's run sums to rank 0
+        comm = ar(4 * nc, n, link) + ar(nc + 192, n, link) + red(12 * ranks[0]["pixel_runs"], n,
+                                                                  link)
+    dev = sum(seg)
+    return {"device_ms": round(dev, 4), "comm_ms": round(comm, 4),
+            "frame_ms": round(dev + comm, 4),
+            "busiest_per_segment": [round(x, 4) for x in seg]}
 
 
 def main():
@@ -102,16 +106,17 @@ def main():
         rows.append(row)
     out = {"model": __doc__.strip().split("\n\n")[2], "links": LINK, "n1_ms": args.n1_ms,
            "rccl_one_rank_floor": rep.get("rccl_one_rank_floor"), "rows": rows}
-    print("| frame | N | partition | busiest lists+keyed | shadows / AO rays | film | device ms "
-          "| comm ms (cons.) | frame ms (cons. / opt.) | x N=1 (cons. / opt.) |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
+    print("| frame | N | partition | busiest rank per segment (ms) | device ms | comm ms (cons.) "
+          "| frame ms (cons. / opt.) | x N=1 (cons. / opt.) |")
+    print("|---|---|---|---|---|---|---|---|")
     sx = lambda v: "-" if v is None else "%.2f" % v  # noqa: E731
     for r in rows:
         c, o = r["conservative"], r["optimistic"]
-        print("| %s | %d | %s | %.3f | %.3f | %.3f | %.3f | %.3f | %.3f / %.3f | %s / %s |" % (
-            r["kind"], r["world"], r["partition"], c["busiest"]["lists+keyed"],
-            c["busiest"]["shadows"], c["busiest"]["film"], c["device_ms"], c["comm_ms"],
-            c["frame_ms"], o["frame_ms"], sx(c["speedup_vs_n1"]), sx(o["speedup_vs_n1"])))
+        print("| %s | %d | %s | %s | %.3f | %.3f | %.3f / %.3f | %s / %s |" % (
+            r["kind"], r["world"], r["partition"],
+            " + ".join("%.3f" % x for x in c["busiest_per_segment"]), c["device_ms"],
+            c["comm_ms"], c["frame_ms"], o["frame_ms"], sx(c["speedup_vs_n1"]),
+            sx(o["speedup_vs_n1"])))
     if args.out:
         with open(args.out, "w") as fh:
             json.dump(out, fh, indent=1)

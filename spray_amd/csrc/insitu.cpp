@@ -884,6 +884,7 @@ int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* 
   uint32_t* dnum = I->rnum.as<uint32_t>();
   if (want_pixmax) GROW(I->rbmax, (n / kBlock + 2) * 4);
   HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, I->rmask.as<uint64_t>()));
+  MARK(1);
   HIPCHK(c, launch_rep_flags(s, I->rmask.as<uint64_t>(), n, I->rank, I->rfc.as<uint8_t>(),
                              I->rfl.as<uint8_t>(), want_pixmax ? pixid : nullptr,
                              want_pixmax ? dnum + 2 : nullptr,
@@ -900,7 +901,7 @@ int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* 
   const size_t nc = cnt[0];
   *nc_out = nc;
   if (pixmax_out) *pixmax_out = want_pixmax ? cnt[2] : 0;
-  MARK(1);
+  MARK(2);
   GROW(I->rkeys_n, n * 8);
   GROW(I->rhits_n, n * 48);
   GROW(I->rkeys_c, nc * 8 + 8);
@@ -933,6 +934,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   size_t nc = 0;
   const bool split = split_keys() && c->ndom <= 255;
   CALL(rep_lists_keys(I, rays, pixid, n, false, &nc, nullptr, !split));
+  MARK(3);
   // the compact film's slots (runs of equal pixels along C), their count on
   // its way to the host while the frame runs on
   GROW(I->rheads, nc * 4 + 4);
@@ -985,7 +987,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
     COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   }
   // ---- 4. shadow rays of every hit, own any hit; the winners shade
-  MARK(2);
+  MARK(4);
   GROW(I->rsray, nc * 32 + 32);
   GROW(I->rsflag, nc + 1);
   GROW(I->rwin, nc + 1);
@@ -1022,6 +1024,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
     if (nc)
       HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
                                              I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
+    MARK(5);
     if (nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
     HIPCHK(c, launch_rep_shade(s, A, tk, lp));
   } else {
@@ -1029,6 +1032,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
     if (nc)
       HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
                                              I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
+    MARK(5);
   }
   // the frame totals behind the occlusion bytes: rank 0 counts the frame's
   // radiance rays, every rank the shadow rays it spawned
@@ -1038,7 +1042,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   COMM(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nc + 192));
   // ---- 6. film of the rays this rank won into the runs' sums, reduced to
   // rank 0 (12 B per run of C instead of the 16-B-per-pixel image)
-  MARK(3);
+  MARK(6);
   HIPCHK(c, hipEventSynchronize(I->ev_np));  // long done: the scan ran before the keyed launch
   const size_t np = nc ? *h_np : 0;
   // the all-reduces' and the reduce's payload
@@ -1051,7 +1055,6 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                                  I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
                                  I->rocc.as<uint8_t>(), scale, 3));
     COMM(I->tr->reduce_f32(I, I->rcompact.as<float>(), np * 3, 0));
-    MARK(3);
     if (I->rank == 0)
       HIPCHK(c, launch_rep_expand(s, image, I->rslot_pix.as<int32_t>(), I->rcompact.as<float>(),
                                   np));
@@ -1060,12 +1063,11 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
     HIPCHK(c, launch_record(s, I->rwin.as<uint8_t>(), nc, 0, 1, I->rsam.as<int32_t>(),
                             I->rhit_c.as<spray_rt_hit>(), I->rsvalid.as<uint8_t>(),
                             I->rocc.as<uint8_t>(), *rec));
-  MARK(4);
   uint8_t* ht = reinterpret_cast<uint8_t*>(I->h_small + 128);  // 192 bytes
   HIPCHK(c, hipMemcpyAsync(ht, I->rocc.as<uint8_t>() + nc, 192, hipMemcpyDeviceToHost, s));
-  MARK(4);
+  MARK(6);
   HIPCHK(c, hipStreamSynchronize(s));
-  flush_phases(I, 5);
+  flush_phases(I, 7);
   unsigned long long tot[3] = {0, 0, 0};
   for (int k = 0; k < 192; ++k) tot[k >> 6] += (unsigned long long)ht[k] << (k & 63);
   if (totals)
@@ -1097,8 +1099,8 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   uint32_t pixmax = 0;
   CALL(rep_lists_keys(I, rays, pixid, n, true, &nc, &pixmax));
   if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C| >= 2^27");
+  MARK(3);
   if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
-  MARK(2);
   const int fb = I->world <= 3 ? 2 : (I->world <= 15 ? 4 : 8);
   const size_t npair = nc * size_t(ns);
   const size_t words = (npair * size_t(fb) + 31) / 32;
@@ -1147,6 +1149,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   I->st[1] += 24 * nc + 4 * words;
   if (nc) COMM(I->tr->allreduce_u64(I, reinterpret_cast<unsigned long long*>(A.pub), 2 * nc));
   // ---- 5. every hit's AO rays (the same pairs on every rank), own any hit
+  MARK(4);
   HIPCHK(c, launch_rep_ao_hits(s, A));
   HIPCHK(c, hipMemsetAsync(dcount, 0, 4, s));
   HIPCHK(c, hipMemsetAsync(I->afields.p, 0, words * 4, s));
@@ -1155,6 +1158,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
                                     A.pix_c, nc, ns, npix, I->apairs.as<uint32_t>(),
                                     I->alv.as<float>(), I->arec.as<float>(), dcount,
                                     I->ascratch.p));
+    MARK(5);
     HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
                                        I->arec.as<float>(), I->alv.as<float>(), ns, dcount,
                                        I->aocc_p.as<uint8_t>(), nullptr));
@@ -1164,15 +1168,14 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   // ---- 6. occlusion OR over the group: a SUM of the count fields' bytes
   if (words) COMM(I->tr->allreduce_sum_u8(I, I->afields.as<uint8_t>(), words * 4));
   // ---- 7. the whole film on rank 0; records of each rank's winners
-  MARK(3);
+  MARK(6);
   if (I->rank == 0) HIPCHK(c, launch_rep_ao_film(s, A, image, 1.0 / double(spp)));
   if (rec) HIPCHK(c, launch_rep_ao_record(s, A, *rec));
-  MARK(4);
   uint32_t* hp = reinterpret_cast<uint32_t*>(I->h_small + 128);
   HIPCHK(c, hipMemcpyAsync(hp, dcount, 4, hipMemcpyDeviceToHost, s));
-  MARK(4);
+  MARK(6);
   HIPCHK(c, hipStreamSynchronize(s));
-  flush_phases(I, 5);
+  flush_phases(I, 7);
   if (totals) {
     totals[0] = n;
     totals[1] = *hp;

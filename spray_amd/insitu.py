@@ -27,7 +27,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._native import SprayRtError, lib
+from ._native import SHADER_AO, SprayRtError, lib
 
 __all__ = ["morton_partition", "PARTITION_GROUP_CLOSE", "PARTITION_ROUND_ROBIN", "horizontal_stripe", "setup_rank_context", "InsituEngine",
            "InsituRecords", "MISS_KEY"]
@@ -297,13 +297,19 @@ class InsituEngine:
         rc = lib().spray_rt_insitu_trace_frame(self.h, C.byref(shader), a, p, s, n, int(spp), im,
                                                rec, C.byref(tot))
         self.rt._check(rc, "insitu_trace_frame")
+        self._rep_kind = "ao" if shader.shader == SHADER_AO else "pt"
         return int(tot[0]), int(tot[1])
 
     def set_timing(self, on=True):
         """Per-phase HIP-event timing of the traces (phase_times)."""
         self.rt._check(lib().spray_rt_insitu_set_timing(self.h, 1 if on else 0), "set_timing")
 
-    REP_PHASES = ("lists", "keyed_closest_hit", "shadows", "film", "totals")
+    # replicated-ray frames (insitu.cpp trace_replicated / trace_replicated_ao)
+    REP_PHASES = ("route", "select", "keyed_closest_hit", "key_prep", "shadow_trace", "shade",
+                  "film_totals")
+    REP_AO_PHASES = ("route", "select", "keyed_closest_hit", "publish", "ao_spawn", "ao_trace",
+                     "film_totals")
+    _rep_kind = "pt"
     PROTOCOL_PHASES = ("route_plan", "ray_pack_unpack", "keyed_closest_hit", "key_composite",
                        "shading", "shadow_route_pack", "shadow_any_hit_return",
                        "film_totals")
@@ -314,7 +320,8 @@ class InsituEngine:
         out = (C.c_double * 9)()
         n = C.c_int(0)
         lib().spray_rt_insitu_phase_times(self.h, C.byref(out), C.byref(n))
-        names = {5: self.REP_PHASES, 8: self.PROTOCOL_PHASES, 1: ("frame",)}.get(
+        rep = self.REP_AO_PHASES if self._rep_kind == "ao" else self.REP_PHASES
+        names = {7: rep, 8: self.PROTOCOL_PHASES, 1: ("frame",)}.get(
             n.value, tuple("phase%d" % k for k in range(n.value)))
         d = {names[k]: float(out[k]) for k in range(n.value)}
         d["collectives"] = float(out[8])
