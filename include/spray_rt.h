@@ -628,28 +628,29 @@ int spray_rt_insitu_trace(spray_rt_insitu_t ins, const spray_rt_shader* shader,
                           unsigned long long totals[3]);
 /* The whole frame with replicated eye rays: rays[n] / pixid / samid are
  * EVERY eye ray of the frame (spray_rt_eye_rays_insitu over the whole
- * blocking tile), the same on every rank.  Instead of moving rays to their
- * domains' owners, each rank
- *   1. computes every ray's owner-rank mask (its domain list through the
- *      partition) -- C = the rays with a non-empty list, the same ascending
- *      list on every rank;
- *   2. traces the rays of C with a domain of its own over its own domains
- *      (keyed closest hit: t, list position, domain);
- *   3. joins one MIN all-reduce of the keys over C -- the sequential walk's
- *      winner of every ray, on every rank (VBuf::compositeTbuf,
- *      insitu_vbuf.h:109-129, per ray instead of per tile);
- *   4. builds the point-light shadow ray of every hit from (org, dir, t),
- *      the winner's bits, and any-hits it over its own domains; the winner
- *      shades (ooc::ShaderPt point light);
- *   5. joins one SUM all-reduce of the occlusion bytes over C, the frame
+ * blocking tile; tnear SPRAY_RAY_EPSILON and tfar +inf, as every radiance
+ * ray of the reference), the same on every rank.  Instead of moving rays to
+ * their domains' owners, each rank
+ *   1. selects C' = the rays that enter the scene's bounding box (a
+ *      superset of the rays with a domain on their list, the same ascending
+ *      list on every rank);
+ *   2. traces C' over its own domains in one launch: keyed closest hit (t,
+ *      list position, domain) and the point-light shading of its own hit;
+ *   3. joins a MIN all-reduce of the t bits, then of the list positions at
+ *      that t (a byte each, beside step 4) -- the sequential walk's winner
+ *      of every ray on every rank (VBuf::compositeTbuf, insitu_vbuf.h:
+ *      109-129, per ray instead of per tile);
+ *   4. any-hits the point-light shadow ray of every hit, built in the lanes
+ *      from (org, dir, minimum t) -- the winner's bits -- over its domains;
+ *   5. joins one SUM all-reduce of the occlusion bytes over C', the frame
  *      totals riding behind them (compositeObuf + WorkStats::reduce);
  *   6. films the unoccluded shadows of the rays it won into per-run sums
- *      (a run = consecutive rays of C with one pixel: the spp samples of a
+ *      (a run = consecutive rays of C' with one pixel: the spp samples of a
  *      pixel), which one RCCL reduce (12 B per run instead of the 16-B-per-
  *      pixel image) brings to rank 0, where they are added to image_rgba.
  * The WHOLE frame lands in rank 0's image; the other ranks' images are not
  * touched (no spray_rt_insitu_composite needed).  No ray, hit or shadow
- * record crosses the wire and no count is exchanged: two all-reduces, one
+ * record crosses the wire and no count is exchanged: three all-reduces, one
  * reduce and one host read per frame.  Results per sample are the
  * protocol's (the same winner, shading and occlusion).
  * AO (ooc::ShaderAo, one bounce, <= 32 samples, diffuse surfaces): after 3.

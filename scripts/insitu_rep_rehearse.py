@@ -86,11 +86,24 @@ def _rank(rank, world, port, mode, frames, out, kind="pt"):
         tot = trace(sh, rays, pix, sam, SPP, image)
     s1 = eng.stats()
     ph = {k: v / frames for k, v in eng.phase_times().items()}
-    # |C| (rays with a non-empty domain list) and the pixel runs along C:
-    # the sizes of the frame's collectives
-    m = torch.empty(n, dtype=torch.int64, device="cuda")
-    rt.route(rays, m)
-    on = m != 0
+    # the sizes of the frame's collectives: PT |C'| (rays entering the
+    # scene's bounding box: k_rep_cull's slab test, the same float ops), AO
+    # |C| (rays with a non-empty domain list), and the pixel runs along them
+    if kind == "pt":
+        lo = torch.tensor(boxes[:, :3].min(0), dtype=torch.float32, device="cuda")
+        hi = torch.tensor(boxes[:, 3:].max(0), dtype=torch.float32, device="cuda")
+        o, dr = rays[:, 0:3], rays[:, 4:7]
+        inv = 1.0 / dr
+        neg = inv < 0
+        t0 = (torch.where(neg, hi, lo) - o) * inv
+        t1 = (torch.where(neg, lo, hi) - o) * inv
+        tmin = t0.max(dim=1).values
+        tmax = t1.min(dim=1).values
+        on = ((tmin <= tmax) & (tmin < float("inf")) & (tmax > 0.001)) | (dr == 0).any(dim=1)
+    else:
+        m = torch.empty(n, dtype=torch.int64, device="cuda")
+        rt.route(rays, m)
+        on = m != 0
     pc = pix[on]
     nc, nruns = int(on.sum()), int(1 + (pc[1:] != pc[:-1]).sum()) if pc.numel() else 0
     res = {"rank": rank, "domains": int((owner == rank).sum()), "phases_ms": ph,

@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -916,8 +917,19 @@ int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* 
 }
 
 // The frame with replicated eye rays (spray_rt_insitu_trace_frame): see
-// include/spray_rt.h.  Phases: 0 lists, 1 keyed closest hit, 2 shadows,
-// 3 film, 4 totals (collectives: kCommPhase).
+// include/spray_rt.h.  Every rank, over C' (the eye rays that enter the
+// scene's bounding box, a superset of the rays with a domain list, the same
+// ascending list on every rank without a top-level walk):
+//   keyed closest hit over its domains + the point-light shading of its own
+//   hit (one launch, launch_scene_rep_keyed) -> MIN all-reduce of the t bits
+//   -> list positions at that t (u8 MIN, on a side stream beside the next
+//   step) -> the shadow ray of every hit from the minimum t, any hit over
+//   its domains (launch_scene_rep_shadows, rays built in the lanes) -> the
+//   winners' flags and shadow count -> SUM all-reduce of the occlusion
+//   bytes + totals -> film of its winners into per-pixel-run sums -> reduce
+//   to rank 0.  One host read (|C'|).  Phases: 0 cull + select, 1 film
+//   slots, 2 keyed closest hit + shading, 3 list positions, 4 shadow any
+//   hit, 5 winners + totals, 6 film (collectives: kCommPhase).
 int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
                      const int32_t* pixid, const int32_t* samid, size_t n, int spp,
                      float* image, const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
@@ -925,18 +937,41 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   hipStream_t s = stream_of(c);
   const double scale = 1.0 / double(spp);
   const spray_rt_light& lt = P->lights[0];
-  RepSpawnArgs A{};
   const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
                              lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                              P->ks[2],       P->shininess};
-  std::memcpy(A.shade10, shade10, sizeof(shade10));
-  // ---- 1-2. lists, own keyed closest hits
-  size_t nc = 0;
-  const bool split = split_keys() && c->ndom <= 255;
-  CALL(rep_lists_keys(I, rays, pixid, n, false, &nc, nullptr, !split));
-  MARK(3);
-  // the compact film's slots (runs of equal pixels along C), their count on
-  // its way to the host while the frame runs on
+  // ---- 1. C' (one host read: |C'| sizes the all-reduces, the same on every rank)
+  MARK(0);
+  SceneBox box{};
+  for (int k = 0; k < 3; ++k) {
+    box.lo[k] = INFINITY;
+    box.hi[k] = -INFINITY;
+  }
+  for (int d = 0; d < c->ndom; ++d)
+    for (int k = 0; k < 3; ++k) {
+      box.lo[k] = std::min(box.lo[k], c->h_boxes[6 * d + k]);
+      box.hi[k] = std::max(box.hi[k], c->h_boxes[6 * d + 3 + k]);
+    }
+  GROW(I->rfc, n);
+  GROW(I->ridx_c, n * 4);
+  GROW(I->rnum, 4 * 4);
+  size_t t1 = 0;
+  HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
+  GROW(I->rsel_tmp, t1);
+  uint32_t* dnum = I->rnum.as<uint32_t>();
+  HIPCHK(c, launch_rep_cull(s, rays, n, box, I->rfc.as<uint8_t>()));
+  HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
+                                  I->rsel_tmp.p, &t1));
+  HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  ++I->st[3];
+  uint32_t nc32 = 0;
+  std::memcpy(&nc32, I->h_small, 4);
+  const size_t nc = nc32;
+  const uint32_t* idx_c = I->ridx_c.as<uint32_t>();
+  // ---- 2. the compact film's slots (runs of equal pixels along C'), their
+  // count on its way to the host while the frame runs on
+  MARK(1);
   GROW(I->rheads, nc * 4 + 4);
   GROW(I->rincl, nc * 4 + 4);
   GROW(I->rslot_c, nc * 4 + 4);
@@ -948,28 +983,36 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                              nullptr, nullptr));
   GROW(I->rscan_tmp, tsc);
   if (!I->ev_np) HIPCHK(c, hipEventCreateWithFlags(&I->ev_np, hipEventDisableTiming));
-  HIPCHK(c, launch_rep_slots(s, I->ridx_c.as<uint32_t>(), pixid, nc, I->rheads.as<uint32_t>(),
-                             I->rincl.as<uint32_t>(), I->rscan_tmp.p, &tsc,
-                             I->rslot_c.as<int32_t>(), I->rslot_pix.as<int32_t>(),
-                             I->rnp.as<uint32_t>()));
+  HIPCHK(c, launch_rep_slots(s, idx_c, pixid, nc, I->rheads.as<uint32_t>(), I->rincl.as<uint32_t>(),
+                             I->rscan_tmp.p, &tsc, I->rslot_c.as<int32_t>(),
+                             I->rslot_pix.as<int32_t>(), I->rnp.as<uint32_t>()));
   uint32_t* h_np = reinterpret_cast<uint32_t*>(I->h_small + 250);
   HIPCHK(c, hipMemcpyAsync(h_np, I->rnp.p, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipEventRecord(I->ev_np, s));
-  // ---- 3. the winning key of every ray of C, on every rank: split (t bits,
-  // then the list positions at that t, the latter beside the shadow rays'
-  // any hit) while list positions fit a byte, else the 64-bit keys
-  uint32_t* tk = nullptr;
+  // ---- 3. own keyed closest hits + shading of the own hits
+  MARK(2);
+  GROW(I->rkeys_c, nc * 8 + 8);
+  GROW(I->rtk, nc * 4 + 4);
+  GROW(I->rsw, nc * 16 + 16);
+  GROW(I->rsvalid, nc + 1);
+  if (rec) GROW(I->rhit_c, nc * 48 + 48);
+  uint64_t* keys = I->rkeys_c.as<uint64_t>();
+  uint32_t* tk = I->rtk.as<uint32_t>();
+  HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
+                                   rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
+                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>()));
+  // ---- 4. the group's minimum t of every ray of C' (then the list
+  // position at that t) -- split while list positions fit a byte, else the
+  // 64-bit keys' MIN
+  const bool split = split_keys() && c->ndom <= 255;
   uint8_t* lp = nullptr;
+  uint64_t* kmin = nullptr;
   if (split) {
-    GROW(I->rtk, nc * 4 + 4);
-    GROW(I->rlp, nc + 1);
-    tk = I->rtk.as<uint32_t>();
-    lp = I->rlp.as<uint8_t>();
-    HIPCHK(c, launch_rep_tkeys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
-                               I->rkeys_n.as<uint64_t>(), tk));
     if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
-    HIPCHK(c, launch_rep_lpos(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
-                              I->rkeys_n.as<uint64_t>(), tk, lp));
+    MARK(3);
+    GROW(I->rlp, nc + 1);
+    lp = I->rlp.as<uint8_t>();
+    HIPCHK(c, launch_rep_lp(s, keys, tk, nc, lp));
     if (nc) {
       if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
       if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
@@ -983,86 +1026,62 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
       }
       HIPCHK(c, hipEventRecord(I->ev_lp1, I->cs));
     }
-  } else if (nc) {
-    COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
-  }
-  // ---- 4. shadow rays of every hit, own any hit; the winners shade
-  MARK(4);
-  GROW(I->rsray, nc * 32 + 32);
-  GROW(I->rsflag, nc + 1);
-  GROW(I->rwin, nc + 1);
-  GROW(I->rsvalid, nc + 1);
-  GROW(I->rsw, nc * 16 + 16);
-  GROW(I->rocc, nc + 192);
-  GROW(I->rpix, nc * 4 + 4);
-  GROW(I->rsam, nc * 4 + 4);
-  GROW(I->rnsh, 8);
-  if (rec) GROW(I->rhit_c, nc * 48 + 48);
-  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, 8, s));
-  A.nc = nc;
-  A.rank = I->rank;
-  A.idx_c = I->ridx_c.as<uint32_t>();
-  A.keys_c = I->rkeys_c.as<uint64_t>();
-  A.keys_n = I->rkeys_n.as<uint64_t>();
-  A.mask = I->rmask.as<uint64_t>();
-  A.rays = reinterpret_cast<const float4*>(rays);
-  A.hits_n = I->rhits_n.as<spray_rt_hit>();
-  A.pix = pixid;
-  A.sam = samid;
-  A.sray = I->rsray.as<float4>();
-  A.sflag = I->rsflag.as<uint8_t>();
-  A.win = I->rwin.as<uint8_t>();
-  A.svalid = I->rsvalid.as<uint8_t>();
-  A.sw = I->rsw.as<float4>();
-  A.occ = I->rocc.as<uint8_t>();
-  A.pix_c = I->rpix.as<int32_t>();
-  A.sam_c = I->rsam.as<int32_t>();
-  A.hit_c = rec ? I->rhit_c.as<spray_rt_hit>() : nullptr;
-  A.nshadow = I->rnsh.as<unsigned long long>();
-  if (split) {
-    HIPCHK(c, launch_rep_shadows(s, A, tk));
-    if (nc)
-      HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
-                                             I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
-    MARK(5);
-    if (nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
-    HIPCHK(c, launch_rep_shade(s, A, tk, lp));
   } else {
-    HIPCHK(c, launch_rep_spawn(s, A));
-    if (nc)
-      HIPCHK(c, launch_scene_occluded_masked(s, view(c), I->rsray.as<spray_rt_ray>(), nc,
-                                             I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>()));
-    MARK(5);
+    GROW(I->rkeys_n, nc * 8 + 8);  // the minimum keys (own keys stay in keys)
+    kmin = I->rkeys_n.as<uint64_t>();
+    HIPCHK(c, hipMemcpyAsync(kmin, keys, nc * 8, hipMemcpyDeviceToDevice, s));
+    if (nc) COMM(I->tr->allreduce_min_u64(I, kmin, nc));
+    MARK(3);
+    HIPCHK(c, launch_tmin_from_keys(s, kmin, nc, tk));
   }
-  // the frame totals behind the occlusion bytes: rank 0 counts the frame's
-  // radiance rays, every rank the shadow rays it spawned
+  // ---- 5. every hit's shadow ray from the minimum t, own any hit
+  MARK(4);
+  GROW(I->rocc, nc + 192);
+  HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nc, s));
+  HIPCHK(c, launch_scene_rep_shadows(s, view(c), rays, n, idx_c, nc, tk, shade10,
+                                     I->rocc.as<uint8_t>()));
+  // ---- 6. the winners (after the list positions' MIN), their shadows
+  // counted behind the occlusion bytes: rank 0 counts the frame's radiance
+  // rays, every rank its winners' shadow rays
+  MARK(5);
+  GROW(I->rwin, nc + 1);
+  GROW(I->rsflag, nc + 1);  // svw: the winners' spawned shadows
+  GROW(I->rnsh, 8);
+  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, 8, s));
+  if (split && nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
+  HIPCHK(c, launch_rep_win(s, keys, tk, lp, kmin, I->rsvalid.as<uint8_t>(), nc,
+                           I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
+                           I->rnsh.as<unsigned long long>()));
   HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nc, I->rank == 0 ? n : 0,
                               I->rnsh.as<unsigned long long>()));
-  // ---- 5. occlusion OR (a byte SUM) + totals
+  // ---- 7. occlusion OR (a byte SUM) + totals
   COMM(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nc + 192));
-  // ---- 6. film of the rays this rank won into the runs' sums, reduced to
-  // rank 0 (12 B per run of C instead of the 16-B-per-pixel image)
+  // ---- 8. film of the rays this rank won into the runs' sums, reduced to
+  // rank 0 (12 B per run of C' instead of the 16-B-per-pixel image)
   MARK(6);
   HIPCHK(c, hipEventSynchronize(I->ev_np));  // long done: the scan ran before the keyed launch
   const size_t np = nc ? *h_np : 0;
   // the all-reduces' and the reduce's payload
-  const size_t pay = (split ? 6 * nc : 9 * nc) + 192 + 12 * np;
+  const size_t pay = (split ? 5 * nc : 8 * nc) + nc + 192 + 12 * np;
   I->st[0] += pay;
   I->st[1] += pay;
   if (np) {
     HIPCHK(c, hipMemsetAsync(I->rcompact.p, 0, np * 12, s));
     HIPCHK(c, launch_film_atomic(s, I->rcompact.as<float>(), I->rslot_c.as<int32_t>(), nc, 1,
-                                 I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
+                                 I->rsw.as<float>(), I->rsflag.as<uint8_t>(),
                                  I->rocc.as<uint8_t>(), scale, 3));
     COMM(I->tr->reduce_f32(I, I->rcompact.as<float>(), np * 3, 0));
     if (I->rank == 0)
       HIPCHK(c, launch_rep_expand(s, image, I->rslot_pix.as<int32_t>(), I->rcompact.as<float>(),
                                   np));
   }
-  if (rec)
+  if (rec) {
+    GROW(I->rsam, nc * 4 + 4);
+    HIPCHK(c, launch_gather_i32(s, idx_c, nc, samid, I->rsam.as<int32_t>()));
     HIPCHK(c, launch_record(s, I->rwin.as<uint8_t>(), nc, 0, 1, I->rsam.as<int32_t>(),
-                            I->rhit_c.as<spray_rt_hit>(), I->rsvalid.as<uint8_t>(),
+                            I->rhit_c.as<spray_rt_hit>(), I->rsflag.as<uint8_t>(),
                             I->rocc.as<uint8_t>(), *rec));
+  }
   uint8_t* ht = reinterpret_cast<uint8_t*>(I->h_small + 128);  // 192 bytes
   HIPCHK(c, hipMemcpyAsync(ht, I->rocc.as<uint8_t>() + nc, 192, hipMemcpyDeviceToHost, s));
   MARK(6);

@@ -70,30 +70,26 @@ hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int r
 // keys_c[j] = keys_n[idx_c[j]] where bit `rank` of its mask is set, else a miss
 hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
                            int rank, const uint64_t* keys_n, uint64_t* keys_c);
-struct RepSpawnArgs {
-  size_t nc;
-  int rank;
-  const uint32_t* idx_c;      // [nc] ray ids of C
-  const uint64_t* keys_c;     // [nc] winning keys (after the MIN all-reduce)
-  const uint64_t* keys_n;     // [n] this rank's keys (valid where its mask bit is set)
-  const uint64_t* mask;       // [n] owner-rank masks
-  const float4* rays;         // [n] eye rays (32 B)
-  const spray_rt_hit* hits_n; // [n] this rank's hit records
-  const int32_t* pix;         // [n]
-  const int32_t* sam;         // [n]
-  float shade10[10];          // light position, radiance, ks, shininess
-  float4* sray;               // [nc] shadow ray of each hit (32 B)
-  uint8_t* sflag;             // [nc] 1: ray j hit (its shadow ray is traced here)
-  uint8_t* win;               // [nc] 1: this rank shades ray j
-  uint8_t* svalid;            // [nc] 1: the winner spawned the shadow ray
-  float4* sw;                 // [nc] its light weight
-  uint8_t* occ;               // [nc] zeroed (any hit writes own-domain occlusion)
-  int32_t* pix_c;             // [nc]
-  int32_t* sam_c;             // [nc]
-  spray_rt_hit* hit_c;        // [nc] winners' hit records (optional: records)
-  unsigned long long* nshadow;  // += spawned shadow rays
+// scene bounding box (the replicated frame's cull)
+struct SceneBox {
+  float lo[3], hi[3];
 };
-hipError_t launch_rep_spawn(hipStream_t s, const RepSpawnArgs& a);
+// fc[i] = ray i enters the box (or has a zero direction component)
+hipError_t launch_rep_cull(hipStream_t s, const spray_rt_ray* rays, size_t n, const SceneBox& b,
+                           uint8_t* fc);
+// lp[j] = list position of keys[j] where its t bits equal tmin[j], else 0xFF
+hipError_t launch_rep_lp(hipStream_t s, const uint64_t* keys, const uint32_t* tmin, size_t nc,
+                         uint8_t* lp);
+// win[j] = keys[j] is the group's minimum (t bits == tmin and list position
+// == lpmin, or, lpmin null, keys == kmin); svw = win && sv; *nshadow += svw
+hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* tmin,
+                          const uint8_t* lpmin, const uint64_t* kmin, const uint8_t* sv, size_t nc,
+                          uint8_t* win, uint8_t* svw, unsigned long long* nshadow);
+// tmin[j] = t bits of kmin[j] (0xFFFFFFFF: a miss)
+hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc, uint32_t* tmin);
+// dst[j] = src[idx[j]]
+hipError_t launch_gather_i32(hipStream_t s, const uint32_t* idx, size_t n, const int32_t* src,
+                             int32_t* dst);
 // The compact film's slots: the runs of equal pixels along C.  slot_c[j] =
 // run of ray j, slot_pix[run] = its pixel, *d_np = runs; heads / incl: [nc]
 // u32 scratch; temp == nullptr: *temp_bytes <- the scan's scratch size.
@@ -103,16 +99,6 @@ hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t*
 // image[4 slot_pix[q] + k] += compact[3 q + k], q < np
 hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
                              const float* compact, size_t np);
-// split keys: tk[j] = this rank's t bits of ray idx_c[j] (0xFFFFFFFF: none);
-// after their MIN, lp[j] = its list position where its t is the minimum
-// (0xFF elsewhere); the shadow rays from the minimum t; the winner's shading
-hipError_t launch_rep_tkeys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
-                            int rank, const uint64_t* keys_n, uint32_t* tk);
-hipError_t launch_rep_lpos(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
-                           int rank, const uint64_t* keys_n, const uint32_t* tmin, uint8_t* lp);
-hipError_t launch_rep_shadows(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin);
-hipError_t launch_rep_shade(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin,
-                            const uint8_t* lpmin);
 // tail[64 c + k] = bit k of {nrad, *nshadow, 0}[c] (192 bytes)
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow);

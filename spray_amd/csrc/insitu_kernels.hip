@@ -348,61 +348,6 @@ __global__ __launch_bounds__(kBlock) void k_rep_keys(const uint32_t* __restrict_
   keys_c[j] = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
 }
 
-// After the MIN all-reduce keys_c[j] is the winning key of ray idx_c[j] on
-// every rank.  Every rank builds the point-light shadow ray of every hit
-// from (org, dir, t) -- RTCRayUtil::hitPosition and PointLight::sample, the
-// operations of shade_pt_point, so the winner's bits -- and marks it for
-// its own any hit; the winner (its own key equals the minimum) shades:
-// spawn rule and light weight of ooc::ShaderPt (shade_pt_point).
-__global__ __launch_bounds__(kBlock) void k_rep_spawn(RepSpawnArgs A) {
-  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  ShadePt sh;
-  for (int k = 0; k < 3; ++k) {
-    sh.lp[k] = A.shade10[k];
-    sh.lr[k] = A.shade10[3 + k];
-    sh.ks[k] = A.shade10[6 + k];
-  }
-  sh.shininess = A.shade10[9];
-  bool spawned = false;
-  if (j < A.nc) {
-    const uint32_t i = A.idx_c[j];
-    const uint64_t key = A.keys_c[j];
-    const bool hit = key != kInsituMissKey;
-    const bool win = hit && ((A.mask[i] >> A.rank) & 1ull) && A.keys_n[i] == key;
-    float4 sw = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 o4 = A.rays[2 * size_t(i)], d4 = A.rays[2 * size_t(i) + 1];
-    const float o[3] = {o4.x, o4.y, o4.z}, d[3] = {d4.x, d4.y, d4.z};
-    float pos[3] = {0.f, 0.f, 0.f}, wi[3] = {0.f, 0.f, 1.f};
-    if (win) {
-      const spray_rt_hit h = A.hits_n[i];
-      float L[3];
-      spawned = shade_pt_point(o, d, h, sh, pos, wi, L);
-      sw = make_float4(L[0], L[1], L[2], 0.f);
-      if (A.hit_c) A.hit_c[j] = h;
-    } else if (hit) {
-      const float t = __uint_as_float(uint32_t(key >> 32));
-      pos[0] = d[0] * t + o[0];
-      pos[1] = d[1] * t + o[1];
-      pos[2] = d[2] * t + o[2];
-      wi[0] = sh.lp[0] - pos[0];
-      wi[1] = sh.lp[1] - pos[1];
-      wi[2] = sh.lp[2] - pos[2];
-      gnorm3(wi);
-    }
-    A.sray[2 * j] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
-    A.sray[2 * j + 1] = make_float4(wi[0], wi[1], wi[2], kInf);
-    A.sflag[j] = hit;
-    A.win[j] = win;
-    A.svalid[j] = spawned;
-    A.sw[j] = sw;
-    A.occ[j] = 0;
-    A.pix_c[j] = A.pix[i];
-    A.sam_c[j] = A.sam[i];
-  }
-  const uint64_t b = __ballot(spawned);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(A.nshadow, (unsigned long long)__popcll(b));
-}
-
 // The frame totals as bits (byte 64 c + k = bit k of total c) behind the
 // occlusion bytes: one SUM all-reduce of bytes adds them up exactly (a
 // byte sums at most `world` ones).
@@ -599,99 +544,77 @@ __global__ __launch_bounds__(kBlock) void k_rep_expand(float* __restrict__ image
   }
 }
 
-// ---- split keys of a replicated PT frame (insitu.cpp, trace_replicated) ---
-// The winner of ray j is the smallest (t, list position): a MIN all-reduce
-// of the t bits (u32: positive floats order as their bits), then one of the
-// list positions of the ranks at that t (u8) -- the shadow rays need only
-// t, so the second all-reduce overlaps their any hit.
-__global__ __launch_bounds__(kBlock) void k_rep_tkeys(const uint32_t* __restrict__ idx_c, size_t nc,
-                                                      const uint64_t* __restrict__ mask, int rank,
-                                                      const uint64_t* __restrict__ keys_n,
-                                                      uint32_t* __restrict__ tk) {
-  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= nc) return;
-  const uint32_t i = idx_c[j];
-  const uint64_t key = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
-  tk[j] = key != kInsituMissKey ? uint32_t(key >> 32) : 0xFFFFFFFFu;
+// ---- replicated PT frames (insitu.cpp, trace_replicated) ----------------
+// C' = the eye rays that enter the scene's bounding box: a superset of the
+// rays with a domain on their list (every domain box lies inside it and the
+// slab test is monotone in the box when no direction component is zero; a
+// ray with one is kept), the same on every rank without a top-level walk.
+__global__ __launch_bounds__(kBlock) void k_rep_cull(const float4* __restrict__ rays, size_t n,
+                                                     SceneBox b, uint8_t* __restrict__ fc) {
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float4 o = rays[2 * i], d = rays[2 * i + 1];
+  bool in = d.x == 0.0f || d.y == 0.0f || d.z == 0.0f;
+  if (!in) {
+    const DRay r = make_dray(o.x, o.y, o.z, d.x, d.y, d.z);
+    float tm;
+    in = aabb_ref6(b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2], r, tm);
+  }
+  fc[i] = in;
 }
 
-// lp[j] = this rank's list position of ray j where its t is the minimum,
-// 0xFF elsewhere (list positions < 255: the caller checks the domain count)
-__global__ __launch_bounds__(kBlock) void k_rep_lpos(const uint32_t* __restrict__ idx_c, size_t nc,
-                                                     const uint64_t* __restrict__ mask, int rank,
-                                                     const uint64_t* __restrict__ keys_n,
-                                                     const uint32_t* __restrict__ tmin,
-                                                     uint8_t* __restrict__ lp) {
+// after the MIN of the t bits: lp[j] = this rank's list position of ray j
+// where its t is the minimum, 0xFF elsewhere (list positions < 255)
+__global__ __launch_bounds__(kBlock) void k_rep_lp(const uint64_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ tmin, size_t nc,
+                                                   uint8_t* __restrict__ lp) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= nc) return;
-  const uint32_t i = idx_c[j];
-  const uint64_t key = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
+  const uint64_t key = keys[j];
   const bool cand = key != kInsituMissKey && uint32_t(key >> 32) == tmin[j];
   lp[j] = cand ? uint8_t((key >> 16) & 0xFFu) : uint8_t(0xFF);
 }
 
-// Every hit's point-light shadow ray from (org, dir, t) -- the operations
-// of shade_pt_point, so the winner's bits -- marked for this rank's any hit.
-__global__ __launch_bounds__(kBlock) void k_rep_shadows(RepSpawnArgs A, const uint32_t* tmin) {
+// the winner of ray j: its key's t and list position are the group's minima
+// (lpmin null: kmin holds the whole 64-bit minimum key); svw = the winner's
+// spawned shadow; *nshadow += this rank's winners' shadows
+__global__ __launch_bounds__(kBlock) void k_rep_win(const uint64_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ tmin,
+                                                    const uint8_t* __restrict__ lpmin,
+                                                    const uint64_t* __restrict__ kmin,
+                                                    const uint8_t* __restrict__ sv, size_t nc,
+                                                    uint8_t* __restrict__ win,
+                                                    uint8_t* __restrict__ svw,
+                                                    unsigned long long* __restrict__ nshadow) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= A.nc) return;
-  const uint32_t i = A.idx_c[j];
-  const uint32_t tb = tmin[j];
-  const bool hit = tb != 0xFFFFFFFFu;
-  const float4 o4 = A.rays[2 * size_t(i)], d4 = A.rays[2 * size_t(i) + 1];
-  float pos[3] = {0.f, 0.f, 0.f}, wi[3] = {0.f, 0.f, 1.f};
-  if (hit) {
-    const float t = __uint_as_float(tb);
-    pos[0] = d4.x * t + o4.x;
-    pos[1] = d4.y * t + o4.y;
-    pos[2] = d4.z * t + o4.z;
-    wi[0] = A.shade10[0] - pos[0];
-    wi[1] = A.shade10[1] - pos[1];
-    wi[2] = A.shade10[2] - pos[2];
-    gnorm3(wi);
+  bool w = false, s = false;
+  if (j < nc) {
+    const uint64_t key = keys[j];
+    w = key != kInsituMissKey &&
+        (lpmin ? (uint32_t(key >> 32) == tmin[j] && uint8_t((key >> 16) & 0xFFu) == lpmin[j])
+               : key == kmin[j]);
+    s = w && sv[j];
+    win[j] = w;
+    svw[j] = s;
   }
-  A.sray[2 * j] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
-  A.sray[2 * j + 1] = make_float4(wi[0], wi[1], wi[2], kInf);
-  A.sflag[j] = hit;
-  A.occ[j] = 0;
+  const uint64_t b = __ballot(s);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(nshadow, (unsigned long long)__popcll(b));
 }
 
-// After the list-position all-reduce: the winner (its t and list position
-// are the minima) shades -- ooc::ShaderPt's spawn rule and light weight.
-__global__ __launch_bounds__(kBlock) void k_rep_shade(RepSpawnArgs A, const uint32_t* tmin,
-                                                      const uint8_t* lpmin) {
+// 64-bit keys: the minimum t bits for the shadow rays
+__global__ __launch_bounds__(kBlock) void k_tmin_from_keys(const uint64_t* __restrict__ kmin,
+                                                           size_t nc, uint32_t* __restrict__ tmin) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  ShadePt sh;
-  for (int k = 0; k < 3; ++k) {
-    sh.lp[k] = A.shade10[k];
-    sh.lr[k] = A.shade10[3 + k];
-    sh.ks[k] = A.shade10[6 + k];
-  }
-  sh.shininess = A.shade10[9];
-  bool spawned = false;
-  if (j < A.nc) {
-    const uint32_t i = A.idx_c[j];
-    const uint64_t key = ((A.mask[i] >> A.rank) & 1ull) ? A.keys_n[i] : kInsituMissKey;
-    const bool win = key != kInsituMissKey && uint32_t(key >> 32) == tmin[j] &&
-                     uint8_t((key >> 16) & 0xFFu) == lpmin[j];
-    float4 sw = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (win) {
-      const float4 o4 = A.rays[2 * size_t(i)], d4 = A.rays[2 * size_t(i) + 1];
-      const float o[3] = {o4.x, o4.y, o4.z}, d[3] = {d4.x, d4.y, d4.z};
-      const spray_rt_hit h = A.hits_n[i];
-      float pos[3], wi[3], L[3];
-      spawned = shade_pt_point(o, d, h, sh, pos, wi, L);
-      sw = make_float4(L[0], L[1], L[2], 0.f);
-      if (A.hit_c) A.hit_c[j] = h;
-    }
-    A.win[j] = win;
-    A.svalid[j] = spawned;
-    A.sw[j] = sw;
-    A.pix_c[j] = A.pix[i];
-    A.sam_c[j] = A.sam[i];
-  }
-  const uint64_t b = __ballot(spawned);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(A.nshadow, (unsigned long long)__popcll(b));
+  if (j >= nc) return;
+  const uint64_t k = kmin[j];
+  tmin[j] = k != kInsituMissKey ? uint32_t(k >> 32) : 0xFFFFFFFFu;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_i32(const uint32_t* __restrict__ idx, size_t n,
+                                                       const int32_t* __restrict__ src,
+                                                       int32_t* __restrict__ dst) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j < n) dst[j] = src[idx[j]];
 }
 }  // namespace
 
@@ -795,29 +718,31 @@ hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, cons
                            int rank, const uint64_t* keys_n, uint64_t* keys_c) {
   LAUNCH(nc, k_rep_keys, idx_c, nc, mask, rank, keys_n, keys_c);
 }
-hipError_t launch_rep_spawn(hipStream_t s, const RepSpawnArgs& a) {
-  LAUNCH(a.nc, k_rep_spawn, a);
-}
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow) {
   k_rep_totals<<<1, 192, 0, s>>>(tail, nrad, nshadow);
   return hipGetLastError();
 }
 
-hipError_t launch_rep_tkeys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
-                            int rank, const uint64_t* keys_n, uint32_t* tk) {
-  LAUNCH(nc, k_rep_tkeys, idx_c, nc, mask, rank, keys_n, tk);
+hipError_t launch_rep_cull(hipStream_t s, const spray_rt_ray* rays, size_t n, const SceneBox& b,
+                           uint8_t* fc) {
+  LAUNCH(n, k_rep_cull, reinterpret_cast<const float4*>(rays), n, b, fc);
 }
-hipError_t launch_rep_lpos(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
-                           int rank, const uint64_t* keys_n, const uint32_t* tmin, uint8_t* lp) {
-  LAUNCH(nc, k_rep_lpos, idx_c, nc, mask, rank, keys_n, tmin, lp);
+hipError_t launch_rep_lp(hipStream_t s, const uint64_t* keys, const uint32_t* tmin, size_t nc,
+                         uint8_t* lp) {
+  LAUNCH(nc, k_rep_lp, keys, tmin, nc, lp);
 }
-hipError_t launch_rep_shadows(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin) {
-  LAUNCH(a.nc, k_rep_shadows, a, tmin);
+hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* tmin,
+                          const uint8_t* lpmin, const uint64_t* kmin, const uint8_t* sv, size_t nc,
+                          uint8_t* win, uint8_t* svw, unsigned long long* nshadow) {
+  LAUNCH(nc, k_rep_win, keys, tmin, lpmin, kmin, sv, nc, win, svw, nshadow);
 }
-hipError_t launch_rep_shade(hipStream_t s, const RepSpawnArgs& a, const uint32_t* tmin,
-                            const uint8_t* lpmin) {
-  LAUNCH(a.nc, k_rep_shade, a, tmin, lpmin);
+hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc, uint32_t* tmin) {
+  LAUNCH(nc, k_tmin_from_keys, kmin, nc, tmin);
+}
+hipError_t launch_gather_i32(hipStream_t s, const uint32_t* idx, size_t n, const int32_t* src,
+                             int32_t* dst) {
+  LAUNCH(n, k_gather_i32, idx, n, src, dst);
 }
 hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
                             uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,

@@ -174,6 +174,19 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
                                  const spray_rt_hit* hits, const int32_t* pixid, size_t M,
                                  int nsamples, size_t npix, uint32_t* out_pairs, float* lv,
                                  float* rec, uint32_t* d_count, void* scratch);
+// Replicated in-situ frames: slot j traces eye ray idx[j] (< n), j < nc,
+// results at j.  Keyed closest hit over the resident domains (keys: 64-bit
+// composite, tkeys: t bits, 0xFFFFFFFF for none) with the point-light
+// shading of the own hit (sw float4, sv); hits optional (null: none).
+hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                  size_t n, const uint32_t* idx, size_t nc,
+                                  const float* shade10, spray_rt_hit* hits, uint64_t* keys,
+                                  uint32_t* tkeys, float* sw, uint8_t* sv);
+// ... and the any hit of the point-light shadow ray of the hit at t bits
+// tmin[j] (none: 0xFFFFFFFF, occ[j] untouched) over the resident domains
+hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                    size_t n, const uint32_t* idx, size_t nc,
+                                    const uint32_t* tmin, const float* shade10, uint8_t* occ);
 // any hit of those pairs' AO rays, each generated in its any-hit lane
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,

@@ -285,6 +285,11 @@ struct SceneArgs {
   const float4* ao_rec;  // per source ray: (origin, pixel), normal, tangent frame
   const float4* ao_lv;   // local hemisphere sample of (pixel, l) at pixel * ao_ns + l
   int ao_ns;
+  // replicated frames: t bits per slot (kEpiKeysShade), the group's minimum
+  // t bits per slot (kEpiShadowGen; 0xFFFFFFFF: no hit)
+  uint32_t* tkeys;
+  const uint32_t* tmin;
+  size_t nrays;  // index lists: ray ids idx[j] < nrays (0: < M)
   // shadow pool of the fused launch (SPRAY_SHADOW_POOL): launch generation
   uint32_t pool_gen;
 };
@@ -318,6 +323,15 @@ constexpr int kEpiShadow = 3; // + PT spawn and the shadow ray's any hit, same l
 constexpr int kEpiShadowFrame = 4;
 // any hit of AO rays generated in the lane from (source ray, sample) pairs
 constexpr int kEpiAoGen = 5;
+// replicated in-situ frames (insitu.cpp trace_replicated): slot j traces ray
+// idx[j] and writes its results at j.  kEpiKeysShade: the keyed closest hit
+// over the rank's domains + the t bits (tkeys) + the point-light shading of
+// the rank's own hit (sw / sh_valid, shade_pt_point); kEpiShadowGen (any
+// hit): the shadow ray of the group's minimum t (tmin), built in the lane
+// with shade_pt_point's operations, occ[j].
+constexpr int kEpiKeysShade = 6;
+constexpr int kEpiShadowGen = 7;
+constexpr bool rep_epi(int e) { return e == kEpiKeysShade || e == kEpiShadowGen; }
 
 // Band q of M rays = [q*S, min((q+1)*S, M)), S = band_size(M): one work
 // queue of the persistent launches; bands 8x .. 8x+7 (a contiguous eighth of
@@ -831,8 +845,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 #pragma unroll
   for (int w = 0; w < W; ++w) m[w] = 0;
   if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
-  uint64_t m0[EPI == kEpiKeys ? W : 1];
-  if (EPI == kEpiKeys) {
+  constexpr bool kKeys = EPI == kEpiKeys || EPI == kEpiKeysShade;
+  uint64_t m0[kKeys ? W : 1];
+  if (kKeys) {
 #pragma unroll
     for (int w = 0; w < W; ++w) m0[w] = m[w];
   }
@@ -947,7 +962,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   // instructions (WRITE_SIZE 1.25x the records).
   const size_t i0 = size_t(__builtin_amdgcn_readfirstlane(uint32_t(i))) |
                     (size_t(__builtin_amdgcn_readfirstlane(uint32_t(i >> 32))) << 32);
-  if (SPRAY_HIT_TRANSPOSE && (i0 & 63) == 0 &&
+  if (EPI == kEpiKeysShade && !A.hits) {
+    // no hit records (the replicated frame keeps keys and shading only)
+  } else if (SPRAY_HIT_TRANSPOSE && (i0 & 63) == 0 &&
       __ballot(valid && i == i0 + size_t(lane)) == ~0ull) {
     const float hv[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
                           h2.x, h2.y, h2.z, h2.w};
@@ -982,7 +999,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     }
   }
   if (!valid) return;
-  if (EPI == kEpiKeys) {
+  if (kKeys) {
     uint64_t key = 0x7FFFFFFFFFFFFFFFull;
     if (best_dom >= 0) {  // position of best_dom in the ray's sorted list
       const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
@@ -1005,6 +1022,23 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
             uint64_t(best_dom);
     }
     A.keys[i] = key;
+    if (EPI == kEpiKeysShade) {
+      A.tkeys[i] = best_dom >= 0 ? __float_as_uint(best.t) : 0xFFFFFFFFu;
+      bool sp = false;
+      if (best_dom >= 0) {
+        spray_rt_hit h;
+        h.t = h0.x;
+        h.color = __float_as_uint(h1.w);
+        h.ns[0] = h2.x;
+        h.ns[1] = h2.y;
+        h.ns[2] = h2.z;
+        const float d3[3] = {d4.x, d4.y, d4.z}, o3[3] = {o4.x, o4.y, o4.z};
+        float L[3];
+        sp = shade_pt_point(o3, d3, h, A.shade, pos, wi, L);
+        if (sp) A.sw[i] = make_float4(L[0], L[1], L[2], 0.f);
+      }
+      A.sh_valid[i] = sp;
+    }
   }
   if (EPI == kEpiShadowFrame && best_dom >= 0) {
     spray_rt_hit h;
@@ -1035,6 +1069,40 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     ray.dir[2] = d4.z;
     spawn = shadow_pt(ray, h, A.shade, pos, wi);
   }
+}
+
+// The ray slot j of a replicated-frame launch traces (rep_epi): eye ray
+// idx[j] (kEpiKeysShade), or the point-light shadow ray of the group's
+// minimum t of it (kEpiShadowGen: RTCRayUtil::hitPosition + PointLight::
+// sample, the operations of shade_pt_point / k_rep_shadows, so the bits of
+// the winner's own shadow ray); false: no ray (no hit anywhere).
+template <int EPI>
+__device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, bool ok,
+                                        float* r6) {
+  if (!ok) return false;
+  const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
+  const float4 o4 = rp[0], d4 = rp[1];
+  if (EPI == kEpiKeysShade) {
+    r6[0] = o4.x;
+    r6[1] = o4.y;
+    r6[2] = o4.z;
+    r6[3] = d4.x;
+    r6[4] = d4.y;
+    r6[5] = d4.z;
+    return true;
+  }
+  const uint32_t tb = A.tmin[j];
+  if (tb == 0xFFFFFFFFu) return false;
+  const float t = __uint_as_float(tb);
+  r6[0] = d4.x * t + o4.x;
+  r6[1] = d4.y * t + o4.y;
+  r6[2] = d4.z * t + o4.z;
+  float w[3] = {A.shade.lp[0] - r6[0], A.shade.lp[1] - r6[1], A.shade.lp[2] - r6[2]};
+  gnorm3(w);
+  r6[3] = w[0];
+  r6[4] = w[1];
+  r6[5] = w[2];
+  return true;
 }
 
 // Diagnostic (SPRAY_WAVE_TIMES builds only): per wave of the persistent
@@ -1366,8 +1434,13 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
     const size_t i = (idx && j < M) ? idx[j] : j;
     // an index list entry past the ray buffer is skipped, never read
-    const bool ok = j < M && i < A.M && (!A.valid || A.valid[i]);
-    if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
+    const bool ok = j < M && i < (A.nrays ? A.nrays : A.M) && (!A.valid || A.valid[i]);
+    if constexpr (rep_epi(EPI)) {
+      float r6[6];
+      const bool okr = rep_ray<EPI>(A, j, i, ok, r6);
+      scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
+          A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
+    } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (kSpread)
       scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task, my_hit);
@@ -1387,6 +1460,13 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     // packet instead of kChunk, so the band's last rays spread over many
     // waves instead of waiting in a few waves' hands
     constexpr uint32_t kTail = ANY ? 0u : uint32_t(SPRAY_CHUNK_TAIL);
+    // a batch smaller than kChunk rays per wave (a rank's share of a
+    // replicated frame) is dealt one packet per dequeue: with kChunk the
+    // first waves would take every chunk and walk its packets one after
+    // another while the rest of the grid idles (measured: 331 K rays in 0.24
+    // ms, the latency of four packet walks in a row)
+    const bool small = M < size_t(gridDim.x) * (kBlock / 64) * kChunk;
+    const bool rtc = kTail != 0 || small;
     const uint32_t xcd = xcc_id() & 7u;
     const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
     for (uint32_t k = 0; k < uint32_t(kQueues); ++k) {
@@ -1396,7 +1476,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
       if (begin >= end) continue;
       uint32_t* head = &A.heads[32 * q];
       const auto chunk_at = [&](uint32_t b) -> uint32_t {
-        return (kTail && begin + b + kTail >= end) ? 64u : kChunk;
+        return (small || (kTail && begin + b + kTail >= end)) ? 64u : kChunk;
       };
       uint32_t base = 0, csz = kChunk;
       if (lane == 0) {
@@ -1407,17 +1487,17 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
         }
       }
       base = __builtin_amdgcn_readfirstlane(base);
-      csz = kTail ? __builtin_amdgcn_readfirstlane(csz) : kChunk;
+      csz = rtc ? __builtin_amdgcn_readfirstlane(csz) : kChunk;
       while (begin + base < end) {
         // the next chunk is dequeued before this one is traced: the atomic's
         // latency overlaps the traversal
         uint32_t next = 0, ncsz = kChunk;
         if (SPRAY_DEQ_AHEAD == 1 && lane == 0) next = atomicAdd(head, kChunk);
         const size_t cbeg = begin + base;
-        for (uint32_t c = 0; c < (kTail ? csz : kChunk); c += 64) {
+        for (uint32_t c = 0; c < (rtc ? csz : kChunk); c += 64) {
           const size_t j = cbeg + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
-          const bool ok = j < end && i < A.M && (!A.valid || A.valid[i]);
+          const bool ok = j < end && i < (A.nrays ? A.nrays : A.M) && (!A.valid || A.valid[i]);
           flag = false;
 #if SPRAY_WAVE_TIMES
           const unsigned long long pt0 = wall_clock64();
@@ -1426,15 +1506,18 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             // the next chunk is dequeued by the chunk's last packet once its
             // rays have landed: the atomic overlaps that packet's walk, and
             // no chunk waits in a wave's hands while another is traced
-            const bool last = c + 64 >= (kTail ? csz : kChunk);
+            const bool last = c + 64 >= (rtc ? csz : kChunk);
             // ray prefetch: this packet's rays came into LDS during the
             // previous packet (not the chunk's first); the next packet's are
             // copied while this one is walked
             const bool pre = kPre && !idx && !A.valid;
             const bool have = pre && c > 0;
             if (have) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            scene_ray_packet<W, ANY, EPI>(
-                A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi, nullptr,
+            float r6[6];
+            const bool okr = rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, r6) : ok;
+            scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
+                A, rep_epi(EPI) ? j : i, okr, stl, sbox, sdom, wstk, flag, pos, wi,
+                rep_epi(EPI) ? r6 : nullptr,
                 [&]() {
                   if (last && lane == 0) {
                     ncsz = chunk_at(base + csz);
@@ -1481,7 +1564,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           next = atomicAdd(head, ncsz);
         }
         base = __builtin_amdgcn_readfirstlane(next);
-        if (kTail) csz = __builtin_amdgcn_readfirstlane(ncsz);
+        if (rtc) csz = __builtin_amdgcn_readfirstlane(ncsz);
         ++wchunks;
       }
     }
@@ -2387,6 +2470,8 @@ static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherenc
   // generated AO rays (hemispheres) walk per lane
   if constexpr (ANY && EPI == kEpiAoGen) {
     return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
+  } else if constexpr (rep_epi(EPI)) {  // camera rays and point-light shadows
+    return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
   } else if constexpr (!ANY && EPI != kEpiNone) {
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
   } else {
@@ -2424,6 +2509,17 @@ static SceneArgs scene_args(const SceneView& v, const spray_rt_ray* rays, size_t
   a.rays = rays;
   a.M = M;
   return a;
+}
+
+static ShadePt shade_from10(const float* s10) {
+  ShadePt sh{};
+  for (int k = 0; k < 3; ++k) {
+    sh.lp[k] = s10[k];
+    sh.lr[k] = s10[3 + k];
+    sh.ks[k] = s10[6 + k];
+  }
+  sh.shininess = s10[9];
+  return sh;
 }
 
 hipError_t launch_scene_intersect(hipStream_t s, const SceneView& v,
@@ -2762,6 +2858,36 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
   k_spawn_ao_index<<<g, kBlock, 0, s>>>(uint32_t(M), uint32_t(nsamples), meta, tiles,
                                         out_pairs, pixid, reinterpret_cast<float4*>(lv));
   return hipGetLastError();
+}
+
+hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                  size_t n, const uint32_t* idx, size_t nc,
+                                  const float* shade10, spray_rt_hit* hits, uint64_t* keys,
+                                  uint32_t* tkeys, float* sw, uint8_t* sv) {
+  if (nc == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, nc);
+  a.nrays = n;
+  a.idx = idx;
+  a.hits = hits;
+  a.keys = keys;
+  a.tkeys = tkeys;
+  a.sw = reinterpret_cast<float4*>(sw);
+  a.sh_valid = sv;
+  a.shade = shade_from10(shade10);
+  return launch_scene_w<false, kEpiKeysShade>(s, a, v);
+}
+
+hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
+                                    size_t n, const uint32_t* idx, size_t nc,
+                                    const uint32_t* tmin, const float* shade10, uint8_t* occ) {
+  if (nc == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, rays, nc);
+  a.nrays = n;
+  a.idx = idx;
+  a.tmin = tmin;
+  a.occ = occ;
+  a.shade = shade_from10(shade10);
+  return launch_scene_w<true, kEpiShadowGen>(s, a, v);
 }
 
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
