@@ -58,7 +58,7 @@ echo done
 # rocprof kernel trace of one rehearsal configuration (REHPROF="world mode kind")
 if [ -n "${REHPROF:-}" ]; then
   set -- $REHPROF
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rehprof" -o run -- python -u scripts/insitu_rep_rehearse.py --worlds $1 --modes $2 --kinds $3 --frames 3 --rccl-floor 0 --out "$OUT/rehprof.json" > "$OUT/rehprof.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/rehprof" -o "%pid%/run" -- python -u scripts/insitu_rep_rehearse.py --worlds $1 --modes $2 --kinds $3 --frames 3 --rccl-floor 0 --out "$OUT/rehprof.json" > "$OUT/rehprof.log" 2>&1
   rc=$?; echo "rehprof rc=$rc"
   [ $rc -ne 0 ] && fail rehprof $rc "$OUT/rehprof.log"
 fi

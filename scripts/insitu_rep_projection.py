@@ -14,10 +14,11 @@ Inputs
 * the measured N = 1 frame (the bench's fused single-GPU frame, --n1-ms).
 
 Model of one frame at N ranks (every rank runs the same sequence):
-  PT: T = max_r(route + select + keyed closest hit + key prep) + AR(4 |C|)
-          + max_r(shadow trace + shade) + AR(|C| + 192) + max_r(film + totals)
-          + RED(12 runs)   (t bits MIN; the list positions' u8 MIN overlaps the
-          shadow any hit; runs = the pixel runs along C, their sums to rank 0)
+  PT: T = max_r(cull + select + film slots + keyed closest hit & shading)
+          + AR(4 |C'|) + max_r(list positions + shadow any hit + winners)
+          + AR(|C'| + 192) + max_r(film + totals) + RED(12 runs)
+          (C' = rays entering the scene box; t bits MIN; the list positions'
+          u8 MIN overlaps the shadow any hit; runs = the pixel runs along C')
   AO: T = max_r(route + select + keyed closest hit) + AR(8 |C|) + max_r(publish)
           + AR(16 |C|) + max_r(AO spawn + any hit) + AR(2 fb |C|)
           + max_r(film + totals)  (fb = 2 / 4 / 8 bits for N <= 3 / 15 / 64;
@@ -52,7 +53,7 @@ def fbits(n):
 
 
 SEGMENTS = {  # phases between the frame's collectives, in order
-    "pt": [("route", "select", "keyed_closest_hit", "key_prep"), ("shadow_trace", "shade"),
+    "pt": [("cull_select", "film_slots", "keyed_shade"), ("list_pos", "shadow_trace", "winners"),
            ("film_totals",)],
     "ao": [("route", "select", "keyed_closest_hit"), ("publish",), ("ao_spawn", "ao_trace"),
            ("film_totals",)],

@@ -1460,12 +1460,12 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     // packet instead of kChunk, so the band's last rays spread over many
     // waves instead of waiting in a few waves' hands
     constexpr uint32_t kTail = ANY ? 0u : uint32_t(SPRAY_CHUNK_TAIL);
-    // a batch smaller than kChunk rays per wave (a rank's share of a
-    // replicated frame) is dealt one packet per dequeue: with kChunk the
-    // first waves would take every chunk and walk its packets one after
-    // another while the rest of the grid idles (measured: 331 K rays in 0.24
-    // ms, the latency of four packet walks in a row)
-    const bool small = M < size_t(gridDim.x) * (kBlock / 64) * kChunk;
+    // a batch of fewer than four kChunk chunks per wave (a rank's share of
+    // a replicated frame) is dealt one packet per dequeue: with kChunk a few
+    // waves take two chunks and walk their packets one after another while
+    // the rest of the grid idles (measured: 331 K rays in 0.24 ms, the
+    // latency of four packet walks in a row)
+    const bool small = M < size_t(gridDim.x) * (kBlock / 64) * kChunk * 4;
     const bool rtc = kTail != 0 || small;
     const uint32_t xcd = xcc_id() & 7u;
     const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;

@@ -305,8 +305,8 @@ class InsituEngine:
         self.rt._check(lib().spray_rt_insitu_set_timing(self.h, 1 if on else 0), "set_timing")
 
     # replicated-ray frames (insitu.cpp trace_replicated / trace_replicated_ao)
-    REP_PHASES = ("route", "select", "keyed_closest_hit", "key_prep", "shadow_trace", "shade",
-                  "film_totals")
+    REP_PHASES = ("cull_select", "film_slots", "keyed_shade", "list_pos", "shadow_trace",
+                  "winners", "film_totals")
     REP_AO_PHASES = ("route", "select", "keyed_closest_hit", "publish", "ao_spawn", "ao_trace",
                      "film_totals")
     _rep_kind = "pt"
