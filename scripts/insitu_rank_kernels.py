@@ -83,6 +83,26 @@ def main():
     report = {"n_rays": n, "n_shadow": int(nsh.item()), "n1_fused_ms": round(t_fused, 4),
               "runs": []}
     print("N=1 fused launch %.3f ms, %d shadow rays" % (t_fused, int(nsh.item())), flush=True)
+    # C' (rays entering the scene box) gathered: keyed closest hit over it
+    # with every domain resident vs. each rank's domains only
+    lo = torch.tensor(boxes[:, :3].min(0), dtype=torch.float32, device="cuda")
+    hi = torch.tensor(boxes[:, 3:].max(0), dtype=torch.float32, device="cuda")
+    o, dr = rays[:, 0:3], rays[:, 4:7]
+    inv = 1.0 / dr
+    neg = inv < 0
+    tmn = ((torch.where(neg, hi, lo) - o) * inv).max(dim=1).values
+    tmx = ((torch.where(neg, lo, hi) - o) * inv).min(dim=1).values
+    cp = rays[((tmn <= tmx) & (tmn < float("inf")) & (tmx > 0.001)) | (dr == 0).any(dim=1)]
+    cp = cp.contiguous()
+    ncp = cp.shape[0]
+    ch = torch.empty((ncp, 12), dtype=torch.float32, device="cuda")
+    ck = torch.empty(ncp, dtype=torch.int64, device="cuda")
+    t_full_keyed = timed(lambda: full.intersect_scene_keyed(cp, ch, ck))
+    t_full_ch = timed(lambda: full.intersect_scene(cp, ch))
+    report["cprime"] = {"n": ncp, "full_keyed_ms": round(t_full_keyed, 4),
+                        "full_ch_ms": round(t_full_ch, 4)}
+    print("C' %d rays: all domains keyed %.3f ms, plain CH %.3f ms" % (ncp, t_full_keyed, t_full_ch),
+          flush=True)
     for world in args.worlds:
         for mode in args.modes:
             pm = insitu.PARTITION_ROUND_ROBIN if mode == "rr" else insitu.PARTITION_GROUP_CLOSE
@@ -104,10 +124,14 @@ def main():
                 t_keyed = timed(lambda: rt.intersect_scene_keyed(lr, lh, lk)) if nl else 0.0
                 so = torch.empty(n, dtype=torch.uint8, device="cuda")
                 t_sh = timed(lambda: rt.occluded_scene_masked(srays, svalid, so))
+                t_ck = timed(lambda: rt.intersect_scene_keyed(cp, ch, ck))
+                t_cc = timed(lambda: rt.intersect_scene(cp, ch))
                 ranks.append({"rank": r, "L": nl, "C": int(on.sum()), "route_ms": round(t_route, 4),
-                              "keyed_ms": round(t_keyed, 4), "shadow_ms": round(t_sh, 4)})
-                print("N=%d %s rank %d: L %d route %.3f keyed %.3f shadow %.3f ms" % (
-                    world, mode, r, nl, t_route, t_keyed, t_sh), flush=True)
+                              "keyed_ms": round(t_keyed, 4), "shadow_ms": round(t_sh, 4),
+                              "cprime_keyed_ms": round(t_ck, 4), "cprime_ch_ms": round(t_cc, 4)})
+                print("N=%d %s rank %d: L %d route %.3f keyed(L) %.3f shadow %.3f keyed(C') %.3f "
+                      "CH(C') %.3f ms" % (world, mode, r, nl, t_route, t_keyed, t_sh, t_ck, t_cc),
+                      flush=True)
                 rt.close()
             report["runs"].append({"world": world, "partition": mode, "ranks": ranks})
     if args.out:

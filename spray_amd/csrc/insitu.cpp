@@ -998,6 +998,11 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   if (rec) GROW(I->rhit_c, nc * 48 + 48);
   uint64_t* keys = I->rkeys_c.as<uint64_t>();
   uint32_t* tk = I->rtk.as<uint32_t>();
+  // lanes whose ray enters no resident domain are not walked: their results
+  // prefilled (a miss, no shading)
+  HIPCHK(c, launch_fill_u64(s, keys, nc, kInsituMissKey));
+  HIPCHK(c, hipMemsetAsync(tk, 0xFF, nc * 4, s));
+  HIPCHK(c, hipMemsetAsync(I->rsvalid.p, 0, nc, s));
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
                                    I->rsw.as<float>(), I->rsvalid.as<uint8_t>()));

@@ -1076,9 +1076,14 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 // minimum t of it (kEpiShadowGen: RTCRayUtil::hitPosition + PointLight::
 // sample, the operations of shade_pt_point / k_rep_shadows, so the bits of
 // the winner's own shadow ray); false: no ray (no hit anywhere).
+// A lane whose ray enters none of the resident domains' boxes (the exact
+// test of the top-level tree's leaves: its list holds no domain of this
+// rank) is dropped before any walk; its outputs keep their prefilled
+// values (a miss, no shadow ray).
 template <int EPI>
 __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, bool ok,
-                                        float* r6) {
+                                        float* r6, const float* sbox, const uint8_t* sres,
+                                        int nres) {
   if (!ok) return false;
   const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
   const float4 o4 = rp[0], d4 = rp[1];
@@ -1089,20 +1094,25 @@ __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, 
     r6[3] = d4.x;
     r6[4] = d4.y;
     r6[5] = d4.z;
-    return true;
+  } else {
+    const uint32_t tb = A.tmin[j];
+    if (tb == 0xFFFFFFFFu) return false;
+    const float t = __uint_as_float(tb);
+    r6[0] = d4.x * t + o4.x;
+    r6[1] = d4.y * t + o4.y;
+    r6[2] = d4.z * t + o4.z;
+    float w[3] = {A.shade.lp[0] - r6[0], A.shade.lp[1] - r6[1], A.shade.lp[2] - r6[2]};
+    gnorm3(w);
+    r6[3] = w[0];
+    r6[4] = w[1];
+    r6[5] = w[2];
   }
-  const uint32_t tb = A.tmin[j];
-  if (tb == 0xFFFFFFFFu) return false;
-  const float t = __uint_as_float(tb);
-  r6[0] = d4.x * t + o4.x;
-  r6[1] = d4.y * t + o4.y;
-  r6[2] = d4.z * t + o4.z;
-  float w[3] = {A.shade.lp[0] - r6[0], A.shade.lp[1] - r6[1], A.shade.lp[2] - r6[2]};
-  gnorm3(w);
-  r6[3] = w[0];
-  r6[4] = w[1];
-  r6[5] = w[2];
-  return true;
+  const DRay dr = make_dray(r6[0], r6[1], r6[2], r6[3], r6[4], r6[5]);
+  for (int k = 0; k < nres; ++k) {
+    float tm;
+    if (aabb_ref(sbox + 6 * int(sres[k]), dr, tm)) return true;
+  }
+  return false;
 }
 
 // Diagnostic (SPRAY_WAVE_TIMES builds only): per wave of the persistent
@@ -1412,6 +1422,18 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < A.ndom; k += kBlock) sdom[k] = ld4(A.domtrav, k);
+  // replicated frames: the resident domains, whose boxes cull the lanes
+  __shared__ uint8_t sres[rep_epi(EPI) ? 64 * W : 1];
+  __shared__ int nres;
+  if (rep_epi(EPI)) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int k = 0;
+      for (int d = 0; d < A.ndom; ++d)
+        if (__float_as_uint(sdom[d].x) | __float_as_uint(sdom[d].y)) sres[k++] = uint8_t(d);
+      nres = k;
+    }
+  }
   __syncthreads();
   if (SPRAY_WAVE_TIMES) wt1 = wall_clock64();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
@@ -1437,7 +1459,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     const bool ok = j < M && i < (A.nrays ? A.nrays : A.M) && (!A.valid || A.valid[i]);
     if constexpr (rep_epi(EPI)) {
       float r6[6];
-      const bool okr = rep_ray<EPI>(A, j, i, ok, r6);
+      const bool okr = rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres);
       scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
           A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
@@ -1514,7 +1536,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             const bool have = pre && c > 0;
             if (have) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             float r6[6];
-            const bool okr = rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, r6) : ok;
+            const bool okr = rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres) : ok;
             scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
                 A, rep_epi(EPI) ? j : i, okr, stl, sbox, sdom, wstk, flag, pos, wi,
                 rep_epi(EPI) ? r6 : nullptr,
