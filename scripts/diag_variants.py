@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 DIAG = os.path.join(ROOT, "spray_amd", "lib", "diag")
 VARIANTS = {"mask_only": ["SPRAY_DIAG_MODE=1"], "mask_select": ["SPRAY_DIAG_MODE=2"],
             "ah_spread": ["SPRAY_AH_SPREAD=1"], "ao_refill": ["SPRAY_AO_REFILL=32"]}
-CHECKED = ("ah_spread", "ao_refill")  # bit-exact variants: parity tests apply
+CHECKED = ("ah_spread", "ao_refill", "aogroup", "aogroup6")  # bit-exact variants: parity tests apply
 EXTRA = dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a)  # name=DEF1,DEF2
 
 
