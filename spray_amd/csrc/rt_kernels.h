@@ -188,10 +188,12 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
                                     size_t n, const uint32_t* idx, size_t nc,
                                     const uint32_t* tmin, const float* shade10, uint8_t* occ);
 // any hit of those pairs' AO rays, each generated in its any-hit lane
+// cull_own (replicated AO frames): AO rays entering no resident domain's
+// box are not walked (occ 0)
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters);
+                                    unsigned long long* counters, bool cull_own = false);
 size_t ao_scratch_bytes(size_t M, int nsamples);
 
 // ---- out-of-core path (ooc_kernels.hip) ----

@@ -290,6 +290,9 @@ struct SceneArgs {
   uint32_t* tkeys;
   const uint32_t* tmin;
   size_t nrays;  // index lists: ray ids idx[j] < nrays (0: < M)
+  // kEpiAoGen of a replicated frame: AO rays entering none of the resident
+  // domains' boxes are not walked (occ 0)
+  int rep_cull;
   // shadow pool of the fused launch (SPRAY_SHADOW_POOL): launch generation
   uint32_t pool_gen;
 };
@@ -366,6 +369,19 @@ __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f
   hemisphere_apply(lv, N, ax, ay, w, pdf);
   a = v4f{op.x, op.y, op.z, kRayEpsilon};
   b = v4f{w[0], w[1], w[2], kInf};
+}
+
+// whether AO ray k enters a resident domain's box (replicated AO frames)
+__device__ __forceinline__ bool ao_own(const SceneArgs& A, size_t k, const float* sbox,
+                                       const uint8_t* sres, int nres) {
+  v4f a, b;
+  ao_gen(A, k, a, b);
+  const DRay dr = make_dray(a.x, a.y, a.z, b.x, b.y, b.z);
+  for (int q = 0; q < nres; ++q) {
+    float tm;
+    if (aabb_ref(sbox + 6 * int(sres[q]), dr, tm)) return true;
+  }
+  return false;
 }
 
 template <int W, bool ANY, bool COUNT, int EPI, int STK>
@@ -1423,9 +1439,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < A.ndom; k += kBlock) sdom[k] = ld4(A.domtrav, k);
   // replicated frames: the resident domains, whose boxes cull the lanes
-  __shared__ uint8_t sres[rep_epi(EPI) ? 64 * W : 1];
+  constexpr bool kRes = rep_epi(EPI) || EPI == kEpiAoGen;
+  __shared__ uint8_t sres[kRes ? 64 * W : 1];
   __shared__ int nres;
-  if (rep_epi(EPI)) {
+  if (kRes && (rep_epi(EPI) || A.rep_cull)) {
     __syncthreads();
     if (threadIdx.x == 0) {
       int k = 0;
@@ -1464,6 +1481,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+    else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
+      A.occ[i] = 0;
     else if (kSpread)
       scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task, my_hit);
     else if (kGroup)
@@ -1564,6 +1583,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
                 have ? my_pre : nullptr);
           } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+          else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
+            A.occ[i] = 0;
           else if (kSpread)
             scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task,
                                              my_hit);
@@ -2915,9 +2936,10 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters) {
+                                    unsigned long long* counters, bool cull_own) {
   if (max_n == 0) return hipSuccess;
   SceneArgs a = scene_args(v, nullptr, max_n);
+  a.rep_cull = cull_own ? 1 : 0;
   a.d_count = d_count;
   a.occ = occ;
   a.counters = counters;
