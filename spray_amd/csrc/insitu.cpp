@@ -171,7 +171,7 @@ struct spray_rt_insitu {
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
   // split keys: t bits and list positions over C; the list positions'
   // all-reduce runs on a second stream (cs) beside the shadow any hit
-  DBuf rtk, rlp, rbmax;
+  DBuf rtk, rlp, rbmax, rtk2, rtstar;
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
   // phase timing (spray_rt_insitu_set_timing): events on the stream
@@ -853,6 +853,16 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
 }
 
 // SPRAY_INSITU_SPLIT_KEYS=0: the replicated PT frame's 64-bit key MIN
+// SPRAY_INSITU_ROUNDS=2: the replicated PT frame's keyed walk in two rounds
+// (first list entries, then the later ones below the round-1 minimum)
+int key_rounds() {
+  static const int r = [] {
+    const char* e = std::getenv("SPRAY_INSITU_ROUNDS");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return r;
+}
+
 bool split_keys() {
   static const bool on = [] {
     const char* e = std::getenv("SPRAY_INSITU_SPLIT_KEYS");
@@ -1000,24 +1010,48 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   uint32_t* tk = I->rtk.as<uint32_t>();
   // lanes whose ray enters no resident domain are not walked: their results
   // prefilled (a miss, no shading)
+  const bool split = split_keys() && c->ndom <= 255;
+  const int rounds = split ? key_rounds() : 1;
   HIPCHK(c, launch_fill_u64(s, keys, nc, kInsituMissKey));
   HIPCHK(c, hipMemsetAsync(tk, 0xFF, nc * 4, s));
   HIPCHK(c, hipMemsetAsync(I->rsvalid.p, 0, nc, s));
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
-                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>()));
+                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
+                                   rounds == 2 ? 1 : 0));
+  // two rounds: the group's round-1 minimum, then the later entries below it
+  uint64_t* keys2 = nullptr;
+  uint32_t* tk2 = nullptr;
+  uint32_t* tstar = tk;  // the winning t of every ray (the shadow rays' origin)
+  if (rounds == 2) {
+    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
+    GROW(I->rkeys_n, nc * 8 + 8);
+    GROW(I->rtk2, nc * 4 + 4);
+    GROW(I->rtstar, nc * 4 + 4);
+    keys2 = I->rkeys_n.as<uint64_t>();
+    tk2 = I->rtk2.as<uint32_t>();
+    HIPCHK(c, launch_fill_u64(s, keys2, nc, kInsituMissKey));
+    HIPCHK(c, hipMemsetAsync(tk2, 0xFF, nc * 4, s));
+    HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
+                                     rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys2, tk2,
+                                     I->rsw.as<float>(), I->rsvalid.as<uint8_t>(), 2, tk));
+  }
   // ---- 4. the group's minimum t of every ray of C' (then the list
   // position at that t) -- split while list positions fit a byte, else the
   // 64-bit keys' MIN
-  const bool split = split_keys() && c->ndom <= 255;
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
   if (split) {
-    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
+    uint32_t* tm = rounds == 2 ? tk2 : tk;
+    if (nc) COMM(I->tr->allreduce_min_u32(I, tm, nc));
     MARK(3);
     GROW(I->rlp, nc + 1);
     lp = I->rlp.as<uint8_t>();
-    HIPCHK(c, launch_rep_lp(s, keys, tk, nc, lp));
+    HIPCHK(c, launch_rep_lp(s, rounds == 2 ? keys2 : keys, tm, nc, lp));
+    if (rounds == 2) {
+      tstar = I->rtstar.as<uint32_t>();
+      HIPCHK(c, launch_min_u32(s, tk, tk2, nc, tstar));
+    }
     if (nc) {
       if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
       if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
@@ -1043,7 +1077,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   MARK(4);
   GROW(I->rocc, nc + 192);
   HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nc, s));
-  HIPCHK(c, launch_scene_rep_shadows(s, view(c), rays, n, idx_c, nc, tk, shade10,
+  HIPCHK(c, launch_scene_rep_shadows(s, view(c), rays, n, idx_c, nc, tstar, shade10,
                                      I->rocc.as<uint8_t>()));
   // ---- 6. the winners (after the list positions' MIN), their shadows
   // counted behind the occlusion bytes: rank 0 counts the frame's radiance
@@ -1054,9 +1088,14 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   GROW(I->rnsh, 8);
   HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, 8, s));
   if (split && nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
-  HIPCHK(c, launch_rep_win(s, keys, tk, lp, kmin, I->rsvalid.as<uint8_t>(), nc,
-                           I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
-                           I->rnsh.as<unsigned long long>()));
+  if (rounds == 2)
+    HIPCHK(c, launch_rep_win2(s, keys, tk, keys2, tk2, lp, I->rsvalid.as<uint8_t>(), nc,
+                              I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
+                              I->rnsh.as<unsigned long long>()));
+  else
+    HIPCHK(c, launch_rep_win(s, keys, tk, lp, kmin, I->rsvalid.as<uint8_t>(), nc,
+                             I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
+                             I->rnsh.as<unsigned long long>()));
   HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nc, I->rank == 0 ? n : 0,
                               I->rnsh.as<unsigned long long>()));
   // ---- 7. occlusion OR (a byte SUM) + totals
@@ -1067,7 +1106,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   HIPCHK(c, hipEventSynchronize(I->ev_np));  // long done: the scan ran before the keyed launch
   const size_t np = nc ? *h_np : 0;
   // the all-reduces' and the reduce's payload
-  const size_t pay = (split ? 5 * nc : 8 * nc) + nc + 192 + 12 * np;
+  const size_t pay = (split ? 5 * nc : 8 * nc) + (rounds == 2 ? 4 * nc : 0) + nc + 192 + 12 * np;
   I->st[0] += pay;
   I->st[1] += pay;
   if (np) {
@@ -1222,7 +1261,8 @@ void free_all(spray_rt_insitu* I) {
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rheads, &I->rincl, &I->rscan_tmp,
-                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax};
+                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax, &I->rtk2,
+                 &I->rtstar};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)

@@ -293,6 +293,9 @@ struct SceneArgs {
   // kEpiAoGen of a replicated frame: AO rays entering none of the resident
   // domains' boxes are not walked (occ 0)
   int rep_cull;
+  // kEpiKeysShade rounds: 0 = every resident entry of the lane's list; 1 =
+  // its first entry only; 2 = the later entries below the round-1 minimum
+  int rround;
   // shadow pool of the fused launch (SPRAY_SHADOW_POOL): launch generation
   uint32_t pool_gen;
 };
@@ -869,6 +872,43 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   }
   Best best{ANY ? 0.f : d4.w, 0xFFFFFFFFu, 0xFFFFFFFFu};
   int best_dom = -1;
+  // replicated frames in two rounds (A.rround): 1 = the lane's first list
+  // entry only (when resident); 2 = the later entries, cut at the group's
+  // round-1 minimum t (A.tmin: an earlier entry holds it, so a later one
+  // wins only when strictly nearer -- best_dom -2 stands for that entry)
+  if (EPI == kEpiKeysShade && A.rround && valid) {
+    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    int first = -1;
+    float tf = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint64_t bits = m[w];
+      while (bits) {
+        const int jb = __ffsll((long long)bits) - 1;
+        bits &= bits - 1;
+        const int b = 64 * w + jb;
+        float tm;
+        aabb_ref(sbox + 6 * b, dr, tm);
+        if (first < 0 || tm < tf) {  // ascending ids: ties keep the smaller
+          first = b;
+          tf = tm;
+        }
+      }
+    }
+    const bool res = first >= 0 && (__float_as_uint(sdom[first].x) | __float_as_uint(sdom[first].y));
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const uint64_t fb = (first >= 0 && w == (first >> 6)) ? (1ull << (first & 63)) : 0ull;
+      m[w] = A.rround == 1 ? (res ? fb : 0ull) : (m[w] & ~fb);
+    }
+    if (A.rround == 2) {
+      const uint32_t ta = A.tmin[i];
+      if (ta != 0xFFFFFFFFu) {
+        best.t = __uint_as_float(ta);
+        best_dom = -2;
+      }
+    }
+  }
   bool occluded = false;
   for (;;) {
     if (SPRAY_DIAG_MODE == 6) break;  // diagnostic: top-level mask only
@@ -928,12 +968,12 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
         for (int w = 0; w < W; ++w) m[w] = 0;
       }
     } else {
-      Best loc{best_dom < 0 ? d4.w : best.t, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      Best loc{best_dom == -1 ? d4.w : best.t, 0xFFFFFFFFu, 0xFFFFFFFFu};
       bool hit = false;
       trace_tree_packet<false>(nodes, tris, prims, r, o4.w, 0.f, loc, act, hit, wstk);
       if (loc.leaf != 0xFFFFFFFFu) {
-        bool take = best_dom < 0 || loc.t < best.t;
-        if (!take && loc.t == best.t) {  // exact tie: the earlier list entry
+        bool take = best_dom == -1 || loc.t < best.t;
+        if (!take && loc.t == best.t && best_dom >= 0) {  // exact tie: the earlier list entry
           const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
           float tmd, tme;
           aabb_ref(sbox + 6 * d, dr, tmd);
@@ -980,6 +1020,14 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
                     (size_t(__builtin_amdgcn_readfirstlane(uint32_t(i >> 32))) << 32);
   if (EPI == kEpiKeysShade && !A.hits) {
     // no hit records (the replicated frame keeps keys and shading only)
+  } else if (EPI == kEpiKeysShade && A.rround == 2) {
+    // round 2 replaces round 1's record only where it found a nearer hit
+    if (valid && best_dom >= 0) {
+      float4* hp = reinterpret_cast<float4*>(A.hits + i);
+      hp[0] = h0;
+      hp[1] = h1;
+      hp[2] = h2;
+    }
   } else if (SPRAY_HIT_TRANSPOSE && (i0 & 63) == 0 &&
       __ballot(valid && i == i0 + size_t(lane)) == ~0ull) {
     const float hv[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
@@ -1040,6 +1088,8 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     A.keys[i] = key;
     if (EPI == kEpiKeysShade) {
       A.tkeys[i] = best_dom >= 0 ? __float_as_uint(best.t) : 0xFFFFFFFFu;
+      // round 2 keeps round 1's shading where it found nothing nearer
+      if (A.rround == 2 && best_dom < 0) return;
       bool sp = false;
       if (best_dom >= 0) {
         spray_rt_hit h;
@@ -2906,9 +2956,12 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
 hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                   size_t n, const uint32_t* idx, size_t nc,
                                   const float* shade10, spray_rt_hit* hits, uint64_t* keys,
-                                  uint32_t* tkeys, float* sw, uint8_t* sv) {
+                                  uint32_t* tkeys, float* sw, uint8_t* sv, int round,
+                                  const uint32_t* tmin_round1) {
   if (nc == 0) return hipSuccess;
   SceneArgs a = scene_args(v, rays, nc);
+  a.rround = round;
+  a.tmin = tmin_round1;
   a.nrays = n;
   a.idx = idx;
   a.hits = hits;
