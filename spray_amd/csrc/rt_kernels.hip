@@ -296,8 +296,6 @@ struct SceneArgs {
   // kEpiKeysShade rounds: 0 = every resident entry of the lane's list; 1 =
   // its first entry only; 2 = the later entries below the round-1 minimum
   int rround;
-  // shadow pool of the fused launch (SPRAY_SHADOW_POOL): launch generation
-  uint32_t pool_gen;
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -827,16 +825,12 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
                                                  const float4* sdom, int32_t* wstk,
                                                  bool& spawn, float* pos, float* wi,
                                                  const float* rin = nullptr,
-                                                 const Post& post = Post(),
-                                                 const float4* lray = nullptr) {
+                                                 const Post& post = Post()) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int lane = threadIdx.x & 63;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  if (valid && lray) {  // the packet's rays, prefetched into the wave's LDS
-    o4 = lray[2 * lane];
-    d4 = lray[2 * lane + 1];
-  } else if (valid && rin) {
+  if (valid && rin) {
     o4 = make_float4(rin[0], rin[1], rin[2], kRayEpsilon);
     d4 = make_float4(rin[3], rin[4], rin[5], kInf);
   } else if (valid) {
@@ -1197,12 +1191,6 @@ __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, 
 #ifndef SPRAY_DEQ_AHEAD
 #define SPRAY_DEQ_AHEAD 2
 #endif
-// next packet's rays copied global -> LDS (global_load_lds) during the
-// current packet's walk (plain closest-hit launches without index list or
-// mask; 0 = off)
-#ifndef SPRAY_RAY_PREFETCH
-#define SPRAY_RAY_PREFETCH 0
-#endif
 // guided chunk size near a band's end (closest-hit launches; 0 = off)
 #ifndef SPRAY_CHUNK_TAIL
 #define SPRAY_CHUNK_TAIL 0
@@ -1324,97 +1312,6 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
   q.n = rest;
 }
 
-// Shadow pool of the fused launch (SPRAY_SHADOW_POOL=1).  A wave that finds
-// its band queues dry publishes the shadow rays still waiting in its LDS
-// queue (fewer than kShadowT) to a launch-wide pool and then drains the
-// pool as 64-ray any-hit packets together with every other idle wave,
-// instead of tracing its own partial packet alone: the launch's last shadow
-// rays leave as full packets, spread over the waves that are free.  Slots
-// are reserved by an atomic on the tail, written, then flagged with the
-// launch's generation (release); a drainer claims up to 64 reserved slots
-// by a CAS on the head and waits for their flags (acquire).  No wave waits
-// for another wave's progress beyond a reserved slot's write: a drainer
-// that finds the pool empty sleeps briefly and leaves after kPoolIdle empty
-// polls, and a publisher drains what it published itself, so every ray is
-// traced even if no other wave is left.
-#ifndef SPRAY_SHADOW_POOL
-#define SPRAY_SHADOW_POOL 0
-#endif
-#if SPRAY_SHADOW_POOL
-constexpr uint32_t kPoolCap = 1u << 19;  // >= resident waves x 64
-constexpr int kPoolIdle = 64;
-__device__ float4 g_pool_ray[2 * kPoolCap];
-__device__ uint32_t g_pool_ready[kPoolCap];
-__device__ uint32_t g_pool_ctr[64];  // [0] reserved tail, [32] claimed head (zeroed per launch)
-
-template <int W>
-__device__ __forceinline__ void shadow_pool(const SceneArgs& A, const ShadowQueue& q,
-                                            const float4* stl, const float* sbox,
-                                            const float4* sdom, int32_t* wstk) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t gen = A.pool_gen;
-  if (q.n) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&g_pool_ctr[0], q.n);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (lane < q.n) {
-      const uint32_t k = base + lane;  // < kPoolCap: the host sizes the grid
-      g_pool_ray[2 * k] =
-          make_float4(q.ray[6 * lane], q.ray[6 * lane + 1], q.ray[6 * lane + 2],
-                      __uint_as_float(q.src[lane]));
-      g_pool_ray[2 * k + 1] =
-          make_float4(q.ray[6 * lane + 3], q.ray[6 * lane + 4], q.ray[6 * lane + 5], 0.f);
-      __hip_atomic_store(&g_pool_ready[k], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  int idle = 0;
-  for (;;) {
-    uint32_t h = 0, n = 0;
-    if (lane == 0) {
-      const uint32_t t = __hip_atomic_load(&g_pool_ctr[0], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      h = __hip_atomic_load(&g_pool_ctr[32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (h < t) {
-        const uint32_t want = t - h < 64u ? t - h : 64u;
-        if (__hip_atomic_compare_exchange_strong(&g_pool_ctr[32], &h, h + want,
-                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          n = want;
-          break;
-        }
-      }
-    }
-    n = __builtin_amdgcn_readfirstlane(n);
-    h = __builtin_amdgcn_readfirstlane(h);
-    if (!n) {
-      if (++idle > kPoolIdle) break;
-      __builtin_amdgcn_s_sleep(16);
-      continue;
-    }
-    idle = 0;
-    const bool v = lane < n;
-    float r6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 1.f};
-    uint32_t src = 0;
-    if (v) {
-      const uint32_t k = h + lane;
-      while (__hip_atomic_load(&g_pool_ready[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
-             gen)
-        __builtin_amdgcn_s_sleep(1);
-      const float4 a = g_pool_ray[2 * k], b = g_pool_ray[2 * k + 1];
-      r6[0] = a.x;
-      r6[1] = a.y;
-      r6[2] = a.z;
-      r6[3] = b.x;
-      r6[4] = b.y;
-      r6[5] = b.z;
-      src = __float_as_uint(a.w);
-    }
-    bool f = false;
-    float p[3], w[3];
-    scene_ray_packet<W, true, kEpiNone>(A, src, v, stl, sbox, sdom, wstk, f, p, w, r6);
-  }
-}
-#endif
 
 // STK: traversal-stack entries per lane, >= the depth of every resident
 // slot tree and of the top-level tree (a node at depth k has at most k
@@ -1469,11 +1366,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   constexpr bool kShadow = EPI == kEpiShadow || EPI == kEpiShadowFrame;
   __shared__ float sq_ray[kShadow ? (kBlock / 64) * kShadowQ * 6 : 1];
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
-  // ray prefetch: one packet (64 rays x 32 B) per wave
-  constexpr bool kPre = SPRAY_RAY_PREFETCH && kPacket && !kAdaptive && SPRAY_DEQ_AHEAD == 2 &&
-                        !ANY && EPI != kEpiAoGen;
-  __shared__ float4 pre_ray[kPre ? (kBlock / 64) * 128 : 1];
-  float4* my_pre = pre_ray + (kPre ? (threadIdx.x >> 6) * 128 : 0);
   ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
                  sq_src + (kShadow ? (threadIdx.x >> 6) * kShadowQ : 0), 0u};
   const unsigned long long wt0 = SPRAY_WAVE_TIMES ? wall_clock64() : 0ull;
@@ -1598,12 +1490,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             // rays have landed: the atomic overlaps that packet's walk, and
             // no chunk waits in a wave's hands while another is traced
             const bool last = c + 64 >= (rtc ? csz : kChunk);
-            // ray prefetch: this packet's rays came into LDS during the
-            // previous packet (not the chunk's first); the next packet's are
-            // copied while this one is walked
-            const bool pre = kPre && !idx && !A.valid;
-            const bool have = pre && c > 0;
-            if (have) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             float r6[6];
             const bool okr = rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres) : ok;
             scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
@@ -1614,23 +1500,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
                     ncsz = chunk_at(base + csz);
                     next = atomicAdd(head, ncsz);
                   }
-                  if (kPre && pre && !last) {
-                    // rays cbeg + c + 64 .. + 127: lane l copies 16 B (half
-                    // of ray l / 2) of each half-packet, LDS = lane order
-                    const size_t n0 = cbeg + c + 64;
-                    for (int h = 0; h < 2; ++h) {
-                      size_t rr = n0 + 32 * h + (lane >> 1);
-                      rr = rr < end ? rr : end - 1;
-                      const GAS char* src =
-                          (const GAS char*)(A.rays + rr) + 16 * (lane & 1);
-                      __builtin_amdgcn_global_load_lds(
-                          (GAS void*)src,
-                          (__attribute__((address_space(3))) void*)(my_pre + 64 * h), 16, 0,
-                          0);
-                    }
-                  }
-                },
-                have ? my_pre : nullptr);
+                });
           } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
@@ -1663,12 +1533,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     }
   }
   if (SPRAY_WAVE_TIMES) wt2 = wall_clock64();
-#if SPRAY_SHADOW_POOL
-  if (kShadow && persist) {  // the wave's last shadow rays through the pool
-    wave_lds_sync();
-    shadow_pool<W>(A, sq, stl, sbox, sdom, wstk);
-  } else
-#endif
   if (kShadow && sq.n) {  // the wave's last shadow rays (fewer than 64)
     wave_lds_sync();
 #if SPRAY_WAVE_TIMES
@@ -2534,16 +2398,6 @@ static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
   }
   hipError_t e = hipSuccess;
   if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
-#if SPRAY_SHADOW_POOL
-  if (e == hipSuccess && kPersist && (EPI == kEpiShadow || EPI == kEpiShadowFrame)) {
-    static void* ctr = nullptr;
-    static uint32_t gen = 0;
-    if (!ctr) e = hipGetSymbolAddress(&ctr, HIP_SYMBOL(g_pool_ctr));
-    if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, 64 * sizeof(uint32_t), s);
-    a.pool_gen = ++gen ? gen : ++gen;  // never 0 (the flags' initial value)
-    if (size_t(grid) * (kBlock / 64) * 64 > kPoolCap) return hipErrorInvalidValue;
-  }
-#endif
   if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) &&
       a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
