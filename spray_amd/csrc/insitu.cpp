@@ -162,7 +162,7 @@ struct spray_rt_insitu {
   unsigned long long* h_small = nullptr;  // pinned: counts, totals
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
   // replicated-ray frames (trace_replicated)
-  DBuf rmask, rfc, rfl, ridx_c, ridx_l, rnum, rsel_tmp, rkeys_n, rhits_n, rkeys_c;
+  DBuf rfc, ridx_c, rnum, rsel_tmp, rkeys_n, rhits_n, rkeys_c;
   DBuf rsray, rsflag, rwin, rsvalid, rsw, rocc, rpix, rsam, rhit_c, rnsh;
   // replicated-ray AO frames (trace_replicated_ao)
   DBuf apub, arays, ahits, apairs, aocc_p, alv, arec, ascratch, afields, acount;
@@ -871,58 +871,44 @@ bool split_keys() {
   return on;
 }
 
-// Steps 1-2 of a replicated-ray frame: owner-rank masks of every eye ray, C
-// and L (one host read: |C|, which sizes the all-reduces -- the same on
-// every rank -- and, for AO, the largest pixel id of C), the own closest
-// hits (keyed) of L and their keys over C.  The caller's MIN all-reduce of
-// keys_c (step 3) makes keys_c[j] the winning key of ray idx_c[j] on every
-// rank.
-int rep_lists_keys(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* pixid, size_t n,
-                   bool want_pixmax, size_t* nc_out, uint32_t* pixmax_out,
-                   bool want_keys_c = true) {
+// C' of a replicated frame: the eye rays entering the scene's bounding box
+// (idx_c, ascending), one host read of |C'| (and, want_pixmax, of the
+// largest pixel id of the frame: the AO frame's sample table).
+int rep_cull_select(spray_rt_insitu* I, const spray_rt_ray* rays, const int32_t* pixid, size_t n,
+                    bool want_pixmax, size_t* nc_out, uint32_t* pixmax_out) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
-  MARK(0);
-  GROW(I->rmask, n * 8);
+  SceneBox box{};
+  for (int k = 0; k < 3; ++k) {
+    box.lo[k] = INFINITY;
+    box.hi[k] = -INFINITY;
+  }
+  for (int d = 0; d < c->ndom; ++d)
+    for (int k = 0; k < 3; ++k) {
+      box.lo[k] = std::min(box.lo[k], c->h_boxes[6 * d + k]);
+      box.hi[k] = std::max(box.hi[k], c->h_boxes[6 * d + 3 + k]);
+    }
   GROW(I->rfc, n);
-  GROW(I->rfl, n);
   GROW(I->ridx_c, n * 4);
-  GROW(I->ridx_l, n * 4);
   GROW(I->rnum, 4 * 4);
   size_t t1 = 0;
   HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
   GROW(I->rsel_tmp, t1);
   uint32_t* dnum = I->rnum.as<uint32_t>();
-  if (want_pixmax) GROW(I->rbmax, (n / kBlock + 2) * 4);
-  HIPCHK(c, launch_route(s, view(c), c->d_owner, rays, n, I->rmask.as<uint64_t>()));
-  MARK(1);
-  HIPCHK(c, launch_rep_flags(s, I->rmask.as<uint64_t>(), n, I->rank, I->rfc.as<uint8_t>(),
-                             I->rfl.as<uint8_t>(), want_pixmax ? pixid : nullptr,
-                             want_pixmax ? dnum + 2 : nullptr,
-                             want_pixmax ? I->rbmax.as<uint32_t>() : nullptr));
+  HIPCHK(c, launch_rep_cull(s, rays, n, box, I->rfc.as<uint8_t>()));
   HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
                                   I->rsel_tmp.p, &t1));
-  HIPCHK(c, launch_select_flagged(s, I->rfl.as<uint8_t>(), n, I->ridx_l.as<uint32_t>(), dnum + 1,
-                                  I->rsel_tmp.p, &t1));
+  if (want_pixmax) {
+    GROW(I->rbmax, (n / kBlock + 2) * 4);
+    HIPCHK(c, launch_pix_max(s, pixid, n, I->rbmax.as<uint32_t>(), dnum + 2));
+  }
   HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 12, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   ++I->st[3];
   uint32_t cnt[3];
   std::memcpy(cnt, I->h_small, 12);
-  const size_t nc = cnt[0];
-  *nc_out = nc;
+  *nc_out = cnt[0];
   if (pixmax_out) *pixmax_out = want_pixmax ? cnt[2] : 0;
-  MARK(2);
-  GROW(I->rkeys_n, n * 8);
-  GROW(I->rhits_n, n * 48);
-  GROW(I->rkeys_c, nc * 8 + 8);
-  if (cnt[1])
-    HIPCHK(c, launch_scene_intersect_keyed_indexed(s, view(c), rays, n, I->ridx_l.as<uint32_t>(),
-                                                   dnum + 1, I->rhits_n.as<spray_rt_hit>(),
-                                                   I->rkeys_n.as<uint64_t>()));
-  if (want_keys_c)
-    HIPCHK(c, launch_rep_keys(s, I->ridx_c.as<uint32_t>(), nc, I->rmask.as<uint64_t>(), I->rank,
-                              I->rkeys_n.as<uint64_t>(), I->rkeys_c.as<uint64_t>()));
   return SPRAY_RT_OK;
 }
 
@@ -952,32 +938,8 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
                              P->ks[2],       P->shininess};
   // ---- 1. C' (one host read: |C'| sizes the all-reduces, the same on every rank)
   MARK(0);
-  SceneBox box{};
-  for (int k = 0; k < 3; ++k) {
-    box.lo[k] = INFINITY;
-    box.hi[k] = -INFINITY;
-  }
-  for (int d = 0; d < c->ndom; ++d)
-    for (int k = 0; k < 3; ++k) {
-      box.lo[k] = std::min(box.lo[k], c->h_boxes[6 * d + k]);
-      box.hi[k] = std::max(box.hi[k], c->h_boxes[6 * d + 3 + k]);
-    }
-  GROW(I->rfc, n);
-  GROW(I->ridx_c, n * 4);
-  GROW(I->rnum, 4 * 4);
-  size_t t1 = 0;
-  HIPCHK(c, launch_select_flagged(s, nullptr, n, nullptr, nullptr, nullptr, &t1));
-  GROW(I->rsel_tmp, t1);
-  uint32_t* dnum = I->rnum.as<uint32_t>();
-  HIPCHK(c, launch_rep_cull(s, rays, n, box, I->rfc.as<uint8_t>()));
-  HIPCHK(c, launch_select_flagged(s, I->rfc.as<uint8_t>(), n, I->ridx_c.as<uint32_t>(), dnum,
-                                  I->rsel_tmp.p, &t1));
-  HIPCHK(c, hipMemcpyAsync(I->h_small, dnum, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  ++I->st[3];
-  uint32_t nc32 = 0;
-  std::memcpy(&nc32, I->h_small, 4);
-  const size_t nc = nc32;
+  size_t nc = 0;
+  CALL(rep_cull_select(I, rays, pixid, n, false, &nc, nullptr));
   const uint32_t* idx_c = I->ridx_c.as<uint32_t>();
   // ---- 2. the compact film's slots (runs of equal pixels along C'), their
   // count on its way to the host while the frame runs on
@@ -1160,8 +1122,21 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   const int ns = P->samples;
   size_t nc = 0;
   uint32_t pixmax = 0;
-  CALL(rep_lists_keys(I, rays, pixid, n, true, &nc, &pixmax));
-  if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C| >= 2^27");
+  MARK(0);
+  CALL(rep_cull_select(I, rays, pixid, n, true, &nc, &pixmax));
+  if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C'| >= 2^27");
+  // own keyed closest hits over C' (keys and hit records at C' positions)
+  MARK(2);
+  GROW(I->rkeys_n, nc * 8 + 8);
+  GROW(I->rhits_n, nc * 48 + 48);
+  GROW(I->rkeys_c, nc * 8 + 8);
+  GROW(I->rtk, nc * 4 + 4);
+  const float zero10[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  HIPCHK(c, launch_fill_u64(s, I->rkeys_n.as<uint64_t>(), nc, kInsituMissKey));
+  HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, I->ridx_c.as<uint32_t>(), nc, zero10,
+                                   I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
+                                   I->rtk.as<uint32_t>(), nullptr, nullptr));
+  HIPCHK(c, hipMemcpyAsync(I->rkeys_c.p, I->rkeys_n.p, nc * 8, hipMemcpyDeviceToDevice, s));
   MARK(3);
   if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
   const int fb = I->world <= 3 ? 2 : (I->world <= 15 ? 4 : 8);
@@ -1190,7 +1165,6 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   A.idx_c = I->ridx_c.as<uint32_t>();
   A.keys_c = I->rkeys_c.as<uint64_t>();
   A.keys_n = I->rkeys_n.as<uint64_t>();
-  A.mask = I->rmask.as<uint64_t>();
   A.rays = reinterpret_cast<const float4*>(rays);
   A.hits_n = I->rhits_n.as<spray_rt_hit>();
   A.pix = pixid;
@@ -1255,8 +1229,8 @@ void free_all(spray_rt_insitu* I) {
                  &I->ohit, &I->okey, &I->obest, &I->owin, &I->ovalid, &I->best, &I->keyback,
                  &I->sray, &I->ssw, &I->ssv, &I->socc, &I->ssel, &I->smask,
                  &I->sidx, &I->sstarts, &I->ashadow, &I->aocc, &I->sret, &I->nsel,
-                 &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot, &I->rmask, &I->rfc, &I->rfl,
-                 &I->ridx_c, &I->ridx_l, &I->rnum, &I->rsel_tmp, &I->rkeys_n, &I->rhits_n,
+                 &I->sel_tmp, &I->dnum, &I->dstats, &I->dtot, &I->rfc,
+                 &I->ridx_c, &I->rnum, &I->rsel_tmp, &I->rkeys_n, &I->rhits_n,
                  &I->rkeys_c, &I->rsray, &I->rsflag, &I->rwin, &I->rsvalid, &I->rsw, &I->rocc,
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,

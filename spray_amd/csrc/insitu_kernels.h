@@ -62,14 +62,6 @@ hipError_t launch_weights_one(hipStream_t s, float* w, size_t n);
 hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_hit* hits,
                             size_t n, uint8_t* win);
 // ---- replicated-ray frames (insitu.cpp, trace_replicated) ----
-// fc[i] = mask[i] != 0 (some domain on the list), fl[i] = bit `rank` of it;
-// pixmax (optional): max of pix[i] over C, through bmax (grid_for(n) u32)
-hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
-                            uint8_t* fl, const int32_t* pix = nullptr,
-                            uint32_t* pixmax = nullptr, uint32_t* bmax = nullptr);
-// keys_c[j] = keys_n[idx_c[j]] where bit `rank` of its mask is set, else a miss
-hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
-                           int rank, const uint64_t* keys_n, uint64_t* keys_c);
 // scene bounding box (the replicated frame's cull)
 struct SceneBox {
   float lo[3], hi[3];
@@ -96,6 +88,9 @@ hipError_t launch_min_u32(hipStream_t s, const uint32_t* a, const uint32_t* b, s
                           uint32_t* out);
 // tmin[j] = t bits of kmin[j] (0xFFFFFFFF: a miss)
 hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc, uint32_t* tmin);
+// *out = max(pix[0..n)) (bmax: grid_for(n) u32 of scratch)
+hipError_t launch_pix_max(hipStream_t s, const int32_t* pix, size_t n, uint32_t* bmax,
+                          uint32_t* out);
 // dst[j] = src[idx[j]]
 hipError_t launch_gather_i32(hipStream_t s, const uint32_t* idx, size_t n, const int32_t* src,
                              int32_t* dst);
@@ -119,10 +114,10 @@ struct RepAoArgs {
   int fb;                       // bits per occlusion count field (2, 4 or 8)
   const uint32_t* idx_c;        // [nc] ray ids of C
   const uint64_t* keys_c;       // [nc] winning keys (after the MIN all-reduce)
-  const uint64_t* keys_n;       // [n] this rank's keys (valid where its mask bit is set)
-  const uint64_t* mask;         // [n] owner-rank masks
+  const uint64_t* keys_n;       // [nc] this rank's keys
+  const uint64_t* mask;         // unused
   const float4* rays;           // [n] eye rays (32 B)
-  const spray_rt_hit* hits_n;   // [n] this rank's hit records
+  const spray_rt_hit* hits_n;   // [nc] this rank's hit records
   const int32_t* pix;           // [n]
   const int32_t* sam;           // [n]
   uint4* pub;                   // [nc] winner's normal bits + colour, zeros elsewhere

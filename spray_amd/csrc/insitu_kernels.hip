@@ -289,36 +289,6 @@ __global__ __launch_bounds__(kBlock) void k_weights_one(float4* __restrict__ w, 
 // Every rank holds the frame's eye rays; C = the rays whose domain list is
 // not empty (the same ascending list on every rank), L = the rays with a
 // domain of this rank on their list.
-// bmax (optional): per block the largest pixel id of C (the AO frame's
-// sample table) -- one plain store per block, no same-address atomics
-// (131 K wave atomics on one word cost ~1.5 ms); k_max_u32 reduces them
-__global__ __launch_bounds__(kBlock) void k_rep_flags(const uint64_t* __restrict__ mask, size_t n,
-                                                      int rank, uint8_t* __restrict__ fc,
-                                                      uint8_t* __restrict__ fl,
-                                                      const int32_t* __restrict__ pix,
-                                                      uint32_t* __restrict__ bmax) {
-  __shared__ uint32_t wmax[kBlock / 64];
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  uint32_t px = 0;
-  if (i < n) {
-    const uint64_t m = mask[i];
-    fc[i] = m != 0;
-    fl[i] = uint8_t((m >> rank) & 1ull);
-    if (bmax && m) px = uint32_t(max(pix[i], 0));
-  }
-  if (bmax) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) px = max(px, uint32_t(__shfl_xor(int(px), off)));
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = px;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t b = 0;
-      for (int w = 0; w < kBlock / 64; ++w) b = max(b, wmax[w]);
-      bmax[blockIdx.x] = b;
-    }
-  }
-}
-
 // *out = max(v[0..n)), one block
 __global__ __launch_bounds__(1024) void k_max_u32(const uint32_t* __restrict__ v, size_t n,
                                                   uint32_t* __restrict__ out) {
@@ -334,18 +304,6 @@ __global__ __launch_bounds__(1024) void k_max_u32(const uint32_t* __restrict__ v
     for (int w = 0; w < 1024 / 64; ++w) b = max(b, part[w]);
     *out = b;
   }
-}
-
-// keys_c[j] = this rank's key of ray idx_c[j] (a miss where no domain of the
-// rank is on its list: the keyed launch did not visit it)
-__global__ __launch_bounds__(kBlock) void k_rep_keys(const uint32_t* __restrict__ idx_c, size_t nc,
-                                                     const uint64_t* __restrict__ mask, int rank,
-                                                     const uint64_t* __restrict__ keys_n,
-                                                     uint64_t* __restrict__ keys_c) {
-  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= nc) return;
-  const uint32_t i = idx_c[j];
-  keys_c[j] = ((mask[i] >> rank) & 1ull) ? keys_n[i] : kInsituMissKey;
 }
 
 // The frame totals as bits (byte 64 c + k = bit k of total c) behind the
@@ -370,11 +328,10 @@ __global__ __launch_bounds__(kBlock) void k_rep_ao_publish(RepAoArgs A) {
   if (j >= A.nc) return;
   const uint32_t i = A.idx_c[j];
   const uint64_t key = A.keys_c[j];
-  const bool win =
-      key != kInsituMissKey && ((A.mask[i] >> A.rank) & 1ull) && A.keys_n[i] == key;
+  const bool win = key != kInsituMissKey && A.keys_n[j] == key;
   uint4 pub = make_uint4(0u, 0u, 0u, 0u);
   if (win) {
-    const spray_rt_hit h = A.hits_n[i];
+    const spray_rt_hit h = A.hits_n[j];
     pub = make_uint4(__float_as_uint(h.ns[0]), __float_as_uint(h.ns[1]),
                      __float_as_uint(h.ns[2]), h.color);
     if (A.hit_c) A.hit_c[j] = h;
@@ -657,6 +614,23 @@ __global__ __launch_bounds__(kBlock) void k_min_u32(const uint32_t* __restrict__
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j < n) out[j] = min(a[j], b[j]);
 }
+
+// pixel-id maxima per block of pix[0..n) (then k_max_u32)
+__global__ __launch_bounds__(kBlock) void k_pix_bmax(const int32_t* __restrict__ pix, size_t n,
+                                                     uint32_t* __restrict__ bmax) {
+  __shared__ uint32_t wmax[kBlock / 64];
+  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  uint32_t px = i < n ? uint32_t(max(pix[i], 0)) : 0u;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) px = max(px, uint32_t(__shfl_xor(int(px), off)));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = px;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (int w = 0; w < kBlock / 64; ++w) b = max(b, wmax[w]);
+    bmax[blockIdx.x] = b;
+  }
+}
 }  // namespace
 
 #define LAUNCH(n, kern, ...)                                  \
@@ -747,18 +721,6 @@ hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_
 hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
 }
-hipError_t launch_rep_flags(hipStream_t s, const uint64_t* mask, size_t n, int rank, uint8_t* fc,
-                            uint8_t* fl, const int32_t* pix, uint32_t* pixmax, uint32_t* bmax) {
-  if (n == 0) return pixmax ? hipMemsetAsync(pixmax, 0, 4, s) : hipSuccess;
-  k_rep_flags<<<grid_for(n), kBlock, 0, s>>>(mask, n, rank, fc, fl, pixmax ? pix : nullptr,
-                                             pixmax ? bmax : nullptr);
-  if (pixmax) k_max_u32<<<1, 1024, 0, s>>>(bmax, grid_for(n), pixmax);
-  return hipGetLastError();
-}
-hipError_t launch_rep_keys(hipStream_t s, const uint32_t* idx_c, size_t nc, const uint64_t* mask,
-                           int rank, const uint64_t* keys_n, uint64_t* keys_c) {
-  LAUNCH(nc, k_rep_keys, idx_c, nc, mask, rank, keys_n, keys_c);
-}
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow) {
   k_rep_totals<<<1, 192, 0, s>>>(tail, nrad, nshadow);
@@ -794,6 +756,13 @@ hipError_t launch_rep_win2(hipStream_t s, const uint64_t* keys1, const uint32_t*
 hipError_t launch_min_u32(hipStream_t s, const uint32_t* a, const uint32_t* b, size_t n,
                           uint32_t* out) {
   LAUNCH(n, k_min_u32, a, b, n, out);
+}
+hipError_t launch_pix_max(hipStream_t s, const int32_t* pix, size_t n, uint32_t* bmax,
+                          uint32_t* out) {
+  if (n == 0) return hipMemsetAsync(out, 0, 4, s);
+  k_pix_bmax<<<grid_for(n), kBlock, 0, s>>>(pix, n, bmax);
+  k_max_u32<<<1, 1024, 0, s>>>(bmax, grid_for(n), out);
+  return hipGetLastError();
 }
 hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
                             uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,

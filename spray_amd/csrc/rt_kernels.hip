@@ -1082,8 +1082,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     A.keys[i] = key;
     if (EPI == kEpiKeysShade) {
       A.tkeys[i] = best_dom >= 0 ? __float_as_uint(best.t) : 0xFFFFFFFFu;
-      // round 2 keeps round 1's shading where it found nothing nearer
-      if (A.rround == 2 && best_dom < 0) return;
+      // round 2 keeps round 1's shading where it found nothing nearer; no
+      // shading arrays: keys only (the replicated AO frame)
+      if ((A.rround == 2 && best_dom < 0) || !A.sh_valid) return;
       bool sp = false;
       if (best_dom >= 0) {
         spray_rt_hit h;
