@@ -99,10 +99,13 @@ def main():
     ck = torch.empty(ncp, dtype=torch.int64, device="cuda")
     t_full_keyed = timed(lambda: full.intersect_scene_keyed(cp, ch, ck))
     t_full_ch = timed(lambda: full.intersect_scene(cp, ch))
+    full.set_coherence(full.RAYS_INCOHERENT)
+    t_full_lane = timed(lambda: full.intersect_scene(cp, ch))
+    full.set_coherence(full.RAYS_COHERENT)
     report["cprime"] = {"n": ncp, "full_keyed_ms": round(t_full_keyed, 4),
-                        "full_ch_ms": round(t_full_ch, 4)}
-    print("C' %d rays: all domains keyed %.3f ms, plain CH %.3f ms" % (ncp, t_full_keyed, t_full_ch),
-          flush=True)
+                        "full_ch_ms": round(t_full_ch, 4), "full_ch_lane_ms": round(t_full_lane, 4)}
+    print("C' %d rays: all domains keyed %.3f ms, plain CH packets %.3f / per lane %.3f ms" % (
+        ncp, t_full_keyed, t_full_ch, t_full_lane), flush=True)
     for world in args.worlds:
         for mode in args.modes:
             pm = insitu.PARTITION_ROUND_ROBIN if mode == "rr" else insitu.PARTITION_GROUP_CLOSE
@@ -126,12 +129,16 @@ def main():
                 t_sh = timed(lambda: rt.occluded_scene_masked(srays, svalid, so))
                 t_ck = timed(lambda: rt.intersect_scene_keyed(cp, ch, ck))
                 t_cc = timed(lambda: rt.intersect_scene(cp, ch))
+                rt.set_coherence(rt.RAYS_INCOHERENT)  # the same launch walked per lane
+                t_cl = timed(lambda: rt.intersect_scene(cp, ch))
+                rt.set_coherence(rt.RAYS_COHERENT)
                 ranks.append({"rank": r, "L": nl, "C": int(on.sum()), "route_ms": round(t_route, 4),
                               "keyed_ms": round(t_keyed, 4), "shadow_ms": round(t_sh, 4),
-                              "cprime_keyed_ms": round(t_ck, 4), "cprime_ch_ms": round(t_cc, 4)})
+                              "cprime_keyed_ms": round(t_ck, 4), "cprime_ch_ms": round(t_cc, 4),
+                              "cprime_ch_lane_ms": round(t_cl, 4)})
                 print("N=%d %s rank %d: L %d route %.3f keyed(L) %.3f shadow %.3f keyed(C') %.3f "
-                      "CH(C') %.3f ms" % (world, mode, r, nl, t_route, t_keyed, t_sh, t_ck, t_cc),
-                      flush=True)
+                      "CH(C') packets %.3f per lane %.3f ms" % (
+                          world, mode, r, nl, t_route, t_keyed, t_sh, t_ck, t_cc, t_cl), flush=True)
                 rt.close()
             report["runs"].append({"world": world, "partition": mode, "ranks": ranks})
     if args.out:
