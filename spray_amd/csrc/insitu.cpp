@@ -853,6 +853,16 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
 }
 
 // SPRAY_INSITU_SPLIT_KEYS=0: the replicated PT frame's 64-bit key MIN
+// SPRAY_INSITU_LANE=1: the replicated frames' launches walked per lane
+// (each lane its own ray) instead of as 64-ray packets
+bool rep_lane() {
+  static const bool on = [] {
+    const char* e = std::getenv("SPRAY_INSITU_LANE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // SPRAY_INSITU_ROUNDS=2: the replicated PT frame's keyed walk in two rounds
 // (first list entries, then the later ones below the round-1 minimum)
 int key_rounds() {
@@ -980,7 +990,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
                                    I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
-                                   rounds == 2 ? 1 : 0));
+                                   rounds == 2 ? 1 : 0, nullptr, rep_lane()));
   // two rounds: the group's round-1 minimum, then the later entries below it
   uint64_t* keys2 = nullptr;
   uint32_t* tk2 = nullptr;
@@ -1040,7 +1050,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   GROW(I->rocc, nc + 192);
   HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nc, s));
   HIPCHK(c, launch_scene_rep_shadows(s, view(c), rays, n, idx_c, nc, tstar, shade10,
-                                     I->rocc.as<uint8_t>()));
+                                     I->rocc.as<uint8_t>(), rep_lane()));
   // ---- 6. the winners (after the list positions' MIN), their shadows
   // counted behind the occlusion bytes: rank 0 counts the frame's radiance
   // rays, every rank its winners' shadow rays
@@ -1135,7 +1145,8 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   HIPCHK(c, launch_fill_u64(s, I->rkeys_n.as<uint64_t>(), nc, kInsituMissKey));
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, I->ridx_c.as<uint32_t>(), nc, zero10,
                                    I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
-                                   I->rtk.as<uint32_t>(), nullptr, nullptr));
+                                   I->rtk.as<uint32_t>(), nullptr, nullptr, 0, nullptr,
+                                   rep_lane()));
   HIPCHK(c, hipMemcpyAsync(I->rkeys_c.p, I->rkeys_n.p, nc * 8, hipMemcpyDeviceToDevice, s));
   MARK(3);
   if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));

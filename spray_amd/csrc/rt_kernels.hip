@@ -296,6 +296,7 @@ struct SceneArgs {
   // kEpiKeysShade rounds: 0 = every resident entry of the lane's list; 1 =
   // its first entry only; 2 = the later entries below the round-1 minimum
   int rround;
+  int rep_lane;  // replicated launches walked per lane instead of as packets
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -391,7 +392,8 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                           const float4* sdom, int32_t* stk, int32_t* wstk,
                                           unsigned& nnode, unsigned& ntri,
                                           unsigned& nvisit, bool& spawn, float* pos,
-                                          float* wi) {
+                                          float* wi, const float* rin = nullptr) {
+  constexpr bool kKeysL = EPI == kEpiKeys || EPI == kEpiKeysShade;
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int ntlas = A.ntlas;
@@ -401,6 +403,9 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     v4f a, b;
     if (EPI == kEpiAoGen) {
       ao_gen(A, i, a, b);
+    } else if (rin) {  // a replicated frame's ray (rep_ray), results at i
+      a = v4f{rin[0], rin[1], rin[2], kRayEpsilon};
+      b = v4f{rin[3], rin[4], rin[5], kInf};
     } else {
       const v4f* rp = reinterpret_cast<const v4f*>(A.rays + i);
       if (SPRAY_NT_IO_LANE) {
@@ -473,7 +478,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
       for (int w = 0; w < W; ++w)
         if (w == (sb >> 6)) m[w] &= ~(1ull << (sb & 63));
       const uint32_t pos_sb = it;
-      if (EPI == kEpiKeys) ++it;
+      if (kKeysL) ++it;
       const float4 dt = sdom[sb];
       const char* nodes = reinterpret_cast<const char*>(
           (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
@@ -506,7 +511,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
                                  ntri);
         if (best.leaf != 0xFFFFFFFFu) {
           best_dom = sb;
-          if (EPI == kEpiKeys) best_it = pos_sb;
+          if (kKeysL) best_it = pos_sb;
         } else {
           best.prim = keep_prim;
           best.leaf = keep_leaf;
@@ -535,17 +540,38 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
         h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
       }
-      float4* hp = reinterpret_cast<float4*>(hits + i);
-      hp[0] = h0;
-      hp[1] = h1;
-      hp[2] = h2;
-      if (EPI == kEpiKeys) {
+      if (!(EPI == kEpiKeysShade && !hits)) {
+        float4* hp = reinterpret_cast<float4*>(hits + i);
+        hp[0] = h0;
+        hp[1] = h1;
+        hp[2] = h2;
+      }
+      if (kKeysL) {
         // in-situ compositing key: the order of the sequential domain walk
         // (t, then the earlier entry of the sorted domain list), unique per
         // domain; misses sort last
         A.keys[i] = best_dom < 0 ? 0x7FFFFFFFFFFFFFFFull
                                  : (uint64_t(__float_as_uint(best.t)) << 32) |
                                        (uint64_t(best_it) << 16) | uint64_t(best_dom);
+      }
+      if (EPI == kEpiKeysShade) {  // the replicated frame (one round, per lane)
+        A.tkeys[i] = best_dom >= 0 ? __float_as_uint(best.t) : 0xFFFFFFFFu;
+        if (A.sh_valid) {
+          bool sp = false;
+          if (best_dom >= 0) {
+            spray_rt_hit h;
+            h.t = h0.x;
+            h.color = __float_as_uint(h1.w);
+            h.ns[0] = h2.x;
+            h.ns[1] = h2.y;
+            h.ns[2] = h2.z;
+            const float d3[3] = {d4.x, d4.y, d4.z}, o3[3] = {o4.x, o4.y, o4.z};
+            float L[3];
+            sp = shade_pt_point(o3, d3, h, A.shade, pos, wi, L);
+            if (sp) A.sw[i] = make_float4(L[0], L[1], L[2], 0.f);
+          }
+          A.sh_valid[i] = sp;
+        }
       }
       if (EPI == kEpiSpawn && best_dom >= 0) {
         spray_rt_hit h;
@@ -1420,8 +1446,12 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     if constexpr (rep_epi(EPI)) {
       float r6[6];
       const bool okr = rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres);
-      scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
-          A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
+      if (kPacket)
+        scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
+            A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
+      else if (okr)
+        scene_ray<W, ANY, COUNT, EPI == kEpiShadowGen ? kEpiNone : EPI, kLStk>(
+            A, j, stl, sbox, sdom, stk, wstk, nnode, ntri, nvisit, flag, pos, wi, r6);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
@@ -1512,7 +1542,12 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           else if (kGroup)
             scene_ray_ao_group<W>(A, i, ok, stl, sbox, sdom,
                                   stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
-          else if (ok)
+          else if (rep_epi(EPI)) {
+            float r6[6];
+            if (rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres))
+              scene_ray<W, ANY, COUNT, EPI == kEpiShadowGen ? kEpiNone : EPI, kLStk>(
+                  A, j, stl, sbox, sdom, stk, wstk, nnode, ntri, nvisit, flag, pos, wi, r6);
+          } else if (ok)
             scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
 #if SPRAY_WAVE_TIMES
@@ -2419,6 +2454,7 @@ static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherenc
   if constexpr (ANY && EPI == kEpiAoGen) {
     return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
   } else if constexpr (rep_epi(EPI)) {  // camera rays and point-light shadows
+    if (a.rep_lane) return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
   } else if constexpr (!ANY && EPI != kEpiNone) {
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
@@ -2812,10 +2848,11 @@ hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray
                                   size_t n, const uint32_t* idx, size_t nc,
                                   const float* shade10, spray_rt_hit* hits, uint64_t* keys,
                                   uint32_t* tkeys, float* sw, uint8_t* sv, int round,
-                                  const uint32_t* tmin_round1) {
+                                  const uint32_t* tmin_round1, bool per_lane) {
   if (nc == 0) return hipSuccess;
   SceneArgs a = scene_args(v, rays, nc);
   a.rround = round;
+  a.rep_lane = per_lane && round == 0 ? 1 : 0;
   a.tmin = tmin_round1;
   a.nrays = n;
   a.idx = idx;
@@ -2830,9 +2867,11 @@ hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray
 
 hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                     size_t n, const uint32_t* idx, size_t nc,
-                                    const uint32_t* tmin, const float* shade10, uint8_t* occ) {
+                                    const uint32_t* tmin, const float* shade10, uint8_t* occ,
+                                    bool per_lane) {
   if (nc == 0) return hipSuccess;
   SceneArgs a = scene_args(v, rays, nc);
+  a.rep_lane = per_lane ? 1 : 0;
   a.nrays = n;
   a.idx = idx;
   a.tmin = tmin;

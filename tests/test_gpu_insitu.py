@@ -268,7 +268,8 @@ def test_engine_two_ranks_one_owner(oracle):
 @pytest.mark.parametrize("world,mode,case", [(2, 0, "pt1"), (8, 0, "pt1"), (8, 1, "pt1"),
                                              (3, 1, "pt1"), (2, 0, "ao16"), (3, 1, "ao16"),
                                              (8, 0, "ao16"), (8, 1, "ao16"), (8, 1, "pt1-u64"),
-                                             (8, 0, "pt1-r2"), (3, 1, "pt1-r2")])
+                                             (8, 0, "pt1-r2"), (3, 1, "pt1-r2"),
+                                             (8, 1, "pt1-lane"), (2, 0, "ao16-lane")])
 def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
     """spray_rt_insitu_trace_frame with world processes sharing the GPU over
     the host transport: every eye ray on every rank, the keys' MIN and the
@@ -289,6 +290,9 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
     if case == "pt1-r2":  # the keyed walk in two rounds (first entries, then the rest)
         monkeypatch.setenv("SPRAY_INSITU_ROUNDS", "2")
         case = "pt1"
+    if case.endswith("-lane"):  # the replicated launches walked per lane
+        monkeypatch.setenv("SPRAY_INSITU_LANE", "1")
+        case = case[:-5]
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
                                     args=(world, _free_port(), out, case, False, True, mode),
