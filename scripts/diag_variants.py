@@ -20,8 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DIAG = os.path.join(ROOT, "spray_amd", "lib", "diag")
 VARIANTS = {"mask_only": ["SPRAY_DIAG_MODE=1"], "mask_select": ["SPRAY_DIAG_MODE=2"],
-            "ah_spread": ["SPRAY_AH_SPREAD=1"], "ao_refill": ["SPRAY_AO_REFILL=32"]}
-CHECKED = ("ah_spread", "ao_refill", "aogroup", "aogroup6")  # bit-exact variants: parity tests apply
+            "ah_spread": ["SPRAY_AH_SPREAD=1"], "ao_refill": ["SPRAY_AO_REFILL=32"],
+            "aogroup": ["SPRAY_AO_GROUP=1"]}
+CHECKED = ("ah_spread", "ao_refill", "aogroup")  # bit-exact variants: parity tests apply
 EXTRA = dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a)  # name=DEF1,DEF2
 
 

@@ -45,7 +45,10 @@ for v in ${AB:-}; do
   done
 done
 if [ -n "${REHEARSE:-}" ]; then
-  timeout -k 10 ${RTIME:-600} python -u scripts/insitu_rep_rehearse.py --worlds $REHEARSE --modes ${MODES:-close rr} --kinds ${KINDS:-pt} --frames ${FRAMES:-3} --out "$OUT/rehearse.json" > "$OUT/rehearse.log" 2>&1
+  # REHKT=1: under a per-process rocprofv3 kernel trace (rehearse_kernel_segments.py)
+  PRE=""
+  [ "${REHKT:-0}" = 1 ] && PRE="rocprofv3 --kernel-trace --output-format csv -d $OUT/rehkt -o %pid%/run --"
+  timeout -k 10 ${RTIME:-600} $PRE python -u scripts/insitu_rep_rehearse.py --worlds $REHEARSE --modes ${MODES:-close rr} --kinds ${KINDS:-pt} --frames ${FRAMES:-3} --out "$OUT/rehearse.json" > "$OUT/rehearse.log" 2>&1
   rc=$?; echo "rehearse rc=$rc"; tail -12 "$OUT/rehearse.log"
   [ $rc -ne 0 ] && fail rehearse $rc "$OUT/rehearse.log"
 fi

@@ -12,6 +12,10 @@ Inputs
   times), and the one-rank RCCL all-reduce times of the frame's message
   sizes (the per-call floor).
 * the measured N = 1 frame (the bench's fused single-GPU frame, --n1-ms).
+* optionally (--kernels) the same runs' per-rank segment times from rocprofv3
+  kernel traces (scripts/rehearse_kernel_segments.py): robust against the
+  rehearsal's clock drops after its long host-collective gaps, and the
+  numbers DESIGN quotes.
 
 Model of one frame at N ranks (every rank runs the same sequence):
   PT: T = max_r(cull + select + film slots + keyed closest hit & shading)
@@ -60,13 +64,15 @@ SEGMENTS = {  # phases between the frame's collectives, in order
 }
 
 
-def project(run, link):
+def project(run, link, seg=None):
     n = run["world"]
     ranks = run["ranks"]
     kind = run.get("kind", "pt")
     ph = lambda r, k: r["phases_ms"].get(k, 0.0)  # noqa: E731
     # every segment ends in a collective all ranks wait for: its busiest rank
-    seg = [max(sum(ph(r, k) for k in names) for r in ranks) for names in SEGMENTS[kind]]
+    # (HIP-event phases, or the kernel traces' segment sums when given)
+    if seg is None:
+        seg = [max(sum(ph(r, k) for k in names) for r in ranks) for names in SEGMENTS[kind]]
     nc = ranks[0]["nc"]
     if kind == "ao":
         fb = fbits(n)
@@ -87,9 +93,16 @@ def main():
     ap.add_argument("rehearse")
     ap.add_argument("--n1-ms", type=float, default=0.77, help="measured N = 1 PT frame")
     ap.add_argument("--n1-ao-ms", type=float, default=None, help="measured N = 1 AO frame")
+    ap.add_argument("--kernels", default=None,
+                    help="segments.json of scripts/rehearse_kernel_segments.py (per-rank "
+                         "kernel-trace segment times of the same runs)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     rep = json.load(open(args.rehearse))
+    ksegs = {}
+    if args.kernels:
+        for r in json.load(open(args.kernels))["runs"]:
+            ksegs[(r["world"], r["partition"], r["kind"])] = r["busiest_per_segment_ms"]
     rows = []
     for run in rep["runs"]:
         if run.get("kind", "pt") not in ("pt", "ao"):
@@ -104,6 +117,13 @@ def main():
             base = args.n1_ms if row["kind"] == "pt" else args.n1_ao_ms
             p["speedup_vs_n1"] = round(base / p["frame_ms"], 3) if base else None
             row[name] = p
+        key = (run["world"], run["partition"], row["kind"])
+        if key in ksegs:  # the same frame from the kernel traces
+            for name, link in LINK.items():
+                p = project(run, link, ksegs[key])
+                base = args.n1_ms if row["kind"] == "pt" else args.n1_ao_ms
+                p["speedup_vs_n1"] = round(base / p["frame_ms"], 3) if base else None
+                row["kernel_trace_" + name] = p
         rows.append(row)
     out = {"model": __doc__.strip().split("\n\n")[2], "links": LINK, "n1_ms": args.n1_ms,
            "rccl_one_rank_floor": rep.get("rccl_one_rank_floor"), "rows": rows}
@@ -118,6 +138,13 @@ def main():
             " + ".join("%.3f" % x for x in c["busiest_per_segment"]), c["device_ms"],
             c["comm_ms"], c["frame_ms"], o["frame_ms"], sx(c["speedup_vs_n1"]),
             sx(o["speedup_vs_n1"])))
+        if "kernel_trace_conservative" in r:
+            c, o = r["kernel_trace_conservative"], r["kernel_trace_optimistic"]
+            print("| %s (kernel trace) | %d | %s | %s | %.3f | %.3f | %.3f / %.3f | %s / %s |" % (
+                r["kind"], r["world"], r["partition"],
+                " + ".join("%.3f" % x for x in c["busiest_per_segment"]), c["device_ms"],
+                c["comm_ms"], c["frame_ms"], o["frame_ms"], sx(c["speedup_vs_n1"]),
+                sx(o["speedup_vs_n1"])))
     if args.out:
         with open(args.out, "w") as fh:
             json.dump(out, fh, indent=1)

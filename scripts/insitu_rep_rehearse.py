@@ -86,6 +86,9 @@ def _rank(rank, world, port, mode, frames, out, kind="pt"):
         tot = trace(sh, rays, pix, sam, SPP, image)
     s1 = eng.stats()
     ph = {k: v / frames for k, v in eng.phase_times().items()}
+    # no device work outside the lock until every rank's frames are done (the
+    # sizes below would run beside a slower rank's last frame)
+    dist.barrier()
     # the sizes of the frame's collectives: PT |C'| (rays entering the
     # scene's bounding box: k_rep_cull's slab test, the same float ops), AO
     # |C| (rays with a non-empty domain list), and the pixel runs along them
@@ -106,7 +109,8 @@ def _rank(rank, world, port, mode, frames, out, kind="pt"):
         on = m != 0
     pc = pix[on]
     nc, nruns = int(on.sum()), int(1 + (pc[1:] != pc[:-1]).sum()) if pc.numel() else 0
-    res = {"rank": rank, "domains": int((owner == rank).sum()), "phases_ms": ph,
+    res = {"rank": rank, "pid": os.getpid(), "domains": int((owner == rank).sum()),
+           "phases_ms": ph,
            "nc": nc, "pixel_runs": nruns,
            "totals": list(tot), "stats": eng.stats(),
            "per_frame": {k: (s1[k] - s0[k]) / frames for k in s1}}

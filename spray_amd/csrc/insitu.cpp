@@ -166,6 +166,7 @@ struct spray_rt_insitu {
   DBuf rsray, rsflag, rwin, rsvalid, rsw, rocc, rpix, rsam, rhit_c, rnsh;
   // replicated-ray AO frames (trace_replicated_ao)
   DBuf apub, arays, ahits, apairs, aocc_p, alv, arec, ascratch, afields, acount;
+  DBuf aflag, aown, asel_tmp;  // replicated AO: the own pairs, compacted
   // compact film of replicated PT frames (runs of equal pixels along C)
   DBuf rheads, rincl, rscan_tmp, rslot_c, rslot_pix, rcompact, rnp;
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
@@ -1057,8 +1058,8 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   MARK(5);
   GROW(I->rwin, nc + 1);
   GROW(I->rsflag, nc + 1);  // svw: the winners' spawned shadows
-  GROW(I->rnsh, 8);
-  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, 8, s));
+  GROW(I->rnsh, kWinCounterBytes);
+  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, kWinCounterBytes, s));
   if (split && nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
   if (rounds == 2)
     HIPCHK(c, launch_rep_win2(s, keys, tk, keys2, tk2, lp, I->rsvalid.as<uint8_t>(), nc,
@@ -1166,7 +1167,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   GROW(I->arec, nc * 64 + 64);
   GROW(I->ascratch, ao_scratch_bytes(nc, ns));
   GROW(I->afields, words * 4 + 4);
-  GROW(I->acount, 8);
+  GROW(I->acount, 16);
   if (rec) GROW(I->rhit_c, nc * 48 + 48);
   RepAoArgs A{};
   A.nc = nc;
@@ -1207,9 +1208,22 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
                                     I->alv.as<float>(), I->arec.as<float>(), dcount,
                                     I->ascratch.p));
     MARK(5);
+    // the pairs entering this rank's boxes, compacted (the rest stay 0)
+    GROW(I->aflag, npair + 1);
+    GROW(I->aown, npair * 4 + 4);
+    size_t tsel = 0;
+    HIPCHK(c, launch_select_flagged(s, nullptr, npair, nullptr, nullptr, nullptr, &tsel));
+    GROW(I->asel_tmp, tsel);
+    HIPCHK(c, hipMemsetAsync(I->aocc_p.p, 0, npair, s));
+    HIPCHK(c, launch_ao_own_flags(s, view(c), npair, I->apairs.as<uint32_t>(),
+                                  I->arec.as<float>(), I->alv.as<float>(), ns, dcount,
+                                  I->aflag.as<uint8_t>()));
+    HIPCHK(c, launch_select_flagged(s, I->aflag.as<uint8_t>(), npair, I->aown.as<uint32_t>(),
+                                    dcount + 1, I->asel_tmp.p, &tsel));
     HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
-                                       I->arec.as<float>(), I->alv.as<float>(), ns, dcount,
-                                       I->aocc_p.as<uint8_t>(), nullptr, true));
+                                       I->arec.as<float>(), I->alv.as<float>(), ns, dcount + 1,
+                                       I->aocc_p.as<uint8_t>(), nullptr, false,
+                                       I->aown.as<uint32_t>()));
     HIPCHK(c, launch_rep_ao_scatter(s, I->apairs.as<uint32_t>(), dcount, npair,
                                     I->aocc_p.as<uint8_t>(), ns, fb, I->afields.as<uint32_t>()));
   }
@@ -1247,7 +1261,7 @@ void free_all(spray_rt_insitu* I) {
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rheads, &I->rincl, &I->rscan_tmp,
                  &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax, &I->rtk2,
-                 &I->rtstar};
+                 &I->rtstar, &I->aflag, &I->aown, &I->asel_tmp};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)

@@ -72,13 +72,20 @@ hipError_t launch_rep_cull(hipStream_t s, const spray_rt_ray* rays, size_t n, co
 // lp[j] = list position of keys[j] where its t bits equal tmin[j], else 0xFF
 hipError_t launch_rep_lp(hipStream_t s, const uint64_t* keys, const uint32_t* tmin, size_t nc,
                          uint8_t* lp);
+// The winners' shadow count: kWinCounters u64 counters kWinStride u64
+// apart (one block adds to counter blockIdx % kWinCounters: a pass over C'
+// with one address would serialise ~nc / 64 atomics at one L2 channel);
+// launch_rep_totals sums them.  Zero kWinCounterBytes before the pass.
+constexpr int kWinCounters = 64;
+constexpr int kWinStride = 32;  // 256 B
+constexpr size_t kWinCounterBytes = size_t(kWinCounters) * kWinStride * 8;
 // win[j] = keys[j] is the group's minimum (t bits == tmin and list position
-// == lpmin, or, lpmin null, keys == kmin); svw = win && sv; *nshadow += svw
+// == lpmin, or, lpmin null, keys == kmin); svw = win && sv; nshadow += svw
 hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* tmin,
                           const uint8_t* lpmin, const uint64_t* kmin, const uint8_t* sv, size_t nc,
                           uint8_t* win, uint8_t* svw, unsigned long long* nshadow);
 // two-round keys: the winner of ray j (round 2's at (tb, lpmin) where tb
-// exists, else round 1's at ta); svw = win && sv; *nshadow += svw
+// exists, else round 1's at ta); svw = win && sv; nshadow += svw
 hipError_t launch_rep_win2(hipStream_t s, const uint64_t* keys1, const uint32_t* ta,
                            const uint64_t* keys2, const uint32_t* tb, const uint8_t* lpmin,
                            const uint8_t* sv, size_t nc, uint8_t* win, uint8_t* svw,
@@ -103,7 +110,7 @@ hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t*
 // image[4 slot_pix[q] + k] += compact[3 q + k], q < np
 hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
                              const float* compact, size_t np);
-// tail[64 c + k] = bit k of {nrad, *nshadow, 0}[c] (192 bytes)
+// tail[64 c + k] = bit k of {nrad, the nshadow counters' sum, 0}[c] (192 bytes)
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow);
 // ---- replicated-ray AO frames (insitu.cpp, trace_replicated_ao) ----

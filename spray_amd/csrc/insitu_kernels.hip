@@ -313,7 +313,9 @@ __global__ void k_rep_totals(uint8_t* __restrict__ tail, unsigned long long nrad
                              const unsigned long long* __restrict__ nshadow) {
   const int k = threadIdx.x;  // 192 threads
   const int c = k >> 6, b = k & 63;
-  const unsigned long long v = c == 0 ? nrad : (c == 1 ? *nshadow : 0ull);
+  unsigned long long v = c == 0 ? nrad : 0ull;
+  if (c == 1)
+    for (int q = 0; q < kWinCounters; ++q) v += nshadow[size_t(q) * kWinStride];
   tail[k] = uint8_t((v >> b) & 1ull);
 }
 
@@ -532,6 +534,19 @@ __global__ __launch_bounds__(kBlock) void k_rep_lp(const uint64_t* __restrict__ 
   lp[j] = cand ? uint8_t((key >> 16) & 0xFFu) : uint8_t(0xFF);
 }
 
+// a block's winners' shadows (cnt per wave) into its spread counter
+__device__ __forceinline__ void win_count(int cnt, unsigned long long* nshadow) {
+  __shared__ int part[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+    if (t) atomicAdd(nshadow + size_t(blockIdx.x % kWinCounters) * kWinStride,
+                     (unsigned long long)t);
+  }
+}
+
 // the winner of ray j: its key's t and list position are the group's minima
 // (lpmin null: kmin holds the whole 64-bit minimum key); svw = the winner's
 // spawned shadow; *nshadow += this rank's winners' shadows
@@ -555,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_rep_win(const uint64_t* __restrict__
     svw[j] = s;
   }
   const uint64_t b = __ballot(s);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(nshadow, (unsigned long long)__popcll(b));
+  win_count(__popcll(b), nshadow);
 }
 
 // 64-bit keys: the minimum t bits for the shadow rays
@@ -605,7 +620,7 @@ __global__ __launch_bounds__(kBlock) void k_rep_win2(const uint64_t* __restrict_
     svw[j] = s;
   }
   const uint64_t bb = __ballot(s);
-  if ((threadIdx.x & 63) == 0 && bb) atomicAdd(nshadow, (unsigned long long)__popcll(bb));
+  win_count(__popcll(bb), nshadow);
 }
 
 __global__ __launch_bounds__(kBlock) void k_min_u32(const uint32_t* __restrict__ a,

@@ -199,7 +199,15 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters, bool cull_own = false);
+                                    unsigned long long* counters, bool cull_own = false,
+                                    const uint32_t* idx = nullptr);
+// flag[k] = AO pair k (k < min(*d_count, max_n)) enters a resident domain's
+// box, 0 for the rest of [0, max_n): the replicated AO frame traces only
+// the flagged pairs (idx of launch_occluded_ao_pairs, from
+// launch_select_flagged).
+hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
+                               const uint32_t* pairs, const float* rec, const float* lv,
+                               int nsamples, const uint32_t* d_count, uint8_t* flag);
 size_t ao_scratch_bytes(size_t M, int nsamples);
 
 // ---- out-of-core path (ooc_kernels.hip) ----

@@ -639,9 +639,10 @@ __device__ __forceinline__ bool occluded_tree_q4_group(const void* nodes, const 
   const uint64_t gm = 0xFFull << (lane & ~7u);
   const char* nbytes = static_cast<const char*>(nodes);
   QRay qr;
-  {
-    const float4 base = ld4(nbytes - sizeof(QGrid), 0);
-    const float4 scale = ld4(nbytes - sizeof(QGrid), 1);
+  {  // nodes null (no resident tree for the group): act is false, no load
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f), one = make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 base = nbytes ? ld4(nbytes - sizeof(QGrid), 0) : z;
+    const float4 scale = nbytes ? ld4(nbytes - sizeof(QGrid), 1) : one;
     q_axis(base.x, scale.x, r.ix, r.ox * r.ix, qr.ix, qr.olx, qr.ohx);
     q_axis(base.y, scale.y, r.iy, r.oy * r.iy, qr.iy, qr.oly, qr.ohy);
     q_axis(base.z, scale.z, r.iz, r.oz * r.iz, qr.iz, qr.olz, qr.ohz);
@@ -652,7 +653,8 @@ __device__ __forceinline__ bool occluded_tree_q4_group(const void* nodes, const 
   for (;;) {
     if (cur != kNone && !(__ballot(alive) & gm)) cur = kNone;  // every lane occluded
     if (!__ballot(cur != kNone)) break;
-    if (cur >= 0) {
+    // kNone is INT_MAX: a finished group idles here while others walk
+    if (cur >= 0 && cur != kNone) {
       const char* qp = nbytes - 128 - 64 * size_t(cur);
       const float4 v = ld4(qp, ql);  // the quad's four lanes: one 16-B piece each
       const float4 a = quad_bcast4(v, 0), b = quad_bcast4(v, 1), c = quad_bcast4(v, 2),
@@ -708,21 +710,24 @@ __device__ __forceinline__ bool occluded_tree_q4_group(const void* nodes, const 
   return hit;
 }
 
+// Every lane of the wave calls this (the quad broadcasts read neighbours):
+// valid = the lane's ray exists, walk = it is traced (valid && not culled);
+// a valid lane that does not walk stores "not occluded".
 template <int W>
 __device__ __forceinline__ void scene_ray_ao_group(const SceneArgs& A, size_t i, bool valid,
-                                                   const float4* stl, const float* sbox,
-                                                   const float4* sdom, int32_t* gstk,
-                                                   int32_t* wstk) {
+                                                   bool walk, const float4* stl,
+                                                   const float* sbox, const float4* sdom,
+                                                   int32_t* gstk, int32_t* wstk) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t gm = 0xFFull << (lane & ~7u);
   v4f a = v4f{0.f, 0.f, 0.f, kRayEpsilon}, b = v4f{0.f, 0.f, 1.f, kInf};
-  if (valid) ao_gen(A, i, a, b);
+  if (walk) ao_gen(A, i, a, b);
   const float4 o4 = make_float4(a.x, a.y, a.z, a.w), d4 = make_float4(b.x, b.y, b.z, b.w);
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
   uint64_t m[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) m[w] = 0;
-  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
+  if (walk) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
   bool occluded = false;
   for (;;) {
     bool has = false;
@@ -1454,13 +1459,13 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             A, j, stl, sbox, sdom, stk, wstk, nnode, ntri, nvisit, flag, pos, wi, r6);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+    else if (kGroup)
+      scene_ray_ao_group<W>(A, i, ok, ok && (!A.rep_cull || ao_own(A, i, sbox, sres, nres)), stl,
+                            sbox, sdom, stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
     else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
       A.occ[i] = 0;
     else if (kSpread)
       scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task, my_hit);
-    else if (kGroup)
-      scene_ray_ao_group<W>(A, i, ok, stl, sbox, sdom, stack + (threadIdx.x >> 3) * kQ4Stack,
-                            wstk);
     else if (ok)
       scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
@@ -1534,14 +1539,15 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
                 });
           } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
+          else if (kGroup)
+            scene_ray_ao_group<W>(A, i, ok,
+                                  ok && (!A.rep_cull || ao_own(A, i, sbox, sres, nres)), stl,
+                                  sbox, sdom, stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
           else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
             A.occ[i] = 0;
           else if (kSpread)
             scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task,
                                              my_hit);
-          else if (kGroup)
-            scene_ray_ao_group<W>(A, i, ok, stl, sbox, sdom,
-                                  stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
           else if (rep_epi(EPI)) {
             float r6[6];
             if (rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres))
@@ -2883,11 +2889,13 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters, bool cull_own) {
+                                    unsigned long long* counters, bool cull_own,
+                                    const uint32_t* idx) {
   if (max_n == 0) return hipSuccess;
   SceneArgs a = scene_args(v, nullptr, max_n);
   a.rep_cull = cull_own ? 1 : 0;
   a.d_count = d_count;
+  a.idx = idx;
   a.occ = occ;
   a.counters = counters;
   a.ao_pairs = pairs;
@@ -2895,6 +2903,50 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
   a.ao_lv = reinterpret_cast<const float4*>(lv);
   a.ao_ns = nsamples;
   return launch_scene_w<true, kEpiAoGen>(s, a, v);
+}
+
+// Replicated AO frames: flag[k] = AO pair k (k < min(*d_count, M)) enters
+// a resident domain's box (ao_own, the in-lane cull's test).  The flagged
+// pairs are compacted and traced alone: culled lanes inside a traced wave
+// would still wait for its slowest lane, so the in-lane cull alone leaves a
+// rank's launch as long as the whole frame's.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint8_t* flag) {
+  __shared__ float sbox[6 * 64 * W];
+  __shared__ uint8_t sres[64 * W];
+  __shared__ int nres;
+  for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
+  if (threadIdx.x == 0) {
+    int q = 0;
+    for (int d = 0; d < A.ndom; ++d) {
+      const float4 t = ld4(A.domtrav, d);
+      if (__float_as_uint(t.x) | __float_as_uint(t.y)) sres[q++] = uint8_t(d);
+    }
+    nres = q;
+  }
+  __syncthreads();
+  const size_t n = A.d_count ? min(size_t(*A.d_count), A.M) : A.M;
+  for (size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x; k < A.M;
+       k += size_t(gridDim.x) * kBlock)
+    flag[k] = k < n && ao_own(A, k, sbox, sres, nres) ? 1 : 0;
+}
+
+hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
+                               const uint32_t* pairs, const float* rec, const float* lv,
+                               int nsamples, const uint32_t* d_count, uint8_t* flag) {
+  if (max_n == 0) return hipSuccess;
+  SceneArgs a = scene_args(v, nullptr, max_n);
+  a.d_count = d_count;
+  a.ao_pairs = pairs;
+  a.ao_rec = reinterpret_cast<const float4*>(rec);
+  a.ao_lv = reinterpret_cast<const float4*>(lv);
+  a.ao_ns = nsamples;
+  const unsigned g = unsigned(std::min<size_t>((max_n + kBlock - 1) / kBlock, 65536));
+  if (a.ndom <= 64)
+    k_ao_own_flags<1><<<g, kBlock, 0, s>>>(a, flag);
+  else
+    k_ao_own_flags<4><<<g, kBlock, 0, s>>>(a, flag);
+  return hipGetLastError();
 }
 
 size_t ao_scratch_bytes(size_t M, int nsamples) {
