@@ -26,6 +26,15 @@ constexpr int kWaves = kBlock / 64;
 #define SPRAY_OOC_MASK_BLOCKS 3072
 #endif
 constexpr unsigned kOocMaskBlocks = SPRAY_OOC_MASK_BLOCKS;
+// diagnostic builds only (timing of k_ooc_masks' parts; wrong queues):
+// 1 = no box confirmation, 2 = no per-block counts, 3 = top-level walk only
+// the per-lane weight table of k_ooc_masks (0: the LDS entry lists, A/B)
+#ifndef SPRAY_OOC_MASK_TAB
+#define SPRAY_OOC_MASK_TAB 1
+#endif
+#ifndef SPRAY_OOC_MASK_DIAG
+#define SPRAY_OOC_MASK_DIAG 0
+#endif
 // adaptive any-hit drains: the largest id span of a wave's rays that still
 // walks as a packet (8 pixels x 8 spp = 64 consecutive camera rays)
 // waves per SIMD the any-hit drain is compiled for (register budget)
@@ -106,8 +115,14 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
   __shared__ float4 stl[4 * 64 * W];
   __shared__ float sbox[6 * 64 * W];
   __shared__ uint32_t cnt[64 * W], sc[64 * W];
-  __shared__ float lte[kLaneList][kBlock];
-  __shared__ int lid[kLaneList][kBlock];
+  // up to 64 domains (W == 1): a lane's confirmed entries in registers and
+  // its weights in a per-lane table (wtab[domain][lane], 16 KB), so the
+  // per-domain sums below read one byte per (lane, domain); wider scenes
+  // keep kLaneList entries in LDS and look weights up by scanning them
+  constexpr bool kTab = W == 1 && SPRAY_OOC_MASK_TAB;
+  __shared__ float lte[kTab ? 1 : kLaneList][kBlock];
+  __shared__ int lid[kTab ? 1 : kLaneList][kBlock];
+  __shared__ uint8_t wtab[kTab ? 64 : 1][kBlock];
   // the top-level tree and the boxes are staged once per block, which then
   // walks ray blocks rb = blockIdx.x, + gridDim.x, ... (one launch-wide
   // staging of 5.5 KB per ray block of 256 rays was 180 MB of L2 reads per
@@ -131,10 +146,14 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
       const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
       tlas_mask_wave<W>(stl, ntlas, wstack + (threadIdx.x >> 6) * kStack, r, o4, d4, m);
     }
-    // confirm; the confirmed entry t's go to the lane's LDS list
+    // confirm; the confirmed entry t's go to the lane's list (registers
+    // for kTab: kReg slots filled by unrolled selects, no dynamic index)
+    constexpr int kReg = 16;
+    float rte[kTab ? kReg : 1];
+    int rid[kTab ? kReg : 1];
     uint32_t k = 0;
     const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-    if (live) {
+    if (live && SPRAY_OOC_MASK_DIAG != 1 && SPRAY_OOC_MASK_DIAG != 3) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         uint64_t bits = m[w];
@@ -143,7 +162,14 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
           bits &= bits - 1;
           float te;
           if (aabb_ref(sbox + 6 * (64 * w + j), dr, te)) {
-            if (k < kLaneList) {
+            if constexpr (kTab) {
+#pragma unroll
+              for (int q = 0; q < kReg; ++q)
+                if (uint32_t(q) == k) {
+                  rte[q] = te;
+                  rid[q] = 64 * w + j;
+                }
+            } else if (k < kLaneList) {
               lte[k][threadIdx.x] = te;
               lid[k][threadIdx.x] = 64 * w + j;
             }
@@ -155,8 +181,44 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
       }
     }
     // list position of each confirmed domain = its rank by (entry t, id);
-    // the weight goes into the entry's upper half
-    if (k <= kLaneList)
+    // the DomainStats weight to wtab (kTab) or the entry's upper half
+    if constexpr (kTab) {
+      // the wave's longest list bounds the unrolled loops (a scalar exit:
+      // sky waves and dead slots skip them)
+      uint32_t kmax = k;
+      for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, uint32_t(__shfl_xor(int(kmax), o)));
+      kmax = uint32_t(__builtin_amdgcn_readfirstlane(int(kmax)));
+      if (SPRAY_OOC_MASK_DIAG < 2) {
+        if (k <= uint32_t(kReg)) {
+#pragma unroll
+          for (int a = 0; a < kReg; ++a) {
+            if (uint32_t(a) >= kmax) break;
+            uint32_t pos = 0;
+#pragma unroll
+            for (int b = 0; b < kReg; ++b) {
+              if (uint32_t(b) >= kmax) break;
+              pos += (uint32_t(b) < k &&
+                      (rte[b] < rte[a] || (rte[b] == rte[a] && rid[b] < rid[a])))
+                         ? 1u
+                         : 0u;
+            }
+            if (uint32_t(a) < k)
+              wtab[rid[a]][threadIdx.x] =
+                  uint8_t(pos < kDomainListSize ? kDomainListSize - pos : 1u);
+          }
+        } else {  // a longer list: positions from the mask (boxes re-tested)
+          uint64_t bits = m[0];
+          while (bits) {
+            const int j = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            float te;
+            aabb_ref(sbox + 6 * j, dr, te);
+            const uint32_t pos = list_pos<W>(m, sbox, j, te, dr);
+            wtab[j][threadIdx.x] = uint8_t(pos < kDomainListSize ? kDomainListSize - pos : 1u);
+          }
+        }
+      }
+    } else if (k <= kLaneList && SPRAY_OOC_MASK_DIAG < 2)
       for (uint32_t a = 0; a < k; ++a) {
         const float ta = lte[a][threadIdx.x];
         const int da = lid[a][threadIdx.x] & 0xFFFF;
@@ -170,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
     // per domain of the wave: pairs and weights summed over the wave first
     // (a wave's rays mostly share domains: same-address LDS atomics serialise)
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
+    for (int w = 0; w < (SPRAY_OOC_MASK_DIAG >= 2 ? 0 : W); ++w) {
       uint64_t u = wave_or64(m[w]);
       while (u) {
         const int j = __ffsll((long long)u) - 1;
@@ -179,7 +241,9 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
         const bool has = (m[w] >> j) & 1;
         uint32_t add = 0;
         if (has) {
-          if (k <= kLaneList) {
+          if constexpr (kTab) {
+            add = wtab[dom][threadIdx.x];
+          } else if (k <= kLaneList) {
             for (uint32_t a = 0; a < k; ++a) {
               const int e = lid[a][threadIdx.x];
               if ((e & 0xFFFF) == dom) add = uint32_t(e) >> 16;
