@@ -27,7 +27,8 @@ constexpr int kWaves = kBlock / 64;
 #endif
 constexpr unsigned kOocMaskBlocks = SPRAY_OOC_MASK_BLOCKS;
 // diagnostic builds only (timing of k_ooc_masks' parts; wrong queues):
-// 1 = no box confirmation, 2 = no per-block counts, 3 = top-level walk only
+// 1 = no box confirmation, 2 = no per-block counts, 3 = top-level walk only,
+// 4 = positions without the per-domain sums, 5 = the sums without positions
 // the per-lane weight table of k_ooc_masks (0: the LDS entry lists, A/B)
 #ifndef SPRAY_OOC_MASK_TAB
 #define SPRAY_OOC_MASK_TAB 1
@@ -93,6 +94,31 @@ __device__ __forceinline__ uint32_t list_pos(const uint64_t* m, const float* box
   return p;
 }
 
+// Ascending (t, id) over the first N of a lane's register entries: a
+// bitonic sorting network, every index a compile-time constant.
+template <int N, int R>
+__device__ __forceinline__ void sort_entries(float (&t)[R], int (&id)[R]) {
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l <= i) continue;
+        const bool up = (i & k) == 0;
+        const bool gt = t[i] > t[l] || (t[i] == t[l] && id[i] > id[l]);
+        if (gt == up) {
+          const float tt = t[i];
+          t[i] = t[l];
+          t[l] = tt;
+          const int ti = id[i];
+          id[i] = id[l];
+          id[l] = ti;
+        }
+      }
+}
+
 // Confirmed domains a lane keeps in LDS for its list positions (longer
 // lists recompute positions from the mask).
 constexpr int kLaneList = 8;
@@ -149,6 +175,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
     // confirm; the confirmed entry t's go to the lane's list (registers
     // for kTab: kReg slots filled by unrolled selects, no dynamic index)
     constexpr int kReg = 16;
+    static_assert(kReg >= int(kDomainListSize), "positions past the list size weigh 1");
     float rte[kTab ? kReg : 1];
     int rid[kTab ? kReg : 1];
     uint32_t k = 0;
@@ -163,12 +190,37 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
           float te;
           if (aabb_ref(sbox + 6 * (64 * w + j), dr, te)) {
             if constexpr (kTab) {
+              // the kReg nearest entries (te, id) stay; any other one is past
+              // list position kReg - 1 >= kDomainListSize - 1: weight 1
+              const int d = 64 * w + j;
+              wtab[d][threadIdx.x] = 1;
+              if (k < uint32_t(kReg)) {
 #pragma unroll
-              for (int q = 0; q < kReg; ++q)
-                if (uint32_t(q) == k) {
-                  rte[q] = te;
-                  rid[q] = 64 * w + j;
+                for (int q = 0; q < kReg; ++q)
+                  if (uint32_t(q) == k) {
+                    rte[q] = te;
+                    rid[q] = d;
+                  }
+              } else {
+                int qm = 0;
+                float tm = rte[0];
+                int im = rid[0];
+#pragma unroll
+                for (int q = 1; q < kReg; ++q)
+                  if (rte[q] > tm || (rte[q] == tm && rid[q] > im)) {
+                    qm = q;
+                    tm = rte[q];
+                    im = rid[q];
+                  }
+                if (te < tm || (te == tm && d < im)) {
+#pragma unroll
+                  for (int q = 0; q < kReg; ++q)
+                    if (q == qm) {
+                      rte[q] = te;
+                      rid[q] = d;
+                    }
                 }
+              }
             } else if (k < kLaneList) {
               lte[k][threadIdx.x] = te;
               lid[k][threadIdx.x] = 64 * w + j;
@@ -188,35 +240,24 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
       uint32_t kmax = k;
       for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, uint32_t(__shfl_xor(int(kmax), o)));
       kmax = uint32_t(__builtin_amdgcn_readfirstlane(int(kmax)));
-      if (SPRAY_OOC_MASK_DIAG < 2) {
-        if (k <= uint32_t(kReg)) {
+      if ((SPRAY_OOC_MASK_DIAG < 2 || SPRAY_OOC_MASK_DIAG == 4) && kmax) {
+        // sort the kept entries by (entry t, id) with a bitonic network in
+        // registers (empty slots last); a slot's index is its list position
+        const uint32_t nk = min(k, uint32_t(kReg));
 #pragma unroll
-          for (int a = 0; a < kReg; ++a) {
-            if (uint32_t(a) >= kmax) break;
-            uint32_t pos = 0;
+        for (int q = 0; q < kReg; ++q)
+          if (uint32_t(q) >= nk) {
+            rte[q] = kInf;
+            rid[q] = INT_MAX;
+          }
+        if (kmax <= 8)
+          sort_entries<8>(rte, rid);
+        else
+          sort_entries<kReg>(rte, rid);
 #pragma unroll
-            for (int b = 0; b < kReg; ++b) {
-              if (uint32_t(b) >= kmax) break;
-              pos += (uint32_t(b) < k &&
-                      (rte[b] < rte[a] || (rte[b] == rte[a] && rid[b] < rid[a])))
-                         ? 1u
-                         : 0u;
-            }
-            if (uint32_t(a) < k)
-              wtab[rid[a]][threadIdx.x] =
-                  uint8_t(pos < kDomainListSize ? kDomainListSize - pos : 1u);
-          }
-        } else {  // a longer list: positions from the mask (boxes re-tested)
-          uint64_t bits = m[0];
-          while (bits) {
-            const int j = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            float te;
-            aabb_ref(sbox + 6 * j, dr, te);
-            const uint32_t pos = list_pos<W>(m, sbox, j, te, dr);
-            wtab[j][threadIdx.x] = uint8_t(pos < kDomainListSize ? kDomainListSize - pos : 1u);
-          }
-        }
+        for (int a = 0; a < kReg; ++a)
+          if (uint32_t(a) < nk)
+            wtab[rid[a]][threadIdx.x] = uint8_t(a < int(kDomainListSize) ? kDomainListSize - a : 1u);
       }
     } else if (k <= kLaneList && SPRAY_OOC_MASK_DIAG < 2)
       for (uint32_t a = 0; a < k; ++a) {
@@ -232,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
     // per domain of the wave: pairs and weights summed over the wave first
     // (a wave's rays mostly share domains: same-address LDS atomics serialise)
 #pragma unroll
-    for (int w = 0; w < (SPRAY_OOC_MASK_DIAG >= 2 ? 0 : W); ++w) {
+    for (int w = 0; w < ((SPRAY_OOC_MASK_DIAG >= 2 && SPRAY_OOC_MASK_DIAG != 5) ? 0 : W); ++w) {
       uint64_t u = wave_or64(m[w]);
       while (u) {
         const int j = __ffsll((long long)u) - 1;
