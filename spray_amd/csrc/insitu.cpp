@@ -1465,9 +1465,14 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t I, const spray_rt_shader* P,
   if (!I->tr->has_rep())
     return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
                 "the host transport gives no allreduce_min_u64 / allreduce_sum_u8");
+  // SPRAY_INSITU_REPLICATED=1: the replicated steps even at world 1 (their
+  // collectives through a one-rank communicator: the product transport's
+  // calls on a one-GPU box)
+  const char* fr = std::getenv("SPRAY_INSITU_REPLICATED");
+  const bool force_rep = fr && fr[0] == '1';
   I->nev = 0;
   I->tr->serial_begin();
-  if (I->world == 1) {
+  if (I->world == 1 && !force_rep) {
     r = trace_local(I, P, rays, pixid, samid, n, spp, image, rec, totals);
     flush_phases(I, 1);
   } else {

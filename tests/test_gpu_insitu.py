@@ -316,6 +316,22 @@ def test_engine_replicated_frame_one_rank_rccl(oracle, case):
     _check(oracle, case, [res])
 
 
+@pytest.mark.parametrize("case", ["pt1", "ao16", "pt1-u64"])
+def test_engine_replicated_steps_one_rank_rccl(oracle, case, monkeypatch):
+    """The replicated frame's steps at world 1 (SPRAY_INSITU_REPLICATED=1):
+    every collective of the N > 1 frame -- t-bits MIN, list-position MIN on
+    the side stream, occlusion SUM, run-sum reduce (PT); key MIN, published
+    normals SUM, count-field SUM (AO) -- through a one-rank RCCL
+    communicator, the same calls the driver's multi-GPU run makes."""
+    monkeypatch.setenv("SPRAY_INSITU_REPLICATED", "1")
+    if case.endswith("-u64"):
+        monkeypatch.setenv("SPRAY_INSITU_SPLIT_KEYS", "0")
+    base = case.split("-")[0]
+    res = _engine_rank(0, 1, base, "rccl", replicated=True)
+    _check(oracle, base, [res])
+    assert res[3]["collectives"] >= 6 and res[3]["exchanges"] == 0, res[3]
+
+
 def test_engine_replicated_frame_unsupported_shading(oracle):
     """Several bounces are not a replicated frame: UNSUPPORTED, and nothing
     traced."""
