@@ -332,6 +332,52 @@ def test_engine_replicated_steps_one_rank_rccl(oracle, case, monkeypatch):
     assert res[3]["collectives"] >= 6 and res[3]["exchanges"] == 0, res[3]
 
 
+@pytest.mark.parametrize("steps", ["local", "replicated"])
+@pytest.mark.parametrize("kind", ["pt", "ao"])
+def test_engine_frame_bit_reproducible(kind, steps, monkeypatch):
+    """Two frames into zeroed images are bit-identical.  The film adds each
+    pixel's samples in a wave-level segmented scan and commits a run with one
+    atomic per wave it spans; a run of <= 8 samples spans at most two waves,
+    and two addends onto zero commute exactly (a + b == b + a), so the image
+    does not depend on the waves' timing.  The replicated steps (one rank
+    through RCCL) sum each pixel run the same way into the compact film,
+    reduce it and add one run per pixel."""
+    import spray_amd
+    from spray_amd import insitu
+    from test_insitu import scene_boxes
+    if steps == "replicated":
+        monkeypatch.setenv("SPRAY_INSITU_REPLICATED", "1")
+    img, spp = 256, 8
+    boxes, bound = scene_boxes()
+    owner = insitu.morton_partition(boxes, bound, 1, 0)
+    rt = spray_amd.RtContext(0)
+    insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, 0)
+    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
+    rt.set_stream(torch.cuda.current_stream())
+    c = H.BENCH_CAMERA
+    cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    block = (0, 0, img, img)
+    n = img * img * spp
+    rays = torch.empty((n, 8), dtype=torch.float32, device="cuda")
+    pix = torch.empty(n, dtype=torch.int32, device="cuda")
+    sam = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.eye_rays_insitu(cam, img, spp, block, block, rays, pix, sam)
+    sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1,
+                                     lights=[(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)])
+    eng = insitu.InsituEngine(rt, 1, 0, transport="rccl")
+    out = []
+    for _ in range(3):
+        image = torch.zeros(img * img * 4, dtype=torch.float32, device="cuda")
+        eng.trace_frame(sh, rays, pix, sam, spp, image)
+        torch.cuda.synchronize()
+        out.append(image.cpu().numpy().view(np.uint32))
+    eng.close()
+    rt.close()
+    assert (out[0].view(np.float32) > 0).sum() > 1000
+    for o in out[1:]:
+        np.testing.assert_array_equal(o, out[0])
+
+
 def test_engine_replicated_frame_unsupported_shading(oracle):
     """Several bounces are not a replicated frame: UNSUPPORTED, and nothing
     traced."""
