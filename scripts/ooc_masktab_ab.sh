@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-masktab}
 mkdir -p "$OUT"
-for v in shipped ooc_masktab0; do
+for v in shipped ${VARS:-ooc_masktab0}; do
   L=""; [ "$v" != shipped ] && L="spray_amd/lib/diag/libspray_rt_$v.so"
   SPRAY_RT_LIB="$L" SPRAY_OOC_TRACE=1 timeout -k 10 200 python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --frame 0 --ao 0 --insitu 0 --ooc 1 > "$OUT/${v}_trace.out" 2> "$OUT/${v}_trace.err"
   rc=$?; echo "$v trace rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$OUT/${v}_trace.err"; exit $rc; }

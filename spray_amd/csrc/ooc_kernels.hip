@@ -131,8 +131,11 @@ constexpr int kLaneList = 8;
 // LIST_SIZE - list position, 1 past the list), summed in LDS, then stored
 // block-major ([block * ndom + d], one coalesced row per block).  Also
 // resets the per-ray results of the pass.
+#ifndef SPRAY_OOC_MASK_WAVES
+#define SPRAY_OOC_MASK_WAVES 6
+#endif
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_ooc_masks(
+__global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_ooc_masks(
     const BvhNode* __restrict__ tlas, int ntlas, const float* __restrict__ boxes, int ndom,
     const spray_rt_ray* __restrict__ rays, const uint8_t* __restrict__ valid, size_t M,
     uint32_t nrb, uint64_t* __restrict__ masks, uint64_t* __restrict__ key_init,
@@ -141,14 +144,15 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
   __shared__ float4 stl[4 * 64 * W];
   __shared__ float sbox[6 * 64 * W];
   __shared__ uint32_t cnt[64 * W], sc[64 * W];
-  // up to 64 domains (W == 1): a lane's confirmed entries in registers and
-  // its weights in a per-lane table (wtab[domain][lane], 16 KB), so the
-  // per-domain sums below read one byte per (lane, domain); wider scenes
-  // keep kLaneList entries in LDS and look weights up by scanning them
+  // up to 64 domains (W == 1): a lane's 16 nearest confirmed entries in
+  // registers, sorted, then packed as 16 domain bytes in list order (the
+  // per-domain sums below find a domain's position among them; LDS stays
+  // small for the latency-bound walk's occupancy); wider scenes keep
+  // kLaneList entries in LDS and look weights up by scanning them
   constexpr bool kTab = W == 1 && SPRAY_OOC_MASK_TAB;
   __shared__ float lte[kTab ? 1 : kLaneList][kBlock];
   __shared__ int lid[kTab ? 1 : kLaneList][kBlock];
-  __shared__ uint8_t wtab[kTab ? 64 : 1][kBlock];
+  uint32_t pk[4] = {~0u, ~0u, ~0u, ~0u};  // kTab: byte q = the q-th nearest domain
   // the top-level tree and the boxes are staged once per block, which then
   // walks ray blocks rb = blockIdx.x, + gridDim.x, ... (one launch-wide
   // staging of 5.5 KB per ray block of 256 rays was 180 MB of L2 reads per
@@ -193,7 +197,6 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
               // the kReg nearest entries (te, id) stay; any other one is past
               // list position kReg - 1 >= kDomainListSize - 1: weight 1
               const int d = 64 * w + j;
-              wtab[d][threadIdx.x] = 1;
               if (k < uint32_t(kReg)) {
 #pragma unroll
                 for (int q = 0; q < kReg; ++q)
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
       }
     }
     // list position of each confirmed domain = its rank by (entry t, id);
-    // the DomainStats weight to wtab (kTab) or the entry's upper half
+    // the DomainStats weight from the packed list (kTab) or the entry's upper half
     if constexpr (kTab) {
       // the wave's longest list bounds the unrolled loops (a scalar exit:
       // sky waves and dead slots skip them)
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
 #pragma unroll
         for (int a = 0; a < kReg; ++a)
           if (uint32_t(a) < nk)
-            wtab[rid[a]][threadIdx.x] = uint8_t(a < int(kDomainListSize) ? kDomainListSize - a : 1u);
+            pk[a >> 2] = (pk[a >> 2] & ~(0xFFu << (8 * (a & 3)))) | (uint32_t(rid[a]) << (8 * (a & 3)));
       }
     } else if (k <= kLaneList && SPRAY_OOC_MASK_DIAG < 2)
       for (uint32_t a = 0; a < k; ++a) {
@@ -283,7 +286,13 @@ __global__ __launch_bounds__(kBlock) void k_ooc_masks(
         uint32_t add = 0;
         if (has) {
           if constexpr (kTab) {
-            add = wtab[dom][threadIdx.x];
+            // list position = its byte among the 16 nearest (absent: past
+            // position 15, weight 1)
+            uint32_t pos = kReg;
+#pragma unroll
+            for (int q = kReg - 1; q >= 0; --q)
+              if (((pk[q >> 2] >> (8 * (q & 3))) & 0xFFu) == uint32_t(dom)) pos = uint32_t(q);
+            add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
           } else if (k <= kLaneList) {
             for (uint32_t a = 0; a < k; ++a) {
               const int e = lid[a][threadIdx.x];
