@@ -286,14 +286,17 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
         el = float(e.item())
     rays_step = tot[0] + tot[1]
     k = args.steps
-    form = ("replicated-ray frame: every rank traces the rays that touch its domains, "
-            "keys MIN-all-reduced, occlusion bytes SUM-all-reduced" if replicated and world > 1
-            and kind == "pt"
+    form = ("replicated-ray frame: every rank holds every eye ray; keyed closest hit + "
+            "shading over its domains, t-bits and list-position MINs all-reduced, shadow "
+            "rays from the minimum t, occlusion bytes SUM-all-reduced, pixel-run sums "
+            "reduced to rank 0" if replicated and world > 1 and kind == "pt"
             else "replicated-ray AO frame: keys MIN-all-reduced, winners' normals and colours "
-            "SUM-all-reduced, every rank any-hits every AO ray over its domains, occlusion "
-            "count fields SUM-all-reduced, film on rank 0" if replicated and world > 1
+            "SUM-all-reduced, every rank any-hits the AO pairs entering its boxes "
+            "(compacted), occlusion count fields SUM-all-reduced, film on rank 0"
+            if replicated and world > 1
             else "all-local frame" if replicated or (world == 1 and not protocol)
-            else "stripe protocol: speculative ray exchange over RCCL all-to-all-v")
+            else "stripe protocol: speculative ray exchange over RCCL all-to-all-v, image "
+                 "composite by RCCL reduce")
     out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
            "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
            "rays_per_step": rays_step, "radiance_rays": tot[0], "shadow_rays": tot[1],
@@ -304,8 +307,7 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
            "rank0_phases_ms": phases,
            "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
            "partition": args.partition,
-           "config": "%s: 64 domains, %d per GPU (Morton partition, %s), 1024x1024x8spp, %s, %s, "
-                     "image composite by RCCL reduce"
+           "config": "%s: 64 domains, %d per GPU (Morton partition, %s), 1024x1024x8spp, %s, %s"
                      % ("configs[4]" if kind == "ao" else "configs[2]",
                         int(np.bincount(owner, minlength=world)[rank]),
                         "round robin" if mode == insitu.PARTITION_ROUND_ROBIN else "close groups",

@@ -59,8 +59,8 @@ def fbits(n):
 SEGMENTS = {  # phases between the frame's collectives, in order
     "pt": [("cull_select", "film_slots", "keyed_shade"), ("list_pos", "shadow_trace", "winners"),
            ("film_totals",)],
-    "ao": [("route", "select", "keyed_closest_hit"), ("publish",), ("ao_spawn", "ao_trace"),
-           ("film_totals",)],
+    "ao": [("route", "cull_select", "select", "keyed_closest_hit"), ("publish",),
+           ("ao_spawn", "ao_trace", "ao_own_trace"), ("film_totals",)],
 }
 
 

@@ -307,8 +307,8 @@ class InsituEngine:
     # replicated-ray frames (insitu.cpp trace_replicated / trace_replicated_ao)
     REP_PHASES = ("cull_select", "film_slots", "keyed_shade", "list_pos", "shadow_trace",
                   "winners", "film_totals")
-    REP_AO_PHASES = ("route", "select", "keyed_closest_hit", "publish", "ao_spawn", "ao_trace",
-                     "film_totals")
+    REP_AO_PHASES = ("cull_select", "unused", "keyed_closest_hit", "publish", "ao_spawn",
+                     "ao_own_trace", "film_totals")
     _rep_kind = "pt"
     PROTOCOL_PHASES = ("route_plan", "ray_pack_unpack", "keyed_closest_hit", "key_composite",
                        "shading", "shadow_route_pack", "shadow_any_hit_return",
@@ -323,7 +323,7 @@ class InsituEngine:
         rep = self.REP_AO_PHASES if self._rep_kind == "ao" else self.REP_PHASES
         names = {7: rep, 8: self.PROTOCOL_PHASES, 1: ("frame",)}.get(
             n.value, tuple("phase%d" % k for k in range(n.value)))
-        d = {names[k]: float(out[k]) for k in range(n.value)}
+        d = {names[k]: float(out[k]) for k in range(n.value) if names[k] != "unused"}
         d["collectives"] = float(out[8])
         return d
 
