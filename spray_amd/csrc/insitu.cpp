@@ -1113,17 +1113,19 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
 }
 
 // The replicated-ray AO frame (ooc::ShaderAo, one bounce, diffuse
-// surfaces): steps 1-3 as trace_replicated; then the winners publish their
-// hits' shading normal and colour (a SUM all-reduce, 16 B per ray of C), so
-// every rank holds every hit's AO spawn input and spawns the same (source,
-// sample) pairs (launch_spawn_ao_pairs, ao_ok exact); each traces them over
-// its own domains; a SUM all-reduce of per-sample occlusion count fields
-// (fb bits each, position j * ns + l) ORs the group's results; rank 0 then
-// holds every weight and occlusion and films the whole frame (the other
-// ranks' images stay untouched: no composite is needed).  Records: each rank
-// its winners.  Totals: radiance rays n, AO rays = the pairs (the same count
-// on every rank), no all-reduce.  Phases: 0 lists, 1 keyed closest hit,
-// 2 AO rays (publish, spawn, any hit), 3 film, 4 totals.
+// surfaces): C' and the keyed closest hit as trace_replicated, then the
+// 64-bit key MIN; the winners publish their hits' shading normal and colour
+// (a SUM all-reduce, 16 B per ray of C'), so every rank holds every hit's AO
+// spawn input and spawns the same (source, sample) pairs
+// (launch_spawn_ao_pairs, ao_ok exact); each compacts the pairs entering its
+// domain boxes (launch_ao_own_flags + select) and any-hits them over its own
+// domains; a SUM all-reduce of per-sample occlusion count fields (fb bits
+// each, position j * ns + l) ORs the group's results; rank 0 then holds
+// every weight and occlusion and films the whole frame (the other ranks'
+// images stay untouched: no composite is needed).  Records: each rank its
+// winners.  Totals: radiance rays n, AO rays = the pairs (the same count on
+// every rank), no all-reduce.  Phases: 0 cull + select, 2 keyed closest hit,
+// 3 publish, 4 AO spawn, 5 own pairs + any hit + count fields, 6 film.
 int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
                         const int32_t* pixid, const int32_t* samid, size_t n, int spp,
                         float* image, const spray_rt_insitu_rec* rec,

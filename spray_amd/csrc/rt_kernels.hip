@@ -594,191 +594,14 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   }
 }
 
-// AO any hit in groups of 8 lanes (SPRAY_AO_GROUP=1).  In the sample-major
-// trace order the 8 lanes of an aligned group are, as a rule, the spp rays
-// of one pixel for one hemisphere sample: the same direction from origins a
-// sub-pixel apart.  The group walks as a packet of 8: its domain order is
-// its first live lane's, its current node and stack are group-uniform (stack
-// in LDS), a child is entered when any live lane's conservative test accepts
-// it (nearest first by the first live lane's entry distance), and each lane
-// tests its own ray against the triangles of the leaves the group visits.
-// A node's 64 B come in with one 16-B load per quad lane (lanes 0-3 and 4-7
-// of a group fetch the same node) and reach every lane of the quad by DPP
-// broadcasts -- 64 lanes x 16 B through the vector memory path per node
-// step instead of 4 x 64 x 16 B -- and a triangle's 48 B likewise.  A lane
-// only ever skips boxes its own test rejected, and testing more triangles
-// cannot change an any-hit answer, so the bits are the per-lane walk's.
 #ifndef SPRAY_AO_GROUP
 #define SPRAY_AO_GROUP 0
 #endif
-template <int SEL>
-__device__ __forceinline__ float quad_bcast(float v) {  // lane SEL of each quad
-  return __int_as_float(
-      __builtin_amdgcn_mov_dpp(__float_as_int(v), SEL * 0x55, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float4 quad_bcast4(const float4& v, int sel) {
-  switch (sel) {
-    case 0: return make_float4(quad_bcast<0>(v.x), quad_bcast<0>(v.y), quad_bcast<0>(v.z),
-                               quad_bcast<0>(v.w));
-    case 1: return make_float4(quad_bcast<1>(v.x), quad_bcast<1>(v.y), quad_bcast<1>(v.z),
-                               quad_bcast<1>(v.w));
-    case 2: return make_float4(quad_bcast<2>(v.x), quad_bcast<2>(v.y), quad_bcast<2>(v.z),
-                               quad_bcast<2>(v.w));
-    default: return make_float4(quad_bcast<3>(v.x), quad_bcast<3>(v.y), quad_bcast<3>(v.z),
-                                quad_bcast<3>(v.w));
-  }
-}
-
-// One domain tree, the groups whose lanes have it on their list (act).
-// gstk: the group's kQ4Stack entries of LDS.  Returns the lane's occlusion.
-__device__ __forceinline__ bool occluded_tree_q4_group(const void* nodes, const void* tris,
-                                                       const Ray& r, float tnear, float tfar,
-                                                       bool act, int32_t* gstk) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t ql = lane & 3u;
-  const uint64_t gm = 0xFFull << (lane & ~7u);
-  const char* nbytes = static_cast<const char*>(nodes);
-  QRay qr;
-  {  // nodes null (no resident tree for the group): act is false, no load
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f), one = make_float4(1.f, 1.f, 1.f, 1.f);
-    const float4 base = nbytes ? ld4(nbytes - sizeof(QGrid), 0) : z;
-    const float4 scale = nbytes ? ld4(nbytes - sizeof(QGrid), 1) : one;
-    q_axis(base.x, scale.x, r.ix, r.ox * r.ix, qr.ix, qr.olx, qr.ohx);
-    q_axis(base.y, scale.y, r.iy, r.oy * r.iy, qr.iy, qr.oly, qr.ohy);
-    q_axis(base.z, scale.z, r.iz, r.oz * r.iz, qr.iz, qr.olz, qr.ohz);
-  }
-  bool alive = act, hit = false;
-  int32_t cur = (__ballot(act) & gm) ? 0 : kNone;  // group-uniform
-  int sp = 0;
-  for (;;) {
-    if (cur != kNone && !(__ballot(alive) & gm)) cur = kNone;  // every lane occluded
-    if (!__ballot(cur != kNone)) break;
-    // kNone is INT_MAX: a finished group idles here while others walk
-    if (cur >= 0 && cur != kNone) {
-      const char* qp = nbytes - 128 - 64 * size_t(cur);
-      const float4 v = ld4(qp, ql);  // the quad's four lanes: one 16-B piece each
-      const float4 a = quad_bcast4(v, 0), b = quad_bcast4(v, 1), c = quad_bcast4(v, 2),
-                   d = quad_bcast4(v, 3);
-      const int32_t ref[4] = {__float_as_int(d.x), __float_as_int(d.y), __float_as_int(d.z),
-                              __float_as_int(d.w)};
-      float t[4];
-      bool h[4];
-      h[0] = slab_q(qr, q_lo(a.x), q_hi(a.x), q_lo(a.y), q_hi(a.y), q_lo(a.z), q_hi(a.z),
-                    tnear, tfar, t[0]);
-      h[1] = slab_q(qr, q_lo(a.w), q_hi(a.w), q_lo(b.x), q_hi(b.x), q_lo(b.y), q_hi(b.y),
-                    tnear, tfar, t[1]);
-      h[2] = slab_q(qr, q_lo(b.z), q_hi(b.z), q_lo(b.w), q_hi(b.w), q_lo(c.x), q_hi(c.x),
-                    tnear, tfar, t[2]);
-      h[3] = slab_q(qr, q_lo(c.y), q_hi(c.y), q_lo(c.z), q_hi(c.z), q_lo(c.w), q_hi(c.w),
-                    tnear, tfar, t[3]);
-      const uint64_t la_b = __ballot(alive) & gm;
-      const int la = la_b ? __ffsll((long long)la_b) - 1 : int(lane);
-      int32_t next = kNone;
-      float tn = kInf;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool e = (__ballot(alive && h[k]) & gm) != 0 && ref[k] != kNoChildRef;
-        // the first live lane's entry distance orders the entered children
-        const float tl = __shfl((alive && h[k]) ? t[k] : kInf, la);
-        if (!e) continue;
-        if (next == kNone || tl < tn) {
-          if (next != kNone) gstk[sp++] = next;
-          next = ref[k];
-          tn = tl;
-        } else {
-          gstk[sp++] = ref[k];
-        }
-      }
-      cur = next != kNone ? next : (sp ? gstk[--sp] : kNone);
-    } else if (cur != kNone) {
-      const uint32_t enc = ~uint32_t(cur);
-      const uint32_t first = enc >> 2, cnt = (enc & 3u) + 1u;
-      for (uint32_t q = 0; q < cnt; ++q) {
-        // lanes 0-2 of the quad fetch the triangle's three 16-B pieces
-        const float4 v = ql < 3 ? ld4(tris, 3 * size_t(first + q) + ql)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 ta = quad_bcast4(v, 0), tb = quad_bcast4(v, 1), tc = quad_bcast4(v, 2);
-        float tt, tu, tv;
-        if (alive && tri_test(r, tnear, ta, tb, tc, tt, tu, tv) && tt <= tfar) {
-          alive = false;
-          hit = true;
-        }
-      }
-      cur = sp ? gstk[--sp] : kNone;
-    }
-  }
-  return hit;
-}
-
-// Every lane of the wave calls this (the quad broadcasts read neighbours):
-// valid = the lane's ray exists, walk = it is traced (valid && not culled);
-// a valid lane that does not walk stores "not occluded".
+// SPRAY_AO_GROUP=1 (rt_kernels_diag.inc): the AO any hit in 8-lane groups
 template <int W>
-__device__ __forceinline__ void scene_ray_ao_group(const SceneArgs& A, size_t i, bool valid,
-                                                   bool walk, const float4* stl,
-                                                   const float* sbox, const float4* sdom,
-                                                   int32_t* gstk, int32_t* wstk) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t gm = 0xFFull << (lane & ~7u);
-  v4f a = v4f{0.f, 0.f, 0.f, kRayEpsilon}, b = v4f{0.f, 0.f, 1.f, kInf};
-  if (walk) ao_gen(A, i, a, b);
-  const float4 o4 = make_float4(a.x, a.y, a.z, a.w), d4 = make_float4(b.x, b.y, b.z, b.w);
-  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  uint64_t m[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) m[w] = 0;
-  if (walk) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
-  bool occluded = false;
-  for (;;) {
-    bool has = false;
-#pragma unroll
-    for (int w = 0; w < W; ++w) has |= m[w] != 0;
-    has = has && !occluded;
-    const uint64_t hb = __ballot(has);
-    if (!hb) break;
-    const uint64_t gh = hb & gm;
-    const int lead = gh ? __ffsll((long long)gh) - 1 : int(lane);
-    // every live lane's nearest remaining domain (fast slab entry distance);
-    // the group takes its first live lane's: the order only steers culling
-    int sb = -1;
-    float st = kInf;
-    if (has) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        uint64_t bits = m[w];
-        while (bits) {
-          const int j = __ffsll((long long)bits) - 1;
-          bits &= bits - 1;
-          const int bx = 64 * w + j;
-          const float* bp = sbox + 6 * bx;
-          float tm;
-          slab(r, bp[0], bp[1], bp[2], bp[3], bp[4], bp[5], -kInf, kInf, tm);
-          if (sb < 0 || tm < st) {
-            st = tm;
-            sb = bx;
-          }
-        }
-      }
-    }
-    const int d = gh ? __shfl(sb, lead) : -1;
-    bool act = false;
-    if (d >= 0) {
-#pragma unroll
-      for (int w = 0; w < W; ++w)
-        if (w == (d >> 6)) {
-          act = has && ((m[w] >> (d & 63)) & 1ull);
-          m[w] &= ~(1ull << (d & 63));
-        }
-    }
-    const float4 dt = sdom[d >= 0 ? d : 0];
-    const char* nodes = reinterpret_cast<const char*>(
-        (uint64_t(__float_as_uint(dt.y)) << 32) | __float_as_uint(dt.x));
-    if (!nodes) act = false;  // not resident here (or empty)
-    const void* tris = nodes ? nodes + __float_as_uint(dt.z) : nullptr;
-    if (occluded_tree_q4_group(nodes, tris, r, o4.w, d4.w, act, gstk)) occluded = true;
-  }
-  if (valid) A.occ[i] = occluded ? 1 : 0;
-}
+__device__ void scene_ray_ao_group(const SceneArgs& A, size_t i, bool valid, bool walk,
+                                   const float4* stl, const float* sbox, const float4* sdom,
+                                   int32_t* gstk, int32_t* wstk);
 
 // Diagnostic variants of the any hit (rt_kernels_diag.inc, compiled only
 // into the builds that enable them: SPRAY_AH_SPREAD=1 -- the leaf triangles
@@ -804,7 +627,7 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 
-#if SPRAY_AH_SPREAD || SPRAY_AO_REFILL || SPRAY_WAVE_TIMES
+#if SPRAY_AH_SPREAD || SPRAY_AO_REFILL || SPRAY_WAVE_TIMES || SPRAY_AO_GROUP
 #include "rt_kernels_diag.inc"
 #endif
 
