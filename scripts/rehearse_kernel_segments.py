@@ -14,7 +14,9 @@ ms in the same process, with no other process's kernel overlapping them in
 the trace).  A multi-GPU frame has gaps of tens of microseconds.  Here a
 segment's time is the sum of its launches' durations (one stream: they
 never overlap), each launch taken at its MINIMUM over the timed frames (a
-frame issues the same launches in the same order on the same data).
+frame issues the same launches in the same order on the same data), and
+the launches whose work is identical on every rank (RANK_INDEPENDENT) at
+their minimum over the ranks too.
 
 Segments (the device work between two of the frame's collectives):
   pt: [cull + select + film slots + keyed closest hit & shading]
@@ -48,9 +50,21 @@ def _epi(name):
     return int(m.group(4)) if m else -1
 
 
+# launches whose work is the same on every rank (the eye rays, C' and the
+# published hits are identical everywhere): taken at their minimum over the
+# ranks as well -- a rank that always resumes after the longest idle gap
+# otherwise carries a clock-ramp artifact in every frame (k_rep_cull 0.06 vs
+# 1.4 ms on one rank of a run)
+RANK_INDEPENDENT = ("k_rep_cull", "k_select_count", "k_scan_blocks", "k_select_write",
+                    "k_rep_heads", "k_rep_slot_pix", "init_lookback_scan_state",
+                    "trampoline_kernel", "k_pix_bmax", "k_max_u32", "k_fill_u64",
+                    "__amd_rocclr_fillBuffer", "k_rep_ao_hits", "k_spawn_ao_hitmask",
+                    "k_spawn_ao_index")
+
+
 def process(path, kind):
-    """[segment ms] of one rank: per launch position the minimum over the
-    timed frames, summed per segment; plus the launch list of one frame."""
+    """Per launch (segment, name, occurrence) of one rank: the minimum over
+    the timed frames; and the number of timed frames."""
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     frames = []
@@ -65,15 +79,24 @@ def process(path, kind):
     if not timed:
         return None
     nl = min(len(f) for f in timed)
-    seg, out, best = 0, [0.0] * len(NAMES[kind]), []
+    seg, best, seen = 0, {}, {}
     for q in range(nl):
         k = timed[0][q][0]
-        dt = min(f[q][1] for f in timed)
-        best.append((k, dt))
-        out[min(seg, len(out) - 1)] += dt
+        key = (min(seg, len(NAMES[kind]) - 1), k, seen.get((seg, k), 0))
+        seen[(seg, k)] = key[2] + 1
+        best[key] = min(f[q][1] for f in timed)
         if seg < len(ENDS[kind]) and ENDS[kind][seg](k):
             seg += 1
-    return out, len(timed)
+    return best, len(timed)
+
+
+def segments(best, kind, floor):
+    out = [0.0] * len(NAMES[kind])
+    for key, dt in best.items():
+        if any(p in key[1] for p in RANK_INDEPENDENT):
+            dt = min(dt, floor.get(key, dt))
+        out[key[0]] += dt
+    return out
 
 
 def main():
@@ -91,17 +114,22 @@ def main():
         kind = run.get("kind", "pt")
         if kind not in NAMES:
             continue
-        ranks = []
+        per = []
         for r in run["ranks"]:
             f = by_pid.get(r.get("pid"))
             res = process(f, kind) if f else None
             if res is None:
-                ranks = None
+                per = None
                 break
-            ranks.append({"rank": r["rank"], "segments_ms": [round(x, 4) for x in res[0]],
-                          "frames": res[1]})
-        if not ranks:
+            per.append((r["rank"], res))
+        if not per:
             continue
+        floor = {}
+        for _, (best, _) in per:
+            for key, dt in best.items():
+                floor[key] = min(dt, floor.get(key, dt))
+        ranks = [{"rank": rk, "segments_ms": [round(x, 4) for x in segments(best, kind, floor)],
+                  "frames": nf} for rk, (best, nf) in per]
         busiest = [round(max(x["segments_ms"][k] for x in ranks), 4)
                    for k in range(len(NAMES[kind]))]
         runs.append({"world": run["world"], "partition": run["partition"], "kind": kind,
