@@ -187,3 +187,72 @@ def test_ooc_any_hit_repeated_passes_fewer_domains(spray, oracle, tmp_path, ndom
     assert oc.stats()["drains"] > 6
     oc.close()
     rt.close()
+
+
+def _expected_scores(oracle, org, d, boxes):
+    """DomainStats of one pass (ooc_domain_stats.cc:60-111, increment): per
+    domain the rays listing it and the sum of SPRAY_RAY_DOMAIN_LIST_SIZE -
+    list position over them (1 past the list), the list sorted by (box entry
+    t, id) (rays.h:71-79)."""
+    ids, _, cnt, _ = oracle.domain_query(org, d, boxes, len(boxes))
+    q = np.zeros(len(boxes), np.int64)
+    score = np.zeros(len(boxes), np.int64)
+    for i in range(len(org)):
+        for p in range(cnt[i]):
+            q[ids[i, p]] += 1
+            score[ids[i, p]] += 16 - p if p < 16 else 1
+    return q, score
+
+
+def _probe_schedule(tmp_path, slots, **case):
+    import os
+    import re
+    import subprocess
+    import sys
+    path = tmp_path / "case.npz"
+    np.savez(path, **case)
+    env = dict(os.environ, SPRAY_OOC_TRACE="1")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__),
+                                                     "ooc_scores_probe.py"), str(path), str(slots)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "probe done" in r.stdout, r.stderr[-2000:]
+    got = {}
+    for m in re.finditer(r" d(\d+) q(\d+) live\d+ score(\d+)", r.stderr):
+        got[int(m.group(1))] = (int(m.group(2)), int(m.group(3)))
+    return got
+
+
+@pytest.mark.parametrize("scene", ["wavelets64", "stacked20"])
+def test_ooc_queue_scores_match_domain_stats(oracle, tmp_path, scene):
+    """The queue pass (k_ooc_masks: each lane's 16 nearest list entries in
+    registers, ranked by a sorting network) against a CPU restatement of
+    DomainStats::increment over the oracle's sorted domain lists: queue
+    lengths and scores of every drained queue.  "stacked20": one mesh at 20
+    overlapping offsets, so rays carry lists longer than 16 (positions past
+    the list weigh 1)."""
+    rng = np.random.default_rng(23)
+    if scene == "wavelets64":
+        from test_insitu import scene_boxes
+        org, d = batch(oracle)
+        boxes = np.asarray(scene_boxes()[0], np.float32)
+        case = dict(org=org, dir=d, desc=np.array(WAVELETS64))
+    else:
+        v, f, c = oracle.load_ply(SCENES + "/wavelet.ply")
+        n = np.zeros_like(v)
+        oracle.lib().or_compute_normals(oracle._p(v), len(v), oracle._p(f), len(f),
+                                        oracle._p(n))
+        shifts = np.array([[0.4 * k, 0.25 * k, 0.0] for k in range(20)], np.float32)
+        boxes = np.stack([np.concatenate([(v + s).min(0), (v + s).max(0)])
+                          for s in shifts]).astype(np.float32)
+        centre = (boxes[:, :3].min(0) + boxes[:, 3:].max(0)) / 2
+        org, d = random_rays(rng, 20000, centre, 40.0)
+        case = dict(org=org, dir=d, v=v, f=f, c=c, n=n, shifts=shifts)
+    q, score = _expected_scores(oracle, org, d, boxes)
+    got = _probe_schedule(tmp_path, 64, **case)
+    nonempty = int((q > 0).sum())
+    assert len(got) >= max(1, nonempty // 2), (len(got), nonempty)
+    if scene == "stacked20":
+        ids, _, cnt, _ = oracle.domain_query(org, d, boxes, len(boxes))
+        assert (cnt > 16).sum() > 100  # long lists exercised
+    for dom, (gq, gs) in got.items():
+        assert (gq, gs) == (int(q[dom]), int(score[dom])), dom
