@@ -1224,7 +1224,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
                                     dcount + 1, I->asel_tmp.p, &tsel));
     HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
                                        I->arec.as<float>(), I->alv.as<float>(), ns, dcount + 1,
-                                       I->aocc_p.as<uint8_t>(), nullptr, false,
+                                       I->aocc_p.as<uint8_t>(), nullptr,
                                        I->aown.as<uint32_t>()));
     HIPCHK(c, launch_rep_ao_scatter(s, I->apairs.as<uint32_t>(), dcount, npair,
                                     I->aocc_p.as<uint8_t>(), ns, fb, I->afields.as<uint32_t>()));

@@ -193,13 +193,12 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
                                     size_t n, const uint32_t* idx, size_t nc,
                                     const uint32_t* tmin, const float* shade10, uint8_t* occ,
                                     bool per_lane = false);
-// any hit of those pairs' AO rays, each generated in its any-hit lane
-// cull_own (replicated AO frames): AO rays entering no resident domain's
-// box are not walked (occ 0)
+// any hit of those pairs' AO rays, each generated in its any-hit lane;
+// idx (optional): only pairs idx[0..*d_count) (occ written at idx[j])
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters, bool cull_own = false,
+                                    unsigned long long* counters,
                                     const uint32_t* idx = nullptr);
 // flag[k] = AO pair k (k < min(*d_count, max_n)) enters a resident domain's
 // box, 0 for the rest of [0, max_n): the replicated AO frame traces only

@@ -290,9 +290,6 @@ struct SceneArgs {
   uint32_t* tkeys;
   const uint32_t* tmin;
   size_t nrays;  // index lists: ray ids idx[j] < nrays (0: < M)
-  // kEpiAoGen of a replicated frame: AO rays entering none of the resident
-  // domains' boxes are not walked (occ 0)
-  int rep_cull;
   // kEpiKeysShade rounds: 0 = every resident entry of the lane's list; 1 =
   // its first entry only; 2 = the later entries below the round-1 minimum
   int rround;
@@ -1236,10 +1233,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < A.ndom; k += kBlock) sdom[k] = ld4(A.domtrav, k);
   // replicated frames: the resident domains, whose boxes cull the lanes
-  constexpr bool kRes = rep_epi(EPI) || EPI == kEpiAoGen;
+  constexpr bool kRes = rep_epi(EPI);
   __shared__ uint8_t sres[kRes ? 64 * W : 1];
   __shared__ int nres;
-  if (kRes && (rep_epi(EPI) || A.rep_cull)) {
+  if (kRes) {
     __syncthreads();
     if (threadIdx.x == 0) {
       int k = 0;
@@ -1283,10 +1280,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (kGroup)
-      scene_ray_ao_group<W>(A, i, ok, ok && (!A.rep_cull || ao_own(A, i, sbox, sres, nres)), stl,
-                            sbox, sdom, stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
-    else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
-      A.occ[i] = 0;
+      scene_ray_ao_group<W>(A, i, ok, ok, stl, sbox, sdom,
+                            stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
     else if (kSpread)
       scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task, my_hit);
     else if (ok)
@@ -1363,11 +1358,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
           } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           else if (kGroup)
-            scene_ray_ao_group<W>(A, i, ok,
-                                  ok && (!A.rep_cull || ao_own(A, i, sbox, sres, nres)), stl,
-                                  sbox, sdom, stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
-          else if (EPI == kEpiAoGen && A.rep_cull && ok && !ao_own(A, i, sbox, sres, nres))
-            A.occ[i] = 0;
+            scene_ray_ao_group<W>(A, i, ok, ok, stl, sbox, sdom,
+                                  stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
           else if (kSpread)
             scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task,
                                              my_hit);
@@ -2712,11 +2704,9 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters, bool cull_own,
-                                    const uint32_t* idx) {
+                                    unsigned long long* counters, const uint32_t* idx) {
   if (max_n == 0) return hipSuccess;
   SceneArgs a = scene_args(v, nullptr, max_n);
-  a.rep_cull = cull_own ? 1 : 0;
   a.d_count = d_count;
   a.idx = idx;
   a.occ = occ;
@@ -2729,10 +2719,10 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
 }
 
 // Replicated AO frames: flag[k] = AO pair k (k < min(*d_count, M)) enters
-// a resident domain's box (ao_own, the in-lane cull's test).  The flagged
-// pairs are compacted and traced alone: culled lanes inside a traced wave
-// would still wait for its slowest lane, so the in-lane cull alone leaves a
-// rank's launch as long as the whole frame's.
+// a resident domain's box (ao_own).  The flagged pairs are compacted and
+// traced alone: culling lanes inside the traced waves instead (measured)
+// left every wave as long as its slowest lane, and a rank's launch as long
+// as the whole frame's.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint8_t* flag) {
   __shared__ float sbox[6 * 64 * W];
