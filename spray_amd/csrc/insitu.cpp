@@ -168,7 +168,7 @@ struct spray_rt_insitu {
   DBuf apub, arays, ahits, apairs, aocc_p, alv, arec, ascratch, afields, acount;
   DBuf aflag, aown, asel_tmp;  // replicated AO: the own pairs, compacted
   // compact film of replicated PT frames (runs of equal pixels along C)
-  DBuf rheads, rincl, rscan_tmp, rslot_c, rslot_pix, rcompact, rnp;
+  DBuf rincl, rscan_tmp, rslot_c, rslot_pix, rcompact, rnp;
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
   // split keys: t bits and list positions over C; the list positions'
   // all-reduce runs on a second stream (cs) beside the shadow any hit
@@ -955,20 +955,19 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   // ---- 2. the compact film's slots (runs of equal pixels along C'), their
   // count on its way to the host while the frame runs on
   MARK(1);
-  GROW(I->rheads, nc * 4 + 4);
   GROW(I->rincl, nc * 4 + 4);
   GROW(I->rslot_c, nc * 4 + 4);
   GROW(I->rslot_pix, nc * 4 + 4);
   GROW(I->rcompact, nc * 12 + 12);
   GROW(I->rnp, 8);
   size_t tsc = 0;
-  HIPCHK(c, launch_rep_slots(s, nullptr, nullptr, nc, nullptr, nullptr, nullptr, &tsc, nullptr,
-                             nullptr, nullptr));
+  HIPCHK(c, launch_rep_slots(s, nullptr, nullptr, nc, nullptr, nullptr, &tsc, nullptr, nullptr,
+                             nullptr));
   GROW(I->rscan_tmp, tsc);
   if (!I->ev_np) HIPCHK(c, hipEventCreateWithFlags(&I->ev_np, hipEventDisableTiming));
-  HIPCHK(c, launch_rep_slots(s, idx_c, pixid, nc, I->rheads.as<uint32_t>(), I->rincl.as<uint32_t>(),
-                             I->rscan_tmp.p, &tsc, I->rslot_c.as<int32_t>(),
-                             I->rslot_pix.as<int32_t>(), I->rnp.as<uint32_t>()));
+  HIPCHK(c, launch_rep_slots(s, idx_c, pixid, nc, I->rincl.as<uint32_t>(), I->rscan_tmp.p, &tsc,
+                             I->rslot_c.as<int32_t>(), I->rslot_pix.as<int32_t>(),
+                             I->rnp.as<uint32_t>()));
   uint32_t* h_np = reinterpret_cast<uint32_t*>(I->h_small + 250);
   HIPCHK(c, hipMemcpyAsync(h_np, I->rnp.p, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipEventRecord(I->ev_np, s));
@@ -981,13 +980,10 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   if (rec) GROW(I->rhit_c, nc * 48 + 48);
   uint64_t* keys = I->rkeys_c.as<uint64_t>();
   uint32_t* tk = I->rtk.as<uint32_t>();
-  // lanes whose ray enters no resident domain are not walked: their results
-  // prefilled (a miss, no shading)
+  // every slot of C' is written by its lane (lanes whose ray enters no
+  // resident domain write a miss and no shading: rep_ray), no prefill
   const bool split = split_keys() && c->ndom <= 255;
   const int rounds = split ? key_rounds() : 1;
-  HIPCHK(c, launch_fill_u64(s, keys, nc, kInsituMissKey));
-  HIPCHK(c, hipMemsetAsync(tk, 0xFF, nc * 4, s));
-  HIPCHK(c, hipMemsetAsync(I->rsvalid.p, 0, nc, s));
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
                                    I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
@@ -1003,8 +999,6 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
     GROW(I->rtstar, nc * 4 + 4);
     keys2 = I->rkeys_n.as<uint64_t>();
     tk2 = I->rtk2.as<uint32_t>();
-    HIPCHK(c, launch_fill_u64(s, keys2, nc, kInsituMissKey));
-    HIPCHK(c, hipMemsetAsync(tk2, 0xFF, nc * 4, s));
     HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
                                      rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys2, tk2,
                                      I->rsw.as<float>(), I->rsvalid.as<uint8_t>(), 2, tk));
@@ -1145,7 +1139,6 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   GROW(I->rkeys_c, nc * 8 + 8);
   GROW(I->rtk, nc * 4 + 4);
   const float zero10[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  HIPCHK(c, launch_fill_u64(s, I->rkeys_n.as<uint64_t>(), nc, kInsituMissKey));
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, I->ridx_c.as<uint32_t>(), nc, zero10,
                                    I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
                                    I->rtk.as<uint32_t>(), nullptr, nullptr, 0, nullptr,
@@ -1261,7 +1254,7 @@ void free_all(spray_rt_insitu* I) {
                  &I->rkeys_c, &I->rsray, &I->rsflag, &I->rwin, &I->rsvalid, &I->rsw, &I->rocc,
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
-                 &I->afields, &I->acount, &I->rheads, &I->rincl, &I->rscan_tmp,
+                 &I->afields, &I->acount, &I->rincl, &I->rscan_tmp,
                  &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax, &I->rtk2,
                  &I->rtstar, &I->aflag, &I->aown, &I->asel_tmp};
   for (DBuf* b : all)

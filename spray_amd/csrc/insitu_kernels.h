@@ -102,10 +102,10 @@ hipError_t launch_pix_max(hipStream_t s, const int32_t* pix, size_t n, uint32_t*
 hipError_t launch_gather_i32(hipStream_t s, const uint32_t* idx, size_t n, const int32_t* src,
                              int32_t* dst);
 // The compact film's slots: the runs of equal pixels along C.  slot_c[j] =
-// run of ray j, slot_pix[run] = its pixel, *d_np = runs; heads / incl: [nc]
-// u32 scratch; temp == nullptr: *temp_bytes <- the scan's scratch size.
+// run of ray j, slot_pix[run] = its pixel, *d_np = runs; incl: [nc] u32
+// scratch; temp == nullptr: *temp_bytes <- the scan's scratch size.
 hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
-                            uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,
+                            uint32_t* incl, void* temp, size_t* temp_bytes,
                             int32_t* slot_c, int32_t* slot_pix, uint32_t* d_np);
 // image[4 slot_pix[q] + k] += compact[3 q + k], q < np
 hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,

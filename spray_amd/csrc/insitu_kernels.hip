@@ -461,14 +461,14 @@ __global__ __launch_bounds__(kBlock) void k_rep_ao_record(RepAoArgs A, spray_rt_
 
 // ---- the compact film of a replicated PT frame -------------------------
 // Slots = the runs of equal pixels along C (the spp samples of a pixel are
-// neighbours): heads[j] = ray j of C starts a run.
-__global__ __launch_bounds__(kBlock) void k_rep_heads(const uint32_t* __restrict__ idx_c,
-                                                      const int32_t* __restrict__ pix, size_t nc,
-                                                      uint32_t* __restrict__ heads) {
-  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= nc) return;
-  heads[j] = (j == 0 || pix[idx_c[j]] != pix[idx_c[j - 1]]) ? 1u : 0u;
-}
+// neighbours), numbered by an inclusive scan of the run heads.
+struct RunHead {  // 1 where ray j of C' starts a run of equal pixels
+  const uint32_t* idx_c;
+  const int32_t* pix;
+  __host__ __device__ uint32_t operator()(uint32_t j) const {
+    return (j == 0 || pix[idx_c[j]] != pix[idx_c[j - 1]]) ? 1u : 0u;
+  }
+};
 
 // slot_c[j] = run of ray j (inclusive count - 1), slot_pix[run] = its pixel,
 // *d_np = the number of runs
@@ -780,8 +780,12 @@ hipError_t launch_pix_max(hipStream_t s, const int32_t* pix, size_t n, uint32_t*
   return hipGetLastError();
 }
 hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t* pix, size_t nc,
-                            uint32_t* heads, uint32_t* incl, void* temp, size_t* temp_bytes,
+                            uint32_t* incl, void* temp, size_t* temp_bytes,
                             int32_t* slot_c, int32_t* slot_pix, uint32_t* d_np) {
+  // the run heads computed inside the scan's input (no heads pass)
+  using Heads = hipcub::TransformInputIterator<uint32_t, RunHead,
+                                               hipcub::CountingInputIterator<uint32_t>>;
+  const Heads heads(hipcub::CountingInputIterator<uint32_t>(0u), RunHead{idx_c, pix});
   if (!temp) {
     size_t b = 0;
     const hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, b, heads, incl,
@@ -790,7 +794,6 @@ hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t*
     return e;
   }
   if (nc == 0) return hipMemsetAsync(d_np, 0, 4, s);
-  k_rep_heads<<<grid_for(nc), kBlock, 0, s>>>(idx_c, pix, nc, heads);
   hipError_t e = hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, heads, incl, int(nc), s);
   if (e != hipSuccess) return e;
   k_rep_slot_pix<<<grid_for(nc), kBlock, 0, s>>>(idx_c, pix, incl, nc, slot_c, slot_pix, d_np);

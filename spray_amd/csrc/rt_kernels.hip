@@ -990,8 +990,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 // the winner's own shadow ray); false: no ray (no hit anywhere).
 // A lane whose ray enters none of the resident domains' boxes (the exact
 // test of the top-level tree's leaves: its list holds no domain of this
-// rank) is dropped before any walk; its outputs keep their prefilled
-// values (a miss, no shadow ray).
+// rank) is dropped before any walk: kEpiKeysShade writes its miss key, t
+// bits and "no shading" here (every slot of C' is written by its lane, no
+// prefill); kEpiShadowGen leaves its occlusion byte at the prefilled 0.
 template <int EPI>
 __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, bool ok,
                                         float* r6, const float* sbox, const uint8_t* sres,
@@ -1023,6 +1024,11 @@ __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, 
   for (int k = 0; k < nres; ++k) {
     float tm;
     if (aabb_ref(sbox + 6 * int(sres[k]), dr, tm)) return true;
+  }
+  if (EPI == kEpiKeysShade) {  // the dropped lane's results: a miss, no shading
+    A.keys[j] = 0x7FFFFFFFFFFFFFFFull;  // the epilogue's miss key (kInsituMissKey)
+    A.tkeys[j] = 0xFFFFFFFFu;
+    if (A.sh_valid && A.rround != 2) A.sh_valid[j] = 0;  // round 2 keeps round 1's
   }
   return false;
 }
