@@ -378,6 +378,48 @@ def test_engine_frame_bit_reproducible(kind, steps, monkeypatch):
         np.testing.assert_array_equal(o, out[0])
 
 
+@pytest.mark.parametrize("kind", ["pt", "ao"])
+@pytest.mark.parametrize("what", ["away", "none"])
+def test_engine_replicated_steps_empty(kind, what, monkeypatch):
+    """Edge cases of the replicated steps (world 1 through RCCL): a camera
+    looking away from the scene (C' empty: no ray enters the scene box) and
+    a frame with no rays at all -- the image stays zero, the totals count
+    the radiance rays and no shadow / AO ray, and nothing faults."""
+    import spray_amd
+    from spray_amd import insitu
+    from test_insitu import scene_boxes
+    monkeypatch.setenv("SPRAY_INSITU_REPLICATED", "1")
+    img, spp = 64, 2
+    boxes, bound = scene_boxes()
+    owner = insitu.morton_partition(boxes, bound, 1, 0)
+    rt = spray_amd.RtContext(0)
+    insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, 0)
+    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
+    rt.set_stream(torch.cuda.current_stream())
+    c = H.BENCH_CAMERA
+    # the camera turned around: looking from its position away from the scene
+    pos = np.array(c["pos"], np.float64)
+    away = (2 * pos - np.array(c["lookat"], np.float64)).tolist()
+    cam = spray_amd.camera_init(c["pos"], away, c["up"], c["fov"], img, img)
+    block = (0, 0, img, img)
+    n = img * img * spp if what == "away" else 0
+    rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device="cuda")[:n]
+    pix = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
+    sam = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")[:n]
+    if n:
+        rt.eye_rays_insitu(cam, img, spp, block, block, rays, pix, sam)
+    sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1,
+                                     lights=[(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)])
+    eng = insitu.InsituEngine(rt, 1, 0, transport="rccl")
+    image = torch.zeros(img * img * 4, dtype=torch.float32, device="cuda")
+    tot = eng.trace_frame(sh, rays, pix, sam, spp, image)
+    torch.cuda.synchronize()
+    assert tot == (n, 0), tot
+    assert float(image.abs().sum()) == 0.0
+    eng.close()
+    rt.close()
+
+
 def test_engine_replicated_frame_unsupported_shading(oracle):
     """Several bounces are not a replicated frame: UNSUPPORTED, and nothing
     traced."""
