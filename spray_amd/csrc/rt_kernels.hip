@@ -370,15 +370,23 @@ __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f
   b = v4f{w[0], w[1], w[2], kInf};
 }
 
-// whether AO ray k enters a resident domain's box (replicated AO frames)
+// whether AO ray k enters a resident domain's box (replicated AO frames):
+// the exact test (the top-level tree's leaf test), each box first through
+// the fast slab on its kTopPad-padded copy (spad) -- the pair the top-level
+// walk itself uses for its internal boxes, a superset of the exact test --
+// so most boxes cost no double-precision test
 __device__ __forceinline__ bool ao_own(const SceneArgs& A, size_t k, const float* sbox,
-                                       const uint8_t* sres, int nres) {
+                                       const float* spad, const uint8_t* sres, int nres) {
   v4f a, b;
   ao_gen(A, k, a, b);
+  const Ray r = make_ray(a.x, a.y, a.z, b.x, b.y, b.z);
   const DRay dr = make_dray(a.x, a.y, a.z, b.x, b.y, b.z);
   for (int q = 0; q < nres; ++q) {
+    const int d = int(sres[q]);
+    const float* pb = spad + 6 * d;
     float tm;
-    if (aabb_ref(sbox + 6 * int(sres[q]), dr, tm)) return true;
+    if (!slab(r, pb[0], pb[1], pb[2], pb[3], pb[4], pb[5], 0.f, kInf, tm)) continue;
+    if (aabb_ref(sbox + 6 * d, dr, tm)) return true;
   }
   return false;
 }
@@ -2732,9 +2740,38 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint8_t* flag) {
   __shared__ float sbox[6 * 64 * W];
+  // padded as build_domain_tree pads internal boxes (kTopPad x the larger
+  // of the box's own scale and the scene's largest finite coordinate, where
+  // the AO rays start)
+  __shared__ float spad[6 * 64 * W];
   __shared__ uint8_t sres[64 * W];
   __shared__ int nres;
+  __shared__ float gmax;
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
+  {
+    float g = 0.f;
+    for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock)
+      if (isfinite(A.boxes[k])) g = fmaxf(g, fabsf(A.boxes[k]));
+    for (int o = 32; o > 0; o >>= 1) g = fmaxf(g, __shfl_xor(g, o));
+    __shared__ float wg[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) wg[threadIdx.x >> 6] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = 0.f;
+      for (int w = 0; w < kBlock / 64; ++w) m = fmaxf(m, wg[w]);
+      gmax = m;
+    }
+    __syncthreads();
+  }
+  for (int k = threadIdx.x; k < 3 * A.ndom; k += kBlock) {
+    const int d = k / 3, j = k - 3 * d;
+    const float lo = A.boxes[6 * d + j], hi = A.boxes[6 * d + 3 + j];
+    const float m = fmaxf(fmaxf(fmaxf(fabsf(lo), fabsf(hi)), hi - lo), gmax);
+    const float p = m * kTopPad;
+    const bool fin = isfinite(A.boxes[6 * d]) && isfinite(A.boxes[6 * d + 3]);
+    spad[6 * d + j] = fin ? lo - p : lo;
+    spad[6 * d + 3 + j] = fin ? hi + p : hi;
+  }
   if (threadIdx.x == 0) {
     int q = 0;
     for (int d = 0; d < A.ndom; ++d) {
@@ -2747,7 +2784,7 @@ __global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint
   const size_t n = A.d_count ? min(size_t(*A.d_count), A.M) : A.M;
   for (size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x; k < A.M;
        k += size_t(gridDim.x) * kBlock)
-    flag[k] = k < n && ao_own(A, k, sbox, sres, nres) ? 1 : 0;
+    flag[k] = k < n && ao_own(A, k, sbox, spad, sres, nres) ? 1 : 0;
 }
 
 hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
@@ -2760,7 +2797,9 @@ hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
   a.ao_rec = reinterpret_cast<const float4*>(rec);
   a.ao_lv = reinterpret_cast<const float4*>(lv);
   a.ao_ns = nsamples;
-  const unsigned g = unsigned(std::min<size_t>((max_n + kBlock - 1) / kBlock, 65536));
+  // a few resident blocks per CU walk the pairs grid-stride: each block's
+  // setup (boxes, padding, resident list) is paid once per ~10 K pairs
+  const unsigned g = unsigned(std::min<size_t>((max_n + kBlock - 1) / kBlock, 2048));
   if (a.ndom <= 64)
     k_ao_own_flags<1><<<g, kBlock, 0, s>>>(a, flag);
   else
