@@ -796,7 +796,10 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
                                lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                                P->ks[2],       P->shininess};
     uint32_t* nshadow = I->dnum.as<uint32_t>();
-    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, n, hits, shade10, occ, sv, sw, nshadow));
+    // hit records only for the per-sample records (the film needs the
+    // shading and occlusion alone: 48 B per ray not written)
+    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, n, rec ? hits : nullptr, shade10, occ, sv,
+                                    sw, nshadow));
     HIPCHK(c, launch_frame_stats_add(s, st, 1, n, nshadow));
     HIPCHK(c, launch_film_atomic(s, image, pixid, n, ns, sw, sv, occ, scale));
     if (rec) {

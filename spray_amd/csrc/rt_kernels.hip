@@ -545,7 +545,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         h1 = make_float4(c.y, c.z, c.w, __uint_as_float(color));
         h2 = make_float4(nsx, nsy, nsz, __int_as_float(best_dom));
       }
-      if (!(EPI == kEpiKeysShade && !hits)) {
+      if (!((EPI == kEpiKeysShade || EPI == kEpiShadowFrame) && !hits)) {
         float4* hp = reinterpret_cast<float4*>(hits + i);
         hp[0] = h0;
         hp[1] = h1;
@@ -871,8 +871,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   // instructions (WRITE_SIZE 1.25x the records).
   const size_t i0 = size_t(__builtin_amdgcn_readfirstlane(uint32_t(i))) |
                     (size_t(__builtin_amdgcn_readfirstlane(uint32_t(i >> 32))) << 32);
-  if (EPI == kEpiKeysShade && !A.hits) {
-    // no hit records (the replicated frame keeps keys and shading only)
+  if ((EPI == kEpiKeysShade || EPI == kEpiShadowFrame) && !A.hits) {
+    // no hit records (the replicated frame keeps keys and shading only; an
+    // in-situ frame without per-sample records keeps shading and shadows)
   } else if (EPI == kEpiKeysShade && A.rround == 2) {
     // round 2 replaces round 1's record only where it found a nearer hit
     if (valid && best_dom >= 0) {
