@@ -215,7 +215,8 @@ int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const floa
     const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
                                lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                                P->ks[2],       P->shininess};
-    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, M, hits, shade10, occ, sv, sw, nshadow));
+    // the film needs the shading and occlusion only: no hit records
+    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, M, nullptr, shade10, occ, sv, sw, nshadow));
     HIPCHK(c, launch_frame_stats_add(s, c->d_fstats, kStatStripes, M, nshadow));
     HIPCHK(c, launch_film(s, image, pixid, M, spp, ns, sw, sv, occ, scale));
     return SPRAY_RT_OK;
