@@ -464,10 +464,7 @@ def run_ooc(args, rt_main, prim, n_prim, slots=4):
     dev = prim.device
     rt, oc = spray_amd.ooc_scene(SCENE, SCENES, slots, device=dev.index or 0)
     rt.set_stream(torch.cuda.current_stream(dev))
-    # drain walk form (A/B): adaptive per wave by default
-    coh = os.environ.get("SPRAY_BENCH_OOC_WALK")
-    if coh:
-        rt.set_coherence({"packet": rt.RAYS_COHERENT, "lane": rt.RAYS_INCOHERENT}[coh])
+    # the drains walk packets (the context's default coherence)
     hits = torch.empty(n_prim * 48, dtype=torch.uint8, device=dev)
     shadow = torch.empty(n_prim * 32, dtype=torch.uint8, device=dev)
     src = torch.empty(n_prim, dtype=torch.int32, device=dev)

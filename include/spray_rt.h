@@ -562,8 +562,11 @@ int spray_rt_write_ppm(const char* path, const float* rgba_host, int w, int h);
 typedef struct spray_rt_insitu* spray_rt_insitu_t;
 
 /* Host-memory collectives of the rank group (every rank calls each one in
- * the same order).  Return 0 on success. */
+ * the same order).  Return 0 on success.  struct_size = the caller's
+ * sizeof(spray_rt_transport): callbacks past it (a caller built against an
+ * older, shorter struct) are taken as NULL, so the struct can grow. */
 typedef struct spray_rt_transport {
+  size_t struct_size;
   void* user;
   /* send_bytes[r] bytes to rank r (consecutive in send), recv_bytes[r] from
    * rank r (consecutive in recv) */

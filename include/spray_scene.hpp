@@ -62,6 +62,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -73,15 +74,32 @@ namespace spray_amd {
 // Scene::SceneInfo (scene.h:57-60): rtc_scene names the loaded domain's
 // engine slot (the cache block), so occluded() -- which gets no cache block
 // in the reference -- finds it.
+//
+// The tracers declare the reference's own record, `spray::SceneInfo
+// sinfo_` (ooc_pcontext.h:83, insitu_tcontext.h:186), whose rtc_scene is
+// Embree 2's opaque handle (`typedef struct __RTCScene* RTCScene`).  load(),
+// intersect(), occluded() and the batched drains are therefore templates on
+// the caller's types: any record with members rtc_scene (a pointer type)
+// and cache_block (an int), and any pointer-typed scene handle.  The slot
+// travels inside the handle's bits (slot + 1; a null handle is no slot), so
+// the caller's handle type never has to be a real Embree scene.
+// spray_amd::SceneInfo / RTCScene below are the same shapes for callers
+// that bring none.
 typedef struct spray_rtc_scene_tag* RTCScene;
 struct SceneInfo {
   RTCScene rtc_scene = nullptr;
   int cache_block = -1;
 };
-inline RTCScene slot_handle(int block) {
-  return reinterpret_cast<RTCScene>(static_cast<uintptr_t>(block) + 1);
+template <typename HandleT = RTCScene>
+inline HandleT slot_handle(int block) {
+  static_assert(std::is_pointer<HandleT>::value, "scene handles are pointer types");
+  return reinterpret_cast<HandleT>(static_cast<uintptr_t>(block) + 1);
 }
-inline int handle_slot(RTCScene s) { return int(reinterpret_cast<uintptr_t>(s)) - 1; }
+template <typename HandleT>
+inline int handle_slot(HandleT s) {
+  static_assert(std::is_pointer<HandleT>::value, "scene handles are pointer types");
+  return int(reinterpret_cast<uintptr_t>(s)) - 1;
+}
 
 // A light of the scene file (SceneLoader, scene_loader.cc:262-313):
 // type = SPRAY_RT_LIGHT_POINT (position, radiance) or
@@ -326,14 +344,16 @@ class Scene {
   }
 
   // Scene::load(id, SceneInfo*) (scene.inl:161-187): not concurrent with
-  // queries (omp single in the reference).
-  void load(int id, SceneInfo* sinfo) {
+  // queries (omp single in the reference).  SceneInfoT: the caller's record
+  // (spray::SceneInfo in the reference's tracers, ooc_pcontext.h:83, 150).
+  template <typename SceneInfoT>
+  void load(int id, SceneInfoT* sinfo) {
     int block = -1;
     if (spray_scene_load(scene_, id, &block))
       throw std::runtime_error(std::string("spray_amd::Scene::load: ") +
                                spray_scene_last_error(scene_));
     sinfo->cache_block = block;
-    sinfo->rtc_scene = slot_handle(block);
+    sinfo->rtc_scene = slot_handle<typename std::decay<decltype(sinfo->rtc_scene)>::type>(block);
     cache_block_ = block;
   }
   // Scene::load(int id) (scene.h:154, scene.inl:161-187): the loaded domain
@@ -348,8 +368,9 @@ class Scene {
 
   // Scene::intersect (scene.h:157-173): makeRadianceRay (rays.h:345-363),
   // closest hit in the cache block's domain, updateIntersection.
-  template <typename IsectT>
-  bool intersect(RTCScene rtc_scene, int cache_block, const float org[3], const float dir[3],
+  template <typename HandleT, typename IsectT,
+            typename = typename std::enable_if<std::is_pointer<HandleT>::value>::type>
+  bool intersect(HandleT rtc_scene, int cache_block, const float org[3], const float dir[3],
                  IsectT* isect) const {
     static_assert(sizeof(IsectT) >= sizeof(spray_rt_ray_intersection),
                   "RTCRayIntersection layout (96 B) expected");
@@ -358,8 +379,9 @@ class Scene {
     lane_call(spray_rt_lane_intersect1M(lane(), cache_block, isect, 1, sizeof(IsectT)));
     return geom_id(isect) != SPRAY_RT_INVALID_ID;
   }
-  template <typename V, typename IsectT>
-  bool intersect(RTCScene rtc_scene, int cache_block, const V& org, const float dir[3],
+  template <typename HandleT, typename V, typename IsectT,
+            typename = typename std::enable_if<std::is_pointer<HandleT>::value>::type>
+  bool intersect(HandleT rtc_scene, int cache_block, const V& org, const float dir[3],
                  IsectT* isect) const {  // the glm::vec3 origin overload
     const float o[3] = {org[0], org[1], org[2]};
     return intersect(rtc_scene, cache_block, o, dir, isect);
@@ -373,15 +395,17 @@ class Scene {
 
   // Scene::occluded (scene.h:175-195): makeShadowRay (rays.h:389-423), any
   // hit in the domain rtc_scene names; geomID = 0 when occluded.
-  template <typename RayT>
-  bool occluded(RTCScene rtc_scene, const float org[3], const float dir[3], RayT* ray) const {
+  template <typename HandleT, typename RayT,
+            typename = typename std::enable_if<std::is_pointer<HandleT>::value>::type>
+  bool occluded(HandleT rtc_scene, const float org[3], const float dir[3], RayT* ray) const {
     static_assert(sizeof(RayT) >= 84, "Embree 2 RTCRay layout expected");
     make_ray(org, dir, ray);
     lane_call(spray_rt_lane_occluded1M(lane(), handle_slot(rtc_scene), ray, 1, sizeof(RayT)));
     return geom_id(ray) != SPRAY_RT_INVALID_ID;
   }
-  template <typename V, typename RayT>
-  bool occluded(RTCScene rtc_scene, const V& org, const V& dir, RayT* ray) const {
+  template <typename HandleT, typename V, typename RayT,
+            typename = typename std::enable_if<std::is_pointer<HandleT>::value>::type>
+  bool occluded(HandleT rtc_scene, const V& org, const V& dir, RayT* ray) const {
     const float o[3] = {org[0], org[1], org[2]}, d[3] = {dir[0], dir[1], dir[2]};
     return occluded(rtc_scene, o, d, ray);
   }
@@ -431,14 +455,14 @@ class Scene {
   // original queue order -- the results are pure functions of the rays, so
   // the VBuf / shading order of the reference is unchanged ("hard
   // parts").  M records of sizeof(RecordT) bytes, host or device memory.
-  template <typename IsectT>
-  void intersect1M(const SceneInfo& sinfo, IsectT* isects, size_t M) const {
+  template <typename SceneInfoT, typename IsectT>
+  void intersect1M(const SceneInfoT& sinfo, IsectT* isects, size_t M) const {
     static_assert(sizeof(IsectT) >= sizeof(spray_rt_ray_intersection),
                   "RTCRayIntersection layout (96 B) expected");
     lane_call(spray_rt_lane_intersect1M(lane(), sinfo.cache_block, isects, M, sizeof(IsectT)));
   }
-  template <typename RayT>
-  void occluded1M(const SceneInfo& sinfo, RayT* rays, size_t M) const {
+  template <typename SceneInfoT, typename RayT>
+  void occluded1M(const SceneInfoT& sinfo, RayT* rays, size_t M) const {
     static_assert(sizeof(RayT) >= 84, "Embree 2 RTCRay layout expected");
     lane_call(spray_rt_lane_occluded1M(lane(), handle_slot(sinfo.rtc_scene), rays, M,
                                        sizeof(RayT)));

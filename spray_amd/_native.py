@@ -12,8 +12,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# SPRAY_RT_LIB selects a diagnostic build (scripts/diag_variants.py); the
-# default is the in-tree engine.
+# SPRAY_RT_LIB selects another build of the engine (A/B runs of
+# spray_amd.build.build(defines=..., out=...)); the default is the in-tree
+# engine.
 LIB_PATH = os.environ.get("SPRAY_RT_LIB") or os.path.join(HERE, "lib", "libspray_rt.so")
 
 # record layouts (include/spray_rt.h)

@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -172,7 +173,7 @@ struct spray_rt_insitu {
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
   // split keys: t bits and list positions over C; the list positions'
   // all-reduce runs on a second stream (cs) beside the shadow any hit
-  DBuf rtk, rlp, rbmax, rtk2, rtstar;
+  DBuf rtk, rlp, rbmax;
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
   // phase timing (spray_rt_insitu_set_timing): events on the stream
@@ -856,27 +857,8 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   return SPRAY_RT_OK;
 }
 
-// SPRAY_INSITU_SPLIT_KEYS=0: the replicated PT frame's 64-bit key MIN
-// SPRAY_INSITU_LANE=1: the replicated frames' launches walked per lane
-// (each lane its own ray) instead of as 64-ray packets
-bool rep_lane() {
-  static const bool on = [] {
-    const char* e = std::getenv("SPRAY_INSITU_LANE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// SPRAY_INSITU_ROUNDS=2: the replicated PT frame's keyed walk in two rounds
-// (first list entries, then the later ones below the round-1 minimum)
-int key_rounds() {
-  static const int r = [] {
-    const char* e = std::getenv("SPRAY_INSITU_ROUNDS");
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
-  return r;
-}
-
+// SPRAY_INSITU_SPLIT_KEYS=0: the replicated PT frame's 64-bit key MIN (the
+// form more than 255 domains need; kept under test)
 bool split_keys() {
   static const bool on = [] {
     const char* e = std::getenv("SPRAY_INSITU_SPLIT_KEYS");
@@ -986,42 +968,21 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   // every slot of C' is written by its lane (lanes whose ray enters no
   // resident domain write a miss and no shading: rep_ray), no prefill
   const bool split = split_keys() && c->ndom <= 255;
-  const int rounds = split ? key_rounds() : 1;
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
-                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>(),
-                                   rounds == 2 ? 1 : 0, nullptr, rep_lane()));
-  // two rounds: the group's round-1 minimum, then the later entries below it
-  uint64_t* keys2 = nullptr;
-  uint32_t* tk2 = nullptr;
+                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>()));
   uint32_t* tstar = tk;  // the winning t of every ray (the shadow rays' origin)
-  if (rounds == 2) {
-    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
-    GROW(I->rkeys_n, nc * 8 + 8);
-    GROW(I->rtk2, nc * 4 + 4);
-    GROW(I->rtstar, nc * 4 + 4);
-    keys2 = I->rkeys_n.as<uint64_t>();
-    tk2 = I->rtk2.as<uint32_t>();
-    HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, shade10,
-                                     rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys2, tk2,
-                                     I->rsw.as<float>(), I->rsvalid.as<uint8_t>(), 2, tk));
-  }
   // ---- 4. the group's minimum t of every ray of C' (then the list
   // position at that t) -- split while list positions fit a byte, else the
   // 64-bit keys' MIN
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
   if (split) {
-    uint32_t* tm = rounds == 2 ? tk2 : tk;
-    if (nc) COMM(I->tr->allreduce_min_u32(I, tm, nc));
+    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
     MARK(3);
     GROW(I->rlp, nc + 1);
     lp = I->rlp.as<uint8_t>();
-    HIPCHK(c, launch_rep_lp(s, rounds == 2 ? keys2 : keys, tm, nc, lp));
-    if (rounds == 2) {
-      tstar = I->rtstar.as<uint32_t>();
-      HIPCHK(c, launch_min_u32(s, tk, tk2, nc, tstar));
-    }
+    HIPCHK(c, launch_rep_lp(s, keys, tk, nc, lp));
     if (nc) {
       if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
       if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
@@ -1048,7 +1009,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   GROW(I->rocc, nc + 192);
   HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nc, s));
   HIPCHK(c, launch_scene_rep_shadows(s, view(c), rays, n, idx_c, nc, tstar, shade10,
-                                     I->rocc.as<uint8_t>(), rep_lane()));
+                                     I->rocc.as<uint8_t>()));
   // ---- 6. the winners (after the list positions' MIN), their shadows
   // counted behind the occlusion bytes: rank 0 counts the frame's radiance
   // rays, every rank its winners' shadow rays
@@ -1058,14 +1019,9 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   GROW(I->rnsh, kWinCounterBytes);
   HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, kWinCounterBytes, s));
   if (split && nc) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
-  if (rounds == 2)
-    HIPCHK(c, launch_rep_win2(s, keys, tk, keys2, tk2, lp, I->rsvalid.as<uint8_t>(), nc,
-                              I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
-                              I->rnsh.as<unsigned long long>()));
-  else
-    HIPCHK(c, launch_rep_win(s, keys, tk, lp, kmin, I->rsvalid.as<uint8_t>(), nc,
-                             I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
-                             I->rnsh.as<unsigned long long>()));
+  HIPCHK(c, launch_rep_win(s, keys, tk, lp, kmin, I->rsvalid.as<uint8_t>(), nc,
+                           I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
+                           I->rnsh.as<unsigned long long>()));
   HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nc, I->rank == 0 ? n : 0,
                               I->rnsh.as<unsigned long long>()));
   // ---- 7. occlusion OR (a byte SUM) + totals
@@ -1076,7 +1032,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   HIPCHK(c, hipEventSynchronize(I->ev_np));  // long done: the scan ran before the keyed launch
   const size_t np = nc ? *h_np : 0;
   // the all-reduces' and the reduce's payload
-  const size_t pay = (split ? 5 * nc : 8 * nc) + (rounds == 2 ? 4 * nc : 0) + nc + 192 + 12 * np;
+  const size_t pay = (split ? 5 * nc : 8 * nc) + nc + 192 + 12 * np;
   I->st[0] += pay;
   I->st[1] += pay;
   if (np) {
@@ -1144,8 +1100,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   const float zero10[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, I->ridx_c.as<uint32_t>(), nc, zero10,
                                    I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
-                                   I->rtk.as<uint32_t>(), nullptr, nullptr, 0, nullptr,
-                                   rep_lane()));
+                                   I->rtk.as<uint32_t>(), nullptr, nullptr));
   HIPCHK(c, hipMemcpyAsync(I->rkeys_c.p, I->rkeys_n.p, nc * 8, hipMemcpyDeviceToDevice, s));
   MARK(3);
   if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
@@ -1258,8 +1213,8 @@ void free_all(spray_rt_insitu* I) {
                  &I->rpix, &I->rsam, &I->rhit_c, &I->rnsh, &I->apub, &I->arays,
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rincl, &I->rscan_tmp,
-                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax, &I->rtk2,
-                 &I->rtstar, &I->aflag, &I->aown, &I->asel_tmp};
+                 &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax,
+                 &I->aflag, &I->aown, &I->asel_tmp};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
@@ -1335,7 +1290,15 @@ int spray_rt_insitu_create(spray_rt_ctx_t c, int world, int rank, const void* nc
     I->tr = std::move(t);
   } else {
     auto t = std::make_unique<HostTransport>();
-    t->cb = *host;
+    // the caller's struct may be shorter than this build's (fields added at
+    // its end): copy what it holds, the rest stays NULL
+    const size_t have = host->struct_size;
+    if (have < offsetof(spray_rt_transport, allreduce_min_u64)) {
+      free_all(I.get());
+      return fail(c, SPRAY_RT_ERR_ARG, "spray_rt_transport.struct_size %zu too small", have);
+    }
+    std::memcpy(&t->cb, host, std::min(have, sizeof(spray_rt_transport)));
+    t->cb.struct_size = sizeof(spray_rt_transport);
     if (const char* lk = std::getenv("SPRAY_INSITU_SERIAL"))
       if (lk[0]) t->lock_fd = open(lk, O_RDWR | O_CREAT, 0666);
     I->tr = std::move(t);

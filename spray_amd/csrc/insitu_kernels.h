@@ -84,15 +84,6 @@ constexpr size_t kWinCounterBytes = size_t(kWinCounters) * kWinStride * 8;
 hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* tmin,
                           const uint8_t* lpmin, const uint64_t* kmin, const uint8_t* sv, size_t nc,
                           uint8_t* win, uint8_t* svw, unsigned long long* nshadow);
-// two-round keys: the winner of ray j (round 2's at (tb, lpmin) where tb
-// exists, else round 1's at ta); svw = win && sv; nshadow += svw
-hipError_t launch_rep_win2(hipStream_t s, const uint64_t* keys1, const uint32_t* ta,
-                           const uint64_t* keys2, const uint32_t* tb, const uint8_t* lpmin,
-                           const uint8_t* sv, size_t nc, uint8_t* win, uint8_t* svw,
-                           unsigned long long* nshadow);
-// out[j] = min(a[j], b[j])
-hipError_t launch_min_u32(hipStream_t s, const uint32_t* a, const uint32_t* b, size_t n,
-                          uint32_t* out);
 // tmin[j] = t bits of kmin[j] (0xFFFFFFFF: a miss)
 hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc, uint32_t* tmin);
 // *out = max(pix[0..n)) (bmax: grid_for(n) u32 of scratch)

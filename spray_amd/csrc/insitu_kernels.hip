@@ -589,47 +589,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_i32(const uint32_t* __restric
   if (j < n) dst[j] = src[idx[j]];
 }
 
-// two-round keys (SPRAY_INSITU_ROUNDS=2): round 1 = each ray's first list
-// entry (t bits tA after the MIN), round 2 = the later entries strictly
-// nearer than tA (tB after the MIN; 0xFFFFFFFF: none nearer).  The winner is
-// round 2's at (tB, minimum list position) when tB exists, else round 1's
-// (the one owner of the first entry).  tstar = the winning t for the shadows.
-__global__ __launch_bounds__(kBlock) void k_rep_win2(const uint64_t* __restrict__ keys1,
-                                                     const uint32_t* __restrict__ ta,
-                                                     const uint64_t* __restrict__ keys2,
-                                                     const uint32_t* __restrict__ tb,
-                                                     const uint8_t* __restrict__ lpmin,
-                                                     const uint8_t* __restrict__ sv, size_t nc,
-                                                     uint8_t* __restrict__ win,
-                                                     uint8_t* __restrict__ svw,
-                                                     unsigned long long* __restrict__ nshadow) {
-  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  bool w = false, s = false;
-  if (j < nc) {
-    const uint32_t b = tb[j];
-    if (b != 0xFFFFFFFFu) {
-      const uint64_t k2 = keys2[j];
-      w = k2 != kInsituMissKey && uint32_t(k2 >> 32) == b &&
-          uint8_t((k2 >> 16) & 0xFFu) == lpmin[j];
-    } else {
-      const uint64_t k1 = keys1[j];
-      w = k1 != kInsituMissKey && uint32_t(k1 >> 32) == ta[j];
-    }
-    s = w && sv[j];
-    win[j] = w;
-    svw[j] = s;
-  }
-  const uint64_t bb = __ballot(s);
-  win_count(__popcll(bb), nshadow);
-}
-
-__global__ __launch_bounds__(kBlock) void k_min_u32(const uint32_t* __restrict__ a,
-                                                    const uint32_t* __restrict__ b, size_t n,
-                                                    uint32_t* __restrict__ out) {
-  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j < n) out[j] = min(a[j], b[j]);
-}
-
 // pixel-id maxima per block of pix[0..n) (then k_max_u32)
 __global__ __launch_bounds__(kBlock) void k_pix_bmax(const int32_t* __restrict__ pix, size_t n,
                                                      uint32_t* __restrict__ bmax) {
@@ -761,16 +720,6 @@ hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc,
 hipError_t launch_gather_i32(hipStream_t s, const uint32_t* idx, size_t n, const int32_t* src,
                              int32_t* dst) {
   LAUNCH(n, k_gather_i32, idx, n, src, dst);
-}
-hipError_t launch_rep_win2(hipStream_t s, const uint64_t* keys1, const uint32_t* ta,
-                           const uint64_t* keys2, const uint32_t* tb, const uint8_t* lpmin,
-                           const uint8_t* sv, size_t nc, uint8_t* win, uint8_t* svw,
-                           unsigned long long* nshadow) {
-  LAUNCH(nc, k_rep_win2, keys1, ta, keys2, tb, lpmin, sv, nc, win, svw, nshadow);
-}
-hipError_t launch_min_u32(hipStream_t s, const uint32_t* a, const uint32_t* b, size_t n,
-                          uint32_t* out) {
-  LAUNCH(n, k_min_u32, a, b, n, out);
 }
 hipError_t launch_pix_max(hipStream_t s, const int32_t* pix, size_t n, uint32_t* bmax,
                           uint32_t* out) {

@@ -287,11 +287,8 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   std::vector<char> done(n, 0);
   int r = SPRAY_RT_OK;
   int rings[4] = {0, 0, 0, 0};
-  static const int lag = [] {
-    const char* e = std::getenv("SPRAY_OOC_LAG");
-    const int v = e ? std::atoi(e) : 1;
-    return v < 1 ? 1 : (v > 3 ? 3 : v);
-  }();
+  // the counts of launch k - 1 (measured the same as k - 2 / k - 3)
+  constexpr int lag = 1;
   static const bool trace = std::getenv("SPRAY_OOC_TRACE") != nullptr;  // schedule log
   if (trace)
     std::fprintf(stderr, "ooc pass %s: %zu queues, %u pairs\n", any_hit ? "any" : "closest",

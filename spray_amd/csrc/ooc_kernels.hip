@@ -26,26 +26,10 @@ constexpr int kWaves = kBlock / 64;
 #define SPRAY_OOC_MASK_BLOCKS 3072
 #endif
 constexpr unsigned kOocMaskBlocks = SPRAY_OOC_MASK_BLOCKS;
-// diagnostic builds only (timing of k_ooc_masks' parts; wrong queues):
-// 1 = no box confirmation, 2 = no per-block counts, 3 = top-level walk only,
-// 4 = positions without the per-domain sums, 5 = the sums without positions
-// the per-lane weight table of k_ooc_masks (0: the LDS entry lists, A/B)
-#ifndef SPRAY_OOC_MASK_TAB
-#define SPRAY_OOC_MASK_TAB 1
-#endif
-#ifndef SPRAY_OOC_MASK_DIAG
-#define SPRAY_OOC_MASK_DIAG 0
-#endif
-// adaptive any-hit drains: the largest id span of a wave's rays that still
-// walks as a packet (8 pixels x 8 spp = 64 consecutive camera rays)
 // waves per SIMD the any-hit drain is compiled for (register budget)
 #ifndef SPRAY_OOC_AH_WAVES
 #define SPRAY_OOC_AH_WAVES 1
 #endif
-#ifndef SPRAY_OOC_PACKET_SPAN
-#define SPRAY_OOC_PACKET_SPAN 1024
-#endif
-constexpr uint32_t kOocPacketSpan = SPRAY_OOC_PACKET_SPAN;
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
   uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
@@ -149,10 +133,10 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
   // per-domain sums below find a domain's position among them; LDS stays
   // small for the latency-bound walk's occupancy); wider scenes keep
   // kLaneList entries in LDS and look weights up by scanning them
-  constexpr bool kTab = W == 1 && SPRAY_OOC_MASK_TAB;
+  // (the LDS entry lists measured the same at W == 1)
+  constexpr bool kTab = W == 1;
   __shared__ float lte[kTab ? 1 : kLaneList][kBlock];
   __shared__ int lid[kTab ? 1 : kLaneList][kBlock];
-  uint32_t pk[4] = {~0u, ~0u, ~0u, ~0u};  // kTab: byte q = the q-th nearest domain
   // the top-level tree and the boxes are staged once per block, which then
   // walks ray blocks rb = blockIdx.x, + gridDim.x, ... (one launch-wide
   // staging of 5.5 KB per ray block of 256 rays was 180 MB of L2 reads per
@@ -165,6 +149,9 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
     const size_t i = size_t(rb) * kBlock + threadIdx.x;
     const bool in = i < M;
     const bool live = in && (!valid || valid[i]);
+    // kTab: byte q = the q-th nearest domain of this ray block's lane (no
+    // byte survives from the previous ray block)
+    uint32_t pk[4] = {~0u, ~0u, ~0u, ~0u};
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
@@ -184,7 +171,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
     int rid[kTab ? kReg : 1];
     uint32_t k = 0;
     const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-    if (live && SPRAY_OOC_MASK_DIAG != 1 && SPRAY_OOC_MASK_DIAG != 3) {
+    if (live) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         uint64_t bits = m[w];
@@ -243,7 +230,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
       uint32_t kmax = k;
       for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, uint32_t(__shfl_xor(int(kmax), o)));
       kmax = uint32_t(__builtin_amdgcn_readfirstlane(int(kmax)));
-      if ((SPRAY_OOC_MASK_DIAG < 2 || SPRAY_OOC_MASK_DIAG == 4) && kmax) {
+      if (kmax) {
         // sort the kept entries by (entry t, id) with a bitonic network in
         // registers (empty slots last); a slot's index is its list position
         const uint32_t nk = min(k, uint32_t(kReg));
@@ -262,7 +249,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
           if (uint32_t(a) < nk)
             pk[a >> 2] = (pk[a >> 2] & ~(0xFFu << (8 * (a & 3)))) | (uint32_t(rid[a]) << (8 * (a & 3)));
       }
-    } else if (k <= kLaneList && SPRAY_OOC_MASK_DIAG < 2)
+    } else if (k <= kLaneList)
       for (uint32_t a = 0; a < k; ++a) {
         const float ta = lte[a][threadIdx.x];
         const int da = lid[a][threadIdx.x] & 0xFFFF;
@@ -276,7 +263,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
     // per domain of the wave: pairs and weights summed over the wave first
     // (a wave's rays mostly share domains: same-address LDS atomics serialise)
 #pragma unroll
-    for (int w = 0; w < ((SPRAY_OOC_MASK_DIAG >= 2 && SPRAY_OOC_MASK_DIAG != 5) ? 0 : W); ++w) {
+    for (int w = 0; w < W; ++w) {
       uint64_t u = wave_or64(m[w]);
       while (u) {
         const int j = __ffsll((long long)u) - 1;
@@ -763,31 +750,15 @@ __device__ __forceinline__ void ah_pair(const OocDomain& D, uint32_t pj, bool ok
   const uint32_t i = ok ? idx[pj] : 0u;
   bool act = ok && !occ[i];
   bool hit = false;
-  bool packet = MODE == 1;
+  constexpr bool packet = MODE == 1;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
   if (act) {
     const float4* rp = reinterpret_cast<const float4*>(rays + i);
     o4 = rp[0];
     d4 = rp[1];
   }
-  if (MODE == 2) {
-    // packets for neighbouring rays: the wave's queue entries (ascending ray
-    // ids) span few rays, and the directions are within ~8 degrees of the
-    // first lane's (the in-core rule); a far domain's sparse queue walks
-    // per lane
-    const uint64_t vb = __ballot(act);
-    const int lead = vb ? __ffsll((long long)vb) - 1 : 0;
-    const int last = vb ? 63 - __clzll((long long)vb) : 0;
-    const uint32_t span = uint32_t(__builtin_amdgcn_readlane(int(i), last)) -
-                          uint32_t(__builtin_amdgcn_readlane(int(i), lead));
-    const float lx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d4.x), lead));
-    const float ly = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d4.y), lead));
-    const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d4.z), lead));
-    const float c = (d4.x * lx + d4.y * ly) + d4.z * lz;
-    packet = span <= kOocPacketSpan && __ballot(act && !(c >= 0.99f)) == 0;
-  }
   const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  if (packet) {
+  if constexpr (packet) {
     Best best{0.f, 0xFFFFFFFFu, 0xFFFFFFFFu};
     if (__ballot(act))
       trace_tree_packet<true>(uniform_ptr(D.nodes), uniform_ptr(D.tris), uniform_ptr(D.prims), r,
@@ -897,17 +868,8 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   return q.npair > q.pair_cap ? hipErrorOutOfMemory : hipSuccess;  // caller grows, redoes
 }
 
-static uint32_t copy_blocks() {
-  static const uint32_t n = [] {
-    const char* e = std::getenv("SPRAY_OOC_COPY_BLOCKS");
-    const int v = e ? std::atoi(e) : kOocCopyBlocks;
-    return uint32_t(v < 1 ? 1 : (v > 256 ? 256 : v));
-  }();
-  return n;
-}
-
 static unsigned batch_grid(OocBatch& B) {
-  B.ncopy = copy_blocks();
+  B.ncopy = kOocCopyBlocks;
   B.wave0[0] = 0;
   for (int k = 0; k < B.count; ++k) B.wave0[k + 1] = B.wave0[k] + (B.n[k] + 63) / 64;
   const unsigned g = (B.wave0[B.count] + kWaves - 1) / kWaves;
@@ -957,26 +919,16 @@ hipError_t launch_ooc_ah_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
                                               snap, ndom)
   // the context's coherence setting: incoherent -> per lane, else packets
   // (measured on configs[3]'s PT shadows, one box: packets 4.08, per lane
-  // 4.60, the per-wave choice 4.72 ms per frame -- the choice's direction
+  // 4.60, a per-wave choice 4.72 ms per frame -- the choice's direction
   // loads and the two walks' registers and stacks cost more than it saves
-  // on queues of neighbouring rays; SPRAY_OOC_AH_ADAPTIVE=1 keeps it)
-  static const bool adaptive = [] {
-    const char* e = std::getenv("SPRAY_OOC_AH_ADAPTIVE");
-    return e && e[0] == '1';
-  }();
-  const int mode = coherence == SPRAY_RT_RAYS_INCOHERENT                  ? 0
-                   : (coherence == SPRAY_RT_RAYS_ADAPTIVE && adaptive) ? 2
-                                                                          : 1;
-  {
-    if (W == 1) {
-      if (mode == 0) SPRAY_AH_LAUNCH(1, 0);
-      else if (mode == 1) SPRAY_AH_LAUNCH(1, 1);
-      else SPRAY_AH_LAUNCH(1, 2);
-    } else {
-      if (mode == 0) SPRAY_AH_LAUNCH(4, 0);
-      else if (mode == 1) SPRAY_AH_LAUNCH(4, 1);
-      else SPRAY_AH_LAUNCH(4, 2);
-    }
+  // on queues of neighbouring rays)
+  const bool per_lane = coherence == SPRAY_RT_RAYS_INCOHERENT;
+  if (W == 1) {
+    if (per_lane) SPRAY_AH_LAUNCH(1, 0);
+    else SPRAY_AH_LAUNCH(1, 1);
+  } else {
+    if (per_lane) SPRAY_AH_LAUNCH(4, 0);
+    else SPRAY_AH_LAUNCH(4, 1);
   }
 #undef SPRAY_AH_LAUNCH
   return hipGetLastError();

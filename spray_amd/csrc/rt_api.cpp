@@ -96,6 +96,7 @@ const char* build_slot_image(const float* verts, size_t nverts, const uint32_t* 
   const size_t b_normals = normals ? align256(3 * nverts * sizeof(float)) : 0;
   out->bytes.assign(
       std::max<size_t>(256, b_q + b_nodes + b_tris + b_prims + b_faces + b_colors + b_normals), 0);
+  out->nbytes = out->bytes.size();
   char* host = out->bytes.data();
   size_t off = 0;
   auto put = [&](const void* src, size_t n, size_t padded) {
@@ -132,7 +133,9 @@ int upload_slot_image(spray_rt_ctx* c, int slot, const SlotImage& img, const voi
   // the previous image may still be read by queued work
   HIPCHK(c, hipStreamSynchronize(stream_of(c)));
   if (sh.ready) HIPCHK(c, hipEventSynchronize(sh.ready));
-  const size_t total = img.bytes.size();
+  const size_t total = img.nbytes;
+  if (!pinned_src && img.bytes.size() != total)
+    return fail(c, SPRAY_RT_ERR_STATE, "slot image bytes released without a pinned copy");
   if (sh.bytes < total) {
     if (sh.dmem) HIPCHK(c, hipFree(sh.dmem));
     sh.dmem = nullptr;

@@ -110,7 +110,8 @@ namespace detail {
 // only (quantized = true): the OOC drains do not read it, so its images
 // stream without it.
 struct SlotImage {
-  std::vector<char> bytes;
+  std::vector<char> bytes;  // may be released once a pinned copy exists
+  size_t nbytes = 0;        // the image's size (== bytes.size() while held)
   size_t o_nodes = 0, o_tris = 0, o_prims = 0, o_faces = 0;
   size_t o_colors = SIZE_MAX, o_normals = SIZE_MAX;  // SIZE_MAX: absent
   uint32_t nnodes = 0, ntris = 0, nverts = 0;

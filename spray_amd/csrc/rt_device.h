@@ -47,41 +47,12 @@ __device__ __forceinline__ float4 ld4(const void* base, size_t i) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// Node / triangle fetch.  When every active lane of the wave fetches the same
-// record (coherent rays walking the same path), one scalar load brings it
-// through the scalar data cache and it is broadcast for free; otherwise each
-// lane loads its own 16-B pieces through the vector memory path (whose data
-// return is what the traversal saturates: TD ~80 % busy, profiles/).
-#ifndef SPRAY_SCALAR_UNIFORM
-#define SPRAY_SCALAR_UNIFORM 0
-#endif
+// Node / triangle fetch of the per-lane walks: each lane loads its own 16-B
+// pieces through the vector memory path (the packet walks fetch through the
+// scalar data cache instead, trace_tree_packet).
 #define CAS __attribute__((address_space(4)))
-// Packet walk child order: 1 = majority vote of the lanes, 0 = the first
-// lane entering both children.
-#ifndef SPRAY_PACKET_VOTE
-#define SPRAY_PACKET_VOTE 0
-#endif
-__device__ __forceinline__ bool wave_uniform_addr(const void* p, uint64_t& u) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
-  u = (uint64_t(hi) << 32) | lo;
-  return __ballot(a != u) == 0;
-}
 __device__ __forceinline__ void ld_node(const void* nodes, size_t nb, float4& n0, float4& n1,
                                         float4& n2, float4& n3) {
-  if (SPRAY_SCALAR_UNIFORM) {
-    uint64_t u;
-    if (wave_uniform_addr(static_cast<const float4*>(nodes) + nb, u)) {
-      const CAS v4f* q = reinterpret_cast<const CAS v4f*>(u);
-      const v4f x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
-      n0 = make_float4(x0.x, x0.y, x0.z, x0.w);
-      n1 = make_float4(x1.x, x1.y, x1.z, x1.w);
-      n2 = make_float4(x2.x, x2.y, x2.z, x2.w);
-      n3 = make_float4(x3.x, x3.y, x3.z, x3.w);
-      return;
-    }
-  }
   n0 = ld4(nodes, nb);
   n1 = ld4(nodes, nb + 1);
   n2 = ld4(nodes, nb + 2);
@@ -89,17 +60,6 @@ __device__ __forceinline__ void ld_node(const void* nodes, size_t nb, float4& n0
 }
 __device__ __forceinline__ void ld_tri(const void* tris, uint32_t p, float4& a, float4& b,
                                        float4& c) {
-  if (SPRAY_SCALAR_UNIFORM) {
-    uint64_t u;
-    if (wave_uniform_addr(static_cast<const float4*>(tris) + 3 * size_t(p), u)) {
-      const CAS v4f* q = reinterpret_cast<const CAS v4f*>(u);
-      const v4f x0 = q[0], x1 = q[1], x2 = q[2];
-      a = make_float4(x0.x, x0.y, x0.z, x0.w);
-      b = make_float4(x1.x, x1.y, x1.z, x1.w);
-      c = make_float4(x2.x, x2.y, x2.z, x2.w);
-      return;
-    }
-  }
   a = ld4(tris, 3 * size_t(p));
   b = ld4(tris, 3 * size_t(p) + 1);
   c = ld4(tris, 3 * size_t(p) + 2);
@@ -589,16 +549,11 @@ __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tri
     const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(n[12]));
     const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(n[13]));
     const uint64_t bl = __ballot(hl), br = __ballot(hr);
-#if SPRAY_PACKET_VOTE
-    const uint64_t vl = __ballot(hl && (!hr || tl <= tr));
-    const uint64_t vr = __ballot(hr && (!hl || tr < tl));
-    const bool lf = __popcll(vl) >= __popcll(vr);
-#else
-    // near side of the first lane that enters both children
+    // near side of the first lane that enters both children (a majority
+    // vote measured slower)
     const uint64_t both = bl & br;
     const bool lf = both ? __builtin_amdgcn_readlane(int(tl <= tr), __ffsll((long long)both) - 1) != 0
                          : true;
-#endif
     int32_t next = kNone;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {

@@ -178,21 +178,15 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
 // results at j.  Keyed closest hit over the resident domains (keys: 64-bit
 // composite, tkeys: t bits, 0xFFFFFFFF for none) with the point-light
 // shading of the own hit (sw float4, sv); hits optional (null: none).
-// round 0: every resident entry of each ray's list; 1: only its first entry
-// (when resident); 2: the later entries, a hit kept only when strictly
-// nearer than tmin_round1[j] (sw / sv then written for kept hits only).
-// per_lane (round 0): each lane walks its own ray instead of the packet.
 hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                   size_t n, const uint32_t* idx, size_t nc,
                                   const float* shade10, spray_rt_hit* hits, uint64_t* keys,
-                                  uint32_t* tkeys, float* sw, uint8_t* sv, int round = 0,
-                                  const uint32_t* tmin_round1 = nullptr, bool per_lane = false);
+                                  uint32_t* tkeys, float* sw, uint8_t* sv);
 // ... and the any hit of the point-light shadow ray of the hit at t bits
 // tmin[j] (none: 0xFFFFFFFF, occ[j] untouched) over the resident domains
 hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                     size_t n, const uint32_t* idx, size_t nc,
-                                    const uint32_t* tmin, const float* shade10, uint8_t* occ,
-                                    bool per_lane = false);
+                                    const uint32_t* tmin, const float* shade10, uint8_t* occ);
 // any hit of those pairs' AO rays, each generated in its any-hit lane;
 // idx (optional): only pairs idx[0..*d_count) (occ written at idx[j])
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,

@@ -47,10 +47,6 @@ namespace {
 #endif
 constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this large persist
 
-// Diagnostic builds (-DSPRAY_DIAG_MODE=n, never shipped): packet form: 5 = no
-// tree walks, 6 = top-level mask only, 7 = no epilogue / spawn; per-lane form: 3 = ray in, record out
-// (no domain tree), 1 = domain mask
-// only, 2 = mask + ordered domain selection, no BVH traversal.
 // Minimum resident waves per SIMD the register allocator must allow (the
 // second __launch_bounds__ operand); 1 = unconstrained.
 // Per-lane any hit: 1 = while-while walk with postponed leaves, 0 = the
@@ -82,27 +78,6 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #endif
 #ifndef SPRAY_WAVES_AOGEN
 #define SPRAY_WAVES_AOGEN 8
-#endif
-#ifndef SPRAY_DIAG_MODE
-#define SPRAY_DIAG_MODE 0
-#endif
-// AO any hit with lane refill (scene_ray_ah_refill, diagnostic builds): a
-// lane whose ray ended takes the next (source, sample) pair of the wave's
-// band queues once at least SPRAY_AO_REFILL lanes are idle; 0 (shipped) =
-// one chunk of 64 rays per wave at a time (scene_ray).  Measured slower at
-// every threshold ("Lane refill"); SPRAY_CHUNK_AO: pairs per
-// queue dequeue.
-#ifndef SPRAY_AO_REFILL
-#define SPRAY_AO_REFILL 0
-#endif
-#ifndef SPRAY_CHUNK_AO
-#define SPRAY_CHUNK_AO 256
-#endif
-// refill granularity: aligned groups of this many lanes take aligned groups
-// of consecutive pairs (the sample-major trace order puts one pixel's 8
-// near-identical rays of a sample side by side; 1 = single lanes)
-#ifndef SPRAY_AO_REFILL_GROUP
-#define SPRAY_AO_REFILL_GROUP 8
 #endif
 
 // ---------------------------------------------------------------------------
@@ -290,10 +265,6 @@ struct SceneArgs {
   uint32_t* tkeys;
   const uint32_t* tmin;
   size_t nrays;  // index lists: ray ids idx[j] < nrays (0: < M)
-  // kEpiKeysShade rounds: 0 = every resident entry of the lane's list; 1 =
-  // its first entry only; 2 = the later entries below the round-1 minimum
-  int rround;
-  int rep_lane;  // replicated launches walked per lane instead of as packets
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -426,22 +397,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
-    if (SPRAY_DIAG_MODE != 3) tlas_mask_wave<W>(stl, ntlas, wstk, r, o4, d4, m);
-    if (SPRAY_DIAG_MODE == 1 || SPRAY_DIAG_MODE >= 3) {  // diagnostic: mask only
-      uint32_t pc = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) pc += __popcll(m[w]);
-      if (!ANY) {  // a whole 48-B record, as the real epilogue writes
-        float4* hp = reinterpret_cast<float4*>(hits + i);
-        const float4 h = make_float4(0.f, 0.f, 0.f, __uint_as_float(pc));
-        hp[0] = h;
-        hp[1] = h;
-        hp[2] = h;
-      } else {
-        occ[i] = uint8_t(pc);
-      }
-      return;
-    }
+    tlas_mask_wave<W>(stl, ntlas, wstk, r, o4, d4, m);
     // Closest hit keeps (t, prim, leaf) of the running winner in place.  A
     // later domain may only win with a strictly smaller t (the earlier
     // entry of the sorted domain list wins ties): its traversal starts with
@@ -491,11 +447,6 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
       const void* tris = nodes + __float_as_uint(dt.z);
       const uint32_t* prims = reinterpret_cast<const uint32_t*>(nodes + __float_as_uint(dt.w));
       if (COUNT) ++nvisit;
-      if (SPRAY_DIAG_MODE == 2) {  // diagnostic: no traversal
-        best.prim = sb;
-        best_dom = sb;
-        continue;
-      }
       if (ANY) {
         // the counting build walks in the canonical order the byte formula
         // is defined on; the fast build postpones leaves (same result)
@@ -531,9 +482,6 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
         h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
         h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
         h2 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-      } else if (SPRAY_DIAG_MODE == 2) {
-        h0 = make_float4(0.f, 0.f, 0.f, __uint_as_float(best.prim));
-        h1 = h2 = h0;
       } else {
         const SlotDesc s = slots[dom2slot[best_dom]];
         float hu, hv;
@@ -599,42 +547,11 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   }
 }
 
-#ifndef SPRAY_AO_GROUP
-#define SPRAY_AO_GROUP 0
-#endif
-// SPRAY_AO_GROUP=1 (rt_kernels_diag.inc): the AO any hit in 8-lane groups
-template <int W>
-__device__ void scene_ray_ao_group(const SceneArgs& A, size_t i, bool valid, bool walk,
-                                   const float4* stl, const float* sbox, const float4* sdom,
-                                   int32_t* gstk, int32_t* wstk);
-
-// Diagnostic variants of the any hit (rt_kernels_diag.inc, compiled only
-// into the builds that enable them: SPRAY_AH_SPREAD=1 -- the leaf triangles
-// of all lanes spread over the wave; SPRAY_AO_REFILL=R -- lane refill of the
-// persistent AO any hit).  Both bit-exact and slower than the shipped walk
-// ("Lane re-packing"); scripts/diag_variants.py builds
-// and checks them.
-#ifndef SPRAY_AH_SPREAD
-#define SPRAY_AH_SPREAD 0
-#endif
-template <int W, int STK, int EPI>
-__device__ void scene_ray_ah_wave(const SceneArgs& A, size_t i, bool valid, const float4* stl,
-                                  const float* sbox, const float4* sdom, int32_t* stk,
-                                  int32_t* wstk, uint8_t* wtask, uint8_t* whit);
-template <int W, int STK, uint32_t kMin, uint32_t kChunk>
-__device__ void scene_ray_ah_refill(const SceneArgs& A, size_t M, size_t S, const float4* stl,
-                                    const float* sbox, const float4* sdom, int32_t* stk,
-                                    int32_t* wstk);
-
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
   return x;
 }
-
-#if SPRAY_AH_SPREAD || SPRAY_AO_REFILL || SPRAY_WAVE_TIMES || SPRAY_AO_GROUP
-#include "rt_kernels_diag.inc"
-#endif
 
 // A wave's rays are coherent when every direction is within ~8 degrees of
 // the first valid lane's (camera rays of neighbouring pixels, shadow rays
@@ -725,46 +642,8 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   }
   Best best{ANY ? 0.f : d4.w, 0xFFFFFFFFu, 0xFFFFFFFFu};
   int best_dom = -1;
-  // replicated frames in two rounds (A.rround): 1 = the lane's first list
-  // entry only (when resident); 2 = the later entries, cut at the group's
-  // round-1 minimum t (A.tmin: an earlier entry holds it, so a later one
-  // wins only when strictly nearer -- best_dom -2 stands for that entry)
-  if (EPI == kEpiKeysShade && A.rround && valid) {
-    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-    int first = -1;
-    float tf = 0.f;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint64_t bits = m[w];
-      while (bits) {
-        const int jb = __ffsll((long long)bits) - 1;
-        bits &= bits - 1;
-        const int b = 64 * w + jb;
-        float tm;
-        aabb_ref(sbox + 6 * b, dr, tm);
-        if (first < 0 || tm < tf) {  // ascending ids: ties keep the smaller
-          first = b;
-          tf = tm;
-        }
-      }
-    }
-    const bool res = first >= 0 && (__float_as_uint(sdom[first].x) | __float_as_uint(sdom[first].y));
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const uint64_t fb = (first >= 0 && w == (first >> 6)) ? (1ull << (first & 63)) : 0ull;
-      m[w] = A.rround == 1 ? (res ? fb : 0ull) : (m[w] & ~fb);
-    }
-    if (A.rround == 2) {
-      const uint32_t ta = A.tmin[i];
-      if (ta != 0xFFFFFFFFu) {
-        best.t = __uint_as_float(ta);
-        best_dom = -2;
-      }
-    }
-  }
   bool occluded = false;
   for (;;) {
-    if (SPRAY_DIAG_MODE == 6) break;  // diagnostic: top-level mask only
     bool has = false;
 #pragma unroll
     for (int w = 0; w < W; ++w) has |= m[w] != 0;
@@ -811,7 +690,6 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     if (!nodes) continue;  // not resident here (or empty)
     const uint64_t tris = nodes + __builtin_amdgcn_readfirstlane(__float_as_uint(dt.z));
     const uint64_t prims = nodes + __builtin_amdgcn_readfirstlane(__float_as_uint(dt.w));
-    if (SPRAY_DIAG_MODE == 5) continue;  // diagnostic: no tree walks
     if (ANY) {
       bool hit = false;
       trace_tree_packet<true>(nodes, tris, prims, r, o4.w, d4.w, best, act, hit, wstk);
@@ -849,9 +727,6 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     h0 = make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
     h1 = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     h2 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-  } else if (SPRAY_DIAG_MODE == 7) {  // diagnostic: no epilogue, no spawn
-    h0 = make_float4(best.t, 0.f, 0.f, __uint_as_float(best.prim));
-    h1 = h2 = h0;
   } else {
     const SlotDesc s = slots[dom2slot[best_dom]];
     float hu, hv;
@@ -874,14 +749,6 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   if ((EPI == kEpiKeysShade || EPI == kEpiShadowFrame) && !A.hits) {
     // no hit records (the replicated frame keeps keys and shading only; an
     // in-situ frame without per-sample records keeps shading and shadows)
-  } else if (EPI == kEpiKeysShade && A.rround == 2) {
-    // round 2 replaces round 1's record only where it found a nearer hit
-    if (valid && best_dom >= 0) {
-      float4* hp = reinterpret_cast<float4*>(A.hits + i);
-      hp[0] = h0;
-      hp[1] = h1;
-      hp[2] = h2;
-    }
   } else if (SPRAY_HIT_TRANSPOSE && (i0 & 63) == 0 &&
       __ballot(valid && i == i0 + size_t(lane)) == ~0ull) {
     const float hv[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
@@ -942,9 +809,8 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     A.keys[i] = key;
     if (EPI == kEpiKeysShade) {
       A.tkeys[i] = best_dom >= 0 ? __float_as_uint(best.t) : 0xFFFFFFFFu;
-      // round 2 keeps round 1's shading where it found nothing nearer; no
-      // shading arrays: keys only (the replicated AO frame)
-      if ((A.rround == 2 && best_dom < 0) || !A.sh_valid) return;
+      // no shading arrays: keys only (the replicated AO frame)
+      if (!A.sh_valid) return;
       bool sp = false;
       if (best_dom >= 0) {
         spray_rt_hit h;
@@ -973,7 +839,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
     spawn = shade_pt_point(o3, d3, h, A.shade, pos, wi, L);
     if (spawn) A.sw[i] = make_float4(L[0], L[1], L[2], 0.f);
   }
-  if ((EPI == kEpiSpawn || EPI == kEpiShadow) && best_dom >= 0 && SPRAY_DIAG_MODE != 7) {
+  if ((EPI == kEpiSpawn || EPI == kEpiShadow) && best_dom >= 0) {
     spray_rt_hit h;
     h.t = h0.x;
     h.color = __float_as_uint(h1.w);
@@ -1037,31 +903,17 @@ __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, 
   if (EPI == kEpiKeysShade) {  // the dropped lane's results: a miss, no shading
     A.keys[j] = 0x7FFFFFFFFFFFFFFFull;  // the epilogue's miss key (kInsituMissKey)
     A.tkeys[j] = 0xFFFFFFFFu;
-    if (A.sh_valid && A.rround != 2) A.sh_valid[j] = 0;  // round 2 keeps round 1's
+    if (A.sh_valid) A.sh_valid[j] = 0;
   }
   return false;
 }
 
-// Diagnostic (SPRAY_WAVE_TIMES builds only): per wave of the persistent
-// scene launches, 100-MHz wall-clock stamps at entry, after the LDS
-// staging, when the band queues ran dry and at exit, plus its chunk count
-// and XCD -- the launch's ramp and tail (scripts/wave_times.py).
-#ifndef SPRAY_WAVE_TIMES
-#define SPRAY_WAVE_TIMES 0
-#endif
-// When a wave takes its next chunk: 1 = before tracing the current one (the
-// atomic in flight during the chunk, but the chunk dequeued ahead waits in
-// the wave's hands while the queues run dry); 0 = after it; 2 = during the
-// walk of the chunk's last packet, once that packet's rays have landed
-// (packet kernels, scene_ray_packet's post hook; the atomic overlaps the
-// walk and nothing waits in a wave's hands for longer than one packet).
-#ifndef SPRAY_DEQ_AHEAD
-#define SPRAY_DEQ_AHEAD 2
-#endif
-// guided chunk size near a band's end (closest-hit launches; 0 = off)
-#ifndef SPRAY_CHUNK_TAIL
-#define SPRAY_CHUNK_TAIL 0
-#endif
+// When a wave takes its next chunk: packet kernels during the walk of the
+// chunk's last packet, once that packet's rays have landed
+// (scene_ray_packet's post hook: the atomic overlaps the walk and nothing
+// waits in a wave's hands for longer than one packet; measured against
+// dequeuing before / after the chunk, DESIGN.md section 4 "Launch tail");
+// per-lane kernels after the chunk.
 
 // Persistent launch: each wave dequeues kChunk-ray chunks from kQueues
 // queues, each owning a contiguous band of the rays.  XCD x's waves start on
@@ -1152,13 +1004,7 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
   if (q.n < kShadowT) return;
   wave_lds_sync();
   const uint32_t cnt = q.n < 64 ? q.n : 64u;
-#if SPRAY_WAVE_TIMES
-  const unsigned long long t0 = wall_clock64();
-#endif
   shadow_trace<W>(A, q, cnt, stl, sbox, sdom, wstk);
-#if SPRAY_WAVE_TIMES
-  pkt_log(1u, cnt, t0);
-#endif
   // the remainder (< 64) moves to the front
   const uint32_t rest = q.n - cnt;
   const bool mv = lane < rest;
@@ -1196,8 +1042,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     SceneArgs A) {
   // packet form for the non-counting kernels; any-hit waves fall back to
   // the per-lane walk when their rays are not coherent (AO hemispheres)
-  constexpr bool kPacket =
-      TRAV != 0 && !COUNT && (SPRAY_DIAG_MODE == 0 || SPRAY_DIAG_MODE >= 5);
+  constexpr bool kPacket = TRAV != 0 && !COUNT;
   constexpr bool kAdaptive = kPacket && TRAV == 2;
   constexpr bool kLaneStack = !kPacket || kAdaptive;
   // the AO any hit's 4-wide walk keeps kLStk entries in LDS and the rest of
@@ -1206,23 +1051,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
                          SPRAY_AH_WW && SPRAY_AOGEN_LSTK < STK)
                             ? SPRAY_AOGEN_LSTK
                             : STK;
-  // the per-lane any hit as one wave-collective loop with the leaf
-  // triangles spread over the wave (scene_ray_ah_wave)
-  constexpr bool kSpread = ANY && !COUNT && kLaneStack && SPRAY_AH_SPREAD && SPRAY_AH_QNODES &&
-                           SPRAY_AH_WW && (EPI == kEpiNone || EPI == kEpiAoGen);
-  // the AO any hit of the persistent launch with lane refill
-  constexpr bool kGroup = ANY && !COUNT && EPI == kEpiAoGen && !kPacket && SPRAY_AO_GROUP &&
-                         SPRAY_AH_QNODES;
-  constexpr bool kRefill = ANY && !COUNT && EPI == kEpiAoGen && TRAV == 0 && !kSpread &&
-                           SPRAY_AO_REFILL > 0 && SPRAY_AH_QNODES && SPRAY_AH_WW &&
-                           SPRAY_DIAG_MODE == 0;
   __shared__ int32_t stack[(kLaneStack ? kLStk : 1) * kBlock];
-  static_assert(!kGroup || (kLaneStack ? kLStk : 1) * kBlock >= (kBlock / 8) * kQ4Stack,
-                "the 8-lane groups' stacks live in the per-lane stack array");
-  __shared__ uint8_t wtask[kSpread ? (kBlock / 64) * 512 : 1];
-  __shared__ uint8_t whit[kSpread ? kBlock : 1];
-  uint8_t* my_task = wtask + (kSpread ? (threadIdx.x >> 6) * 512 : 0);
-  uint8_t* my_hit = whit + (kSpread ? (threadIdx.x & ~63u) : 0);
   __shared__ float4 stl[4 * 64 * W];   // top-level tree
   __shared__ float sbox[6 * 64 * W];   // domain boxes (exact, for the sort)
   __shared__ float4 sdom[64 * W];      // DomTrav per domain
@@ -1235,9 +1064,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
   ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
                  sq_src + (kShadow ? (threadIdx.x >> 6) * kShadowQ : 0), 0u};
-  const unsigned long long wt0 = SPRAY_WAVE_TIMES ? wall_clock64() : 0ull;
-  unsigned long long wt1 = 0, wt2 = 0;
-  uint32_t wchunks = 0;
   size_t M = A.M;
   if (A.d_count) {  // ray count produced on the device
     const size_t dc = *A.d_count;
@@ -1261,7 +1087,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     }
   }
   __syncthreads();
-  if (SPRAY_WAVE_TIMES) wt1 = wall_clock64();
   unsigned nnode = 0, ntri = 0, nvisit = 0;
   int32_t* stk = stack + threadIdx.x;
   int32_t* wstk = wstack + (threadIdx.x >> 6) * STK;
@@ -1270,11 +1095,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   // spawned shadow rays of the wave, added to *sh_count once at its end (a
   // same-address atomic per chunk queued ~10^5 atomics behind each other)
   uint32_t wcount = 0;
-  if constexpr (kRefill) {  // always persistent (launch_scene_t); pairs, no index list
-    scene_ray_ah_refill<W, kLStk, uint32_t(SPRAY_AO_REFILL), uint32_t(SPRAY_CHUNK_AO)>(
-        A, M, S, stl, sbox, sdom, stk, wstk);
-    return;
-  }
   const bool persist = ANY ? (SPRAY_PERSIST_AH != 0 || A.persist != 0) : SPRAY_PERSIST_CH != 0;
   const int lane = threadIdx.x & 63;
   const uint32_t* __restrict__ idx = A.idx;
@@ -1286,19 +1106,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     if constexpr (rep_epi(EPI)) {
       float r6[6];
       const bool okr = rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres);
-      if (kPacket)
-        scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
-            A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
-      else if (okr)
-        scene_ray<W, ANY, COUNT, EPI == kEpiShadowGen ? kEpiNone : EPI, kLStk>(
-            A, j, stl, sbox, sdom, stk, wstk, nnode, ntri, nvisit, flag, pos, wi, r6);
+      scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
+          A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
-    else if (kGroup)
-      scene_ray_ao_group<W>(A, i, ok, ok, stl, sbox, sdom,
-                            stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
-    else if (kSpread)
-      scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task, my_hit);
     else if (ok)
       scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode, ntri,
                                       nvisit, flag, pos, wi);
@@ -1307,18 +1118,13 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   } else {
     constexpr uint32_t kChunk = ANY ? SPRAY_CHUNK_AH : SPRAY_CHUNK_CH;
     constexpr uint32_t kPerXcd = kQueues / 8;
-    // guided chunks (SPRAY_CHUNK_TAIL > 0, closest hit): a dequeue that
-    // finds fewer than SPRAY_CHUNK_TAIL rays left in its band takes one
-    // packet instead of kChunk, so the band's last rays spread over many
-    // waves instead of waiting in a few waves' hands
-    constexpr uint32_t kTail = ANY ? 0u : uint32_t(SPRAY_CHUNK_TAIL);
     // a batch of fewer than four kChunk chunks per wave (a rank's share of
     // a replicated frame) is dealt one packet per dequeue: with kChunk a few
     // waves take two chunks and walk their packets one after another while
     // the rest of the grid idles (measured: 331 K rays in 0.24 ms, the
     // latency of four packet walks in a row)
     const bool small = M < size_t(gridDim.x) * (kBlock / 64) * kChunk * 4;
-    const bool rtc = kTail != 0 || small;
+    const uint32_t csz = small ? 64u : kChunk;
     const uint32_t xcd = xcc_id() & 7u;
     const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
     for (uint32_t k = 0; k < uint32_t(kQueues); ++k) {
@@ -1327,107 +1133,52 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
       const size_t end = begin + S < M ? begin + S : M;
       if (begin >= end) continue;
       uint32_t* head = &A.heads[32 * q];
-      const auto chunk_at = [&](uint32_t b) -> uint32_t {
-        return (small || (kTail && begin + b + kTail >= end)) ? 64u : kChunk;
-      };
-      uint32_t base = 0, csz = kChunk;
+      uint32_t base = 0;
       if (lane == 0) {
         base = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (begin + base < end) {
-          csz = chunk_at(base);
-          base = atomicAdd(head, csz);
-        }
+        if (begin + base < end) base = atomicAdd(head, csz);
       }
       base = __builtin_amdgcn_readfirstlane(base);
-      csz = rtc ? __builtin_amdgcn_readfirstlane(csz) : kChunk;
       while (begin + base < end) {
-        // the next chunk is dequeued before this one is traced: the atomic's
-        // latency overlaps the traversal
-        uint32_t next = 0, ncsz = kChunk;
-        if (SPRAY_DEQ_AHEAD == 1 && lane == 0) next = atomicAdd(head, kChunk);
+        uint32_t next = 0;
         const size_t cbeg = begin + base;
-        for (uint32_t c = 0; c < (rtc ? csz : kChunk); c += 64) {
+        for (uint32_t c = 0; c < csz; c += 64) {
           const size_t j = cbeg + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
           const bool ok = j < end && i < (A.nrays ? A.nrays : A.M) && (!A.valid || A.valid[i]);
           flag = false;
-#if SPRAY_WAVE_TIMES
-          const unsigned long long pt0 = wall_clock64();
-#endif
-          if (kPacket && !kAdaptive && SPRAY_DEQ_AHEAD == 2) {
+          if (kPacket && !kAdaptive) {
             // the next chunk is dequeued by the chunk's last packet once its
             // rays have landed: the atomic overlaps that packet's walk, and
             // no chunk waits in a wave's hands while another is traced
-            const bool last = c + 64 >= (rtc ? csz : kChunk);
+            const bool last = c + 64 >= csz;
             float r6[6];
             const bool okr = rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres) : ok;
             scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
                 A, rep_epi(EPI) ? j : i, okr, stl, sbox, sdom, wstk, flag, pos, wi,
                 rep_epi(EPI) ? r6 : nullptr,
                 [&]() {
-                  if (last && lane == 0) {
-                    ncsz = chunk_at(base + csz);
-                    next = atomicAdd(head, ncsz);
-                  }
+                  if (last && lane == 0) next = atomicAdd(head, csz);
                 });
-          } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
+          } else if (kPacket && wave_coherent(A, i, ok)) {
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
-          else if (kGroup)
-            scene_ray_ao_group<W>(A, i, ok, ok, stl, sbox, sdom,
-                                  stack + (threadIdx.x >> 3) * kQ4Stack, wstk);
-          else if (kSpread)
-            scene_ray_ah_wave<W, kLStk, EPI>(A, i, ok, stl, sbox, sdom, stk, wstk, my_task,
-                                             my_hit);
-          else if (rep_epi(EPI)) {
-            float r6[6];
-            if (rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres))
-              scene_ray<W, ANY, COUNT, EPI == kEpiShadowGen ? kEpiNone : EPI, kLStk>(
-                  A, j, stl, sbox, sdom, stk, wstk, nnode, ntri, nvisit, flag, pos, wi, r6);
-          } else if (ok)
+          } else if (ok) {
             scene_ray<W, ANY, COUNT, EPI, kLStk>(A, i, stl, sbox, sdom, stk, wstk, nnode,
                                             ntri, nvisit, flag, pos, wi);
-#if SPRAY_WAVE_TIMES
-          pkt_log(0u, (cbeg + c) / 64, pt0);
-#endif
+          }
           if (EPI == kEpiSpawn) store_shadow(A, j < end, flag, i, pos, wi, wcount);
           if (kShadow)
             shadow_push<W>(A, sq, j < end, flag, i, pos, wi, stl, sbox, sdom, wstk, wcount);
         }
-        if ((SPRAY_DEQ_AHEAD == 0 || (SPRAY_DEQ_AHEAD == 2 && !(kPacket && !kAdaptive))) &&
-            lane == 0) {
-          ncsz = chunk_at(base + csz);
-          next = atomicAdd(head, ncsz);
-        }
+        if (!(kPacket && !kAdaptive) && lane == 0) next = atomicAdd(head, csz);
         base = __builtin_amdgcn_readfirstlane(next);
-        if (rtc) csz = __builtin_amdgcn_readfirstlane(ncsz);
-        ++wchunks;
       }
     }
   }
-  if (SPRAY_WAVE_TIMES) wt2 = wall_clock64();
   if (kShadow && sq.n) {  // the wave's last shadow rays (fewer than 64)
     wave_lds_sync();
-#if SPRAY_WAVE_TIMES
-    const unsigned long long t0 = wall_clock64();
-#endif
     shadow_trace<W>(A, sq, sq.n, stl, sbox, sdom, wstk);
-#if SPRAY_WAVE_TIMES
-    pkt_log(2u, sq.n, t0);
-#endif
   }
-#if SPRAY_WAVE_TIMES
-  if (persist && lane == 0) {
-    const uint32_t wid = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (wid < 16384) {
-      unsigned long long* o = g_wave_times + 5 * size_t(wid);
-      o[0] = wt0;
-      o[1] = wt1;
-      o[2] = wt2;
-      o[3] = wall_clock64();
-      o[4] = (unsigned long long)wchunks | ((unsigned long long)(xcc_id() & 7u) << 32);
-    }
-  }
-#endif
   if ((EPI == kEpiSpawn || kShadow) && A.sh_count && wcount && lane == 0)
     atomicAdd(A.sh_count, wcount);
   if (COUNT) {
@@ -1819,9 +1570,6 @@ __global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
 // contiguous and the lanes of one hit share its record loads.  Output order
 // is q ascending -- the reference's (hits in order, samples l = 0..ns-1):
 // count pass (ao_ok), one scan of the tile totals, write pass.
-#ifndef SPRAY_AO_DIAG
-#define SPRAY_AO_DIAG 0
-#endif
 constexpr int kAoPer = 16;
 constexpr int kAoTile = kBlock * kAoPer;
 // source rays per sample-major trace-order block (divides kBlock)
@@ -1893,16 +1641,7 @@ __global__ __launch_bounds__(kBlock) void k_spawn_ao_write(
     const uint32_t q = base + uint32_t(r * kBlock);
     const uint32_t i = q / ns;
     const uint32_t k = spre[r][threadIdx.x];
-#if SPRAY_AO_DIAG == 1  // diagnostic: stores only
-    AoOut a;
-    a.o[0] = a.o[1] = a.o[2] = float(i);
-    a.w[0] = a.w[1] = a.w[2] = float(q);
-#else
     const AoOut a = ao_sample(rays[i], hits[i], pixid[i], int(q - i * ns), int(ns));
-#endif
-#if SPRAY_AO_DIAG == 2  // diagnostic: sampling only
-    if (a.w[0] != 12345.f) continue;
-#endif
     float4* op = reinterpret_cast<float4*>(out + k);
     op[0] = make_float4(a.o[0], a.o[1], a.o[2], kRayEpsilon);
     op[1] = make_float4(a.w[0], a.w[1], a.w[2], kInf);
@@ -2185,29 +1924,6 @@ __global__ __launch_bounds__(kBlock) void k_iota(uint32_t* __restrict__ out, uin
 
 }  // namespace
 
-#if SPRAY_WAVE_TIMES
-// copies the last persistent scene launch's wave stamps (n words, 5 per wave)
-extern "C" int spray_rt_diag_packet_log(void* host_log, void* host_n, int reset) {
-  if (reset) {
-    static unsigned int zero[6144];
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_pkt_n), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-  }
-  if (hipMemcpyFromSymbol(host_n, HIP_SYMBOL(g_pkt_n), 6144 * 4, 0, hipMemcpyDeviceToHost) !=
-      hipSuccess)
-    return -1;
-  return hipMemcpyFromSymbol(host_log, HIP_SYMBOL(g_pkt_log), size_t(2) * 6144 * 256 * 8, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess
-             ? 0
-             : -1;
-}
-extern "C" int spray_rt_diag_wave_times(void* host, size_t n) {
-  if (n > 5 * 16384) n = 5 * 16384;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_times), n * 8, 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess
-             ? 0
-             : -1;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // launchers
@@ -2249,12 +1965,8 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
-  // the AO rays generated in the lanes walk with lane refill at every size
-  constexpr bool kRefillLaunch = ANY && !COUNT && EPI == kEpiAoGen && TRAV == 0 &&
-                                 SPRAY_AO_REFILL > 0 && SPRAY_AH_QNODES && SPRAY_AH_WW &&
-                                 !SPRAY_AH_SPREAD && SPRAY_DIAG_MODE == 0;
-  const bool kPersist = kRefillLaunch || (ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays)
-                                              : SPRAY_PERSIST_CH != 0);
+  const bool kPersist =
+      ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays) : SPRAY_PERSIST_CH != 0;
   a.persist = kPersist ? 1 : 0;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
   if (kPersist && !grid) {
@@ -2290,7 +2002,6 @@ static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherenc
   if constexpr (ANY && EPI == kEpiAoGen) {
     return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
   } else if constexpr (rep_epi(EPI)) {  // camera rays and point-light shadows
-    if (a.rep_lane) return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
   } else if constexpr (!ANY && EPI != kEpiNone) {
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
@@ -2683,13 +2394,9 @@ hipError_t launch_spawn_ao_pairs(hipStream_t s, const spray_rt_ray* rays,
 hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                   size_t n, const uint32_t* idx, size_t nc,
                                   const float* shade10, spray_rt_hit* hits, uint64_t* keys,
-                                  uint32_t* tkeys, float* sw, uint8_t* sv, int round,
-                                  const uint32_t* tmin_round1, bool per_lane) {
+                                  uint32_t* tkeys, float* sw, uint8_t* sv) {
   if (nc == 0) return hipSuccess;
   SceneArgs a = scene_args(v, rays, nc);
-  a.rround = round;
-  a.rep_lane = per_lane && round == 0 ? 1 : 0;
-  a.tmin = tmin_round1;
   a.nrays = n;
   a.idx = idx;
   a.hits = hits;
@@ -2703,11 +2410,9 @@ hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray
 
 hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                     size_t n, const uint32_t* idx, size_t nc,
-                                    const uint32_t* tmin, const float* shade10, uint8_t* occ,
-                                    bool per_lane) {
+                                    const uint32_t* tmin, const float* shade10, uint8_t* occ) {
   if (nc == 0) return hipSuccess;
   SceneArgs a = scene_args(v, rays, nc);
-  a.rep_lane = per_lane ? 1 : 0;
   a.nrays = n;
   a.idx = idx;
   a.tmin = tmin;

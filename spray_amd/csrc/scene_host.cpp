@@ -531,6 +531,14 @@ int GpuScene::init(const std::string& desc, const std::string& ply_path,
       r = load(int(id), &s);
       if (r) return r;
     }
+    // every domain is resident for good: no miss will read a pinned image
+    // again (an upload after all would rebuild it, build_image)
+    if (hipDeviceSynchronize() != hipSuccess) return fail(SPRAY_RT_ERR_HIP, "warm-up uploads");
+    for (void*& p : pinned_)
+      if (p) {
+        (void)hipHostFree(p);
+        p = nullptr;
+      }
   }
   return SPRAY_RT_OK;
 }
@@ -561,23 +569,25 @@ int GpuScene::build_image(int id, std::string* err) {
     return SPRAY_RT_ERR_ARG;
   }
   void* p = nullptr;
-  if (hipHostMalloc(&p, img.bytes.size(), hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&p, img.nbytes, hipHostMallocDefault) != hipSuccess) {
     *err = "pinned host memory for a domain image";
     return SPRAY_RT_ERR_NOMEM;
   }
-  std::memcpy(p, img.bytes.data(), img.bytes.size());
+  std::memcpy(p, img.bytes.data(), img.nbytes);
   pinned_[size_t(id)] = p;
+  std::vector<char>().swap(img.bytes);  // one host copy: the pinned one
   return SPRAY_RT_OK;
 }
 
 // The misses of an LRU cache would each build a domain image inside the
 // tracer's `omp single` while every other thread waits; building them all up
 // front (in parallel: the meshes first, then one image per task) leaves a
-// miss one async DMA.  Bounded by a host-memory budget (the images' bytes
-// ~ 100 B per triangle); past it images are built on their first miss.
+// miss one async DMA.  Bounded by a budget of page-locked host memory (the
+// images' bytes ~ 100 B per triangle, one pinned copy each); past it images
+// are built on their first miss.
 int GpuScene::prebuild_images() {
   const char* e = std::getenv("SPRAY_SCENE_PREBUILD_MB");
-  const double budget_mb = e ? std::atof(e) : 16384.0;
+  const double budget_mb = e ? std::atof(e) : 4096.0;
   if (budget_mb <= 0.0) return SPRAY_RT_OK;
   double tris = 0.0;
   for (const Domain& d : domains_) {

@@ -132,7 +132,8 @@ class GpuScene {
   // thread-safe for distinct ids once the domain's PLY is in ply_cache_
   int build_image(int id, std::string* err);
   // every image built up front, in parallel, when they fit the host budget
-  // (SPRAY_SCENE_PREBUILD_MB, default 16384; 0 = each on its first miss)
+  // (SPRAY_SCENE_PREBUILD_MB of pinned memory, default 4096; 0 = each on
+  // its first miss); an all-resident cache frees them after its warm-up
   int prebuild_images();
   int fail(int code, const std::string& msg);
 

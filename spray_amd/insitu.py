@@ -97,7 +97,8 @@ _RED = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int)
 
 
 class Transport(C.Structure):
-    _fields_ = [("user", C.c_void_p), ("alltoallv", _A2A), ("allreduce_u64", _AR),
+    _fields_ = [("struct_size", C.c_size_t), ("user", C.c_void_p), ("alltoallv", _A2A),
+                ("allreduce_u64", _AR),
                 ("reduce_f32", _RED), ("allreduce_min_u64", _AR), ("allreduce_sum_u8", _AR)]
 
 
@@ -180,7 +181,7 @@ class _HostCollectives:
                 return 1
 
         self._cbs = (_A2A(a2a), _AR(ar), _RED(red), _AR(armin), _AR(arsum8))  # kept alive
-        self.struct = Transport(None, *self._cbs)
+        self.struct = Transport(C.sizeof(Transport), None, *self._cbs)
 
 
 class InsituRecords:
@@ -355,4 +356,4 @@ class _LocalCollectives:
 
         self._cbs = (_A2A(a2a), _AR(lambda u, d, n: 0), _RED(lambda u, d, n, r: 0),
                      _AR(lambda u, d, n: 0), _AR(lambda u, d, n: 0))
-        self.struct = Transport(None, *self._cbs)
+        self.struct = Transport(C.sizeof(Transport), None, *self._cbs)

@@ -28,6 +28,10 @@
 
 #include "spray_scene.hpp"
 
+// Embree 2's opaque scene handle (embree2/rtcore_scene.h), which the
+// reference's Scene::SceneInfo holds (src/render/scene.h:57-60).
+typedef struct __RTCScene* RTCScene;
+
 namespace glm {
 
 struct vec2 {
@@ -66,6 +70,15 @@ inline float pow(float x, float y) { return float(std::pow(double(x), double(y))
 }  // namespace glm
 
 namespace spray {
+
+// Scene::SceneInfo as the reference declares it (scene.h:57-60); the
+// tracers hold `spray::SceneInfo sinfo_` (ooc_pcontext.h:83) and pass
+// sinfo.rtc_scene / sinfo.cache_block to the scene (ooc_tcontext.inl:37,
+// 59, 79).  The adapter takes it as is: its handle carries the slot.
+struct SceneInfo {
+  RTCScene rtc_scene;
+  int cache_block;
+};
 
 #define MOCK_SPRAY_PI 3.14159265358979323846       // SPRAY_PI = M_PI (spray.h:48)
 #define MOCK_SPRAY_ONE_OVER_PI 0.3183098861837907f  // spray.h:50

@@ -209,7 +209,7 @@ int run_single(const char* desc, const char* ply, int T, int cache, bool current
     for (int d : lists[i]) queue[d].push_back(long(i));
 
   // the drains: load in omp single, every thread intersects / occludes
-  spray_amd::SceneInfo sinfo;
+  spray::SceneInfo sinfo;  // the reference's own record (ooc_pcontext.h:83)
 #pragma omp parallel num_threads(T)
   {
     RTCRayIntersection rtc_isect_;
@@ -315,7 +315,7 @@ int run_batched(const char* desc, const char* ply, int T, int cache, int img) {
   };
   std::vector<std::vector<Part>> parts(nd, std::vector<Part>(T));
   std::atomic<long> npair{0}, nshadow{0}, ncalls{0};
-  spray_amd::SceneInfo sinfo;
+  spray::SceneInfo sinfo;  // the reference's own record (ooc_pcontext.h:83)
   // warm the lanes (first call per thread creates its stream)
   scene.load(0, &sinfo);
 #pragma omp parallel num_threads(T)
@@ -602,7 +602,7 @@ int run_shade(const char* desc, const char* ply, int T, int cache, int img) {
     std::vector<RTCRay> srays;
   };
   std::vector<std::vector<Part>> parts(nd, std::vector<Part>(T));
-  spray_amd::SceneInfo sinfo;
+  spray::SceneInfo sinfo;  // the reference's own record (ooc_pcontext.h:83)
 #pragma omp parallel num_threads(T)
   {
     const int me = omp_get_thread_num();

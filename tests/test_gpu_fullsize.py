@@ -189,15 +189,16 @@ def test_ao16_full_frame_vs_oracle(spray, oracle, oframe):
     scene.close()
 
 
-def _oracle_insitu_frame(oracle, shader_rows):
+def _oracle_insitu_frame(oracle, shader_rows, kind="pt", samples=1):
     """The whole-scene oracle of the in-situ frame (one blocking tile = the
-    frame, (pixid, sample) seeds), one PT bounce, vectorised: per sample its
-    hit, shadow-slot bits; the image; (radiance, shadow) totals."""
+    frame, (pixid, sample) seeds), one PT bounce (or AO with `samples` rays
+    per hit), vectorised: per sample its hit, shadow-slot bits; the image;
+    (radiance, shadow) totals."""
     c = BENCH_CAMERA
     cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], W, H)
     org, d, pix, sam = oracle.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), (0, 0, W, H))
     sc, doms, _ = oracle.load_scene(WAVELETS64, SCENES)
-    sh = oracle.shader("pt", 1, 1, (0.4, 0.4, 0.4), 10.0, shader_rows)
+    sh = oracle.shader(kind, 1, samples, (0.4, 0.4, 0.4), 10.0, shader_rows)
     bs = oracle.scene_bsdfs(doms)
     n = len(org)
     hits, _ = sc.intersect(org, d)
@@ -209,12 +210,17 @@ def _oracle_insitu_frame(oracle, shader_rows):
     so, sd, sw, sv, bad = oracle.shade(sh, bs, 0, org, d, hits, w, valid, pix, sam)
     occ = np.zeros(n * ns, np.uint8)
     sel = np.flatnonzero(sv)
-    occ[sel], _ = sc.occluded(so[sel], sd[sel])
+    occ[sel], _ = sc.occluded(np.ascontiguousarray(so[sel]), np.ascontiguousarray(sd[sel]))
+    del so, sd
     image = np.zeros(W * H * 4, np.float32)
     oracle.film(image, pix, SPP, ns, sw, sv, occ, 1.0 / SPP)
-    bits = (np.uint64(1) << np.arange(ns, dtype=np.uint64))
-    vb = (sv.reshape(n, ns).astype(np.uint64) * bits).sum(1).astype(np.uint64)
-    ob = ((sv & occ).reshape(n, ns).astype(np.uint64) * bits).sum(1).astype(np.uint64)
+    del sw
+    vb = np.zeros(n, np.uint64)
+    ob = np.zeros(n, np.uint64)
+    svm, ocm = sv.reshape(n, ns), (sv & occ).reshape(n, ns)
+    for k in range(ns):  # slot k = bit k, one column at a time (ns up to 16 here)
+        vb |= svm[:, k].astype(np.uint64) << np.uint64(k)
+        ob |= ocm[:, k].astype(np.uint64) << np.uint64(k)
     shaded = hits["domain"] >= 0
     order = np.argsort(sam[shaded], kind="stable")
     return {"samid": sam[shaded][order], "hits": hits[shaded][order], "svalid": vb[shaded][order],
@@ -264,9 +270,10 @@ def test_insitu_full_frame_rccl_one_rank(spray, oracle):
     rt.close()
 
 
-def _rep_rank_main(rank, world, port, out, mode):
+def _rep_rank_main(rank, world, port, out, mode, kind="pt"):
     """One rank of the full-size replicated-ray frame (8 processes sharing the
-    GPU, gloo + the engine's host transport): records to out/r<rank>.npz."""
+    GPU, gloo + the engine's host transport; kind "pt" or "ao" = AO-16):
+    records to out/r<rank>.npz."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -292,8 +299,8 @@ def _rep_rank_main(rank, world, port, out, mode):
         pix = torch.empty(N, dtype=torch.int32, device="cuda")
         sam = torch.empty(N, dtype=torch.int32, device="cuda")
         rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), (0, 0, W, H), rays, pix, sam)
-        sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
-                                         lights=lights)
+        sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1, ks=SHADE[6:9],
+                                         shininess=SHADE[9], lights=lights)
         image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
         recs = insitu.InsituRecords(N // 2)
         tot = eng.trace_frame(sh, rays, pix, sam, SPP, image, recs)
@@ -310,27 +317,20 @@ def _rep_rank_main(rank, world, port, out, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_replicated_full_frame_eight_ranks(spray, oracle, mode):
-    """configs[2] at N = 8, the bench's replicated-ray frame at full size
-    (1024x1024x8spp, every eye ray on every rank, 8 domains per rank, both
-    partitions), 8 engine processes sharing the GPU over the host transport:
-    every shaded sample's record bit-exact against the whole-scene oracle,
-    shaded exactly once across the ranks, totals exact, the composited image
-    within summation order."""
+def _run_replicated(world, mode, kind):
     import socket
     import tempfile
-    from spray_amd.engine import host_parse_scene
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    world = 8
     with tempfile.TemporaryDirectory() as out:
-        torch.multiprocessing.spawn(_rep_rank_main, args=(world, port, out, mode), nprocs=world)
-        parts = [dict(np.load(os.path.join(out, "r%d.npz" % r))) for r in range(world)]
-    _, lights = host_parse_scene(WAVELETS64, SCENES)
-    ref = _oracle_insitu_frame(oracle, [tuple(float(x) for x in l) for l in lights])
+        torch.multiprocessing.spawn(_rep_rank_main, args=(world, port, out, mode, kind),
+                                    nprocs=world)
+        return [dict(np.load(os.path.join(out, "r%d.npz" % r))) for r in range(world)]
+
+
+def _check_replicated(parts, ref):
     for p in parts:
         assert tuple(p["tot"]) == ref["totals"]
     assert sum(len(p["samid"]) > 10_000 for p in parts) >= 4  # the shading is spread
@@ -342,3 +342,40 @@ def test_replicated_full_frame_eight_ranks(spray, oracle, mode):
     assert np.array_equal(np.concatenate([p["svalid"] for p in parts])[order], ref["svalid"])
     assert np.array_equal(np.concatenate([p["occluded"] for p in parts])[order], ref["occluded"])
     np.testing.assert_allclose(parts[0]["image"], ref["image"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_replicated_full_frame_eight_ranks(spray, oracle, mode):
+    """configs[2] at N = 8, the bench's replicated-ray frame at full size
+    (1024x1024x8spp, every eye ray on every rank, 8 domains per rank, both
+    partitions), 8 engine processes sharing the GPU over the host transport:
+    every shaded sample's record bit-exact against the whole-scene oracle,
+    shaded exactly once across the ranks, totals exact, the composited image
+    within summation order."""
+    from spray_amd.engine import host_parse_scene
+    parts = _run_replicated(8, mode, "pt")
+    _, lights = host_parse_scene(WAVELETS64, SCENES)
+    _check_replicated(parts, _oracle_insitu_frame(
+        oracle, [tuple(float(x) for x in l) for l in lights]))
+
+
+@pytest.fixture(scope="module")
+def ao_insitu_ref(oracle):
+    from spray_amd.engine import host_parse_scene
+    _, lights = host_parse_scene(WAVELETS64, SCENES)
+    ref = _oracle_insitu_frame(oracle, [tuple(float(x) for x in l) for l in lights], "ao", 16)
+    assert ref["bad"] == 0 and 30_000_000 < ref["totals"][1] < 40_000_000
+    return ref
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_replicated_ao16_full_frame_eight_ranks(spray, oracle, ao_insitu_ref, mode):
+    """configs[4] at N = 8, the bench's N > 1 "ao" line at its size: the
+    replicated-ray AO-16 frame (1024x1024x8spp, ~36.6 M AO rays, 8 domains
+    per rank, both partitions), 8 engine processes sharing the GPU over the
+    host transport -- every shaded sample's winning record and all 16
+    AO-slot spawn / occlusion bits bit-exact against the whole-scene oracle
+    (ooc::ShaderAo, src/ooc/ooc_shader_ao.h:131-144), each sample shaded
+    exactly once across the ranks, totals exact, rank 0's film within
+    summation order."""
+    _check_replicated(_run_replicated(8, mode, "ao"), ao_insitu_ref)

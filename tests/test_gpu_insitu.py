@@ -267,9 +267,7 @@ def test_engine_two_ranks_one_owner(oracle):
 
 @pytest.mark.parametrize("world,mode,case", [(2, 0, "pt1"), (8, 0, "pt1"), (8, 1, "pt1"),
                                              (3, 1, "pt1"), (2, 0, "ao16"), (3, 1, "ao16"),
-                                             (8, 0, "ao16"), (8, 1, "ao16"), (8, 1, "pt1-u64"),
-                                             (8, 0, "pt1-r2"), (3, 1, "pt1-r2"),
-                                             (8, 1, "pt1-lane"), (2, 0, "ao16-lane")])
+                                             (8, 0, "ao16"), (8, 1, "ao16"), (8, 1, "pt1-u64")])
 def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
     """spray_rt_insitu_trace_frame with world processes sharing the GPU over
     the host transport: every eye ray on every rank, the keys' MIN and the
@@ -280,19 +278,11 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
     shaded sample bit-exact against the whole-scene
     oracle, totals exact, the image within summation-order tolerance; both
     partitions.  PT's winner keys are split (a MIN of the t bits, then of
-    the list positions at that t); "pt1-u64" keeps the 64-bit key MIN,
-    "pt1-r2" walks each ray's first list entry, then the rest below the
-    group's first-round minimum."""
+    the list positions at that t); "pt1-u64" keeps the 64-bit key MIN."""
     import pickle
     if case == "pt1-u64":
         monkeypatch.setenv("SPRAY_INSITU_SPLIT_KEYS", "0")
         case = "pt1"
-    if case == "pt1-r2":  # the keyed walk in two rounds (first entries, then the rest)
-        monkeypatch.setenv("SPRAY_INSITU_ROUNDS", "2")
-        case = "pt1"
-    if case.endswith("-lane"):  # the replicated launches walked per lane
-        monkeypatch.setenv("SPRAY_INSITU_LANE", "1")
-        case = case[:-5]
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
                                     args=(world, _free_port(), out, case, False, True, mode),
