@@ -671,6 +671,44 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t ins, const spray_rt_shader* sh
                                 const spray_rt_ray* rays, const int32_t* pixid,
                                 const int32_t* samid, size_t n, int spp, float* image_rgba,
                                 const spray_rt_insitu_rec* rec, unsigned long long totals[3]);
+/* The replicated-ray frame of a camera (the N > 1 in-situ frame of
+ * bench.py): the frame of spray_rt_insitu_trace_frame for the eye rays of
+ * the whole image_w x image_h x spp image as one blocking tile
+ * (insitu::genMultiSampleEyeRays, insitu_ray.h:103-182; the rays, pixel and
+ * sample ids spray_rt_eye_rays_insitu writes for tile = stripe = image),
+ * generated in the lanes from cam (spray_rt_camera_init's 14 floats, for
+ * that image size) -- no ray buffer.  Each rank's work follows its own
+ * domains instead of the frame: the pixels whose eye rays may enter one of
+ * its resident domain boxes (the boxes' conservative screen footprints) are
+ * the closest-hit launch, the pixels whose hit points' point-light shadow
+ * rays may cross one of its boxes the any-hit launch; the ranks agree
+ * through the same collectives over U (the pixels any domain box may be
+ * seen through, the same on every rank), with no host read.  Same results
+ * per sample as spray_rt_insitu_trace_frame on those rays.  AO: U's eye rays
+ * generated in one pass, then the replicated AO frame over them.  World 1:
+ * the eye rays, then the all-local frame. */
+int spray_rt_insitu_trace_camera(spray_rt_insitu_t ins, const spray_rt_shader* shader,
+                                 const float cam[14], int image_w, int image_h, int spp,
+                                 float* image_rgba, const spray_rt_insitu_rec* rec,
+                                 unsigned long long totals[3]);
+/* A view-aligned partition of n domain boxes (float[n][6]) over nranks for
+ * camera cam: the box centres projected to the image and dealt by recursive
+ * median splits (image x, then y, alternating; ties by domain id) into
+ * groups of n / nranks (+1) -- each rank the domains along neighbouring
+ * lines of sight, so that a ray's domain list mostly stays on one rank.  An
+ * addition to InsituPartition's modes (data_partition.h:59-155) for a fixed
+ * camera; results do not depend on the partition. */
+int spray_rt_insitu_partition_view(const float* boxes, int n, const float cam[14], int nranks,
+                                   int* owner);
+/* Footprint primitives of the camera frames (tests): the inclusive pixel
+ * rectangle {x0, x1, y0, y1} holding every eye ray of cam that may enter
+ * box (returns 0 = none, 1 = rect, 2 = the whole image; -1 bad arguments);
+ * the box holding every hit point inside scene whose shadow ray toward the
+ * point light may cross box (returns 0 = out holds it, 1 = everywhere). */
+int spray_rt_camera_box_rect(const float cam[14], int image_w, int image_h, const float box[6],
+                             int rect[4]);
+int spray_rt_camera_shadow_region(const float box[6], const float scene[6], const float light[3],
+                                  float out[6]);
 /* Per-phase device time of the traces since the last call (then reset),
  * HIP events on the context's stream, when phase timing is on
  * (spray_rt_insitu_set_timing).  out_ms[9]; *nphases = phases of the last

@@ -138,6 +138,10 @@ SIGNATURES = {
     "spray_rt_insitu_partition_mode": (I, [P, I, P, I, I, P]),
     "spray_rt_insitu_trace": (I, [P, P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_insitu_trace_frame": (I, [P, P, P, P, P, SZ, I, P, P, P]),
+    "spray_rt_insitu_trace_camera": (I, [P, P, P, I, I, I, P, P, P]),
+    "spray_rt_insitu_partition_view": (I, [P, I, P, I, P]),
+    "spray_rt_camera_box_rect": (I, [P, I, I, P, P]),
+    "spray_rt_camera_shadow_region": (I, [P, P, P, P]),
     "spray_rt_insitu_set_timing": (I, [P, I]),
     "spray_rt_insitu_phase_times": (I, [P, P, P]),
     "spray_rt_insitu_composite": (I, [P, P, SZ]),

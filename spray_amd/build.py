@@ -25,9 +25,10 @@ LIB = os.path.join(LIBDIR, "libspray_rt.so")
 ARCH = os.environ.get("SPRAY_AMD_ARCH", "gfx950")
 
 SOURCES = ["rt_kernels.hip", "ooc_kernels.hip", "frame_kernels.hip", "insitu_kernels.hip",
-           "rt_api.cpp", "ooc.cpp", "frame.cpp", "insitu.cpp", "bvh_build.cpp", "scene_host.cpp"]
-HEADERS = ["rt_common.h", "rt_device.h", "shade_device.h", "rt_kernels.h", "rt_ctx.h",
-           "bvh_build.h", "scene_host.h", "insitu_kernels.h"]
+           "rt_api.cpp", "ooc.cpp", "frame.cpp", "insitu.cpp", "bvh_build.cpp", "scene_host.cpp",
+           "footprint.cpp"]
+HEADERS = ["rt_common.h", "rt_device.h", "shade_device.h", "cam_device.h", "rt_kernels.h", "rt_ctx.h",
+           "bvh_build.h", "scene_host.h", "insitu_kernels.h", "footprint.h"]
 PUBLIC = [os.path.join(ROOT, "include", h) for h in ("spray_rt.h", "spray_scene.h")]
 
 

@@ -29,6 +29,7 @@
 #include <string>
 #include <vector>
 
+#include "footprint.h"
 #include "insitu_kernels.h"
 #include "rt_ctx.h"
 #include "rt_kernels.h"
@@ -126,9 +127,11 @@ struct InsituTransport {
   virtual bool has_rep() const { return true; }
   virtual int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) = 0;
   virtual int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) = 0;
-  // split keys: MIN of u32 t bits; MIN of u8 list positions on stream st
-  // (overlapping the main stream's work; the host form runs it in order)
-  virtual int allreduce_min_u32(spray_rt_insitu* I, uint32_t* dev, size_t n) = 0;
+  // split keys: MIN of u32 t bits (src -> dst; in place when equal); MIN of
+  // u8 list positions on stream st (overlapping the main stream's work; the
+  // host form runs it in order)
+  virtual int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
+                                size_t n) = 0;
   virtual int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t st) = 0;
   // rehearsal only: the rank's device work runs while it holds a lock
   // shared by the group's processes (SPRAY_INSITU_SERIAL), so the phase
@@ -174,6 +177,15 @@ struct spray_rt_insitu {
   // split keys: t bits and list positions over C; the list positions'
   // all-reduce runs on a second stream (cs) beside the shadow any hit
   DBuf rtk, rlp, rbmax;
+  // camera frames (trace_camera): the run tables of the last camera (U =
+  // the pixels any box may be seen through; E / S = this rank's eye and
+  // shadow footprints), their key, and the frame's arrays over U
+  std::vector<float> cam_key;
+  DBuf tu_runs, tu_first, te_runs, te_first, ts_runs, ts_first;
+  CamTable tu{}, te{}, ts{};
+  uint32_t tu_pixmax = 0;
+  DBuf ctmin, ccomp, crays, cpix, csam, ciota;
+  size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
   // phase timing (spray_rt_insitu_set_timing): events on the stream
@@ -280,9 +292,10 @@ struct RcclTransport : InsituTransport {
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclSum, comm, stream_of(I->ctx)),
                "ncclAllReduce(sum u8)");
   }
-  int allreduce_min_u32(spray_rt_insitu* I, uint32_t* dev, size_t n) override {
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
+                        size_t n) override {
     ++I->st[4];
-    return chk(I, nccl().AllReduce(dev, dev, n, ncclUint32, ncclMin, comm, stream_of(I->ctx)),
+    return chk(I, nccl().AllReduce(src, dst, n, ncclUint32, ncclMin, comm, stream_of(I->ctx)),
                "ncclAllReduce(min u32)");
   }
   int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t st) override {
@@ -365,8 +378,11 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u32(spray_rt_insitu* I, uint32_t* dev, size_t n) override {
-    return min_widened(I, dev, n);
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
+                        size_t n) override {
+    if (src != dst && n)
+      HIPCHK(I->ctx, hipMemcpyAsync(dst, src, n * 4, hipMemcpyDeviceToDevice, stream_of(I->ctx)));
+    return min_widened(I, dst, n);
   }
   int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t) override {
     return min_widened(I, dev, n);
@@ -978,7 +994,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
   if (split) {
-    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, nc));
+    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, tk, nc));
     MARK(3);
     GROW(I->rlp, nc + 1);
     lp = I->rlp.as<uint8_t>();
@@ -1079,17 +1095,24 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
 // winners.  Totals: radiance rays n, AO rays = the pairs (the same count on
 // every rank), no all-reduce.  Phases: 0 cull + select, 2 keyed closest hit,
 // 3 publish, 4 AO spawn, 5 own pairs + any hit + count fields, 6 film.
+// C (idx_c != null, nc rays, the largest pixel id pixmax_c): the camera
+// frame's U slots, whose rays / pixels / samples the caller generated (C =
+// all of them); else C' of the given eye rays.
 int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
                         const int32_t* pixid, const int32_t* samid, size_t n, int spp,
                         float* image, const spray_rt_insitu_rec* rec,
-                        unsigned long long totals[3]) {
+                        unsigned long long totals[3], const uint32_t* idx_c = nullptr,
+                        size_t nc_c = 0, uint32_t pixmax_c = 0) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
   const int ns = P->samples;
-  size_t nc = 0;
-  uint32_t pixmax = 0;
+  size_t nc = nc_c;
+  uint32_t pixmax = pixmax_c;
   MARK(0);
-  CALL(rep_cull_select(I, rays, pixid, n, true, &nc, &pixmax));
+  if (!idx_c) {
+    CALL(rep_cull_select(I, rays, pixid, n, true, &nc, &pixmax));
+    idx_c = I->ridx_c.as<uint32_t>();
+  }
   if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C'| >= 2^27");
   // own keyed closest hits over C' (keys and hit records at C' positions)
   MARK(2);
@@ -1098,7 +1121,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   GROW(I->rkeys_c, nc * 8 + 8);
   GROW(I->rtk, nc * 4 + 4);
   const float zero10[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, I->ridx_c.as<uint32_t>(), nc, zero10,
+  HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, zero10,
                                    I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
                                    I->rtk.as<uint32_t>(), nullptr, nullptr));
   HIPCHK(c, hipMemcpyAsync(I->rkeys_c.p, I->rkeys_n.p, nc * 8, hipMemcpyDeviceToDevice, s));
@@ -1127,7 +1150,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   A.rank = I->rank;
   A.ns = ns;
   A.fb = fb;
-  A.idx_c = I->ridx_c.as<uint32_t>();
+  A.idx_c = idx_c;
   A.keys_c = I->rkeys_c.as<uint64_t>();
   A.keys_n = I->rkeys_n.as<uint64_t>();
   A.rays = reinterpret_cast<const float4*>(rays);
@@ -1200,6 +1223,237 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   return SPRAY_RT_OK;
 }
 
+// ---- replicated frames from the camera (spray_rt_insitu_trace_camera) ----
+// The run tables of camera F (footprint.h): U, this rank's eye table E (its
+// resident boxes' footprints) and shadow table S (the hit points whose
+// point-light shadow ray may cross a resident box; light == null: none),
+// rebuilt when the camera, the light or the residency changes.
+int upload_table(spray_rt_insitu* I, const fp::Table& t, DBuf& runs, DBuf& first, CamTable* out) {
+  spray_rt_ctx* c = I->ctx;
+  GROW(runs, t.runs.size() * sizeof(CamRun));
+  GROW(first, t.first.size() * sizeof(uint32_t));
+  HIPCHK(c, hipMemcpy(runs.p, t.runs.data(), t.runs.size() * sizeof(CamRun),
+                      hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(first.p, t.first.data(), t.first.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice));
+  out->runs = runs.as<CamRun>();
+  out->first = first.as<uint32_t>();
+  out->nruns = uint32_t(t.runs.size() - 1);
+  out->npix = t.npix;
+  return SPRAY_RT_OK;
+}
+
+int prepare_camera(spray_rt_insitu* I, const CamFrame& F, int image_h, const float* light) {
+  spray_rt_ctx* c = I->ctx;
+  const int n = c->ndom;
+  std::vector<float> key(F.cam, F.cam + 14);
+  key.push_back(float(F.image_w));
+  key.push_back(float(image_h));
+  for (int k = 0; k < 3; ++k) key.push_back(light ? light[k] : NAN);
+  for (int d = 0; d < n; ++d)
+    key.push_back(size_t(d) < c->dom2slot.size() && c->dom2slot[size_t(d)] >= 0 ? 1.f : 0.f);
+  for (int k = 0; k < 6 * n; ++k) key.push_back(c->h_boxes[size_t(k)]);
+  if (key.size() == I->cam_key.size() &&
+      std::memcmp(key.data(), I->cam_key.data(), key.size() * sizeof(float)) == 0)
+    return SPRAY_RT_OK;
+  fp::Proj pj;
+  if (!fp::make_proj(F.cam, &pj)) return fail(c, SPRAY_RT_ERR_ARG, "degenerate camera");
+  float scene[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int d = 0; d < n; ++d)
+    for (int k = 0; k < 3; ++k) {
+      scene[k] = std::min(scene[k], c->h_boxes[6 * size_t(d) + k]);
+      scene[3 + k] = std::max(scene[3 + k], c->h_boxes[6 * size_t(d) + 3 + k]);
+    }
+  const size_t rows = static_cast<size_t>(image_h);
+  fp::Rows U(rows), E(rows), S(rows);
+  bool s_all = false;
+  for (int d = 0; d < n; ++d) {
+    const float* b = &c->h_boxes[6 * size_t(d)];
+    int rect[4];
+    if (fp::box_rect(pj, b, F.image_w, image_h, rect)) fp::add_rect(U, rect);
+    const bool own = size_t(d) < c->dom2slot.size() && c->dom2slot[size_t(d)] >= 0;
+    if (!own) continue;
+    if (fp::box_rect(pj, b, F.image_w, image_h, rect)) fp::add_rect(E, rect);
+    if (light) {
+      float reg[6];
+      if (fp::shadow_region(b, scene, light, reg))
+        s_all = true;
+      else if (fp::box_rect(pj, reg, F.image_w, image_h, rect))
+        fp::add_rect(S, rect);
+    }
+  }
+  fp::merge_rows(U);
+  fp::merge_rows(E);
+  fp::merge_rows(S);
+  try {
+    const fp::Table tu = fp::make_table(U, F.image_w, nullptr);
+    const fp::Table te = fp::make_table(E, F.image_w, &tu);
+    const fp::Table ts = fp::make_table(s_all ? U : fp::intersect_rows(S, U), F.image_w, &tu);
+    if (size_t(tu.npix) * size_t(F.spp) >= (size_t(1) << 31))
+      return fail(c, SPRAY_RT_ERR_LIMIT, "camera frame: |U| x spp >= 2^31");
+    CALL(upload_table(I, tu, I->tu_runs, I->tu_first, &I->tu));
+    CALL(upload_table(I, te, I->te_runs, I->te_first, &I->te));
+    CALL(upload_table(I, ts, I->ts_runs, I->ts_first, &I->ts));
+    I->tu_pixmax = tu.ymax_pix;
+  } catch (const std::exception& e) {
+    return fail(c, SPRAY_RT_ERR_STATE, "camera frame tables: %s", e.what());
+  }
+  I->cam_key.swap(key);
+  return SPRAY_RT_OK;
+}
+
+// The replicated PT frame from the camera: trace_replicated's steps with U
+// for C' and every device pass over this rank's own tables -- the keyed
+// closest hit + shading over E's eye rays (generated in the lanes), the
+// list positions, winners and film over E, the shadow any hit over S -- so
+// a rank's device work follows its domains' footprints, not the frame.  No
+// host read; collectives: t-bits MIN (own t bits -> group minimum), list
+// positions MIN (side stream), occlusion bytes + totals SUM, the per-U-pixel
+// film reduced to rank 0.  Phases as trace_replicated (0: the tables and
+// prefills).
+int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame& F, int image_h,
+                    float* image, const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  const int spp = F.spp;
+  const double scale = 1.0 / double(spp);
+  const spray_rt_light& lt = P->lights[0];
+  const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
+                             lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
+                             P->ks[2],       P->shininess};
+  MARK(0);
+  CALL(prepare_camera(I, F, image_h, lt.pos));
+  const size_t nu = size_t(I->tu.npix) * size_t(spp);  // U slots
+  const size_t npu = I->tu.npix;                       // U pixels
+  const bool split = split_keys() && c->ndom <= 255;
+  GROW(I->rkeys_c, nu * 8 + 8);
+  GROW(I->rtk, nu * 4 + 4);
+  GROW(I->ctmin, nu * 4 + 4);
+  GROW(I->rsw, nu * 16 + 16);
+  GROW(I->rsvalid, nu + 1);
+  GROW(I->rlp, nu + 1);
+  GROW(I->rocc, nu + 192);
+  GROW(I->rwin, nu + 1);
+  GROW(I->rsflag, nu + 1);
+  GROW(I->rnsh, kWinCounterBytes);
+  GROW(I->ccomp, npu * 12 + 12);
+  if (rec) GROW(I->rhit_c, nu * 48 + 48);
+  uint64_t* keys = I->rkeys_c.as<uint64_t>();
+  uint32_t* tk = I->rtk.as<uint32_t>();      // own t bits (0xFFFFFFFF: no own hit)
+  uint32_t* tmin = I->ctmin.as<uint32_t>();  // the group's minimum
+  HIPCHK(c, hipMemsetAsync(tk, 0xFF, nu * 4, s));
+  if (!split) HIPCHK(c, launch_fill_u64(s, keys, nu, kInsituMissKey));
+  if (rec) HIPCHK(c, hipMemsetAsync(I->rwin.p, 0, nu, s));
+  // ---- own keyed closest hits + shading over E (results at U slots)
+  MARK(2);
+  HIPCHK(c, launch_scene_cam_keyed(s, view(c), F, I->te, shade10,
+                                   rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
+                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>()));
+  // ---- the group's minimum t of every U slot (then the list position)
+  uint8_t* lp = nullptr;
+  uint64_t* kmin = nullptr;
+  if (split) {
+    if (nu) COMM(I->tr->allreduce_min_u32(I, tk, tmin, nu));
+    MARK(3);
+    lp = I->rlp.as<uint8_t>();
+    HIPCHK(c, hipMemsetAsync(lp, 0xFF, nu, s));
+    HIPCHK(c, launch_cam_lp(s, I->te, spp, keys, tk, tmin, lp));
+    if (nu) {
+      if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
+      if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
+      if (!I->ev_lp1) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp1, hipEventDisableTiming));
+      if (I->tr->side_stream()) {
+        HIPCHK(c, hipEventRecord(I->ev_lp0, s));
+        HIPCHK(c, hipStreamWaitEvent(I->cs, I->ev_lp0, 0));
+        CALL(I->tr->allreduce_min_u8(I, lp, nu, I->cs));
+      } else {
+        COMM(I->tr->allreduce_min_u8(I, lp, nu, s));
+      }
+      HIPCHK(c, hipEventRecord(I->ev_lp1, I->cs));
+    }
+  } else {
+    GROW(I->rkeys_n, nu * 8 + 8);
+    kmin = I->rkeys_n.as<uint64_t>();
+    HIPCHK(c, hipMemcpyAsync(kmin, keys, nu * 8, hipMemcpyDeviceToDevice, s));
+    if (nu) COMM(I->tr->allreduce_min_u64(I, kmin, nu));
+    MARK(3);
+    HIPCHK(c, launch_tmin_from_keys(s, kmin, nu, tmin));
+  }
+  // ---- the shadow ray of every hit in S from the minimum t, own any hit
+  MARK(4);
+  HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nu, s));
+  HIPCHK(c, launch_scene_cam_shadows(s, view(c), F, I->ts, tmin, shade10, I->rocc.as<uint8_t>()));
+  // ---- the winners among E's slots, their shadows counted
+  MARK(5);
+  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, kWinCounterBytes, s));
+  if (split && nu) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
+  HIPCHK(c, launch_cam_win(s, I->te, spp, keys, tk, tmin, lp, kmin, I->rsvalid.as<uint8_t>(),
+                           I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
+                           I->rnsh.as<unsigned long long>()));
+  const unsigned long long nrad = I->rank == 0 ? (unsigned long long)F.image_w *
+                                                     (unsigned long long)image_h *
+                                                     (unsigned long long)spp
+                                               : 0ull;
+  HIPCHK(c, launch_rep_totals(s, I->rocc.as<uint8_t>() + nu, nrad,
+                              I->rnsh.as<unsigned long long>()));
+  // ---- occlusion OR (a byte SUM) + totals
+  COMM(I->tr->allreduce_sum_u8(I, I->rocc.as<uint8_t>(), nu + 192));
+  // ---- film of the rank's winners into per-U-pixel sums, reduced to rank 0
+  MARK(6);
+  const size_t pay = (split ? 5 * nu : 8 * nu) + nu + 192 + 12 * npu;
+  I->st[0] += pay;
+  I->st[1] += pay;
+  if (npu) {
+    HIPCHK(c, hipMemsetAsync(I->ccomp.p, 0, npu * 12, s));
+    HIPCHK(c, launch_cam_film(s, I->te, spp, I->ccomp.as<float>(), I->rsw.as<float>(),
+                              I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>(), scale));
+    COMM(I->tr->reduce_f32(I, I->ccomp.as<float>(), npu * 3, 0));
+    if (I->rank == 0)
+      HIPCHK(c, launch_cam_expand(s, I->tu, F.image_w, I->ccomp.as<float>(), image));
+  }
+  if (rec)
+    HIPCHK(c, launch_cam_record(s, I->te, spp, F.image_w, I->rwin.as<uint8_t>(),
+                                I->rhit_c.as<spray_rt_hit>(), I->rsflag.as<uint8_t>(),
+                                I->rocc.as<uint8_t>(), *rec));
+  uint8_t* ht = reinterpret_cast<uint8_t*>(I->h_small + 128);  // 192 bytes
+  HIPCHK(c, hipMemcpyAsync(ht, I->rocc.as<uint8_t>() + nu, 192, hipMemcpyDeviceToHost, s));
+  MARK(6);
+  HIPCHK(c, hipStreamSynchronize(s));
+  flush_phases(I, 7);
+  unsigned long long tot[3] = {0, 0, 0};
+  for (int k = 0; k < 192; ++k) tot[k >> 6] += (unsigned long long)ht[k] << (k & 63);
+  if (totals)
+    for (int k = 0; k < 3; ++k) totals[k] = tot[k];
+  ++I->st[5];
+  return SPRAY_RT_OK;
+}
+
+// The replicated AO frame from the camera: U's eye rays, pixels and samples
+// generated into U-ordered arrays (one pass), then trace_replicated_ao over
+// C = U.
+int trace_camera_ao(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame& F, int image_h,
+                    float* image, const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+  spray_rt_ctx* c = I->ctx;
+  hipStream_t s = stream_of(c);
+  MARK(0);
+  CALL(prepare_camera(I, F, image_h, nullptr));
+  const size_t nu = size_t(I->tu.npix) * size_t(F.spp);
+  GROW(I->crays, nu * 32 + 32);
+  GROW(I->cpix, nu * 4 + 4);
+  GROW(I->csam, nu * 4 + 4);
+  if (I->ciota_n < nu) {
+    GROW(I->ciota, nu * 4 + 4);
+    HIPCHK(c, launch_iota_u32(s, I->ciota.as<uint32_t>(), nu));
+    I->ciota_n = nu;
+  }
+  HIPCHK(c, launch_cam_eye_rays(s, I->tu, F, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
+                                I->csam.as<int32_t>()));
+  const size_t n = size_t(F.image_w) * size_t(image_h) * size_t(F.spp);
+  return trace_replicated_ao(I, P, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
+                             I->csam.as<int32_t>(), n, F.spp, image, rec, totals,
+                             I->ciota.as<uint32_t>(), nu, I->tu_pixmax);
+}
+
 void free_all(spray_rt_insitu* I) {
   DBuf* all[] = {&I->hray[0], &I->hray[1], &I->hw[0], &I->hw[1], &I->hpix[0], &I->hpix[1],
                  &I->hsam[0], &I->hsam[1], &I->mask, &I->idx, &I->starts, &I->plan_tmp,
@@ -1214,7 +1468,9 @@ void free_all(spray_rt_insitu* I) {
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rincl, &I->rscan_tmp,
                  &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax,
-                 &I->aflag, &I->aown, &I->asel_tmp};
+                 &I->aflag, &I->aown, &I->asel_tmp, &I->tu_runs, &I->tu_first,
+                 &I->te_runs, &I->te_first, &I->ts_runs, &I->ts_first, &I->ctmin, &I->ccomp,
+                 &I->crays, &I->cpix, &I->csam, &I->ciota};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
@@ -1442,6 +1698,86 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t I, const spray_rt_shader* P,
   }
   I->tr->serial_end();
   return r;
+}
+
+int spray_rt_insitu_trace_camera(spray_rt_insitu_t I, const spray_rt_shader* P,
+                                 const float cam[14], int image_w, int image_h, int spp,
+                                 float* image, const spray_rt_insitu_rec* rec,
+                                 unsigned long long totals[3]) {
+  if (!I || !cam) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = I->ctx;
+  if (spray_rt_shadow_slots(P) < 0 || spp <= 0 || image_w <= 0 || image_h <= 0)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad shader or frame configuration");
+  if (float(image_w) != cam[12] || float(image_h) != cam[13])
+    return fail(c, SPRAY_RT_ERR_ARG, "the camera record is for a %gx%g image", cam[12], cam[13]);
+  if (rec && (!rec->d_count || !is_device_ptr(rec->d_count)))
+    return fail(c, SPRAY_RT_ERR_ARG, "records need a device counter");
+  const size_t n = size_t(image_w) * size_t(image_h) * size_t(spp);
+  if (n > 0x7FFFFFFFull) return fail(c, SPRAY_RT_ERR_LIMIT, "frame > 2^31 samples");
+  if (!image || !is_device_ptr(image)) return fail(c, SPRAY_RT_ERR_ARG, "needs a device image");
+  int r = scene_common(c, image, 1, image);
+  if (r) return r;
+  if (!c->d_owner) return fail(c, SPRAY_RT_ERR_STATE, "no owner map set");
+  const bool ao = P->shader == SPRAY_RT_SHADER_AO && P->bounces == 1 && !c->bsdf_delta &&
+                  P->samples >= 1 && P->samples <= 32;
+  if (!fused_pt_shading(c, P) && !ao)
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
+                "replicated frames need one bounce, diffuse surfaces and one point light "
+                "(PT) or <= 32 samples (AO)");
+  if (!I->tr->has_rep())
+    return fail(c, SPRAY_RT_ERR_UNSUPPORTED,
+                "the host transport gives no allreduce_min_u64 / allreduce_sum_u8");
+  CamFrame F{};
+  for (int k = 0; k < 14; ++k) F.cam[k] = cam[k];
+  F.image_w = image_w;
+  F.spp = spp;
+  const char* fr = std::getenv("SPRAY_INSITU_REPLICATED");
+  const bool force_rep = fr && fr[0] == '1';
+  I->nev = 0;
+  I->tr->serial_begin();
+  if (I->world == 1 && !force_rep) {
+    // one rank: the whole frame's eye rays, then the all-local fused frame
+    hipStream_t s = stream_of(c);
+    r = grow(I, I->crays, n * 32 + 32);
+    if (!r) r = grow(I, I->cpix, n * 4 + 4);
+    if (!r) r = grow(I, I->csam, n * 4 + 4);
+    if (!r && launch_eye_rays_insitu(s, cam, image_w, spp, 0, 0, image_w, 0, 0, image_w, image_h,
+                                     I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
+                                     I->csam.as<int32_t>()) != hipSuccess)
+      r = fail(c, SPRAY_RT_ERR_HIP, "eye rays");
+    if (!r)
+      r = trace_local(I, P, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
+                      I->csam.as<int32_t>(), n, spp, image, rec, totals);
+    flush_phases(I, 1);
+  } else {
+    r = ao ? trace_camera_ao(I, P, F, image_h, image, rec, totals)
+           : trace_camera_pt(I, P, F, image_h, image, rec, totals);
+  }
+  I->tr->serial_end();
+  return r;
+}
+
+int spray_rt_insitu_partition_view(const float* boxes, int n, const float cam[14], int nranks,
+                                   int* owner) {
+  if (!boxes || !cam || !owner || n < 0 || nranks <= 0) return SPRAY_RT_ERR_ARG;
+  fp::Proj pj;
+  if (!fp::make_proj(cam, &pj)) return SPRAY_RT_ERR_ARG;
+  fp::partition_view(boxes, n, pj, nranks, owner);
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_camera_box_rect(const float cam[14], int image_w, int image_h, const float box[6],
+                             int rect[4]) {
+  if (!cam || !box || !rect || image_w <= 0 || image_h <= 0) return -1;
+  fp::Proj pj;
+  if (!fp::make_proj(cam, &pj)) return -1;
+  return fp::box_rect(pj, box, image_w, image_h, rect);
+}
+
+int spray_rt_camera_shadow_region(const float box[6], const float scene[6], const float light[3],
+                                  float out[6]) {
+  if (!box || !scene || !light || !out) return -1;
+  return fp::shadow_region(box, scene, light, out);
 }
 
 int spray_rt_insitu_set_timing(spray_rt_insitu_t I, int on) {

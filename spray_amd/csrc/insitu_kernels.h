@@ -84,6 +84,28 @@ constexpr size_t kWinCounterBytes = size_t(kWinCounters) * kWinStride * 8;
 hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* tmin,
                           const uint8_t* lpmin, const uint64_t* kmin, const uint8_t* sv, size_t nc,
                           uint8_t* win, uint8_t* svw, unsigned long long* nshadow);
+// ---- replicated PT frames from the camera (trace_camera): passes over the
+// rank's eye table T, the shared arrays addressed by U slot (rt_kernels.h)
+// lp[u] = own list position where own t bits tk[u] == tmin[u] (lp prefilled 0xFF)
+hipError_t launch_cam_lp(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
+                        const uint32_t* tk, const uint32_t* tmin, uint8_t* lp);
+// win / svw at u as launch_rep_win (own t bits tk: 0xFFFFFFFF = no own hit)
+hipError_t launch_cam_win(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
+                         const uint32_t* tk, const uint32_t* tmin, const uint8_t* lpmin,
+                         const uint64_t* kmin, const uint8_t* sv, uint8_t* win, uint8_t* svw,
+                         unsigned long long* nshadow);
+// compact[3 q ..] += scale * sw of the unoccluded winners' shadows, q = u / spp
+hipError_t launch_cam_film(hipStream_t s, const CamTable& T, int spp, float* compact,
+                          const float* sw, const uint8_t* svw, const uint8_t* occ, double scale);
+// image pixel of U pixel q += compact[3 q ..] (U: the frame's U table)
+hipError_t launch_cam_expand(hipStream_t s, const CamTable& U, int image_w, const float* compact,
+                            float* image);
+hipError_t launch_cam_record(hipStream_t s, const CamTable& T, int spp, int image_w,
+                            const uint8_t* win, const spray_rt_hit* hits, const uint8_t* svw,
+                            const uint8_t* occ, const spray_rt_insitu_rec& rec);
+// eye rays, pixel and sample ids of table T's work items at their U slots
+hipError_t launch_cam_eye_rays(hipStream_t s, const CamTable& T, const CamFrame& F,
+                              spray_rt_ray* rays, int32_t* pixid, int32_t* samid);
 // tmin[j] = t bits of kmin[j] (0xFFFFFFFF: a miss)
 hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc, uint32_t* tmin);
 // *out = max(pix[0..n)) (bmax: grid_for(n) u32 of scratch)

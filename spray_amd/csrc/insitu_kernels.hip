@@ -11,6 +11,7 @@
 
 #include <algorithm>
 
+#include "cam_device.h"
 #include "insitu_kernels.h"
 #include "rt_device.h"
 #include "shade_device.h"
@@ -573,6 +574,148 @@ __global__ __launch_bounds__(kBlock) void k_rep_win(const uint64_t* __restrict__
   win_count(__popcll(b), nshadow);
 }
 
+// ---- replicated PT frames from the camera (insitu.cpp, trace_camera) ----
+// Every pass runs over the rank's own eye-ray table T (its domains' screen
+// footprints; a winner is always among them) and addresses the frame's
+// shared arrays by U slot (cam_item).  The arrays over U start prefilled
+// (memsets: t bits 0xFFFFFFFF = no hit, list positions 0xFF, occlusion 0).
+// lp[u] = this rank's list position of its hit where its t is the group's
+// minimum
+__global__ __launch_bounds__(kBlock) void k_cam_lp(CamTable T, int spp,
+                                                   const uint64_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ tk,
+                                                   const uint32_t* __restrict__ tmin,
+                                                   uint8_t* __restrict__ lp) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= size_t(T.npix) * uint32_t(spp)) return;
+  int x, y, s;
+  size_t u;
+  cam_item(T, spp, j, x, y, s, u);
+  const uint32_t t = tk[u];
+  if (t != 0xFFFFFFFFu && t == tmin[u]) lp[u] = uint8_t((keys[u] >> 16) & 0xFFu);
+}
+
+// the winners among the rank's slots (as k_rep_win): win / svw at u
+__global__ __launch_bounds__(kBlock) void k_cam_win(CamTable T, int spp,
+                                                    const uint64_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ tk,
+                                                    const uint32_t* __restrict__ tmin,
+                                                    const uint8_t* __restrict__ lpmin,
+                                                    const uint64_t* __restrict__ kmin,
+                                                    const uint8_t* __restrict__ sv,
+                                                    uint8_t* __restrict__ win,
+                                                    uint8_t* __restrict__ svw,
+                                                    unsigned long long* __restrict__ nshadow) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  bool w = false, sw = false;
+  if (j < size_t(T.npix) * uint32_t(spp)) {
+    int x, y, s;
+    size_t u;
+    cam_item(T, spp, j, x, y, s, u);
+    const uint32_t t = tk[u];
+    if (t != 0xFFFFFFFFu) {
+      const uint64_t key = keys[u];
+      w = lpmin ? (t == tmin[u] && uint8_t((key >> 16) & 0xFFu) == lpmin[u]) : key == kmin[u];
+    }
+    sw = w && sv[u];
+    win[u] = w;
+    svw[u] = sw;
+  }
+  win_count(__popcll(__ballot(sw)), nshadow);
+}
+
+// the rank's winners' unoccluded shadows into per-U-pixel sums (compact,
+// 3 floats per pixel of U; a pixel's spp slots are neighbours, film_runs)
+__global__ __launch_bounds__(kBlock) void k_cam_film(CamTable T, int spp,
+                                                     float* __restrict__ compact,
+                                                     const float4* __restrict__ sw,
+                                                     const uint8_t* __restrict__ svw,
+                                                     const uint8_t* __restrict__ occ,
+                                                     double scale) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool in = j < size_t(T.npix) * uint32_t(spp);
+  int32_t q = -1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  bool any = false;
+  if (in) {
+    int x, y, s;
+    size_t u;
+    cam_item(T, spp, j, x, y, s, u);
+    q = int32_t(u / uint32_t(spp));
+    if (svw[u] && !occ[u]) {
+      const float4 L = sw[u];
+      a0 = float(scale * double(L.x));
+      a1 = float(scale * double(L.y));
+      a2 = float(scale * double(L.z));
+      any = true;
+    }
+  }
+  film_runs(compact, in, q, any, a0, a1, a2, 3);
+}
+
+// rank 0: the group's per-U-pixel sums into the image (U's own table: U
+// pixel q = work item q at one sample per pixel)
+__global__ __launch_bounds__(kBlock) void k_cam_expand(CamTable U, int image_w,
+                                                       const float* __restrict__ compact,
+                                                       float* __restrict__ image) {
+  const size_t q = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (q >= U.npix) return;
+  int x, y, s;
+  size_t u;
+  cam_item(U, 1, q, x, y, s, u);
+  float* px = image + 4 * (size_t(y) * size_t(image_w) + size_t(x));
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float v = compact[3 * q + k];
+    if (v != 0.0f) px[k] += v;
+  }
+}
+
+// per-sample records of the rank's winners (tests): samid of the blocking
+// tile = the frame, (W y + x) spp + s (k_eye_rays_insitu)
+__global__ __launch_bounds__(kBlock) void k_cam_record(CamTable T, int spp, int image_w,
+                                                       const uint8_t* __restrict__ win,
+                                                       const spray_rt_hit* __restrict__ hits,
+                                                       const uint8_t* __restrict__ svw,
+                                                       const uint8_t* __restrict__ occ,
+                                                       spray_rt_insitu_rec rec) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= size_t(T.npix) * uint32_t(spp)) return;
+  int x, y, s;
+  size_t u;
+  cam_item(T, spp, j, x, y, s, u);
+  if (!win[u]) return;
+  const uint32_t k = atomicAdd(rec.d_count, 1u);
+  if (k >= rec.cap) return;
+  const int32_t pix = image_w * y + x;
+  rec.samid[k] = spp > 1 ? pix * spp + s : pix;
+  rec.bounce[k] = 0;
+  rec.hits[k] = hits[u];
+  rec.svalid[k] = svw[u] ? 1ull : 0ull;
+  rec.occluded[k] = (svw[u] && occ[u]) ? 1ull : 0ull;
+}
+
+// the eye rays of table T at their U slots (the replicated AO frame's
+// inputs): k_eye_rays_insitu's operations, pixid, samid
+__global__ __launch_bounds__(kBlock) void k_cam_eye_rays(CamTable T, Cam cam, int image_w, int spp,
+                                                         float4* __restrict__ rays,
+                                                         int32_t* __restrict__ pixid,
+                                                         int32_t* __restrict__ samid) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= size_t(T.npix) * uint32_t(spp)) return;
+  int x, y, s;
+  size_t u;
+  cam_item(T, spp, j, x, y, s, u);
+  float fx, fy, d[3];
+  insitu_jitter(image_w, spp, x, y, s, fx, fy);
+  cam_dir(cam, fx, fy, d);
+  rays[2 * u] = make_float4(cam.p[0], cam.p[1], cam.p[2], kRayEpsilon);
+  rays[2 * u + 1] = make_float4(d[0], d[1], d[2], kInf);
+  const int32_t pix = image_w * y + x;
+  pixid[u] = pix;
+  samid[u] = spp > 1 ? pix * spp + s : pix;
+}
+
 // 64-bit keys: the minimum t bits for the shadow rays
 __global__ __launch_bounds__(kBlock) void k_tmin_from_keys(const uint64_t* __restrict__ kmin,
                                                            size_t nc, uint32_t* __restrict__ tmin) {
@@ -713,6 +856,38 @@ hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* t
                           const uint8_t* lpmin, const uint64_t* kmin, const uint8_t* sv, size_t nc,
                           uint8_t* win, uint8_t* svw, unsigned long long* nshadow) {
   LAUNCH(nc, k_rep_win, keys, tmin, lpmin, kmin, sv, nc, win, svw, nshadow);
+}
+hipError_t launch_cam_lp(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
+                        const uint32_t* tk, const uint32_t* tmin, uint8_t* lp) {
+  LAUNCH(size_t(T.npix) * uint32_t(spp), k_cam_lp, T, spp, keys, tk, tmin, lp);
+}
+hipError_t launch_cam_win(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
+                         const uint32_t* tk, const uint32_t* tmin, const uint8_t* lpmin,
+                         const uint64_t* kmin, const uint8_t* sv, uint8_t* win, uint8_t* svw,
+                         unsigned long long* nshadow) {
+  LAUNCH(size_t(T.npix) * uint32_t(spp), k_cam_win, T, spp, keys, tk, tmin, lpmin, kmin, sv, win,
+         svw, nshadow);
+}
+hipError_t launch_cam_film(hipStream_t s, const CamTable& T, int spp, float* compact,
+                          const float* sw, const uint8_t* svw, const uint8_t* occ, double scale) {
+  LAUNCH(size_t(T.npix) * uint32_t(spp), k_cam_film, T, spp, compact,
+         reinterpret_cast<const float4*>(sw), svw, occ, scale);
+}
+hipError_t launch_cam_expand(hipStream_t s, const CamTable& U, int image_w, const float* compact,
+                            float* image) {
+  LAUNCH(size_t(U.npix), k_cam_expand, U, image_w, compact, image);
+}
+hipError_t launch_cam_record(hipStream_t s, const CamTable& T, int spp, int image_w,
+                            const uint8_t* win, const spray_rt_hit* hits, const uint8_t* svw,
+                            const uint8_t* occ, const spray_rt_insitu_rec& rec) {
+  LAUNCH(size_t(T.npix) * uint32_t(spp), k_cam_record, T, spp, image_w, win, hits, svw, occ, rec);
+}
+hipError_t launch_cam_eye_rays(hipStream_t s, const CamTable& T, const CamFrame& F,
+                              spray_rt_ray* rays, int32_t* pixid, int32_t* samid) {
+  Cam cam;
+  for (int k = 0; k < 14; ++k) cam.p[k] = F.cam[k];
+  LAUNCH(size_t(T.npix) * uint32_t(F.spp), k_cam_eye_rays, T, cam, F.image_w, F.spp,
+         reinterpret_cast<float4*>(rays), pixid, samid);
 }
 hipError_t launch_tmin_from_keys(hipStream_t s, const uint64_t* kmin, size_t nc, uint32_t* tmin) {
   LAUNCH(nc, k_tmin_from_keys, kmin, nc, tmin);

@@ -187,6 +187,42 @@ hipError_t launch_scene_rep_keyed(hipStream_t s, const SceneView& v, const spray
 hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                     size_t n, const uint32_t* idx, size_t nc,
                                     const uint32_t* tmin, const float* shade10, uint8_t* occ);
+// out[j] = j, j < n
+hipError_t launch_iota_u32(hipStream_t s, uint32_t* out, size_t n);
+// ---- replicated frames from the camera (insitu.cpp, trace_camera) ----
+// A set of the frame's pixels as row runs: pixels x0 .. x0 + len - 1 of row
+// y, len = the next run's pbase - pbase (pbase: pixels of the table before
+// the run); ubase: the U-space index of pixel (x0, y) (U = the pixels whose
+// eye rays may enter a domain box: the union of every box's screen
+// footprint, the index space every rank's replicated arrays share).  Work
+// item j of a table = sample j % spp of its pixel j / spp; its slot in U =
+// (ubase + x - x0) * spp + s.  first[g] = the run holding pixel 8 g of the
+// table (one load and a short forward scan per lane instead of a search).
+struct CamRun {
+  int32_t y, x0;
+  uint32_t pbase, ubase;
+};
+struct CamTable {
+  const CamRun* runs;  // [nruns + 1]: a sentinel run with pbase = npix
+  const uint32_t* first;
+  uint32_t nruns, npix;
+};
+struct CamFrame {
+  float cam[14];  // camera_init's record (eye, image-plane corner, u / v axes, w, h)
+  int image_w, spp;
+};
+// keyed closest hit + point-light shading of the eye rays of table T's
+// pixels, generated in the lanes (k_eye_rays_insitu's operations), culled by
+// the resident boxes; results at their U slots (slots of dropped lanes
+// untouched)
+hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFrame& F,
+                                  const CamTable& T, const float* shade10, spray_rt_hit* hits,
+                                  uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv);
+// any hit of the point-light shadow ray of every hit in T's pixels (t bits
+// tmin[u]; none: 0xFFFFFFFF), the eye ray regenerated in the lane
+hipError_t launch_scene_cam_shadows(hipStream_t s, const SceneView& v, const CamFrame& F,
+                                    const CamTable& T, const uint32_t* tmin,
+                                    const float* shade10, uint8_t* occ);
 // any hit of those pairs' AO rays, each generated in its any-hit lane;
 // idx (optional): only pairs idx[0..*d_count) (occ written at idx[j])
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,

@@ -16,6 +16,7 @@
 #include <climits>
 #include <cstdint>
 
+#include "cam_device.h"
 #include "rt_device.h"
 #include "shade_device.h"
 
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_domains(
   counts[i] = n;
 }
 
+
 // ---------------------------------------------------------------------------
 // fused scene path
 // ---------------------------------------------------------------------------
@@ -265,6 +267,12 @@ struct SceneArgs {
   uint32_t* tkeys;
   const uint32_t* tmin;
   size_t nrays;  // index lists: ray ids idx[j] < nrays (0: < M)
+  // replicated frames from the camera (cam_runs != null): work item j is
+  // sample j of table cam's pixels, generated in the lane, results at its
+  // U slot (cam_item)
+  CamTable cam_tab;
+  Cam cam;
+  int cam_w, cam_spp;
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -869,26 +877,57 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
 // bits and "no shading" here (every slot of C' is written by its lane, no
 // prefill); kEpiShadowGen leaves its occlusion byte at the prefilled 0.
 template <int EPI>
-__device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, bool ok,
-                                        float* r6, const float* sbox, const uint8_t* sres,
-                                        int nres) {
-  if (!ok) return false;
-  const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
-  const float4 o4 = rp[0], d4 = rp[1];
-  if (EPI == kEpiKeysShade) {
-    r6[0] = o4.x;
-    r6[1] = o4.y;
-    r6[2] = o4.z;
-    r6[3] = d4.x;
-    r6[4] = d4.y;
-    r6[5] = d4.z;
+__device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, bool ok, bool inb,
+                                        size_t& at, float* r6, const float* sbox,
+                                        const uint8_t* sres, int nres) {
+  const bool cam = A.cam_tab.runs != nullptr;
+  at = j;
+  // a dropped slot of C' gets the miss results (every slot of C' is written
+  // by its lane, no prefill); camera slots are prefilled (the memset of U)
+  const auto miss = [&]() {
+    if (EPI == kEpiKeysShade && !cam && inb) {
+      A.keys[j] = 0x7FFFFFFFFFFFFFFFull;  // the epilogue's miss key (kInsituMissKey)
+      A.tkeys[j] = 0xFFFFFFFFu;
+      if (A.sh_valid) A.sh_valid[j] = 0;
+    }
+    return false;
+  };
+  float o[3], d[3];
+  if (cam) {
+    if (!inb) return false;
+    int x, y, s;
+    cam_item(A.cam_tab, A.cam_spp, j, x, y, s, at);
+    float fx, fy;
+    insitu_jitter(A.cam_w, A.cam_spp, x, y, s, fx, fy);
+    cam_dir(A.cam, fx, fy, d);
+    o[0] = A.cam.p[0];
+    o[1] = A.cam.p[1];
+    o[2] = A.cam.p[2];
   } else {
-    const uint32_t tb = A.tmin[j];
+    if (!ok) return miss();
+    const float4* rp = reinterpret_cast<const float4*>(A.rays + i);
+    const float4 o4 = rp[0], d4 = rp[1];
+    o[0] = o4.x;
+    o[1] = o4.y;
+    o[2] = o4.z;
+    d[0] = d4.x;
+    d[1] = d4.y;
+    d[2] = d4.z;
+  }
+  if (EPI == kEpiKeysShade) {
+    r6[0] = o[0];
+    r6[1] = o[1];
+    r6[2] = o[2];
+    r6[3] = d[0];
+    r6[4] = d[1];
+    r6[5] = d[2];
+  } else {
+    const uint32_t tb = A.tmin[at];
     if (tb == 0xFFFFFFFFu) return false;
     const float t = __uint_as_float(tb);
-    r6[0] = d4.x * t + o4.x;
-    r6[1] = d4.y * t + o4.y;
-    r6[2] = d4.z * t + o4.z;
+    r6[0] = d[0] * t + o[0];
+    r6[1] = d[1] * t + o[1];
+    r6[2] = d[2] * t + o[2];
     float w[3] = {A.shade.lp[0] - r6[0], A.shade.lp[1] - r6[1], A.shade.lp[2] - r6[2]};
     gnorm3(w);
     r6[3] = w[0];
@@ -900,12 +939,7 @@ __device__ __forceinline__ bool rep_ray(const SceneArgs& A, size_t j, size_t i, 
     float tm;
     if (aabb_ref(sbox + 6 * int(sres[k]), dr, tm)) return true;
   }
-  if (EPI == kEpiKeysShade) {  // the dropped lane's results: a miss, no shading
-    A.keys[j] = 0x7FFFFFFFFFFFFFFFull;  // the epilogue's miss key (kInsituMissKey)
-    A.tkeys[j] = 0xFFFFFFFFu;
-    if (A.sh_valid) A.sh_valid[j] = 0;
-  }
-  return false;
+  return miss();
 }
 
 // When a wave takes its next chunk: packet kernels during the walk of the
@@ -1105,9 +1139,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     const bool ok = j < M && i < (A.nrays ? A.nrays : A.M) && (!A.valid || A.valid[i]);
     if constexpr (rep_epi(EPI)) {
       float r6[6];
-      const bool okr = rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres);
+      size_t at;
+      const bool okr = rep_ray<EPI>(A, j, i, ok, j < M, at, r6, sbox, sres, nres);
       scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
-          A, j, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
+          A, at, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (ok)
@@ -1153,9 +1188,11 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
             // no chunk waits in a wave's hands while another is traced
             const bool last = c + 64 >= csz;
             float r6[6];
-            const bool okr = rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, r6, sbox, sres, nres) : ok;
+            size_t at = i;
+            const bool okr =
+                rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, j < end, at, r6, sbox, sres, nres) : ok;
             scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
-                A, rep_epi(EPI) ? j : i, okr, stl, sbox, sdom, wstk, flag, pos, wi,
+                A, at, okr, stl, sbox, sdom, wstk, flag, pos, wi,
                 rep_epi(EPI) ? r6 : nullptr,
                 [&]() {
                   if (last && lane == 0) next = atomicAdd(head, csz);
@@ -1241,9 +1278,6 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
 // ---------------------------------------------------------------------------
 // ray sources
 // ---------------------------------------------------------------------------
-struct Cam {
-  float p[14];
-};
 
 // ooc::Tracer::genMultiEyes (src/ooc/ooc_tracer.inl:124-172) + Camera::
 // generateRay (camera.h:168-209), glm operand order: ray `bufid` of tile
@@ -1327,24 +1361,14 @@ __global__ __launch_bounds__(kBlock) void k_eye_rays_insitu(
   const int p = int(bufid / spp);
   const int x = tx + p % tw, y = ty + p / tw;
   const int pid = image_w * y + x;
-  float fx = float(x), fy = float(y);
-  if (spp > 1) {
-    uint32_t st = mm_fin(mm_mix(mm_mix(0u, uint32_t(pid)), uint32_t(s)));
-    fx = float(x) + sampler_1d(st);
-    fy = float(y) + sampler_1d(st);
-  }
+  float fx, fy;
+  insitu_jitter(image_w, spp, x, y, s, fx, fy);
+  float d[3];
+  cam_dir(cam, fx, fy, d);
   const float* c = cam.p;
-  const float u = fx / c[12], v = fy / c[13];
-  float dx = ((c[3] + c[6] * u) + c[9] * v) - c[0];
-  float dy = ((c[4] + c[7] * u) + c[10] * v) - c[1];
-  float dz = ((c[5] + c[8] * u) + c[11] * v) - c[2];
-  const float inv = 1.0f / sqrtf((dx * dx + dy * dy) + dz * dz);
-  dx = dx * inv;
-  dy = dy * inv;
-  dz = dz * inv;
   float4* rp = reinterpret_cast<float4*>(rays + bufid);
   rp[0] = make_float4(c[0], c[1], c[2], kRayEpsilon);
-  rp[1] = make_float4(dx, dy, dz, kInf);
+  rp[1] = make_float4(d[0], d[1], d[2], kInf);
   if (pixid) pixid[bufid] = pid;
   if (samid)
     samid[bufid] = spp > 1 ? (bw * (y - by) + (x - bx)) * spp + s : bw * (y - by) + (x - bx);
@@ -2415,6 +2439,46 @@ hipError_t launch_scene_rep_shadows(hipStream_t s, const SceneView& v, const spr
   SceneArgs a = scene_args(v, rays, nc);
   a.nrays = n;
   a.idx = idx;
+  a.tmin = tmin;
+  a.occ = occ;
+  a.shade = shade_from10(shade10);
+  return launch_scene_w<true, kEpiShadowGen>(s, a, v);
+}
+
+hipError_t launch_iota_u32(hipStream_t s, uint32_t* out, size_t n) {
+  if (n == 0) return hipSuccess;
+  k_iota<<<grid_for(n), kBlock, 0, s>>>(out, uint32_t(n));
+  return hipGetLastError();
+}
+
+static SceneArgs cam_args(const SceneView& v, const CamFrame& F, const CamTable& T) {
+  SceneArgs a = scene_args(v, nullptr, size_t(T.npix) * size_t(F.spp));
+  a.cam_tab = T;
+  for (int k = 0; k < 14; ++k) a.cam.p[k] = F.cam[k];
+  a.cam_w = F.image_w;
+  a.cam_spp = F.spp;
+  return a;
+}
+
+hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFrame& F,
+                                  const CamTable& T, const float* shade10, spray_rt_hit* hits,
+                                  uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv) {
+  if (T.npix == 0) return hipSuccess;
+  SceneArgs a = cam_args(v, F, T);
+  a.hits = hits;
+  a.keys = keys;
+  a.tkeys = tkeys;
+  a.sw = reinterpret_cast<float4*>(sw);
+  a.sh_valid = sv;
+  a.shade = shade_from10(shade10);
+  return launch_scene_w<false, kEpiKeysShade>(s, a, v);
+}
+
+hipError_t launch_scene_cam_shadows(hipStream_t s, const SceneView& v, const CamFrame& F,
+                                    const CamTable& T, const uint32_t* tmin,
+                                    const float* shade10, uint8_t* occ) {
+  if (T.npix == 0) return hipSuccess;
+  SceneArgs a = cam_args(v, F, T);
   a.tmin = tmin;
   a.occ = occ;
   a.shade = shade_from10(shade10);

@@ -29,14 +29,63 @@ import numpy as np
 
 from ._native import SHADER_AO, SprayRtError, lib
 
-__all__ = ["morton_partition", "PARTITION_GROUP_CLOSE", "PARTITION_ROUND_ROBIN", "horizontal_stripe", "setup_rank_context", "InsituEngine",
-           "InsituRecords", "MISS_KEY"]
+__all__ = ["morton_partition", "view_partition", "partition", "PARTITION_GROUP_CLOSE",
+           "PARTITION_ROUND_ROBIN", "PARTITION_VIEW", "horizontal_stripe", "setup_rank_context",
+           "InsituEngine", "InsituRecords", "MISS_KEY", "box_rect", "shadow_region"]
 
 MISS_KEY = 0x7FFFFFFFFFFFFFFF
 
 
 PARTITION_GROUP_CLOSE = 0
 PARTITION_ROUND_ROBIN = 1
+PARTITION_VIEW = 2  # spray_rt_insitu_partition_view (needs the camera)
+
+
+def view_partition(boxes, cam, nranks):
+    """Owner rank per domain, view-aligned (spray_rt_insitu_partition_view):
+    the box centres projected by camera record `cam` (camera_init, 14
+    floats), dealt by recursive median splits into groups of equal count."""
+    b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+    c = np.ascontiguousarray(cam, np.float32).reshape(14)
+    if nranks <= 0:
+        raise ValueError("nranks must be > 0")
+    owner = np.zeros(len(b), np.int32)
+    rc = lib().spray_rt_insitu_partition_view(b.ctypes.data, len(b), c.ctypes.data, int(nranks),
+                                              owner.ctypes.data)
+    if rc:
+        raise RuntimeError("spray_rt_insitu_partition_view failed (%d)" % rc)
+    return owner
+
+
+def partition(boxes, scene_bound, nranks, mode, cam=None):
+    """morton_partition (GROUP_CLOSE / ROUND_ROBIN) or view_partition (VIEW)"""
+    if mode == PARTITION_VIEW:
+        return view_partition(boxes, cam, nranks)
+    return morton_partition(boxes, scene_bound, nranks, mode)
+
+
+def box_rect(cam, image_w, image_h, box):
+    """(kind, [x0, x1, y0, y1]) of spray_rt_camera_box_rect: kind 0 = no eye
+    ray enters the box, 1 = the rectangle, 2 = the whole image"""
+    c = np.ascontiguousarray(cam, np.float32).reshape(14)
+    b = np.ascontiguousarray(box, np.float32).reshape(6)
+    r = np.zeros(4, np.int32)
+    k = lib().spray_rt_camera_box_rect(c.ctypes.data, int(image_w), int(image_h), b.ctypes.data,
+                                       r.ctypes.data)
+    if k < 0:
+        raise ValueError("bad camera or box")
+    return k, r
+
+
+def shadow_region(box, scene, light):
+    """(kind, box6) of spray_rt_camera_shadow_region: kind 0 = the region's
+    box, 1 = everywhere"""
+    out = np.zeros(6, np.float32)
+    k = lib().spray_rt_camera_shadow_region(
+        np.ascontiguousarray(box, np.float32).ctypes.data,
+        np.ascontiguousarray(scene, np.float32).ctypes.data,
+        np.ascontiguousarray(light, np.float32).ctypes.data, out.ctypes.data)
+    return k, out
 
 
 def morton_partition(boxes, scene_bound, nranks, mode=PARTITION_GROUP_CLOSE):
@@ -301,14 +350,33 @@ class InsituEngine:
         self._rep_kind = "ao" if shader.shader == SHADER_AO else "pt"
         return int(tot[0]), int(tot[1])
 
+    def trace_camera(self, shader, cam, image_w, image_h, spp, image, records=None):
+        """The whole frame of camera record `cam` (spray_rt_insitu_trace_camera):
+        the eye rays generated in the lanes, each rank's work bounded by its
+        domains' screen footprints.  Returns the group's (radiance rays,
+        shadow rays)."""
+        from .engine import _addr
+        c = np.ascontiguousarray(cam, np.float32).reshape(14)
+        im, k4 = _addr(image)
+        tot = (C.c_ulonglong * 3)()
+        rec = C.byref(records.struct) if records is not None else None
+        rc = lib().spray_rt_insitu_trace_camera(self.h, C.byref(shader), c.ctypes.data,
+                                                int(image_w), int(image_h), int(spp), im, rec,
+                                                C.byref(tot))
+        self.rt._check(rc, "insitu_trace_camera")
+        self._rep_kind = "ao" if shader.shader == SHADER_AO else "pt"
+        return int(tot[0]), int(tot[1])
+
     def set_timing(self, on=True):
         """Per-phase HIP-event timing of the traces (phase_times)."""
         self.rt._check(lib().spray_rt_insitu_set_timing(self.h, 1 if on else 0), "set_timing")
 
     # replicated-ray frames (insitu.cpp trace_replicated / trace_replicated_ao)
-    REP_PHASES = ("cull_select", "film_slots", "keyed_shade", "list_pos", "shadow_trace",
+    # phase 0: C' (trace_frame) or the footprint tables and prefills
+    # (trace_camera; its film needs no slots)
+    REP_PHASES = ("prepare", "film_slots", "keyed_shade", "list_pos", "shadow_trace",
                   "winners", "film_totals")
-    REP_AO_PHASES = ("cull_select", "unused", "keyed_closest_hit", "publish", "ao_spawn",
+    REP_AO_PHASES = ("prepare", "unused", "keyed_closest_hit", "publish", "ao_spawn",
                      "ao_own_trace", "film_totals")
     _rep_kind = "pt"
     PROTOCOL_PHASES = ("route_plan", "ray_pack_unpack", "keyed_closest_hit", "key_composite",

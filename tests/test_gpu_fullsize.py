@@ -271,9 +271,10 @@ def test_insitu_full_frame_rccl_one_rank(spray, oracle):
 
 
 def _rep_rank_main(rank, world, port, out, mode, kind="pt"):
-    """One rank of the full-size replicated-ray frame (8 processes sharing the
-    GPU, gloo + the engine's host transport; kind "pt" or "ao" = AO-16):
-    records to out/r<rank>.npz."""
+    """One rank of the full-size camera frame (spray_rt_insitu_trace_camera,
+    bench.py's N > 1 form; 8 processes sharing the GPU, gloo + the engine's
+    host transport; kind "pt" or "ao" = AO-16; mode: the partition, 2 =
+    view-aligned): records to out/r<rank>.npz."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -287,24 +288,19 @@ def _rep_rank_main(rank, world, port, out, mode, kind="pt"):
     try:
         boxes, lights = host_parse_scene(WAVELETS64, SCENES)
         bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
-        owner = insitu.morton_partition(boxes, bound, world, mode)
+        c = BENCH_CAMERA
+        cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], W, H)
+        owner = insitu.partition(boxes, bound, world, mode, cam)
         rt = spray_amd.RtContext(0)
         insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
         rt.set_bsdfs(host_scene_bsdfs(WAVELETS64))
         rt.set_stream(torch.cuda.current_stream())
         eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport="host")
-        c = BENCH_CAMERA
-        cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], W, H)
-        rays = torch.empty((N, 8), dtype=torch.float32, device="cuda")
-        pix = torch.empty(N, dtype=torch.int32, device="cuda")
-        sam = torch.empty(N, dtype=torch.int32, device="cuda")
-        rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), (0, 0, W, H), rays, pix, sam)
         sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1, ks=SHADE[6:9],
                                          shininess=SHADE[9], lights=lights)
         image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
         recs = insitu.InsituRecords(N // 2)
-        tot = eng.trace_frame(sh, rays, pix, sam, SPP, image, recs)
-        eng.composite(image)
+        tot = eng.trace_camera(sh, cam, W, H, SPP, image, recs)
         torch.cuda.synchronize()
         g = recs.numpy()
         np.savez(os.path.join(out, "r%d.npz" % rank), samid=g["samid"], bounce=g["bounce"],
@@ -344,14 +340,14 @@ def _check_replicated(parts, ref):
     np.testing.assert_allclose(parts[0]["image"], ref["image"], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 2])
 def test_replicated_full_frame_eight_ranks(spray, oracle, mode):
-    """configs[2] at N = 8, the bench's replicated-ray frame at full size
-    (1024x1024x8spp, every eye ray on every rank, 8 domains per rank, both
-    partitions), 8 engine processes sharing the GPU over the host transport:
-    every shaded sample's record bit-exact against the whole-scene oracle,
-    shaded exactly once across the ranks, totals exact, the composited image
-    within summation order."""
+    """configs[2] at N = 8, the bench's camera frame at full size
+    (1024x1024x8spp, the eye rays generated in the lanes, 8 domains per rank,
+    GROUP_CLOSE and the view-aligned partition), 8 engine processes sharing
+    the GPU over the host transport: every shaded sample's record bit-exact
+    against the whole-scene oracle, shaded exactly once across the ranks,
+    totals exact, rank 0's image within summation order."""
     from spray_amd.engine import host_parse_scene
     parts = _run_replicated(8, mode, "pt")
     _, lights = host_parse_scene(WAVELETS64, SCENES)
@@ -368,11 +364,11 @@ def ao_insitu_ref(oracle):
     return ref
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 2])
 def test_replicated_ao16_full_frame_eight_ranks(spray, oracle, ao_insitu_ref, mode):
     """configs[4] at N = 8, the bench's N > 1 "ao" line at its size: the
-    replicated-ray AO-16 frame (1024x1024x8spp, ~36.6 M AO rays, 8 domains
-    per rank, both partitions), 8 engine processes sharing the GPU over the
+    camera AO-16 frame (1024x1024x8spp, ~36.6 M AO rays, 8 domains per rank,
+    GROUP_CLOSE and view-aligned), 8 engine processes sharing the GPU over the
     host transport -- every shaded sample's winning record and all 16
     AO-slot spawn / occlusion bits bit-exact against the whole-scene oracle
     (ooc::ShaderAo, src/ooc/ooc_shader_ao.h:131-144), each sample shaded

@@ -103,23 +103,24 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, repli
                  mode=0):
     """One rank's engine frame of CASES[case]: returns (records, totals, image).
     one_owner: the last rank owns every domain (the others hold rays only).
-    replicated: spray_rt_insitu_trace_frame with every eye ray on every rank;
-    mode: the partition (GROUP_CLOSE / ROUND_ROBIN)."""
+    replicated: spray_rt_insitu_trace_frame with every eye ray on every rank
+    (True) or spray_rt_insitu_trace_camera ("camera": the rays generated in
+    the lanes); mode: the partition (GROUP_CLOSE / ROUND_ROBIN / VIEW)."""
     import spray_amd
     from spray_amd import insitu
     from oracle import pyoracle as po
     from test_insitu import scene_boxes
     kind, bounces, samples, img, spp = CASES[case]
     boxes, bound = scene_boxes()
-    owner = insitu.morton_partition(boxes, bound, world, mode)
+    c = H.BENCH_CAMERA
+    cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    owner = insitu.partition(boxes, bound, world, mode, cam)
     if one_owner:
         owner = np.full_like(owner, world - 1)
     rt = spray_amd.RtContext(0)
     insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
     rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
     rt.set_stream(torch.cuda.current_stream())
-    c = H.BENCH_CAMERA
-    cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
     block = (0, 0, img, img)
     stripe = block if replicated else insitu.horizontal_stripe(world, rank, block)
     n = stripe[2] * stripe[3] * spp
@@ -132,7 +133,11 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, repli
     eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport=transport)
     recs = insitu.InsituRecords(img * img * spp * bounces + 16)
     image = torch.zeros(img * img * 4, dtype=torch.float32, device="cuda")
-    trace = eng.trace_frame if replicated else eng.trace
+    if replicated == "camera":
+        def trace(sh, rays, pix, sam, spp, image, recs=None):
+            return eng.trace_camera(sh, cam, img, img, spp, image, recs)
+    else:
+        trace = eng.trace_frame if replicated else eng.trace
     eng.set_timing(True)
     tot = trace(sh, rays, pix, sam, spp, image, recs)
     # a second trace reuses the engine's buffers: same totals, image doubles
@@ -297,6 +302,56 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
         assert r[3]["exchanges"] == 0 and r[3]["host_count_reads"] == 2
     # the whole film on rank 0, the other ranks' images untouched
     assert all(not r[2].any() for r in res[1:]) and res[0][2].any()
+
+
+VIEW = 2  # insitu.PARTITION_VIEW
+
+
+@pytest.mark.parametrize("world,mode,case", [(2, VIEW, "pt1"), (3, 0, "pt1"), (8, 0, "pt1"),
+                                             (8, 1, "pt1"), (8, VIEW, "pt1"), (8, VIEW, "ao16"),
+                                             (3, 1, "ao16"), (8, 0, "pt1-u64")])
+def test_engine_camera_frame_ranks(oracle, world, mode, case, monkeypatch):
+    """spray_rt_insitu_trace_camera with world processes sharing the GPU over
+    the host transport: the eye rays generated in the lanes, each rank's
+    closest hit / shadow / film passes over its domains' screen footprints
+    only, the t / list-position MINs and occlusion SUM over U -- every shaded
+    sample bit-exact against the whole-scene oracle, totals exact, the image
+    (rank 0's) within summation order; GROUP_CLOSE, ROUND_ROBIN and the
+    view-aligned partition.  No exchange and no host read."""
+    import pickle
+    if case == "pt1-u64":
+        monkeypatch.setenv("SPRAY_INSITU_SPLIT_KEYS", "0")
+        case = "pt1"
+    with tempfile.TemporaryDirectory() as out:
+        torch.multiprocessing.spawn(_gpu_rank_main,
+                                    args=(world, _free_port(), out, case, False, "camera", mode),
+                                    nprocs=world)
+        res = []
+        for r in range(world):
+            with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
+                res.append(pickle.load(fh))
+    _check(oracle, case, res)
+    assert sum(len(r[0]["samid"]) > 50 for r in res) >= max(2, world // 2)
+    for r in res:
+        assert r[3]["exchanges"] == 0 and r[3]["host_count_reads"] == 0
+    assert all(not r[2].any() for r in res[1:]) and res[0][2].any()
+
+
+@pytest.mark.parametrize("case", ["pt1", "ao16", "pt1-u64"])
+def test_engine_camera_steps_one_rank_rccl(oracle, case, monkeypatch):
+    """The camera frame's replicated steps at world 1 through a one-rank RCCL
+    communicator (SPRAY_INSITU_REPLICATED=1): the calls of the multi-GPU run
+    -- out-of-place t-bits MIN, list-position MIN on the side stream,
+    occlusion SUM, U-pixel film reduce (PT); key MIN, normals SUM, count
+    fields SUM (AO).  Without it world 1 takes the all-local frame."""
+    base = case.split("-")[0]
+    _check(oracle, base, [_engine_rank(0, 1, base, "rccl", replicated="camera")])
+    monkeypatch.setenv("SPRAY_INSITU_REPLICATED", "1")
+    if case.endswith("-u64"):
+        monkeypatch.setenv("SPRAY_INSITU_SPLIT_KEYS", "0")
+    res = _engine_rank(0, 1, base, "rccl", replicated="camera")
+    _check(oracle, base, [res])
+    assert res[3]["collectives"] >= 6 and res[3]["exchanges"] == 0, res[3]
 
 
 @pytest.mark.parametrize("case", ["pt1", "ao16"])
