@@ -181,28 +181,35 @@ def cpu_baseline(target_s=10.0):
                       "%.1f s traversal+spawn" % (reps, n, threads, dt)}
 
 
-def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
+PARTITIONS = {"close": 0, "rr": 1, "view": 2}  # insitu.PARTITION_*
+PARTITION_NAMES = {"close": "Morton, close groups (the reference's compiled mode)",
+                   "rr": "Morton, round robin", "view": "view-aligned"}
+
+
+def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False, partition=None):
     """configs[2] (kind "pt": one bounce, the scene's point light) and
     configs[4] (kind "ao": 16 AO rays per hit): one in-situ frame per step,
     the domains sharded by the reference's Morton partition (64/N per GPU;
     --partition: GROUP_CLOSE or ROUND_ROBIN).
 
-    PT at N > 1 is the replicated-ray frame (spray_rt_insitu_trace_frame):
-    every rank holds the frame's eye rays, traces the rays that touch its
-    domains over its domains, and the ranks agree on every ray's winner with
-    one MIN all-reduce of the hit keys and on every shadow ray's occlusion with
-    one SUM all-reduce of bytes -- no ray crosses the wire.  AO at N > 1 is
-    the replicated-ray AO frame: the same keys, the winners' normals and
-    colours SUM-all-reduced, every rank any-hits every AO ray over its own
-    domains, occlusion count fields SUM-all-reduced, rank 0 films the whole
-    frame.  Replicated frames leave the whole image on rank 0 (PT: per-pixel-
-    run sums reduced there).  protocol=True is the stripe protocol
+    PT at N > 1 is the camera frame (spray_rt_insitu_trace_camera): every
+    rank generates in its lanes the eye rays of the pixels its domains may be
+    seen through (their screen footprints) and traces them over its domains,
+    any-hits the shadow rays of the hit points whose shadow rays may cross
+    its domains, and the ranks agree on every ray's winner with MIN
+    all-reduces of the t bits and list positions and on every shadow ray's
+    occlusion with one SUM all-reduce of bytes -- no ray crosses the wire.
+    AO at N > 1 is the camera AO frame: the same keys, the winners' normals
+    and colours SUM-all-reduced, every rank any-hits the AO rays entering its
+    boxes, occlusion count fields SUM-all-reduced, rank 0 films the whole
+    frame.  Both leave the whole image on rank 0 (PT: per-pixel sums reduced
+    there).  At N = 1 the camera frame is the eye rays + the all-local fused
+    frame.  protocol=True is the stripe protocol
     (spray_rt_insitu_trace): each rank its horizontal stripe of eye rays,
     count-first RCCL all-to-all-v exchanges of rays to their owners, key
     composite, shading at the winner, shadow exchange; the ranks' images are
-    composited by one RCCL reduce (HdrImage::composite).  Eye rays are made once before timing (resident,
-    like the main line).  RCCL is used at every N, N = 1 included (at N = 1
-    PT runs the all-local fused frame unless protocol=True).  Timed like the
+    composited by one RCCL reduce (HdrImage::composite); its eye rays are made
+    once before timing.  RCCL is used at every N, N = 1 included.  Timed like the
     main line (barrier + max over ranks); the per-phase device times come
     from a separate pass with HIP-event timing on."""
     import torch
@@ -212,8 +219,8 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     dev = torch.device("cuda", local)
     boxes, lights = host_parse_scene(SCENE, SCENES)
     bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
-    mode = insitu.PARTITION_ROUND_ROBIN if args.partition == "rr" else insitu.PARTITION_GROUP_CLOSE
-    owner = insitu.morton_partition(boxes, bound, world, mode)
+    mode = PARTITIONS[partition or args.partition]
+    owner = insitu.partition(boxes, bound, world, mode, cam)
     rt = spray_amd.RtContext(local)
     insitu.setup_rank_context(rt, SCENE, SCENES, owner, rank)
     rt.set_bsdfs(host_scene_bsdfs(SCENE))
@@ -221,12 +228,13 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     eng = insitu.InsituEngine(rt, world, rank, dist=dist if world > 1 else None,
                               transport="host" if REHEARSE else "rccl")
     replicated = not protocol
-    stripe = (0, 0, W, H) if replicated else insitu.horizontal_stripe(world, rank, (0, 0, W, H))
-    n = stripe[2] * stripe[3] * SPP
-    rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)[:n]
-    pix = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
-    sam = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
-    rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, pix, sam)
+    if not replicated:  # the protocol's stripe of eye rays, made before timing
+        stripe = insitu.horizontal_stripe(world, rank, (0, 0, W, H))
+        n = stripe[2] * stripe[3] * SPP
+        rays = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)[:n]
+        pix = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+        sam = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+        rt.eye_rays_insitu(cam, W, SPP, (0, 0, W, H), stripe, rays, pix, sam)
     if kind == "ao":
         sh = spray_amd.frame.make_shader("ao", 1, 16, ks=SHADE[6:9], shininess=SHADE[9],
                                          lights=lights)
@@ -237,16 +245,13 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
     old_local = os.environ.get("SPRAY_INSITU_LOCAL")
     if protocol:
         os.environ["SPRAY_INSITU_LOCAL"] = "0"  # the whole protocol, even at one rank
-    trace = eng.trace_frame if replicated else eng.trace
-
-    # replicated frames leave the whole image on rank 0: no composite
-    composite = not replicated
-
+    # camera frames leave the whole image on rank 0: no composite
     def frame():
         image.zero_()
-        t = trace(sh, rays, pix, sam, SPP, image)
-        if composite:
-            eng.composite(image)
+        if replicated:
+            return eng.trace_camera(sh, cam, W, H, SPP, image)
+        t = eng.trace(sh, rays, pix, sam, SPP, image)
+        eng.composite(image)
         return t
 
     try:
@@ -286,15 +291,16 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
         el = float(e.item())
     rays_step = tot[0] + tot[1]
     k = args.steps
-    form = ("replicated-ray frame: every rank holds every eye ray; keyed closest hit + "
-            "shading over its domains, t-bits and list-position MINs all-reduced, shadow "
-            "rays from the minimum t, occlusion bytes SUM-all-reduced, pixel-run sums "
-            "reduced to rank 0" if replicated and world > 1 and kind == "pt"
-            else "replicated-ray AO frame: keys MIN-all-reduced, winners' normals and colours "
+    form = ("camera frame: each rank's eye rays generated in the lanes over its domains' "
+            "screen footprints, keyed closest hit + shading over its domains, t-bits and "
+            "list-position MINs all-reduced, shadow rays from the minimum t over its shadow "
+            "footprint, occlusion bytes SUM-all-reduced, per-pixel sums reduced to rank 0"
+            if replicated and world > 1 and kind == "pt"
+            else "camera AO frame: keys MIN-all-reduced, winners' normals and colours "
             "SUM-all-reduced, every rank any-hits the AO pairs entering its boxes "
             "(compacted), occlusion count fields SUM-all-reduced, film on rank 0"
             if replicated and world > 1
-            else "all-local frame" if replicated or (world == 1 and not protocol)
+            else "eye rays + all-local frame" if replicated or (world == 1 and not protocol)
             else "stripe protocol: speculative ray exchange over RCCL all-to-all-v, image "
                  "composite by RCCL reduce")
     out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
@@ -306,11 +312,11 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False):
            "rank0_collectives_per_step": (s1["collectives"] - s0["collectives"]) / k,
            "rank0_phases_ms": phases,
            "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
-           "partition": args.partition,
-           "config": "%s: 64 domains, %d per GPU (Morton partition, %s), 1024x1024x8spp, %s, %s"
+           "partition": partition or args.partition,
+           "config": "%s: 64 domains, %d per GPU (%s partition), 1024x1024x8spp, %s, %s"
                      % ("configs[4]" if kind == "ao" else "configs[2]",
                         int(np.bincount(owner, minlength=world)[rank]),
-                        "round robin" if mode == insitu.PARTITION_ROUND_ROBIN else "close groups",
+                        PARTITION_NAMES[partition or args.partition],
                         "AO-16 rays per hit" if kind == "ao" else "PT point-light shadows", form)}
     eng.close()
     rt.close()
@@ -512,9 +518,11 @@ def main():
     ap.add_argument("--insitu", type=int, default=1,
                     help="also measure configs[2] through the engine's RCCL in-situ tracer "
                          "(always on with more than one rank: it is the headline there)")
-    ap.add_argument("--partition", choices=("close", "rr"), default="close",
+    ap.add_argument("--partition", choices=("close", "rr", "view"), default="view",
                     help="in-situ domain partition: close (GROUP_CLOSE_DOMAINS, the reference's "
-                         "compiled mode) or rr (round robin over the Morton order)")
+                         "compiled mode), rr (round robin over the Morton order) or view (the "
+                         "view-aligned partition: domains along neighbouring lines of sight "
+                         "grouped per rank); at N > 1 the other partitions are timed too")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
@@ -674,6 +682,13 @@ def main():
         # the one-rank RCCL communicator (SPRAY_INSITU_LOCAL=0), phase split
         out["insitu_protocol"] = run_insitu(args, dist, world, rank, local, cam, protocol=True)
     if world > 1:
+        # the same frame under the other partitions (the reference's compiled
+        # GROUP_CLOSE among them), each a secondary key
+        out["insitu_partitions"] = {
+            p: {k: v for k, v in run_insitu(args, dist, world, rank, local, cam,
+                                            partition=p).items()
+                if k in ("value", "ms_per_step", "rank0_phases_ms")}
+            for p in PARTITIONS if p != args.partition}
         # configs[2] is the N > 1 headline: the frame split across the GPUs by
         # domain (strong scaling); the frame replicas stay as a secondary key
         ins = out["insitu"]

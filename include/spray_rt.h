@@ -709,6 +709,24 @@ int spray_rt_camera_box_rect(const float cam[14], int image_w, int image_h, cons
                              int rect[4]);
 int spray_rt_camera_shadow_region(const float box[6], const float scene[6], const float light[3],
                                   float out[6]);
+/* Measurement: one rank of an N-rank group rehearsed alone on one GPU.  A
+ * replay context's collectives do not communicate: the camera frame's
+ * t-bits and list-position MINs copy the group results given by
+ * spray_rt_insitu_replay_set (device arrays over U, as
+ * spray_rt_insitu_replay_capture reads them after a one-rank replicated
+ * camera frame with every domain resident, SPRAY_INSITU_REPLICATED=1), the
+ * SUMs and the reduce keep the rank's own values.  Its device work is the
+ * rank's exact share of the N-rank frame (its launches, their sizes and the
+ * rays they walk), back to back on its stream; the film and totals it
+ * produces are not the frame's.  PT camera frames with split keys only. */
+int spray_rt_insitu_create_replay(spray_rt_ctx_t ctx, int world, int rank,
+                                  spray_rt_insitu_t* out);
+int spray_rt_insitu_replay_set(spray_rt_insitu_t ins, const uint32_t* d_tmin,
+                               const uint8_t* d_lpmin, size_t n);
+/* *n = U slots of the last camera PT frame; with d_tmin / d_lpmin (device,
+ * cap entries) copies its group t-bits minima and list-position minima. */
+int spray_rt_insitu_replay_capture(spray_rt_insitu_t ins, uint32_t* d_tmin, uint8_t* d_lpmin,
+                                   size_t cap, size_t* n);
 /* Per-phase device time of the traces since the last call (then reset),
  * HIP events on the context's stream, when phase timing is on
  * (spray_rt_insitu_set_timing).  out_ms[9]; *nphases = phases of the last

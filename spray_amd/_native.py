@@ -140,6 +140,9 @@ SIGNATURES = {
     "spray_rt_insitu_trace_frame": (I, [P, P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_insitu_trace_camera": (I, [P, P, P, I, I, I, P, P, P]),
     "spray_rt_insitu_partition_view": (I, [P, I, P, I, P]),
+    "spray_rt_insitu_create_replay": (I, [P, I, I, P]),
+    "spray_rt_insitu_replay_set": (I, [P, P, P, SZ]),
+    "spray_rt_insitu_replay_capture": (I, [P, P, P, SZ, P]),
     "spray_rt_camera_box_rect": (I, [P, I, I, P, P]),
     "spray_rt_camera_shadow_region": (I, [P, P, P, P]),
     "spray_rt_insitu_set_timing": (I, [P, I]),

@@ -184,6 +184,7 @@ struct spray_rt_insitu {
   DBuf tu_runs, tu_first, te_runs, te_first, ts_runs, ts_first;
   CamTable tu{}, te{}, ts{};
   uint32_t tu_pixmax = 0;
+  size_t last_nu = 0;  // U slots of the last camera PT frame
   DBuf ctmin, ccomp, crays, cpix, csam, ciota;
   size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
@@ -308,6 +309,60 @@ struct RcclTransport : InsituTransport {
   ~RcclTransport() override {
     if (comm) nccl().CommDestroy(comm);
   }
+};
+
+// ---- replay (measurement: one rank of an N-rank group alone on one GPU) ----
+// The group results of a camera frame given up front (the t-bits and
+// list-position MINs over U, captured from a one-rank frame with every
+// domain resident): the MINs copy them, the SUMs and the reduce keep the
+// rank's own values.  The rank's device work is then its exact share of the
+// N-rank frame, back to back on its stream with no idle gaps between
+// collectives (the per-rank segment times of the multi-GPU projection).
+struct ReplayTransport : InsituTransport {
+  const uint32_t* tmin = nullptr;
+  const uint8_t* lpmin = nullptr;
+  size_t n = 0;
+  int copy(spray_rt_insitu* I, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    ++I->st[4];
+    if (bytes) HIPCHK(I->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    return SPRAY_RT_OK;
+  }
+  int need(spray_rt_insitu* I, size_t m) {
+    if (!tmin || m != n)
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu slots given, the frame has %zu", n, m);
+    return SPRAY_RT_OK;
+  }
+  int counts(spray_rt_insitu* I, const int64_t*, int64_t*, int64_t*) override {
+    return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
+  }
+  int alltoallv(spray_rt_insitu* I, const void*, const size_t*, void*, const size_t*,
+                bool) override {
+    return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
+  }
+  int allreduce_u64(spray_rt_insitu* I, unsigned long long*, size_t) override {
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int reduce_f32(spray_rt_insitu* I, float*, size_t, int) override {
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int allreduce_min_u64(spray_rt_insitu* I, uint64_t*, size_t) override {
+    return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: split keys only");
+  }
+  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t*, size_t) override {
+    ++I->st[4];
+    return SPRAY_RT_OK;
+  }
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t*, uint32_t* dst, size_t m) override {
+    CALL(need(I, m));
+    return copy(I, dst, tmin, m * 4, stream_of(I->ctx));
+  }
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t m, hipStream_t st) override {
+    CALL(need(I, m));
+    return copy(I, dev, lpmin, m, st);
+  }
+  bool side_stream() const override { return true; }
 };
 
 // ---- host callbacks (staged) ----
@@ -1326,6 +1381,7 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   const size_t nu = size_t(I->tu.npix) * size_t(spp);  // U slots
   const size_t npu = I->tu.npix;                       // U pixels
   const bool split = split_keys() && c->ndom <= 255;
+  I->last_nu = nu;
   GROW(I->rkeys_c, nu * 8 + 8);
   GROW(I->rtk, nu * 4 + 4);
   GROW(I->ctmin, nu * 4 + 4);
@@ -1560,6 +1616,57 @@ int spray_rt_insitu_create(spray_rt_ctx_t c, int world, int rank, const void* nc
     I->tr = std::move(t);
   }
   *out = I.release();
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_create_replay(spray_rt_ctx_t c, int world, int rank,
+                                  spray_rt_insitu_t* out) {
+  if (!c || !out) return SPRAY_RT_ERR_ARG;
+  *out = nullptr;
+  if (world < 1 || world > 64 || rank < 0 || rank >= world)
+    return fail(c, SPRAY_RT_ERR_ARG, "in-situ group: world %d rank %d (world in [1, 64])", world,
+                rank);
+  HIPCHK(c, hipSetDevice(c->device));
+  std::unique_ptr<spray_rt_insitu> I(new (std::nothrow) spray_rt_insitu);
+  if (!I) return SPRAY_RT_ERR_NOMEM;
+  I->ctx = c;
+  I->world = world;
+  I->rank = rank;
+  HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&I->h_small), 256 * 8, hipHostMallocDefault));
+  I->tr = std::make_unique<ReplayTransport>();
+  *out = I.release();
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_replay_set(spray_rt_insitu_t I, const uint32_t* d_tmin,
+                               const uint8_t* d_lpmin, size_t n) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  auto* t = dynamic_cast<ReplayTransport*>(I->tr.get());
+  if (!t) return fail(I->ctx, SPRAY_RT_ERR_STATE, "not a replay context");
+  if (n && (!is_device_ptr(d_tmin) || !is_device_ptr(d_lpmin)))
+    return fail(I->ctx, SPRAY_RT_ERR_ARG, "replay arrays must be device memory");
+  t->tmin = d_tmin;
+  t->lpmin = d_lpmin;
+  t->n = n;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_replay_capture(spray_rt_insitu_t I, uint32_t* d_tmin, uint8_t* d_lpmin,
+                                   size_t cap, size_t* n) {
+  if (!I || !n) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = I->ctx;
+  // U slots of the last camera frame: the U pixels times its spp (the
+  // group MIN arrays were sized for them)
+  if (I->cam_key.empty() || !I->ctmin.p || !I->rlp.p)
+    return fail(c, SPRAY_RT_ERR_STATE, "no replicated camera frame traced yet");
+  const size_t m = I->last_nu;
+  *n = m;
+  if (!d_tmin || !d_lpmin) return SPRAY_RT_OK;  // size query
+  if (cap < m) return fail(c, SPRAY_RT_ERR_LIMIT, "replay capture: %zu slots, cap %zu", m, cap);
+  hipStream_t s = stream_of(c);
+  HIPCHK(c, hipMemcpyAsync(d_tmin, I->ctmin.p, m * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_lpmin, I->rlp.p, m, hipMemcpyDeviceToDevice, s));
+  HIPCHK(c, hipStreamSynchronize(s));
   return SPRAY_RT_OK;
 }
 

@@ -268,7 +268,9 @@ class InsituEngine:
 
     transport="rccl" (the product): RCCL communicator from an id made on
     rank 0 and broadcast over ``dist`` (world 1 needs no ``dist``).
-    transport="host": host-staged collectives over ``dist`` (tests)."""
+    transport="host": host-staged collectives over ``dist`` (tests).
+    transport="replay": no collectives -- the group results of a camera
+    frame replayed from replay_set (measurement of one rank alone)."""
 
     def __init__(self, rt, world=1, rank=0, dist=None, transport="rccl", group=None):
         import torch
@@ -298,8 +300,10 @@ class InsituEngine:
                 self._host = _LocalCollectives()
             rc = L.spray_rt_insitu_create(rt.h, self.world, self.rank, None,
                                           C.byref(self._host.struct), C.byref(h))
+        elif transport == "replay":
+            rc = L.spray_rt_insitu_create_replay(rt.h, self.world, self.rank, C.byref(h))
         else:
-            raise ValueError("transport must be 'rccl' or 'host'")
+            raise ValueError("transport must be 'rccl', 'host' or 'replay'")
         rt._check(rc, "insitu_create")
         self.h = h.value
 
@@ -366,6 +370,26 @@ class InsituEngine:
         self.rt._check(rc, "insitu_trace_camera")
         self._rep_kind = "ao" if shader.shader == SHADER_AO else "pt"
         return int(tot[0]), int(tot[1])
+
+    def replay_capture(self):
+        """(tmin u32, lpmin u8) device tensors of the last camera PT frame's
+        group minima over U (spray_rt_insitu_replay_capture)."""
+        import torch
+        n = C.c_size_t(0)
+        self.rt._check(lib().spray_rt_insitu_replay_capture(self.h, None, None, 0, C.byref(n)),
+                       "replay_capture")
+        t = torch.empty(max(n.value, 1), dtype=torch.int32, device="cuda")[:n.value]
+        lp = torch.empty(max(n.value, 1), dtype=torch.uint8, device="cuda")[:n.value]
+        self.rt._check(lib().spray_rt_insitu_replay_capture(self.h, t.data_ptr(), lp.data_ptr(),
+                                                            n.value, C.byref(n)),
+                       "replay_capture")
+        return t, lp
+
+    def replay_set(self, tmin, lpmin):
+        """The group results a replay context's collectives hand back."""
+        self._replay = (tmin, lpmin)  # keep the tensors alive
+        self.rt._check(lib().spray_rt_insitu_replay_set(self.h, tmin.data_ptr(), lpmin.data_ptr(),
+                                                        tmin.numel()), "replay_set")
 
     def set_timing(self, on=True):
         """Per-phase HIP-event timing of the traces (phase_times)."""
