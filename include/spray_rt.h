@@ -700,15 +700,16 @@ int spray_rt_insitu_trace_camera(spray_rt_insitu_t ins, const spray_rt_shader* s
  * camera; results do not depend on the partition. */
 int spray_rt_insitu_partition_view(const float* boxes, int n, const float cam[14], int nranks,
                                    int* owner);
-/* Footprint primitives of the camera frames (tests): the inclusive pixel
- * rectangle {x0, x1, y0, y1} holding every eye ray of cam that may enter
- * box (returns 0 = none, 1 = rect, 2 = the whole image; -1 bad arguments);
- * the box holding every hit point inside scene whose shadow ray toward the
- * point light may cross box (returns 0 = out holds it, 1 = everywhere). */
-int spray_rt_camera_box_rect(const float cam[14], int image_w, int image_h, const float box[6],
-                             int rect[4]);
-int spray_rt_camera_shadow_region(const float box[6], const float scene[6], const float light[3],
-                                  float out[6]);
+/* Footprint primitives of the camera frames (tests): per image row y the
+ * inclusive pixel range [x0[y], x1[y]] holding every eye ray of cam that
+ * may enter box (x0 > x1: none; returns 0 = no pixel, 1 = rows, 2 = the
+ * whole image; -1 bad arguments); the k slice boxes (out float[k][6])
+ * whose union holds every hit point inside scene whose shadow ray toward
+ * the point light may cross box (returns their count, -1 = everywhere). */
+int spray_rt_camera_box_rows(const float cam[14], int image_w, int image_h, const float box[6],
+                             int* x0, int* x1);
+int spray_rt_camera_shadow_boxes(const float box[6], const float scene[6], const float light[3],
+                                 int k, float* out);
 /* Measurement: one rank of an N-rank group rehearsed alone on one GPU.  A
  * replay context's collectives do not communicate: the camera frame's
  * t-bits and list-position MINs copy the group results given by

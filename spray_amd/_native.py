@@ -143,8 +143,8 @@ SIGNATURES = {
     "spray_rt_insitu_create_replay": (I, [P, I, I, P]),
     "spray_rt_insitu_replay_set": (I, [P, P, P, SZ]),
     "spray_rt_insitu_replay_capture": (I, [P, P, P, SZ, P]),
-    "spray_rt_camera_box_rect": (I, [P, I, I, P, P]),
-    "spray_rt_camera_shadow_region": (I, [P, P, P, P]),
+    "spray_rt_camera_box_rows": (I, [P, I, I, P, P, P]),
+    "spray_rt_camera_shadow_boxes": (I, [P, P, P, I, P]),
     "spray_rt_insitu_set_timing": (I, [P, I]),
     "spray_rt_insitu_phase_times": (I, [P, P, P]),
     "spray_rt_insitu_composite": (I, [P, P, SZ]),

@@ -46,9 +46,84 @@ void project(const Proj& p, const double X[3], double* x, double* y, double* dep
   *y = c / a * p.h;
 }
 
-int box_rect(const Proj& p, const float box[6], int image_w, int image_h, int rect[4]) {
-  double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
-  int front = 0, behind = 0;
+namespace {
+
+struct P2 {
+  double x, y;
+};
+
+// Andrew's monotone chain; the hull counter-clockwise without repeats
+std::vector<P2> hull(std::vector<P2> p) {
+  std::sort(p.begin(), p.end(), [](const P2& a, const P2& b) {
+    return a.x < b.x || (a.x == b.x && a.y < b.y);
+  });
+  if (p.size() < 3) return p;
+  std::vector<P2> h(2 * p.size());
+  size_t k = 0;
+  const auto cross = [](const P2& o, const P2& a, const P2& b) {
+    return (a.x - o.x) * (b.y - o.y) - (a.y - o.y) * (b.x - o.x);
+  };
+  for (size_t i = 0; i < p.size(); ++i) {
+    while (k >= 2 && cross(h[k - 2], h[k - 1], p[i]) <= 0) --k;
+    h[k++] = p[i];
+  }
+  for (size_t i = p.size() - 1, t = k + 1; i > 0; --i) {
+    while (k >= t && cross(h[k - 2], h[k - 1], p[i - 1]) <= 0) --k;
+    h[k++] = p[i - 1];
+  }
+  h.resize(k - 1);
+  return h;
+}
+
+// x-extent of convex polygon `poly` within the band ya <= y <= yb (false:
+// empty): the polygon clipped by the two lines (Sutherland-Hodgman)
+bool band_extent(const std::vector<P2>& poly, double ya, double yb, double* x0, double* x1) {
+  std::vector<P2> a = poly, b;
+  const auto clip = [](const std::vector<P2>& in, std::vector<P2>& out, double y, bool keep_above) {
+    out.clear();
+    const size_t n = in.size();
+    for (size_t i = 0; i < n; ++i) {
+      const P2& c = in[i];
+      const P2& d = in[(i + 1) % n];
+      const bool ci = keep_above ? c.y >= y : c.y <= y;
+      const bool di = keep_above ? d.y >= y : d.y <= y;
+      if (ci) out.push_back(c);
+      if (ci != di) {
+        const double t = (y - c.y) / (d.y - c.y);
+        out.push_back(P2{c.x + t * (d.x - c.x), y});
+      }
+    }
+  };
+  if (a.size() < 3) {  // degenerate hull: its points in the band
+    double lo = INFINITY, hi = -INFINITY;
+    for (const P2& q : a)
+      if (q.y >= ya && q.y <= yb) {
+        lo = std::min(lo, q.x);
+        hi = std::max(hi, q.x);
+      }
+    *x0 = lo;
+    *x1 = hi;
+    return lo <= hi;
+  }
+  clip(a, b, ya, true);
+  if (b.empty()) return false;
+  clip(b, a, yb, false);
+  if (a.empty()) return false;
+  double lo = INFINITY, hi = -INFINITY;
+  for (const P2& q : a) {
+    lo = std::min(lo, q.x);
+    hi = std::max(hi, q.x);
+  }
+  *x0 = lo;
+  *x1 = hi;
+  return true;
+}
+
+}  // namespace
+
+int box_rows(const Proj& p, const float box[6], int image_w, int image_h, Rows& rows) {
+  std::vector<P2> pts;
+  int behind = 0;
   for (int k = 0; k < 8; ++k) {
     const double X[3] = {box[(k & 1) ? 3 : 0], box[(k & 2) ? 4 : 1], box[(k & 4) ? 5 : 2]};
     double x, y, d;
@@ -59,73 +134,70 @@ int box_rect(const Proj& p, const float box[6], int image_w, int image_h, int re
       ++behind;
       continue;
     }
-    ++front;
-    xmin = std::min(xmin, x);
-    xmax = std::max(xmax, x);
-    ymin = std::min(ymin, y);
-    ymax = std::max(ymax, y);
+    pts.push_back(P2{x, y});
   }
-  if (!front) return 0;  // wholly behind the eye: no eye ray enters it
-  if (behind) {
-    rect[0] = 0;
-    rect[1] = image_w - 1;
-    rect[2] = 0;
-    rect[3] = image_h - 1;
-    return 2;
+  if (pts.empty()) return 0;  // wholly behind the eye: no eye ray enters it
+  if (behind) return 2;
+  double ymin = INFINITY, ymax = -INFINITY;
+  for (const P2& q : pts) {
+    ymin = std::min(ymin, q.y);
+    ymax = std::max(ymax, q.y);
   }
-  const auto clampi = [](double v, int lo, int hi) {
-    if (!(v > lo)) return lo;
-    if (!(v < hi)) return hi;
-    return int(v);
-  };
-  const int x0 = clampi(std::floor(xmin) - kGuard, 0, image_w - 1);
-  const int x1 = clampi(std::floor(xmax) + kGuard, 0, image_w - 1);
-  const int y0 = clampi(std::floor(ymin) - kGuard, 0, image_h - 1);
-  const int y1 = clampi(std::floor(ymax) + kGuard, 0, image_h - 1);
-  // wholly off one side of the image
-  if (std::floor(xmax) + kGuard < 0 || std::floor(xmin) - kGuard > image_w - 1 ||
-      std::floor(ymax) + kGuard < 0 || std::floor(ymin) - kGuard > image_h - 1)
-    return 0;
-  rect[0] = x0;
-  rect[1] = x1;
-  rect[2] = y0;
-  rect[3] = y1;
-  return 1;
+  const double ylo = std::floor(ymin) - kGuard, yhi = std::floor(ymax) + kGuard;
+  if (yhi < 0 || ylo > image_h - 1) return 0;
+  const std::vector<P2> h = hull(pts);
+  const int y0 = int(std::max(ylo, 0.0)), y1 = int(std::min(yhi, double(image_h - 1)));
+  bool any = false;
+  for (int y = y0; y <= y1; ++y) {
+    // rays of row y have image y in [y, y + 1); kGuard rows of margin
+    double xa, xb;
+    if (!band_extent(h, double(y - kGuard), double(y + 1 + kGuard), &xa, &xb)) continue;
+    const double lo = std::floor(xa) - kGuard, hi = std::floor(xb) + kGuard;
+    if (hi < 0 || lo > image_w - 1) continue;
+    rows[size_t(y)].push_back({int(std::max(lo, 0.0)), int(std::min(hi, double(image_w - 1)))});
+    any = true;
+  }
+  return any ? 1 : 0;
 }
 
-int shadow_region(const float box[6], const float scene[6], const float light[3], float out[6]) {
+int shadow_boxes(const float box[6], const float scene[6], const float light[3], int k,
+                 float* out) {
   double ext = 0.0;
   for (int a = 0; a < 3; ++a) ext = std::max(ext, double(scene[3 + a]) - double(scene[a]));
   const double pad = 1e-3 * std::max(ext, 1.0);
   bool inside = true;
   for (int a = 0; a < 3; ++a)
     inside = inside && light[a] >= scene[a] - pad && light[a] <= scene[3 + a] + pad;
-  if (inside) return 1;
+  if (inside) return -1;
   double smax = INFINITY;
   for (int a = 0; a < 3; ++a) {
     const double lo = box[a], hi = box[3 + a], L = light[a];
     if (L < lo) smax = std::min(smax, (double(scene[3 + a]) - lo) / (lo - L));
     if (L > hi) smax = std::min(smax, (hi - double(scene[a])) / (L - hi));
   }
-  if (!std::isfinite(smax)) return 1;
+  if (!std::isfinite(smax)) return -1;
   smax = std::max(smax, 0.0);
-  for (int a = 0; a < 3; ++a) {
-    const double lo = box[a], hi = box[3 + a], L = light[a];
-    const double lo2 = (1.0 + smax) * lo - smax * L, hi2 = (1.0 + smax) * hi - smax * L;
-    const double rlo = std::max(std::min(lo, lo2) - pad, double(scene[a]) - pad);
-    const double rhi = std::min(std::max(hi, hi2) + pad, double(scene[3 + a]) + pad);
-    out[a] = float(rlo);
-    out[3 + a] = float(rhi);
-    // float rounding of the bounds: outward
-    if (double(out[a]) > rlo) out[a] = std::nextafter(out[a], -INFINITY);
-    if (double(out[3 + a]) < rhi) out[3 + a] = std::nextafter(out[3 + a], INFINITY);
+  int n = 0;
+  for (int i = 0; i < k; ++i) {
+    const double s0 = smax * i / k, s1 = smax * (i + 1) / k;
+    float* o = out + 6 * n;
+    bool empty = false;
+    for (int a = 0; a < 3; ++a) {
+      const double lo = box[a], hi = box[3 + a], L = light[a];
+      const double l0 = lo + s0 * (lo - L), l1 = lo + s1 * (lo - L);
+      const double h0 = hi + s0 * (hi - L), h1 = hi + s1 * (hi - L);
+      const double rlo = std::max(std::min(l0, l1) - pad, double(scene[a]) - pad);
+      const double rhi = std::min(std::max(h0, h1) + pad, double(scene[3 + a]) + pad);
+      if (rlo > rhi) empty = true;
+      o[a] = float(rlo);
+      o[3 + a] = float(rhi);
+      // float rounding of the bounds: outward
+      if (double(o[a]) > rlo) o[a] = std::nextafter(o[a], -INFINITY);
+      if (double(o[3 + a]) < rhi) o[3 + a] = std::nextafter(o[3 + a], INFINITY);
+    }
+    if (!empty) ++n;
   }
-  return 0;
-}
-
-void add_rect(Rows& rows, const int rect[4]) {
-  for (int y = rect[2]; y <= rect[3]; ++y)
-    if (y >= 0 && y < int(rows.size())) rows[size_t(y)].push_back({rect[0], rect[1]});
+  return n;
 }
 
 void merge_rows(Rows& rows) {

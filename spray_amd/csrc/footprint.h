@@ -34,21 +34,27 @@ bool make_proj(const float cam[14], Proj* p);
 // ray (> 0: in front of the eye)
 void project(const Proj& p, const double X[3], double* x, double* y, double* depth);
 
-// rect = [x0, x1] x [y0, y1] (inclusive pixels) of the eye rays that may
-// enter box (lo[3], hi[3]); returns 0 = none, 1 = rect, 2 = the whole image
-int box_rect(const Proj& p, const float box[6], int image_w, int image_h, int rect[4]);
-
-// The hit points p inside scene box S whose shadow ray toward point light L
-// may cross box B: {q + s (q - L) : q in B, s >= 0} within S, bounded by the
-// box AABB(B u B') n S with B' = (1 + s_max) B - s_max L (s_max: where the
-// scaled copy leaves S along the first axis L lies outside B's slab in).
-// Returns 0 and that box in out, or 1 = every point (L inside S: an
-// unbounded shadow ray may meet B beyond the light).
-int shadow_region(const float box[6], const float scene[6], const float light[3], float out[6]);
-
 // per image row: sorted, disjoint inclusive x intervals
 using Rows = std::vector<std::vector<std::pair<int, int>>>;
-void add_rect(Rows& rows, const int rect[4]);
+
+// The pixels whose eye rays may enter box (lo[3], hi[3]): per row, the
+// x-extent of the projected box (the convex hull of its eight projected
+// corners) over the row's band, widened by kGuard pixels in x and y, added
+// to rows (which has image_h rows).  Returns 0 = none, 1 = added, 2 = the
+// whole image (a corner at or behind the eye plane; nothing added).
+int box_rows(const Proj& p, const float box[6], int image_w, int image_h, Rows& rows);
+
+// The hit points p inside scene box S whose shadow ray toward point light L
+// may cross box B: {q + s (q - L) : q in B, 0 <= s <= s_max} within S
+// (s_max: where the scaled copy (1 + s) B - s L leaves S along the first
+// axis L lies outside B's slab in), as the union of k boxes: slice i is
+// AABB(B(s_i) u B(s_i+1)) n S for s_i = s_max i / k -- the coordinates are
+// affine in s, so each slice holds its interval's copies.  Returns the
+// boxes written to out (<= k, float[k][6]), or -1 = every point (L inside
+// S: an unbounded shadow ray may meet B beyond the light).
+int shadow_boxes(const float box[6], const float scene[6], const float light[3], int k,
+                 float* out);
+constexpr int kShadowSlices = 16;
 void merge_rows(Rows& rows);
 Rows intersect_rows(const Rows& a, const Rows& b);
 

@@ -1321,22 +1321,27 @@ int prepare_camera(spray_rt_insitu* I, const CamFrame& F, int image_h, const flo
     }
   const size_t rows = static_cast<size_t>(image_h);
   fp::Rows U(rows), E(rows), S(rows);
-  bool s_all = false;
+  bool u_all = false, e_all = false, s_all = false;
+  float reg[6 * fp::kShadowSlices];
   for (int d = 0; d < n; ++d) {
     const float* b = &c->h_boxes[6 * size_t(d)];
-    int rect[4];
-    if (fp::box_rect(pj, b, F.image_w, image_h, rect)) fp::add_rect(U, rect);
     const bool own = size_t(d) < c->dom2slot.size() && c->dom2slot[size_t(d)] >= 0;
+    const int k = fp::box_rows(pj, b, F.image_w, image_h, U);
+    u_all = u_all || k == 2;
     if (!own) continue;
-    if (fp::box_rect(pj, b, F.image_w, image_h, rect)) fp::add_rect(E, rect);
+    e_all = e_all || fp::box_rows(pj, b, F.image_w, image_h, E) == 2;
     if (light) {
-      float reg[6];
-      if (fp::shadow_region(b, scene, light, reg))
-        s_all = true;
-      else if (fp::box_rect(pj, reg, F.image_w, image_h, rect))
-        fp::add_rect(S, rect);
+      const int ns = fp::shadow_boxes(b, scene, light, fp::kShadowSlices, reg);
+      if (ns < 0) s_all = true;
+      for (int q = 0; q < ns; ++q)
+        s_all = s_all || fp::box_rows(pj, reg + 6 * q, F.image_w, image_h, S) == 2;
     }
   }
+  const auto whole = [&](fp::Rows& r) {
+    for (auto& row : r) row.assign(1, {0, F.image_w - 1});
+  };
+  if (u_all) whole(U);
+  if (e_all) whole(E);
   fp::merge_rows(U);
   fp::merge_rows(E);
   fp::merge_rows(S);
@@ -1873,18 +1878,25 @@ int spray_rt_insitu_partition_view(const float* boxes, int n, const float cam[14
   return SPRAY_RT_OK;
 }
 
-int spray_rt_camera_box_rect(const float cam[14], int image_w, int image_h, const float box[6],
-                             int rect[4]) {
-  if (!cam || !box || !rect || image_w <= 0 || image_h <= 0) return -1;
+int spray_rt_camera_box_rows(const float cam[14], int image_w, int image_h, const float box[6],
+                             int* x0, int* x1) {
+  if (!cam || !box || !x0 || !x1 || image_w <= 0 || image_h <= 0) return -1;
   fp::Proj pj;
   if (!fp::make_proj(cam, &pj)) return -1;
-  return fp::box_rect(pj, box, image_w, image_h, rect);
+  fp::Rows rows(static_cast<size_t>(image_h));
+  const int k = fp::box_rows(pj, box, image_w, image_h, rows);
+  for (int y = 0; y < image_h; ++y) {
+    const auto& r = rows[size_t(y)];
+    x0[y] = k == 2 ? 0 : (r.empty() ? image_w : r.front().first);
+    x1[y] = k == 2 ? image_w - 1 : (r.empty() ? -1 : r.back().second);
+  }
+  return k;
 }
 
-int spray_rt_camera_shadow_region(const float box[6], const float scene[6], const float light[3],
-                                  float out[6]) {
-  if (!box || !scene || !light || !out) return -1;
-  return fp::shadow_region(box, scene, light, out);
+int spray_rt_camera_shadow_boxes(const float box[6], const float scene[6], const float light[3],
+                                 int k, float* out) {
+  if (!box || !scene || !light || !out || k <= 0) return -2;
+  return fp::shadow_boxes(box, scene, light, k, out);
 }
 
 int spray_rt_insitu_set_timing(spray_rt_insitu_t I, int on) {

@@ -22,14 +22,7 @@ namespace {
 
 constexpr float kInf = __builtin_inff();
 constexpr int32_t kNone = INT_MAX;
-constexpr int32_t kNoChildRef = INT32_MIN;
-// 4-wide any hit: 0 = the nearest entered child next, the others pushed in
-// child order; 1 = entered children pushed far to near (sorted; measured
-// 4.30 vs 4.11 ms for the AO-16 any hit); 2 = no ordering (first entered
-// child next)
-#ifndef SPRAY_Q4_SORT
-#define SPRAY_Q4_SORT 0
-#endif  // empty child (bvh_build.h kNoChild)
+constexpr int32_t kNoChildRef = INT32_MIN;  // empty child (bvh_build.h kNoChild)
 
 inline unsigned grid_for(size_t M) { return unsigned((M + kBlock - 1) / kBlock); }
 
@@ -439,46 +432,8 @@ __device__ __forceinline__ bool occluded_tree_q4(const void* nodes, const void* 
                     tnear, tfar, t[2]);
       h[3] = slab_q(qr, q_lo(c.y), q_hi(c.y), q_lo(c.z), q_hi(c.z), q_lo(c.w), q_hi(c.w),
                     tnear, tfar, t[3]);
-#if SPRAY_Q4_SORT == 2
-      // no ordering: the first entered child next, the others pushed
-      int32_t next = kNone;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (!h[k] || ref[k] == kNoChildRef) continue;
-        if (next == kNone)
-          next = ref[k];
-        else
-          push(ref[k]);
-      }
-#elif SPRAY_Q4_SORT == 1
-      // entered children sorted near to far (a 5-exchange network), pushed
-      // far first: the next pops are the nearer siblings
-      int32_t rs[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool e = h[k] && ref[k] != kNoChildRef;
-        rs[k] = e ? ref[k] : kNone;
-        t[k] = e ? t[k] : kInf;
-      }
-      auto cx = [&](int x, int y) {
-        const bool sw = t[y] < t[x];
-        const float tx = t[x];
-        const int32_t rx = rs[x];
-        t[x] = sw ? t[y] : tx;
-        t[y] = sw ? tx : t[y];
-        rs[x] = sw ? rs[y] : rx;
-        rs[y] = sw ? rx : rs[y];
-      };
-      cx(0, 1);
-      cx(2, 3);
-      cx(0, 2);
-      cx(1, 3);
-      cx(1, 2);
-      if (rs[3] != kNone) push(rs[3]);
-      if (rs[2] != kNone) push(rs[2]);
-      if (rs[1] != kNone) push(rs[1]);
-      const int32_t next = rs[0];
-#else
+      // the nearest entered child next, the others pushed (sorting them far
+      // to near, or no order at all, measured slower: DESIGN.md section 4)
       int32_t next = kNone;
       float tn = kInf;
 #pragma unroll
@@ -492,7 +447,6 @@ __device__ __forceinline__ bool occluded_tree_q4(const void* nodes, const void* 
           push(ref[k]);
         }
       }
-#endif
       cur = next != kNone ? next : pop();
       if (cur < 0 && leaf == kNone) {  // park the leaf, keep descending
         leaf = cur;

@@ -31,7 +31,7 @@ from ._native import SHADER_AO, SprayRtError, lib
 
 __all__ = ["morton_partition", "view_partition", "partition", "PARTITION_GROUP_CLOSE",
            "PARTITION_ROUND_ROBIN", "PARTITION_VIEW", "horizontal_stripe", "setup_rank_context",
-           "InsituEngine", "InsituRecords", "MISS_KEY", "box_rect", "shadow_region"]
+           "InsituEngine", "InsituRecords", "MISS_KEY", "box_rows", "shadow_boxes"]
 
 MISS_KEY = 0x7FFFFFFFFFFFFFFF
 
@@ -64,28 +64,33 @@ def partition(boxes, scene_bound, nranks, mode, cam=None):
     return morton_partition(boxes, scene_bound, nranks, mode)
 
 
-def box_rect(cam, image_w, image_h, box):
-    """(kind, [x0, x1, y0, y1]) of spray_rt_camera_box_rect: kind 0 = no eye
-    ray enters the box, 1 = the rectangle, 2 = the whole image"""
+def box_rows(cam, image_w, image_h, box):
+    """(kind, x0[h], x1[h]) of spray_rt_camera_box_rows: per image row the
+    pixel range whose eye rays may enter the box (x0 > x1: none); kind 0 =
+    none, 1 = rows, 2 = the whole image"""
     c = np.ascontiguousarray(cam, np.float32).reshape(14)
     b = np.ascontiguousarray(box, np.float32).reshape(6)
-    r = np.zeros(4, np.int32)
-    k = lib().spray_rt_camera_box_rect(c.ctypes.data, int(image_w), int(image_h), b.ctypes.data,
-                                       r.ctypes.data)
+    x0 = np.zeros(int(image_h), np.int32)
+    x1 = np.zeros(int(image_h), np.int32)
+    k = lib().spray_rt_camera_box_rows(c.ctypes.data, int(image_w), int(image_h), b.ctypes.data,
+                                       x0.ctypes.data, x1.ctypes.data)
     if k < 0:
         raise ValueError("bad camera or box")
-    return k, r
+    return k, x0, x1
 
 
-def shadow_region(box, scene, light):
-    """(kind, box6) of spray_rt_camera_shadow_region: kind 0 = the region's
-    box, 1 = everywhere"""
-    out = np.zeros(6, np.float32)
-    k = lib().spray_rt_camera_shadow_region(
+def shadow_boxes(box, scene, light, k=16):
+    """spray_rt_camera_shadow_boxes: the slice boxes [n, 6] whose union holds
+    the hit points whose shadow ray toward `light` may cross `box` (None:
+    everywhere)"""
+    out = np.zeros((k, 6), np.float32)
+    n = lib().spray_rt_camera_shadow_boxes(
         np.ascontiguousarray(box, np.float32).ctypes.data,
         np.ascontiguousarray(scene, np.float32).ctypes.data,
-        np.ascontiguousarray(light, np.float32).ctypes.data, out.ctypes.data)
-    return k, out
+        np.ascontiguousarray(light, np.float32).ctypes.data, int(k), out.ctypes.data)
+    if n < -1:
+        raise ValueError("bad arguments")
+    return None if n < 0 else out[:n]
 
 
 def morton_partition(boxes, scene_bound, nranks, mode=PARTITION_GROUP_CLOSE):

@@ -1,8 +1,9 @@
 """The camera frame's footprints (spray_amd/csrc/footprint.cpp) are
 conservative, checked on the CPU against the oracle: every eye ray whose
-domain list holds a box lies in that box's pixel rectangle, and every hit
-point whose point-light shadow ray's list holds a box lies in the box's
-shadow region and its pixel in that region's rectangle -- on the bench
+domain list holds a box lies in that box's pixel rows (the projected hull,
+per image row), and every hit point whose point-light shadow ray's list
+holds a box lies in one of the box's shadow slices and its pixel in that
+slice's rows -- on the bench
 frame (wavelets64, 1024x1024x8spp, insitu seeds).  Also the view-aligned
 partition's counts and the degenerate cases (eye inside a box, a box
 behind the eye).  No GPU: the footprint primitives are host code of the
@@ -37,18 +38,15 @@ def test_eye_footprints_hold_every_listed_ray(oracle, frame):
     rows = np.repeat(np.arange(len(cnt)), cnt)
     dom = ids[ids >= 0]
     assert len(dom) == cnt.sum() > 1_000_000
-    area = 0
     for b in range(len(frame["boxes"])):
-        kind, r = insitu.box_rect(frame["cam"], W, H, frame["boxes"][b])
+        kind, x0, x1 = insitu.box_rows(frame["cam"], W, H, frame["boxes"][b])
         sel = rows[dom == b]
-        assert kind in (1, 2)  # every wavelet domain is in view
-        if kind == 1:
-            inside = (x[sel] >= r[0]) & (x[sel] <= r[1]) & (y[sel] >= r[2]) & (y[sel] <= r[3])
-            assert inside.all(), (b, (~inside).sum())
-            area += (r[1] - r[0] + 1) * (r[3] - r[2] + 1)
-    # the rectangles are tight: together not far beyond the listed pixels
-    listed = len(np.unique(frame["pix"][rows]))
-    assert area < 4 * listed * 8  # 64 overlapping boxes
+        assert kind == 1  # every wavelet domain is in view, in front of the eye
+        inside = (x[sel] >= x0[y[sel]]) & (x[sel] <= x1[y[sel]])
+        assert inside.all(), (b, (~inside).sum())
+        # the hull rows are tight: the box's listed pixels fill most of them
+        listed = len(np.unique(frame["pix"][sel]))
+        assert np.maximum(x1 - x0 + 1, 0).sum() < 1.6 * listed + 4 * H, b
 
 
 def test_shadow_regions_hold_every_crossing_hit(oracle, frame):
@@ -66,29 +64,34 @@ def test_shadow_regions_hold_every_crossing_hit(oracle, frame):
     pix = frame["pix"][src]
     x, y = pix % W, pix // W
     for b in range(len(boxes)):
-        kind, reg = insitu.shadow_region(boxes[b], scene, LIGHT)
-        assert kind == 0  # the light is outside the scene
+        sl = insitu.shadow_boxes(boxes[b], scene, LIGHT)
+        assert sl is not None and 0 < len(sl) <= 16  # the light is outside the scene
         sel = rows[dom == b]
         p = so[sel]
-        assert ((p >= reg[:3]) & (p <= reg[3:])).all(), b
-        k2, r = insitu.box_rect(frame["cam"], W, H, reg)
-        if k2 == 1:
-            inside = (x[sel] >= r[0]) & (x[sel] <= r[1]) & (y[sel] >= r[2]) & (y[sel] <= r[3])
-            assert inside.all(), (b, (~inside).sum())
+        in_box = np.zeros(len(sel), bool)
+        in_rows = np.zeros(len(sel), bool)
+        for q in sl:
+            in_box |= ((p >= q[:3]) & (p <= q[3:])).all(1)
+            kind, x0, x1 = insitu.box_rows(frame["cam"], W, H, q)
+            if kind == 2:
+                in_rows[:] = True
+            elif kind == 1:
+                in_rows |= (x[sel] >= x0[y[sel]]) & (x[sel] <= x1[y[sel]])
+        assert in_box.all(), (b, (~in_box).sum())
+        assert in_rows.all(), (b, (~in_rows).sum())
     # a light inside the scene: every hit point may be shadowed by any box
-    k, _ = insitu.shadow_region(boxes[0], scene, scene[:3] + 1.0)
-    assert k == 1
+    assert insitu.shadow_boxes(boxes[0], scene, scene[:3] + 1.0) is None
 
 
 def test_footprint_degenerate_cases(frame):
     from spray_amd import insitu
     cam = frame["cam"]
     eye = cam[0:3]
-    k, r = insitu.box_rect(cam, W, H, np.concatenate([eye - 1.0, eye + 1.0]))
-    assert k == 2 and list(r) == [0, W - 1, 0, H - 1]  # the eye inside the box
+    k, x0, x1 = insitu.box_rows(cam, W, H, np.concatenate([eye - 1.0, eye + 1.0]))
+    assert k == 2 and (x0 == 0).all() and (x1 == W - 1).all()  # the eye inside the box
     back = eye + (eye - np.array(BENCH_CAMERA["lookat"], np.float32)) * 2.0
-    k, _ = insitu.box_rect(cam, W, H, np.concatenate([back - 1.0, back + 1.0]))
-    assert k == 0  # wholly behind the eye
+    k, x0, x1 = insitu.box_rows(cam, W, H, np.concatenate([back - 1.0, back + 1.0]))
+    assert k == 0 and (x0 > x1).all()  # wholly behind the eye
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
