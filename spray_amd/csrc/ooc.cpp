@@ -93,8 +93,7 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   const size_t nchk = (rblk + kOocChunk - 1) / kOocChunk * size_t(64 * W);
   const size_t b_masks = align256(M * W * sizeof(uint64_t));
   const size_t b_v = align256(pairs * sizeof(uint32_t));
-  const size_t b_cnt = align256(M * sizeof(uint32_t));
-  const size_t b_wl = align256(M * kOocBatch * sizeof(uint32_t));
+  const size_t b_pk = align256(pairs * sizeof(uint64_t));
   const size_t b_blk = align256(nblk * sizeof(uint32_t));
   const size_t b_dom = align256(257 * sizeof(uint32_t));
   const size_t b_score = align256(256 * sizeof(unsigned long long));
@@ -102,10 +101,8 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   // two sets: an any-hit launch adds to one while it publishes the other
   const size_t b_dsh = align256(2 * 256 * kOocDeadShards * sizeof(uint32_t));
   const size_t total =
-      b_masks + b_v + b_cnt + b_wl + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score + b_dsh;
+      b_masks + 2 * b_v + b_pk + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score + b_dsh;
   HIPCHK(c, hipMalloc(&o->q_mem, total));
-  // the rays' pair counters start unstamped (stamps are never 0)
-  HIPCHK(c, hipMemset(static_cast<char*>(o->q_mem) + b_masks + b_v, 0, b_cnt));
   char* p = static_cast<char*>(o->q_mem);
   auto take = [&](size_t n) {
     char* r = p;
@@ -114,8 +111,8 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   };
   o->q.masks = reinterpret_cast<uint64_t*>(take(b_masks));
   o->q.val = reinterpret_cast<uint32_t*>(take(b_v));
-  o->q.rcnt = reinterpret_cast<uint32_t*>(take(b_cnt));
-  o->q.wleaf = reinterpret_cast<uint32_t*>(take(b_wl));
+  o->q.pleaf = reinterpret_cast<uint32_t*>(take(b_v));
+  o->q.pkey = reinterpret_cast<uint64_t*>(take(b_pk));
   o->q.bc = reinterpret_cast<uint32_t*>(take(b_blk));
   o->q.sb = reinterpret_cast<uint32_t*>(take(b_blk));
   o->q.off = reinterpret_cast<uint32_t*>(take(b_blk));
@@ -367,7 +364,7 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
     }
     o->drains += cur.count;
     rings[S.launch % 4] = ring;
-    const uint32_t pub = 1u;  // launch k's counts are published by launch k + 1 (lag >= 1)
+    const uint32_t pub = any_hit ? 1u : 0u;  // the publisher's offset (lag >= 1)
     if (S.launch >= uint32_t(lag) &&
         (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag + pub) % 4])))
       return r;

@@ -123,8 +123,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
     const BvhNode* __restrict__ tlas, int ntlas, const float* __restrict__ boxes, int ndom,
     const spray_rt_ray* __restrict__ rays, const uint8_t* __restrict__ valid, size_t M,
     uint32_t nrb, uint64_t* __restrict__ masks, uint64_t* __restrict__ key_init,
-    uint32_t* __restrict__ rcnt, uint8_t* __restrict__ occ_clear, uint32_t* __restrict__ bc,
-    uint32_t* __restrict__ sb) {
+    uint8_t* __restrict__ occ_clear, uint32_t* __restrict__ bc, uint32_t* __restrict__ sb) {
   __shared__ int32_t wstack[kWaves * kStack];
   __shared__ float4 stl[4 * 64 * W];
   __shared__ float sbox[6 * 64 * W];
@@ -304,10 +303,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
     if (in) {
 #pragma unroll
       for (int w = 0; w < W; ++w) masks[i * W + w] = m[w];
-      if (key_init) {  // a closest-hit pass: the key and the pair counter
-        key_init[i] = kOocMissKey;
-        rcnt[i] = 0u;
-      }
+      if (key_init) key_init[i] = kOocMissKey;
       if (occ_clear && live) occ_clear[i] = 0;
     }
     __syncthreads();
@@ -604,23 +600,14 @@ __device__ __forceinline__ void write_snapshot(uint32_t* live, uint32_t* dshard,
 // and a hit enters the ray's 64-bit key (t bits | list position | domain) by
 // atomicMin.  The key order is the sequential walk's winner rule (nearer t,
 // then the earlier list entry) and keys are unique per (ray, domain), so the
-// result is the same in any drain order and any interleaving.
-// The record (updateIntersection, trimesh_buffer.cc:328-360) is written in
-// the same launch, while the batch's domains are resident: every pair of the
-// ray in the batch (dead ones too) counts itself on the ray's counter
-// (stamped with the launch), the last one reads the ray's key and, when its
-// domain is in the batch, builds the winner's record from the winning
-// pair's triangle (wleaf, by batch slot).  A later batch with a smaller key
-// rewrites the record.  The counter's acquire-release CAS orders every
-// pair's key and triangle before the last pair's reads.
+// result is the same in any drain order and any interleaving.  The pair's
+// own key and winning triangle go to pkey / pleaf for k_ooc_ch_resolve.
 template <int W>
-__device__ __forceinline__ void ch_pair(const OocBatch& B, int s, uint32_t pj, bool valid,
+__device__ __forceinline__ void ch_pair(const OocDomain& D, uint32_t pj, bool valid,
                                         const spray_rt_ray* rays, const uint32_t* idx,
                                         const uint64_t* masks, const float* boxes,
-                                        uint64_t* key, uint32_t* rcnt, uint32_t* wleaf,
-                                        spray_rt_hit* hits, uint32_t stamp, int32_t* stack,
-                                        uint32_t* dead) {
-  const OocDomain& D = B.d[s];
+                                        uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
+                                        int32_t* stack, uint32_t* dead) {
   const uint32_t i = valid ? idx[pj] : 0u;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
   uint64_t k0 = kOocMissKey;
@@ -647,14 +634,13 @@ __device__ __forceinline__ void ch_pair(const OocBatch& B, int s, uint32_t pj, b
 #pragma unroll
   for (int w = 0; w < W; ++w) dm[w] = 0;
   if (valid) {
-    uint64_t m[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
+    uint64_t mine = kOocMissKey;
     if (best.leaf != 0xFFFFFFFFu) {
-      const uint64_t mine =
-          (uint64_t(__float_as_uint(best.t)) << 32) |
-          (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
-      wleaf[size_t(i) * kOocBatch + uint32_t(s)] = best.leaf;
+      uint64_t m[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
+      mine = (uint64_t(__float_as_uint(best.t)) << 32) |
+             (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
       const uint64_t old =
           atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
       if (mine < old) {
@@ -662,90 +648,73 @@ __device__ __forceinline__ void ch_pair(const OocBatch& B, int s, uint32_t pj, b
         if (best.t < to) death_mask<W>(m, boxes, dr, best.t, to, dm);
       }
     }
-    // this launch's pairs of the ray: its list domains in the batch
-    uint32_t expect = 0;
-    for (int k = 0; k < B.count; ++k) {
-      const int d = B.d[k].domain;
-#pragma unroll
-      for (int w = 0; w < W; ++w)
-        if (w == (d >> 6)) expect += uint32_t((m[w] >> (d & 63)) & 1ull);
-    }
-    uint32_t v = __hip_atomic_load(rcnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      const uint32_t nv = (v >> 8) == stamp ? v + 1u : ((stamp << 8) | 1u);
-      if (__hip_atomic_compare_exchange_strong(rcnt + i, &v, nv, __ATOMIC_ACQ_REL,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        v = nv;
-        break;
-      }
-    }
-    if ((v & 0xFFu) == expect) {  // the ray's last pair of the batch
-      const uint64_t kf = __hip_atomic_load(key + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int sw = -1;
-      if (kf != kOocMissKey)
-        for (int k = 0; k < B.count; ++k)
-          if (B.d[k].domain == int(kf & 0xFFFFu)) sw = k;
-      if (sw >= 0) {
-        const OocDomain& E = B.d[sw];
-        const uint32_t leaf = wleaf[size_t(i) * kOocBatch + uint32_t(sw)];
-        SlotDesc sd{};
-        sd.tris = static_cast<const float*>(E.tris);
-        sd.faces = E.faces;
-        sd.colors = E.colors;
-        sd.normals = E.normals;
-        const uint32_t prim = reinterpret_cast<const GAS uint32_t*>(gptr(E.prims))[leaf];
-        float hu, hv;
-        const float4 c = hit_uv(sd, r, o4.w, leaf, hu, hv);
-        uint32_t color;
-        float nsx, nsy, nsz;
-        epilogue(sd, prim, hu, hv, color, nsx, nsy, nsz);
-        float4* hp = reinterpret_cast<float4*>(hits + i);
-        hp[0] = make_float4(__uint_as_float(uint32_t(kf >> 32)), hu, hv, __uint_as_float(prim));
-        hp[1] = make_float4(c.y, c.z, c.w, __uint_as_float(color));
-        hp[2] = make_float4(nsx, nsy, nsz, __int_as_float(E.domain));
-      }
-    }
+    pkey[pj] = mine;
+    pleaf[pj] = best.leaf;
   }
   wave_add_deaths<W>(dm, dead);
 }
 
-// One closest-hit launch: block 0 publishes the previous launch's live
-// counts (as the any-hit launches do: its deaths in the other shard set,
-// complete at this kernel's start), the drain blocks follow, then the copy
-// blocks of the next batch's images.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
-    uint64_t* __restrict__ key, uint32_t* __restrict__ rcnt, uint32_t* __restrict__ wleaf,
-    spray_rt_hit* __restrict__ hits, uint32_t* __restrict__ dshard, uint32_t* __restrict__ live,
-    OocSnapshot S, int ndom) {
-  const size_t set = size_t(ndom) * kOocDeadShards;
-  if (blockIdx.x == 0) {
-    if (S.launch > 0) {
-      OocSnapshot P = S;
-      P.launch = S.launch - 1;
-      write_snapshot(live, dshard + ((S.launch - 1) & 1u) * set, P, ndom);
-    }
+    uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf,
+    uint32_t* __restrict__ dshard) {
+  if (blockIdx.x >= B.copy0) {
+    prefetch_copy(B, blockIdx.x);
     return;
   }
-  const uint32_t blk = blockIdx.x - 1;
-  if (blk >= B.copy0) {
-    prefetch_copy(B, blk);
-    return;
-  }
-  dshard += (S.launch & 1u) * set;
   __shared__ int32_t wstack[kWaves * kStack];
   __shared__ uint32_t dead[64 * W];
   for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
   __syncthreads();
   uint32_t pj;
   bool valid;
-  const int s = batch_pair(B, pj, valid, blk);
+  const int s = batch_pair(B, pj, valid, blockIdx.x);
   if (s >= 0)
-    ch_pair<W>(B, s, pj, valid, rays, idx, masks, boxes, key, rcnt, wleaf, hits,
-               (S.launch + 1u) & 0xFFFFFFu, wstack + (threadIdx.x >> 6) * kStack, dead);
+    ch_pair<W>(B.d[s], pj, valid, rays, idx, masks, boxes, key, pkey, pleaf,
+               wstack + (threadIdx.x >> 6) * kStack, dead);
   flush_deaths<W>(dead, dshard);
+}
+
+// Hit records of the batch's winners: the one pair whose key equals its
+// ray's minimum runs updateIntersection (trimesh_buffer.cc:328-360) while
+// its domain is still resident.  A later batch with a smaller key rewrites
+// the record.  Block 0 first publishes the batch's live counts.
+__global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
+    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
+    const uint64_t* __restrict__ key, const uint64_t* __restrict__ pkey,
+    const uint32_t* __restrict__ pleaf, spray_rt_hit* __restrict__ hits,
+    uint32_t* __restrict__ live, uint32_t* __restrict__ dshard, OocSnapshot S, int ndom) {
+  if (blockIdx.x == 0) write_snapshot(live, dshard, S, ndom);
+  uint32_t pj;
+  bool valid;
+  const int s = batch_pair(B, pj, valid, blockIdx.x);
+  if (s < 0 || !valid) return;
+  const uint64_t mine = pkey[pj];
+  if (mine == kOocMissKey) return;
+  const uint32_t i = idx[pj];
+  if (key[i] != mine) return;
+  const OocDomain& D = B.d[s];
+  const float4* rp = reinterpret_cast<const float4*>(rays + i);
+  const float4 o4 = rp[0], d4 = rp[1];
+  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+  SlotDesc sd{};
+  sd.tris = static_cast<const float*>(D.tris);
+  sd.faces = D.faces;
+  sd.colors = D.colors;
+  sd.normals = D.normals;
+  const uint32_t leaf = pleaf[pj];
+  const uint32_t prim = reinterpret_cast<const GAS uint32_t*>(gptr(D.prims))[leaf];
+  float hu, hv;
+  const float4 c = hit_uv(sd, r, o4.w, leaf, hu, hv);
+  uint32_t color;
+  float nsx, nsy, nsz;
+  epilogue(sd, prim, hu, hv, color, nsx, nsy, nsz);
+  float4* hp = reinterpret_cast<float4*>(hits + i);
+  hp[0] = make_float4(__uint_as_float(uint32_t(mine >> 32)), hu, hv, __uint_as_float(prim));
+  hp[1] = make_float4(c.y, c.z, c.w, __uint_as_float(color));
+  hp[2] = make_float4(nsx, nsy, nsz, __int_as_float(D.domain));
 }
 
 // Miss records of the rays whose key is still kOocMissKey after the last
@@ -867,10 +836,10 @@ hipError_t launch_ooc_queues(hipStream_t s, const BvhNode* tlas, int ntlas, int 
   const unsigned gm = g < kOocMaskBlocks ? g : kOocMaskBlocks;
   if (W == 1)
     k_ooc_masks<1><<<gm, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, g, q.masks,
-                                         key_init, q.rcnt, occ_clear, q.bc, q.sb);
+                                         key_init, occ_clear, q.bc, q.sb);
   else
     k_ooc_masks<4><<<gm, kBlock, 0, s>>>(tlas, ntlas, boxes, ndom, rays, valid, M, g, q.masks,
-                                         key_init, q.rcnt, occ_clear, q.bc, q.sb);
+                                         key_init, occ_clear, q.bc, q.sb);
   const unsigned nch = (g + kOocChunk - 1) / kOocChunk;
   if (size_t(ndom) * nch > q.chunk_cap) return hipErrorInvalidValue;  // the caller sizes for M
   k_ooc_chunk_sums<<<dim3(ndom, nch), kScanBlock, 0, s>>>(q.bc, q.sb, g, ndom, q.csum, q.cw);
@@ -913,15 +882,21 @@ hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
                                spray_rt_hit* hits, OocSnapshot snap) {
   if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
   const int ndom = 64 * W;
-  // block 0 publishes the previous launch's counts, then the drain blocks,
-  // then the copy blocks
-  const unsigned g = 1 + batch_grid(B) + (B.pf_count ? B.ncopy : 0);
-  if (W == 1)
-    k_ooc_ch_batch<1><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.rcnt, q.wleaf,
-                                           hits, q.dshard, q.live, snap, ndom);
-  else
-    k_ooc_ch_batch<4><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.rcnt, q.wleaf,
-                                           hits, q.dshard, q.live, snap, ndom);
+  unsigned g = batch_grid(B);
+  const unsigned gc = g + (B.pf_count ? B.ncopy : 0);
+  if (g == 0) g = 1;  // the resolve publishes even when empty
+  if (gc) {
+    if (W == 1)
+      k_ooc_ch_batch<1><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
+                                              q.pleaf, q.dshard);
+    else
+      k_ooc_ch_batch<4><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
+                                              q.pleaf, q.dshard);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, q.val, key, q.pkey, q.pleaf, hits, q.live,
+                                        q.dshard, snap, ndom);
   return hipGetLastError();
 }
 

@@ -484,13 +484,6 @@ __device__ __forceinline__ bool occluded_tree_q4(const void* nodes, const void* 
 // hit and leaves the packet; the walk ends when no lane participates.
 // wstk: kStack entries of LDS per wave.
 typedef float v16f __attribute__((ext_vector_type(16)));
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-// closest hit: the leaf's face ids fetched with its triangles (one 16-B
-// scalar load beside the three 64-B ones) instead of one dependent fetch
-// per accepted candidate
-#ifndef SPRAY_LEAF_PIDS
-#define SPRAY_LEAF_PIDS 1
-#endif
 
 template <bool ANY>
 __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tris_u,
@@ -528,11 +521,6 @@ __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tri
         // the leaf's (up to four) 48-B triangles in three scalar fetches
         const CAS v16f* tq = reinterpret_cast<const CAS v16f*>(tris_u + 48ull * first);
         const v16f t0 = tq[0], t1 = tq[1], t2 = tq[2];
-        // (the leaf's up to four ids; past the array's end the load stays
-        // inside the slot's 256-B padded allocation and is not used)
-        v4u pids = {0u, 0u, 0u, 0u};
-        if (!ANY && SPRAY_LEAF_PIDS)
-          pids = *reinterpret_cast<const CAS v4u*>(prims_u + 4ull * first);
         const float tv[48] = {t0[0], t0[1], t0[2],  t0[3],  t0[4],  t0[5],  t0[6],  t0[7],
                               t0[8], t0[9], t0[10], t0[11], t0[12], t0[13], t0[14], t0[15],
                               t1[0], t1[1], t1[2],  t1[3],  t1[4],  t1[5],  t1[6],  t1[7],
@@ -556,8 +544,7 @@ __device__ __forceinline__ void trace_tree_packet(uint64_t nodes_u, uint64_t tri
               act = false;
             }
           } else {
-            const uint32_t pid = SPRAY_LEAF_PIDS ? pids[qq]
-                                                 : reinterpret_cast<const CAS uint32_t*>(prims_u)[p];
+            const uint32_t pid = reinterpret_cast<const CAS uint32_t*>(prims_u)[p];
             if (t < best.t || (t == best.t && pid < best.prim)) {
               best.t = t;
               best.prim = pid;

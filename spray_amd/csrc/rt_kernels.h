@@ -265,8 +265,8 @@ struct OocScratch {
   unsigned long long* score;  // [256] DomainStats score per domain
   uint32_t* live;             // [256] live pairs per queue (see k_ooc_ch_batch)
   uint32_t* dshard;           // [2][256 * kOocDeadShards] deaths since the last snapshot
-  uint32_t* rcnt;             // [M] closest-hit pairs of the ray done in this launch (stamped)
-  uint32_t* wleaf;            // [M * kOocBatch] triangle (leaf order) of the ray's pair in batch slot k
+  uint64_t* pkey;             // [pair_cap] closest-hit key of each (ray, domain) pair
+  uint32_t* pleaf;            // [pair_cap] its triangle (leaf order)
   size_t block_cap;           // >= ndom * ray blocks
   size_t chunk_cap;           // >= ndom * ceil(ray blocks / kOocChunk)
   size_t pair_cap;
@@ -320,10 +320,9 @@ struct OocBatch {
   uint32_t ncopy;    // copy blocks (filled by the launcher)
 };
 constexpr int kOocCopyBlocks = 8;  // copy blocks of a launch with prefetches (default; 8 vs 16: ooc 2.88 vs 2.94 ms, r3)
-// Closest hit of a batch (traversal + key atomicMin; the last pair of a ray
-// in the batch writes the record of the batch's winner) over the queues of
-// q; boxes the domain boxes.  Pairs whose ray gets a nearer hit are counted
-// off q.live; block 0 publishes the previous launch's counts.
+// Closest hit of a batch (traversal + key atomicMin, then the winners'
+// records) over the queues of q; boxes the domain boxes.  Pairs whose ray
+// gets a nearer hit are counted off q.live; the snapshot follows.
 hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
                                const OocScratch& q, const float* boxes, uint64_t* key,
                                spray_rt_hit* hits, OocSnapshot snap);
