@@ -129,11 +129,10 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
   __shared__ float sbox[6 * 64 * W];
   __shared__ uint32_t cnt[64 * W], sc[64 * W];
   // up to 64 domains (W == 1): a lane's 16 nearest confirmed entries in
-  // registers, sorted, then packed as 16 domain bytes in list order (the
-  // per-domain sums below find a domain's position among them; LDS stays
-  // small for the latency-bound walk's occupancy); wider scenes keep
-  // kLaneList entries in LDS and look weights up by scanning them
-  // (the LDS entry lists measured the same at W == 1)
+  // registers, sorted (a slot's index is its list position; LDS stays small
+  // for the latency-bound walk's occupancy); wider scenes keep kLaneList
+  // entries in LDS and look weights up by scanning them (the LDS entry
+  // lists measured the same at W == 1)
   constexpr bool kTab = W == 1;
   __shared__ float lte[kTab ? 1 : kLaneList][kBlock];
   __shared__ int lid[kTab ? 1 : kLaneList][kBlock];
@@ -149,9 +148,6 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
     const size_t i = size_t(rb) * kBlock + threadIdx.x;
     const bool in = i < M;
     const bool live = in && (!valid || valid[i]);
-    // kTab: byte q = the q-th nearest domain of this ray block's lane (no
-    // byte survives from the previous ray block)
-    uint32_t pk[4] = {~0u, ~0u, ~0u, ~0u};
     uint64_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0;
@@ -223,7 +219,7 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
       }
     }
     // list position of each confirmed domain = its rank by (entry t, id);
-    // the DomainStats weight from the packed list (kTab) or the entry's upper half
+    // its DomainStats weight kDomainListSize - position (1 past the list)
     if constexpr (kTab) {
       // the wave's longest list bounds the unrolled loops (a scalar exit:
       // sky waves and dead slots skip them)
@@ -244,59 +240,88 @@ __global__ __launch_bounds__(kBlock, W == 1 ? SPRAY_OOC_MASK_WAVES : 1) void k_o
           sort_entries<8>(rte, rid);
         else
           sort_entries<kReg>(rte, rid);
+        // per list position a (the same weight in every lane): the lanes
+        // holding the same domain there are counted together -- coherent
+        // waves hold one or two domains per position
 #pragma unroll
-        for (int a = 0; a < kReg; ++a)
-          if (uint32_t(a) < nk)
-            pk[a >> 2] = (pk[a >> 2] & ~(0xFFu << (8 * (a & 3)))) | (uint32_t(rid[a]) << (8 * (a & 3)));
-      }
-    } else if (k <= kLaneList)
-      for (uint32_t a = 0; a < k; ++a) {
-        const float ta = lte[a][threadIdx.x];
-        const int da = lid[a][threadIdx.x] & 0xFFFF;
-        uint32_t pos = 0;
-        for (uint32_t b = 0; b < k; ++b) {
-          const float tb = lte[b][threadIdx.x];
-          pos += (tb < ta || (tb == ta && (lid[b][threadIdx.x] & 0xFFFF) < da)) ? 1u : 0u;
-        }
-        lid[a][threadIdx.x] = da | int((pos < kDomainListSize ? kDomainListSize - pos : 1u) << 16);
-      }
-    // per domain of the wave: pairs and weights summed over the wave first
-    // (a wave's rays mostly share domains: same-address LDS atomics serialise)
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint64_t u = wave_or64(m[w]);
-      while (u) {
-        const int j = __ffsll((long long)u) - 1;
-        u &= u - 1;
-        const int dom = 64 * w + j;
-        const bool has = (m[w] >> j) & 1;
-        uint32_t add = 0;
-        if (has) {
-          if constexpr (kTab) {
-            // list position = its byte among the 16 nearest (absent: past
-            // position 15, weight 1)
-            uint32_t pos = kReg;
-#pragma unroll
-            for (int q = kReg - 1; q >= 0; --q)
-              if (((pk[q >> 2] >> (8 * (q & 3))) & 0xFFu) == uint32_t(dom)) pos = uint32_t(q);
-            add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
-          } else if (k <= kLaneList) {
-            for (uint32_t a = 0; a < k; ++a) {
-              const int e = lid[a][threadIdx.x];
-              if ((e & 0xFFFF) == dom) add = uint32_t(e) >> 16;
+        for (int a = 0; a < kReg; ++a) {
+          if (uint32_t(a) >= kmax) break;
+          const int d = uint32_t(a) < nk ? rid[a] : -1;
+          const uint32_t wt = uint32_t(a) < kDomainListSize ? kDomainListSize - uint32_t(a) : 1u;
+          uint64_t todo = __ballot(d >= 0);
+          while (todo) {
+            const int dd = __builtin_amdgcn_readlane(d, __ffsll((long long)todo) - 1);
+            const uint64_t same = __ballot(d == dd);
+            todo &= ~same;
+            if ((threadIdx.x & 63) == 0) {
+              const uint32_t n = uint32_t(__popcll(same));
+              atomicAdd(&cnt[dd], n);
+              atomicAdd(&sc[dd], n * wt);
             }
-          } else {  // long list: the position from the mask
-            float te;
-            aabb_ref(sbox + 6 * dom, dr, te);
-            const uint32_t pos = list_pos<W>(m, sbox, dom, te, dr);
-            add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
           }
         }
-        const uint32_t n = uint32_t(__popcll(__ballot(has)));
-        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o);
-        if ((threadIdx.x & 63) == 0) {
-          atomicAdd(&cnt[dom], n);
-          atomicAdd(&sc[dom], add);
+        if (kmax > uint32_t(kReg)) {
+          // lists longer than kReg: the entries past the kept ones weigh 1
+          uint64_t extra = 0;
+          if (k > uint32_t(kReg)) {
+            extra = m[0];
+#pragma unroll
+            for (int q = 0; q < kReg; ++q) extra &= ~(1ull << (rid[q] & 63));
+          }
+          uint64_t u = wave_or64(extra);
+          while (u) {
+            const int j = __ffsll((long long)u) - 1;
+            u &= u - 1;
+            const uint32_t n = uint32_t(__popcll(__ballot((extra >> j) & 1ull)));
+            if ((threadIdx.x & 63) == 0) {
+              atomicAdd(&cnt[j], n);
+              atomicAdd(&sc[j], n);
+            }
+          }
+        }
+      }
+    } else {
+      if (k <= kLaneList)
+        for (uint32_t a = 0; a < k; ++a) {
+          const float ta = lte[a][threadIdx.x];
+          const int da = lid[a][threadIdx.x] & 0xFFFF;
+          uint32_t pos = 0;
+          for (uint32_t b = 0; b < k; ++b) {
+            const float tb = lte[b][threadIdx.x];
+            pos += (tb < ta || (tb == ta && (lid[b][threadIdx.x] & 0xFFFF) < da)) ? 1u : 0u;
+          }
+          lid[a][threadIdx.x] = da | int((pos < kDomainListSize ? kDomainListSize - pos : 1u) << 16);
+        }
+      // per domain of the wave: pairs and weights summed over the wave first
+      // (a wave's rays mostly share domains: same-address LDS atomics serialise)
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t u = wave_or64(m[w]);
+        while (u) {
+          const int j = __ffsll((long long)u) - 1;
+          u &= u - 1;
+          const int dom = 64 * w + j;
+          const bool has = (m[w] >> j) & 1;
+          uint32_t add = 0;
+          if (has) {
+            if (k <= kLaneList) {
+              for (uint32_t a = 0; a < k; ++a) {
+                const int e = lid[a][threadIdx.x];
+                if ((e & 0xFFFF) == dom) add = uint32_t(e) >> 16;
+              }
+            } else {  // long list: the position from the mask
+              float te;
+              aabb_ref(sbox + 6 * dom, dr, te);
+              const uint32_t pos = list_pos<W>(m, sbox, dom, te, dr);
+              add = pos < kDomainListSize ? kDomainListSize - pos : 1u;
+            }
+          }
+          const uint32_t n = uint32_t(__popcll(__ballot(has)));
+          for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o);
+          if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&cnt[dom], n);
+            atomicAdd(&sc[dom], add);
+          }
         }
       }
     }
