@@ -186,6 +186,8 @@ def lib():
                 "(there is no CPU fallback)" % LIB_PATH)
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("SPRAY_RT_LIB") and not hasattr(L, name):
+                continue  # an A/B build that predates the symbol (never the in-tree library)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
