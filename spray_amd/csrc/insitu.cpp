@@ -127,12 +127,14 @@ struct InsituTransport {
   virtual bool has_rep() const { return true; }
   virtual int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) = 0;
   virtual int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) = 0;
-  // split keys: MIN of u32 t bits (src -> dst; in place when equal); MIN of
-  // u8 list positions on stream st (overlapping the main stream's work; the
-  // host form runs it in order)
+  // split keys: MIN of u32 t bits (src -> dst; in place when equal) and of
+  // u8 list positions, on stream st (RCCL: overlapping the other streams'
+  // work; the host form runs them in order, blocking); off = the slots'
+  // first index in the frame's U (the replay's captured arrays)
   virtual int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
-                                size_t n) = 0;
-  virtual int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t st) = 0;
+                                size_t n, size_t off, hipStream_t st) = 0;
+  virtual int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t off,
+                               hipStream_t st) = 0;
   // rehearsal only: the rank's device work runs while it holds a lock
   // shared by the group's processes (SPRAY_INSITU_SERIAL), so the phase
   // timings of ranks sharing one GPU are not inflated by each other
@@ -293,13 +295,14 @@ struct RcclTransport : InsituTransport {
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclSum, comm, stream_of(I->ctx)),
                "ncclAllReduce(sum u8)");
   }
-  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
-                        size_t n) override {
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
+                        size_t, hipStream_t st) override {
     ++I->st[4];
-    return chk(I, nccl().AllReduce(src, dst, n, ncclUint32, ncclMin, comm, stream_of(I->ctx)),
+    return chk(I, nccl().AllReduce(src, dst, n, ncclUint32, ncclMin, comm, st),
                "ncclAllReduce(min u32)");
   }
-  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t st) override {
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t,
+                       hipStream_t st) override {
     ++I->st[4];
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclMin, comm, st),
                "ncclAllReduce(min u8)");
@@ -327,9 +330,10 @@ struct ReplayTransport : InsituTransport {
     if (bytes) HIPCHK(I->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
     return SPRAY_RT_OK;
   }
-  int need(spray_rt_insitu* I, size_t m) {
-    if (!tmin || m != n)
-      return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu slots given, the frame has %zu", n, m);
+  int need(spray_rt_insitu* I, size_t m, size_t off) {
+    if (!tmin || off + m > n || I->last_nu != n)
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu slots given, the frame has %zu", n,
+                  I->last_nu);
     return SPRAY_RT_OK;
   }
   int counts(spray_rt_insitu* I, const int64_t*, int64_t*, int64_t*) override {
@@ -354,13 +358,15 @@ struct ReplayTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t*, uint32_t* dst, size_t m) override {
-    CALL(need(I, m));
-    return copy(I, dst, tmin, m * 4, stream_of(I->ctx));
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t*, uint32_t* dst, size_t m,
+                        size_t off, hipStream_t st) override {
+    CALL(need(I, m, off));
+    return copy(I, dst, tmin + off, m * 4, st);
   }
-  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t m, hipStream_t st) override {
-    CALL(need(I, m));
-    return copy(I, dev, lpmin, m, st);
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t m, size_t off,
+                       hipStream_t st) override {
+    CALL(need(I, m, off));
+    return copy(I, dev, lpmin + off, m, st);
   }
   bool side_stream() const override { return true; }
 };
@@ -413,34 +419,34 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  // the narrow MINs through the 64-bit host callback (widened on the host)
+  // the narrow MINs through the 64-bit host callback (widened on the host),
+  // staged on the stream that produced them
   template <typename T>
-  int min_widened(spray_rt_insitu* I, T* dev, size_t n) {
+  int min_widened(spray_rt_insitu* I, T* dev, size_t n, hipStream_t st) {
     std::vector<T> h(std::max<size_t>(n, 1));
     std::vector<unsigned long long> w(std::max<size_t>(n, 1));
-    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost,
-                                  stream_of(I->ctx)));
-    CALL(sync(I));
+    HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost, st));
+    HIPCHK(I->ctx, hipStreamSynchronize(st));
     for (size_t k = 0; k < n; ++k) w[k] = h[k];
     serial_end();
     const int bad = cb.allreduce_min_u64(cb.user, w.data(), n);
     serial_begin();
     if (bad) return fail(I->ctx, SPRAY_RT_ERR_STATE, "host transport: min all-reduce failed");
     for (size_t k = 0; k < n; ++k) h[k] = T(w[k]);
-    HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * sizeof(T), hipMemcpyHostToDevice,
-                                  stream_of(I->ctx)));
-    CALL(sync(I));
+    HIPCHK(I->ctx, hipMemcpyAsync(dev, h.data(), n * sizeof(T), hipMemcpyHostToDevice, st));
+    HIPCHK(I->ctx, hipStreamSynchronize(st));
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
-                        size_t n) override {
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
+                        size_t, hipStream_t st) override {
     if (src != dst && n)
-      HIPCHK(I->ctx, hipMemcpyAsync(dst, src, n * 4, hipMemcpyDeviceToDevice, stream_of(I->ctx)));
-    return min_widened(I, dst, n);
+      HIPCHK(I->ctx, hipMemcpyAsync(dst, src, n * 4, hipMemcpyDeviceToDevice, st));
+    return min_widened(I, dst, n, st);
   }
-  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, hipStream_t) override {
-    return min_widened(I, dev, n);
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t,
+                       hipStream_t st) override {
+    return min_widened(I, dev, n, st);
   }
   int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
              int64_t* h_recv) override {
@@ -1049,7 +1055,7 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
   if (split) {
-    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, tk, nc));
+    if (nc) COMM(I->tr->allreduce_min_u32(I, tk, tk, nc, 0, s));
     MARK(3);
     GROW(I->rlp, nc + 1);
     lp = I->rlp.as<uint8_t>();
@@ -1061,9 +1067,9 @@ int trace_replicated(spray_rt_insitu* I, const spray_rt_shader* P, const spray_r
       if (I->tr->side_stream()) {
         HIPCHK(c, hipEventRecord(I->ev_lp0, s));
         HIPCHK(c, hipStreamWaitEvent(I->cs, I->ev_lp0, 0));
-        CALL(I->tr->allreduce_min_u8(I, lp, nc, I->cs));
+        CALL(I->tr->allreduce_min_u8(I, lp, nc, 0, I->cs));
       } else {
-        COMM(I->tr->allreduce_min_u8(I, lp, nc, s));
+        COMM(I->tr->allreduce_min_u8(I, lp, nc, 0, s));
       }
       HIPCHK(c, hipEventRecord(I->ev_lp1, I->cs));
     }
@@ -1414,7 +1420,7 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
   if (split) {
-    if (nu) COMM(I->tr->allreduce_min_u32(I, tk, tmin, nu));
+    if (nu) COMM(I->tr->allreduce_min_u32(I, tk, tmin, nu, 0, s));
     MARK(3);
     lp = I->rlp.as<uint8_t>();
     HIPCHK(c, hipMemsetAsync(lp, 0xFF, nu, s));
@@ -1426,9 +1432,9 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
       if (I->tr->side_stream()) {
         HIPCHK(c, hipEventRecord(I->ev_lp0, s));
         HIPCHK(c, hipStreamWaitEvent(I->cs, I->ev_lp0, 0));
-        CALL(I->tr->allreduce_min_u8(I, lp, nu, I->cs));
+        CALL(I->tr->allreduce_min_u8(I, lp, nu, 0, I->cs));
       } else {
-        COMM(I->tr->allreduce_min_u8(I, lp, nu, s));
+        COMM(I->tr->allreduce_min_u8(I, lp, nu, 0, s));
       }
       HIPCHK(c, hipEventRecord(I->ev_lp1, I->cs));
     }
