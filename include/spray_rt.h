@@ -676,7 +676,7 @@ int spray_rt_insitu_trace_frame(spray_rt_insitu_t ins, const spray_rt_shader* sh
  * the whole image_w x image_h x spp image as one blocking tile
  * (insitu::genMultiSampleEyeRays, insitu_ray.h:103-182; the rays, pixel and
  * sample ids spray_rt_eye_rays_insitu writes for tile = stripe = image),
- * generated in the lanes from cam (spray_rt_camera_init's 14 floats, for
+ * generated in the lanes from cam (spray_camera_init's 14 floats, for
  * that image size) -- no ray buffer.  Each rank's work follows its own
  * domains instead of the frame: the pixels whose eye rays may enter one of
  * its resident domain boxes (the boxes' conservative screen footprints) are
