@@ -1411,11 +1411,17 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   HIPCHK(c, hipMemsetAsync(tk, 0xFF, nu * 4, s));
   if (!split) HIPCHK(c, launch_fill_u64(s, keys, nu, kInsituMissKey));
   if (rec) HIPCHK(c, hipMemsetAsync(I->rwin.p, 0, nu, s));
+  // a rank with few domains tests their boxes in the lanes instead of the
+  // top-level walk (the list positions then computed for its winners only)
+  int nres = 0;
+  for (int v : c->dom2slot) nres += v >= 0 ? 1 : 0;
+  const bool direct = nres <= kDirectRes;
+  const bool defer = split && direct;
   // ---- own keyed closest hits + shading over E (results at U slots)
   MARK(2);
   HIPCHK(c, launch_scene_cam_keyed(s, view(c), F, I->te, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
-                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>()));
+                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>(), defer));
   // ---- the group's minimum t of every U slot (then the list position)
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
@@ -1424,7 +1430,8 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
     MARK(3);
     lp = I->rlp.as<uint8_t>();
     HIPCHK(c, hipMemsetAsync(lp, 0xFF, nu, s));
-    HIPCHK(c, launch_cam_lp(s, I->te, spp, keys, tk, tmin, lp));
+    HIPCHK(c, launch_cam_lp(s, I->te, spp, keys, tk, tmin, lp, defer ? &F : nullptr,
+                            c->d_boxes, c->d_tlas, c->ntlas));
     if (nu) {
       if (!I->cs) HIPCHK(c, hipStreamCreateWithFlags(&I->cs, hipStreamNonBlocking));
       if (!I->ev_lp0) HIPCHK(c, hipEventCreateWithFlags(&I->ev_lp0, hipEventDisableTiming));
@@ -1449,7 +1456,8 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   // ---- the shadow ray of every hit in S from the minimum t, own any hit
   MARK(4);
   HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nu, s));
-  HIPCHK(c, launch_scene_cam_shadows(s, view(c), F, I->ts, tmin, shade10, I->rocc.as<uint8_t>()));
+  HIPCHK(c, launch_scene_cam_shadows(s, view(c), F, I->ts, tmin, shade10, I->rocc.as<uint8_t>(),
+                                     direct));
   // ---- the winners among E's slots, their shadows counted
   MARK(5);
   HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, kWinCounterBytes, s));

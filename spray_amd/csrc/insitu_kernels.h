@@ -86,9 +86,14 @@ hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* t
                           uint8_t* win, uint8_t* svw, unsigned long long* nshadow);
 // ---- replicated PT frames from the camera (trace_camera): passes over the
 // rank's eye table T, the shared arrays addressed by U slot (rt_kernels.h)
-// lp[u] = own list position where own t bits tk[u] == tmin[u] (lp prefilled 0xFF)
-hipError_t launch_cam_lp(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
-                        const uint32_t* tk, const uint32_t* tmin, uint8_t* lp);
+// lp[u] = own list position where own t bits tk[u] == tmin[u] (lp prefilled
+// 0xFF); defer (the keyed launch's defer_lp): the position computed here on
+// the regenerated eye ray (the domain boxes and the top-level tree over them)
+// and written into the key
+hipError_t launch_cam_lp(hipStream_t s, const CamTable& T, int spp, uint64_t* keys,
+                        const uint32_t* tk, const uint32_t* tmin, uint8_t* lp,
+                        const CamFrame* defer, const float* boxes, const BvhNode* tlas,
+                        int ntlas);
 // win / svw at u as launch_rep_win (own t bits tk: 0xFFFFFFFF = no own hit)
 hipError_t launch_cam_win(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
                          const uint32_t* tk, const uint32_t* tmin, const uint8_t* lpmin,

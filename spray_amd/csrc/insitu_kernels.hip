@@ -581,18 +581,94 @@ __global__ __launch_bounds__(kBlock) void k_rep_win(const uint64_t* __restrict__
 // (memsets: t bits 0xFFFFFFFF = no hit, list positions 0xFF, occlusion 0).
 // lp[u] = this rank's list position of its hit where its t is the group's
 // minimum
+// Deferred list positions (the keyed launch tested only the rank's boxes):
+// the position of the own hit's domain d in the ray's sorted list -- the
+// number of domains whose box the ray enters before d's (entry t, then id:
+// the keyed epilogue's count, the same exact box tests) -- for the slots
+// where the own t is the group's minimum, written to lp and into the key.
+// The winners of a wave walk the top-level tree together (nodes by scalar
+// fetch, a wave-uniform stack), an inner node only when some lane may enter
+// it before its own domain.
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ uint32_t list_pos_wave(uint64_t tlas_u, int32_t* wstk, const Ray& r,
+                                                  const DRay& dr, float tb, int bd) {
+  const __attribute__((address_space(4))) v16f_t* nodes =
+      reinterpret_cast<const __attribute__((address_space(4))) v16f_t*>(tlas_u);
+  const float tcut = tb > 0.f ? tb : kInf;  // tb * kTfarSlack < tb below 0
+  uint32_t p = 0;
+  int sp = 0;
+  int32_t cur = 0;
+  for (;;) {
+    const v16f_t n = nodes[cur];
+    const int32_t cl = __builtin_amdgcn_readfirstlane(__float_as_int(n[12]));
+    const int32_t cr = __builtin_amdgcn_readfirstlane(__float_as_int(n[13]));
+    int32_t next = kNone;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int32_t c = k ? cr : cl;
+      if (c == INT_MIN) continue;
+      float b6[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) b6[q] = n[6 * k + q];
+      float tm;
+      if (c < 0) {
+        const int b = int(~uint32_t(c) >> 2);
+        if (aabb_ref6(b6[0], b6[1], b6[2], b6[3], b6[4], b6[5], dr, tm) &&
+            (tm < tb || (tm == tb && b < bd)))
+          ++p;
+      } else if (__ballot(slab(r, b6[0], b6[1], b6[2], b6[3], b6[4], b6[5], -kInf, tcut, tm))) {
+        if (next == kNone) {
+          next = c;
+        } else {
+          wstk[sp] = c;
+          ++sp;
+        }
+      }
+    }
+    if (next == kNone) {
+      if (sp == 0) break;
+      --sp;
+      next = __builtin_amdgcn_readfirstlane(wstk[sp]);
+    }
+    cur = next;
+  }
+  return p;
+}
+
 __global__ __launch_bounds__(kBlock) void k_cam_lp(CamTable T, int spp,
-                                                   const uint64_t* __restrict__ keys,
+                                                   uint64_t* __restrict__ keys,
                                                    const uint32_t* __restrict__ tk,
                                                    const uint32_t* __restrict__ tmin,
-                                                   uint8_t* __restrict__ lp) {
+                                                   uint8_t* __restrict__ lp, int defer, Cam cam,
+                                                   int cam_w, const float* __restrict__ boxes,
+                                                   const BvhNode* __restrict__ tlas, int ntlas) {
+  __shared__ int32_t wstack[(kBlock / 64) * kStack];
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= size_t(T.npix) * uint32_t(spp)) return;
-  int x, y, s;
-  size_t u;
-  cam_item(T, spp, j, x, y, s, u);
-  const uint32_t t = tk[u];
-  if (t != 0xFFFFFFFFu && t == tmin[u]) lp[u] = uint8_t((keys[u] >> 16) & 0xFFu);
+  bool win = false;
+  size_t u = 0;
+  int x = 0, y = 0, s = 0;
+  if (j < size_t(T.npix) * uint32_t(spp)) {
+    cam_item(T, spp, j, x, y, s, u);
+    const uint32_t t = tk[u];
+    win = t != 0xFFFFFFFFu && t == tmin[u];
+  }
+  if (!win) return;
+  uint64_t key = keys[u];
+  if (defer && ntlas > 0) {
+    float fx, fy, d[3];
+    insitu_jitter(cam_w, spp, x, y, s, fx, fy);
+    cam_dir(cam, fx, fy, d);
+    const Ray r = make_ray(cam.p[0], cam.p[1], cam.p[2], d[0], d[1], d[2]);
+    const DRay dr = make_dray(cam.p[0], cam.p[1], cam.p[2], d[0], d[1], d[2]);
+    const int bd = int(key & 0xFFFFu);
+    float tb;
+    aabb_ref(boxes + 6 * bd, dr, tb);
+    const uint32_t p = list_pos_wave(reinterpret_cast<uint64_t>(tlas),
+                                     wstack + (threadIdx.x >> 6) * kStack, r, dr, tb, bd);
+    key = (key & ~(0xFFFFull << 16)) | (uint64_t(p) << 16);
+    keys[u] = key;
+  }
+  lp[u] = uint8_t((key >> 16) & 0xFFu);
 }
 
 // the winners among the rank's slots (as k_rep_win): win / svw at u
@@ -857,9 +933,16 @@ hipError_t launch_rep_win(hipStream_t s, const uint64_t* keys, const uint32_t* t
                           uint8_t* win, uint8_t* svw, unsigned long long* nshadow) {
   LAUNCH(nc, k_rep_win, keys, tmin, lpmin, kmin, sv, nc, win, svw, nshadow);
 }
-hipError_t launch_cam_lp(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
-                        const uint32_t* tk, const uint32_t* tmin, uint8_t* lp) {
-  LAUNCH(size_t(T.npix) * uint32_t(spp), k_cam_lp, T, spp, keys, tk, tmin, lp);
+hipError_t launch_cam_lp(hipStream_t s, const CamTable& T, int spp, uint64_t* keys,
+                        const uint32_t* tk, const uint32_t* tmin, uint8_t* lp,
+                        const CamFrame* defer, const float* boxes, const BvhNode* tlas,
+                        int ntlas) {
+  if (defer && (!boxes || !tlas)) return hipErrorInvalidValue;
+  Cam cam{};
+  if (defer)
+    for (int k = 0; k < 14; ++k) cam.p[k] = defer->cam[k];
+  LAUNCH(size_t(T.npix) * uint32_t(spp), k_cam_lp, T, spp, keys, tk, tmin, lp, defer ? 1 : 0,
+         cam, defer ? defer->image_w : 0, boxes, tlas, ntlas);
 }
 hipError_t launch_cam_win(hipStream_t s, const CamTable& T, int spp, const uint64_t* keys,
                          const uint32_t* tk, const uint32_t* tmin, const uint8_t* lpmin,

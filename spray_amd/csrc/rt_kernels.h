@@ -207,6 +207,9 @@ struct CamTable {
   const uint32_t* first;
   uint32_t nruns, npix;
 };
+// resident domains up to which the camera launches test a lane's boxes
+// directly instead of walking the top-level tree
+constexpr int kDirectRes = 32;
 struct CamFrame {
   float cam[14];  // camera_init's record (eye, image-plane corner, u / v axes, w, h)
   int image_w, spp;
@@ -214,15 +217,19 @@ struct CamFrame {
 // keyed closest hit + point-light shading of the eye rays of table T's
 // pixels, generated in the lanes (k_eye_rays_insitu's operations), culled by
 // the resident boxes; results at their U slots (slots of dropped lanes
-// untouched)
+// untouched).  defer_lp (split keys, at most kDirectRes resident domains):
+// a lane tests the resident boxes instead of walking the top-level tree,
+// and the keys' list-position byte stays 0 for launch_cam_lp
 hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFrame& F,
                                   const CamTable& T, const float* shade10, spray_rt_hit* hits,
-                                  uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv);
+                                  uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv,
+                                  bool defer_lp);
 // any hit of the point-light shadow ray of every hit in T's pixels (t bits
-// tmin[u]; none: 0xFFFFFFFF), the eye ray regenerated in the lane
+// tmin[u]; none: 0xFFFFFFFF), the eye ray regenerated in the lane; direct:
+// the resident boxes tested instead of the top-level walk (<= kDirectRes)
 hipError_t launch_scene_cam_shadows(hipStream_t s, const SceneView& v, const CamFrame& F,
                                     const CamTable& T, const uint32_t* tmin,
-                                    const float* shade10, uint8_t* occ);
+                                    const float* shade10, uint8_t* occ, bool direct);
 // any hit of those pairs' AO rays, each generated in its any-hit lane;
 // idx (optional): only pairs idx[0..*d_count) (occ written at idx[j])
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,

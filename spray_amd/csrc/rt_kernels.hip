@@ -273,6 +273,10 @@ struct SceneArgs {
   CamTable cam_tab;
   Cam cam;
   int cam_w, cam_spp;
+  // camera frames of a rank holding few domains: a lane's domain list is its
+  // test of the rank's resident boxes (no top-level walk); keyed launches
+  // leave the list-position byte of the key 0 (launch_cam_lp fills it in)
+  int direct_res;
 };
 
 // Packet path ray loads / hit stores: 1 = non-temporal, so the 671 MB of
@@ -609,7 +613,8 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
                                                  const float4* sdom, int32_t* wstk,
                                                  bool& spawn, float* pos, float* wi,
                                                  const float* rin = nullptr,
-                                                 const Post& post = Post()) {
+                                                 const Post& post = Post(),
+                                                 const uint8_t* sres = nullptr, int nres = 0) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int lane = threadIdx.x & 63;
@@ -641,7 +646,23 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   uint64_t m[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) m[w] = 0;
-  if (valid) tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
+  const bool direct = sres && A.direct_res;  // wave-uniform
+  if (valid && direct) {
+    // exactly the mask's resident bits: tlas_mask_wave's leaf test is this
+    // intersectAabb on the same box
+    const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
+    for (int k = 0; k < nres; ++k) {
+      const int d = int(sres[k]);
+      float tm;
+      if (aabb_ref(sbox + 6 * d, dr, tm)) {
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (w == (d >> 6)) m[w] |= 1ull << (d & 63);
+      }
+    }
+  } else if (valid) {
+    tlas_mask_wave<W>(stl, A.ntlas, wstk, r, o4, d4, m);
+  }
   constexpr bool kKeys = EPI == kEpiKeys || EPI == kEpiKeysShade;
   uint64_t m0[kKeys ? W : 1];
   if (kKeys) {
@@ -794,7 +815,9 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   if (!valid) return;
   if (kKeys) {
     uint64_t key = 0x7FFFFFFFFFFFFFFFull;
-    if (best_dom >= 0) {  // position of best_dom in the ray's sorted list
+    if (best_dom >= 0 && direct) {  // the position is filled in by launch_cam_lp
+      key = (uint64_t(__float_as_uint(best.t)) << 32) | uint64_t(best_dom);
+    } else if (best_dom >= 0) {  // position of best_dom in the ray's sorted list
       const DRay dr = make_dray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
       float tb;
       aabb_ref(sbox + 6 * best_dom, dr, tb);
@@ -1142,7 +1165,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
       size_t at;
       const bool okr = rep_ray<EPI>(A, j, i, ok, j < M, at, r6, sbox, sres, nres);
       scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
-          A, at, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6);
+          A, at, okr, stl, sbox, sdom, wstk, flag, pos, wi, r6, NoPost(), sres, nres);
     } else if (kPacket && (!kAdaptive || wave_coherent(A, i, ok)))
       scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
     else if (ok)
@@ -1196,7 +1219,8 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
                 rep_epi(EPI) ? r6 : nullptr,
                 [&]() {
                   if (last && lane == 0) next = atomicAdd(head, csz);
-                });
+                },
+                rep_epi(EPI) ? sres : nullptr, kRes ? nres : 0);
           } else if (kPacket && wave_coherent(A, i, ok)) {
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           } else if (ok) {
@@ -2462,9 +2486,11 @@ static SceneArgs cam_args(const SceneView& v, const CamFrame& F, const CamTable&
 
 hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFrame& F,
                                   const CamTable& T, const float* shade10, spray_rt_hit* hits,
-                                  uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv) {
+                                  uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv,
+                                  bool defer_lp) {
   if (T.npix == 0) return hipSuccess;
   SceneArgs a = cam_args(v, F, T);
+  a.direct_res = defer_lp ? 1 : 0;
   a.hits = hits;
   a.keys = keys;
   a.tkeys = tkeys;
@@ -2476,9 +2502,10 @@ hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFr
 
 hipError_t launch_scene_cam_shadows(hipStream_t s, const SceneView& v, const CamFrame& F,
                                     const CamTable& T, const uint32_t* tmin,
-                                    const float* shade10, uint8_t* occ) {
+                                    const float* shade10, uint8_t* occ, bool direct) {
   if (T.npix == 0) return hipSuccess;
   SceneArgs a = cam_args(v, F, T);
+  a.direct_res = direct ? 1 : 0;
   a.tmin = tmin;
   a.occ = occ;
   a.shade = shade_from10(shade10);

@@ -100,26 +100,30 @@ LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3,
 
 
 def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, replicated=False,
-                 mode=0):
+                 mode=0, scene=None, owner=None):
     """One rank's engine frame of CASES[case]: returns (records, totals, image).
     one_owner: the last rank owns every domain (the others hold rays only).
     replicated: spray_rt_insitu_trace_frame with every eye ray on every rank
     (True) or spray_rt_insitu_trace_camera ("camera": the rays generated in
-    the lanes); mode: the partition (GROUP_CLOSE / ROUND_ROBIN / VIEW)."""
+    the lanes); mode: the partition (GROUP_CLOSE / ROUND_ROBIN / VIEW);
+    scene / owner: another scene file (meshes from SCENES) and its owners."""
     import spray_amd
     from spray_amd import insitu
     from oracle import pyoracle as po
     from test_insitu import scene_boxes
     kind, bounces, samples, img, spp = CASES[case]
-    boxes, bound = scene_boxes()
     c = H.BENCH_CAMERA
     cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
-    owner = insitu.partition(boxes, bound, world, mode, cam)
+    scene = scene or WAVELETS64
+    if owner is None:
+        boxes, bound = scene_boxes()
+        owner = insitu.partition(boxes, bound, world, mode, cam)
+    owner = np.asarray(owner, np.int32)
     if one_owner:
         owner = np.full_like(owner, world - 1)
     rt = spray_amd.RtContext(0)
-    insitu.setup_rank_context(rt, WAVELETS64, SCENES, owner, rank)
-    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
+    insitu.setup_rank_context(rt, scene, SCENES, owner, rank)
+    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(scene))
     rt.set_stream(torch.cuda.current_stream())
     block = (0, 0, img, img)
     stripe = block if replicated else insitu.horizontal_stripe(world, rank, block)
@@ -215,7 +219,8 @@ def test_engine_one_rank_protocol_forced(oracle, monkeypatch):
     assert res[3]["exchanges"] > 0
 
 
-def _gpu_rank_main(rank, world, port, out, case, one_owner=False, replicated=False, mode=0):
+def _gpu_rank_main(rank, world, port, out, case, one_owner=False, replicated=False, mode=0,
+                   scene=None, owner=None):
     import pickle
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -225,7 +230,8 @@ def _gpu_rank_main(rank, world, port, out, case, one_owner=False, replicated=Fal
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _engine_rank(rank, world, case, "host", dist, one_owner, replicated, mode)
+        res = _engine_rank(rank, world, case, "host", dist, one_owner, replicated, mode, scene,
+                           owner)
         with open(os.path.join(out, "r%d.pkl" % rank), "wb") as fh:
             pickle.dump(res, fh)
     finally:
@@ -335,6 +341,64 @@ def test_engine_camera_frame_ranks(oracle, world, mode, case, monkeypatch):
     for r in res:
         assert r[3]["exchanges"] == 0 and r[3]["host_count_reads"] == 0
     assert all(not r[2].any() for r in res[1:]) and res[0][2].any()
+
+
+TIE_DOMAINS = [  # (bound lo, bound hi, translate): wavelet.ply copies
+    ((-10, -10, -10), (10, 9.324713, 10), (0, 0, 0)),
+    ((-15, -15, -15), (15, 14.324713, 15), (0, 0, 0)),  # the same mesh, a wider box
+    ((-10, -10, -10), (10, 9.324713, 10), (20, 0, 0)),
+    ((-10, -10, -10), (10, 9.324713, 10), (20, 0, 0)),  # the same mesh, the same box
+]
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_engine_camera_frame_cross_rank_ties(oracle, split, monkeypatch, tmp_path):
+    """Exact t ties between ranks: domains 0 / 1 hold the same mesh in a
+    tight and a wider box, domains 2 / 3 the same mesh in the same box, and
+    each pair is split over the two ranks.  The sequential walk keeps the
+    earlier list entry -- domain 1 (its wider box is entered first) and
+    domain 2 (equal entry, smaller id) -- so the list positions decide the
+    winner (the camera frame computes them for a rank's winners only, after
+    testing the rank's boxes directly); the 64-bit key MIN as well."""
+    import pickle
+    lines = ["light point 0 500 1000 1 1 1", ""]
+    for lo, hi, tr in TIE_DOMAINS:
+        lines += ["domain", "file wavelet.ply", "mtl diffuse 1 1 1",
+                  "bound %f %f %f %f %f %f" % (lo + hi), "face 5480", "vertex 2840",
+                  "translate %f %f %f" % tr, ""]
+    scene = str(tmp_path / "ties.spray")
+    with open(scene, "w") as fh:
+        fh.write("\n".join(lines))
+    if not split:
+        monkeypatch.setenv("SPRAY_INSITU_SPLIT_KEYS", "0")
+    owner = [0, 1, 1, 0]
+    with tempfile.TemporaryDirectory() as out:
+        torch.multiprocessing.spawn(_gpu_rank_main,
+                                    args=(2, _free_port(), out, "pt1", False, "camera", 0,
+                                          scene, owner),
+                                    nprocs=2)
+        res = []
+        for r in range(2):
+            with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
+                res.append(pickle.load(fh))
+    kind, bounces, samples, img, spp = CASES["pt1"]
+    c = H.BENCH_CAMERA
+    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    _, doms, _ = oracle.load_scene(scene, SCENES)
+    sh = H.insitu_shader(oracle, kind, bounces, samples)
+    ref, _, ref_tot = H.reference_frame(oracle, sh, oracle.scene_bsdfs(doms), cam, img, img, spp,
+                                        (0, 0, img, img), desc=scene)
+    merged = []
+    for recs, tot, _, _ in res:
+        assert tot == ref_tot
+        d = H.records_dict(recs)
+        merged += [(b, s) + v for (b, s), v in d.items()]
+    got = H.records_dict(merged)
+    H.compare_records(got, ref)
+    # both kinds of tie occurred, and went to the earlier list entry
+    dom = np.array([np.frombuffer(v[0], np.int32)[11] for v in ref.values()])
+    assert (dom == 1).sum() > 100 and (dom == 2).sum() > 100
+    assert not ((dom == 0) | (dom == 3)).any()
 
 
 @pytest.mark.parametrize("case", ["pt1", "ao16", "pt1-u64"])
