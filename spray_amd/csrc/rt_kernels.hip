@@ -63,6 +63,12 @@ constexpr size_t kPersistAhRays = size_t(16) << 20;  // any-hit batches this lar
 #ifndef SPRAY_WAVES_CH
 #define SPRAY_WAVES_CH 6
 #endif
+// the keyed closest hit + shading of in-situ frames (5 / 4 waves per SIMD:
+// rank launches at N = 8 0.185 / 0.188 vs 0.195 ms, at N = 2 0.319 / 0.328
+// vs 0.311 ms -- within the run-to-run spread)
+#ifndef SPRAY_WAVES_KEYED
+#define SPRAY_WAVES_KEYED 6
+#endif
 #ifndef SPRAY_WAVES_SHADOW
 #define SPRAY_WAVES_SHADOW 6
 #endif
@@ -1094,6 +1100,7 @@ template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN : SPRAY_WAVES_AH)
                                      : (W == 1 && STK == 16
                                             ? (EPI == kEpiShadow || EPI == kEpiShadowFrame ? SPRAY_WAVES_SHADOW
+                                               : EPI == kEpiKeysShade ? SPRAY_WAVES_KEYED
                                                                  : SPRAY_WAVES_CH)
                                             : 1)) void k_scene(
     SceneArgs A) {
@@ -1127,7 +1134,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
     M = dc < M ? dc : M;
   }
   const size_t S = band_size(M);
-  for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
+  // (camera launches testing the resident boxes directly never walk it)
+  if (!(rep_epi(EPI) && A.direct_res))
+    for (int k = threadIdx.x; k < 4 * A.ntlas; k += kBlock) stl[k] = ld4(A.tlas, k);
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   for (int k = threadIdx.x; k < A.ndom; k += kBlock) sdom[k] = ld4(A.domtrav, k);
   // replicated frames: the resident domains, whose boxes cull the lanes
