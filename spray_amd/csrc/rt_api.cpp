@@ -1081,7 +1081,7 @@ int spray_rt_spawn_shadows_pt(spray_rt_ctx_t c, const spray_rt_ray* rays,
   HIPCHK(c, hipSetDevice(c->device));
   size_t nb = (M + kBlock - 1) / kBlock + 1;
   void* bc = c->d_block_counts;
-  int r = ensure(c, &bc, &c->block_cap, nb * sizeof(uint32_t));
+  int r = ensure(c, &bc, &c->block_cap, nb * sizeof(unsigned long long));
   if (r) return r;
   c->d_block_counts = static_cast<uint32_t*>(bc);
   HIPCHK(c, launch_spawn_pt(stream_of(c), rays, hits, M, shade, out_rays,

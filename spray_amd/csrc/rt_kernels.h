@@ -146,13 +146,14 @@ hipError_t launch_eye_rays_ooc_tiles(hipStream_t s, const float* cam14, int imag
                                     const int* tiles, int ntiles, spray_rt_ray* rays,
                                     int32_t* pixid, int32_t* samid);
 
-// Deterministic (ascending source index) compaction of PT shadow rays.
-// block_counts: device scratch of ceil(M/kBlock) + 1 uint32.
+// Deterministic (ascending source index) compaction of PT shadow rays, in
+// one pass (decoupled look-back).  scratch: device memory of
+// (ceil(M/kBlock) + 1) uint64.
 hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
                            const spray_rt_hit* hits, size_t M,
                            const float* shade10, spray_rt_ray* out_rays,
                            int32_t* out_src, uint32_t* d_count,
-                           uint32_t* block_counts);
+                           void* scratch);
 
 // Ambient-occlusion rays of ooc::ShaderAo, nsamples per hit, compacted in
 // (source ray, sample) order; scratch: ao_scratch_bytes(M, nsamples) of

@@ -1426,20 +1426,6 @@ __device__ __forceinline__ uint32_t block_prefix(bool flag, uint32_t& total) {
   return before + in_wave;
 }
 
-__global__ __launch_bounds__(kBlock) void k_spawn_pt_count(
-    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
-    size_t M, ShadePt sh, uint32_t* __restrict__ block_counts) {
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  bool f = false;
-  if (i < M) {
-    float pos[3], wi[3];
-    f = shadow_pt(rays[i], hits[i], sh, pos, wi);
-  }
-  uint32_t total;
-  (void)block_prefix(f, total);
-  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
-}
-
 // single-block exclusive scan over nb block counts (coalesced 1024-wide
 // chunks, hipCUB block scan); writes the total to *d_count
 __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ c,
@@ -1601,22 +1587,102 @@ __global__ __launch_bounds__(kBlock) void k_select_write(const uint8_t* __restri
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_spawn_pt_write(
-    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits,
-    size_t M, ShadePt sh, const uint32_t* __restrict__ block_offsets,
-    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src) {
-  const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  bool f = false;
-  float pos[3] = {0, 0, 0}, wi[3] = {0, 0, 0};
-  if (i < M) f = shadow_pt(rays[i], hits[i], sh, pos, wi);
-  uint32_t total;
-  const uint32_t k = block_prefix(f, total) + block_offsets[blockIdx.x];
-  if (f) {
-    float4* op = reinterpret_cast<float4*>(out + k);
-    op[0] = make_float4(pos[0], pos[1], pos[2], kRayEpsilon);
-    op[1] = make_float4(wi[0], wi[1], wi[2], kInf);
-    if (src) src[k] = int32_t(i);
+// The PT shadow spawn (shadow_pt) compacted in ray order in one pass (a
+// decoupled look-back scan): blocks take ordered tickets, publish their
+// count (aggregate) at once, then sum their predecessors' published values
+// back to the first inclusive prefix and publish their own inclusive prefix.  A block only
+// waits on blocks with earlier tickets, which are already running and
+// publish without waiting, so every wait ends; the values travel inside the
+// 64-bit status words, so relaxed atomics order everything.  Same output
+// order (ray order) as the two-pass form, one read of the rays and hits.
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+// rays per thread: a block covers kBlock * kSpawnPer rays (OOC frame with
+// 1 / 2 / 4 / 8: 3.06 / 2.89 / 2.84-2.85 / 2.89-2.91 ms, the two-pass form
+// 2.86-2.87 ms: fewer blocks shorten the look-back chain, more rays per
+// thread cost registers)
+constexpr int kSpawnPer = 4;
+__global__ __launch_bounds__(kBlock) void k_spawn_pt_onepass(
+    const spray_rt_ray* __restrict__ rays, const spray_rt_hit* __restrict__ hits, size_t M,
+    ShadePt sh, unsigned long long* __restrict__ state, uint32_t nb,
+    spray_rt_ray* __restrict__ out, int32_t* __restrict__ src, uint32_t* __restrict__ d_count) {
+  __shared__ uint32_t s_b;
+  __shared__ unsigned long long s_excl;
+  if (threadIdx.x == 0) s_b = uint32_t(atomicAdd(state, 1ull));
+  __syncthreads();
+  const uint32_t b = s_b;
+  // ray base + kBlock j + t: coalesced loads, ray order = (j, t) order
+  const size_t base = size_t(b) * (kBlock * kSpawnPer) + threadIdx.x;
+  float pos[kSpawnPer][3], wi[kSpawnPer][3];
+  uint32_t fm = 0;
+#pragma unroll
+  for (int j = 0; j < kSpawnPer; ++j) {
+    const size_t i = base + size_t(j) * kBlock;
+    pos[j][0] = pos[j][1] = pos[j][2] = 0.f;
+    wi[j][0] = wi[j][1] = wi[j][2] = 0.f;
+    if (i < M && shadow_pt(rays[i], hits[i], sh, pos[j], wi[j])) fm |= 1u << j;
   }
+  uint32_t k[kSpawnPer], run = 0;
+#pragma unroll
+  for (int j = 0; j < kSpawnPer; ++j) {
+    uint32_t tot;
+    k[j] = run + block_prefix((fm >> j) & 1u, tot);
+    run += tot;
+    __syncthreads();  // block_prefix's partial sums are reused by the next j
+  }
+  if (threadIdx.x < 64) {
+    // the look-back by the first wave: lane l reads predecessor pend - l, so
+    // one round trip covers 64 predecessors
+    const int lane = int(threadIdx.x);
+    unsigned long long* st = state + 1;
+    unsigned long long excl = 0;
+    if (b == 0) {
+      if (lane == 0)
+        __hip_atomic_store(st, kLbInc | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(st + b, kLbAgg | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t pend = int64_t(b) - 1;
+      for (;;) {
+        const int64_t p = pend - lane;
+        // before the first block: an inclusive prefix of 0
+        const unsigned long long v =
+            p >= 0 ? __hip_atomic_load(st + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : kLbInc;
+        const uint64_t inc = __ballot((v & kLbInc) != 0);
+        const uint64_t ready = __ballot((v >> 62) != 0);
+        const int first = inc ? __ffsll((long long)inc) - 1 : 63;
+        const uint64_t need = first == 63 ? ~0ull : ((2ull << first) - 1);
+        if ((ready & need) != need) continue;  // a predecessor has not published yet
+        unsigned long long add = lane <= first ? (v & kLbVal) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint32_t lo = uint32_t(__shfl_xor(int(uint32_t(add)), o));
+          const uint32_t hi = uint32_t(__shfl_xor(int(uint32_t(add >> 32)), o));
+          add += (uint64_t(hi) << 32) | lo;
+        }
+        excl += add;
+        if (inc) break;
+        pend -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(st + b, kLbInc | (excl + run), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_excl = excl;
+      if (b == nb - 1) *d_count = uint32_t(excl + run);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSpawnPer; ++j)
+    if ((fm >> j) & 1u) {
+      const size_t o = size_t(s_excl) + k[j];
+      float4* op = reinterpret_cast<float4*>(out + o);
+      op[0] = make_float4(pos[j][0], pos[j][1], pos[j][2], kRayEpsilon);
+      op[1] = make_float4(wi[j][0], wi[j][1], wi[j][2], kInf);
+      if (src) src[o] = int32_t(base + size_t(j) * kBlock);
+    }
 }
 
 // ao_sample / ao_ok: shade_device.h
@@ -2383,7 +2449,7 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
                            const spray_rt_hit* hits, size_t M,
                            const float* shade10, spray_rt_ray* out_rays,
                            int32_t* out_src, uint32_t* d_count,
-                           uint32_t* block_counts) {
+                           void* scratch) {
   ShadePt sh;
   for (int k = 0; k < 3; ++k) {
     sh.lp[k] = shade10[k];
@@ -2392,11 +2458,12 @@ hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,
   }
   sh.shininess = shade10[9];
   if (M == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
-  const unsigned g = grid_for(M);
-  k_spawn_pt_count<<<g, kBlock, 0, s>>>(rays, hits, M, sh, block_counts);
-  k_scan_blocks<<<1, 1024, 0, s>>>(block_counts, g, d_count);
-  k_spawn_pt_write<<<g, kBlock, 0, s>>>(rays, hits, M, sh, block_counts,
-                                        out_rays, out_src);
+  const unsigned g = unsigned((M + size_t(kBlock) * kSpawnPer - 1) / (size_t(kBlock) * kSpawnPer));
+  unsigned long long* state = static_cast<unsigned long long*>(scratch);
+  hipError_t e = hipMemsetAsync(state, 0, (size_t(g) + 1) * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  k_spawn_pt_onepass<<<g, kBlock, 0, s>>>(rays, hits, M, sh, state, g, out_rays, out_src,
+                                          d_count);
   return hipGetLastError();
 }
 
