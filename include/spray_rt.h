@@ -719,7 +719,8 @@ int spray_rt_camera_shadow_boxes(const float box[6], const float scene[6], const
  * SUMs and the reduce keep the rank's own values.  Its device work is the
  * rank's exact share of the N-rank frame (its launches, their sizes and the
  * rays they walk), back to back on its stream; the film and totals it
- * produces are not the frame's.  PT camera frames with split keys only. */
+ * produces are not the frame's.  PT camera frames with split keys, and AO
+ * camera frames (spray_rt_insitu_replay_set_ao). */
 int spray_rt_insitu_create_replay(spray_rt_ctx_t ctx, int world, int rank,
                                   spray_rt_insitu_t* out);
 int spray_rt_insitu_replay_set(spray_rt_insitu_t ins, const uint32_t* d_tmin,
@@ -728,6 +729,14 @@ int spray_rt_insitu_replay_set(spray_rt_insitu_t ins, const uint32_t* d_tmin,
  * cap entries) copies its group t-bits minima and list-position minima. */
 int spray_rt_insitu_replay_capture(spray_rt_insitu_t ins, uint32_t* d_tmin, uint8_t* d_lpmin,
                                    size_t cap, size_t* n);
+/* The same for AO camera frames: the 64-bit key minima over U (d_kmin, n)
+ * and the winners' published normals and colours (d_pub, 2 n uint64 --
+ * the publish step's SUM); capture after a one-rank replicated AO camera
+ * frame with every domain resident. */
+int spray_rt_insitu_replay_set_ao(spray_rt_insitu_t ins, const uint64_t* d_kmin,
+                                  const uint64_t* d_pub, size_t n);
+int spray_rt_insitu_replay_capture_ao(spray_rt_insitu_t ins, uint64_t* d_kmin, uint64_t* d_pub,
+                                      size_t cap, size_t* n);
 /* Per-phase device time of the traces since the last call (then reset),
  * HIP events on the context's stream, when phase timing is on
  * (spray_rt_insitu_set_timing).  out_ms[9]; *nphases = phases of the last

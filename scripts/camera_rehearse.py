@@ -42,6 +42,10 @@ SPP = 8
 SHADE = [0.0, 500.0, 1000.0, 1.0, 1.0, 1.0, 0.4, 0.4, 0.4, 10.0]
 MODES = {"close": 0, "rr": 1, "view": 2}
 SEGMENTS = [("prepare", "keyed_shade"), ("list_pos", "shadow_trace", "winners"), ("film_totals",)]
+# AO-16 (configs[4]): between the key MIN, the publish SUM and the occlusion SUM
+SEGMENTS_AO = [("prepare", "keyed_closest_hit"), ("publish",), ("ao_spawn", "ao_own_trace"),
+               ("film_totals",)]
+AO_SAMPLES = 16
 # ring all-reduce / reduce on N GPUs: alpha per call (ms) and bus bandwidth (GB/s)
 LINK = {"cons": (0.030, 300.0), "opt": (0.015, 500.0)}
 
@@ -59,12 +63,27 @@ def comm_ms(world, nu, npu, model):
     return ar(4 * nu) + ar(nu + 192) + rd(12 * npu)
 
 
+def comm_ao_ms(world, nu, model):
+    """AO: key MIN (8 B / slot), published normals + colours SUM (16 B /
+    slot), occlusion count fields SUM (fb bits per (slot, sample)); rank 0
+    films (no reduce)"""
+    if world == 1:
+        return 0.0
+    a, bw = LINK[model]
+    f = (world - 1) / world
+    fb = 2 if world <= 3 else (4 if world <= 15 else 8)
+    ar = lambda b: a + 2 * f * b / (bw * 1e6)  # noqa: E731
+    return ar(8 * nu) + ar(16 * nu) + ar(nu * AO_SAMPLES * fb / 8)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--modes", nargs="+", default=["close", "rr", "view"])
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/cam/rehearse.json")
+    ap.add_argument("--shader", choices=("pt", "ao"), default="pt",
+                    help="pt: configs[2] (PT point-light shadows); ao: configs[4] (AO-16)")
     args = ap.parse_args()
     import torch
     import spray_amd
@@ -77,8 +96,13 @@ def main():
     boxes, lights = host_parse_scene(SCENE, SCENES)
     bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
     cam = spray_amd.camera_init(CAM["pos"], CAM["lookat"], CAM["up"], CAM["fov"], W, H)
-    sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
-                                     lights=lights)
+    ao = args.shader == "ao"
+    segments = SEGMENTS_AO if ao else SEGMENTS
+    if ao:
+        sh = spray_amd.frame.make_shader("ao", 1, AO_SAMPLES, lights=lights)
+    else:
+        sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
+                                         lights=lights)
     image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
 
     # 1. the group results (every domain on one rank, replicated steps)
@@ -89,13 +113,18 @@ def main():
     rt.set_stream(stream)
     eng = insitu.InsituEngine(rt, 1, 0, transport="rccl")
     tot = eng.trace_camera(sh, cam, W, H, SPP, image)
-    tmin, lpmin = eng.replay_capture()
-    nu = tmin.numel()
+    if ao:
+        kmin, pub = eng.replay_capture_ao()
+        nu = kmin.numel()
+    else:
+        tmin, lpmin = eng.replay_capture()
+        nu = tmin.numel()
     print("capture: %d U slots (%d pixels), totals %s" % (nu, nu // SPP, tot), flush=True)
     eng.close()
     rt.close()
     os.environ.pop("SPRAY_INSITU_REPLICATED")
-    report = {"frame": "wavelets64 1024x1024x8spp PT camera frame (configs[2])", "u_slots": nu,
+    report = {"frame": "wavelets64 1024x1024x8spp %s camera frame (%s)" % (
+                  ("AO-16", "configs[4]") if ao else ("PT", "configs[2]")), "u_slots": nu,
               "u_pixels": nu // SPP, "totals": list(tot), "link": LINK, "runs": []}
 
     for mode in args.modes:
@@ -109,7 +138,10 @@ def main():
                 rt.set_bsdfs(host_scene_bsdfs(SCENE))
                 rt.set_stream(stream)
                 eng = insitu.InsituEngine(rt, world, r, transport="replay")
-                eng.replay_set(tmin, lpmin)
+                if ao:
+                    eng.replay_set_ao(kmin, pub)
+                else:
+                    eng.replay_set(tmin, lpmin)
                 for _ in range(3):
                     eng.trace_camera(sh, cam, W, H, SPP, image)
                 eng.set_timing(True)
@@ -129,20 +161,22 @@ def main():
                     eng.trace_camera(sh, cam, W, H, SPP, image)
                 ev2[1].record(stream)
                 torch.cuda.synchronize()
-                seg = [sum(ph.get(k, 0.0) for k in s) for s in SEGMENTS]
+                seg = [sum(ph.get(k, 0.0) for k in s) for s in segments]
                 ranks.append({"rank": r, "domains": int((owner == r).sum()),
                               "phases_ms": {k: round(v, 4) for k, v in ph.items()},
                               "segments_ms": [round(x, 4) for x in seg],
                               "frame_ms": round(ev2[0].elapsed_time(ev2[1]) / args.frames, 4)})
                 eng.close()
                 rt.close()
-            busiest = [max(rk["segments_ms"][k] for rk in ranks) for k in range(len(SEGMENTS))]
+            busiest = [max(rk["segments_ms"][k] for rk in ranks) for k in range(len(segments))]
             dev = sum(busiest)
-            proj = {m: dev + comm_ms(world, nu, nu // SPP, m) for m in LINK}
+            cm = {m: (comm_ao_ms(world, nu, m) if ao else comm_ms(world, nu, nu // SPP, m))
+                  for m in LINK}
+            proj = {m: dev + cm[m] for m in LINK}
             run = {"world": world, "partition": mode, "ranks": ranks,
                    "busiest_segments_ms": [round(x, 4) for x in busiest],
                    "device_ms": round(dev, 4),
-                   "comm_ms": {m: round(comm_ms(world, nu, nu // SPP, m), 4) for m in LINK},
+                   "comm_ms": {m: round(cm[m], 4) for m in LINK},
                    "frame_ms": {m: round(v, 4) for m, v in proj.items()}}
             report["runs"].append(run)
             print("N=%d %-5s (%.0f s): busiest segments %s = %.3f ms device; frame %.3f / %.3f ms"

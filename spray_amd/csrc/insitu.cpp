@@ -186,7 +186,8 @@ struct spray_rt_insitu {
   DBuf tu_runs, tu_first, te_runs, te_first, ts_runs, ts_first;
   CamTable tu{}, te{}, ts{};
   uint32_t tu_pixmax = 0;
-  size_t last_nu = 0;  // U slots of the last camera PT frame
+  size_t last_nu = 0;     // U slots of the last camera PT frame
+  size_t last_nc_ao = 0;  // C slots of the last replicated AO frame
   DBuf ctmin, ccomp, crays, cpix, csam, ciota;
   size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
@@ -325,6 +326,11 @@ struct ReplayTransport : InsituTransport {
   const uint32_t* tmin = nullptr;
   const uint8_t* lpmin = nullptr;
   size_t n = 0;
+  // AO camera frames: the key MIN over U and the published winners'
+  // normals and colours (the SUM of the publish step, 16 B per slot)
+  const uint64_t* kmin = nullptr;
+  const uint64_t* pub = nullptr;
+  size_t nk = 0;
   int copy(spray_rt_insitu* I, void* dst, const void* src, size_t bytes, hipStream_t s) {
     ++I->st[4];
     if (bytes) HIPCHK(I->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
@@ -343,16 +349,23 @@ struct ReplayTransport : InsituTransport {
                 bool) override {
     return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
   }
-  int allreduce_u64(spray_rt_insitu* I, unsigned long long*, size_t) override {
-    ++I->st[4];
-    return SPRAY_RT_OK;
+  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t m) override {
+    if (!pub) {  // keep the rank's own values
+      ++I->st[4];
+      return SPRAY_RT_OK;
+    }
+    if (m != 2 * nk) return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu publish words given, "
+                                 "the frame has %zu", 2 * nk, m);
+    return copy(I, dev, pub, m * 8, stream_of(I->ctx));
   }
   int reduce_f32(spray_rt_insitu* I, float*, size_t, int) override {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u64(spray_rt_insitu* I, uint64_t*, size_t) override {
-    return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: split keys only");
+  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t m) override {
+    if (!kmin || m != nk)
+      return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu keys given, the frame has %zu", nk, m);
+    return copy(I, dev, kmin, m * 8, stream_of(I->ctx));
   }
   int allreduce_sum_u8(spray_rt_insitu* I, uint8_t*, size_t) override {
     ++I->st[4];
@@ -1163,7 +1176,8 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
                         const int32_t* pixid, const int32_t* samid, size_t n, int spp,
                         float* image, const spray_rt_insitu_rec* rec,
                         unsigned long long totals[3], const uint32_t* idx_c = nullptr,
-                        size_t nc_c = 0, uint32_t pixmax_c = 0) {
+                        size_t nc_c = 0, uint32_t pixmax_c = 0, const CamFrame* cam = nullptr,
+                        const CamTable* te = nullptr) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
   const int ns = P->samples;
@@ -1175,6 +1189,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
     idx_c = I->ridx_c.as<uint32_t>();
   }
   if (nc >= (size_t(1) << 27)) return fail(c, SPRAY_RT_ERR_LIMIT, "replicated AO: |C'| >= 2^27");
+  I->last_nc_ao = nc;
   // own keyed closest hits over C' (keys and hit records at C' positions)
   MARK(2);
   GROW(I->rkeys_n, nc * 8 + 8);
@@ -1182,9 +1197,18 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   GROW(I->rkeys_c, nc * 8 + 8);
   GROW(I->rtk, nc * 4 + 4);
   const float zero10[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, zero10,
-                                   I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
-                                   I->rtk.as<uint32_t>(), nullptr, nullptr));
+  if (cam) {
+    // camera frames (C = U): only the rank's eye table E is traced, its rays
+    // generated in the lanes; every other slot keeps the miss key
+    HIPCHK(c, launch_fill_u64(s, I->rkeys_n.as<uint64_t>(), nc, kInsituMissKey));
+    HIPCHK(c, launch_scene_cam_keyed(s, view(c), *cam, *te, zero10,
+                                     I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
+                                     I->rtk.as<uint32_t>(), nullptr, nullptr, false));
+  } else {
+    HIPCHK(c, launch_scene_rep_keyed(s, view(c), rays, n, idx_c, nc, zero10,
+                                     I->rhits_n.as<spray_rt_hit>(), I->rkeys_n.as<uint64_t>(),
+                                     I->rtk.as<uint32_t>(), nullptr, nullptr));
+  }
   HIPCHK(c, hipMemcpyAsync(I->rkeys_c.p, I->rkeys_n.p, nc * 8, hipMemcpyDeviceToDevice, s));
   MARK(3);
   if (nc) COMM(I->tr->allreduce_min_u64(I, I->rkeys_c.as<uint64_t>(), nc));
@@ -1504,8 +1528,9 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
 }
 
 // The replicated AO frame from the camera: U's eye rays, pixels and samples
-// generated into U-ordered arrays (one pass), then trace_replicated_ao over
-// C = U.
+// generated into U-ordered arrays (one pass; the spawn and film read them),
+// then trace_replicated_ao over C = U with the keyed closest hit over the
+// rank's eye table E only (its rays generated in the lanes).
 int trace_camera_ao(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame& F, int image_h,
                     float* image, const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
   spray_rt_ctx* c = I->ctx;
@@ -1526,7 +1551,7 @@ int trace_camera_ao(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   const size_t n = size_t(F.image_w) * size_t(image_h) * size_t(F.spp);
   return trace_replicated_ao(I, P, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
                              I->csam.as<int32_t>(), n, F.spp, image, rec, totals,
-                             I->ciota.as<uint32_t>(), nu, I->tu_pixmax);
+                             I->ciota.as<uint32_t>(), nu, I->tu_pixmax, &F, &I->te);
 }
 
 void free_all(spray_rt_insitu* I) {
@@ -1667,6 +1692,36 @@ int spray_rt_insitu_replay_set(spray_rt_insitu_t I, const uint32_t* d_tmin,
   t->tmin = d_tmin;
   t->lpmin = d_lpmin;
   t->n = n;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_replay_set_ao(spray_rt_insitu_t I, const uint64_t* d_kmin,
+                                  const uint64_t* d_pub, size_t n) {
+  if (!I) return SPRAY_RT_ERR_ARG;
+  auto* t = dynamic_cast<ReplayTransport*>(I->tr.get());
+  if (!t) return fail(I->ctx, SPRAY_RT_ERR_STATE, "not a replay context");
+  if (n && (!is_device_ptr(d_kmin) || !is_device_ptr(d_pub)))
+    return fail(I->ctx, SPRAY_RT_ERR_ARG, "replay arrays must be device memory");
+  t->kmin = d_kmin;
+  t->pub = d_pub;
+  t->nk = n;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_replay_capture_ao(spray_rt_insitu_t I, uint64_t* d_kmin, uint64_t* d_pub,
+                                      size_t cap, size_t* n) {
+  if (!I || !n) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = I->ctx;
+  if (I->cam_key.empty() || !I->rkeys_c.p || !I->apub.p || !I->last_nc_ao)
+    return fail(c, SPRAY_RT_ERR_STATE, "no replicated AO camera frame traced yet");
+  const size_t m = I->last_nc_ao;
+  *n = m;
+  if (!d_kmin || !d_pub) return SPRAY_RT_OK;  // size query
+  if (cap < m) return fail(c, SPRAY_RT_ERR_LIMIT, "replay capture: %zu slots, cap %zu", m, cap);
+  hipStream_t s = stream_of(c);
+  HIPCHK(c, hipMemcpyAsync(d_kmin, I->rkeys_c.p, m * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pub, I->apub.p, m * 16, hipMemcpyDeviceToDevice, s));
+  HIPCHK(c, hipStreamSynchronize(s));
   return SPRAY_RT_OK;
 }
 

@@ -390,6 +390,27 @@ class InsituEngine:
                        "replay_capture")
         return t, lp
 
+    def replay_capture_ao(self):
+        """(kmin u64, pub u64 [2 n]) device tensors of the last AO camera
+        frame's key minima and published normals over U
+        (spray_rt_insitu_replay_capture_ao)."""
+        import torch
+        n = C.c_size_t(0)
+        self.rt._check(lib().spray_rt_insitu_replay_capture_ao(self.h, None, None, 0,
+                                                               C.byref(n)), "replay_capture_ao")
+        k = torch.empty(max(n.value, 1), dtype=torch.int64, device="cuda")[:n.value]
+        pub = torch.empty(max(2 * n.value, 1), dtype=torch.int64, device="cuda")[:2 * n.value]
+        self.rt._check(lib().spray_rt_insitu_replay_capture_ao(self.h, k.data_ptr(), pub.data_ptr(),
+                                                               n.value, C.byref(n)),
+                       "replay_capture_ao")
+        return k, pub
+
+    def replay_set_ao(self, kmin, pub):
+        """The AO frame's group results a replay context hands back."""
+        self._replay_ao = (kmin, pub)
+        self.rt._check(lib().spray_rt_insitu_replay_set_ao(self.h, kmin.data_ptr(), pub.data_ptr(),
+                                                           kmin.numel()), "replay_set_ao")
+
     def replay_set(self, tmin, lpmin):
         """The group results a replay context's collectives hand back."""
         self._replay = (tmin, lpmin)  # keep the tensors alive
