@@ -737,6 +737,12 @@ int spray_rt_insitu_replay_set_ao(spray_rt_insitu_t ins, const uint64_t* d_kmin,
                                   const uint64_t* d_pub, size_t n);
 int spray_rt_insitu_replay_capture_ao(spray_rt_insitu_t ins, uint64_t* d_kmin, uint64_t* d_pub,
                                       size_t cap, size_t* n);
+/* The AO frame's first-round occlusion bits (a pair occluded by its home
+ * rank, which depend on the partition): with d_out, copies the last frame's
+ * own bits (*n bytes; rehearse every rank once, OR them); else sets d_bits
+ * (nbytes, the group's OR) as the result of that SUM; *n = the byte count. */
+int spray_rt_insitu_replay_bits_ao(spray_rt_insitu_t ins, const uint8_t* d_bits, uint8_t* d_out,
+                                   size_t nbytes, size_t* n);
 /* Per-phase device time of the traces since the last call (then reset),
  * HIP events on the context's stream, when phase timing is on
  * (spray_rt_insitu_set_timing).  out_ms[9]; *nphases = phases of the last

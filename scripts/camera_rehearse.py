@@ -65,15 +65,16 @@ def comm_ms(world, nu, npu, model):
 
 def comm_ao_ms(world, nu, model):
     """AO: key MIN (8 B / slot), published normals + colours SUM (16 B /
-    slot), occlusion count fields SUM (fb bits per (slot, sample)); rank 0
-    films (no reduce)"""
+    slot), the first round's occlusion bits SUM (1 bit per (slot, sample)),
+    occlusion count fields SUM (fb bits per (slot, sample)); rank 0 films
+    (no reduce)"""
     if world == 1:
         return 0.0
     a, bw = LINK[model]
     f = (world - 1) / world
     fb = 2 if world <= 3 else (4 if world <= 15 else 8)
     ar = lambda b: a + 2 * f * b / (bw * 1e6)  # noqa: E731
-    return ar(8 * nu) + ar(16 * nu) + ar(nu * AO_SAMPLES * fb / 8)
+    return ar(8 * nu) + ar(16 * nu) + ar(nu * AO_SAMPLES / 8) + ar(nu * AO_SAMPLES * fb / 8)
 
 
 def main():
@@ -132,6 +133,22 @@ def main():
             owner = insitu.partition(boxes, bound, world, MODES[mode], cam)
             ranks = []
             t0 = time.time()
+            bits = None
+            if ao:
+                # the first round's occlusion bits depend on the partition:
+                # every rank once, OR-ed, then handed back by that SUM
+                for r in range(world):
+                    rt = spray_amd.RtContext(0)
+                    insitu.setup_rank_context(rt, SCENE, SCENES, owner, r)
+                    rt.set_bsdfs(host_scene_bsdfs(SCENE))
+                    rt.set_stream(stream)
+                    eng = insitu.InsituEngine(rt, world, r, transport="replay")
+                    eng.replay_set_ao(kmin, pub)
+                    eng.trace_camera(sh, cam, W, H, SPP, image)
+                    own = eng.replay_bits_ao()
+                    bits = own.clone() if bits is None else bits | own
+                    eng.close()
+                    rt.close()
             for r in range(world):
                 rt = spray_amd.RtContext(0)
                 insitu.setup_rank_context(rt, SCENE, SCENES, owner, r)
@@ -140,6 +157,7 @@ def main():
                 eng = insitu.InsituEngine(rt, world, r, transport="replay")
                 if ao:
                     eng.replay_set_ao(kmin, pub)
+                    eng.replay_bits_ao(bits)
                 else:
                     eng.replay_set(tmin, lpmin)
                 for _ in range(3):

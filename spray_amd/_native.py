@@ -145,6 +145,7 @@ SIGNATURES = {
     "spray_rt_insitu_replay_capture": (I, [P, P, P, SZ, P]),
     "spray_rt_insitu_replay_set_ao": (I, [P, P, P, SZ]),
     "spray_rt_insitu_replay_capture_ao": (I, [P, P, P, SZ, P]),
+    "spray_rt_insitu_replay_bits_ao": (I, [P, P, P, SZ, P]),
     "spray_rt_camera_box_rows": (I, [P, I, I, P, P, P]),
     "spray_rt_camera_shadow_boxes": (I, [P, P, P, I, P]),
     "spray_rt_insitu_set_timing": (I, [P, I]),

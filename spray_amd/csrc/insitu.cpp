@@ -173,6 +173,7 @@ struct spray_rt_insitu {
   // replicated-ray AO frames (trace_replicated_ao)
   DBuf apub, arays, ahits, apairs, aocc_p, alv, arec, ascratch, afields, acount;
   DBuf aflag, aown, asel_tmp;  // replicated AO: the own pairs, compacted
+  DBuf abits;                  // their first round's occlusion, one bit per pair
   // compact film of replicated PT frames (runs of equal pixels along C)
   DBuf rincl, rscan_tmp, rslot_c, rslot_pix, rcompact, rnp;
   hipEvent_t ev_np = nullptr;  // the run count's copy to the host
@@ -188,6 +189,7 @@ struct spray_rt_insitu {
   uint32_t tu_pixmax = 0;
   size_t last_nu = 0;     // U slots of the last camera PT frame
   size_t last_nc_ao = 0;  // C slots of the last replicated AO frame
+  size_t last_npair_ao = 0;  // and its AO pairs (nc x samples)
   DBuf ctmin, ccomp, crays, cpix, csam, ciota;
   size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
@@ -331,6 +333,10 @@ struct ReplayTransport : InsituTransport {
   const uint64_t* kmin = nullptr;
   const uint64_t* pub = nullptr;
   size_t nk = 0;
+  // and the first round's occlusion bits of the group (the SUM of that
+  // many bytes); other SUMs keep the rank's own values
+  const uint8_t* bits = nullptr;
+  size_t nbits_bytes = 0;
   int copy(spray_rt_insitu* I, void* dst, const void* src, size_t bytes, hipStream_t s) {
     ++I->st[4];
     if (bytes) HIPCHK(I->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
@@ -367,7 +373,8 @@ struct ReplayTransport : InsituTransport {
       return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu keys given, the frame has %zu", nk, m);
     return copy(I, dev, kmin, m * 8, stream_of(I->ctx));
   }
-  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t*, size_t) override {
+  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t m) override {
+    if (bits && m == nbits_bytes) return copy(I, dev, bits, m, stream_of(I->ctx));
     ++I->st[4];
     return SPRAY_RT_OK;
   }
@@ -1269,22 +1276,42 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
                                     I->alv.as<float>(), I->arec.as<float>(), dcount,
                                     I->ascratch.p));
     MARK(5);
-    // the pairs entering this rank's boxes, compacted (the rest stay 0)
+    // the pairs entering this rank's boxes, compacted and traced (the rest
+    // stay 0), in two rounds: first the pairs starting in one of its
+    // domains (an AO ray is mostly occluded near its start), then -- once
+    // the group knows which pairs the first round occluded -- the other
+    // pairs entering its boxes that are still open.  A pair occluded by its
+    // home rank is not walked by the ranks its ray passes through.
     GROW(I->aflag, npair + 1);
     GROW(I->aown, npair * 4 + 4);
+    const size_t nbits = (npair + 31) / 32;
+    I->last_npair_ao = npair;
+    GROW(I->abits, nbits * 4 + 4);
     size_t tsel = 0;
     HIPCHK(c, launch_select_flagged(s, nullptr, npair, nullptr, nullptr, nullptr, &tsel));
     GROW(I->asel_tmp, tsel);
     HIPCHK(c, hipMemsetAsync(I->aocc_p.p, 0, npair, s));
-    HIPCHK(c, launch_ao_own_flags(s, view(c), npair, I->apairs.as<uint32_t>(),
-                                  I->arec.as<float>(), I->alv.as<float>(), ns, dcount,
-                                  I->aflag.as<uint8_t>()));
-    HIPCHK(c, launch_select_flagged(s, I->aflag.as<uint8_t>(), npair, I->aown.as<uint32_t>(),
-                                    dcount + 1, I->asel_tmp.p, &tsel));
-    HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
-                                       I->arec.as<float>(), I->alv.as<float>(), ns, dcount + 1,
-                                       I->aocc_p.as<uint8_t>(), nullptr,
-                                       I->aown.as<uint32_t>()));
+    const uint64_t* kmin = I->rkeys_c.as<uint64_t>();
+    for (int round = 1; round <= 2; ++round) {
+      HIPCHK(c, launch_ao_own_flags(s, view(c), npair, I->apairs.as<uint32_t>(),
+                                    I->arec.as<float>(), I->alv.as<float>(), ns, dcount,
+                                    I->aflag.as<uint8_t>(), kmin, I->abits.as<uint32_t>(),
+                                    round));
+      HIPCHK(c, launch_select_flagged(s, I->aflag.as<uint8_t>(), npair, I->aown.as<uint32_t>(),
+                                      dcount + round, I->asel_tmp.p, &tsel));
+      HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
+                                         I->arec.as<float>(), I->alv.as<float>(), ns,
+                                         dcount + round, I->aocc_p.as<uint8_t>(), nullptr,
+                                         I->aown.as<uint32_t>()));
+      if (round == 1) {
+        // the first round's occlusion over the group: one bit per pair, set
+        // only by the pair's home rank, so a SUM of the bytes is their OR
+        HIPCHK(c, launch_pack_bits(s, I->aocc_p.as<uint8_t>(), npair, I->abits.as<uint32_t>()));
+        I->st[0] += 4 * nbits;
+        I->st[1] += 4 * nbits;
+        COMM(I->tr->allreduce_sum_u8(I, I->abits.as<uint8_t>(), nbits * 4));
+      }
+    }
     HIPCHK(c, launch_rep_ao_scatter(s, I->apairs.as<uint32_t>(), dcount, npair,
                                     I->aocc_p.as<uint8_t>(), ns, fb, I->afields.as<uint32_t>()));
   }
@@ -1568,7 +1595,7 @@ void free_all(spray_rt_insitu* I) {
                  &I->ahits, &I->apairs, &I->aocc_p, &I->alv, &I->arec, &I->ascratch,
                  &I->afields, &I->acount, &I->rincl, &I->rscan_tmp,
                  &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax,
-                 &I->aflag, &I->aown, &I->asel_tmp, &I->tu_runs, &I->tu_first,
+                 &I->aflag, &I->aown, &I->asel_tmp, &I->abits, &I->tu_runs, &I->tu_first,
                  &I->te_runs, &I->te_first, &I->ts_runs, &I->ts_first, &I->ctmin, &I->ccomp,
                  &I->crays, &I->cpix, &I->csam, &I->ciota};
   for (DBuf* b : all)
@@ -1705,6 +1732,27 @@ int spray_rt_insitu_replay_set_ao(spray_rt_insitu_t I, const uint64_t* d_kmin,
   t->kmin = d_kmin;
   t->pub = d_pub;
   t->nk = n;
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_replay_bits_ao(spray_rt_insitu_t I, const uint8_t* d_bits, uint8_t* d_out,
+                                   size_t nbytes, size_t* n) {
+  if (!I || !n) return SPRAY_RT_ERR_ARG;
+  auto* t = dynamic_cast<ReplayTransport*>(I->tr.get());
+  if (!t) return fail(I->ctx, SPRAY_RT_ERR_STATE, "not a replay context");
+  *n = I->abits.p ? (I->last_npair_ao + 31) / 32 * 4 : 0;
+  if (d_out) {  // the last frame's own first-round bits
+    if (nbytes < *n) return fail(I->ctx, SPRAY_RT_ERR_LIMIT, "replay bits: cap %zu < %zu",
+                                 nbytes, *n);
+    hipStream_t s = stream_of(I->ctx);
+    HIPCHK(I->ctx, hipMemcpyAsync(d_out, I->abits.p, *n, hipMemcpyDeviceToDevice, s));
+    HIPCHK(I->ctx, hipStreamSynchronize(s));
+    return SPRAY_RT_OK;
+  }
+  if (d_bits && !is_device_ptr(d_bits))
+    return fail(I->ctx, SPRAY_RT_ERR_ARG, "replay arrays must be device memory");
+  t->bits = d_bits;
+  t->nbits_bytes = d_bits ? nbytes : 0;
   return SPRAY_RT_OK;
 }
 

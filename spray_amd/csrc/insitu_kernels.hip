@@ -381,6 +381,19 @@ __global__ __launch_bounds__(kBlock) void k_rep_ao_scatter(const uint32_t* __res
   atomicOr(fields + pos / per, 1u << (uint32_t(pos % per) * uint32_t(fb)));
 }
 
+// bits[w] bit b = occ[32 w + b] != 0 over [0, n)
+__global__ __launch_bounds__(kBlock) void k_pack_bits(const uint8_t* __restrict__ occ, size_t n,
+                                                      uint32_t* __restrict__ bits) {
+  const size_t w = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (w >= (n + 31) / 32) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 32; ++b) {
+    const size_t k = 32 * w + size_t(b);
+    if (k < n && occ[k]) v |= 1u << b;
+  }
+  bits[w] = v;
+}
+
 __device__ __forceinline__ bool rep_ao_occluded(const uint32_t* __restrict__ fields, size_t pos,
                                                 int fb) {
   const uint32_t per = 32u / uint32_t(fb);
@@ -1015,6 +1028,9 @@ hipError_t launch_rep_ao_publish(hipStream_t s, const RepAoArgs& a) {
 }
 hipError_t launch_rep_ao_hits(hipStream_t s, const RepAoArgs& a) {
   LAUNCH(a.nc, k_rep_ao_hits, a);
+}
+hipError_t launch_pack_bits(hipStream_t s, const uint8_t* occ, size_t n, uint32_t* bits) {
+  LAUNCH((n + 31) / 32, k_pack_bits, occ, n, bits);
 }
 hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uint32_t* d_count,
                                  size_t max_n, const uint8_t* occ, int ns, int fb,

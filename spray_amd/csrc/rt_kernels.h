@@ -241,10 +241,14 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
 // flag[k] = AO pair k (k < min(*d_count, max_n)) enters a resident domain's
 // box, 0 for the rest of [0, max_n): the replicated AO frame traces only
 // the flagged pairs (idx of launch_occluded_ao_pairs, from
-// launch_select_flagged).
+// launch_select_flagged).  mode 1: the pairs starting in a resident domain
+// (the domain of the source's key minimum, kmin[pair >> 5] & 0xFFFF); mode
+// 2: the other pairs entering a resident box with bit k of bits_a clear.
 hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
                                const uint32_t* pairs, const float* rec, const float* lv,
-                               int nsamples, const uint32_t* d_count, uint8_t* flag);
+                               int nsamples, const uint32_t* d_count, uint8_t* flag,
+                               const uint64_t* kmin = nullptr, const uint32_t* bits_a = nullptr,
+                               int mode = 0);
 size_t ao_scratch_bytes(size_t M, int nsamples);
 
 // ---- out-of-core path (ooc_kernels.hip) ----

@@ -2610,9 +2610,18 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
 // traced alone: culling lanes inside the traced waves instead (measured)
 // left every wave as long as its slowest lane, and a rank's launch as long
 // as the whole frame's.
+// mode 1 / 2 split the pairs between two rounds (trace_replicated_ao): 1 =
+// the pairs that start in a resident domain (the winner's domain, the low
+// bits of the source's key minimum kmin), 2 = the other pairs entering a
+// resident box whose bit in bits_a (the first round's occlusion over the
+// group) is clear; 0 = every pair entering a resident box.
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint8_t* flag) {
+__global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint8_t* flag,
+                                                        const uint64_t* __restrict__ kmin,
+                                                        const uint32_t* __restrict__ bits_a,
+                                                        int mode) {
   __shared__ float sbox[6 * 64 * W];
+  __shared__ uint32_t resm[2 * W];  // resident domains as a bit mask
   // padded as build_domain_tree pads internal boxes (kTopPad x the larger
   // of the box's own scale and the scene's largest finite coordinate, where
   // the AO rays start)
@@ -2647,22 +2656,43 @@ __global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint
   }
   if (threadIdx.x == 0) {
     int q = 0;
+    for (int w = 0; w < 2 * W; ++w) resm[w] = 0u;
     for (int d = 0; d < A.ndom; ++d) {
       const float4 t = ld4(A.domtrav, d);
-      if (__float_as_uint(t.x) | __float_as_uint(t.y)) sres[q++] = uint8_t(d);
+      if (__float_as_uint(t.x) | __float_as_uint(t.y)) {
+        sres[q++] = uint8_t(d);
+        resm[d >> 5] |= 1u << (d & 31);
+      }
     }
     nres = q;
   }
   __syncthreads();
   const size_t n = A.d_count ? min(size_t(*A.d_count), A.M) : A.M;
   for (size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x; k < A.M;
-       k += size_t(gridDim.x) * kBlock)
-    flag[k] = k < n && ao_own(A, k, sbox, spad, sres, nres) ? 1 : 0;
+       k += size_t(gridDim.x) * kBlock) {
+    bool f = false;
+    if (k < n) {
+      if (mode == 0) {
+        f = ao_own(A, k, sbox, spad, sres, nres);
+      } else {
+        const uint32_t d = uint32_t(kmin[A.ao_pairs[k] >> 5] & 0xFFFFu);
+        const bool home = d < uint32_t(A.ndom) && ((resm[d >> 5] >> (d & 31)) & 1u);
+        if (mode == 1)
+          f = home;
+        else
+          f = !home && !((bits_a[k >> 5] >> (k & 31)) & 1u) && ao_own(A, k, sbox, spad, sres, nres);
+      }
+    }
+    flag[k] = f ? 1 : 0;
+  }
 }
 
 hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
                                const uint32_t* pairs, const float* rec, const float* lv,
-                               int nsamples, const uint32_t* d_count, uint8_t* flag) {
+                               int nsamples, const uint32_t* d_count, uint8_t* flag,
+                               const uint64_t* kmin, const uint32_t* bits_a, int mode) {
+  if (mode != 0 && !kmin) return hipErrorInvalidValue;
+  if (mode == 2 && !bits_a) return hipErrorInvalidValue;
   if (max_n == 0) return hipSuccess;
   SceneArgs a = scene_args(v, nullptr, max_n);
   a.d_count = d_count;
@@ -2674,9 +2704,9 @@ hipError_t launch_ao_own_flags(hipStream_t s, const SceneView& v, size_t max_n,
   // setup (boxes, padding, resident list) is paid once per ~10 K pairs
   const unsigned g = unsigned(std::min<size_t>((max_n + kBlock - 1) / kBlock, 2048));
   if (a.ndom <= 64)
-    k_ao_own_flags<1><<<g, kBlock, 0, s>>>(a, flag);
+    k_ao_own_flags<1><<<g, kBlock, 0, s>>>(a, flag, kmin, bits_a, mode);
   else
-    k_ao_own_flags<4><<<g, kBlock, 0, s>>>(a, flag);
+    k_ao_own_flags<4><<<g, kBlock, 0, s>>>(a, flag, kmin, bits_a, mode);
   return hipGetLastError();
 }
 

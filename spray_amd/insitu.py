@@ -411,6 +411,26 @@ class InsituEngine:
         self.rt._check(lib().spray_rt_insitu_replay_set_ao(self.h, kmin.data_ptr(), pub.data_ptr(),
                                                            kmin.numel()), "replay_set_ao")
 
+    def replay_bits_ao(self, bits=None):
+        """Without bits: the last AO frame's own first-round occlusion bits
+        (uint8 device tensor); with bits: the group's OR, handed back by that
+        SUM in the following frames (spray_rt_insitu_replay_bits_ao)."""
+        import torch
+        n = C.c_size_t(0)
+        if bits is None:
+            self.rt._check(lib().spray_rt_insitu_replay_bits_ao(self.h, None, None, 0, C.byref(n)),
+                           "replay_bits_ao")
+            out = torch.empty(max(n.value, 1), dtype=torch.uint8, device="cuda")[:n.value]
+            self.rt._check(lib().spray_rt_insitu_replay_bits_ao(self.h, None, out.data_ptr(),
+                                                                n.value, C.byref(n)),
+                           "replay_bits_ao")
+            return out
+        self._replay_bits = bits
+        self.rt._check(lib().spray_rt_insitu_replay_bits_ao(self.h, bits.data_ptr(), None,
+                                                            bits.numel(), C.byref(n)),
+                       "replay_bits_ao")
+        return None
+
     def replay_set(self, tmin, lpmin):
         """The group results a replay context's collectives hand back."""
         self._replay = (tmin, lpmin)  # keep the tensors alive
