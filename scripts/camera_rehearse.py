@@ -66,15 +66,17 @@ def comm_ms(world, nu, npu, model):
 def comm_ao_ms(world, nu, model):
     """AO: key MIN (8 B / slot), published normals + colours SUM (16 B /
     slot), the first round's occlusion bits SUM (1 bit per (slot, sample)),
-    occlusion count fields SUM (fb bits per (slot, sample)); rank 0 films
-    (no reduce)"""
+    occlusion count fields SUM (fb bits per (slot, sample)), the per-pixel
+    film slices reduced to rank 0 (12 B per U pixel)"""
     if world == 1:
         return 0.0
     a, bw = LINK[model]
     f = (world - 1) / world
     fb = 2 if world <= 3 else (4 if world <= 15 else 8)
     ar = lambda b: a + 2 * f * b / (bw * 1e6)  # noqa: E731
-    return ar(8 * nu) + ar(16 * nu) + ar(nu * AO_SAMPLES / 8) + ar(nu * AO_SAMPLES * fb / 8)
+    rd = lambda b: a + f * b / (bw * 1e6)  # noqa: E731
+    return (ar(8 * nu) + ar(16 * nu) + ar(nu * AO_SAMPLES / 8) + ar(nu * AO_SAMPLES * fb / 8) +
+            rd(12 * nu / SPP))
 
 
 def main():

@@ -1319,7 +1319,21 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   if (words) COMM(I->tr->allreduce_sum_u8(I, I->afields.as<uint8_t>(), words * 4));
   // ---- 7. the whole film on rank 0; records of each rank's winners
   MARK(6);
-  if (I->rank == 0) HIPCHK(c, launch_rep_ao_film(s, A, image, 1.0 / double(spp)));
+  if (cam) {
+    // camera frames: each rank films a slice of U's pixels, the compact
+    // per-pixel sums are reduced to rank 0, which adds them to its image
+    const size_t npu = nc / size_t(spp);
+    GROW(I->ccomp, npu * 12 + 12);
+    HIPCHK(c, hipMemsetAsync(I->ccomp.p, 0, npu * 12, s));
+    const size_t q0 = npu * size_t(I->rank) / size_t(I->world);
+    const size_t q1 = npu * size_t(I->rank + 1) / size_t(I->world);
+    HIPCHK(c, launch_rep_ao_film_pix(s, A, spp, q0, q1, I->ccomp.as<float>(), 1.0 / double(spp)));
+    if (npu) COMM(I->tr->reduce_f32(I, I->ccomp.as<float>(), npu * 3, 0));
+    if (I->rank == 0 && npu)
+      HIPCHK(c, launch_cam_expand(s, I->tu, cam->image_w, I->ccomp.as<float>(), image));
+  } else if (I->rank == 0) {
+    HIPCHK(c, launch_rep_ao_film(s, A, image, 1.0 / double(spp)));
+  }
   if (rec) HIPCHK(c, launch_rep_ao_record(s, A, *rec));
   uint32_t* hp = reinterpret_cast<uint32_t*>(I->h_small + 128);
   HIPCHK(c, hipMemcpyAsync(hp, dcount, 4, hipMemcpyDeviceToHost, s));

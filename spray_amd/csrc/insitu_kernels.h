@@ -165,6 +165,10 @@ hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uin
                                  size_t max_n, const uint8_t* occ, int ns, int fb,
                                  uint32_t* fields);
 hipError_t launch_rep_ao_film(hipStream_t s, const RepAoArgs& a, float* image, double scale);
+// camera frames: the film of U pixels [q0, q1) into compact (3 floats per U
+// pixel; slot j of pixel q = q spp + sample), the other pixels untouched
+hipError_t launch_rep_ao_film_pix(hipStream_t s, const RepAoArgs& a, int spp, size_t q0,
+                                  size_t q1, float* compact, double scale);
 hipError_t launch_rep_ao_record(hipStream_t s, const RepAoArgs& a, const spray_rt_insitu_rec& rec);
 // counts[r] = starts[r + 1] - starts[r], r < world (<= 64)
 hipError_t launch_counts_from_starts(hipStream_t s, const int64_t* starts, int world,

@@ -450,6 +450,83 @@ __global__ __launch_bounds__(kBlock) void k_rep_ao_film(RepAoArgs A, float* __re
   film_runs(image, in, p, any, a0, a1, a2);
 }
 
+// Camera frames: the film of U pixels [q0, q1) (pixel q's slots q spp ..
+// q spp + spp - 1, in order, each slot's samples in order) into compact
+// (3 floats per U pixel, zero elsewhere); the ranks take disjoint slices and
+// the reduce of compact adds zeros, so every pixel's sum is one rank's
+// sequential sum whatever the rank count.
+__global__ __launch_bounds__(kBlock) void k_rep_ao_film_pix(RepAoArgs A, int spp, size_t q0,
+                                                            size_t q1,
+                                                            float* __restrict__ compact,
+                                                            double scale) {
+  const size_t q = q0 + size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (q >= q1) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int sm = 0; sm < spp; ++sm) {
+    const size_t j = q * size_t(spp) + size_t(sm);
+    if (j >= A.nc) break;
+    const spray_rt_hit h = A.hits_all[j];
+    if (h.domain < 0) continue;
+    const int32_t p = A.pix_c[j];
+    const spray_rt_ray* ray = reinterpret_cast<const spray_rt_ray*>(A.rays_c) + j;
+    float kd[3];
+    unpack_rgb(h.color, kd);
+    for (int l = 0; l < A.ns; ++l) {
+      if (!ao_ok(ray, h, p, l, A.ns)) continue;
+      if (rep_ao_occluded(A.fields, j * size_t(A.ns) + l, A.fb)) continue;
+      float L[3];
+      rep_ao_weight(A, j, p, l, kd, L);
+      a0 += float(scale * double(L[0]));
+      a1 += float(scale * double(L[1]));
+      a2 += float(scale * double(L[2]));
+    }
+  }
+  compact[3 * q] = a0;
+  compact[3 * q + 1] = a1;
+  compact[3 * q + 2] = a2;
+}
+
+// The same with one lane per slot when spp is a power of two <= 64: a
+// pixel's spp neighbouring lanes add their sums by a fixed butterfly, and
+// its first lane writes them -- the same bits at every rank count.
+__global__ __launch_bounds__(kBlock) void k_rep_ao_film_slots(RepAoArgs A, int spp, size_t q0,
+                                                              size_t q1,
+                                                              float* __restrict__ compact,
+                                                              double scale) {
+  const size_t j = q0 * size_t(spp) + size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool in = j < q1 * size_t(spp) && j < A.nc;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  if (in) {
+    const spray_rt_hit h = A.hits_all[j];
+    if (h.domain >= 0) {
+      const int32_t p = A.pix_c[j];
+      const spray_rt_ray* ray = reinterpret_cast<const spray_rt_ray*>(A.rays_c) + j;
+      float kd[3];
+      unpack_rgb(h.color, kd);
+      for (int l = 0; l < A.ns; ++l) {
+        if (!ao_ok(ray, h, p, l, A.ns)) continue;
+        if (rep_ao_occluded(A.fields, j * size_t(A.ns) + l, A.fb)) continue;
+        float L[3];
+        rep_ao_weight(A, j, p, l, kd, L);
+        a0 += float(scale * double(L[0]));
+        a1 += float(scale * double(L[1]));
+        a2 += float(scale * double(L[2]));
+      }
+    }
+  }
+  for (int o = 1; o < spp; o <<= 1) {
+    a0 += __shfl_xor(a0, o);
+    a1 += __shfl_xor(a1, o);
+    a2 += __shfl_xor(a2, o);
+  }
+  if (in && j % size_t(spp) == 0) {
+    const size_t q = j / size_t(spp);
+    compact[3 * q] = a0;
+    compact[3 * q + 1] = a1;
+    compact[3 * q + 2] = a2;
+  }
+}
+
 // records of the rays this rank won: the winner's hit record, the spawned
 // samples (ao_ok) and the occluded ones
 __global__ __launch_bounds__(kBlock) void k_rep_ao_record(RepAoArgs A, spray_rt_insitu_rec rec) {
@@ -1039,6 +1116,14 @@ hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uin
 }
 hipError_t launch_rep_ao_film(hipStream_t s, const RepAoArgs& a, float* image, double scale) {
   LAUNCH(a.nc, k_rep_ao_film, a, image, scale);
+}
+hipError_t launch_rep_ao_film_pix(hipStream_t s, const RepAoArgs& a, int spp, size_t q0,
+                                  size_t q1, float* compact, double scale) {
+  if (spp > 0 && spp <= 64 && (spp & (spp - 1)) == 0) {
+    LAUNCH(q1 > q0 ? (q1 - q0) * size_t(spp) : 0, k_rep_ao_film_slots, a, spp, q0, q1, compact,
+           scale);
+  }
+  LAUNCH(q1 > q0 ? q1 - q0 : 0, k_rep_ao_film_pix, a, spp, q0, q1, compact, scale);
 }
 hipError_t launch_rep_ao_record(hipStream_t s, const RepAoArgs& a,
                                 const spray_rt_insitu_rec& rec) {
