@@ -1302,7 +1302,7 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
       HIPCHK(c, launch_occluded_ao_pairs(s, view(c), npair, I->apairs.as<uint32_t>(),
                                          I->arec.as<float>(), I->alv.as<float>(), ns,
                                          dcount + round, I->aocc_p.as<uint8_t>(), nullptr,
-                                         I->aown.as<uint32_t>()));
+                                         I->aown.as<uint32_t>(), I->afields.as<uint32_t>(), fb));
       if (round == 1) {
         // the first round's occlusion over the group: one bit per pair, set
         // only by the pair's home rank, so a SUM of the bytes is their OR
@@ -1312,8 +1312,6 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
         COMM(I->tr->allreduce_sum_u8(I, I->abits.as<uint8_t>(), nbits * 4));
       }
     }
-    HIPCHK(c, launch_rep_ao_scatter(s, I->apairs.as<uint32_t>(), dcount, npair,
-                                    I->aocc_p.as<uint8_t>(), ns, fb, I->afields.as<uint32_t>()));
   }
   // ---- 6. occlusion OR over the group: a SUM of the count fields' bytes
   if (words) COMM(I->tr->allreduce_sum_u8(I, I->afields.as<uint8_t>(), words * 4));

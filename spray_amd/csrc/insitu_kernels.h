@@ -158,12 +158,8 @@ struct RepAoArgs {
 };
 hipError_t launch_rep_ao_publish(hipStream_t s, const RepAoArgs& a);
 hipError_t launch_rep_ao_hits(hipStream_t s, const RepAoArgs& a);
-// fields[(j * ns + l) field] |= 1 for every occluded pair k < *d_count
 // bits[w] bit b = occ[32 w + b] != 0 for k = 32 w + b < n
 hipError_t launch_pack_bits(hipStream_t s, const uint8_t* occ, size_t n, uint32_t* bits);
-hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uint32_t* d_count,
-                                 size_t max_n, const uint8_t* occ, int ns, int fb,
-                                 uint32_t* fields);
 hipError_t launch_rep_ao_film(hipStream_t s, const RepAoArgs& a, float* image, double scale);
 // camera frames: the film of U pixels [q0, q1) into compact (3 floats per U
 // pixel; slot j of pixel q = q spp + sample), the other pixels untouched

@@ -364,34 +364,27 @@ __global__ __launch_bounds__(kBlock) void k_rep_ao_hits(RepAoArgs A) {
                      __int_as_float(hit ? int32_t(key & 0xFFFFull) : -1));
 }
 
-// occlusion of pair k (this rank's domains) into the positional count field
-// of (source, sample): fields of fb bits (a SUM of `world` ones fits), so the
-// SUM all-reduce of their bytes counts the ranks that found an occluder
-__global__ __launch_bounds__(kBlock) void k_rep_ao_scatter(const uint32_t* __restrict__ pairs,
-                                                           const uint32_t* __restrict__ d_count,
-                                                           size_t max_n,
-                                                           const uint8_t* __restrict__ occ,
-                                                           int ns, int fb,
-                                                           uint32_t* __restrict__ fields) {
-  const size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= max_n || k >= *d_count || !occ[k]) return;
-  const uint32_t pr = pairs[k];
-  const size_t pos = size_t(pr >> 5) * uint32_t(ns) + (pr & 31u);
-  const uint32_t per = 32u / uint32_t(fb);
-  atomicOr(fields + pos / per, 1u << (uint32_t(pos % per) * uint32_t(fb)));
-}
-
-// bits[w] bit b = occ[32 w + b] != 0 over [0, n)
+// bits[w] bit b = occ[32 w + b] != 0 over [0, n): thread t reads bytes
+// [16 t, 16 t + 16) as one 16-B load, and the even thread of each pair writes
+// the word of both halves
 __global__ __launch_bounds__(kBlock) void k_pack_bits(const uint8_t* __restrict__ occ, size_t n,
                                                       uint32_t* __restrict__ bits) {
-  const size_t w = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (w >= (n + 31) / 32) return;
-  uint32_t v = 0;
-  for (int b = 0; b < 32; ++b) {
-    const size_t k = 32 * w + size_t(b);
-    if (k < n && occ[k]) v |= 1u << b;
+  const size_t t = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const size_t b0 = 16 * t;
+  uint32_t m = 0;
+  if (b0 + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(occ + b0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m |= uint32_t(((w[q] >> (8 * j)) & 0xFFu) != 0u) << (4 * q + j);
+  } else {
+    for (int j = 0; j < 16; ++j)
+      if (b0 + j < n && occ[b0 + j]) m |= 1u << j;
   }
-  bits[w] = v;
+  const uint32_t hi = __shfl_down(m, 1);  // every lane of the wave takes part
+  if ((t & 1) == 0 && b0 < n) bits[t >> 1] = m | (b0 + 16 < n ? hi << 16 : 0u);
 }
 
 __device__ __forceinline__ bool rep_ao_occluded(const uint32_t* __restrict__ fields, size_t pos,
@@ -1107,12 +1100,7 @@ hipError_t launch_rep_ao_hits(hipStream_t s, const RepAoArgs& a) {
   LAUNCH(a.nc, k_rep_ao_hits, a);
 }
 hipError_t launch_pack_bits(hipStream_t s, const uint8_t* occ, size_t n, uint32_t* bits) {
-  LAUNCH((n + 31) / 32, k_pack_bits, occ, n, bits);
-}
-hipError_t launch_rep_ao_scatter(hipStream_t s, const uint32_t* pairs, const uint32_t* d_count,
-                                 size_t max_n, const uint8_t* occ, int ns, int fb,
-                                 uint32_t* fields) {
-  LAUNCH(max_n, k_rep_ao_scatter, pairs, d_count, max_n, occ, ns, fb, fields);
+  LAUNCH((n + 15) / 16, k_pack_bits, occ, n, bits);
 }
 hipError_t launch_rep_ao_film(hipStream_t s, const RepAoArgs& a, float* image, double scale) {
   LAUNCH(a.nc, k_rep_ao_film, a, image, scale);

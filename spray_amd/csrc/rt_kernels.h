@@ -237,7 +237,8 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
                                     unsigned long long* counters,
-                                    const uint32_t* idx = nullptr);
+                                    const uint32_t* idx = nullptr, uint32_t* fields = nullptr,
+                                    int fb = 0);
 // flag[k] = AO pair k (k < min(*d_count, max_n)) enters a resident domain's
 // box, 0 for the rest of [0, max_n): the replicated AO frame traces only
 // the flagged pairs (idx of launch_occluded_ao_pairs, from

@@ -268,6 +268,10 @@ struct SceneArgs {
   const float4* ao_rec;  // per source ray: (origin, pixel), normal, tangent frame
   const float4* ao_lv;   // local hemisphere sample of (pixel, l) at pixel * ao_ns + l
   int ao_ns;
+  // replicated AO frames: an occluded pair also sets its count field (fb
+  // bits at (source, sample) position source * ao_ns + sample) here
+  uint32_t* ao_fields;
+  int ao_fb;
   // replicated frames: t bits per slot (kEpiKeysShade), the group's minimum
   // t bits per slot (kEpiShadowGen; 0xFFFFFFFF: no hit)
   uint32_t* tkeys;
@@ -345,18 +349,41 @@ __device__ __forceinline__ void wave_lds_sync() {
 // tangent frame from its record and the local hemisphere sample (the double
 // sincos) from the (pixel, l) table, both written by k_spawn_ao_index, so
 // the same bits as the written ray.
-__device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f& b) {
-  const uint32_t pr = A.ao_pairs[k];
+// the pair's operands: its source's record (origin + pixel, normal, tangent
+// frame) and its hemisphere sample
+struct AoSrc {
+  float4 op, n4, x4, y4, l4;
+};
+__device__ __forceinline__ AoSrc ao_load(const SceneArgs& A, uint32_t pr) {
   const uint32_t i = pr >> 5, l = pr & 31u;
   const float4* rec = A.ao_rec + 4 * size_t(i);
-  const float4 op = rec[0], n4 = rec[1], x4 = rec[2], y4 = rec[3];
-  const float4 l4 = A.ao_lv[size_t(__float_as_uint(op.w)) * uint32_t(A.ao_ns) + l];
-  const float N[3] = {n4.x, n4.y, n4.z}, ax[3] = {x4.x, x4.y, x4.z}, ay[3] = {y4.x, y4.y, y4.z};
-  const float lv[3] = {l4.x, l4.y, l4.z};
+  AoSrc o;
+  o.op = rec[0];
+  o.n4 = rec[1];
+  o.x4 = rec[2];
+  o.y4 = rec[3];
+  o.l4 = A.ao_lv[size_t(__float_as_uint(o.op.w)) * uint32_t(A.ao_ns) + l];
+  return o;
+}
+__device__ __forceinline__ void ao_ray(const AoSrc& o, v4f& a, v4f& b) {
+  const float N[3] = {o.n4.x, o.n4.y, o.n4.z}, ax[3] = {o.x4.x, o.x4.y, o.x4.z},
+              ay[3] = {o.y4.x, o.y4.y, o.y4.z};
+  const float lv[3] = {o.l4.x, o.l4.y, o.l4.z};
   float w[3], pdf;
   hemisphere_apply(lv, N, ax, ay, w, pdf);
-  a = v4f{op.x, op.y, op.z, kRayEpsilon};
+  a = v4f{o.op.x, o.op.y, o.op.z, kRayEpsilon};
   b = v4f{w[0], w[1], w[2], kInf};
+}
+__device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f& b) {
+  ao_ray(ao_load(A, A.ao_pairs[k]), a, b);
+}
+// the count field of occluded pair k (the fields are zeroed per frame; the
+// group's SUM of their bytes counts the ranks that found an occluder)
+__device__ __forceinline__ void ao_field(const SceneArgs& A, size_t k) {
+  const uint32_t pr = A.ao_pairs[k];
+  const size_t pos = size_t(pr >> 5) * uint32_t(A.ao_ns) + (pr & 31u);
+  const uint32_t per = 32u / uint32_t(A.ao_fb);
+  atomicOr(A.ao_fields + pos / per, 1u << (uint32_t(pos % per) * uint32_t(A.ao_fb)));
 }
 
 // whether AO ray k enters a resident domain's box (replicated AO frames):
@@ -364,17 +391,22 @@ __device__ __forceinline__ void ao_gen(const SceneArgs& A, size_t k, v4f& a, v4f
 // the fast slab on its kTopPad-padded copy (spad) -- the pair the top-level
 // walk itself uses for its internal boxes, a superset of the exact test --
 // so most boxes cost no double-precision test
-__device__ __forceinline__ bool ao_own(const SceneArgs& A, size_t k, const float* sbox,
-                                       const float* spad, const uint8_t* sres, int nres) {
+// sun: the union of the resident padded boxes, tested first -- its slab
+// accepts every ray a resident padded box accepts (the slab is monotone in
+// the bounds), so a ray it rejects enters no resident box; the exact test's
+// inverse direction is formed only once a padded box passes
+__device__ __forceinline__ bool ao_own(const AoSrc& o, const float* sbox, const float* spad,
+                                       const float* sun, const uint8_t* sres, int nres) {
   v4f a, b;
-  ao_gen(A, k, a, b);
+  ao_ray(o, a, b);
   const Ray r = make_ray(a.x, a.y, a.z, b.x, b.y, b.z);
-  const DRay dr = make_dray(a.x, a.y, a.z, b.x, b.y, b.z);
+  float tm;
+  if (!slab(r, sun[0], sun[1], sun[2], sun[3], sun[4], sun[5], 0.f, kInf, tm)) return false;
   for (int q = 0; q < nres; ++q) {
     const int d = int(sres[q]);
     const float* pb = spad + 6 * d;
-    float tm;
     if (!slab(r, pb[0], pb[1], pb[2], pb[3], pb[4], pb[5], 0.f, kInf, tm)) continue;
+    const DRay dr = make_dray(a.x, a.y, a.z, b.x, b.y, b.z);
     if (aabb_ref(sbox + 6 * d, dr, tm)) return true;
   }
   return false;
@@ -494,6 +526,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     }
     if (ANY) {
       occ[i] = occluded ? 1 : 0;
+      if (EPI == kEpiAoGen && A.ao_fields && occluded) ao_field(A, i);
     } else {
       float4 h0, h1, h2;
       if (best_dom < 0) {
@@ -755,6 +788,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   }
   if (ANY) {
     if (valid) A.occ[i] = occluded ? 1 : 0;
+    if (EPI == kEpiAoGen && valid && A.ao_fields && occluded) ao_field(A, i);
     return;
   }
   float4 h0, h1, h2;  // invalid lanes: best_dom < 0, never stored
@@ -2591,8 +2625,10 @@ hipError_t launch_scene_cam_shadows(hipStream_t s, const SceneView& v, const Cam
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
                                     const uint32_t* pairs, const float* rec, const float* lv,
                                     int nsamples, const uint32_t* d_count, uint8_t* occ,
-                                    unsigned long long* counters, const uint32_t* idx) {
+                                    unsigned long long* counters, const uint32_t* idx,
+                                    uint32_t* fields, int fb) {
   if (max_n == 0) return hipSuccess;
+  if (fields && fb != 2 && fb != 4 && fb != 8) return hipErrorInvalidValue;
   SceneArgs a = scene_args(v, nullptr, max_n);
   a.d_count = d_count;
   a.idx = idx;
@@ -2602,6 +2638,8 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
   a.ao_rec = reinterpret_cast<const float4*>(rec);
   a.ao_lv = reinterpret_cast<const float4*>(lv);
   a.ao_ns = nsamples;
+  a.ao_fields = fields;
+  a.ao_fb = fb;
   return launch_scene_w<true, kEpiAoGen>(s, a, v);
 }
 
@@ -2627,17 +2665,24 @@ __global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint
   // the AO rays start)
   __shared__ float spad[6 * 64 * W];
   __shared__ uint8_t sres[64 * W];
+  __shared__ float sun[6];  // union of the resident padded boxes
   __shared__ int nres;
   __shared__ float gmax;
+  __shared__ float wg[kBlock / 64];
   for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock) sbox[k] = A.boxes[k];
   {
     float g = 0.f;
     for (int k = threadIdx.x; k < 6 * A.ndom; k += kBlock)
       if (isfinite(A.boxes[k])) g = fmaxf(g, fabsf(A.boxes[k]));
     for (int o = 32; o > 0; o >>= 1) g = fmaxf(g, __shfl_xor(g, o));
-    __shared__ float wg[kBlock / 64];
     if ((threadIdx.x & 63) == 0) wg[threadIdx.x >> 6] = g;
+    // the resident domains, one thread per domain (their bits in domain order)
+    if (threadIdx.x < 2 * W) resm[threadIdx.x] = 0u;
     __syncthreads();
+    for (int d = threadIdx.x; d < A.ndom; d += kBlock) {
+      const float4 t = ld4(A.domtrav, d);
+      if (__float_as_uint(t.x) | __float_as_uint(t.y)) atomicOr(&resm[d >> 5], 1u << (d & 31));
+    }
     if (threadIdx.x == 0) {
       float m = 0.f;
       for (int w = 0; w < kBlock / 64; ++w) m = fmaxf(m, wg[w]);
@@ -2654,33 +2699,53 @@ __global__ __launch_bounds__(kBlock) void k_ao_own_flags(const SceneArgs A, uint
     spad[6 * d + j] = fin ? lo - p : lo;
     spad[6 * d + 3 + j] = fin ? hi + p : hi;
   }
-  if (threadIdx.x == 0) {
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the resident list in domain order, their union
     int q = 0;
-    for (int w = 0; w < 2 * W; ++w) resm[w] = 0u;
-    for (int d = 0; d < A.ndom; ++d) {
-      const float4 t = ld4(A.domtrav, d);
-      if (__float_as_uint(t.x) | __float_as_uint(t.y)) {
+    float u[6] = {kInf, kInf, kInf, -kInf, -kInf, -kInf};
+    for (int w = 0; w < 2 * W; ++w) {
+      uint32_t b = resm[w];
+      while (b) {
+        const int d = 32 * w + __ffs(b) - 1;
+        b &= b - 1;
         sres[q++] = uint8_t(d);
-        resm[d >> 5] |= 1u << (d & 31);
+        for (int j = 0; j < 3; ++j) {
+          u[j] = fminf(u[j], spad[6 * d + j]);
+          u[3 + j] = fmaxf(u[3 + j], spad[6 * d + 3 + j]);
+        }
       }
     }
+    for (int j = 0; j < 6; ++j) sun[j] = u[j];
     nres = q;
   }
   __syncthreads();
   const size_t n = A.d_count ? min(size_t(*A.d_count), A.M) : A.M;
-  for (size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x; k < A.M;
-       k += size_t(gridDim.x) * kBlock) {
+  // the grid-stride loop is a chain of dependent loads per pair (pair ->
+  // key minimum / record -> sample): the next pair is loaded one iteration
+  // ahead, and a mode-2 pair's record and sample are loaded beside its key
+  // minimum, before the flag says whether its ray is needed (16 pairs share
+  // a record, 8 sources of a pixel its samples: mostly cache hits)
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  size_t k = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  uint32_t pr_next = k < n ? A.ao_pairs[k] : 0u;
+  for (; k < A.M; k += stride) {
+    const uint32_t pr = pr_next;
+    pr_next = k + stride < n ? A.ao_pairs[k + stride] : 0u;
     bool f = false;
     if (k < n) {
       if (mode == 0) {
-        f = ao_own(A, k, sbox, spad, sres, nres);
+        f = ao_own(ao_load(A, pr), sbox, spad, sun, sres, nres);
       } else {
-        const uint32_t d = uint32_t(kmin[A.ao_pairs[k] >> 5] & 0xFFFFu);
+        const uint64_t km = kmin[pr >> 5];
+        const uint32_t bw = mode == 2 ? bits_a[k >> 5] : 0u;
+        AoSrc o{};
+        if (mode == 2) o = ao_load(A, pr);
+        const uint32_t d = uint32_t(km & 0xFFFFu);
         const bool home = d < uint32_t(A.ndom) && ((resm[d >> 5] >> (d & 31)) & 1u);
         if (mode == 1)
           f = home;
         else
-          f = !home && !((bits_a[k >> 5] >> (k & 31)) & 1u) && ao_own(A, k, sbox, spad, sres, nres);
+          f = !home && !((bw >> (k & 31)) & 1u) && ao_own(o, sbox, spad, sun, sres, nres);
       }
     }
     flag[k] = f ? 1 : 0;
