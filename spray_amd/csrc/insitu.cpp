@@ -1237,6 +1237,16 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   GROW(I->afields, words * 4 + 4);
   GROW(I->acount, 16);
   if (rec) GROW(I->rhit_c, nc * 48 + 48);
+  if (cam) GROW(I->ccomp, nc / size_t(spp) * 12 + 12);
+  {  // the frame's counters, count fields, occlusion bytes and film sums in one launch
+    ClearSeg cs[kClearSegs];
+    int q = 0;
+    cs[q++] = {I->acount.p, 16, 0};
+    cs[q++] = {I->afields.p, words * 4, 0};
+    cs[q++] = {I->aocc_p.p, npair, 0};
+    if (cam) cs[q++] = {I->ccomp.p, nc / size_t(spp) * 12, 0};
+    HIPCHK(c, launch_clear(s, cs, q));
+  }
   RepAoArgs A{};
   A.nc = nc;
   A.rank = I->rank;
@@ -1268,8 +1278,6 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
   // ---- 5. every hit's AO rays (the same pairs on every rank), own any hit
   MARK(4);
   HIPCHK(c, launch_rep_ao_hits(s, A));
-  HIPCHK(c, hipMemsetAsync(dcount, 0, 4, s));
-  HIPCHK(c, hipMemsetAsync(I->afields.p, 0, words * 4, s));
   if (nc) {
     HIPCHK(c, launch_spawn_ao_pairs(s, reinterpret_cast<const spray_rt_ray*>(A.rays_c), A.hits_all,
                                     A.pix_c, nc, ns, npix, I->apairs.as<uint32_t>(),
@@ -1290,7 +1298,6 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
     size_t tsel = 0;
     HIPCHK(c, launch_select_flagged(s, nullptr, npair, nullptr, nullptr, nullptr, &tsel));
     GROW(I->asel_tmp, tsel);
-    HIPCHK(c, hipMemsetAsync(I->aocc_p.p, 0, npair, s));
     const uint64_t* kmin = I->rkeys_c.as<uint64_t>();
     for (int round = 1; round <= 2; ++round) {
       HIPCHK(c, launch_ao_own_flags(s, view(c), npair, I->apairs.as<uint32_t>(),
@@ -1321,8 +1328,6 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
     // camera frames: each rank films a slice of U's pixels, the compact
     // per-pixel sums are reduced to rank 0, which adds them to its image
     const size_t npu = nc / size_t(spp);
-    GROW(I->ccomp, npu * 12 + 12);
-    HIPCHK(c, hipMemsetAsync(I->ccomp.p, 0, npu * 12, s));
     const size_t q0 = npu * size_t(I->rank) / size_t(I->world);
     const size_t q1 = npu * size_t(I->rank + 1) / size_t(I->world);
     HIPCHK(c, launch_rep_ao_film_pix(s, A, spp, q0, q1, I->ccomp.as<float>(), 1.0 / double(spp)));
@@ -1471,9 +1476,23 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   uint64_t* keys = I->rkeys_c.as<uint64_t>();
   uint32_t* tk = I->rtk.as<uint32_t>();      // own t bits (0xFFFFFFFF: no own hit)
   uint32_t* tmin = I->ctmin.as<uint32_t>();  // the group's minimum
-  HIPCHK(c, hipMemsetAsync(tk, 0xFF, nu * 4, s));
+  // the frame's buffers cleared in one launch (t bits, list positions,
+  // occlusion, shadow counters, film sums, winners, the keyed launch's queue
+  // heads): the per-buffer memsets cost ~4 us each at N = 8
+  uint32_t* heads1 = c->d_heads + kHeadsBytes / sizeof(uint32_t);
+  {
+    ClearSeg cs[kClearSegs];
+    int ns = 0;
+    cs[ns++] = {tk, nu * 4, 0xFF};
+    if (split) cs[ns++] = {I->rlp.p, nu, 0xFF};
+    cs[ns++] = {I->rocc.p, nu, 0};
+    cs[ns++] = {I->rnsh.p, kWinCounterBytes, 0};
+    cs[ns++] = {I->ccomp.p, npu * 12, 0};
+    cs[ns++] = {heads1, kHeadsBytes, 0};
+    if (rec) cs[ns++] = {I->rwin.p, nu, 0};
+    HIPCHK(c, launch_clear(s, cs, ns));
+  }
   if (!split) HIPCHK(c, launch_fill_u64(s, keys, nu, kInsituMissKey));
-  if (rec) HIPCHK(c, hipMemsetAsync(I->rwin.p, 0, nu, s));
   // a rank with few domains tests their boxes in the lanes instead of the
   // top-level walk (the list positions then computed for its winners only)
   int nres = 0;
@@ -1484,7 +1503,7 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   MARK(2);
   HIPCHK(c, launch_scene_cam_keyed(s, view(c), F, I->te, shade10,
                                    rec ? I->rhit_c.as<spray_rt_hit>() : nullptr, keys, tk,
-                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>(), defer));
+                                   I->rsw.as<float>(), I->rsvalid.as<uint8_t>(), defer, heads1));
   // ---- the group's minimum t of every U slot (then the list position)
   uint8_t* lp = nullptr;
   uint64_t* kmin = nullptr;
@@ -1492,7 +1511,6 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
     if (nu) COMM(I->tr->allreduce_min_u32(I, tk, tmin, nu, 0, s));
     MARK(3);
     lp = I->rlp.as<uint8_t>();
-    HIPCHK(c, hipMemsetAsync(lp, 0xFF, nu, s));
     HIPCHK(c, launch_cam_lp(s, I->te, spp, keys, tk, tmin, lp, defer ? &F : nullptr,
                             c->d_boxes, c->d_tlas, c->ntlas));
     if (nu) {
@@ -1518,12 +1536,10 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   }
   // ---- the shadow ray of every hit in S from the minimum t, own any hit
   MARK(4);
-  HIPCHK(c, hipMemsetAsync(I->rocc.p, 0, nu, s));
   HIPCHK(c, launch_scene_cam_shadows(s, view(c), F, I->ts, tmin, shade10, I->rocc.as<uint8_t>(),
                                      direct));
   // ---- the winners among E's slots, their shadows counted
   MARK(5);
-  HIPCHK(c, hipMemsetAsync(I->rnsh.p, 0, kWinCounterBytes, s));
   if (split && nu) HIPCHK(c, hipStreamWaitEvent(s, I->ev_lp1, 0));
   HIPCHK(c, launch_cam_win(s, I->te, spp, keys, tk, tmin, lp, kmin, I->rsvalid.as<uint8_t>(),
                            I->rwin.as<uint8_t>(), I->rsflag.as<uint8_t>(),
@@ -1542,7 +1558,6 @@ int trace_camera_pt(spray_rt_insitu* I, const spray_rt_shader* P, const CamFrame
   I->st[0] += pay;
   I->st[1] += pay;
   if (npu) {
-    HIPCHK(c, hipMemsetAsync(I->ccomp.p, 0, npu * 12, s));
     HIPCHK(c, launch_cam_film(s, I->te, spp, I->ccomp.as<float>(), I->rsw.as<float>(),
                               I->rsflag.as<uint8_t>(), I->rocc.as<uint8_t>(), scale));
     COMM(I->tr->reduce_f32(I, I->ccomp.as<float>(), npu * 3, 0));

@@ -316,7 +316,7 @@ int spray_rt::detail::scene_common(spray_rt_ctx* c, const void* rays, size_t M,
   if (M && (!rays || !out)) return fail(c, SPRAY_RT_ERR_ARG, "null buffer");
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->d_heads)
-    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), kHeadsBytes));
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_heads), 2 * kHeadsBytes));
   return prepare(c);
 }
 

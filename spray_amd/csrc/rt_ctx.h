@@ -72,7 +72,9 @@ struct spray_rt_ctx {
   void* d_stage3 = nullptr;
   size_t stage3_cap = 0;
   uint32_t* d_block_counts = nullptr;
-  uint32_t* d_heads = nullptr;  // work-queue heads of the persistent launches
+  // work-queue heads of the persistent launches: [0, kHeadsBytes) zeroed by
+  // each launch, [kHeadsBytes, 2 kHeadsBytes) zeroed by a frame's launch_clear
+  uint32_t* d_heads = nullptr;
   void* d_sel = nullptr;        // selected indices + count + select scratch
   size_t sel_cap = 0;
   size_t block_cap = 0;

@@ -221,10 +221,21 @@ struct CamFrame {
 // untouched).  defer_lp (split keys, at most kDirectRes resident domains):
 // a lane tests the resident boxes instead of walking the top-level tree,
 // and the keys' list-position byte stays 0 for launch_cam_lp
+// heads (optional): kHeadsBytes of queue heads the caller has zeroed (its
+// frame's launch_clear), used instead of the context's heads and their memset
 hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFrame& F,
                                   const CamTable& T, const float* shade10, spray_rt_hit* hits,
                                   uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv,
-                                  bool defer_lp);
+                                  bool defer_lp, uint32_t* heads = nullptr);
+// Several buffers set to a byte value in one launch (a frame's clears: one
+// kernel instead of a memset -- often two fill kernels -- per buffer)
+struct ClearSeg {
+  void* p;
+  size_t bytes;
+  int value;
+};
+constexpr int kClearSegs = 8;
+hipError_t launch_clear(hipStream_t s, const ClearSeg* segs, int n);
 // any hit of the point-light shadow ray of every hit in T's pixels (t bits
 // tmin[u]; none: 0xFFFFFFFF), the eye ray regenerated in the lane; direct:
 // the resident boxes tested instead of the top-level walk (<= kDirectRes)

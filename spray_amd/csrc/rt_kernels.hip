@@ -248,6 +248,7 @@ struct SceneArgs {
   unsigned long long* counters;
   uint32_t* heads;  // kQueues queue heads, 32 words apart (persistent launch)
   int persist;      // any hit: persistent waves (set by the launcher)
+  int heads_ready;  // heads zeroed by the caller (no memset before the launch)
   // fused PT shadow spawn (closest hit): positional output
   ShadePt shade;
   spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
@@ -2138,7 +2139,7 @@ static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
   hipError_t e = hipSuccess;
-  if (kPersist) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
+  if (kPersist && !a.heads_ready) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
   if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) &&
       a.sh_count)
     e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
@@ -2597,9 +2598,13 @@ static SceneArgs cam_args(const SceneView& v, const CamFrame& F, const CamTable&
 hipError_t launch_scene_cam_keyed(hipStream_t s, const SceneView& v, const CamFrame& F,
                                   const CamTable& T, const float* shade10, spray_rt_hit* hits,
                                   uint64_t* keys, uint32_t* tkeys, float* sw, uint8_t* sv,
-                                  bool defer_lp) {
+                                  bool defer_lp, uint32_t* heads) {
   if (T.npix == 0) return hipSuccess;
   SceneArgs a = cam_args(v, F, T);
+  if (heads) {
+    a.heads = heads;
+    a.heads_ready = 1;
+  }
   a.direct_res = defer_lp ? 1 : 0;
   a.hits = hits;
   a.keys = keys;
@@ -2620,6 +2625,43 @@ hipError_t launch_scene_cam_shadows(hipStream_t s, const SceneView& v, const Cam
   a.occ = occ;
   a.shade = shade_from10(shade10);
   return launch_scene_w<true, kEpiShadowGen>(s, a, v);
+}
+
+struct ClearList {
+  ClearSeg seg[kClearSegs];
+  int n;
+};
+// each segment: 16-B stores over its 16-B aligned body (the buffers are
+// allocation-aligned), bytes for the rest
+__global__ __launch_bounds__(kBlock) void k_clear(const ClearList L) {
+  const size_t tid = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  const size_t nth = size_t(gridDim.x) * kBlock;
+  for (int q = 0; q < L.n; ++q) {
+    uint8_t* p = static_cast<uint8_t*>(L.seg[q].p);
+    const size_t bytes = L.seg[q].bytes;
+    const uint32_t b = uint32_t(L.seg[q].value) & 0xFFu;
+    const uint32_t w = b * 0x01010101u;
+    const uint4 v = make_uint4(w, w, w, w);
+    const size_t nv = bytes / 16;
+    for (size_t i = tid; i < nv; i += nth) reinterpret_cast<uint4*>(p)[i] = v;
+    for (size_t i = 16 * nv + tid; i < bytes; i += nth) p[i] = uint8_t(b);
+  }
+}
+
+hipError_t launch_clear(hipStream_t s, const ClearSeg* segs, int n) {
+  if (n < 0 || n > kClearSegs) return hipErrorInvalidValue;
+  ClearList L{};
+  size_t total = 0;
+  for (int q = 0; q < n; ++q) {
+    if (segs[q].bytes && (!segs[q].p || (reinterpret_cast<uintptr_t>(segs[q].p) & 15u)))
+      return hipErrorInvalidValue;
+    L.seg[L.n++] = segs[q];
+    total += segs[q].bytes;
+  }
+  if (total == 0) return hipSuccess;
+  const unsigned g = unsigned(std::min<size_t>((total / 16 + kBlock - 1) / kBlock, 4096));
+  k_clear<<<g, kBlock, 0, s>>>(L);
+  return hipGetLastError();
 }
 
 hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t max_n,
