@@ -319,6 +319,11 @@ constexpr int kEpiShadow = 3; // + PT spawn and the shadow ray's any hit, same l
 constexpr int kEpiShadowFrame = 4;
 // any hit of AO rays generated in the lane from (source ray, sample) pairs
 constexpr int kEpiAoGen = 5;
+// kEpiAoGen for replicated AO frames: an occluded pair also sets its count
+// field (A.ao_fields) -- its own instantiation, so the one-GPU AO kernel
+// carries none of it
+constexpr int kEpiAoGenF = 8;
+constexpr bool ao_epi(int e) { return e == kEpiAoGen || e == kEpiAoGenF; }
 // replicated in-situ frames (insitu.cpp trace_replicated): slot j traces ray
 // idx[j] and writes its results at j.  kEpiKeysShade: the keyed closest hit
 // over the rank's domains + the t bits (tkeys) + the point-light shading of
@@ -428,7 +433,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
   uint8_t* __restrict__ occ = A.occ;
   {
     v4f a, b;
-    if (EPI == kEpiAoGen) {
+    if (ao_epi(EPI)) {
       ao_gen(A, i, a, b);
     } else if (rin) {  // a replicated frame's ray (rep_ray), results at i
       a = v4f{rin[0], rin[1], rin[2], kRayEpsilon};
@@ -527,7 +532,7 @@ __device__ __forceinline__ void scene_ray(const SceneArgs& A, size_t i,
     }
     if (ANY) {
       occ[i] = occluded ? 1 : 0;
-      if (EPI == kEpiAoGen && A.ao_fields && occluded) ao_field(A, i);
+      if (EPI == kEpiAoGenF && occluded) ao_field(A, i);
     } else {
       float4 h0, h1, h2;
       if (best_dom < 0) {
@@ -789,7 +794,7 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
   }
   if (ANY) {
     if (valid) A.occ[i] = occluded ? 1 : 0;
-    if (EPI == kEpiAoGen && valid && A.ao_fields && occluded) ao_field(A, i);
+    if (EPI == kEpiAoGenF && valid && occluded) ao_field(A, i);
     return;
   }
   float4 h0, h1, h2;  // invalid lanes: best_dom < 0, never stored
@@ -1132,7 +1137,7 @@ __device__ __forceinline__ void shadow_push(const SceneArgs& A, ShadowQueue& q, 
 // and per-lane for the others (any-hit only; the counting variants always
 // walk per lane, the canonical order the counts are defined on).
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
-__global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN : SPRAY_WAVES_AH)
+__global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SPRAY_WAVES_AH)
                                      : (W == 1 && STK == 16
                                             ? (EPI == kEpiShadow || EPI == kEpiShadowFrame ? SPRAY_WAVES_SHADOW
                                                : EPI == kEpiKeysShade ? SPRAY_WAVES_KEYED
@@ -1146,7 +1151,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (EPI == kEpiAoGen ? SPRAY_WAVES_AOGEN
   constexpr bool kLaneStack = !kPacket || kAdaptive;
   // the AO any hit's 4-wide walk keeps kLStk entries in LDS and the rest of
   // its kQ4Stack in private memory (LDS for more resident blocks)
-  constexpr int kLStk = (ANY && EPI == kEpiAoGen && !COUNT && SPRAY_AH_QNODES &&
+  constexpr int kLStk = (ANY && ao_epi(EPI) && !COUNT && SPRAY_AH_QNODES &&
                          SPRAY_AH_WW && SPRAY_AOGEN_LSTK < STK)
                             ? SPRAY_AOGEN_LSTK
                             : STK;
@@ -2157,7 +2162,7 @@ static hipError_t launch_scene_c(hipStream_t s, const SceneArgs& a, int coherenc
   if (a.counters) return launch_scene_t<W, ANY, true, EPI, STK, 0>(s, a);
   // the fused spawn / keyed closest-hit forms serve camera rays: packets;
   // generated AO rays (hemispheres) walk per lane
-  if constexpr (ANY && EPI == kEpiAoGen) {
+  if constexpr (ANY && ao_epi(EPI)) {
     return launch_scene_t<W, ANY, false, EPI, STK, 0>(s, a);
   } else if constexpr (rep_epi(EPI)) {  // camera rays and point-light shadows
     return launch_scene_t<W, ANY, false, EPI, STK, 1>(s, a);
@@ -2682,7 +2687,7 @@ hipError_t launch_occluded_ao_pairs(hipStream_t s, const SceneView& v, size_t ma
   a.ao_ns = nsamples;
   a.ao_fields = fields;
   a.ao_fb = fb;
-  return launch_scene_w<true, kEpiAoGen>(s, a, v);
+  return fields ? launch_scene_w<true, kEpiAoGenF>(s, a, v) : launch_scene_w<true, kEpiAoGen>(s, a, v);
 }
 
 // Replicated AO frames: flag[k] = AO pair k (k < min(*d_count, M)) enters

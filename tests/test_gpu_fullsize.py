@@ -283,8 +283,7 @@ def _rep_rank_main(rank, world, port, out, mode, kind="pt"):
     import spray_amd
     from spray_amd import insitu
     from spray_amd.engine import host_parse_scene, host_scene_bsdfs
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         boxes, lights = host_parse_scene(WAVELETS64, SCENES)
         bound = np.concatenate([boxes[:, :3].min(0), boxes[:, 3:].max(0)])
@@ -314,13 +313,10 @@ def _rep_rank_main(rank, world, port, out, mode, kind="pt"):
 
 
 def _run_replicated(world, mode, kind):
-    import socket
     import tempfile
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     with tempfile.TemporaryDirectory() as out:
+        # file:// rendezvous in the run's own directory: no TCP port to collide
+        port = os.path.join(out, "rdv")
         torch.multiprocessing.spawn(_rep_rank_main, args=(world, port, out, mode, kind),
                                     nprocs=world)
         return [dict(np.load(os.path.join(out, "r%d.npz" % r))) for r in range(world)]

@@ -6,7 +6,6 @@ host transport with 2 and 8 processes sharing the box's one GPU -- against
 the whole-scene oracle: every shaded sample bit-exact, totals exact, the
 composited image within summation-order tolerance."""
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -83,11 +82,13 @@ def test_route_and_keys_match_oracle(spray, oracle):
     rt.close()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
+def _rendezvous_file():
+    """A fresh rendezvous file for a gloo group: file:// init needs no TCP
+    port (a probed free port can be taken by another process before the
+    store binds it: EADDRINUSE)."""
+    fd, p = tempfile.mkstemp(prefix="spray_rdv_")
+    os.close(fd)
+    os.unlink(p)
     return p
 
 
@@ -227,8 +228,7 @@ def _gpu_rank_main(rank, world, port, out, case, one_owner=False, replicated=Fal
     sys.path.insert(0, here)
     sys.path.insert(0, os.path.dirname(here))
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         res = _engine_rank(rank, world, case, "host", dist, one_owner, replicated, mode, scene,
                            owner)
@@ -247,7 +247,7 @@ def test_engine_ranks_on_gpu(oracle, world, case):
     (one GPU cannot hold an RCCL group of several ranks)."""
     import pickle
     with tempfile.TemporaryDirectory() as out:
-        torch.multiprocessing.spawn(_gpu_rank_main, args=(world, _free_port(), out, case),
+        torch.multiprocessing.spawn(_gpu_rank_main, args=(world, _rendezvous_file(), out, case),
                                     nprocs=world)
         res = []
         for r in range(world):
@@ -266,7 +266,7 @@ def test_engine_two_ranks_one_owner(oracle):
     import pickle
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
-                                    args=(2, _free_port(), out, "pt1", True), nprocs=2)
+                                    args=(2, _rendezvous_file(), out, "pt1", True), nprocs=2)
         res = []
         for r in range(2):
             with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
@@ -296,7 +296,7 @@ def test_engine_replicated_frame_ranks(oracle, world, mode, case, monkeypatch):
         case = "pt1"
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
-                                    args=(world, _free_port(), out, case, False, True, mode),
+                                    args=(world, _rendezvous_file(), out, case, False, True, mode),
                                     nprocs=world)
         res = []
         for r in range(world):
@@ -330,7 +330,7 @@ def test_engine_camera_frame_ranks(oracle, world, mode, case, monkeypatch):
         case = "pt1"
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
-                                    args=(world, _free_port(), out, case, False, "camera", mode),
+                                    args=(world, _rendezvous_file(), out, case, False, "camera", mode),
                                     nprocs=world)
         res = []
         for r in range(world):
@@ -374,7 +374,7 @@ def test_engine_camera_frame_cross_rank_ties(oracle, split, monkeypatch, tmp_pat
     owner = [0, 1, 1, 0]
     with tempfile.TemporaryDirectory() as out:
         torch.multiprocessing.spawn(_gpu_rank_main,
-                                    args=(2, _free_port(), out, "pt1", False, "camera", 0,
+                                    args=(2, _rendezvous_file(), out, "pt1", False, "camera", 0,
                                           scene, owner),
                                     nprocs=2)
         res = []

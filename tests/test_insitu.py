@@ -7,7 +7,6 @@ every shaded sample's winning hit and shadow bits bit-exact, the ray totals
 exact, the image within float-summation-order tolerance.  The engine's own
 protocol runs the same cases on the GPU (tests/test_gpu_insitu.py)."""
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -126,11 +125,13 @@ def test_horizontal_stripe():
     assert [insitu.horizontal_stripe(4, r, t)[3] for r in range(4)] == [1, 1, 0, 0]
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
+def _rendezvous_file():
+    """A fresh rendezvous file for a gloo group: file:// init needs no TCP
+    port (a probed free port can be taken by another process before the
+    store binds it: EADDRINUSE)."""
+    fd, p = tempfile.mkstemp(prefix="spray_rdv_")
+    os.close(fd)
+    os.unlink(p)
     return p
 
 
@@ -149,9 +150,9 @@ def _rank_main(rank, world, port, out, case, mode=0, replicated=False):
     import torch.distributed as dist
     from oracle import insitu_ref, pyoracle as po
     import insitu_helpers as H
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method="file://" + port, rank=rank,
+                                world_size=world)
     try:
         kind, bounces, samples, img, spp = CASES[case]
         boxes, bound = scene_boxes()
@@ -184,7 +185,7 @@ def test_insitu_protocol_gloo(oracle, world, case, mode, replicated=False):
     import pickle
     import insitu_helpers as H
     with tempfile.TemporaryDirectory() as out:
-        port = _free_port()
+        port = _rendezvous_file()
         if world == 1:
             _rank_main(0, 1, port, out, case, mode, replicated)
         else:
