@@ -50,6 +50,52 @@ AO_SAMPLES = 16
 LINK = {"cons": (0.030, 300.0), "opt": (0.015, 500.0)}
 
 
+def balanced_partition(boxes, w, world, cam, mode):
+    """Experimental equal-count partitions balancing weights w: hitlpt =
+    largest weight first to the lightest rank with room; hitaxis = recursive
+    equal-count splits of the projected box centres, each along the screen
+    axis whose halves' weights differ least."""
+    n = len(boxes)
+    per = n // world
+    if mode == "hitlpt":
+        owner = np.zeros(n, np.int32)
+        load = np.zeros(world)
+        cnt = np.zeros(world, np.int64)
+        for d in np.argsort(-w, kind="stable"):
+            r = min((k for k in range(world) if cnt[k] < per), key=lambda k: (load[k], k))
+            owner[d] = r
+            load[r] += w[d]
+            cnt[r] += 1
+        return owner
+    pos = np.asarray(cam["pos"], np.float64)
+    f = np.asarray(cam["lookat"], np.float64) - pos
+    f /= np.linalg.norm(f)
+    rt = np.cross(f, np.asarray(cam["up"], np.float64))
+    rt /= np.linalg.norm(rt)
+    up = np.cross(rt, f)
+    c = 0.5 * (boxes[:, :3] + boxes[:, 3:]).astype(np.float64) - pos
+    z = c @ f
+    xy = np.stack([(c @ rt) / z, (c @ up) / z], 1)
+    owner = np.zeros(n, np.int32)
+
+    def split(ids, r0, k):
+        if k == 1:
+            owner[ids] = r0
+            return
+        best = None
+        for ax in (0, 1):
+            o = ids[np.argsort(xy[ids, ax], kind="stable")]
+            h = len(o) // 2
+            diff = abs(w[o[:h]].sum() - w[o[h:]].sum())
+            if best is None or diff < best[0]:
+                best = (diff, o[:h], o[h:])
+        split(best[1], r0, k // 2)
+        split(best[2], r0 + k // 2, k // 2)
+
+    split(np.arange(n), 0, world)
+    return owner
+
+
 def comm_ms(world, nu, npu, model):
     """t MIN (4 B / slot) + occlusion SUM (1 B / slot + 192) all-reduces and
     the film reduce (12 B / U pixel); ring all-reduce moves 2 (N-1)/N of the
@@ -82,7 +128,8 @@ def comm_ao_ms(world, nu, model):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
-    ap.add_argument("--modes", nargs="+", default=["close", "rr", "view"])
+    ap.add_argument("--modes", nargs="+", default=["close", "rr", "view"],
+                    help="close / rr / view, or (AO, experimental) hitlpt / hitaxis")
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/cam/rehearse.json")
     ap.add_argument("--shader", choices=("pt", "ao"), default="pt",
@@ -130,9 +177,20 @@ def main():
                   ("AO-16", "configs[4]") if ao else ("PT", "configs[2]")), "u_slots": nu,
               "u_pixels": nu // SPP, "totals": list(tot), "link": LINK, "runs": []}
 
+    # per-domain AO / eye-ray work weights for the experimental balanced
+    # partitions: the U slots each domain wins (the captured key minima)
+    win = None
+    if ao:
+        km = kmin.cpu().numpy().astype(np.uint64)
+        hit = km != np.uint64(0x7FFFFFFFFFFFFFFF)
+        win = np.bincount((km[hit] & np.uint64(0xFFFF)).astype(np.int64),
+                          minlength=len(boxes)).astype(np.float64)
     for mode in args.modes:
         for world in args.worlds:
-            owner = insitu.partition(boxes, bound, world, MODES[mode], cam)
+            if mode in ("hitlpt", "hitaxis"):
+                owner = balanced_partition(boxes, win, world, CAM, mode)
+            else:
+                owner = insitu.partition(boxes, bound, world, MODES[mode], cam)
             ranks = []
             t0 = time.time()
             bits = None
