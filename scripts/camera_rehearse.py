@@ -129,7 +129,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--modes", nargs="+", default=["close", "rr", "view"],
-                    help="close / rr / view, or (AO, experimental) hitlpt / hitaxis")
+                    help="close / rr / view, or (AO, experimental) hitlpt / hitaxis / fplpt")
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/cam/rehearse.json")
     ap.add_argument("--shader", choices=("pt", "ao"), default="pt",
@@ -189,6 +189,10 @@ def main():
         for world in args.worlds:
             if mode in ("hitlpt", "hitaxis"):
                 owner = balanced_partition(boxes, win, world, CAM, mode)
+            elif mode == "fplpt":  # weights: the boxes' screen footprints (pixels)
+                fpw = np.array([float(np.clip(x1 - x0 + 1, 0, None).sum()) if k == 1 else float(W * H)
+                                for k, x0, x1 in (insitu.box_rows(cam, W, H, b) for b in boxes)])
+                owner = balanced_partition(boxes, fpw, world, CAM, "hitlpt")
             else:
                 owner = insitu.partition(boxes, bound, world, MODES[mode], cam)
             ranks = []
