@@ -562,9 +562,18 @@ int spray_rt_write_ppm(const char* path, const float* rgba_host, int w, int h);
 typedef struct spray_rt_insitu* spray_rt_insitu_t;
 
 /* Host-memory collectives of the rank group (every rank calls each one in
- * the same order).  Return 0 on success.  struct_size = the caller's
- * sizeof(spray_rt_transport): callbacks past it (a caller built against an
- * older, shorter struct) are taken as NULL, so the struct can grow. */
+ * the same order).  Return 0 on success.
+ * ABI: this is layout version 2 (SPRAY_RT_TRANSPORT_ABI), which put
+ * struct_size in FRONT of `user` -- a breaking change against version 1
+ * (round <= 4 callers, `user` at offset 0).  spray_rt_insitu_create reads
+ * struct_size before any other field and rejects a value outside
+ * [offsetof(allreduce_min_u64), SPRAY_RT_TRANSPORT_MAX_SIZE] with
+ * SPRAY_RT_ERR_ARG: a version-1 caller's `user` pointer (or NULL) read as
+ * struct_size fails that check instead of shifting every callback.  Within
+ * version 2 the struct only grows at its end: a caller's struct_size below
+ * sizeof(spray_rt_transport) leaves the later callbacks NULL. */
+#define SPRAY_RT_TRANSPORT_ABI 2
+#define SPRAY_RT_TRANSPORT_MAX_SIZE 4096
 typedef struct spray_rt_transport {
   size_t struct_size;
   void* user;
@@ -759,6 +768,17 @@ int spray_rt_insitu_composite(spray_rt_insitu_t ins, float* image_rgba, size_t n
 /* out[6] = bytes sent to other ranks, bytes received, exchanges, host
  * count reads, collectives issued, traces -- since creation. */
 int spray_rt_insitu_stats(spray_rt_insitu_t ins, unsigned long long out[6]);
+/* The issue log of the group's collectives since creation or the last
+ * clear, in host call order -- what every rank must enqueue identically for
+ * RCCL (per communicator, across its streams).  Entry = op << 56 | side << 51
+ * | element count (48 bits); op: 1 count all-to-all (int64[world]), 2 data
+ * all-to-all-v (bytes; count 0: per-peer counts differ by rank and match
+ * pairwise), 3 all-reduce SUM u64, 4 reduce SUM f32 to rank 0, 5 all-reduce
+ * MIN u64, 6 all-reduce SUM u8, 7 all-reduce MIN u32, 8 all-reduce MIN u8;
+ * side = enqueued on the engine's second stream.  *n = entries logged (the
+ * first min(cap, 65536) are copied to out); clear != 0 empties the log. */
+int spray_rt_insitu_collective_log(spray_rt_insitu_t ins, uint64_t* out, size_t cap, size_t* n,
+                                   int clear);
 
 #ifdef __cplusplus
 }

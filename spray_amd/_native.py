@@ -152,6 +152,7 @@ SIGNATURES = {
     "spray_rt_insitu_phase_times": (I, [P, P, P]),
     "spray_rt_insitu_composite": (I, [P, P, SZ]),
     "spray_rt_insitu_stats": (I, [P, P]),
+    "spray_rt_insitu_collective_log": (I, [P, P, SZ, P, I]),
     # spray_scene.h
     "spray_scene_create": (I, [C.c_char_p, C.c_char_p, I, I, P, C.c_char_p, SZ]),
     "spray_scene_destroy": (I, [P]),

@@ -112,29 +112,62 @@ struct DBuf {
 // ---------------------------------------------------------------------------
 // transports
 // ---------------------------------------------------------------------------
+// The issue log of the group's collectives (spray_rt_insitu_collective_log):
+// RCCL needs every rank to enqueue the same collectives in the same order
+// (per communicator, across its streams), so each call is recorded as
+// op << 56 | side stream << 51 | element count (48 bits) before it runs.
+// The all-to-all-v's per-peer byte counts legitimately differ between ranks
+// (they match pairwise), so those entries carry no count.
+enum CollOp : uint64_t {
+  kCollCounts = 1,        // int64[world] count all-to-all
+  kCollAlltoallv = 2,     // bytes, per-peer counts
+  kCollSumU64 = 3,        // all-reduce SUM u64
+  kCollReduceF32 = 4,     // reduce SUM f32 to a root
+  kCollMinU64 = 5,        // all-reduce MIN u64
+  kCollSumU8 = 6,         // all-reduce SUM u8
+  kCollMinU32 = 7,        // all-reduce MIN u32 (t bits)
+  kCollMinU8 = 8,         // all-reduce MIN u8 (list positions)
+};
+void collective_log(spray_rt_insitu* I, uint64_t op, size_t n, hipStream_t st);
+
 struct InsituTransport {
   virtual ~InsituTransport() = default;
   // per-peer counts: dev_send (device int64[world]) -> host send / recv
-  virtual int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
-                     int64_t* h_recv) = 0;
+  int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send, int64_t* h_recv);
   // device buffers; byte counts per peer (host)
   // skip_self: the rank's own segment is not moved (its offsets still count)
-  virtual int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
-                        const size_t* rb, bool skip_self = false) = 0;
-  virtual int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) = 0;
-  virtual int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) = 0;
+  int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+                const size_t* rb, bool skip_self = false);
+  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n);
+  int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root);
   // replicated-ray frames: MIN of u64 keys, SUM of bytes (device, in place)
   virtual bool has_rep() const { return true; }
-  virtual int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) = 0;
-  virtual int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) = 0;
+  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n);
+  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n);
   // split keys: MIN of u32 t bits (src -> dst; in place when equal) and of
   // u8 list positions, on stream st (RCCL: overlapping the other streams'
   // work; the host form runs them in order, blocking); off = the slots'
   // first index in the frame's U (the replay's captured arrays)
-  virtual int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
-                                size_t n, size_t off, hipStream_t st) = 0;
-  virtual int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t off,
-                               hipStream_t st) = 0;
+  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
+                        size_t off, hipStream_t st);
+  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t off, hipStream_t st);
+
+ protected:
+  // the transports' implementations of the calls above (which log first)
+  virtual int do_counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+                        int64_t* h_recv) = 0;
+  virtual int do_alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+                           const size_t* rb, bool skip_self) = 0;
+  virtual int do_allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) = 0;
+  virtual int do_reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) = 0;
+  virtual int do_allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) = 0;
+  virtual int do_allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) = 0;
+  virtual int do_allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
+                                   size_t n, size_t off, hipStream_t st) = 0;
+  virtual int do_allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t off,
+                                  hipStream_t st) = 0;
+
+ public:
   // rehearsal only: the rank's device work runs while it holds a lock
   // shared by the group's processes (SPRAY_INSITU_SERIAL), so the phase
   // timings of ranks sharing one GPU are not inflated by each other
@@ -201,7 +234,56 @@ struct spray_rt_insitu {
   int ev_phase[kMaxEv] = {};
   int nev = 0, nph = 0, cur_phase = 0;
   double phase_ms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8]: inside collectives
+  // the collectives' issue log since the last read (CollOp entries; at most
+  // kMaxLog kept, clog_total counts every one)
+  static constexpr size_t kMaxLog = 1 << 16;
+  std::vector<uint64_t> clog;
+  uint64_t clog_total = 0;
 };
+
+void collective_log(spray_rt_insitu* I, uint64_t op, size_t n, hipStream_t st) {
+  const uint64_t side = (st && st != stream_of(I->ctx)) ? 1 : 0;
+  if (I->clog.size() < spray_rt_insitu::kMaxLog)
+    I->clog.push_back(op << 56 | side << 51 | (uint64_t(n) & ((uint64_t(1) << 48) - 1)));
+  ++I->clog_total;
+}
+
+int InsituTransport::counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+                            int64_t* h_recv) {
+  collective_log(I, kCollCounts, size_t(I->world), nullptr);
+  return do_counts(I, dev_send, h_send, h_recv);
+}
+int InsituTransport::alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+                               const size_t* rb, bool skip_self) {
+  collective_log(I, kCollAlltoallv, 0, nullptr);
+  return do_alltoallv(I, send, sb, recv, rb, skip_self);
+}
+int InsituTransport::allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) {
+  collective_log(I, kCollSumU64, n, nullptr);
+  return do_allreduce_u64(I, dev, n);
+}
+int InsituTransport::reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) {
+  collective_log(I, kCollReduceF32, n, nullptr);
+  return do_reduce_f32(I, dev, n, root);
+}
+int InsituTransport::allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) {
+  collective_log(I, kCollMinU64, n, nullptr);
+  return do_allreduce_min_u64(I, dev, n);
+}
+int InsituTransport::allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) {
+  collective_log(I, kCollSumU8, n, nullptr);
+  return do_allreduce_sum_u8(I, dev, n);
+}
+int InsituTransport::allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst,
+                                       size_t n, size_t off, hipStream_t st) {
+  collective_log(I, kCollMinU32, n, st);
+  return do_allreduce_min_u32(I, src, dst, n, off, st);
+}
+int InsituTransport::allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t off,
+                                      hipStream_t st) {
+  collective_log(I, kCollMinU8, n, st);
+  return do_allreduce_min_u8(I, dev, n, off, st);
+}
 
 namespace {
 
@@ -240,12 +322,12 @@ struct RcclTransport : InsituTransport {
     if (r == ncclSuccess) return SPRAY_RT_OK;
     return fail(I->ctx, SPRAY_RT_ERR_HIP, "%s: %s", what, nccl().GetErrorString(r));
   }
-  int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+  int do_counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
              int64_t* h_recv) override {
     const int W = I->world;
     int64_t* dev_recv = const_cast<int64_t*>(dev_send) + 64;
     std::vector<size_t> b(W, sizeof(int64_t));
-    CALL(alltoallv(I, dev_send, b.data(), dev_recv, b.data(), false));
+    CALL(do_alltoallv(I, dev_send, b.data(), dev_recv, b.data(), false));
     hipStream_t s = stream_of(I->ctx);
     HIPCHK(I->ctx, hipMemcpyAsync(I->h_small, dev_send, 128 * sizeof(int64_t),
                                   hipMemcpyDeviceToHost, s));
@@ -255,7 +337,7 @@ struct RcclTransport : InsituTransport {
     ++I->st[3];
     return SPRAY_RT_OK;
   }
-  int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+  int do_alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
                 const size_t* rb, bool skip_self) override {
     const NcclApi& N = nccl();
     hipStream_t s = stream_of(I->ctx);
@@ -278,33 +360,33 @@ struct RcclTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) override {
+  int do_allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) override {
     ++I->st[4];
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint64, ncclSum, comm, stream_of(I->ctx)),
                "ncclAllReduce");
   }
-  int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) override {
+  int do_reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) override {
     ++I->st[4];
     return chk(I, nccl().Reduce(dev, dev, n, ncclFloat32, ncclSum, root, comm, stream_of(I->ctx)),
                "ncclReduce");
   }
-  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) override {
+  int do_allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) override {
     ++I->st[4];
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint64, ncclMin, comm, stream_of(I->ctx)),
                "ncclAllReduce(min)");
   }
-  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) override {
+  int do_allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) override {
     ++I->st[4];
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclSum, comm, stream_of(I->ctx)),
                "ncclAllReduce(sum u8)");
   }
-  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
+  int do_allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
                         size_t, hipStream_t st) override {
     ++I->st[4];
     return chk(I, nccl().AllReduce(src, dst, n, ncclUint32, ncclMin, comm, st),
                "ncclAllReduce(min u32)");
   }
-  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t,
+  int do_allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t,
                        hipStream_t st) override {
     ++I->st[4];
     return chk(I, nccl().AllReduce(dev, dev, n, ncclUint8, ncclMin, comm, st),
@@ -348,14 +430,14 @@ struct ReplayTransport : InsituTransport {
                   I->last_nu);
     return SPRAY_RT_OK;
   }
-  int counts(spray_rt_insitu* I, const int64_t*, int64_t*, int64_t*) override {
+  int do_counts(spray_rt_insitu* I, const int64_t*, int64_t*, int64_t*) override {
     return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
   }
-  int alltoallv(spray_rt_insitu* I, const void*, const size_t*, void*, const size_t*,
+  int do_alltoallv(spray_rt_insitu* I, const void*, const size_t*, void*, const size_t*,
                 bool) override {
     return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
   }
-  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t m) override {
+  int do_allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t m) override {
     if (!pub) {  // keep the rank's own values
       ++I->st[4];
       return SPRAY_RT_OK;
@@ -364,26 +446,26 @@ struct ReplayTransport : InsituTransport {
                                  "the frame has %zu", 2 * nk, m);
     return copy(I, dev, pub, m * 8, stream_of(I->ctx));
   }
-  int reduce_f32(spray_rt_insitu* I, float*, size_t, int) override {
+  int do_reduce_f32(spray_rt_insitu* I, float*, size_t, int) override {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t m) override {
+  int do_allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t m) override {
     if (!kmin || m != nk)
       return fail(I->ctx, SPRAY_RT_ERR_STATE, "replay: %zu keys given, the frame has %zu", nk, m);
     return copy(I, dev, kmin, m * 8, stream_of(I->ctx));
   }
-  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t m) override {
+  int do_allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t m) override {
     if (bits && m == nbits_bytes) return copy(I, dev, bits, m, stream_of(I->ctx));
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t*, uint32_t* dst, size_t m,
+  int do_allreduce_min_u32(spray_rt_insitu* I, const uint32_t*, uint32_t* dst, size_t m,
                         size_t off, hipStream_t st) override {
     CALL(need(I, m, off));
     return copy(I, dst, tmin + off, m * 4, st);
   }
-  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t m, size_t off,
+  int do_allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t m, size_t off,
                        hipStream_t st) override {
     CALL(need(I, m, off));
     return copy(I, dev, lpmin + off, m, st);
@@ -413,7 +495,7 @@ struct HostTransport : InsituTransport {
     return SPRAY_RT_OK;
   }
   bool has_rep() const override { return cb.allreduce_min_u64 && cb.allreduce_sum_u8; }
-  int allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) override {
+  int do_allreduce_min_u64(spray_rt_insitu* I, uint64_t* dev, size_t n) override {
     std::vector<unsigned long long> h(std::max<size_t>(n, 1));
     HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 8, hipMemcpyDeviceToHost, stream_of(I->ctx)));
     CALL(sync(I));
@@ -426,7 +508,7 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) override {
+  int do_allreduce_sum_u8(spray_rt_insitu* I, uint8_t* dev, size_t n) override {
     std::vector<uint8_t> h(std::max<size_t>(n, 1));
     HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n, hipMemcpyDeviceToHost, stream_of(I->ctx)));
     CALL(sync(I));
@@ -458,17 +540,17 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
+  int do_allreduce_min_u32(spray_rt_insitu* I, const uint32_t* src, uint32_t* dst, size_t n,
                         size_t, hipStream_t st) override {
     if (src != dst && n)
       HIPCHK(I->ctx, hipMemcpyAsync(dst, src, n * 4, hipMemcpyDeviceToDevice, st));
     return min_widened(I, dst, n, st);
   }
-  int allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t,
+  int do_allreduce_min_u8(spray_rt_insitu* I, uint8_t* dev, size_t n, size_t,
                        hipStream_t st) override {
     return min_widened(I, dev, n, st);
   }
-  int counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
+  int do_counts(spray_rt_insitu* I, const int64_t* dev_send, int64_t* h_send,
              int64_t* h_recv) override {
     const int W = I->world;
     HIPCHK(I->ctx, hipMemcpyAsync(h_send, dev_send, W * sizeof(int64_t), hipMemcpyDeviceToHost,
@@ -483,7 +565,7 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
+  int do_alltoallv(spray_rt_insitu* I, const void* send, const size_t* sb, void* recv,
                 const size_t* rb, bool) override {  // the self segment travels (unused)
     const int W = I->world;
     const size_t ts = std::accumulate(sb, sb + W, size_t(0));
@@ -502,7 +584,7 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) override {
+  int do_allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t n) override {
     std::vector<unsigned long long> h(n);
     HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 8, hipMemcpyDeviceToHost, stream_of(I->ctx)));
     CALL(sync(I));
@@ -515,7 +597,7 @@ struct HostTransport : InsituTransport {
     ++I->st[4];
     return SPRAY_RT_OK;
   }
-  int reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) override {
+  int do_reduce_f32(spray_rt_insitu* I, float* dev, size_t n, int root) override {
     std::vector<float> h(n);
     HIPCHK(I->ctx, hipMemcpyAsync(h.data(), dev, n * 4, hipMemcpyDeviceToHost, stream_of(I->ctx)));
     CALL(sync(I));
@@ -1672,8 +1754,25 @@ int spray_rt_insitu_create(spray_rt_ctx_t c, int world, int rank, const void* nc
   if (world < 1 || world > 64 || rank < 0 || rank >= world)
     return fail(c, SPRAY_RT_ERR_ARG, "in-situ group: world %d rank %d (world in [1, 64])", world,
                 rank);
-  if (!nccl_id && (!host || !host->alltoallv || !host->allreduce_u64 || !host->reduce_f32))
+  if (!nccl_id && !host)
     return fail(c, SPRAY_RT_ERR_ARG, "in-situ group needs an RCCL id or host collectives");
+  spray_rt_transport cb{};
+  if (!nccl_id) {
+    // struct_size first, before any callback field is read (spray_rt.h: a
+    // layout-1 caller's `user` pointer lands here and fails the range check)
+    const size_t have = host->struct_size;
+    if (have < offsetof(spray_rt_transport, allreduce_min_u64) ||
+        have > SPRAY_RT_TRANSPORT_MAX_SIZE)
+      return fail(c, SPRAY_RT_ERR_ARG,
+                  "spray_rt_transport.struct_size %zu outside [%zu, %d] (layout %d expected)",
+                  have, offsetof(spray_rt_transport, allreduce_min_u64),
+                  SPRAY_RT_TRANSPORT_MAX_SIZE, SPRAY_RT_TRANSPORT_ABI);
+    std::memcpy(&cb, host, std::min(have, sizeof(spray_rt_transport)));
+    cb.struct_size = sizeof(spray_rt_transport);
+    if (!cb.alltoallv || !cb.allreduce_u64 || !cb.reduce_f32)
+      return fail(c, SPRAY_RT_ERR_ARG, "host collectives: alltoallv / allreduce_u64 / "
+                                       "reduce_f32 are required");
+  }
   HIPCHK(c, hipSetDevice(c->device));
   std::unique_ptr<spray_rt_insitu> I(new (std::nothrow) spray_rt_insitu);
   if (!I) return SPRAY_RT_ERR_NOMEM;
@@ -1700,15 +1799,7 @@ int spray_rt_insitu_create(spray_rt_ctx_t c, int world, int rank, const void* nc
     I->tr = std::move(t);
   } else {
     auto t = std::make_unique<HostTransport>();
-    // the caller's struct may be shorter than this build's (fields added at
-    // its end): copy what it holds, the rest stays NULL
-    const size_t have = host->struct_size;
-    if (have < offsetof(spray_rt_transport, allreduce_min_u64)) {
-      free_all(I.get());
-      return fail(c, SPRAY_RT_ERR_ARG, "spray_rt_transport.struct_size %zu too small", have);
-    }
-    std::memcpy(&t->cb, host, std::min(have, sizeof(spray_rt_transport)));
-    t->cb.struct_size = sizeof(spray_rt_transport);
+    t->cb = cb;  // validated above; callbacks past the caller's struct_size stay NULL
     if (const char* lk = std::getenv("SPRAY_INSITU_SERIAL"))
       if (lk[0]) t->lock_fd = open(lk, O_RDWR | O_CREAT, 0666);
     I->tr = std::move(t);
@@ -2071,6 +2162,19 @@ int spray_rt_insitu_composite(spray_rt_insitu_t I, float* image, size_t nfloats)
 int spray_rt_insitu_stats(spray_rt_insitu_t I, unsigned long long out[6]) {
   if (!I || !out) return SPRAY_RT_ERR_ARG;
   for (int k = 0; k < 6; ++k) out[k] = I->st[k];
+  return SPRAY_RT_OK;
+}
+
+int spray_rt_insitu_collective_log(spray_rt_insitu_t I, uint64_t* out, size_t cap, size_t* n,
+                                   int clear) {
+  if (!I || !n || (cap && !out)) return SPRAY_RT_ERR_ARG;
+  *n = size_t(I->clog_total);
+  const size_t m = std::min(cap, I->clog.size());
+  if (m) std::memcpy(out, I->clog.data(), m * sizeof(uint64_t));
+  if (clear) {
+    I->clog.clear();
+    I->clog_total = 0;
+  }
   return SPRAY_RT_OK;
 }
 

@@ -584,10 +584,12 @@ int GpuScene::build_image(int id, std::string* err) {
 // front (in parallel: the meshes first, then one image per task) leaves a
 // miss one async DMA.  Bounded by a budget of page-locked host memory (the
 // images' bytes ~ 100 B per triangle, one pinned copy each); past it images
-// are built on their first miss.
+// are built on their first miss, and the skip is logged.  The default, 8 GB,
+// keeps the triangle capacity of the earlier 16 GB budget that held each
+// image twice (a vector and a pinned copy): ~86 M triangles.
 int GpuScene::prebuild_images() {
   const char* e = std::getenv("SPRAY_SCENE_PREBUILD_MB");
-  const double budget_mb = e ? std::atof(e) : 4096.0;
+  const double budget_mb = e ? std::atof(e) : 8192.0;
   if (budget_mb <= 0.0) return SPRAY_RT_OK;
   double tris = 0.0;
   for (const Domain& d : domains_) {
@@ -600,7 +602,13 @@ int GpuScene::prebuild_images() {
     }
     tris += double(it->second.faces.size() / 3);
   }
-  if (tris * 100.0 > budget_mb * 1048576.0) return SPRAY_RT_OK;
+  if (tris * 100.0 > budget_mb * 1048576.0) {
+    std::fprintf(stderr,
+                 "spray_scene: %.0f triangles need ~%.0f MB of pinned domain images, over the "
+                 "SPRAY_SCENE_PREBUILD_MB budget of %.0f MB: images are built on their first "
+                 "cache miss\n", tris, tris * 100.0 / 1048576.0, budget_mb);
+    return SPRAY_RT_OK;
+  }
   const int nd = int(domains_.size());
   const int nt = std::max(1, std::min(nd, int(std::min(16u, std::thread::hardware_concurrency()))));
   std::vector<int> rc(nd, SPRAY_RT_OK);

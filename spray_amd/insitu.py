@@ -474,6 +474,27 @@ class InsituEngine:
         self.rt._check(rc, "insitu_composite")
         return image
 
+    COLL_OPS = {1: "counts_a2a_i64", 2: "alltoallv_u8", 3: "allreduce_sum_u64",
+                4: "reduce_sum_f32", 5: "allreduce_min_u64", 6: "allreduce_sum_u8",
+                7: "allreduce_min_u32", 8: "allreduce_min_u8"}
+
+    def collective_log(self, clear=True):
+        """The collectives this rank issued since the last read, in call order
+        (spray_rt_insitu_collective_log): [(op, count, stream)] with stream
+        "main" or "side".  Every rank of a group must issue the same list."""
+        n = C.c_size_t(0)
+        lib().spray_rt_insitu_collective_log(self.h, None, 0, C.byref(n), 0)
+        buf = (C.c_uint64 * max(n.value, 1))()
+        self.rt._check(lib().spray_rt_insitu_collective_log(self.h, buf, n.value, C.byref(n),
+                                                            1 if clear else 0),
+                       "collective_log")
+        out = []
+        for k in range(min(n.value, 1 << 16)):
+            e = int(buf[k])
+            out.append((self.COLL_OPS.get(e >> 56, "op%d" % (e >> 56)), e & ((1 << 48) - 1),
+                        "side" if (e >> 51) & 1 else "main"))
+        return out
+
     def stats(self):
         out = (C.c_ulonglong * 6)()
         lib().spray_rt_insitu_stats(self.h, C.byref(out))

@@ -299,10 +299,14 @@ def _rep_rank_main(rank, world, port, out, mode, kind="pt"):
                                          shininess=SHADE[9], lights=lights)
         image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
         recs = insitu.InsituRecords(N // 2)
+        eng.collective_log()  # the issue log of this frame only
         tot = eng.trace_camera(sh, cam, W, H, SPP, image, recs)
         torch.cuda.synchronize()
         g = recs.numpy()
-        np.savez(os.path.join(out, "r%d.npz" % rank), samid=g["samid"], bounce=g["bounce"],
+        ops = list(insitu.InsituEngine.COLL_OPS.values())
+        clog = np.array([(ops.index(op), n, s == "side") for op, n, s in eng.collective_log()],
+                        np.int64).reshape(-1, 3)
+        np.savez(os.path.join(out, "r%d.npz" % rank), samid=g["samid"], bounce=g["bounce"], clog=clog,
                  hits=g["hits"], svalid=g["svalid"], occluded=g["occluded"],
                  tot=np.array(tot, np.int64), image=image.cpu().numpy() if rank == 0 else
                  np.zeros(0, np.float32))
@@ -323,6 +327,11 @@ def _run_replicated(world, mode, kind):
 
 
 def _check_replicated(parts, ref):
+    # RCCL's rule: every rank enqueues the same collectives in the same order,
+    # the side stream's included
+    assert len(parts[0]["clog"]) >= 3
+    for p in parts[1:]:
+        assert np.array_equal(p["clog"], parts[0]["clog"])
     for p in parts:
         assert tuple(p["tot"]) == ref["totals"]
     assert sum(len(p["samid"]) > 10_000 for p in parts) >= 4  # the shading is spread

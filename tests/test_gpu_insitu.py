@@ -96,8 +96,17 @@ CASES = {  # name: (shader kind, bounces, samples, image size, spp)
     "pt1": ("pt", 1, 1, 128, 2),
     "ao16": ("ao", 1, 16, 64, 2),
     "pt3": ("pt", 3, 2, 96, 2),
+    # footprint edge cases of the camera frame (footprint.cpp): the eye
+    # inside domain 0's box (box_rows kind 2: E and U take the whole image)
+    # and a point light inside the scene bound (S becomes U)
+    "pt1-eyein": ("pt", 1, 1, 96, 2),
+    "pt1-lightin": ("pt", 1, 1, 96, 2),
 }
-LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)]}
+LIGHTS = {"pt3": [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0), (1, 0, 0, 0, 0.3, 0.3, 0.3)],
+          "pt1-eyein": [(0, -300.0, 500.0, -200.0, 1.0, 1.0, 1.0)],
+          "pt1-lightin": [(0, 69.0, 66.5, 69.0, 1.0, 1.0, 1.0)]}  # scene bound hi 70 67.3 70
+CAMERAS = {"pt1-eyein": dict(pos=[9.0, 8.5, -9.0], lookat=[30.0, 28.649426, 30.0],
+                             up=[0.0, 1.0, 0.0], fov=90.0)}  # domain 0's box: +-10
 
 
 def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, replicated=False,
@@ -113,7 +122,7 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, repli
     from oracle import pyoracle as po
     from test_insitu import scene_boxes
     kind, bounces, samples, img, spp = CASES[case]
-    c = H.BENCH_CAMERA
+    c = CAMERAS.get(case, H.BENCH_CAMERA)
     cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
     scene = scene or WAVELETS64
     if owner is None:
@@ -152,6 +161,7 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, repli
     assert tot2 == tot
     image.mul_(0.5)
     st = eng.stats()
+    st["clog"] = eng.collective_log()  # both frames' collectives, in issue order
     out = (recs.numpy(), tot, image.cpu().numpy(), st)
     eng.close()
     rt.close()
@@ -160,7 +170,7 @@ def _engine_rank(rank, world, case, transport, dist=None, one_owner=False, repli
 
 def _reference(oracle, case):
     kind, bounces, samples, img, spp = CASES[case]
-    c = H.BENCH_CAMERA
+    c = CAMERAS.get(case, H.BENCH_CAMERA)
     cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
     _, doms, _ = oracle.load_scene(WAVELETS64, SCENES)
     sh = H.insitu_shader(oracle, kind, bounces, samples, LIGHTS.get(case))
@@ -168,7 +178,19 @@ def _reference(oracle, case):
                              (0, 0, img, img))
 
 
+def same_collectives(results):
+    """Every rank issued the same collectives in the same order, on the same
+    streams (RCCL's rule for one communicator)."""
+    logs = [r[3]["clog"] for r in results]
+    assert logs[0], "no collective logged"
+    for k, lg in enumerate(logs[1:], 1):
+        assert lg == logs[0], "rank %d issued %s, rank 0 %s" % (k, lg[:12], logs[0][:12])
+    return logs[0]
+
+
 def _check(oracle, case, results):
+    if len(results) > 1:
+        same_collectives(results)
     ref, ref_img, ref_tot = _reference(oracle, case)
     merged = []
     for recs, tot, _, _ in results:
@@ -315,7 +337,9 @@ VIEW = 2  # insitu.PARTITION_VIEW
 
 @pytest.mark.parametrize("world,mode,case", [(2, VIEW, "pt1"), (3, 0, "pt1"), (8, 0, "pt1"),
                                              (8, 1, "pt1"), (8, VIEW, "pt1"), (8, VIEW, "ao16"),
-                                             (3, 1, "ao16"), (8, 0, "pt1-u64")])
+                                             (3, 1, "ao16"), (8, 0, "pt1-u64"),
+                                             (3, VIEW, "pt1-eyein"), (2, 0, "pt1-eyein"),
+                                             (3, VIEW, "pt1-lightin"), (2, 0, "pt1-lightin")])
 def test_engine_camera_frame_ranks(oracle, world, mode, case, monkeypatch):
     """spray_rt_insitu_trace_camera with world processes sharing the GPU over
     the host transport: the eye rays generated in the lanes, each rank's
@@ -388,6 +412,7 @@ def test_engine_camera_frame_cross_rank_ties(oracle, split, monkeypatch, tmp_pat
     sh = H.insitu_shader(oracle, kind, bounces, samples)
     ref, _, ref_tot = H.reference_frame(oracle, sh, oracle.scene_bsdfs(doms), cam, img, img, spp,
                                         (0, 0, img, img), desc=scene)
+    same_collectives(res)
     merged = []
     for recs, tot, _, _ in res:
         assert tot == ref_tot
@@ -535,6 +560,39 @@ def test_engine_replicated_frame_unsupported_shading(oracle):
     import spray_amd
     with pytest.raises(spray_amd.SprayRtError, match="-6|replicated"):
         _engine_rank(0, 1, "pt3", "rccl", replicated=True)
+
+
+def test_transport_layout1_rejected(spray):
+    """spray_rt_transport layout 2 put struct_size in front of `user`
+    (include/spray_rt.h, SPRAY_RT_TRANSPORT_ABI): a caller built against
+    layout 1 (`user` first) must get SPRAY_RT_ERR_ARG, not callbacks shifted
+    by one slot -- its `user` pointer (or NULL) read as struct_size fails
+    the range check before any callback is read."""
+    import ctypes as C
+    from spray_amd import insitu
+    from spray_amd._native import lib
+
+    class Layout1(C.Structure):
+        _fields_ = [("user", C.c_void_p), ("alltoallv", insitu._A2A),
+                    ("allreduce_u64", insitu._AR), ("reduce_f32", insitu._RED),
+                    ("allreduce_min_u64", insitu._AR), ("allreduce_sum_u8", insitu._AR)]
+
+    keep = insitu._LocalCollectives()
+    rt = spray.RtContext(0)
+    anchor = C.c_int(7)
+    for user in (C.addressof(anchor), None, 8):
+        s = Layout1(user, *keep._cbs)
+        h = C.c_void_p()
+        rc = lib().spray_rt_insitu_create(rt.h, 2, 0, None, C.byref(s), C.byref(h))
+        assert rc == -1 and not h.value, (user, rc)
+    # the current layout is accepted, a shorter version-2 struct too (the
+    # callbacks past its size are NULL: replicated frames unsupported)
+    for size in (C.sizeof(insitu.Transport), insitu.Transport.allreduce_min_u64.offset):
+        s = insitu.Transport(size, None, *keep._cbs)
+        h = C.c_void_p()
+        assert lib().spray_rt_insitu_create(rt.h, 1, 0, None, C.byref(s), C.byref(h)) == 0
+        assert lib().spray_rt_insitu_destroy(h.value) == 0
+    rt.close()
 
 
 def test_domain_mask_exact_on_box_boundaries(spray, oracle):
