@@ -323,6 +323,83 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False, p
     return out
 
 
+def run_image(args, dist, world, rank, local, cam):
+    """The image-parallel strong split of configs[1] (the
+    reference's ooc mode shards as replicas, only the image is composited;
+    spray_rt_insitu_trace_image): every GPU holds all 64 domains (24 MB) and
+    traces its row bands of the 1024x1024x8spp frame (eye rays in a pass,
+    the fused closest hit + PT spawn + shadow any hit launch, film), then the
+    rows go to rank 0 in one RCCL gather (each rank sends 1/N of the image)
+    and the totals in one 24-B all-reduce.  Strong scaling: the frame is
+    fixed, N GPUs share it.  Timed like the main line (barrier + max over
+    ranks); max_rank_frame_ms = the busiest rank's device time outside the
+    collectives (HIP events, a separate pass)."""
+    import torch
+    import spray_amd
+    from spray_amd import insitu
+    from spray_amd.engine import host_parse_scene, host_scene_bsdfs
+    dev = torch.device("cuda", local)
+    boxes, lights = host_parse_scene(SCENE, SCENES)
+    rt = spray_amd.RtContext(local)
+    insitu.setup_rank_context(rt, SCENE, SCENES, np.full(len(boxes), rank, np.int32), rank)
+    rt.set_bsdfs(host_scene_bsdfs(SCENE))
+    rt.set_stream(torch.cuda.current_stream(dev))
+    eng = insitu.InsituEngine(rt, world, rank, dist=dist if world > 1 else None,
+                              transport="host" if REHEARSE else "rccl")
+    sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
+                                     lights=lights)
+    image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    bands = args.image_bands if world > 1 else 1
+
+    def frame():
+        image.zero_()
+        return eng.trace_image(sh, cam, W, H, SPP, image, bands)
+
+    tot = None
+    for _ in range(max(args.warmup, 1)):
+        tot = frame()
+    eng.collective_log()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tot = frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    clog = eng.collective_log()
+    eng.set_timing(True)
+    eng.phase_times()
+    nph = 3
+    for _ in range(nph):
+        frame()
+    torch.cuda.synchronize()
+    phases = {k: round(v / nph, 4) for k, v in eng.phase_times().items()}
+    eng.set_timing(False)
+    mx = phases.get("frame", 0.0)
+    if world > 1:
+        e = torch.tensor([el, mx], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el, mx = float(e[0].item()), float(e[1].item())
+    rays_step = tot[0] + tot[1]
+    k = args.steps
+    out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
+           "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
+           "rays_per_step": rays_step, "radiance_rays": tot[0], "shadow_rays": tot[1],
+           "max_rank_frame_ms": round(mx, 4), "rank0_phases_ms": phases,
+           "bands_per_rank": bands,
+           "rank0_collectives_per_step": [list(c) for c in clog[:len(clog) // max(k, 1)]],
+           "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
+           "config": "configs[1] frame split by image rows over %d GPU(s): all 64 domains resident "
+                     "per GPU, %d row band(s) per rank, eye rays + fused closest hit / PT shadow "
+                     "any hit + film per rank, rows gathered to rank 0 over RCCL" % (world, bands)}
+    eng.close()
+    rt.close()
+    return out
+
+
 def run_ao(args, dist, world, rt, prim, pixid, n_prim, sbytes, nsamples=16):
     """configs[4] workload on one GPU (all 64 domains resident): closest hit
     of the frame, ooc::ShaderAo spawn of 16 rays per hit on the device, any
@@ -523,6 +600,10 @@ def main():
                          "compiled mode), rr (round robin over the Morton order) or view (the "
                          "view-aligned partition: domains along neighbouring lines of sight "
                          "grouped per rank); at N > 1 the other partitions are timed too")
+    ap.add_argument("--image", type=int, default=1,
+                    help="also measure the image-parallel strong split (spray_rt_insitu_trace_image)")
+    ap.add_argument("--image-bands", type=int, default=4,
+                    help="row bands per rank of the image-parallel split (interleaved)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
@@ -699,7 +780,14 @@ def main():
         out["value"], out["ms_per_step"] = ins["value"], ins["ms_per_step"]
         out["config"] = {"workload": ins["config"], "rays_per_step": ins["rays_per_step"],
                          "primary_rays": ins["radiance_rays"], "shadow_rays": ins["shadow_rays"],
-                         "parallelism": "domain-parallel in-situ x%d (strong)" % world}
+                         "parallelism": "domain-parallel in-situ x%d (strong), %s partition%s"
+                                        % (world, args.partition,
+                                           " (NOT the reference's: its compiled GROUP_CLOSE is "
+                                           "timed under insitu_partitions.close)"
+                                           if args.partition != "close" else
+                                           " (the reference's compiled GROUP_CLOSE)")}
+    if args.image:
+        out["image_parallel"] = run_image(args, dist, world, rank, local, cam)
     if args.ao:
         if world > 1:  # configs[4]: AO-16 on the domain-sharded frame
             out["ao"] = run_insitu(args, dist, world, rank, local, cam, kind="ao")

@@ -700,6 +700,28 @@ int spray_rt_insitu_trace_camera(spray_rt_insitu_t ins, const spray_rt_shader* s
                                  const float cam[14], int image_w, int image_h, int spp,
                                  float* image_rgba, const spray_rt_insitu_rec* rec,
                                  unsigned long long totals[3]);
+/* The image-parallel frame of a camera (the reference's ooc
+ * mode shards as replicas -- any rank may hold any domain -- and only the
+ * image is composited): EVERY domain resident on every rank (ERR_STATE
+ * otherwise), the image_h rows cut into world * bands horizontal bands of
+ * equal height (bands > 1: image_h divisible by world * bands), rank r
+ * owns bands r, r + world, ... (bands = 1: makeHorizontalStripe,
+ * tile.cc:187-209).  Each rank generates its bands' eye rays
+ * (insitu::genMultiSampleEyeRays seeds: (pixel, sample), so any split
+ * gives every pixel the same bits), traces them with the all-local frame of
+ * world 1 (any shading spray_rt_insitu_trace supports: the fused PT launch,
+ * or bounces, area lights, AO, delta BSDFs through the frame passes), adds
+ * its film to its own rows of image_rgba, and the rows go to rank 0 in one
+ * gather (HdrImage::composite, image.h:167-181, an MPI_Reduce SUM of
+ * disjoint pixels there; here each rank sends only its own rows, 1/world of
+ * the image): rank 0's image holds the whole frame, its other ranks' rows
+ * REPLACED by theirs (clear the images first, HdrImage::clear).  One row
+ * gather (the data all-to-all-v, every rank but 0 sending) and one totals
+ * all-reduce per frame; totals = the group's. */
+int spray_rt_insitu_trace_image(spray_rt_insitu_t ins, const spray_rt_shader* shader,
+                                const float cam[14], int image_w, int image_h, int spp, int bands,
+                                float* image_rgba, const spray_rt_insitu_rec* rec,
+                                unsigned long long totals[3]);
 /* A view-aligned partition of n domain boxes (float[n][6]) over nranks for
  * camera cam: the box centres projected to the image and dealt by recursive
  * median splits (image x, then y, alternating; ties by domain id) into

@@ -139,6 +139,7 @@ SIGNATURES = {
     "spray_rt_insitu_trace": (I, [P, P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_insitu_trace_frame": (I, [P, P, P, P, P, SZ, I, P, P, P]),
     "spray_rt_insitu_trace_camera": (I, [P, P, P, I, I, I, P, P, P]),
+    "spray_rt_insitu_trace_image": (I, [P, P, P, I, I, I, I, P, P, P]),
     "spray_rt_insitu_partition_view": (I, [P, I, P, I, P]),
     "spray_rt_insitu_create_replay": (I, [P, I, I, P]),
     "spray_rt_insitu_replay_set": (I, [P, P, P, SZ]),

@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -224,6 +225,7 @@ struct spray_rt_insitu {
   size_t last_nc_ao = 0;  // C slots of the last replicated AO frame
   size_t last_npair_ao = 0;  // and its AO pairs (nc x samples)
   DBuf ctmin, ccomp, crays, cpix, csam, ciota;
+  DBuf gpack;  // image frames: the rank's interleaved bands packed / the root's gather
   size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
@@ -433,9 +435,12 @@ struct ReplayTransport : InsituTransport {
   int do_counts(spray_rt_insitu* I, const int64_t*, int64_t*, int64_t*) override {
     return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
   }
+  // only the image frame's row gather reaches here (the protocol stops at
+  // its count exchange above): the rank keeps its own rows
   int do_alltoallv(spray_rt_insitu* I, const void*, const size_t*, void*, const size_t*,
-                bool) override {
-    return fail(I->ctx, SPRAY_RT_ERR_UNSUPPORTED, "replay transport: camera frames only");
+                   bool) override {
+    ++I->st[4];
+    return SPRAY_RT_OK;
   }
   int do_allreduce_u64(spray_rt_insitu* I, unsigned long long* dev, size_t m) override {
     if (!pub) {  // keep the rank's own values
@@ -947,7 +952,8 @@ bool all_local(const spray_rt_insitu* I) { return I->world == 1; }
 
 int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray* rays,
                 const int32_t* pixid, const int32_t* samid, size_t n, int spp, float* image,
-                const spray_rt_insitu_rec* rec, unsigned long long totals[3]) {
+                const spray_rt_insitu_rec* rec, unsigned long long totals[3],
+                const std::function<int()>& before_totals = {}) {
   spray_rt_ctx* c = I->ctx;
   hipStream_t s = stream_of(c);
   const int ns = spray_rt_shadow_slots(P);
@@ -1018,6 +1024,7 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
         HIPCHK(c, launch_record(s, I->owin.as<uint8_t>(), n, b, ns, samid, hits, sv, occ, *rec));
     }
   }
+  if (before_totals) CALL(before_totals());  // the image frame's row gather
   // the group's totals: radiance rays = live slots shaded, shadows, aborts
   unsigned long long* dt = I->dtot.as<unsigned long long>();
   HIPCHK(c, hipMemcpyAsync(dt, st + 3, 8, hipMemcpyDeviceToDevice, s));
@@ -2100,6 +2107,108 @@ int spray_rt_insitu_trace_camera(spray_rt_insitu_t I, const spray_rt_shader* P,
     r = ao ? trace_camera_ao(I, P, F, image_h, image, rec, totals)
            : trace_camera_pt(I, P, F, image_h, image, rec, totals);
   }
+  I->tr->serial_end();
+  return r;
+}
+
+// Rows of band b of bt bands over h rows: [b h / bt, (b + 1) h / bt).
+inline int band_row(int b, int bt, int h) { return int((long long)b * h / bt); }
+
+int spray_rt_insitu_trace_image(spray_rt_insitu_t I, const spray_rt_shader* P,
+                                const float cam[14], int image_w, int image_h, int spp, int bands,
+                                float* image, const spray_rt_insitu_rec* rec,
+                                unsigned long long totals[3]) {
+  if (!I || !cam) return SPRAY_RT_ERR_ARG;
+  spray_rt_ctx* c = I->ctx;
+  if (spray_rt_shadow_slots(P) < 0 || spp <= 0 || image_w <= 0 || image_h <= 0 || bands <= 0)
+    return fail(c, SPRAY_RT_ERR_ARG, "bad shader or frame configuration");
+  if (float(image_w) != cam[12] || float(image_h) != cam[13])
+    return fail(c, SPRAY_RT_ERR_ARG, "the camera record is for a %gx%g image", cam[12], cam[13]);
+  const int W = I->world, bt = W * bands;
+  if (bt > image_h) return fail(c, SPRAY_RT_ERR_ARG, "%d bands over %d rows", bt, image_h);
+  if (rec && (spray_rt_shadow_slots(P) > 64 || !rec->d_count || !is_device_ptr(rec->d_count)))
+    return fail(c, SPRAY_RT_ERR_ARG, "records need <= 64 shadow slots and a device counter");
+  if (size_t(image_w) * size_t(image_h) * size_t(spp) > 0x7FFFFFFFull)
+    return fail(c, SPRAY_RT_ERR_LIMIT, "frame > 2^31 samples");
+  if (!image || !is_device_ptr(image)) return fail(c, SPRAY_RT_ERR_ARG, "needs a device image");
+  int r = scene_common(c, image, 1, image);
+  if (r) return r;
+  // image-parallel: every domain resident on every rank (the reference's ooc
+  // mode, where any rank may load any domain)
+  for (int d = 0; d < c->ndom; ++d)
+    if (size_t(d) >= c->dom2slot.size() || c->dom2slot[size_t(d)] < 0)
+      return fail(c, SPRAY_RT_ERR_STATE,
+                  "image-parallel frames need every domain resident (domain %d is not)", d);
+  hipStream_t s = stream_of(c);
+  const size_t row = size_t(image_w) * 4;  // floats per image row
+  // this rank's bands: r, r + W, r + 2W, ... ; their rows in band order
+  std::vector<std::pair<int, int>> mine;  // (first row, rows)
+  size_t rows = 0;
+  for (int b = I->rank; b < bt; b += W) {
+    const int y0 = band_row(b, bt, image_h), y1 = band_row(b + 1, bt, image_h);
+    mine.emplace_back(y0, y1 - y0);
+    rows += size_t(y1 - y0);
+  }
+  const size_t n = rows * size_t(image_w) * size_t(spp);
+  I->nev = 0;
+  I->tr->serial_begin();
+  r = grow(I, I->crays, n * 32 + 32);
+  if (!r) r = grow(I, I->cpix, n * 4 + 4);
+  if (!r) r = grow(I, I->csam, n * 4 + 4);
+  if (!r) r = mark(I, 0);
+  size_t off = 0;
+  for (const auto& bnd : mine) {  // eye rays, (pixel, sample) seeds: any split, the same bits
+    if (r || !bnd.second) continue;
+    if (launch_eye_rays_insitu(s, cam, image_w, spp, 0, 0, image_w, 0, bnd.first, image_w,
+                               bnd.second, I->crays.as<spray_rt_ray>() + off,
+                               I->cpix.as<int32_t>() + off, I->csam.as<int32_t>() + off) !=
+        hipSuccess)
+      r = fail(c, SPRAY_RT_ERR_HIP, "eye rays");
+    off += size_t(bnd.second) * size_t(image_w) * size_t(spp);
+  }
+  // the rows to rank 0 (HdrImage::composite, image.h:167-181: an MPI_Reduce
+  // SUM of disjoint pixels in the reference; here each rank's rows alone):
+  // bands = 1 -> rank order is row order, so rank 0 receives straight into
+  // its image; else the bands are packed and unpacked by 2-D copies
+  auto gather = [&]() -> int {
+    if (W == 1) return SPRAY_RT_OK;
+    std::vector<size_t> sb(size_t(W), 0), rb(size_t(W), 0);
+    std::vector<size_t> rrows(size_t(W), 0);  // rows of each rank
+    for (int b = 0; b < bt; ++b)
+      rrows[size_t(b % W)] += size_t(band_row(b + 1, bt, image_h) - band_row(b, bt, image_h));
+    const size_t mine_b = rows * row * 4;
+    sb[0] = mine_b;
+    if (I->rank == 0)
+      for (int k = 0; k < W; ++k) rb[size_t(k)] = rrows[size_t(k)] * row * 4;
+    if (bands == 1) {
+      float* base = image + size_t(mine.front().first) * row;
+      COMM(I->tr->alltoallv(I, base, sb.data(), image, rb.data(), true));
+      return SPRAY_RT_OK;
+    }
+    const size_t band_b = size_t(band_row(1, bt, image_h)) * row * 4;  // uniform bands only
+    for (int b = 0; b < bt; ++b)
+      if (size_t(band_row(b + 1, bt, image_h) - band_row(b, bt, image_h)) * row * 4 != band_b)
+        return fail(c, SPRAY_RT_ERR_ARG, "interleaved bands need %d | %d rows", bt, image_h);
+    const size_t total = size_t(image_h) * row * 4;
+    GROW(I->gpack, I->rank == 0 ? total : mine_b);
+    char* pk = I->gpack.as<char>();
+    // band k of this rank sits at row (rank + k W) * band rows
+    if (I->rank != 0)
+      HIPCHK(c, hipMemcpy2DAsync(pk, band_b, reinterpret_cast<char*>(image) + I->rank * band_b,
+                                 size_t(W) * band_b, band_b, size_t(bands),
+                                 hipMemcpyDeviceToDevice, s));
+    COMM(I->tr->alltoallv(I, pk, sb.data(), pk, rb.data(), true));
+    if (I->rank == 0)
+      for (int k = 1; k < W; ++k)  // rank k's segment: its bands, in order
+        HIPCHK(c, hipMemcpy2DAsync(reinterpret_cast<char*>(image) + k * band_b,
+                                   size_t(W) * band_b, pk + size_t(k) * size_t(bands) * band_b,
+                                   band_b, band_b, size_t(bands), hipMemcpyDeviceToDevice, s));
+    return SPRAY_RT_OK;
+  };
+  if (!r)
+    r = trace_local(I, P, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
+                    I->csam.as<int32_t>(), n, spp, image, rec, totals, gather);
+  flush_phases(I, 1);
   I->tr->serial_end();
   return r;
 }

@@ -376,6 +376,22 @@ class InsituEngine:
         self._rep_kind = "ao" if shader.shader == SHADER_AO else "pt"
         return int(tot[0]), int(tot[1])
 
+    def trace_image(self, shader, cam, image_w, image_h, spp, image, bands=1, records=None):
+        """The image-parallel frame (spray_rt_insitu_trace_image): every domain
+        resident on every rank, this rank's row bands traced with the
+        all-local frame, the rows gathered into rank 0's image.  Returns the
+        group's (radiance rays, shadow rays)."""
+        from .engine import _addr
+        c = np.ascontiguousarray(cam, np.float32).reshape(14)
+        im, k4 = _addr(image)
+        tot = (C.c_ulonglong * 3)()
+        rec = C.byref(records.struct) if records is not None else None
+        rc = lib().spray_rt_insitu_trace_image(self.h, C.byref(shader), c.ctypes.data,
+                                               int(image_w), int(image_h), int(spp), int(bands),
+                                               im, rec, C.byref(tot))
+        self.rt._check(rc, "insitu_trace_image")
+        return int(tot[0]), int(tot[1])
+
     def replay_capture(self):
         """(tmin u32, lpmin u8) device tensors of the last camera PT frame's
         group minima over U (spray_rt_insitu_replay_capture)."""

@@ -652,3 +652,139 @@ def test_domain_mask_exact_on_box_boundaries(spray, oracle):
     assert (mask == ref).all(), np.nonzero(mask != ref)[0][:10]
     assert (cnt >= 4).sum() > 100
     rt.close()
+
+
+# ---- image-parallel frames (spray_rt_insitu_trace_image) ----
+IMG_CASES = {"pt1": ("pt", 1, 1, 128, 8, [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)]),
+             "ao16": ("ao", 1, 16, 64, 4, [(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)]),
+             "pt3": ("pt", 3, 2, 96, 2, LIGHTS["pt3"])}
+
+
+def _image_frame(rank, world, case, transport, dist=None, bands=1, how="image"):
+    """One frame of IMG_CASES[case] into a zeroed image, every domain resident:
+    spray_rt_insitu_trace_image (how "image") or, at one rank, the whole
+    image's eye rays through spray_rt_insitu_trace (how "rays").  Returns (records, totals, image, stats)."""
+    import spray_amd
+    from spray_amd import insitu
+    kind, bounces, samples, img, spp, lights = IMG_CASES[case]
+    c = H.BENCH_CAMERA
+    cam = spray_amd.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    rt = spray_amd.RtContext(0)
+    nd = len(spray_amd.engine.host_parse_scene(WAVELETS64, SCENES)[0])
+    insitu.setup_rank_context(rt, WAVELETS64, SCENES, np.full(nd, rank, np.int32), rank)
+    rt.set_bsdfs(spray_amd.engine.host_scene_bsdfs(WAVELETS64))
+    rt.set_stream(torch.cuda.current_stream())
+    sh = spray_amd.frame.make_shader(kind, bounces, samples, lights=lights)
+    eng = insitu.InsituEngine(rt, world, rank, dist=dist, transport=transport)
+    recs = insitu.InsituRecords(img * img * spp * bounces + 16)
+    image = torch.zeros(img * img * 4, dtype=torch.float32, device="cuda")
+    if how == "image":
+        tot = eng.trace_image(sh, cam, img, img, spp, image, bands, recs)
+    else:  # the whole image's stored eye rays through the one-rank all-local frame
+        n = img * img * spp
+        rays = torch.empty((n, 8), dtype=torch.float32, device="cuda")
+        pix = torch.empty(n, dtype=torch.int32, device="cuda")
+        sam = torch.empty(n, dtype=torch.int32, device="cuda")
+        rt.eye_rays_insitu(cam, img, spp, (0, 0, img, img), (0, 0, img, img), rays, pix, sam)
+        tot = eng.trace(sh, rays, pix, sam, spp, image, recs)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    st["clog"] = eng.collective_log()
+    out = (recs.numpy(), tot, image.cpu().numpy(), st)
+    eng.close()
+    rt.close()
+    return out
+
+
+def _image_rank_main(rank, world, port, out, case, bands):
+    import pickle
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
+    try:
+        res = _image_frame(rank, world, case, "host", dist, bands)
+        with open(os.path.join(out, "r%d.pkl" % rank), "wb") as fh:
+            pickle.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+def _image_reference(oracle, case):
+    kind, bounces, samples, img, spp, lights = IMG_CASES[case]
+    c = H.BENCH_CAMERA
+    cam = oracle.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], img, img)
+    _, doms, _ = oracle.load_scene(WAVELETS64, SCENES)
+    sh = H.insitu_shader(oracle, kind, bounces, samples, lights)
+    return H.reference_frame(oracle, sh, oracle.scene_bsdfs(doms), cam, img, img, spp,
+                             (0, 0, img, img))
+
+
+@pytest.mark.parametrize("world,bands,case", [(1, 1, "pt1"), (1, 2, "ao16"), (2, 1, "pt1"),
+                                              (2, 4, "pt1"), (3, 1, "ao16"), (3, 1, "pt3"),
+                                              (8, 2, "pt1"), (8, 1, "ao16")])
+def test_engine_image_frame_ranks(oracle, world, bands, case):
+    """The image-parallel strong split (ooc mode): world
+    processes sharing the GPU over the host transport (world 1: RCCL), every
+    domain resident on each, rank r tracing its row bands -- every shaded
+    sample's record bit-exact against the whole-scene oracle and shaded on
+    exactly one rank, totals exact, the same collectives on every rank, and
+    rank 0's gathered image BIT-EQUAL to the one-rank frame's (the
+    pixels are disjoint and the (pixel, sample) seeds do not see the split),
+    the other ranks holding their own rows only."""
+    import pickle
+    if world == 1:
+        res = [_image_frame(0, 1, case, "rccl", None, bands)]
+    else:
+        with tempfile.TemporaryDirectory() as out:
+            torch.multiprocessing.spawn(_image_rank_main,
+                                        args=(world, _rendezvous_file(), out, case, bands),
+                                        nprocs=world)
+            res = []
+            for r in range(world):
+                with open(os.path.join(out, "r%d.pkl" % r), "rb") as fh:
+                    res.append(pickle.load(fh))
+        log = same_collectives(res)
+        assert [op for op, _, _ in log] == ["alltoallv_u8", "allreduce_sum_u64"], log
+    ref, ref_img, ref_tot = _image_reference(oracle, case)
+    merged = []
+    for recs, tot, _, st in res:
+        assert tot == ref_tot
+        assert st["exchanges"] == 0 and st["host_count_reads"] == 0
+        merged += [(b, s) + v for (b, s), v in H.records_dict(recs).items()]
+    assert len(merged) == len({(m[0], m[1]) for m in merged})  # shaded once
+    H.compare_records(H.records_dict(merged), ref)
+    np.testing.assert_allclose(res[0][2], ref_img, rtol=1e-5, atol=1e-6)
+    one = _image_frame(0, 1, case, "rccl", how="rays")[2]
+    assert (one > 0).sum() > 500
+    np.testing.assert_array_equal(res[0][2].view(np.uint32), one.view(np.uint32))
+    img = IMG_CASES[case][3]
+    for r in range(1, world):  # a rank's image: its own bands' rows only
+        rows = np.zeros(img, bool)
+        bt = world * bands
+        for b in range(r, bt, world):
+            rows[b * img // bt:(b + 1) * img // bt] = True
+        im = res[r][2].reshape(img, img, 4)
+        np.testing.assert_array_equal(im[rows].view(np.uint32),
+                                      one.reshape(img, img, 4)[rows].view(np.uint32))
+        assert not im[~rows].any()
+
+
+def test_engine_image_frame_needs_every_domain(spray):
+    """A rank missing a domain cannot trace an image-parallel frame."""
+    from spray_amd import insitu
+    from test_insitu import scene_boxes
+    boxes, bound = scene_boxes()
+    rt = spray.RtContext(0)
+    insitu.setup_rank_context(rt, WAVELETS64, SCENES, insitu.morton_partition(boxes, bound, 2), 0)
+    eng = insitu.InsituEngine(rt, 1, 0, transport="rccl")
+    c = H.BENCH_CAMERA
+    cam = spray.camera_init(c["pos"], c["lookat"], c["up"], c["fov"], 64, 64)
+    sh = spray.frame.make_shader("pt", 1, 1, lights=[(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)])
+    image = torch.zeros(64 * 64 * 4, dtype=torch.float32, device="cuda")
+    with pytest.raises(spray.SprayRtError, match="-3|resident"):
+        eng.trace_image(sh, cam, 64, 64, 2, image)
+    eng.close()
+    rt.close()
