@@ -57,6 +57,8 @@ struct spray_rt_ooc {
   void* q_mem = nullptr;
   uint64_t* tie = nullptr;  // per-ray closest-hit key (kOocMissKey: none yet)
   size_t tie_cap = 0;
+  void* rec = nullptr;  // closest-hit records per (ray, batch position), OocScratch::rec
+  size_t rec_cap = 0;
   std::vector<uint32_t> first;
   std::vector<unsigned long long> score;  // DomainStats scores of the last queue build
   // drain launches: one event per launch in a ring (slot reuse, error
@@ -81,6 +83,19 @@ void free_scratch(spray_rt_ooc* o) {
   o->q_rays = 0;
 }
 
+// Domains drained per launch: half the slots (the other half takes the next
+// batch's images during the launch).  SPRAY_OOC_PER overrides (A/B, tests):
+// up to slots - 1 measured the same (4.14-4.22 vs 4.15-4.25 ms per frame,
+// batches of 3 / 1), every slot with the uploads as DMAs between the
+// launches slower (4.37 ms).
+int batch_per(const spray_rt_ooc* o) {
+  const char* per_s = std::getenv("SPRAY_OOC_PER");  // read per pass (tests set it)
+  const int per_env = per_s ? std::atoi(per_s) : 0;
+  const int nslots = int(o->slot.size());
+  return std::max(1, std::min<int>(kOocBatch, per_env > 0 ? std::min(per_env, nslots)
+                                                           : nslots / 2));
+}
+
 // (Re)allocates the queue scratch for M rays and `pairs` (domain, ray) pairs.
 int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   spray_rt_ctx* c = o->ctx;
@@ -93,15 +108,15 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   const size_t nchk = (rblk + kOocChunk - 1) / kOocChunk * size_t(64 * W);
   const size_t b_masks = align256(M * W * sizeof(uint64_t));
   const size_t b_v = align256(pairs * sizeof(uint32_t));
-  const size_t b_pk = align256(pairs * sizeof(uint64_t));
   const size_t b_blk = align256(nblk * sizeof(uint32_t));
   const size_t b_dom = align256(257 * sizeof(uint32_t));
   const size_t b_score = align256(256 * sizeof(unsigned long long));
+  const size_t b_dpos = align256(256);
   const size_t b_ch = align256(nchk * sizeof(uint32_t));
   // two sets: an any-hit launch adds to one while it publishes the other
   const size_t b_dsh = align256(2 * 256 * kOocDeadShards * sizeof(uint32_t));
   const size_t total =
-      b_masks + 2 * b_v + b_pk + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score + b_dsh;
+      b_masks + b_v + 3 * b_blk + 2 * b_dom + 2 * b_ch + b_score + b_dsh + b_dpos;
   HIPCHK(c, hipMalloc(&o->q_mem, total));
   char* p = static_cast<char*>(o->q_mem);
   auto take = [&](size_t n) {
@@ -111,8 +126,6 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   };
   o->q.masks = reinterpret_cast<uint64_t*>(take(b_masks));
   o->q.val = reinterpret_cast<uint32_t*>(take(b_v));
-  o->q.pleaf = reinterpret_cast<uint32_t*>(take(b_v));
-  o->q.pkey = reinterpret_cast<uint64_t*>(take(b_pk));
   o->q.bc = reinterpret_cast<uint32_t*>(take(b_blk));
   o->q.sb = reinterpret_cast<uint32_t*>(take(b_blk));
   o->q.off = reinterpret_cast<uint32_t*>(take(b_blk));
@@ -122,6 +135,7 @@ int size_scratch(spray_rt_ooc* o, size_t M, size_t pairs, int W) {
   o->q.cw = reinterpret_cast<uint32_t*>(take(b_ch));
   o->q.score = reinterpret_cast<unsigned long long*>(take(b_score));
   o->q.dshard = reinterpret_cast<uint32_t*>(take(b_dsh));
+  o->q.dpos = reinterpret_cast<uint8_t*>(take(b_dpos));
   o->q.block_cap = nblk;
   o->q.chunk_cap = nchk;
   o->q.pair_cap = pairs;
@@ -238,15 +252,7 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   spray_rt_ctx* c = o->ctx;
   hipStream_t s = stream_of(c);
   const int n = c->ndom;
-  // slots / 2 domains per launch, so that the next batch's uploads fit the
-  // other slots.  SPRAY_OOC_PER overrides (A/B): up to slots - 1 measured
-  // the same (4.14-4.22 vs 4.15-4.25 ms per frame, batches of 3 / 1), every
-  // slot with the uploads as DMAs between the launches slower (4.37 ms).
-  const char* per_s = std::getenv("SPRAY_OOC_PER");  // read per pass (tests set it)
-  const int per_env = per_s ? std::atoi(per_s) : 0;
-  const int nslots = int(o->slot.size());
-  const int per = std::max(1, std::min<int>(kOocBatch, per_env > 0 ? std::min(per_env, nslots)
-                                                                   : nslots / 2));
+  const int per = batch_per(o);  // slots / 2 domains per launch
   std::vector<int> order;
   std::vector<uint32_t> live(n, 0);
   for (int d = 0; d < n; ++d) {
@@ -267,9 +273,8 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
   const unsigned long long g = (unsigned long long)S.gen << 32;
   // waits for launch `k` of this pass (0-based) to publish (or complete),
   // then folds the newest counts in
-  // launch k's counts are published by launch k (closest hit: its resolve)
-  // or by launch k + 1 (any hit: a block of the next drain), so the wait
-  // watches the publisher's event
+  // launch k's counts are published by launch k + 1 (a block of the next
+  // drain), so the wait watches the publisher's event
   auto absorb = [&](uint32_t k, int ring) -> int {
     for (unsigned spins = 0; snap[256] < g + k + 1; ++spins) {
       if ((spins & 1023) == 1023) {  // also watch the launch itself (errors)
@@ -364,9 +369,9 @@ int drain(spray_rt_ooc* o, bool any_hit, const std::vector<float>& boxes, Launch
     }
     o->drains += cur.count;
     rings[S.launch % 4] = ring;
-    const uint32_t pub = any_hit ? 1u : 0u;  // the publisher's offset (lag >= 1)
+    // launch k's counts are published by launch k + 1 (its block 0)
     if (S.launch >= uint32_t(lag) &&
-        (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag + pub) % 4])))
+        (r = absorb(S.launch - uint32_t(lag), rings[(S.launch - lag + 1) % 4])))
       return r;
     ++S.launch;
     cur = nxt;
@@ -432,6 +437,7 @@ int spray_rt_ooc_destroy(spray_rt_ooc_t o) {
     if (d.pinned) (void)hipHostFree(d.pinned);
   free_scratch(o);
   if (o->tie) (void)hipFree(o->tie);
+  if (o->rec) (void)hipFree(o->rec);
   if (o->snap) (void)hipHostFree(o->snap);
   if (o->done) (void)hipFree(o->done);
   for (hipEvent_t ev : o->launch_ev)
@@ -486,14 +492,26 @@ int spray_rt_ooc_intersect(spray_rt_ooc_t o, const spray_rt_ray* rays, size_t M,
     o->tie_cap = M;
   }
   const std::vector<float>& boxes = c->h_boxes;
+  // the drains' hit records: one 48-B slot per (ray, batch position)
+  const int per = batch_per(o);
+  const size_t rec_bytes = M * size_t(per) * 48;
+  if (o->rec_cap < rec_bytes) {
+    if (o->rec) HIPCHK(c, hipFree(o->rec));
+    o->rec = nullptr;
+    o->rec_cap = 0;
+    HIPCHK(c, hipMalloc(&o->rec, rec_bytes));
+    o->rec_cap = rec_bytes;
+  }
   uint64_t* key = o->tie;
   if ((r = build_queues(o, rays, nullptr, M, key, nullptr))) return r;
+  o->q.rec = static_cast<uint4*>(o->rec);
+  o->q.rec_per = per;
   const int W = c->ndom <= 64 ? 1 : 4;
   r = drain(o, false, boxes, [&](hipStream_t s, const OocBatch& B, const OocSnapshot& S) {
     return launch_ooc_ch_batch(s, B, W, rays, o->q, c->d_boxes, key, hits, S);
   });
   if (r) return r;
-  HIPCHK(c, launch_ooc_finish(stream_of(c), key, hits, M));
+  HIPCHK(c, launch_ooc_finish(stream_of(c), key, o->q, hits, M));
   return SPRAY_RT_OK;
 }
 

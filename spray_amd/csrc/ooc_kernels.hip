@@ -625,14 +625,27 @@ __device__ __forceinline__ void write_snapshot(uint32_t* live, uint32_t* dshard,
 // and a hit enters the ray's 64-bit key (t bits | list position | domain) by
 // atomicMin.  The key order is the sequential walk's winner rule (nearer t,
 // then the earlier list entry) and keys are unique per (ray, domain), so the
-// result is the same in any drain order and any interleaving.  The pair's
-// own key and winning triangle go to pkey / pleaf for k_ooc_ch_resolve.
+// result is the same in any drain order and any interleaving.
+//
+// The hit record (updateIntersection, trimesh_buffer.cc:328-360) is made in
+// the drain, while the domain is resident, by every pair whose atomicMin
+// lowered the ray's key -- into the ray's record slot of the pair's batch
+// position s (one pair per ray per position per launch).  The final winner
+// lowered the key when it entered it (keys are unique, so the old value was
+// larger), and a slot is written only by a pair that lowers the key:
+// nothing after the winner overwrites its slot.  A domain is drained once
+// per pass, at one batch position (dpos[domain], written by the launch), so
+// k_ooc_finish reads the winner's slot from the final key's domain.  No
+// pair reads another's record inside a launch, so no
+// agent-scope acquire / release is needed (the round-5 in-drain resolve
+// counted each ray's last pair and needed one: L2 write-back + invalidate
+// per pair, 2.4x slower); every read is after a kernel boundary.
 template <int W>
-__device__ __forceinline__ void ch_pair(const OocDomain& D, uint32_t pj, bool valid,
+__device__ __forceinline__ void ch_pair(const OocDomain& D, int slot, uint32_t pj, bool valid,
                                         const spray_rt_ray* rays, const uint32_t* idx,
                                         const uint64_t* masks, const float* boxes,
-                                        uint64_t* key, uint64_t* pkey, uint32_t* pleaf,
-                                        int32_t* stack, uint32_t* dead) {
+                                        uint64_t* key, uint4* rec, int per, int32_t* stack,
+                                        uint32_t* dead) {
   const uint32_t i = valid ? idx[pj] : 0u;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
   uint64_t k0 = kOocMissKey;
@@ -658,103 +671,107 @@ __device__ __forceinline__ void ch_pair(const OocDomain& D, uint32_t pj, bool va
   uint64_t dm[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) dm[w] = 0;
-  if (valid) {
-    uint64_t mine = kOocMissKey;
-    if (best.leaf != 0xFFFFFFFFu) {
-      uint64_t m[W];
+  bool lowered = false;
+  uint64_t mine = kOocMissKey;
+  if (valid && best.leaf != 0xFFFFFFFFu) {
+    uint64_t m[W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
-      mine = (uint64_t(__float_as_uint(best.t)) << 32) |
-             (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
-      const uint64_t old =
-          atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
-      if (mine < old) {
-        const float to = old == kOocMissKey ? kInf : __uint_as_float(uint32_t(old >> 32));
-        if (best.t < to) death_mask<W>(m, boxes, dr, best.t, to, dm);
-      }
+    for (int w = 0; w < W; ++w) m[w] = masks[size_t(i) * W + w];
+    mine = (uint64_t(__float_as_uint(best.t)) << 32) |
+           (uint64_t(list_pos<W>(m, boxes, D.domain, te, dr)) << 16) | uint64_t(D.domain);
+    const uint64_t old =
+        atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)mine);
+    if (mine < old) {
+      lowered = true;
+      const float to = old == kOocMissKey ? kInf : __uint_as_float(uint32_t(old >> 32));
+      if (best.t < to) death_mask<W>(m, boxes, dr, best.t, to, dm);
     }
-    pkey[pj] = mine;
-    pleaf[pj] = best.leaf;
+  }
+  if (lowered) {
+    SlotDesc sd{};
+    sd.tris = static_cast<const float*>(D.tris);
+    sd.faces = D.faces;
+    sd.colors = D.colors;
+    sd.normals = D.normals;
+    const uint32_t prim = reinterpret_cast<const GAS uint32_t*>(gptr(D.prims))[best.leaf];
+    float hu, hv;
+    const float4 c = hit_uv(sd, r, o4.w, best.leaf, hu, hv);
+    uint32_t color;
+    float nsx, nsy, nsz;
+    epilogue(sd, prim, hu, hv, color, nsx, nsy, nsz);
+    // the hit record (spray_rt_hit: t u v prim | Ng color | Ns domain)
+    uint4* rp = rec + (size_t(i) * size_t(per) + size_t(slot)) * 3;
+    rp[0] = make_uint4(__float_as_uint(best.t), __float_as_uint(hu), __float_as_uint(hv), prim);
+    rp[1] = make_uint4(__float_as_uint(c.y), __float_as_uint(c.z), __float_as_uint(c.w), color);
+    rp[2] = make_uint4(__float_as_uint(nsx), __float_as_uint(nsy), __float_as_uint(nsz),
+                       uint32_t(D.domain));
   }
   wave_add_deaths<W>(dm, dead);
 }
 
+// The launch's deaths go to shard set S.launch & 1; its block 0 publishes
+// the launch before it (set (S.launch - 1) & 1, complete at this kernel's
+// start: block 0 is dispatched first), as the any-hit drains do -- the
+// closest-hit pass needs no resolve launch of its own.  The drain and copy
+// blocks follow at blockIdx.x - 1.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_ooc_ch_batch(
     OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
     const uint64_t* __restrict__ masks, const float* __restrict__ boxes,
-    uint64_t* __restrict__ key, uint64_t* __restrict__ pkey, uint32_t* __restrict__ pleaf,
-    uint32_t* __restrict__ dshard) {
-  if (blockIdx.x >= B.copy0) {
-    prefetch_copy(B, blockIdx.x);
+    uint64_t* __restrict__ key, uint4* __restrict__ rec, int per, uint8_t* __restrict__ dpos,
+    uint32_t* __restrict__ dshard, uint32_t* __restrict__ live, OocSnapshot S, int ndom) {
+  const size_t set = size_t(ndom) * kOocDeadShards;
+  if (blockIdx.x == 0) {  // the batch's positions, the previous launch's counts
+    if (threadIdx.x < unsigned(B.count)) dpos[B.d[threadIdx.x].domain] = uint8_t(threadIdx.x);
+    if (S.launch > 0) {
+      OocSnapshot P = S;
+      P.launch = S.launch - 1;
+      write_snapshot(live, dshard + ((S.launch - 1) & 1u) * set, P, ndom);
+    }
     return;
   }
+  const uint32_t blk = blockIdx.x - 1;
+  if (blk >= B.copy0) {
+    prefetch_copy(B, blk);
+    return;
+  }
+  dshard += (S.launch & 1u) * set;
   __shared__ int32_t wstack[kWaves * kStack];
   __shared__ uint32_t dead[64 * W];
   for (int k = threadIdx.x; k < 64 * W; k += kBlock) dead[k] = 0;
   __syncthreads();
   uint32_t pj;
   bool valid;
-  const int s = batch_pair(B, pj, valid, blockIdx.x);
+  const int s = batch_pair(B, pj, valid, blk);
   if (s >= 0)
-    ch_pair<W>(B.d[s], pj, valid, rays, idx, masks, boxes, key, pkey, pleaf,
+    ch_pair<W>(B.d[s], s, pj, valid, rays, idx, masks, boxes, key, rec, per,
                wstack + (threadIdx.x >> 6) * kStack, dead);
   flush_deaths<W>(dead, dshard);
 }
 
-// Hit records of the batch's winners: the one pair whose key equals its
-// ray's minimum runs updateIntersection (trimesh_buffer.cc:328-360) while
-// its domain is still resident.  A later batch with a smaller key rewrites
-// the record.  Block 0 first publishes the batch's live counts.
-__global__ __launch_bounds__(kBlock) void k_ooc_ch_resolve(
-    OocBatch B, const spray_rt_ray* __restrict__ rays, const uint32_t* __restrict__ idx,
-    const uint64_t* __restrict__ key, const uint64_t* __restrict__ pkey,
-    const uint32_t* __restrict__ pleaf, spray_rt_hit* __restrict__ hits,
-    uint32_t* __restrict__ live, uint32_t* __restrict__ dshard, OocSnapshot S, int ndom) {
-  if (blockIdx.x == 0) write_snapshot(live, dshard, S, ndom);
-  uint32_t pj;
-  bool valid;
-  const int s = batch_pair(B, pj, valid, blockIdx.x);
-  if (s < 0 || !valid) return;
-  const uint64_t mine = pkey[pj];
-  if (mine == kOocMissKey) return;
-  const uint32_t i = idx[pj];
-  if (key[i] != mine) return;
-  const OocDomain& D = B.d[s];
-  const float4* rp = reinterpret_cast<const float4*>(rays + i);
-  const float4 o4 = rp[0], d4 = rp[1];
-  const Ray r = make_ray(o4.x, o4.y, o4.z, d4.x, d4.y, d4.z);
-  SlotDesc sd{};
-  sd.tris = static_cast<const float*>(D.tris);
-  sd.faces = D.faces;
-  sd.colors = D.colors;
-  sd.normals = D.normals;
-  const uint32_t leaf = pleaf[pj];
-  const uint32_t prim = reinterpret_cast<const GAS uint32_t*>(gptr(D.prims))[leaf];
-  float hu, hv;
-  const float4 c = hit_uv(sd, r, o4.w, leaf, hu, hv);
-  uint32_t color;
-  float nsx, nsy, nsz;
-  epilogue(sd, prim, hu, hv, color, nsx, nsy, nsz);
-  float4* hp = reinterpret_cast<float4*>(hits + i);
-  hp[0] = make_float4(__uint_as_float(uint32_t(mine >> 32)), hu, hv, __uint_as_float(prim));
-  hp[1] = make_float4(c.y, c.z, c.w, __uint_as_float(color));
-  hp[2] = make_float4(nsx, nsy, nsz, __int_as_float(D.domain));
-}
-
-// Miss records of the rays whose key is still kOocMissKey after the last
-// batch (every other record was written by its winner's resolve); one lane
-// per 16-byte quarter of a record, so a wave stores whole lines.
+// The hit records of a closest-hit pass: a miss record where the key is
+// still kOocMissKey, else the winner's record slot -- the batch position its
+// domain had (dpos, k_ooc_ch_batch).  One lane per 16-B quarter of a
+// record, so a wave stores whole lines.
 __global__ __launch_bounds__(kBlock) void k_ooc_finish(const uint64_t* __restrict__ key,
+                                                       const uint4* __restrict__ rec, int per,
+                                                       const uint8_t* __restrict__ dpos,
                                                        spray_rt_hit* __restrict__ hits,
                                                        size_t M) {
   const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
   const size_t i = j / 3;
-  if (i >= M || key[i] != kOocMissKey) return;
+  if (i >= M) return;
   const int part = int(j - 3 * i);
-  const float4 v = part == 0   ? make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu))
-                   : part == 1 ? make_float4(0.f, 0.f, 0.f, __uint_as_float(0u))
-                               : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  const uint64_t k = key[i];
+  float4 v = part == 0   ? make_float4(kInf, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu))
+             : part == 1 ? make_float4(0.f, 0.f, 0.f, __uint_as_float(0u))
+                         : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  if (k != kOocMissKey) {
+    const uint32_t s = dpos[uint32_t(k) & 0xFFFFu];
+    const uint4 q = rec[(size_t(i) * size_t(per) + s) * 3 + size_t(part)];
+    v = make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z),
+                    __uint_as_float(q.w));
+  }
   reinterpret_cast<float4*>(hits)[j] = v;
 }
 
@@ -905,29 +922,25 @@ static unsigned batch_grid(OocBatch& B) {
 hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_ray* rays,
                                const OocScratch& q, const float* boxes, uint64_t* key,
                                spray_rt_hit* hits, OocSnapshot snap) {
-  if (B.count <= 0 || B.count > kOocBatch) return hipErrorInvalidValue;
+  (void)hits;  // the records go to q.rec; k_ooc_finish writes hits
+  if (B.count <= 0 || B.count > kOocBatch || B.count > q.rec_per) return hipErrorInvalidValue;
   const int ndom = 64 * W;
   unsigned g = batch_grid(B);
-  const unsigned gc = g + (B.pf_count ? B.ncopy : 0);
-  if (g == 0) g = 1;  // the resolve publishes even when empty
-  if (gc) {
-    if (W == 1)
-      k_ooc_ch_batch<1><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
-                                              q.pleaf, q.dshard);
-    else
-      k_ooc_ch_batch<4><<<gc, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.pkey,
-                                              q.pleaf, q.dshard);
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  k_ooc_ch_resolve<<<g, kBlock, 0, s>>>(B, rays, q.val, key, q.pkey, q.pleaf, hits, q.live,
-                                        q.dshard, snap, ndom);
+  g += B.pf_count ? B.ncopy : 0;
+  g += 1;  // block 0 publishes the previous launch's counts
+  if (W == 1)
+    k_ooc_ch_batch<1><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.rec, q.rec_per,
+                                           q.dpos, q.dshard, q.live, snap, ndom);
+  else
+    k_ooc_ch_batch<4><<<g, kBlock, 0, s>>>(B, rays, q.val, q.masks, boxes, key, q.rec, q.rec_per,
+                                           q.dpos, q.dshard, q.live, snap, ndom);
   return hipGetLastError();
 }
 
-hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* hits, size_t M) {
+hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, const OocScratch& q,
+                             spray_rt_hit* hits, size_t M) {
   if (M == 0) return hipSuccess;
-  k_ooc_finish<<<grid_for(3 * M), kBlock, 0, s>>>(key, hits, M);
+  k_ooc_finish<<<grid_for(3 * M), kBlock, 0, s>>>(key, q.rec, q.rec_per, q.dpos, hits, M);
   return hipGetLastError();
 }
 

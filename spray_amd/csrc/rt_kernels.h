@@ -289,8 +289,9 @@ struct OocScratch {
   unsigned long long* score;  // [256] DomainStats score per domain
   uint32_t* live;             // [256] live pairs per queue (see k_ooc_ch_batch)
   uint32_t* dshard;           // [2][256 * kOocDeadShards] deaths since the last snapshot
-  uint64_t* pkey;             // [pair_cap] closest-hit key of each (ray, domain) pair
-  uint32_t* pleaf;            // [pair_cap] its triangle (leaf order)
+  uint4* rec;                 // [M][rec_per][3] closest-hit records per batch position
+  int rec_per;                // batch positions per ray (the drain's batch size)
+  uint8_t* dpos;              // [256] a domain's batch position in the closest-hit pass
   size_t block_cap;           // >= ndom * ray blocks
   size_t chunk_cap;           // >= ndom * ceil(ray blocks / kOocChunk)
   size_t pair_cap;
@@ -351,7 +352,8 @@ hipError_t launch_ooc_ch_batch(hipStream_t s, OocBatch B, int W, const spray_rt_
                                const OocScratch& q, const float* boxes, uint64_t* key,
                                spray_rt_hit* hits, OocSnapshot snap);
 // Miss records of the rays no batch hit (after the last closest-hit batch).
-hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, spray_rt_hit* hits, size_t M);
+hipError_t launch_ooc_finish(hipStream_t s, const uint64_t* key, const OocScratch& q,
+                             spray_rt_hit* hits, size_t M);
 // Any hit of a batch; the pairs of newly occluded rays are counted off
 // q.live.  Launch k adds its deaths to shard set k & 1 of q.dshard (sets
 // 64 * W * kOocDeadShards words apart); its block 0 publishes launch k - 1's
