@@ -262,6 +262,7 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False, p
         if world > 1:
             dist.barrier()
         s0 = eng.stats()
+        eng.collective_log()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             tot = frame()
@@ -270,6 +271,7 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False, p
             dist.barrier()
         el = time.perf_counter() - t0
         s1 = eng.stats()
+        clog = eng.collective_log()
         # per-phase device times (HIP events on the stream), a separate pass
         eng.set_timing(True)
         eng.phase_times()
@@ -310,6 +312,9 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False, p
            "rank0_host_count_reads_per_step": (s1["host_count_reads"] -
                                                s0["host_count_reads"]) / k,
            "rank0_collectives_per_step": (s1["collectives"] - s0["collectives"]) / k,
+           # one frame's issue sequence (op, count, stream): identical on every
+           # rank (RCCL's rule; tests/test_gpu_insitu.py::same_collectives)
+           "rank0_collective_log": [list(c) for c in clog[:len(clog) // max(k, 1)]],
            "rank0_phases_ms": phases,
            "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
            "partition": partition or args.partition,
@@ -390,7 +395,7 @@ def run_image(args, dist, world, rank, local, cam):
            "rays_per_step": rays_step, "radiance_rays": tot[0], "shadow_rays": tot[1],
            "max_rank_frame_ms": round(mx, 4), "rank0_phases_ms": phases,
            "bands_per_rank": bands,
-           "rank0_collectives_per_step": [list(c) for c in clog[:len(clog) // max(k, 1)]],
+           "rank0_collective_log": [list(c) for c in clog[:len(clog) // max(k, 1)]],
            "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
            "config": "configs[1] frame split by image rows over %d GPU(s): all 64 domains resident "
                      "per GPU, %d row band(s) per rank, eye rays + fused closest hit / PT shadow "

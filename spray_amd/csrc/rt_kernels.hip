@@ -1201,7 +1201,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
   // spawned shadow rays of the wave, added to *sh_count once at its end (a
   // same-address atomic per chunk queued ~10^5 atomics behind each other)
   uint32_t wcount = 0;
-  const bool persist = ANY ? (SPRAY_PERSIST_AH != 0 || A.persist != 0) : SPRAY_PERSIST_CH != 0;
+  // persistent waves dequeue chunks; a launch of at most one packet per
+  // resident wave runs one packet per wave instead (set by the launcher)
+  const bool persist = A.persist != 0;
   const int lane = threadIdx.x & 63;
   const uint32_t* __restrict__ idx = A.idx;
   if (!persist) {
@@ -2128,9 +2130,7 @@ hipError_t launch_domains(hipStream_t s, const float* boxes, int ndom,
 
 template <int W, bool ANY, bool COUNT, int EPI, int STK, int TRAV>
 static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
-  const bool kPersist =
-      ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays) : SPRAY_PERSIST_CH != 0;
-  a.persist = kPersist ? 1 : 0;
+  bool kPersist = ANY ? (SPRAY_PERSIST_AH != 0 || a.M >= kPersistAhRays) : SPRAY_PERSIST_CH != 0;
   static int grid = 0;  // resident blocks (per process; gfx950 only)
   if (kPersist && !grid) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -2143,6 +2143,13 @@ static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
     if (e != hipSuccess) return e;
     grid = cus * (per_cu > 0 ? per_cu : 1);
   }
+  // No more packets than the persistent grid has waves (a rank's share of a
+  // camera frame, a small batch): one packet per wave, no queue.  Every
+  // wave of a persistent grid dequeues from the few non-empty queues at once
+  // and then sweeps the drained ones -- ~45-55 us for a launch of one
+  // packet, against one block's walk here.
+  if (kPersist && !a.d_count && (a.M + 63) / 64 <= size_t(grid) * (kBlock / 64)) kPersist = false;
+  a.persist = kPersist ? 1 : 0;
   hipError_t e = hipSuccess;
   if (kPersist && !a.heads_ready) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
   if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) &&
