@@ -354,7 +354,9 @@ def run_image(args, dist, world, rank, local, cam):
     sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
                                      lights=lights)
     image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
-    bands = args.image_bands if world > 1 else 1
+    bands = args.image_bands or (4 if world <= 4 else 1)
+    if world == 1:
+        bands = 1
 
     def frame():
         image.zero_()
@@ -607,8 +609,9 @@ def main():
                          "grouped per rank); at N > 1 the other partitions are timed too")
     ap.add_argument("--image", type=int, default=1,
                     help="also measure the image-parallel strong split (spray_rt_insitu_trace_image)")
-    ap.add_argument("--image-bands", type=int, default=4,
-                    help="row bands per rank of the image-parallel split (interleaved)")
+    ap.add_argument("--image-bands", type=int, default=0,
+                    help="row bands per rank of the image-parallel split (interleaved); 0: 4 up "
+                         "to 4 ranks, 1 above (profiles/r6_image_rehearse.txt)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")
