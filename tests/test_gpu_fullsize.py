@@ -328,7 +328,7 @@ def _run_replicated(world, mode, kind):
 
 def _check_replicated(parts, ref):
     # RCCL's rule: every rank enqueues the same collectives in the same order,
-    # the side stream's included (INTEGRATION.md section 5)
+    # the side stream's included (INTEGRATION.md section 4)
     assert len(parts[0]["clog"]) >= 3
     for p in parts[1:]:
         assert np.array_equal(p["clog"], parts[0]["clog"])

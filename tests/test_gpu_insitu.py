@@ -180,7 +180,7 @@ def _reference(oracle, case):
 
 def same_collectives(results):
     """Every rank issued the same collectives in the same order, on the same
-    streams (RCCL's rule for one communicator; INTEGRATION.md section 5)."""
+    streams (RCCL's rule for one communicator; INTEGRATION.md section 4)."""
     logs = [r[3]["clog"] for r in results]
     assert logs[0], "no collective logged"
     for k, lg in enumerate(logs[1:], 1):
