@@ -302,7 +302,8 @@ def run_insitu(args, dist, world, rank, local, cam, kind="pt", protocol=False, p
             "SUM-all-reduced, every rank any-hits the AO pairs entering its boxes "
             "(compacted), occlusion count fields SUM-all-reduced, film on rank 0"
             if replicated and world > 1
-            else "eye rays + all-local frame" if replicated or (world == 1 and not protocol)
+            else "the eye rays of the pixels some box's footprint covers (the others counted as "
+                 "misses) + all-local frame" if replicated or (world == 1 and not protocol)
             else "stripe protocol: speculative ray exchange over RCCL all-to-all-v, image "
                  "composite by RCCL reduce")
     out = {"value": round(rays_step * k / el / 1e6, 3), "unit": "Mrays/s",
@@ -354,7 +355,7 @@ def run_image(args, dist, world, rank, local, cam):
     sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
                                      lights=lights)
     image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
-    bands = args.image_bands or (4 if world <= 4 else 1)
+    bands = args.image_bands or (1 if world <= 2 else 4)
     if world == 1:
         bands = 1
 
@@ -400,7 +401,8 @@ def run_image(args, dist, world, rank, local, cam):
            "rank0_collective_log": [list(c) for c in clog[:len(clog) // max(k, 1)]],
            "image_mean": round(float(image.view(-1, 4)[:, :3].mean()), 6) if rank == 0 else None,
            "config": "configs[1] frame split by image rows over %d GPU(s): all 64 domains resident "
-                     "per GPU, %d row band(s) per rank, eye rays + fused closest hit / PT shadow "
+                     "per GPU, %d row band(s) per rank, the eye rays of the band pixels some box's "
+                     "footprint covers (the others counted as misses) + fused closest hit / PT shadow "
                      "any hit + film per rank, rows gathered to rank 0 over RCCL" % (world, bands)}
     eng.close()
     rt.close()
@@ -610,8 +612,8 @@ def main():
     ap.add_argument("--image", type=int, default=1,
                     help="also measure the image-parallel strong split (spray_rt_insitu_trace_image)")
     ap.add_argument("--image-bands", type=int, default=0,
-                    help="row bands per rank of the image-parallel split (interleaved); 0: 4 up "
-                         "to 4 ranks, 1 above (profiles/r6_image_rehearse.txt)")
+                    help="row bands per rank of the image-parallel split (interleaved); 0: 1 up "
+                         "to 2 ranks, 4 above (profiles/r6_image_cull_rehearse.txt)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")

@@ -226,6 +226,12 @@ struct spray_rt_insitu {
   size_t last_npair_ao = 0;  // and its AO pairs (nc x samples)
   DBuf ctmin, ccomp, crays, cpix, csam, ciota;
   DBuf gpack;  // image frames: the rank's interleaved bands packed / the root's gather
+  // image frames: the run table of U within this rank's bands (its eye
+  // rays), its key, and U's pixel count over the whole image
+  std::vector<float> img_key;
+  DBuf ti_runs, ti_first;
+  CamTable ti{};
+  uint64_t img_upix = 0;
   size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
@@ -1713,7 +1719,8 @@ void free_all(spray_rt_insitu* I) {
                  &I->rslot_c, &I->rslot_pix, &I->rcompact, &I->rnp, &I->rtk, &I->rlp, &I->rbmax,
                  &I->aflag, &I->aown, &I->asel_tmp, &I->abits, &I->tu_runs, &I->tu_first,
                  &I->te_runs, &I->te_first, &I->ts_runs, &I->ts_first, &I->ctmin, &I->ccomp,
-                 &I->crays, &I->cpix, &I->csam, &I->ciota};
+                 &I->crays, &I->cpix, &I->csam, &I->ciota, &I->gpack, &I->ti_runs,
+                 &I->ti_first};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
@@ -2087,32 +2094,62 @@ int spray_rt_insitu_trace_camera(spray_rt_insitu_t I, const spray_rt_shader* P,
   F.spp = spp;
   const char* fr = std::getenv("SPRAY_INSITU_REPLICATED");
   const bool force_rep = fr && fr[0] == '1';
+  // one rank: the one-band image frame (U's eye rays, then the all-local
+  // fused frame); every domain is resident at world 1
+  if (I->world == 1 && !force_rep)
+    return spray_rt_insitu_trace_image(I, P, cam, image_w, image_h, spp, 1, image, rec, totals);
   I->nev = 0;
   I->tr->serial_begin();
-  if (I->world == 1 && !force_rep) {
-    // one rank: the whole frame's eye rays, then the all-local fused frame
-    hipStream_t s = stream_of(c);
-    r = grow(I, I->crays, n * 32 + 32);
-    if (!r) r = grow(I, I->cpix, n * 4 + 4);
-    if (!r) r = grow(I, I->csam, n * 4 + 4);
-    if (!r && launch_eye_rays_insitu(s, cam, image_w, spp, 0, 0, image_w, 0, 0, image_w, image_h,
-                                     I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
-                                     I->csam.as<int32_t>()) != hipSuccess)
-      r = fail(c, SPRAY_RT_ERR_HIP, "eye rays");
-    if (!r)
-      r = trace_local(I, P, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
-                      I->csam.as<int32_t>(), n, spp, image, rec, totals);
-    flush_phases(I, 1);
-  } else {
-    r = ao ? trace_camera_ao(I, P, F, image_h, image, rec, totals)
-           : trace_camera_pt(I, P, F, image_h, image, rec, totals);
-  }
+  r = ao ? trace_camera_ao(I, P, F, image_h, image, rec, totals)
+         : trace_camera_pt(I, P, F, image_h, image, rec, totals);
   I->tr->serial_end();
   return r;
 }
 
 // Rows of band b of bt bands over h rows: [b h / bt, (b + 1) h / bt).
 inline int band_row(int b, int bt, int h) { return int((long long)b * h / bt); }
+
+// The image frame's eye-ray table: U (the pixels whose eye rays may enter a
+// domain box: the union of every box's screen footprint, footprint.h)
+// restricted to this rank's bands, rebuilt when the camera, the boxes or the
+// split change; img_upix = U's pixels over the whole image.
+int prepare_image(spray_rt_insitu* I, const float cam[14], int image_w, int image_h, int bands) {
+  spray_rt_ctx* c = I->ctx;
+  const int n = c->ndom;
+  std::vector<float> key(cam, cam + 14);
+  for (int v : {image_w, image_h, bands, I->world, I->rank}) key.push_back(float(v));
+  for (int k = 0; k < 6 * n; ++k) key.push_back(c->h_boxes[size_t(k)]);
+  if (key.size() == I->img_key.size() &&
+      std::memcmp(key.data(), I->img_key.data(), key.size() * sizeof(float)) == 0)
+    return SPRAY_RT_OK;
+  fp::Proj pj;
+  if (!fp::make_proj(cam, &pj)) return fail(c, SPRAY_RT_ERR_ARG, "degenerate camera");
+  fp::Rows U(static_cast<size_t>(image_h));
+  bool all = false;
+  for (int d = 0; d < n; ++d)
+    all = fp::box_rows(pj, &c->h_boxes[6 * size_t(d)], image_w, image_h, U) == 2 || all;
+  if (all)
+    for (auto& row : U) row.assign(1, {0, image_w - 1});
+  fp::merge_rows(U);
+  uint64_t upix = 0;
+  for (const auto& row : U)
+    for (const auto& iv : row) upix += uint64_t(iv.second - iv.first + 1);
+  const int bt = I->world * bands;
+  std::vector<char> keep(static_cast<size_t>(image_h), 0);
+  for (int b = I->rank; b < bt; b += I->world)
+    for (int y = band_row(b, bt, image_h); y < band_row(b + 1, bt, image_h); ++y)
+      keep[size_t(y)] = 1;
+  for (size_t y = 0; y < U.size(); ++y)
+    if (!keep[y]) U[y].clear();
+  try {
+    CALL(upload_table(I, fp::make_table(U, image_w, nullptr), I->ti_runs, I->ti_first, &I->ti));
+  } catch (const std::exception& e) {
+    return fail(c, SPRAY_RT_ERR_STATE, "image frame table: %s", e.what());
+  }
+  I->img_upix = upix;
+  I->img_key.swap(key);
+  return SPRAY_RT_OK;
+}
 
 int spray_rt_insitu_trace_image(spray_rt_insitu_t I, const spray_rt_shader* P,
                                 const float cam[14], int image_w, int image_h, int spp, int bands,
@@ -2149,22 +2186,46 @@ int spray_rt_insitu_trace_image(spray_rt_insitu_t I, const spray_rt_shader* P,
     mine.emplace_back(y0, y1 - y0);
     rows += size_t(y1 - y0);
   }
-  const size_t n = rows * size_t(image_w) * size_t(spp);
+  // The eye rays of U's pixels only: a ray outside every box's footprint
+  // misses the whole domain list (the reference's ISector drops it at the
+  // top level), so it is counted as a traced radiance ray and not launched.
+  // A pixel's samples stay consecutive in one wave (film_runs sums them in
+  // order), so the film's bits match the full frame's when spp | 64; other
+  // spp trace the bands whole.
+  const char* ce = std::getenv("SPRAY_IMAGE_CULL");
+  const bool cull = 64 % spp == 0 && !(ce && ce[0] == '0');
+  if (cull) {
+    r = prepare_image(I, cam, image_w, image_h, bands);
+    if (r) return r;
+  }
+  const size_t n = cull ? size_t(I->ti.npix) * size_t(spp) : rows * size_t(image_w) * size_t(spp);
   I->nev = 0;
   I->tr->serial_begin();
   r = grow(I, I->crays, n * 32 + 32);
   if (!r) r = grow(I, I->cpix, n * 4 + 4);
   if (!r) r = grow(I, I->csam, n * 4 + 4);
   if (!r) r = mark(I, 0);
-  size_t off = 0;
-  for (const auto& bnd : mine) {  // eye rays, (pixel, sample) seeds: any split, the same bits
-    if (r || !bnd.second) continue;
-    if (launch_eye_rays_insitu(s, cam, image_w, spp, 0, 0, image_w, 0, bnd.first, image_w,
-                               bnd.second, I->crays.as<spray_rt_ray>() + off,
-                               I->cpix.as<int32_t>() + off, I->csam.as<int32_t>() + off) !=
-        hipSuccess)
-      r = fail(c, SPRAY_RT_ERR_HIP, "eye rays");
-    off += size_t(bnd.second) * size_t(image_w) * size_t(spp);
+  if (cull) {
+    if (!r && n) {
+      CamFrame F{};
+      for (int k = 0; k < 14; ++k) F.cam[k] = cam[k];
+      F.image_w = image_w;
+      F.spp = spp;
+      if (launch_cam_eye_rays(s, I->ti, F, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
+                              I->csam.as<int32_t>()) != hipSuccess)
+        r = fail(c, SPRAY_RT_ERR_HIP, "eye rays");
+    }
+  } else {
+    size_t off = 0;
+    for (const auto& bnd : mine) {  // eye rays, (pixel, sample) seeds: any split, the same bits
+      if (r || !bnd.second) continue;
+      if (launch_eye_rays_insitu(s, cam, image_w, spp, 0, 0, image_w, 0, bnd.first, image_w,
+                                 bnd.second, I->crays.as<spray_rt_ray>() + off,
+                                 I->cpix.as<int32_t>() + off, I->csam.as<int32_t>() + off) !=
+          hipSuccess)
+        r = fail(c, SPRAY_RT_ERR_HIP, "eye rays");
+      off += size_t(bnd.second) * size_t(image_w) * size_t(spp);
+    }
   }
   // the rows to rank 0 (HdrImage::composite, image.h:167-181: an MPI_Reduce
   // SUM of disjoint pixels in the reference; here each rank's rows alone):
@@ -2208,6 +2269,8 @@ int spray_rt_insitu_trace_image(spray_rt_insitu_t I, const spray_rt_shader* P,
   if (!r)
     r = trace_local(I, P, I->crays.as<spray_rt_ray>(), I->cpix.as<int32_t>(),
                     I->csam.as<int32_t>(), n, spp, image, rec, totals, gather);
+  if (!r && cull && totals)  // the group's culled eye rays: every pixel outside U
+    totals[0] += (uint64_t(image_w) * uint64_t(image_h) - I->img_upix) * uint64_t(spp);
   flush_phases(I, 1);
   I->tr->serial_end();
   return r;

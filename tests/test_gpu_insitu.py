@@ -772,6 +772,41 @@ def test_engine_image_frame_ranks(oracle, world, bands, case):
         assert not im[~rows].any()
 
 
+@pytest.mark.parametrize("case", ["pt1", "ao16"])
+def test_engine_image_frame_cull_matches_whole_bands(monkeypatch, case):
+    """The image frame launches U's eye rays only (pixels outside every box's
+    footprint are counted, not traced): image bits, totals and records equal
+    to the frame that traces its bands whole (SPRAY_IMAGE_CULL=0)."""
+    culled = _image_frame(0, 1, case, "rccl", bands=2)
+    monkeypatch.setenv("SPRAY_IMAGE_CULL", "0")
+    whole = _image_frame(0, 1, case, "rccl", bands=2)
+    assert culled[1] == whole[1]
+    np.testing.assert_array_equal(culled[2].view(np.uint32), whole[2].view(np.uint32))
+    assert H.records_dict(culled[0]) == H.records_dict(whole[0])
+
+
+def test_engine_image_frame_facing_away(spray):
+    """A camera that sees no box: no eye ray launched, every one counted."""
+    from spray_amd import insitu
+    rt = spray.RtContext(0)
+    nd = len(spray.engine.host_parse_scene(WAVELETS64, SCENES)[0])
+    insitu.setup_rank_context(rt, WAVELETS64, SCENES, np.zeros(nd, np.int32), 0)
+    rt.set_bsdfs(spray.engine.host_scene_bsdfs(WAVELETS64))
+    rt.set_stream(torch.cuda.current_stream())
+    eng = insitu.InsituEngine(rt, 1, 0, transport="rccl")
+    c = H.BENCH_CAMERA
+    away = [2 * p - q for p, q in zip(c["pos"], c["lookat"])]
+    cam = spray.camera_init(c["pos"], away, c["up"], 60.0, 64, 48)
+    sh = spray.frame.make_shader("pt", 1, 1, lights=[(0, 0.0, 500.0, 1000.0, 1.0, 1.0, 1.0)])
+    image = torch.zeros(64 * 48 * 4, dtype=torch.float32, device="cuda")
+    tot = eng.trace_image(sh, cam, 64, 48, 4, image)
+    torch.cuda.synchronize()
+    assert tuple(tot) == (64 * 48 * 4, 0)
+    assert not image.any()
+    eng.close()
+    rt.close()
+
+
 def test_engine_image_frame_needs_every_domain(spray):
     """A rank missing a domain cannot trace an image-parallel frame."""
     from spray_amd import insitu
