@@ -976,24 +976,31 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   GROW(I->ssv, MS);
   GROW(I->socc, MS);
   MARK(0);
-  HIPCHK(c, hipMemsetAsync(I->dstats.p, 0, 4 * 8, s));
   unsigned long long* st = I->dstats.as<unsigned long long>();
+  unsigned long long* dt = I->dtot.as<unsigned long long>();
   spray_rt_hit* hits = I->ohit.as<spray_rt_hit>();
   uint8_t* sv = I->ssv.as<uint8_t>();
   uint8_t* occ = I->socc.as<uint8_t>();
   float* sw = I->ssw.as<float>();
-  if (n && fused_pt_shading(c, P)) {
+  // the fused PT frame: three launches -- the queue heads and the shadow
+  // count cleared, the fused launch, the film writing the totals (no
+  // counters pass, no copies)
+  const bool fused = n && fused_pt_shading(c, P);
+  if (!fused) HIPCHK(c, hipMemsetAsync(I->dstats.p, 0, 4 * 8, s));
+  if (fused) {
     const spray_rt_light& lt = P->lights[0];
     const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
                                lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                                P->ks[2],       P->shininess};
     uint32_t* nshadow = I->dnum.as<uint32_t>();
+    uint32_t* heads1 = c->d_heads + kHeadsBytes / sizeof(uint32_t);
+    const ClearSeg cs[2] = {{heads1, kHeadsBytes, 0}, {nshadow, 4, 0}};
+    HIPCHK(c, launch_clear(s, cs, 2));
     // hit records only for the per-sample records (the film needs the
     // shading and occlusion alone: 48 B per ray not written)
     HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, n, rec ? hits : nullptr, shade10, occ, sv,
-                                    sw, nshadow));
-    HIPCHK(c, launch_frame_stats_add(s, st, 1, n, nshadow));
-    HIPCHK(c, launch_film_atomic(s, image, pixid, n, ns, sw, sv, occ, scale));
+                                    sw, nshadow, heads1));
+    HIPCHK(c, launch_film_atomic(s, image, pixid, n, ns, sw, sv, occ, scale, 4, dt, nshadow, n));
     if (rec) {
       HIPCHK(c, launch_hit_flags(s, nullptr, hits, n, I->owin.as<uint8_t>()));
       HIPCHK(c, launch_record(s, I->owin.as<uint8_t>(), n, 0, ns, samid, hits, sv, occ, *rec));
@@ -1032,10 +1039,7 @@ int trace_local(spray_rt_insitu* I, const spray_rt_shader* P, const spray_rt_ray
   }
   if (before_totals) CALL(before_totals());  // the image frame's row gather
   // the group's totals: radiance rays = live slots shaded, shadows, aborts
-  unsigned long long* dt = I->dtot.as<unsigned long long>();
-  HIPCHK(c, hipMemcpyAsync(dt, st + 3, 8, hipMemcpyDeviceToDevice, s));
-  HIPCHK(c, hipMemcpyAsync(dt + 1, st + 1, 8, hipMemcpyDeviceToDevice, s));
-  HIPCHK(c, hipMemcpyAsync(dt + 2, st, 8, hipMemcpyDeviceToDevice, s));
+  if (!fused) HIPCHK(c, launch_totals_of_stats(s, st, dt));
   COMM(I->tr->allreduce_u64(I, dt, 3));
   unsigned long long* ht = I->h_small + 200;
   HIPCHK(c, hipMemcpyAsync(ht, dt, 3 * 8, hipMemcpyDeviceToHost, s));

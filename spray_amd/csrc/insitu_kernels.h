@@ -46,10 +46,13 @@ hipError_t launch_winners(hipStream_t s, const uint64_t* key, const uint64_t* be
 // occ[sel[idx[j]]] = 1 where ret[j]
 hipError_t launch_occ_return(hipStream_t s, const int64_t* idx, const uint8_t* ret, size_t n,
                              const uint32_t* sel, uint8_t* occ);
-// image + stride * pix[i] (+0, +1, +2) += the unoccluded weights of copy i
+// image + stride * pix[i] (+0, +1, +2) += the unoccluded weights of copy i;
+// tot (optional): {nrad, *nsh, 0} written by the first lane (a fused
+// frame's totals without a counters pass)
 hipError_t launch_film_atomic(hipStream_t s, float* image, const int32_t* pix, size_t m, int ns,
                               const float* sw, const uint8_t* sv, const uint8_t* occ,
-                              double scale, int stride = 4);
+                              double scale, int stride = 4, unsigned long long* tot = nullptr,
+                              const uint32_t* nsh = nullptr, unsigned long long nrad = 0);
 hipError_t launch_record(hipStream_t s, const uint8_t* win, size_t m, int bounce, int ns,
                          const int32_t* sam, const spray_rt_hit* hits, const uint8_t* sv,
                          const uint8_t* occ, const spray_rt_insitu_rec& rec);
@@ -129,6 +132,9 @@ hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t*
 hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
                              const float* compact, size_t np);
 // tail[64 c + k] = bit k of {nrad, the nshadow counters' sum, 0}[c] (192 bytes)
+// tot = {stats[3] (live slots shaded), stats[1] (shadows), stats[0] (aborts)}
+hipError_t launch_totals_of_stats(hipStream_t s, const unsigned long long* stats,
+                                  unsigned long long* tot);
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow);
 // ---- replicated-ray AO frames (insitu.cpp, trace_replicated_ao) ----

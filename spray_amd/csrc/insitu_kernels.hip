@@ -208,8 +208,16 @@ __global__ __launch_bounds__(kBlock) void k_film_atomic(float* __restrict__ imag
                                                         const float4* __restrict__ sw,
                                                         const uint8_t* __restrict__ sv,
                                                         const uint8_t* __restrict__ occ,
-                                                        double scale, int stride) {
+                                                        double scale, int stride,
+                                                        unsigned long long* __restrict__ tot,
+                                                        const uint32_t* __restrict__ nsh,
+                                                        unsigned long long nrad) {
   const size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (tot && i == 0) {
+    tot[0] = nrad;
+    tot[1] = *nsh;
+    tot[2] = 0;
+  }
   const bool in = i < m;
   const int32_t p = in ? pix[i] : -1;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
@@ -972,10 +980,13 @@ hipError_t launch_occ_return(hipStream_t s, const int64_t* idx, const uint8_t* r
 }
 hipError_t launch_film_atomic(hipStream_t s, float* image, const int32_t* pix, size_t m, int ns,
                               const float* sw, const uint8_t* sv, const uint8_t* occ,
-                              double scale, int stride) {
-  if (ns == 0) return hipSuccess;
-  LAUNCH(m, k_film_atomic, image, pix, m, ns, reinterpret_cast<const float4*>(sw), sv, occ,
-         scale, stride);
+                              double scale, int stride, unsigned long long* tot,
+                              const uint32_t* nsh, unsigned long long nrad) {
+  if (ns == 0 && !tot) return hipSuccess;
+  k_film_atomic<<<std::max(grid_for(m), 1u), kBlock, 0, s>>>(
+      image, pix, m, ns, reinterpret_cast<const float4*>(sw), sv, occ, scale, stride, tot, nsh,
+      nrad);
+  return hipGetLastError();
 }
 hipError_t launch_record(hipStream_t s, const uint8_t* win, size_t m, int bounce, int ns,
                          const int32_t* sam, const spray_rt_hit* hits, const uint8_t* sv,
@@ -996,6 +1007,15 @@ hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_
 }
 hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
+}
+__global__ void k_totals_of_stats(const unsigned long long* __restrict__ st,
+                                  unsigned long long* __restrict__ tot) {
+  if (threadIdx.x < 3) tot[threadIdx.x] = st[threadIdx.x == 0 ? 3 : threadIdx.x == 1 ? 1 : 0];
+}
+hipError_t launch_totals_of_stats(hipStream_t s, const unsigned long long* stats,
+                                  unsigned long long* tot) {
+  k_totals_of_stats<<<1, 64, 0, s>>>(stats, tot);
+  return hipGetLastError();
 }
 hipError_t launch_rep_totals(hipStream_t s, uint8_t* tail, unsigned long long nrad,
                              const unsigned long long* nshadow) {

@@ -93,7 +93,9 @@ hipError_t launch_scene_intersect_shadow_pt(hipStream_t s, const SceneView& v,
 hipError_t launch_scene_frame_pt(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                  size_t M, spray_rt_hit* hits, const float* shade10,
                                  uint8_t* occluded, uint8_t* sh_valid, float* sw,
-                                 uint32_t* d_count);
+                                 uint32_t* d_count, uint32_t* heads = nullptr);
+// (heads: kHeadsBytes of queue heads the caller zeroed, with *d_count, in
+// one launch -- no memsets before the launch)
 // stats[live], stats[shadows] of the frame counters += M, *d_count
 hipError_t launch_frame_stats_add(hipStream_t s, unsigned long long* stats, int stripes,
                                   size_t M, const uint32_t* d_count);

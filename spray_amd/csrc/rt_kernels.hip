@@ -249,6 +249,7 @@ struct SceneArgs {
   uint32_t* heads;  // kQueues queue heads, 32 words apart (persistent launch)
   int persist;      // any hit: persistent waves (set by the launcher)
   int heads_ready;  // heads zeroed by the caller (no memset before the launch)
+  int count_ready;  // sh_count zeroed by the caller
   // fused PT shadow spawn (closest hit): positional output
   ShadePt shade;
   spray_rt_ray* sh_out;  // [M] shadow ray of source i (valid entries only)
@@ -2150,12 +2151,17 @@ static hipError_t launch_scene_t(hipStream_t s, SceneArgs a) {
   // packet, against one block's walk here.
   if (kPersist && !a.d_count && (a.M + 63) / 64 <= size_t(grid) * (kBlock / 64)) kPersist = false;
   a.persist = kPersist ? 1 : 0;
-  hipError_t e = hipSuccess;
-  if (kPersist && !a.heads_ready) e = hipMemsetAsync(a.heads, 0, kQueues * 32 * sizeof(uint32_t), s);
-  if (e == hipSuccess && (EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) &&
-      a.sh_count)
-    e = hipMemsetAsync(a.sh_count, 0, sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
+  // the queue heads and the spawn count zeroed in one launch
+  ClearSeg cs[2];
+  int ncs = 0;
+  if (kPersist && !a.heads_ready) cs[ncs++] = {a.heads, kHeadsBytes, 0};
+  if ((EPI == kEpiSpawn || EPI == kEpiShadow || EPI == kEpiShadowFrame) && a.sh_count &&
+      !a.count_ready)
+    cs[ncs++] = {a.sh_count, sizeof(uint32_t), 0};
+  if (ncs) {
+    const hipError_t e = launch_clear(s, cs, ncs);
+    if (e != hipSuccess) return e;
+  }
   const unsigned g = kPersist ? unsigned(grid) : grid_for(a.M);
   k_scene<W, ANY, COUNT, EPI, STK, TRAV><<<g, kBlock, 0, s>>>(a);
   return hipGetLastError();
@@ -2340,9 +2346,15 @@ hipError_t launch_scene_intersect_shadow_pt(hipStream_t s, const SceneView& v,
 hipError_t launch_scene_frame_pt(hipStream_t s, const SceneView& v, const spray_rt_ray* rays,
                                  size_t M, spray_rt_hit* hits, const float* shade10,
                                  uint8_t* occluded, uint8_t* sh_valid, float* sw,
-                                 uint32_t* d_count) {
-  if (M == 0) return d_count ? hipMemsetAsync(d_count, 0, sizeof(uint32_t), s) : hipSuccess;
+                                 uint32_t* d_count, uint32_t* heads) {
+  if (M == 0)
+    return d_count && !heads ? hipMemsetAsync(d_count, 0, sizeof(uint32_t), s) : hipSuccess;
   SceneArgs a = scene_args(v, rays, M);
+  if (heads) {  // the caller zeroed them and the count in one launch
+    a.heads = heads;
+    a.heads_ready = 1;
+    a.count_ready = 1;
+  }
   a.hits = hits;
   for (int k = 0; k < 3; ++k) {
     a.shade.lp[k] = shade10[k];
@@ -2665,13 +2677,14 @@ hipError_t launch_clear(hipStream_t s, const ClearSeg* segs, int n) {
   ClearList L{};
   size_t total = 0;
   for (int q = 0; q < n; ++q) {
-    if (segs[q].bytes && (!segs[q].p || (reinterpret_cast<uintptr_t>(segs[q].p) & 15u)))
+    if (segs[q].bytes && (!segs[q].p || (segs[q].bytes >= 16 &&
+                                         (reinterpret_cast<uintptr_t>(segs[q].p) & 15u))))
       return hipErrorInvalidValue;
     L.seg[L.n++] = segs[q];
     total += segs[q].bytes;
   }
   if (total == 0) return hipSuccess;
-  const unsigned g = unsigned(std::min<size_t>((total / 16 + kBlock - 1) / kBlock, 4096));
+  const unsigned g = unsigned(std::min<size_t>((total / 16 + kBlock) / kBlock, 4096));
   k_clear<<<g, kBlock, 0, s>>>(L);
   return hipGetLastError();
 }
