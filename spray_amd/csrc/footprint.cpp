@@ -215,6 +215,21 @@ void merge_rows(Rows& rows) {
   }
 }
 
+Rows union_rows(const Proj& p, const float* boxes, int n, int image_w, int image_h,
+                uint64_t* npix) {
+  Rows U(static_cast<size_t>(image_h));
+  bool all = false;
+  for (int d = 0; d < n; ++d) all = box_rows(p, boxes + 6 * size_t(d), image_w, image_h, U) == 2 || all;
+  if (all)
+    for (auto& row : U) row.assign(1, {0, image_w - 1});
+  merge_rows(U);
+  uint64_t np = 0;
+  for (const auto& row : U)
+    for (const auto& iv : row) np += uint64_t(iv.second - iv.first + 1);
+  if (npix) *npix = np;
+  return U;
+}
+
 Rows intersect_rows(const Rows& a, const Rows& b) {
   Rows out(std::min(a.size(), b.size()));
   for (size_t y = 0; y < out.size(); ++y) {
@@ -261,6 +276,12 @@ Table make_table(const Rows& rows, int image_w, const Table* U) {
       np += len;
     }
   t.npix = np;
+  finish_table(t);
+  return t;
+}
+
+void finish_table(Table& t) {
+  const uint32_t np = t.npix;
   t.runs.push_back(CamRun{0, 0, np, np});  // sentinel
   t.first.assign((np + 7) / 8 + 1, 0u);
   uint32_t r = 0;
@@ -269,7 +290,6 @@ Table make_table(const Rows& rows, int image_w, const Table* U) {
     while (r + 1 < t.runs.size() - 1 && t.runs[r + 1].pbase <= pix) ++r;
     t.first[g] = r;
   }
-  return t;
 }
 
 void partition_view(const float* boxes, int n, const Proj& p, int nranks, int* owner) {

@@ -56,6 +56,10 @@ int shadow_boxes(const float box[6], const float scene[6], const float light[3],
                  float* out);
 constexpr int kShadowSlices = 16;
 void merge_rows(Rows& rows);
+// U: the union of n boxes' footprints (merged rows; a box straddling the eye
+// plane: the whole image); *npix = its pixels
+Rows union_rows(const Proj& p, const float* boxes, int n, int image_w, int image_h,
+                uint64_t* npix);
 Rows intersect_rows(const Rows& a, const Rows& b);
 
 struct Table {
@@ -67,6 +71,8 @@ struct Table {
 // the run table of `rows`; with U (rows inside U's), ubase = the U index of
 // each run's first pixel, else ubase = pbase (the table is U)
 Table make_table(const Rows& rows, int image_w, const Table* U);
+// t.runs (pbase ascending) and t.npix set: the sentinel run and first[]
+void finish_table(Table& t);
 
 // View-aligned partition: the domains' box centres projected to the image,
 // dealt into nranks groups of (nearly) equal count by recursive median

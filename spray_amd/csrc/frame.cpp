@@ -12,6 +12,10 @@
 #include <cstdio>
 #include <vector>
 
+#include <cstdlib>
+#include <cstring>
+
+#include "footprint.h"
 #include "rt_ctx.h"
 #include "rt_kernels.h"
 #include "spray_rt.h"
@@ -57,6 +61,74 @@ struct Carve {
 // film.
 bool fused_frame(const spray_rt_ctx* c, const spray_rt_shader* P) {
   return SPRAY_FRAME_FUSED && spray_rt::detail::fused_pt_shading(c, P);
+}
+
+// The fused frame's eye rays over U only: U = the pixels some domain box's
+// screen footprint covers (footprint.h, conservative for any jitter inside
+// the pixel); an eye ray outside U misses the whole domain list, so it is
+// counted as a radiance ray and not launched.  The run table holds, per
+// tile, the runs of U within it (ubase = the run's first pixel's tile-local
+// id: the jitter seed and sample id of the tile launch), cached by
+// (camera, tiles, boxes).  Returns false when it does not apply
+// (SPRAY_FRAME_CULL=0, a degenerate camera).
+bool frame_table(spray_rt_ctx* c, const float cam[14], int image_w, const int* tiles, int ntiles,
+                 CamTable* T, int* err) {
+  *err = SPRAY_RT_OK;
+  const char* e = std::getenv("SPRAY_FRAME_CULL");
+  if (e && e[0] == '0') return false;
+  std::vector<float> key(cam, cam + 14);
+  key.push_back(float(image_w));
+  key.push_back(float(ntiles));
+  for (int k = 0; k < 4 * ntiles; ++k) key.push_back(float(tiles[k]));
+  key.insert(key.end(), c->h_boxes.begin(), c->h_boxes.end());
+  if (key.size() != c->ftab_key.size() ||
+      std::memcmp(key.data(), c->ftab_key.data(), key.size() * sizeof(float)) != 0) {
+    fp::Proj pj;
+    if (!fp::make_proj(cam, &pj)) return false;
+    const int image_h = int(cam[13]);
+    const fp::Rows U = fp::union_rows(pj, c->h_boxes.data(), c->ndom, image_w, image_h, nullptr);
+    fp::Table t;
+    uint32_t np = 0;
+    for (int k = 0; k < ntiles; ++k) {
+      const int tx = tiles[4 * k], ty = tiles[4 * k + 1], tw = tiles[4 * k + 2],
+                th = tiles[4 * k + 3];
+      for (int y = ty; y < ty + th; ++y)
+        for (const auto& iv : U[size_t(y)]) {
+          const int lo = std::max(iv.first, tx), hi = std::min(iv.second, tx + tw - 1);
+          if (lo > hi) continue;
+          t.runs.push_back(CamRun{y, lo, np, uint32_t((y - ty) * tw + (lo - tx))});
+          np += uint32_t(hi - lo + 1);
+        }
+    }
+    t.npix = np;
+    fp::finish_table(t);
+    // the previous frame's launches may still read the old table
+    if (hipStreamSynchronize(stream_of(c)) != hipSuccess) {
+      *err = fail(c, SPRAY_RT_ERR_HIP, "frame table: stream sync");
+      return false;
+    }
+    const size_t rb = align256(t.runs.size() * sizeof(CamRun));
+    const size_t bytes = rb + t.first.size() * sizeof(uint32_t);
+    *err = ensure(c, &c->d_ftab, &c->ftab_cap, bytes);
+    if (*err) return false;
+    char* d = static_cast<char*>(c->d_ftab);
+    if (hipMemcpy(d, t.runs.data(), t.runs.size() * sizeof(CamRun), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMemcpy(d + rb, t.first.data(), t.first.size() * sizeof(uint32_t),
+                  hipMemcpyHostToDevice) != hipSuccess) {
+      *err = fail(c, SPRAY_RT_ERR_HIP, "frame table upload");
+      return false;
+    }
+    c->ftab_nruns = uint32_t(t.runs.size() - 1);
+    c->ftab_npix = np;
+    c->ftab_first_off = rb;
+    c->ftab_key.swap(key);
+  }
+  T->runs = static_cast<const CamRun*>(c->d_ftab);
+  T->first = reinterpret_cast<const uint32_t*>(static_cast<char*>(c->d_ftab) + c->ftab_first_off);
+  T->nruns = c->ftab_nruns;
+  T->npix = c->ftab_npix;
+  return true;
 }
 
 }  // namespace
@@ -208,19 +280,30 @@ int spray_rt_render_tiles(spray_rt_ctx_t c, const spray_rt_shader* P, const floa
   // each tile's eye rays (tile-local sampler seeds) at its offset; from
   // here on every pass is per slot (or per pixel group of spp slots), so
   // the batch gives each tile exactly its own-launch result
-  HIPCHK(c, launch_eye_rays_ooc_tiles(s, cam, image_w, spp, tiles, ntiles, rays, pixid, samid));
   const double scale = 1.0 / double(spp);
   if (fused_frame(c, P)) {
     const spray_rt_light& lt = P->lights[0];
     const float shade10[10] = {lt.pos[0],      lt.pos[1],      lt.pos[2], lt.radiance[0],
                                lt.radiance[1], lt.radiance[2], P->ks[0],  P->ks[1],
                                P->ks[2],       P->shininess};
+    // the eye rays of U's pixels (frame_table) or of the whole tiles
+    CamTable T{};
+    size_t Mt = M;  // rays launched
+    if (frame_table(c, cam, image_w, tiles, ntiles, &T, &r)) {
+      Mt = size_t(T.npix) * size_t(spp);
+      HIPCHK(c, launch_eye_rays_ooc_table(s, cam, image_w, spp, T, rays, pixid, samid));
+    } else {
+      if (r) return r;
+      HIPCHK(c,
+             launch_eye_rays_ooc_tiles(s, cam, image_w, spp, tiles, ntiles, rays, pixid, samid));
+    }
     // the film needs the shading and occlusion only: no hit records
-    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, M, nullptr, shade10, occ, sv, sw, nshadow));
+    HIPCHK(c, launch_scene_frame_pt(s, view(c), rays, Mt, nullptr, shade10, occ, sv, sw, nshadow));
     HIPCHK(c, launch_frame_stats_add(s, c->d_fstats, kStatStripes, M, nshadow));
-    HIPCHK(c, launch_film(s, image, pixid, M, spp, ns, sw, sv, occ, scale));
+    HIPCHK(c, launch_film(s, image, pixid, Mt, spp, ns, sw, sv, occ, scale));
     return SPRAY_RT_OK;
   }
+  HIPCHK(c, launch_eye_rays_ooc_tiles(s, cam, image_w, spp, tiles, ntiles, rays, pixid, samid));
   HIPCHK(c, launch_path_init(s, w, valid, M));
   const int user = c->coherence;
   for (int b = 0; b < P->bounces; ++b) {

@@ -2128,16 +2128,8 @@ int prepare_image(spray_rt_insitu* I, const float cam[14], int image_w, int imag
     return SPRAY_RT_OK;
   fp::Proj pj;
   if (!fp::make_proj(cam, &pj)) return fail(c, SPRAY_RT_ERR_ARG, "degenerate camera");
-  fp::Rows U(static_cast<size_t>(image_h));
-  bool all = false;
-  for (int d = 0; d < n; ++d)
-    all = fp::box_rows(pj, &c->h_boxes[6 * size_t(d)], image_w, image_h, U) == 2 || all;
-  if (all)
-    for (auto& row : U) row.assign(1, {0, image_w - 1});
-  fp::merge_rows(U);
   uint64_t upix = 0;
-  for (const auto& row : U)
-    for (const auto& iv : row) upix += uint64_t(iv.second - iv.first + 1);
+  fp::Rows U = fp::union_rows(pj, c->h_boxes.data(), n, image_w, image_h, &upix);
   const int bt = I->world * bands;
   std::vector<char> keep(static_cast<size_t>(image_h), 0);
   for (int b = I->rank; b < bt; b += I->world)
@@ -2258,16 +2250,10 @@ int spray_rt_insitu_trace_image(spray_rt_insitu_t I, const spray_rt_shader* P,
     GROW(I->gpack, I->rank == 0 ? total : mine_b);
     char* pk = I->gpack.as<char>();
     // band k of this rank sits at row (rank + k W) * band rows
-    if (I->rank != 0)
-      HIPCHK(c, hipMemcpy2DAsync(pk, band_b, reinterpret_cast<char*>(image) + I->rank * band_b,
-                                 size_t(W) * band_b, band_b, size_t(bands),
-                                 hipMemcpyDeviceToDevice, s));
+    if (I->rank != 0) HIPCHK(c, launch_bands_copy(s, image, pk, W, bands, band_b, I->rank, 1, 1));
     COMM(I->tr->alltoallv(I, pk, sb.data(), pk, rb.data(), true));
-    if (I->rank == 0)
-      for (int k = 1; k < W; ++k)  // rank k's segment: its bands, in order
-        HIPCHK(c, hipMemcpy2DAsync(reinterpret_cast<char*>(image) + k * band_b,
-                                   size_t(W) * band_b, pk + size_t(k) * size_t(bands) * band_b,
-                                   band_b, band_b, size_t(bands), hipMemcpyDeviceToDevice, s));
+    if (I->rank == 0)  // rank k's segment: its bands, in order
+      HIPCHK(c, launch_bands_copy(s, image, pk, W, bands, band_b, 1, W - 1, 0));
     return SPRAY_RT_OK;
   };
   if (!r)

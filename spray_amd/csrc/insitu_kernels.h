@@ -132,6 +132,13 @@ hipError_t launch_rep_slots(hipStream_t s, const uint32_t* idx_c, const int32_t*
 hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pix,
                              const float* compact, size_t np);
 // tail[64 c + k] = bit k of {nrad, the nshadow counters' sum, 0}[c] (192 bytes)
+// Image frames' interleaved bands (band b of the frame = rows b * band16 * 16
+// bytes on; rank r holds bands r, r + W, ...): pack = 1 copies rank r0's
+// bands from the image into pk (its bands in order); pack = 0 copies ranks
+// r0 .. r0 + nr - 1's segments of the gathered pk (rank k's bands at
+// k * bands * band16 uint4) into the image.  One launch for every band.
+hipError_t launch_bands_copy(hipStream_t s, float* image, void* pk, int W, int bands,
+                             size_t band_bytes, int r0, int nr, int pack);
 // tot = {stats[3] (live slots shaded), stats[1] (shadows), stats[0] (aborts)}
 hipError_t launch_totals_of_stats(hipStream_t s, const unsigned long long* stats,
                                   unsigned long long* tot);

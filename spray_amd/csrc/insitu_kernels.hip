@@ -1008,6 +1008,29 @@ hipError_t launch_hit_flags(hipStream_t s, const uint8_t* valid, const spray_rt_
 hipError_t launch_weights_one(hipStream_t s, float* w, size_t n) {
   LAUNCH(n, k_weights_one, reinterpret_cast<float4*>(w), n);
 }
+__global__ __launch_bounds__(kBlock) void k_bands_copy(uint4* __restrict__ image,
+                                                       uint4* __restrict__ pk, int W, int bands,
+                                                       size_t band16, int r0, size_t n,
+                                                       int pack) {
+  const size_t idx = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (idx >= n) return;
+  const size_t seg = idx / band16, off = idx % band16;
+  const size_t i = seg / size_t(bands), j = seg % size_t(bands);
+  const size_t rank = size_t(r0) + i;
+  const size_t io = (rank + j * size_t(W)) * band16 + off;
+  if (pack)
+    pk[j * band16 + off] = image[io];
+  else
+    image[io] = pk[(rank * size_t(bands) + j) * band16 + off];
+}
+hipError_t launch_bands_copy(hipStream_t s, float* image, void* pk, int W, int bands,
+                             size_t band_bytes, int r0, int nr, int pack) {
+  if (band_bytes % 16) return hipErrorInvalidValue;
+  const size_t band16 = band_bytes / 16;
+  const size_t n = size_t(nr) * size_t(bands) * band16;
+  LAUNCH(n, k_bands_copy, reinterpret_cast<uint4*>(image), static_cast<uint4*>(pk), W, bands,
+         band16, r0, n, pack);
+}
 __global__ void k_totals_of_stats(const unsigned long long* __restrict__ st,
                                   unsigned long long* __restrict__ tot) {
   if (threadIdx.x < 3) tot[threadIdx.x] = st[threadIdx.x == 0 ? 3 : threadIdx.x == 1 ? 1 : 0];

@@ -365,7 +365,7 @@ int spray_rt_destroy(spray_rt_ctx_t c) {
   }
   void* bufs[] = {c->d_slots, c->d_boxes, c->d_dom2slot, c->d_domtrav, c->d_owner, c->d_tlas, c->d_seg_slot,
                   c->d_seg_off, c->d_stage, c->d_stage2, c->d_stage3,
-                  c->d_block_counts, c->d_heads, c->d_sel, c->d_bsdf, c->d_frame, c->d_fstats};
+                  c->d_block_counts, c->d_heads, c->d_sel, c->d_bsdf, c->d_frame, c->d_fstats, c->d_ftab};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -85,6 +85,13 @@ struct spray_rt_ctx {
   void* d_frame = nullptr;  // render_tile path buffers
   size_t frame_cap = 0;
   unsigned long long* d_fstats = nullptr;  // render_tile totals (shade stats)
+  // render_tiles' footprint-culled frame: the run table of the last
+  // (camera, tiles, boxes) -- runs then first, frame.cpp -- and its key
+  std::vector<float> ftab_key;
+  void* d_ftab = nullptr;
+  size_t ftab_cap = 0;
+  uint32_t ftab_nruns = 0, ftab_npix = 0;
+  size_t ftab_first_off = 0;  // bytes from d_ftab to the first[] array
   std::string err;
   std::mutex mu;  // lanes: the lazy table rebuild (prepare) runs under it
 };

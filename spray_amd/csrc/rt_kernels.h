@@ -210,6 +210,12 @@ struct CamTable {
   const uint32_t* first;
   uint32_t nruns, npix;
 };
+// render_tiles' footprint-culled eye rays: table T's pixels (each run's
+// ubase = the tile-local pixel id of its first pixel), the tile launch's
+// rays, pixel and tile-local sample ids at compact indices
+hipError_t launch_eye_rays_ooc_table(hipStream_t s, const float* cam14, int image_w, int spp,
+                                    const CamTable& T, spray_rt_ray* rays, int32_t* pixid,
+                                    int32_t* samid);
 // resident domains up to which the camera launches test a lane's boxes
 // directly instead of walking the top-level tree
 constexpr int kDirectRes = 32;

@@ -1358,12 +1358,9 @@ __global__ __launch_bounds__(kBlock) void k_route(const BvhNode* __restrict__ tl
 // ooc::Tracer::genMultiEyes (src/ooc/ooc_tracer.inl:124-172) + Camera::
 // generateRay (camera.h:168-209), glm operand order: ray `bufid` of tile
 // (tx, ty, tw), written at out[0] (pixid / samid optional).
-__device__ __forceinline__ void eye_ray_ooc(const Cam& cam, int image_w, int spp, int tx, int ty,
-                                            int tw, size_t bufid, spray_rt_ray* out,
-                                            int32_t* pixid, int32_t* samid) {
-  const int p = int(bufid / spp);
-  const int x0 = p % tw, y0 = p / tw;
-  const int x = tx + x0, y = ty + y0;
+__device__ __forceinline__ void eye_ray_ooc_xy(const Cam& cam, int image_w, int spp, int x, int y,
+                                               size_t bufid, spray_rt_ray* out, int32_t* pixid,
+                                               int32_t* samid) {
   float fx = float(x), fy = float(y);
   if (spp > 1) {
     uint32_t st = mm_fin(mm_mix(0u, uint32_t(bufid)));
@@ -1384,6 +1381,12 @@ __device__ __forceinline__ void eye_ray_ooc(const Cam& cam, int image_w, int spp
   rp[1] = make_float4(dx, dy, dz, kInf);
   if (pixid) *pixid = y * image_w + x;
   if (samid) *samid = int32_t(bufid);
+}
+__device__ __forceinline__ void eye_ray_ooc(const Cam& cam, int image_w, int spp, int tx, int ty,
+                                            int tw, size_t bufid, spray_rt_ray* out,
+                                            int32_t* pixid, int32_t* samid) {
+  const int p = int(bufid / spp);
+  eye_ray_ooc_xy(cam, image_w, spp, tx + p % tw, ty + p / tw, bufid, out, pixid, samid);
 }
 
 __global__ __launch_bounds__(kBlock) void k_eye_rays_ooc(
@@ -1420,6 +1423,21 @@ __global__ __launch_bounds__(kBlock) void k_eye_rays_ooc_tiles(
   }
   eye_ray_ooc(cam, image_w, spp, T.t[lo][0], T.t[lo][1], T.t[lo][2], j - T.off[lo], rays + j,
               pixid ? pixid + j : nullptr, samid ? samid + j : nullptr);
+}
+
+// The eye rays of run table T's pixels (render_tiles' footprint-culled
+// frame): each run's ubase is the tile-local pixel id of its first pixel,
+// so the slot cam_item returns is eye_ray_ooc's tile-local sample id and
+// the ray, pixel and sample ids are the tile launch's, at compact index j.
+__global__ __launch_bounds__(kBlock) void k_eye_rays_ooc_table(
+    Cam cam, int image_w, int spp, CamTable T, spray_rt_ray* __restrict__ rays,
+    int32_t* __restrict__ pixid, int32_t* __restrict__ samid) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= size_t(T.npix) * uint32_t(spp)) return;
+  int x, y, s;
+  size_t slot;
+  cam_item(T, spp, j, x, y, s, slot);
+  eye_ray_ooc_xy(cam, image_w, spp, x, y, slot, rays + j, pixid + j, samid + j);
 }
 
 // insitu::genMultiSampleEyeRays / genSingleSampleEyeRays (src/insitu/
@@ -2502,6 +2520,17 @@ hipError_t launch_eye_rays_ooc_tiles(hipStream_t s, const float* cam14, int imag
     base += off;
   }
   return hipSuccess;
+}
+
+hipError_t launch_eye_rays_ooc_table(hipStream_t s, const float* cam14, int image_w, int spp,
+                                    const CamTable& T, spray_rt_ray* rays, int32_t* pixid,
+                                    int32_t* samid) {
+  const size_t n = size_t(T.npix) * size_t(spp);
+  if (n == 0) return hipSuccess;
+  Cam c;
+  for (int k = 0; k < 14; ++k) c.p[k] = cam14[k];
+  k_eye_rays_ooc_table<<<grid_for(n), kBlock, 0, s>>>(c, image_w, spp, T, rays, pixid, samid);
+  return hipGetLastError();
 }
 
 hipError_t launch_spawn_pt(hipStream_t s, const spray_rt_ray* rays,

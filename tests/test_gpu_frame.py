@@ -235,3 +235,32 @@ def test_batched_tiles_equal_per_tile(spray, oracle, scene64, kind):
     assert c1 == c2 and c1[0] > 0
     a, b = one.cpu().numpy(), many.cpu().numpy()
     assert (a > 0).sum() > 1000 and a.tobytes() == b.tobytes()
+
+
+def test_fused_frame_cull_matches_whole_tiles(spray, oracle, scene64, monkeypatch):
+    """The fused frame launches only the eye rays of pixels some domain box's
+    footprint covers (the others counted as misses): image bits and ray
+    counts equal to the frame that launches the whole tiles
+    (SPRAY_FRAME_CULL=0), for a batch of tiles and for a camera that sees
+    no box at all."""
+    sc, osc, doms, slights = scene64
+    w, h, spp = 96, 80, 4
+    rows = oracle.scene_lights(slights)
+    sc.rt.set_bsdfs(oracle.scene_bsdfs(doms))
+    sh = spray.frame.make_shader("pt", 1, 1, lights=rows)
+    c = BENCH_CAMERA
+    away = [2 * p - q for p, q in zip(c["pos"], c["lookat"])]
+    for cam in (camera(oracle, w, h), oracle.camera_init(c["pos"], away, c["up"], 60.0, w, h)):
+        tiles = [t for t in spray.frame.tile_list(w, h, spp, 1, 0, 5000) if t[2] * t[3]]
+        out = []
+        for cull in ("1", "0"):
+            monkeypatch.setenv("SPRAY_FRAME_CULL", cull)
+            img = torch.zeros(w * h * 4, dtype=torch.float32, device="cuda")
+            sc.rt.frame_stats(reset=True)
+            sc.rt.render_tiles(sh, cam, w, spp, tiles, img)
+            cnt = sc.rt.frame_stats(reset=True)
+            torch.cuda.synchronize()
+            out.append((img.cpu().numpy(), cnt))
+        assert out[0][1] == out[1][1] and out[0][1][0] == w * h * spp
+        assert out[0][0].tobytes() == out[1][0].tobytes()
+    assert out[0][1][1] == 0 and not out[0][0].any()  # the camera facing away
