@@ -303,6 +303,14 @@ struct SceneArgs {
 #ifndef SPRAY_HIT_TRANSPOSE
 #define SPRAY_HIT_TRANSPOSE 1
 #endif
+// Closest-hit packet walks of plain ray buffers: 1 = the next packet of the
+// chunk is copied global -> LDS (global_load_lds, no VGPRs) while the
+// current packet walks, so its rays are waiting in LDS when it starts.
+#ifndef SPRAY_RAY_PREFETCH
+#define SPRAY_RAY_PREFETCH 1
+#endif
+typedef __attribute__((address_space(1))) const void* glds_src_t;
+typedef __attribute__((address_space(3))) void* glds_dst_t;
 // The same for the per-lane path's ray loads and the AO rays' stores
 // (measured: AO step 6.27 vs 6.41 ms).
 #ifndef SPRAY_NT_IO_LANE
@@ -660,12 +668,22 @@ __device__ __forceinline__ void scene_ray_packet(const SceneArgs& A, size_t i, b
                                                  bool& spawn, float* pos, float* wi,
                                                  const float* rin = nullptr,
                                                  const Post& post = Post(),
-                                                 const uint8_t* sres = nullptr, int nres = 0) {
+                                                 const uint8_t* sres = nullptr, int nres = 0,
+                                                 const float4* lray = nullptr) {
   const SlotDesc* __restrict__ slots = A.slots;
   const int* __restrict__ dom2slot = A.dom2slot;
   const int lane = threadIdx.x & 63;
   float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 1.f, 0.f);
-  if (valid && rin) {
+  if (lray) {
+    // the wave's rays copied to LDS by the previous packet (global_load_lds:
+    // lane l's 32 B at lray[l], lray[64 + l]); the copy is a vector-memory
+    // operation hipcc does not count, so wait for it here
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (valid) {
+      o4 = lray[lane];
+      d4 = lray[64 + lane];
+    }
+  } else if (valid && rin) {
     o4 = make_float4(rin[0], rin[1], rin[2], kRayEpsilon);
     d4 = make_float4(rin[3], rin[4], rin[5], kInf);
   } else if (valid) {
@@ -1166,6 +1184,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
   __shared__ int32_t wstack[(kBlock / 64) * STK];
   constexpr bool kShadow = EPI == kEpiShadow || EPI == kEpiShadowFrame;
   __shared__ float sq_ray[kShadow ? (kBlock / 64) * kShadowQ * 6 : 1];
+  // the next packet's rays, per wave (SPRAY_RAY_PREFETCH)
+  constexpr bool kPre = SPRAY_RAY_PREFETCH && kPacket && !kAdaptive && !ANY && !rep_epi(EPI);
+  __shared__ float4 spre[kPre ? (kBlock / 64) * 128 : 1];
   __shared__ uint32_t sq_src[kShadow ? (kBlock / 64) * kShadowQ : 1];
   ShadowQueue sq{sq_ray + (kShadow ? (threadIdx.x >> 6) * kShadowQ * 6 : 0),
                  sq_src + (kShadow ? (threadIdx.x >> 6) * kShadowQ : 0), 0u};
@@ -1235,6 +1256,9 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
     // latency of four packet walks in a row)
     const bool small = M < size_t(gridDim.x) * (kBlock / 64) * kChunk * 4;
     const uint32_t csz = small ? 64u : kChunk;
+    // plain ray buffers: the chunk's next packet is prefetched into LDS
+    const bool pre_on = kPre && !idx && !A.valid && !A.nrays;
+    float4* wpre = spre + (kPre ? (threadIdx.x >> 6) * 128 : 0);
     const uint32_t xcd = xcc_id() & 7u;
     const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
     for (uint32_t k = 0; k < uint32_t(kQueues); ++k) {
@@ -1252,6 +1276,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
       while (begin + base < end) {
         uint32_t next = 0;
         const size_t cbeg = begin + base;
+        bool have = false;  // wave-uniform: this packet's rays are in wpre
         for (uint32_t c = 0; c < csz; c += 64) {
           const size_t j = cbeg + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
@@ -1266,13 +1291,23 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
             size_t at = i;
             const bool okr =
                 rep_epi(EPI) ? rep_ray<EPI>(A, j, i, ok, j < end, at, r6, sbox, sres, nres) : ok;
+            // the chunk's next packet, copied to LDS during this one's walk
+            const bool pre = pre_on && !last && cbeg + c + 64 < end;
             scene_ray_packet<W, ANY, EPI == kEpiShadowGen ? kEpiNone : EPI>(
                 A, at, okr, stl, sbox, sdom, wstk, flag, pos, wi,
                 rep_epi(EPI) ? r6 : nullptr,
                 [&]() {
                   if (last && lane == 0) next = atomicAdd(head, csz);
+                  if (kPre && pre && j + 64 < end) {
+                    const spray_rt_ray* src = A.rays + (j + 64);
+                    __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)wpre, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(
+                        (glds_src_t)(reinterpret_cast<const char*>(src) + 16),
+                        (glds_dst_t)(wpre + 64), 16, 0, 0);
+                  }
                 },
-                rep_epi(EPI) ? sres : nullptr, kRes ? nres : 0);
+                rep_epi(EPI) ? sres : nullptr, kRes ? nres : 0, kPre && have ? wpre : nullptr);
+            have = pre;
           } else if (kPacket && wave_coherent(A, i, ok)) {
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           } else if (ok) {
