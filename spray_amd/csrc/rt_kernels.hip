@@ -1259,6 +1259,7 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
     // plain ray buffers: the chunk's next packet is prefetched into LDS
     const bool pre_on = kPre && !idx && !A.valid && !A.nrays;
     float4* wpre = spre + (kPre ? (threadIdx.x >> 6) * 128 : 0);
+    bool have = false;  // wave-uniform: the next packet's rays are in wpre
     const uint32_t xcd = xcc_id() & 7u;
     const uint32_t sub = (blockIdx.x >> 3) % kPerXcd;
     for (uint32_t k = 0; k < uint32_t(kQueues); ++k) {
@@ -1276,7 +1277,6 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
       while (begin + base < end) {
         uint32_t next = 0;
         const size_t cbeg = begin + base;
-        bool have = false;  // wave-uniform: this packet's rays are in wpre
         for (uint32_t c = 0; c < csz; c += 64) {
           const size_t j = cbeg + c + lane;
           const size_t i = (idx && j < end) ? idx[j] : j;
@@ -1307,7 +1307,24 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
                   }
                 },
                 rep_epi(EPI) ? sres : nullptr, kRes ? nres : 0, kPre && have ? wpre : nullptr);
-            have = pre;
+            // the next chunk's first packet: its head came back during this
+            // walk; copied to LDS beside the epilogue and the shadow packets
+            bool pre_next = false;
+            if (kPre && last && pre_on) {
+              const uint32_t nb = __builtin_amdgcn_readfirstlane(next);
+              if (begin + nb < end) {
+                const size_t jn = begin + nb + lane;
+                if (jn < end) {
+                  const spray_rt_ray* src = A.rays + jn;
+                  __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)wpre, 16, 0, 0);
+                  __builtin_amdgcn_global_load_lds(
+                      (glds_src_t)(reinterpret_cast<const char*>(src) + 16),
+                      (glds_dst_t)(wpre + 64), 16, 0, 0);
+                }
+                pre_next = true;
+              }
+            }
+            have = pre || pre_next;
           } else if (kPacket && wave_coherent(A, i, ok)) {
             scene_ray_packet<W, ANY, EPI>(A, i, ok, stl, sbox, sdom, wstk, flag, pos, wi);
           } else if (ok) {
