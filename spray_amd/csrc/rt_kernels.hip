@@ -309,6 +309,11 @@ struct SceneArgs {
 #ifndef SPRAY_RAY_PREFETCH
 #define SPRAY_RAY_PREFETCH 1
 #endif
+// cache policy of those copies (gfx950 CPol: 2 = nt, the non-temporal hint
+// of the plain ray loads, SPRAY_NT_IO)
+#ifndef SPRAY_GLDS_AUX
+#define SPRAY_GLDS_AUX 0
+#endif
 typedef __attribute__((address_space(1))) const void* glds_src_t;
 typedef __attribute__((address_space(3))) void* glds_dst_t;
 // The same for the per-lane path's ray loads and the AO rays' stores
@@ -1300,10 +1305,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
                   if (last && lane == 0) next = atomicAdd(head, csz);
                   if (kPre && pre && j + 64 < end) {
                     const spray_rt_ray* src = A.rays + (j + 64);
-                    __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)wpre, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)wpre, 16, 0, SPRAY_GLDS_AUX);
                     __builtin_amdgcn_global_load_lds(
                         (glds_src_t)(reinterpret_cast<const char*>(src) + 16),
-                        (glds_dst_t)(wpre + 64), 16, 0, 0);
+                        (glds_dst_t)(wpre + 64), 16, 0, SPRAY_GLDS_AUX);
                   }
                 },
                 rep_epi(EPI) ? sres : nullptr, kRes ? nres : 0, kPre && have ? wpre : nullptr);
@@ -1316,10 +1321,10 @@ __global__ __launch_bounds__(kBlock, ANY ? (ao_epi(EPI) ? SPRAY_WAVES_AOGEN : SP
                 const size_t jn = begin + nb + lane;
                 if (jn < end) {
                   const spray_rt_ray* src = A.rays + jn;
-                  __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)wpre, 16, 0, 0);
+                  __builtin_amdgcn_global_load_lds((glds_src_t)src, (glds_dst_t)wpre, 16, 0, SPRAY_GLDS_AUX);
                   __builtin_amdgcn_global_load_lds(
                       (glds_src_t)(reinterpret_cast<const char*>(src) + 16),
-                      (glds_dst_t)(wpre + 64), 16, 0, 0);
+                      (glds_dst_t)(wpre + 64), 16, 0, SPRAY_GLDS_AUX);
                 }
                 pre_next = true;
               }
