@@ -1458,6 +1458,9 @@ int trace_replicated_ao(spray_rt_insitu* I, const spray_rt_shader* P, const spra
 // rebuilt when the camera, the light or the residency changes.
 int upload_table(spray_rt_insitu* I, const fp::Table& t, DBuf& runs, DBuf& first, CamTable* out) {
   spray_rt_ctx* c = I->ctx;
+  // the previous frame's launches may still read the old table (the copies
+  // below are synchronous on the null stream, not ordered after them)
+  HIPCHK(c, hipStreamSynchronize(stream_of(c)));
   GROW(runs, t.runs.size() * sizeof(CamRun));
   GROW(first, t.first.size() * sizeof(uint32_t));
   HIPCHK(c, hipMemcpy(runs.p, t.runs.data(), t.runs.size() * sizeof(CamRun),
