@@ -355,7 +355,11 @@ def run_image(args, dist, world, rank, local, cam):
     sh = spray_amd.frame.make_shader("pt", 1, 1, ks=SHADE[6:9], shininess=SHADE[9],
                                      lights=lights)
     image = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
-    bands = args.image_bands or (1 if world <= 2 else 4)
+    bands = args.image_bands
+    if not bands:  # interleaved bands of 16 rows from 4 ranks on (uniform: world x bands | H)
+        bands = 1 if world <= 2 else max(1, H // (16 * world))
+        while bands > 1 and H % (world * bands):
+            bands -= 1
     if world == 1:
         bands = 1
 
@@ -613,7 +617,7 @@ def main():
                     help="also measure the image-parallel strong split (spray_rt_insitu_trace_image)")
     ap.add_argument("--image-bands", type=int, default=0,
                     help="row bands per rank of the image-parallel split (interleaved); 0: 1 up "
-                         "to 2 ranks, 4 above (profiles/r6_image_cull_rehearse.txt)")
+                         "to 2 ranks, bands of 16 rows above (profiles/r6_image_bands.txt)")
     ap.add_argument("--ooc", type=int, default=-1,
                     help="also measure configs[3] (default: on one rank)")
     ap.add_argument("--ao", type=int, default=1, help="also measure the configs[4] workload")

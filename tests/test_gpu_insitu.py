@@ -724,7 +724,7 @@ def _image_reference(oracle, case):
 
 @pytest.mark.parametrize("world,bands,case", [(1, 1, "pt1"), (1, 2, "ao16"), (2, 1, "pt1"),
                                               (2, 4, "pt1"), (3, 1, "ao16"), (3, 1, "pt3"),
-                                              (8, 2, "pt1"), (8, 1, "ao16")])
+                                              (4, 16, "ao16"), (8, 8, "pt1"), (8, 1, "ao16")])
 def test_engine_image_frame_ranks(oracle, world, bands, case):
     """The image-parallel strong split (ooc mode): world
     processes sharing the GPU over the host transport (world 1: RCCL), every
