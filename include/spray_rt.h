@@ -714,8 +714,10 @@ int spray_rt_insitu_trace_camera(spray_rt_insitu_t ins, const spray_rt_shader* s
  * its film to its own rows of image_rgba, and the rows go to rank 0 in one
  * gather (HdrImage::composite, image.h:167-181, an MPI_Reduce SUM of
  * disjoint pixels there; here each rank sends only its own rows, 1/world of
- * the image): rank 0's image holds the whole frame, its other ranks' rows
- * REPLACED by theirs (clear the images first, HdrImage::clear).  One row
+ * the image -- when only the eye rays of pixels some domain box's footprint
+ * covers are traced, see SPRAY_IMAGE_CULL, only those pixels' RGB, 12 B
+ * each): rank 0's image holds the whole frame, its other ranks' pixels
+ * REPLACED by theirs (clear the images first, HdrImage::clear).  One
  * gather (the data all-to-all-v, every rank but 0 sending) and one totals
  * all-reduce per frame; totals = the group's. */
 int spray_rt_insitu_trace_image(spray_rt_insitu_t ins, const spray_rt_shader* shader,

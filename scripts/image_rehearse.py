@@ -11,10 +11,11 @@ go to rank 0 in one gather and the totals in one 24-B all-reduce.  A replay
 engine (spray_rt_insitu_create_replay) runs a rank's part exactly -- its eye
 rays, launches and film -- with the gather and the all-reduce keeping the
 rank's own data, so the per-rank device time is measured, not modelled.
-Projection: the busiest rank's frame + the gather (every rank but 0 sends its
-16 MiB / N of rows to rank 0 on its own xGMI link: alpha + bytes / link
-bandwidth, conservative / optimistic) + the totals all-reduce (alpha).  No
-multi-GPU box is available to this build: the link terms are modelled.
+Projection: the busiest rank's frame + the gather (every rank but 0 sends
+the RGB of its rows' pixels in U -- those some domain box's footprint covers,
+12 B each -- to rank 0 on its own xGMI link: alpha + the largest rank's bytes
+/ link bandwidth, conservative / optimistic) + the totals all-reduce (alpha).
+No multi-GPU box is available to this build: the link terms are modelled.
 """
 import argparse
 import json
@@ -37,6 +38,29 @@ SHADE = [0.0, 500.0, 1000.0, 1.0, 1.0, 1.0, 0.4, 0.4, 0.4, 10.0]
 # the small all-reduce: alpha only
 LINK = {"cons": (0.030, 100.0), "opt": (0.015, 140.0)}
 AR_ALPHA = {"cons": 0.030, "opt": 0.015}
+
+
+def u_rows(cam, boxes):
+    """Per image row the pixels of U (the union of the boxes' footprints)."""
+    from spray_amd import insitu
+    cover = np.zeros((H, W), bool)
+    for b in boxes:
+        k, x0, x1 = insitu.box_rows(cam, W, H, b[:6])
+        if k == 2:
+            cover[:] = True
+        elif k == 1:
+            for y in np.nonzero(x1 >= x0)[0]:
+                cover[y, x0[y]:x1[y] + 1] = True
+    return cover.sum(1)
+
+
+def gather_bytes(urow, world, bands):
+    """Bytes each rank sends to rank 0 (its bands' U pixels, 12 B each)."""
+    bt = world * bands
+    out = np.zeros(world)
+    for b in range(bt):
+        out[b % world] += urow[b * H // bt:(b + 1) * H // bt].sum() * 12
+    return out
 
 
 def main():
@@ -62,7 +86,8 @@ def main():
     torch.cuda.set_stream(stream)
     rt.set_stream(stream)
     image = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
-    out = {"runs": [], "link": LINK, "frames": args.frames}
+    urow = u_rows(cam, boxes)
+    out = {"runs": [], "link": LINK, "frames": args.frames, "u_pixels": int(urow.sum())}
     for kind in args.kinds:
         sh = spray_amd.frame.make_shader(kind, 1, 16 if kind == "ao" else 1, ks=SHADE[6:9],
                                          shininess=SHADE[9], lights=lights)
@@ -89,13 +114,15 @@ def main():
                                   "wall_ms": wall, "rays": tot[0] + tot[1]})
                     eng.close()
                 busiest = max(r["frame_ms"] for r in ranks)
+                gb = gather_bytes(urow, world, bands)
                 proj = {}
                 for k, (alpha, bw) in LINK.items():
                     comm = 0.0
                     if world > 1:
-                        comm = alpha + (W * H * 16 / world) / (bw * 1e9) * 1e3 + AR_ALPHA[k]
+                        comm = alpha + gb[1:].max() / (bw * 1e9) * 1e3 + AR_ALPHA[k]
                     proj[k] = round(busiest + comm, 4)
                 run = {"kind": kind, "world": world, "bands": bands, "ranks": ranks,
+                       "gather_bytes": [int(x) for x in gb],
                        "busiest_ms": round(busiest, 4),
                        "mean_ms": round(float(np.mean([r["frame_ms"] for r in ranks])), 4),
                        "sum_ms": round(float(np.sum([r["frame_ms"] for r in ranks])), 4),

@@ -232,6 +232,11 @@ struct spray_rt_insitu {
   DBuf ti_runs, ti_first;
   CamTable ti{};
   uint64_t img_upix = 0;
+  // the compact gather: every rank's pixels of U (its table's npix), and on
+  // rank 0 the table of the other ranks' U pixels in rank order
+  std::vector<uint32_t> img_counts;
+  DBuf tg_runs, tg_first;
+  CamTable tg{};
   size_t ciota_n = 0;  // entries of ciota filled (0 .. n - 1)
   hipStream_t cs = nullptr;
   hipEvent_t ev_lp0 = nullptr, ev_lp1 = nullptr;
@@ -1727,7 +1732,7 @@ void free_all(spray_rt_insitu* I) {
                  &I->aflag, &I->aown, &I->asel_tmp, &I->abits, &I->tu_runs, &I->tu_first,
                  &I->te_runs, &I->te_first, &I->ts_runs, &I->ts_first, &I->ctmin, &I->ccomp,
                  &I->crays, &I->cpix, &I->csam, &I->ciota, &I->gpack, &I->ti_runs,
-                 &I->ti_first};
+                 &I->ti_first, &I->tg_runs, &I->tg_first};
   for (DBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : I->ev)
@@ -2134,17 +2139,33 @@ int prepare_image(spray_rt_insitu* I, const float cam[14], int image_w, int imag
   uint64_t upix = 0;
   fp::Rows U = fp::union_rows(pj, c->h_boxes.data(), n, image_w, image_h, &upix);
   const int bt = I->world * bands;
-  std::vector<char> keep(static_cast<size_t>(image_h), 0);
-  for (int b = I->rank; b < bt; b += I->world)
-    for (int y = band_row(b, bt, image_h); y < band_row(b + 1, bt, image_h); ++y)
-      keep[size_t(y)] = 1;
-  for (size_t y = 0; y < U.size(); ++y)
-    if (!keep[y]) U[y].clear();
-  try {
-    CALL(upload_table(I, fp::make_table(U, image_w, nullptr), I->ti_runs, I->ti_first, &I->ti));
-  } catch (const std::exception& e) {
-    return fail(c, SPRAY_RT_ERR_STATE, "image frame table: %s", e.what());
+  // rank k's pixels of U, its rows in ascending order (its table's order);
+  // rank 0 also gets the other ranks' runs, rank by rank (the gather's order)
+  fp::Table mine, others;
+  I->img_counts.assign(size_t(I->world), 0u);
+  for (int k = 0; k < I->world; ++k) {
+    fp::Table& t = k == I->rank ? mine : others;
+    if (k != I->rank && !(I->rank == 0 && k > 0)) {
+      uint32_t n = 0;
+      for (int b = k; b < bt; b += I->world)
+        for (int y = band_row(b, bt, image_h); y < band_row(b + 1, bt, image_h); ++y)
+          for (const auto& iv : U[size_t(y)]) n += uint32_t(iv.second - iv.first + 1);
+      I->img_counts[size_t(k)] = n;
+      continue;
+    }
+    const uint32_t np0 = t.npix;
+    for (int b = k; b < bt; b += I->world)
+      for (int y = band_row(b, bt, image_h); y < band_row(b + 1, bt, image_h); ++y)
+        for (const auto& iv : U[size_t(y)]) {
+          t.runs.push_back(CamRun{y, iv.first, t.npix, t.npix});
+          t.npix += uint32_t(iv.second - iv.first + 1);
+        }
+    I->img_counts[size_t(k)] = t.npix - np0;
   }
+  fp::finish_table(mine);
+  fp::finish_table(others);
+  CALL(upload_table(I, mine, I->ti_runs, I->ti_first, &I->ti));
+  CALL(upload_table(I, others, I->tg_runs, I->tg_first, &I->tg));
   I->img_upix = upix;
   I->img_key.swap(key);
   return SPRAY_RT_OK;
@@ -2233,6 +2254,18 @@ int spray_rt_insitu_trace_image(spray_rt_insitu_t I, const spray_rt_shader* P,
   auto gather = [&]() -> int {
     if (W == 1) return SPRAY_RT_OK;
     std::vector<size_t> sb(size_t(W), 0), rb(size_t(W), 0);
+    if (cull) {
+      // the RGB of the U pixels only (the film writes nothing else): rank k
+      // packs its table's pixels, rank 0 unpacks the others' in rank order
+      for (int k = 1; k < W; ++k) rb[size_t(k)] = I->rank == 0 ? size_t(I->img_counts[size_t(k)]) * 12 : 0;
+      sb[0] = I->rank == 0 ? 0 : size_t(I->ti.npix) * 12;  // rank 0: nothing to itself
+      GROW(I->gpack, I->rank == 0 ? size_t(I->tg.npix) * 12 + 16 : sb[0] + 16);
+      float* pk = I->gpack.as<float>();
+      if (I->rank != 0) HIPCHK(c, launch_pack_rgb(s, I->ti, image_w, image, pk));
+      COMM(I->tr->alltoallv(I, pk, sb.data(), pk, rb.data(), true));
+      if (I->rank == 0) HIPCHK(c, launch_unpack_rgb(s, I->tg, image_w, pk, image));
+      return SPRAY_RT_OK;
+    }
     std::vector<size_t> rrows(size_t(W), 0);  // rows of each rank
     for (int b = 0; b < bt; ++b)
       rrows[size_t(b % W)] += size_t(band_row(b + 1, bt, image_h) - band_row(b, bt, image_h));

@@ -139,6 +139,12 @@ hipError_t launch_rep_expand(hipStream_t s, float* image, const int32_t* slot_pi
 // k * bands * band16 uint4) into the image.  One launch for every band.
 hipError_t launch_bands_copy(hipStream_t s, float* image, void* pk, int W, int bands,
                              size_t band_bytes, int r0, int nr, int pack);
+// Image frames' compact gather: the RGB of table T's pixels (footprint.h
+// runs, in table order) packed from / unpacked into the image, 12 B a pixel
+hipError_t launch_pack_rgb(hipStream_t s, const CamTable& T, int image_w, const float* image,
+                           float* out);
+hipError_t launch_unpack_rgb(hipStream_t s, const CamTable& T, int image_w, const float* in,
+                             float* image);
 // tot = {stats[3] (live slots shaded), stats[1] (shadows), stats[0] (aborts)}
 hipError_t launch_totals_of_stats(hipStream_t s, const unsigned long long* stats,
                                   unsigned long long* tot);

@@ -1031,6 +1031,34 @@ hipError_t launch_bands_copy(hipStream_t s, float* image, void* pk, int W, int b
   LAUNCH(n, k_bands_copy, reinterpret_cast<uint4*>(image), static_cast<uint4*>(pk), W, bands,
          band16, r0, n, pack);
 }
+__global__ __launch_bounds__(kBlock) void k_pack_rgb(CamTable T, int image_w,
+                                                     const float* __restrict__ image,
+                                                     float* __restrict__ out, int unpack) {
+  const size_t j = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= T.npix) return;
+  int x, y, sm;
+  size_t slot;
+  cam_item(T, 1, j, x, y, sm, slot);
+  const size_t px = 4 * (size_t(image_w) * size_t(y) + size_t(x));
+  float* im = const_cast<float*>(image);
+  if (unpack) {
+    im[px] = out[3 * j];
+    im[px + 1] = out[3 * j + 1];
+    im[px + 2] = out[3 * j + 2];
+  } else {
+    out[3 * j] = image[px];
+    out[3 * j + 1] = image[px + 1];
+    out[3 * j + 2] = image[px + 2];
+  }
+}
+hipError_t launch_pack_rgb(hipStream_t s, const CamTable& T, int image_w, const float* image,
+                           float* out) {
+  LAUNCH(size_t(T.npix), k_pack_rgb, T, image_w, image, out, 0);
+}
+hipError_t launch_unpack_rgb(hipStream_t s, const CamTable& T, int image_w, const float* in,
+                             float* image) {
+  LAUNCH(size_t(T.npix), k_pack_rgb, T, image_w, image, const_cast<float*>(in), 1);
+}
 __global__ void k_totals_of_stats(const unsigned long long* __restrict__ st,
                                   unsigned long long* __restrict__ tot) {
   if (threadIdx.x < 3) tot[threadIdx.x] = st[threadIdx.x == 0 ? 3 : threadIdx.x == 1 ? 1 : 0];
