@@ -407,7 +407,8 @@ def run_image(args, dist, world, rank, local, cam):
            "config": "configs[1] frame split by image rows over %d GPU(s): all 64 domains resident "
                      "per GPU, %d row band(s) per rank, the eye rays of the band pixels some box's "
                      "footprint covers (the others counted as misses) + fused closest hit / PT shadow "
-                     "any hit + film per rank, rows gathered to rank 0 over RCCL" % (world, bands)}
+                     "any hit + film per rank, those pixels' RGB gathered to rank 0 over RCCL"
+                     % (world, bands)}
     eng.close()
     rt.close()
     return out
